@@ -1,0 +1,125 @@
+// Fused global-norm clip + TF-variant Adam over ONE flat fp32 parameter buffer (K13 + K14 of
+// SURVEY.md §2.3).  The reference runs `clip_by_global_norm` (model.py:91-92) and
+// `AdamOptimizer(lr).apply_gradients` (model.py:94-98) as ~2×#vars small TF kernels on the PS
+// CPU; here all parameters, gradients and Adam slots live in flat buffers so the whole
+// optimizer is two launches regardless of the number of variables:
+//   1. sumsq_partials: grid-stride float4 sum of g^2, one partial per block (fixed grid =>
+//      deterministic order).
+//   2. adam_apply: every block re-reduces the (<=1024) partials in LDS, derives
+//      scale = clip / max(||g||, clip) and applies
+//        m = b1 m + (1-b1) g s ;  v = b2 v + (1-b2) (g s)^2 ;  p -= lr_t m / (sqrt(v) + eps)
+//      with TF's lr_t = lr * sqrt(1-b2^t) / (1-b1^t) computed on the host (TF "epsilon-hat").
+//      Optionally refreshes a bf16 mirror of the parameters in the same pass.
+#include "common.h"
+#include "kernels.h"
+
+namespace dcr {
+
+constexpr int kOptThreads = 256;
+
+__global__ void __launch_bounds__(kOptThreads) sumsq_partials_kernel(const float* __restrict__ g,
+                                                                     int64_t n,
+                                                                     float* __restrict__ partials) {
+  __shared__ float red[kOptThreads / 64];
+  float acc = 0.f;
+  const int64_t n4 = n >> 2;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  for (int64_t i = blockIdx.x * (int64_t)kOptThreads + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * kOptThreads) {
+    const float4 x = g4[i];
+    acc += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
+  }
+  if (blockIdx.x == 0) {  // tail
+    for (int64_t i = (n4 << 2) + threadIdx.x; i < n; i += kOptThreads) acc += g[i] * g[i];
+  }
+  const float t = block_sum<kOptThreads>(acc, red);
+  if (threadIdx.x == 0) partials[blockIdx.x] = t;
+}
+
+__device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, float s, float lr_t,
+                                         float b1, float b2, float eps) {
+  g *= s;
+  m = b1 * m + (1.f - b1) * g;
+  v = b2 * v + (1.f - b2) * g * g;
+  p -= lr_t * m / (sqrtf(v) + eps);
+}
+
+__global__ void __launch_bounds__(kOptThreads) adam_apply_kernel(
+    float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+    bf16* __restrict__ pbf, int64_t n, const float* __restrict__ partials, int nparts,
+    float* __restrict__ norm_out, float lr_t, float b1, float b2, float eps, float clip) {
+  __shared__ float red[kOptThreads / 64];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += kOptThreads) acc += partials[i];
+  const float sumsq = block_sum<kOptThreads>(acc, red);
+  const float norm = sqrtf(sumsq);
+  // TF clip_by_global_norm: t * clip / max(norm, clip); clip <= 0 disables clipping.
+  const float s = (clip > 0.f) ? clip / fmaxf(norm, clip) : 1.f;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && norm_out) norm_out[0] = norm;
+
+  const int64_t n4 = n >> 2;
+  float4* p4 = reinterpret_cast<float4*>(p);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  float4* m4 = reinterpret_cast<float4*>(m);
+  float4* v4 = reinterpret_cast<float4*>(v);
+  for (int64_t i = blockIdx.x * (int64_t)kOptThreads + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * kOptThreads) {
+    float4 pp = p4[i], mm = m4[i], vv = v4[i];
+    const float4 gg = g4[i];
+    adam_one(pp.x, gg.x, mm.x, vv.x, s, lr_t, b1, b2, eps);
+    adam_one(pp.y, gg.y, mm.y, vv.y, s, lr_t, b1, b2, eps);
+    adam_one(pp.z, gg.z, mm.z, vv.z, s, lr_t, b1, b2, eps);
+    adam_one(pp.w, gg.w, mm.w, vv.w, s, lr_t, b1, b2, eps);
+    p4[i] = pp;
+    m4[i] = mm;
+    v4[i] = vv;
+    if (pbf) {
+      bf16x4 o;
+      o[0] = f2bf(pp.x); o[1] = f2bf(pp.y); o[2] = f2bf(pp.z); o[3] = f2bf(pp.w);
+      *reinterpret_cast<bf16x4*>(pbf + 4 * i) = o;
+    }
+  }
+  if (blockIdx.x == 0) {
+    for (int64_t i = (n4 << 2) + threadIdx.x; i < n; i += kOptThreads) {
+      float pp = p[i], mm = m[i], vv = v[i];
+      adam_one(pp, g[i], mm, vv, s, lr_t, b1, b2, eps);
+      p[i] = pp; m[i] = mm; v[i] = vv;
+      if (pbf) pbf[i] = f2bf(pp);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kOptThreads) norm_only_kernel(const float* __restrict__ partials,
+                                                                int nparts, float* __restrict__ out) {
+  __shared__ float red[kOptThreads / 64];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += kOptThreads) acc += partials[i];
+  const float t = block_sum<kOptThreads>(acc, red);
+  if (threadIdx.x == 0) out[0] = sqrtf(t);
+}
+
+int opt_num_partials(int64_t n) {
+  // 4 blocks per CU-ish cap; enough to stream a few-MB buffer at HBM rate.
+  int64_t blocks = (n / 4 + kOptThreads - 1) / kOptThreads;
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) blocks = 1;
+  return (int)blocks;
+}
+
+void launch_global_norm(const float* g, int64_t n, float* partials, float* norm_out,
+                        hipStream_t stream) {
+  const int nb = opt_num_partials(n);
+  sumsq_partials_kernel<<<nb, kOptThreads, 0, stream>>>(g, n, partials);
+  norm_only_kernel<<<1, kOptThreads, 0, stream>>>(partials, nb, norm_out);
+}
+
+void launch_adam_clip(float* p, const float* g, float* m, float* v, bf16* pbf, int64_t n,
+                      float* partials, float* norm_out, float lr_t, float b1, float b2, float eps,
+                      float clip, hipStream_t stream) {
+  const int nb = opt_num_partials(n);
+  sumsq_partials_kernel<<<nb, kOptThreads, 0, stream>>>(g, n, partials);
+  adam_apply_kernel<<<nb, kOptThreads, 0, stream>>>(p, g, m, v, pbf, n, partials, nb, norm_out,
+                                                    lr_t, b1, b2, eps, clip);
+}
+
+}  // namespace dcr

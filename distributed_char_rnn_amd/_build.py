@@ -1,0 +1,134 @@
+"""In-tree native build: compiles ``csrc/*.hip`` (device kernels, gfx950 only) and
+``csrc/*.cpp`` (torch op bindings) with ``hipcc`` and links them into
+``distributed_char_rnn_amd/_C.so``.
+
+No hipify, no JIT cache, no CUDA path: the library is built for ``--offload-arch=gfx950`` and
+loaded with ``torch.ops.load_library`` (see ``ops/native.py``).  Objects are cached under
+``build/`` and rebuilt when the source or any ``csrc/*.h`` header is newer.
+
+Usage: ``python -m distributed_char_rnn_amd._build [--force] [-j N]``
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(REPO, "csrc")
+BUILD = os.path.join(REPO, "build", "native")
+OUT = os.path.join(PKG_DIR, "_C.so")
+ARCH = os.environ.get("DCR_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    cand = os.path.join(rocm, "bin", "hipcc")
+    if os.path.exists(cand):
+        return cand
+    found = shutil.which("hipcc")
+    if not found:
+        raise RuntimeError("hipcc not found: set ROCM_PATH")
+    return found
+
+
+def _cxx() -> str:
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    clang = os.path.join(rocm, "lib", "llvm", "bin", "clang++")  # understands __bf16 on x86
+    return os.environ.get("DCR_CXX", clang if os.path.exists(clang) else "c++")
+
+
+def _torch_flags():
+    import torch
+    from torch.utils import cpp_extension as ce
+
+    inc = ce.include_paths(device_type="cuda")
+    libdirs = ce.library_paths(device_type="cuda")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cflags = [f"-I{p}" for p in inc] + [
+        f"-I{sysconfig.get_paths()['include']}",
+        f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+        "-DUSE_ROCM=1",
+        "-D__HIP_PLATFORM_AMD__=1",
+    ]
+    torch_lib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    ldflags = [f"-L{torch_lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+               f"-Wl,-rpath,{torch_lib}"]
+    return cflags, ldflags, libdirs
+
+
+COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
+          "-ffp-contract=fast"]
+
+
+def _stale(obj: str, src: str, headers) -> bool:
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    if os.path.getmtime(src) > t:
+        return True
+    return any(os.path.getmtime(h) > t for h in headers)
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    hipcc = _hipcc()
+    cflags, ldflags, _ = _torch_flags()
+    headers = glob.glob(os.path.join(CSRC, "*.h"))
+    dev_srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    host_srcs = sorted(glob.glob(os.path.join(CSRC, "*.cpp")))
+    jobs = jobs or min(8, max(1, (os.cpu_count() or 2)))
+    jobs = min(jobs, 16)
+
+    def compile_one(src: str):
+        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        if not force and not _stale(obj, src, headers):
+            return obj, None
+        if src.endswith(".hip"):
+            cmd = [hipcc, *COMMON, "-I", CSRC, "-c", src, "-o", obj]
+        else:  # torch bindings: host-only C++ (no device code), compiled by the host compiler
+            cmd = [_cxx(), "-O2", "-std=c++17", "-fPIC", "-I", CSRC, *cflags, "-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            return obj, f"{' '.join(cmd)}\n{r.stdout}\n{r.stderr}"
+        return obj, None
+
+    with ThreadPoolExecutor(jobs) as ex:
+        results = list(ex.map(compile_one, dev_srcs + host_srcs))
+    errs = [e for _, e in results if e]
+    if errs:
+        raise RuntimeError("native build failed:\n" + "\n\n".join(errs))
+    objs = [o for o, _ in results]
+    if force or not os.path.exists(OUT) or any(os.path.getmtime(o) > os.path.getmtime(OUT)
+                                               for o in objs):
+        tmp = OUT + ".tmp"
+        cmd = [hipcc, *COMMON, "-shared", "-o", tmp, *objs, *ldflags]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, OUT)
+    return OUT
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    out = build(force=a.force, jobs=a.jobs, verbose=a.verbose)
+    print(out)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

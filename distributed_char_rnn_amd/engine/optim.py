@@ -1,0 +1,95 @@
+"""TF-1.x-compatible Adam with global-norm clipping over the flat parameter buffer.
+
+Reference: ``grads, _ = clip_by_global_norm(tf.gradients(cost, tvars), grad_clip)`` then
+``AdamOptimizer(lr).apply_gradients(...)`` (model.py:88-98), lr assigned per epoch as
+``learning_rate * decay_rate ** epoch`` (train.py:146-148, 187).  TF's Adam uses the
+"epsilon-hat" form: ``lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t)``,
+``theta -= lr_t * m / (sqrt(v) + eps)`` with ``b1 = .9, b2 = .999, eps = 1e-8`` [TF-ext].
+The embedding's IndexedSlices update in TF decays m/v densely and updates every row, which is
+exactly dense Adam with a zero gradient for unseen rows, so one dense kernel matches it.
+
+On the GPU the whole update is the two-launch fused kernel in ``csrc/optim.hip``; on CPU the
+same math runs as torch ops.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from ..models.params import ParamStore
+
+
+def lr_for_epoch(learning_rate: float, decay_rate: float, epoch: int) -> float:
+    return float(learning_rate) * float(decay_rate) ** int(epoch)
+
+
+class TFAdam:
+    def __init__(self, store: ParamStore, beta1: float = 0.9, beta2: float = 0.999,
+                 eps: float = 1e-8, clip: float = 5.0, bf16_mirror: bool = False):
+        self.store = store
+        self.b1, self.b2, self.eps, self.clip = beta1, beta2, eps, clip
+        self.m = torch.zeros_like(store.flat)
+        self.v = torch.zeros_like(store.flat)
+        self.t = 0  # number of applied updates (TF beta{1,2}_power = b^t after t updates)
+        self.native = store.device.type == "cuda"
+        self.last_norm = torch.zeros(1, device=store.device)
+        self.mirror: Optional[torch.Tensor] = None
+        if bf16_mirror:
+            self.mirror = store.flat.to(torch.bfloat16)
+        if self.native:
+            from ..ops import native
+
+            self._ops = native.ops()
+            self._partials = torch.zeros(self._ops.opt_num_partials(store.numel),
+                                         device=store.device)
+
+    def lr_t(self, lr: float) -> float:
+        t = self.t + 1
+        return lr * math.sqrt(1.0 - self.b2 ** t) / (1.0 - self.b1 ** t)
+
+    @torch.no_grad()
+    def step(self, lr: float) -> torch.Tensor:
+        """Clip the (already averaged) flat gradient by global norm and apply one update.
+        Returns the pre-clip global norm as a 1-element device tensor (no host sync)."""
+        lr_t = self.lr_t(lr)
+        p, g = self.store.flat, self.store.grad
+        if self.native:
+            self._ops.adam_clip(p, g, self.m, self.v, self.mirror, self._partials, self.last_norm,
+                                lr_t, self.b1, self.b2, self.eps, self.clip)
+        else:
+            norm = torch.sqrt((g.double() * g.double()).sum()).float()
+            s = self.clip / torch.clamp(norm, min=self.clip) if self.clip > 0 else torch.ones(())
+            gs = g * s
+            self.m.mul_(self.b1).add_(gs, alpha=1 - self.b1)
+            self.v.mul_(self.b2).addcmul_(gs, gs, value=1 - self.b2)
+            p.sub_(lr_t * self.m / (self.v.sqrt() + self.eps))
+            self.last_norm.copy_(norm.reshape(1))
+            if self.mirror is not None:
+                self.mirror.copy_(p)
+        self.t += 1
+        return self.last_norm
+
+    # -- checkpoint support (TF slot names) ----------------------------------------------
+    def slot_state(self):
+        """TF-named Adam slots + beta powers for the checkpoint."""
+        out = {}
+        for s in self.store.specs:
+            out[f"{s.name}/Adam"] = self.store.view(s.name, self.m).detach().cpu().clone()
+            out[f"{s.name}/Adam_1"] = self.store.view(s.name, self.v).detach().cpu().clone()
+        out["beta1_power"] = torch.tensor(self.b1 ** (self.t + 1), dtype=torch.float32)
+        out["beta2_power"] = torch.tensor(self.b2 ** (self.t + 1), dtype=torch.float32)
+        return out
+
+    def load_slot_state(self, sd) -> None:
+        for s in self.store.specs:
+            if f"{s.name}/Adam" in sd:
+                self.store.view(s.name, self.m).copy_(torch.as_tensor(sd[f"{s.name}/Adam"]))
+                self.store.view(s.name, self.v).copy_(torch.as_tensor(sd[f"{s.name}/Adam_1"]))
+        if "beta1_power" in sd:
+            bp = float(torch.as_tensor(sd["beta1_power"]))
+            # TF stores b1^(t+1) after t updates; invert (robust to float rounding)
+            self.t = max(0, int(round(math.log(bp) / math.log(self.b1))) - 1)
+        if self.mirror is not None:
+            self.mirror.copy_(self.store.flat)

@@ -1,0 +1,270 @@
+"""Training orchestration (reference: ``train(args)``, train.py:73-218).
+
+Per epoch ``e``: ``lr = learning_rate * decay_rate**e``; reset the batch pointer and the TBPTT
+state to zeros; per batch feed the previous batch's final state (stateful truncated BPTT,
+train.py:185-199), all-reduce gradients (sync DP), clip by global norm + Adam, print the
+reference progress line, and save ``model.ckpt-<e*nb+b>`` when ``(e*nb+b) % save_every == 0`` or
+on the final batch (train.py:209-217; A-18 kept so ``model.ckpt-14`` exists after 15 one-batch
+epochs).
+
+Distributed: sync data parallel over RCCL (see parallel/).  Every rank runs the same number of
+steps per epoch (min over ranks); only rank 0 writes config/vocab/checkpoints/logs (fixes the
+benign write race of train.py:109-115).  Without ``--tensor_file`` the corpus is sharded
+in-process with ``np.array_split`` (any world size).
+
+The loss of step k is read back to the host only after step k+1 has been queued, so the GPU
+never idles on the progress print.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..models.char_rnn import CharRNN
+from ..models.params import ModelConfig
+from ..parallel import process_group, topology
+from ..parallel.grad_sync import GradSync
+from ..utils import checkpoint as ckpt
+from ..utils import data as data_mod
+from ..utils import safe_pickle
+from ..utils.metrics import MetricsLogger, PhaseProfiler, progress_line
+from .optim import TFAdam, lr_for_epoch
+
+NEED_BE_SAME = ["model", "rnn_size", "num_layers", "seq_length"]
+
+
+def _log(msg: str, rank: int = 0):
+    if rank == 0:
+        print(msg, flush=True)
+
+
+def make_loader(args, ctx) -> data_mod.TextLoader:
+    rank, world = max(ctx.rank, 0), ctx.world_size
+    B, T = args.batch_size, args.seq_length
+    if args.synthetic_text:
+        toks = data_mod.synthetic_tokens(args.synthetic_text, 65, seed=1234)
+        if world > 1:
+            toks = data_mod.shard(toks, world)[rank]
+        return data_mod.ArrayLoader(toks, data_mod.synthetic_chars(65), B, T)
+    if args.tensor_file:
+        return data_mod.TextLoader(args.data_dir, B, T, tensor_file=args.tensor_file,
+                                   verbose=rank == 0)
+    if world == 1:
+        return data_mod.TextLoader(args.data_dir, B, T)
+    # rank 0 preprocesses (may write vocab.pkl / data.npy), the others read after a barrier
+    full = None
+    if rank == 0:
+        full = data_mod.TextLoader(args.data_dir, 1, 1, verbose=True)
+    ctx.barrier()
+    if full is None:
+        full = data_mod.TextLoader(args.data_dir, 1, 1, verbose=False)
+    part = data_mod.shard(full.tensor, world)[rank]
+    return data_mod.ArrayLoader(part, full.chars, B, T)
+
+
+def check_init_from(args, loader) -> str:
+    """train.py:87-107: required files and model/vocab compatibility."""
+    d = args.init_from
+    assert os.path.isdir(d), f" {d} must be a a path"
+    assert os.path.isfile(os.path.join(d, "config.pkl")), f"config.pkl file does not exist in path {d}"
+    assert os.path.isfile(os.path.join(d, "chars_vocab.pkl")), \
+        f"chars_vocab.pkl.pkl file does not exist in path {d}"
+    prefix = ckpt.latest_checkpoint(d)
+    assert prefix, "No checkpoint found"
+    saved = safe_pickle.load(os.path.join(d, "config.pkl"))
+    for k in NEED_BE_SAME:
+        assert vars(saved)[k] == vars(args)[k], \
+            f"Command line argument and saved model disagree on '{k}' "
+    saved_chars, saved_vocab = safe_pickle.load(os.path.join(d, "chars_vocab.pkl"))
+    assert tuple(saved_chars) == tuple(loader.chars), "Data and loaded model disagree on character set!"
+    assert dict(saved_vocab) == dict(loader.vocab), "Data and loaded model disagree on dictionary mappings!"
+    return prefix
+
+
+def checkpoint_tensors(model: CharRNN, opt: TFAdam, global_step: int, lr: float, epoch: int,
+                       batch: int, state=None):
+    t = {}
+    t.update(model.store.state_dict())
+    t.update(opt.slot_state())
+    t["global_step"] = np.array(global_step, dtype=np.int64)
+    t["Variable"] = np.array(lr, dtype=np.float32)
+    t["dcr/epoch"] = np.array(epoch, dtype=np.int64)
+    t["dcr/batch_pointer"] = np.array(batch, dtype=np.int64)
+    if state is not None:
+        for li, st in enumerate(state):
+            for si, s in enumerate(st):
+                t[f"dcr/state/{li}/{si}"] = s.detach().float().cpu()
+    return t
+
+
+def restore(model: CharRNN, opt: TFAdam, prefix: str):
+    sd = ckpt.Saver.restore(prefix)
+    model.store.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()
+                                 if k in model.store.by_name})
+    opt.load_slot_state({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    model.params_changed()
+    return sd
+
+
+def build_model(args, vocab_size: int, device) -> CharRNN:
+    cfg = ModelConfig(model=args.model, vocab_size=vocab_size, rnn_size=args.rnn_size,
+                      num_layers=args.num_layers, input_keep_prob=args.input_keep_prob,
+                      output_keep_prob=args.output_keep_prob)
+    return CharRNN(cfg, device=device, seed=args.seed, dtype=getattr(args, "dtype", "auto"))
+
+
+def train(args: argparse.Namespace) -> int:
+    topo = topology.from_args(args)
+    if topo.role == "ps":
+        return process_group.run_ps(topo)
+    device = process_group.pick_device(topo, getattr(args, "device", "auto"))
+    ctx = process_group.init(topo, device, getattr(args, "dist_backend", "auto"),
+                             getattr(args, "dist_timeout", 600.0))
+    rank = max(ctx.rank, 0)
+    chief = rank == 0
+    try:
+        return _train(args, ctx, device, rank, chief)
+    finally:
+        ctx.shutdown()
+
+
+def _train(args, ctx, device, rank: int, chief: bool) -> int:
+    loader = make_loader(args, ctx)
+    args.vocab_size = loader.vocab_size
+    prefix: Optional[str] = None
+    if args.init_from is not None:
+        prefix = check_init_from(args, loader)
+    elif ctx.world_size > 1 and ckpt.latest_checkpoint(args.save_dir):
+        # MonitoredTrainingSession's chief auto-restores from checkpoint_dir (train.py:157-163)
+        prefix = ckpt.latest_checkpoint(args.save_dir)
+
+    if chief:
+        os.makedirs(args.save_dir, exist_ok=True)
+        safe_pickle.dump(args, os.path.join(args.save_dir, "config.pkl"))
+        safe_pickle.dump((tuple(loader.chars), dict(loader.vocab)),
+                         os.path.join(args.save_dir, "chars_vocab.pkl"))
+
+    model = build_model(args, loader.vocab_size, device)
+    opt = TFAdam(model.store, clip=args.grad_clip)
+    global_step = 0
+    start_epoch, start_batch = 0, 0
+    if prefix is not None:
+        sd = restore(model, opt, prefix)
+        global_step = int(sd.get("global_step", 0))
+        if getattr(args, "resume_exact", False):
+            start_epoch = int(sd.get("dcr/epoch", 0))
+            start_batch = int(sd.get("dcr/batch_pointer", -1)) + 1
+        _log(f"restored {prefix} (global_step {global_step})", rank)
+
+    sync = GradSync(model.store, ctx.world_size, getattr(args, "bucket_mb", 8.0),
+                    getattr(args, "allreduce_dtype", "fp32"))
+    if ctx.world_size > 1:
+        sync.broadcast_params(0)
+        ctx.broadcast_(opt.m)
+        ctx.broadcast_(opt.v)
+        model.params_changed()
+    ctx.start_heartbeat(getattr(args, "heartbeat", 0.0))
+
+    nb = ctx.min_int(loader.num_batches)
+    if nb != loader.num_batches:
+        _log(f"equalising steps per epoch across ranks: {loader.num_batches} -> {nb}", rank)
+    total = args.num_epochs * nb
+    saver = ckpt.Saver(max_to_keep=5)
+    logger = MetricsLogger(args.log_dir, enabled=chief, jsonl_path=getattr(args, "metrics_file", None))
+    prof = PhaseProfiler(getattr(args, "profile", False), device)
+    chars_per_step = args.batch_size * args.seq_length * ctx.world_size
+    log_every = max(1, getattr(args, "log_every", 1))
+    summary_every = getattr(args, "summary_every", 100)
+    max_steps = getattr(args, "max_steps", 0)
+    steps_done = 0
+    pending = None  # (global_step, epoch, loss_tensor, t_start)
+    last_t = time.time()
+
+    def flush(p, now):
+        nonlocal last_t
+        gs, e, loss_t, t0 = p
+        dt = now - t0
+        loss = float(loss_t)
+        if chief and (gs % log_every == 0 or gs == total):
+            print(progress_line(gs, total, e, loss, dt, chars_per_step / max(dt, 1e-9)), flush=True)
+        logger.log({"step": gs, "epoch": e, "loss": loss, "time_per_batch": dt,
+                    "chars_per_sec": chars_per_step / max(dt, 1e-9), "rank_world": ctx.world_size})
+        logger.scalar("train_loss", loss, gs)
+
+    stop = False
+    state = None
+    for e in range(start_epoch, args.num_epochs):
+        lr = lr_for_epoch(args.learning_rate, args.decay_rate, e)
+        loader.reset_batch_pointer()
+        state = model.zero_state(args.batch_size)
+        b0 = start_batch if e == start_epoch else 0
+        if b0:
+            loader.pointer = b0
+        for b in range(b0, nb):
+            t0 = time.time()
+            x, y = loader.next_batch()
+            want = chief and summary_every > 0 and (global_step % summary_every == 0)
+            with prof.phase("fwd_bwd"):
+                loss_t, state, extras = _step(model, x, y, state, sync, want)
+            with prof.phase("grad_sync"):
+                sync.finish()
+            with prof.phase("optimizer"):
+                opt.step(lr)
+            global_step += 1
+            steps_done += 1
+            if pending is not None:
+                flush(pending, t0)
+            pending = (global_step, e, loss_t, t0)
+            if want and extras:
+                if extras.get("logits") is not None:
+                    logger.histogram("logits", extras["logits"].float().cpu().numpy(), global_step)
+                if extras.get("loss") is not None:
+                    logger.histogram("loss", extras["loss"].float().cpu().numpy(), global_step)
+            step_idx = e * nb + b
+            last = (e == args.num_epochs - 1 and b == nb - 1)
+            if max_steps and steps_done >= max_steps:
+                last, stop = True, True
+            if step_idx % args.save_every == 0 or last:
+                if pending is not None:
+                    flush(pending, time.time())
+                    pending = None
+                if chief:
+                    tensors = checkpoint_tensors(model, opt, global_step, lr, e, b,
+                                                 state if getattr(args, "save_state", False) else None)
+                    path = saver.save(args.save_dir, tensors, step_idx)
+                    print("model saved to {}".format(os.path.join(args.save_dir, "model.ckpt")),
+                          flush=True)
+                    logger.log({"step": global_step, "saved": path})
+            if stop:
+                break
+        if stop:
+            break
+    if pending is not None:
+        flush(pending, time.time())
+    if prof.enabled and chief:
+        print(prof.table(), flush=True)
+    logger.close()
+    return 0
+
+
+def _step(model: CharRNN, x, y, state, sync: GradSync, want_extras: bool):
+    sync.reset()
+    loss, new_state, extras = model.train_step(x, y, state, sync, want_extras=want_extras)
+    return loss, new_state, (extras if want_extras else None)
+
+
+def main(argv=None) -> int:
+    from ..utils.config import train_parser
+
+    args = train_parser().parse_args(argv)
+    return train(args)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,74 @@
+"""``CharRNN``: the model facade used by the trainer, sampler and benchmark.
+
+Equivalent of the reference ``Model`` (model.py:8-140) minus the TF graph: parameters live in a
+:class:`ParamStore` (flat fp32 buffers, TF names) and execution is delegated to a backend:
+
+* ``native``    -- gfx950 HIP kernels (engine/native_backend.py): fused recurrent cell
+                   kernels, fused softmax-CE, embedding-projection gather/segment-sum, etc.
+                   Mandatory on GPU; raises if the native library is missing.
+* ``reference`` -- pure PyTorch autograd with TF cell semantics (models/reference.py); the
+                   CPU path and the numerical oracle.
+
+``Model.__init__`` in the reference mutates the caller's args to B = T = 1 for inference
+(model.py:11-13); here inference simply calls :meth:`step_logits` with any batch.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .params import ModelConfig, ParamStore
+from .reference import ReferenceBackend, State, zero_state
+
+
+def _as_ids(x, device: torch.device) -> torch.Tensor:
+    if isinstance(x, torch.Tensor):
+        return x.to(device=device, dtype=torch.int32, non_blocking=True)
+    t = torch.from_numpy(np.ascontiguousarray(x, dtype=np.int32))
+    if device.type == "cuda":
+        t = t.pin_memory()
+    return t.to(device, non_blocking=True)
+
+
+class CharRNN:
+    def __init__(self, cfg: ModelConfig, device="cpu", seed: Optional[int] = 0,
+                 backend: str = "auto", dtype: str = "auto"):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.store = ParamStore(cfg, self.device, seed)
+        if backend == "auto":
+            backend = "native" if self.device.type == "cuda" else "reference"
+        self.backend_name = backend
+        if backend == "native":
+            from ..engine.native_backend import NativeBackend
+
+            self.backend = NativeBackend(self.store, dtype=dtype, seed=seed or 0)
+        elif backend == "reference":
+            self.backend = ReferenceBackend(self.store, seed=seed or 0)
+        else:
+            raise ValueError(f"unknown backend {backend}")
+
+    def zero_state(self, batch: int) -> State:
+        return zero_state(self.cfg, batch, self.device)
+
+    def train_step(self, x, y, state: State, grad_sync=None, want_extras: bool = False):
+        """One TBPTT step: forward, loss, backward into ``store.grad``.  ``grad_sync.ready``
+        is called as gradient ranges become final.  Returns (cost tensor, final_state,
+        extras)."""
+        xi, yi = _as_ids(x, self.device), _as_ids(y, self.device)
+        cb = grad_sync.ready if grad_sync is not None else None
+        return self.backend.train_step(xi, yi, state, cb, want_extras=want_extras)
+
+    def step_logits(self, x_t, state: State):
+        return self.backend.step_logits(_as_ids(x_t, self.device), state)
+
+    def eval_loss(self, x, y, state: State):
+        return self.backend.eval_loss(_as_ids(x, self.device), _as_ids(y, self.device), state)
+
+    def params_changed(self):
+        """Call after parameters were modified outside the optimizer (restore/broadcast)."""
+        hook = getattr(self.backend, "params_changed", None)
+        if hook is not None:
+            hook()

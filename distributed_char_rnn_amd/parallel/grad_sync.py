@@ -1,0 +1,97 @@
+"""Bucketed, backward-overlapped gradient all-reduce over the flat gradient buffer.
+
+Replaces the reference's per-step worker->PS gradient push + PS-side ApplyAdam (CS3/CS4 of
+SURVEY.md §2.4, model.py:98 under replica_device_setter, train.py:132-133) with synchronous
+data parallelism: every rank keeps a full replica, gradients are summed with RCCL all-reduce
+and every rank applies the identical clipped Adam update.
+
+The flat gradient buffer is laid out in reverse backward-availability order (softmax head,
+top layer, ..., layer 0, embedding; models/params.py), so buckets are *contiguous slices*.
+The backend calls :meth:`ready(upto)` when every gradient below flat offset ``upto`` is final;
+all buckets completely below it are launched immediately as async all-reduces on RCCL's own
+stream (which orders itself after the work already queued on the compute stream), so the
+head's and upper layers' communication overlaps the BPTT of lower layers.  :meth:`finish`
+joins the outstanding work and averages.
+
+Bucket sizing (``--bucket_mb``): xGMI is point-to-point, 7 links x ~153 GB/s per MI355X; a
+ring all-reduce of S bytes on N GPUs moves 2(N-1)/N·S per link, so an 8 MB bucket is ~90 us of
+wire time on 8 GPUs -- large enough to amortise RCCL's per-call latency (~10-30 us), small
+enough that the first bucket starts while BPTT of the lower layers still has >=1 ms to run.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from ..models.params import ParamStore
+
+
+class GradSync:
+    def __init__(self, store: ParamStore, world_size: int, bucket_mb: float = 8.0,
+                 wire_dtype: str = "fp32", group=None, enabled: Optional[bool] = None):
+        self.store = store
+        self.world = world_size
+        self.group = group
+        self.enabled = (world_size > 1) if enabled is None else enabled
+        self.wire_bf16 = wire_dtype == "bf16"
+        self.buckets = self._make_buckets(bucket_mb)
+        self._next = 0
+        self._work: List[Tuple[object, int, int, Optional[torch.Tensor]]] = []
+
+    def _make_buckets(self, bucket_mb: float) -> List[Tuple[int, int]]:
+        """Cut the flat buffer at tensor boundaries into ~bucket_mb slices."""
+        cap = max(1, int(bucket_mb * (1 << 20) / 4))
+        cuts, lo, cur = [], 0, 0
+        for s in self.store.specs:
+            end = s.offset + s.numel
+            cur = end
+            if cur - lo >= cap:
+                cuts.append((lo, cur))
+                lo = cur
+        if cur > lo:
+            cuts.append((lo, cur))
+        # the flat buffer may have alignment padding at the end: cover it in the last bucket
+        if cuts:
+            cuts[-1] = (cuts[-1][0], self.store.numel)
+        return cuts
+
+    def reset(self):
+        self._next = 0
+        self._work.clear()
+
+    def ready(self, upto: Optional[int] = None):
+        """Launch every not-yet-launched bucket that ends at or below flat offset ``upto``
+        (``None`` = everything)."""
+        if not self.enabled:
+            return
+        lim = self.store.numel if upto is None else upto
+        while self._next < len(self.buckets) and self.buckets[self._next][1] <= lim:
+            lo, hi = self.buckets[self._next]
+            g = self.store.grad[lo:hi]
+            if self.wire_bf16:
+                wire = g.to(torch.bfloat16)
+                w = dist.all_reduce(wire, group=self.group, async_op=True)
+                self._work.append((w, lo, hi, wire))
+            else:
+                w = dist.all_reduce(g, group=self.group, async_op=True)
+                self._work.append((w, lo, hi, None))
+            self._next += 1
+
+    def finish(self):
+        """Wait for all buckets and average (sum / world)."""
+        if not self.enabled:
+            return
+        self.ready(None)
+        for w, lo, hi, wire in self._work:
+            w.wait()
+            if wire is not None:
+                self.store.grad[lo:hi].copy_(wire)
+        self._work.clear()
+        self._next = 0
+        self.store.grad.mul_(1.0 / self.world)
+
+    def broadcast_params(self, src: int = 0):
+        if self.enabled:
+            dist.broadcast(self.store.flat, src, group=self.group)

@@ -1,0 +1,43 @@
+"""Numerics of the fused global-norm clip + TF-Adam kernel (csrc/optim.hip) against a plain
+PyTorch fp32 reference of TF 1.x `clip_by_global_norm` + `AdamOptimizer` (model.py:91-98)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(p, g, m, v, lr, b1, b2, eps, clip, t):
+    norm = torch.sqrt((g.double() ** 2).sum()).float()
+    s = clip / max(norm.item(), clip) if clip > 0 else 1.0
+    g = g * s
+    lr_t = lr * math.sqrt(1 - b2 ** t) / (1 - b1 ** t)
+    m = b1 * m + (1 - b1) * g
+    v = b2 * v + (1 - b2) * g * g
+    p = p - lr_t * m / (torch.sqrt(v) + eps)
+    return p, m, v, norm
+
+
+@pytest.mark.parametrize("n", [1, 7, 4096, 1 << 20, 4265025])
+@pytest.mark.parametrize("clip", [5.0, 0.01, 0.0])
+def test_adam_clip_matches_reference(dcr_ops, n, clip):
+    torch.manual_seed(0)
+    dev = "cuda"
+    p = torch.randn(n, device=dev)
+    g = torch.randn(n, device=dev) * 0.1
+    m = torch.randn(n, device=dev) * 0.01
+    v = torch.rand(n, device=dev) * 0.01
+    pbf = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    parts = torch.empty(dcr_ops.opt_num_partials(n), device=dev)
+    norm = torch.empty(1, device=dev)
+    lr, b1, b2, eps, t = 2e-3, 0.9, 0.999, 1e-8, 3
+    rp, rm, rv, rn = _ref(p.clone(), g.clone(), m.clone(), v.clone(), lr, b1, b2, eps, clip, t)
+    lr_t = lr * math.sqrt(1 - b2 ** t) / (1 - b1 ** t)
+    dcr_ops.adam_clip(p, g, m, v, pbf, parts, norm, lr_t, b1, b2, eps, clip)
+    torch.cuda.synchronize()
+    assert torch.allclose(norm.cpu(), rn.cpu(), rtol=1e-5)
+    torch.testing.assert_close(m, rm, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(v, rv, rtol=1e-5, atol=1e-9)
+    torch.testing.assert_close(p, rp, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(pbf.float(), p.to(torch.bfloat16).float(), rtol=0, atol=0)
