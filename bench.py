@@ -1,0 +1,149 @@
+#!/usr/bin/env python
+"""Headline benchmark: whole-node training throughput (chars/sec) of the 2-layer LSTM-512,
+seq 128, vocab 65 char-RNN (BASELINE.json), bf16, synthetic Shakespeare-shaped text,
+random-init weights, synchronous data parallel over RCCL (one process per GPU).
+
+    python bench.py --gpus 1 --steps 20 --warmup 5
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29500 bench.py --gpus 8 --steps 20 --warmup 5
+
+Each timed step is a complete training step of the framework: device batch of token ids ->
+forward (fused HIP recurrent kernels) -> fused softmax-CE -> BPTT -> bucketed gradient
+all-reduce (RCCL) -> fused global-norm clip + TF-Adam -> weights refreshed for the next step,
+with the TBPTT state carried across steps as in train.py.  Per-GPU batch is fixed as N grows
+(weak scaling).  Rank 0 prints ONE JSON line; the time is the max over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+METRIC = "chars/sec (whole node), 2-layer LSTM-512 seq128, at 1/2/4/8 MI355X"
+MIOPEN_1GPU_CPS = 2098017.9  # torch.nn.LSTM (MIOpen) bf16, B=256, same config, 1x MI355X
+                             # (scripts/bench_miopen_lstm.py)
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch (sequences)")
+    ap.add_argument("--seq", type=int, default=128)
+    ap.add_argument("--hidden", type=int, default=512)
+    ap.add_argument("--layers", type=int, default=2)
+    ap.add_argument("--vocab", type=int, default=65)
+    ap.add_argument("--model", default="lstm")
+    ap.add_argument("--bucket_mb", type=float, default=8.0)
+    ap.add_argument("--allreduce_dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--profile", action="store_true", help="print a per-phase timing table")
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    a = parse(argv)
+    from distributed_char_rnn_amd.engine.optim import TFAdam
+    from distributed_char_rnn_amd.models.char_rnn import CharRNN
+    from distributed_char_rnn_amd.models.params import ModelConfig
+    from distributed_char_rnn_amd.parallel import process_group, topology
+    from distributed_char_rnn_amd.parallel.grad_sync import GradSync
+    from distributed_char_rnn_amd.utils.data import synthetic_tokens
+
+    topo = topology.from_env() or topology.Topology()
+    if topo.world_size != a.gpus:
+        if a.gpus > 1 and topo.world_size == 1:
+            print(f"--gpus {a.gpus} needs torch.distributed.run with {a.gpus} processes",
+                  file=sys.stderr)
+            return 2
+    device = process_group.pick_device(topo, "cuda")
+    ctx = process_group.init(topo, device, "nccl" if device.type == "cuda" else "gloo")
+    rank, world = max(ctx.rank, 0), ctx.world_size
+
+    cfg = ModelConfig(model=a.model, vocab_size=a.vocab, rnn_size=a.hidden, num_layers=a.layers)
+    model = CharRNN(cfg, device=device, seed=1234)
+    opt = TFAdam(model.store, clip=5.0)
+    sync = GradSync(model.store, world, a.bucket_mb, a.allreduce_dtype)
+    sync.broadcast_params(0)
+    model.params_changed()
+
+    B, T = a.batch, a.seq
+    nbat = 16
+    toks = synthetic_tokens(nbat * B * T + 1, a.vocab, seed=1000 + rank)
+    data = torch.from_numpy(toks).to(device)
+    xs = data[:-1].view(B, nbat * T)          # row-contiguous streams like TextLoader
+    ys = data[1:].view(B, nbat * T)
+    state = model.zero_state(B)
+    prof = None
+    if a.profile:
+        from distributed_char_rnn_amd.utils.metrics import PhaseProfiler
+
+        prof = PhaseProfiler(True, device)
+
+    def step(i, state):
+        k = i % nbat
+        x = xs[:, k * T:(k + 1) * T]
+        y = ys[:, k * T:(k + 1) * T]
+        if k == 0:
+            state = model.zero_state(B)
+        sync.reset()
+        if prof is None:
+            loss, state, _ = model.train_step(x, y, state, sync)
+            sync.finish()
+            opt.step(2e-3)
+        else:
+            with prof.phase("fwd_bwd"):
+                loss, state, _ = model.train_step(x, y, state, sync)
+            with prof.phase("grad_sync"):
+                sync.finish()
+            with prof.phase("optimizer"):
+                opt.step(2e-3)
+        return loss, state
+
+    for i in range(a.warmup):
+        loss, state = step(i, state)
+    torch.cuda.synchronize()
+    if prof is not None:
+        prof.collect()
+        prof.totals.clear()
+        prof.counts.clear()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        loss, state = step(a.warmup + i, state)
+    ctx.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    dt = ctx.all_reduce_scalar(dt, dist.ReduceOp.MAX) if world > 1 else dt
+    final_loss = float(loss)
+    ms = dt / a.steps * 1e3
+    cps = world * B * T * a.steps / dt
+    if rank == 0:
+        if prof is not None:
+            print(prof.table(), file=sys.stderr)
+        out = {
+            "metric": METRIC, "value": cps, "unit": "chars/sec", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16", "data": "synthetic (Shakespeare-unigram token stream, random-init weights)",
+            "config": {"model": f"{a.layers}-layer {a.model.upper()}-{a.hidden} (vocab {a.vocab})",
+                       "global_batch": B * world, "per_gpu_batch": B, "seq_len": T,
+                       "parallelism": f"dp{world}"},
+            "vs_torch_nn_lstm_miopen": (cps / (MIOPEN_1GPU_CPS * world)
+                                        if (a.model, a.hidden, a.layers, T, B) ==
+                                        ("lstm", 512, 2, 128, 256) else None),
+            "final_loss": final_loss,
+        }
+        print(json.dumps(out), flush=True)
+    ctx.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

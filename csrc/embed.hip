@@ -1,0 +1,121 @@
+// Segmented (by token id) row sums: out[v][c] = sum_{n : ids[n] == v} X[n][c].
+//
+// Reference: the embedding gradient of `tf.nn.embedding_lookup` is an IndexedSlices
+// ([B*T, H] values + ids) that TF densifies with UnsortedSegmentSum before Adam (model.py:55,
+// 91-98; K2 of SURVEY.md §2.3).  With V = 65 every id repeats ~500x per batch, so global atomics
+// would serialise on 65 hot rows.  Here each workgroup owns a (row chunk, 128-column strip),
+// accumulates into an LDS-resident [V x 128] fp32 tile with LDS atomics, and writes one partial
+// per row chunk; a second pass sums the partials in a fixed order (bitwise reproducible).
+//
+// Uses in the native backend:
+//  * layer-0 fusion: Zx0 = (E·W_x0 + b0)[ids], so the backward needs dEW = segsum(dZ0, ids)
+//    [V, G·H] and then dE = dEW·W_x0ᵀ, dW_x0 = Eᵀ·dEW, db0 = colsum(dEW) -- all tiny;
+//  * dropout path: dE = segsum(dX0, ids);
+//  * bias gradients: ids == nullptr puts every row in bucket 0 (a column sum).
+// Large vocabularies (V > kSegLdsMaxV) use fp32 global atomics into a zeroed output instead.
+#include "common.h"
+#include "kernels.h"
+
+namespace dcr {
+
+constexpr int kSegThreads = 256;
+constexpr int kSegCols = 128;
+constexpr int kSegLdsMaxV = 96;
+
+template <typename T>
+__global__ void __launch_bounds__(kSegThreads) segsum_lds_kernel(
+    const T* __restrict__ X, int ldx, const int* __restrict__ ids, int N, int W, int V,
+    int rows_per_chunk, float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float acc[];  // [V][kSegCols]
+  const int c0 = blockIdx.x * kSegCols;
+  const int chunk = blockIdx.y;
+  for (int i = threadIdx.x; i < V * kSegCols; i += kSegThreads) acc[i] = 0.f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // each lane owns columns c0+lane and c0+64+lane: a wave reads 64 consecutive elements per
+  // row per access (coalesced for any width/stride, odd vocabularies included)
+  const int ca = c0 + lane, cb = c0 + 64 + lane;
+  const bool va = ca < W, vb = cb < W;
+  const int r0 = chunk * rows_per_chunk;
+  const int r1 = min(N, r0 + rows_per_chunk);
+  for (int n = r0 + wave; n < r1; n += kSegThreads / 64) {
+    const int v = ids ? ids[n] : 0;
+    const T* row = X + (size_t)n * ldx;
+    if (va) atomicAdd(&acc[v * kSegCols + lane], (float)row[ca]);
+    if (vb) atomicAdd(&acc[v * kSegCols + 64 + lane], (float)row[cb]);
+  }
+  __syncthreads();
+  float* out = partial + (size_t)chunk * V * W;
+  for (int i = threadIdx.x; i < V * kSegCols; i += kSegThreads) {
+    const int v = i / kSegCols, cc = c0 + (i % kSegCols);
+    if (cc < W) out[(size_t)v * W + cc] = acc[i];
+  }
+}
+
+__global__ void __launch_bounds__(kSegThreads) segsum_reduce_kernel(const float* __restrict__ partial,
+                                                                   int nchunks, int64_t VW,
+                                                                   float* __restrict__ out,
+                                                                   int accumulate) {
+  for (int64_t i = blockIdx.x * (int64_t)kSegThreads + threadIdx.x; i < VW;
+       i += (int64_t)gridDim.x * kSegThreads) {
+    float s = 0.f;
+    for (int k = 0; k < nchunks; ++k) s += partial[(size_t)k * VW + i];
+    out[i] = accumulate ? out[i] + s : s;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kSegThreads) segsum_atomic_kernel(const T* __restrict__ X, int ldx,
+                                                                   const int* __restrict__ ids,
+                                                                   int N, int W,
+                                                                   float* __restrict__ out) {
+  const int n = blockIdx.y;
+  const int v = ids ? ids[n] : 0;
+  for (int c = blockIdx.x * kSegThreads + threadIdx.x; c < W; c += gridDim.x * kSegThreads)
+    atomicAdd(out + (size_t)v * W + c, (float)X[(size_t)n * ldx + c]);
+}
+
+int segsum_rows_per_chunk(int N) {
+  // ~16-32 chunks for large N: enough blocks to fill the chip with few partials
+  int r = (N + 31) / 32;
+  r = ((r + 255) / 256) * 256;
+  return r < 256 ? 256 : r;
+}
+
+size_t segsum_workspace_floats(int N, int W, int V) {
+  if (V > kSegLdsMaxV) return 0;
+  const int rpc = segsum_rows_per_chunk(N);
+  const int nchunks = (N + rpc - 1) / rpc;
+  return (size_t)nchunks * V * W;
+}
+
+template <typename T>
+static void launch_segsum_t(const T* X, int ldx, const int* ids, int N, int W, int V, float* out,
+                            float* workspace, int accumulate, hipStream_t s) {
+  if (V > kSegLdsMaxV) {
+    if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float) * (size_t)V * W, s);
+    dim3 grid((W + kSegThreads - 1) / kSegThreads, N);
+    segsum_atomic_kernel<T><<<grid, kSegThreads, 0, s>>>(X, ldx, ids, N, W, out);
+    return;
+  }
+  const int rpc = segsum_rows_per_chunk(N);
+  const int nchunks = (N + rpc - 1) / rpc;
+  dim3 grid((W + kSegCols - 1) / kSegCols, nchunks);
+  const size_t lds = sizeof(float) * V * kSegCols;
+  segsum_lds_kernel<T><<<grid, kSegThreads, lds, s>>>(X, ldx, ids, N, W, V, rpc, workspace);
+  const int64_t VW = (int64_t)V * W;
+  int nb = (int)((VW + kSegThreads - 1) / kSegThreads);
+  if (nb > 2048) nb = 2048;
+  segsum_reduce_kernel<<<nb, kSegThreads, 0, s>>>(workspace, nchunks, VW, out, accumulate);
+}
+
+void launch_segsum_bf16(const bf16* X, int ldx, const int* ids, int N, int W, int V, float* out,
+                        float* workspace, int accumulate, hipStream_t s) {
+  launch_segsum_t<bf16>(X, ldx, ids, N, W, V, out, workspace, accumulate, s);
+}
+void launch_segsum_f32(const float* X, int ldx, const int* ids, int N, int W, int V, float* out,
+                       float* workspace, int accumulate, hipStream_t s) {
+  launch_segsum_t<float>(X, ldx, ids, N, W, V, out, workspace, accumulate, s);
+}
+
+}  // namespace dcr

@@ -16,4 +16,89 @@ void launch_adam_clip(float* p, const float* g, float* m, float* v, bf16* pbf, i
                       float* partials, float* norm_out, float lr_t, float b1, float b2, float eps,
                       float clip, hipStream_t stream);
 
+// ---- rnn_step.hip -----------------------------------------------------------------------
+enum CellKind { CELL_LSTM = 0, CELL_GRU_A = 1, CELL_GRU_B = 2, CELL_RNN = 3, CELL_NAS = 4 };
+
+struct FwdStepArgs {
+  const bf16* WT;        // [G*H, H] bf16: transposed recurrent weights (row = gate column)
+  const float* zx;       // [B, zx_ld] fp32 input projection (+bias) of this step, or the
+                         // [V, zx_ld] E·W_x table when ids != nullptr (layer-0 gather mode)
+  const int* ids;        // [B] token ids of this step (gather mode) or nullptr
+  int zx_ld, zx_off;     // row stride and column offset of this cell's gate block in zx
+  const bf16* hop;       // [B, H] bf16 MFMA B-operand (h_{t-1}; r*h for GRU_B)
+  const float* hprev32;  // [B, H] fp32 h_{t-1} (GRU)
+  const float* cprev;    // [B, H] fp32 c_{t-1} (LSTM, NAS)
+  bf16* hout;            // [B, H] bf16 h_t
+  float* hout32;         // [B, H] fp32 h_t (GRU always; others optional)
+  float* cout;           // [B, H] fp32 c_t (LSTM, NAS)
+  bf16* gates;           // [B, gates_ld] bf16 activation cache for backward
+  float* pre;            // NAS: [B, gates_ld] fp32 pre-activations
+  float* aux;            // NAS: [B, H] fp32 recurrent branch-3 pre-activation
+  bf16* rh;              // GRU_A: [B, H] bf16 r*h_{t-1}
+  int gates_ld;
+  int B, H;
+  float forget_bias;
+};
+
+struct BwdStepArgs {
+  const bf16* W;         // [H, K] bf16 recurrent weights in TF layout (row = unit, k contiguous)
+  const bf16* dz_next;   // [B, dz_ld] bf16 GEMM operand (dZ of step t+1), nullptr => no GEMM
+  int K, dz_ld;
+  const float* dtop;     // [B, H] fp32 gradient arriving from above/the loss at this step
+  const bf16* gates;     // [B, gates_ld] activation cache
+  const float* pre;      // NAS pre-activations [B, gates_ld]
+  const float* aux;      // NAS zm3 [B, H]
+  const float* zx3;      // NAS: input branch 3 pre-activation, row stride zx3_ld
+  int zx3_ld;
+  const float* c;        // [B, H] c_t
+  const float* cprev;    // [B, H] c_{t-1}
+  const float* hprev32;  // GRU h_{t-1}
+  const bf16* hcur;      // RNN h_t
+  float* dc;             // [B, H] fp32 carry: dc (LSTM/NAS), dh' (GRU)
+  float* partial;        // GRU [B, H] fp32 partial dh_{t-1}
+  bf16* dz_out;          // [B, dz_out_ld] bf16 dZ_t (NAS: recurrent-branch dZm)
+  bf16* dzx_out;         // NAS: input-branch dZx
+  int dz_out_ld, gates_ld;
+  int B, H;
+};
+
+void launch_fwd_step(int cell, const FwdStepArgs& a, hipStream_t s);
+void launch_bwd_step(int cell, const BwdStepArgs& a, hipStream_t s);
+
+// ---- xent.hip ---------------------------------------------------------------------------
+int xent_num_partials(int N);
+void launch_xent(const float* logits, const int* targets, int N, int V, float grad_scale,
+                 float* row_loss, bf16* dlogits, float* partial, float* loss_out, hipStream_t s);
+
+// ---- embed.hip --------------------------------------------------------------------------
+int segsum_rows_per_chunk(int N);
+size_t segsum_workspace_floats(int N, int W, int V);
+void launch_segsum_bf16(const bf16* X, int ldx, const int* ids, int N, int W, int V, float* out,
+                        float* workspace, int accumulate, hipStream_t s);
+void launch_segsum_f32(const float* X, int ldx, const int* ids, int N, int W, int V, float* out,
+                       float* workspace, int accumulate, hipStream_t s);
+
+// ---- lstm_persist.hip -------------------------------------------------------------------
+struct PersistArgs {
+  const bf16* W;         // fwd: W_hᵀ [4H, H]; bwd: W_h [H, 4H] (TF layout)
+  const float* zx;       // fwd: [T, B, zx_ld] input projection, or [V, zx_ld] table with ids
+  const int* ids;        // fwd gather mode: [T, B] token ids
+  int zx_ld;
+  bf16* hbuf;            // [T+1, B, H] bf16 (slot 0 = h_0)
+  float* cbuf;           // [T+1, B, H] fp32 (slot 0 = c_0)
+  bf16* gates;           // [T, B, 4H] bf16 activation cache (sigma(i), tanh(j), sigma(f), sigma(o))
+  float* hlast32;        // [B, H] fp32 final h
+  const float* dtop;     // bwd: [T, B, H] fp32 gradient from above
+  bf16* dz;              // bwd: [T, B, 4H] bf16 gate-pre-activation gradients
+  unsigned* cnt;         // [B/16, T+1] arrival counters (zeroed by the launcher)
+  unsigned* err;         // timeout / error word (0 = ok)
+  int B, H, T;
+  float forget_bias;
+  unsigned spin_limit;
+};
+int lstm_persist_supported(int H, int B, int cus);
+int lstm_persist_grid(int H, int B, int cus);
+void launch_lstm_fwd_persist(const PersistArgs& a, int cus, hipStream_t s);
+void launch_lstm_bwd_persist(const PersistArgs& a, int cus, hipStream_t s);
+
 }  // namespace dcr

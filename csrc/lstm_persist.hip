@@ -1,0 +1,360 @@
+// Persistent, weights-resident LSTM recurrence (forward and BPTT) for gfx950.
+//
+// Reference: TF's statically unrolled LSTMCell chain (model.py:61-73) and its tf.gradients
+// backward: per time step and layer one cuBLAS GEMM + ~11 pointwise kernels (K4/K5/K12 of
+// SURVEY.md §2.3).  The per-step kernels in rnn_step.hip already fuse GEMM + cell, but they
+// re-stream W_h from L2 every step and pay a launch boundary per step; this file removes both.
+//
+// Decomposition.  One launch runs all T steps of one layer.  Workgroup (ubk, bg) owns UB*16
+// hidden units x 16 batch rows for the whole sequence.  Its 4 waves split the GEMM's K range in
+// four and keep their slice of the recurrent weights RESIDENT IN VGPRs as ready-made MFMA A
+// fragments (mfma_f32_16x16x32_bf16, swapped operands: A = weight rows, B = batch rows), so a
+// step streams only activations:
+//   fwd: z[b][g*H+u] = sum_k h_{t-1}[b][k] * W_h[k][g*H+u]      (K = H,  A = W_hᵀ rows)
+//   bwd: dh[b][u]    = sum_k dZ_{t+1}[b][k] * W_h[u][k]          (K = 4H, A = W_h rows)
+// The four K-partials meet in LDS; one wave per 16-unit block runs the fused cell epilogue with
+// the cell state c (fwd) / the carry dc (bwd) held in registers across all T steps.
+//
+// Cross-workgroup hand-off (h_t in fwd, dZ_t in bwd) follows the placement-independent form of
+// cdna_hip_programming.md §6 Guideline 16 / MI355X_MICROARCH.md "Valid forms" row 1, with no
+// acquire/release fences: every handed-off byte is stored `sc1` (write-through) by the single
+// storing wave, which drains with `s_waitcnt vmcnt(0)` before ONE lane does an agent-scope
+// atomic add on the (batch group, step) counter; ONE lane of each consumer polls that counter
+// with `sc1` loads (+ s_sleep), the workgroup barrier releases the other waves, and EVERY load
+// of handed-off bytes is a `buffer_load ... sc1`.  Counters are zeroed by a memset node before
+// every launch; every spin is bounded and a timeout sets an error word and drains the grid.
+// Residency: the host only launches when the whole grid fits (<= 2 workgroups per CU here) and
+// otherwise falls back to the per-step kernels.
+#include "common.h"
+#include "kernels.h"
+
+namespace dcr {
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kAuxSc1 = 16;  // buffer-op cache-policy bits: sc1 (bypass L1, write-through)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, size_t bytes) {
+  const unsigned n = bytes > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (unsigned)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, n, 0x00020000);
+}
+__device__ __forceinline__ bf16x8 ld8_sc1(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, kAuxSc1);
+  return __builtin_bit_cast(bf16x8, v);
+}
+__device__ __forceinline__ void st4bf_sc1(bf16* p, float a, float b, float c, float d) {
+  bf16x4 v;
+  v[0] = f2bf(a); v[1] = f2bf(b); v[2] = f2bf(c); v[3] = f2bf(d);
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), __builtin_bit_cast(uint64_t, v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st4bf(bf16* p, float a, float b, float c, float d) {
+  bf16x4 v;
+  v[0] = f2bf(a); v[1] = f2bf(b); v[2] = f2bf(c); v[3] = f2bf(d);
+  *reinterpret_cast<bf16x4*>(p) = v;
+}
+__device__ __forceinline__ void ld4bf(const bf16* p, float (&o)[4]) {
+  const bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+  o[0] = (float)v[0]; o[1] = (float)v[1]; o[2] = (float)v[2]; o[3] = (float)v[3];
+}
+__device__ __forceinline__ void ld4f(const float* p, float (&o)[4]) {
+  const float4 v = *reinterpret_cast<const float4*>(p);
+  o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+}
+
+// One lane of the workgroup polls `*cnt >= target` (relaxed agent-scope = sc1 loads); the
+// result is broadcast through LDS by the barrier that follows.  Returns false on timeout.
+__device__ __forceinline__ bool poll_counter(unsigned* cnt, unsigned target, unsigned limit,
+                                             unsigned* err, unsigned code) {
+  unsigned spins = 0;
+  while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    if (++spins > limit) {
+      __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+
+__device__ __forceinline__ void arrive(unsigned* cnt) {
+  // every store of this wave must be complete (write-through) before the counter moves
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------------
+template <int KS, int UB>  // KS = k-steps (of 32) per wave = H/128; UB = 16-unit blocks per WG
+__global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a) {
+  __shared__ __attribute__((aligned(16))) float part[4][UB][64][16];
+  __shared__ int ok_flag;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int H = a.H, B = a.B, T = a.T;
+  const int nwg_u = H / (16 * UB);
+  const int ubk = blockIdx.x % nwg_u, bg = blockIdx.x / nwg_u;
+  const int ub0 = ubk * 16 * UB, b0 = bg * 16;
+  const int kq = 8 * (lane >> 4);
+  const int kbase = w * (KS * 32);
+  unsigned* cnt = a.cnt + (size_t)bg * (T + 1);
+
+  // resident A fragments: rows g*H + ub + (lane&15) of W_hᵀ, this wave's K quarter
+  bf16x8 wf[UB][4][KS];
+#pragma unroll
+  for (int ui = 0; ui < UB; ++ui)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        wf[ui][g][s] = ld8(a.W + (size_t)(g * H + ub0 + ui * 16 + (lane & 15)) * H + kbase +
+                           s * 32 + kq);
+
+  const int b = b0 + (lane & 15);
+  const unsigned hoff = (unsigned)(((size_t)b * H + kbase + kq) * sizeof(bf16));
+
+  // epilogue ownership: wave ui (< UB) owns unit block ui; lane: batch b, units u0..u0+3
+  const bool epi = w < UB;
+  const int u0 = ub0 + (epi ? w : 0) * 16 + 4 * (lane >> 4);
+  const size_t bh = (size_t)b * H + u0;
+  float c[4] = {0.f, 0.f, 0.f, 0.f};
+  if (epi) ld4f(a.cbuf + bh, c);
+
+  for (int t = 0; t < T; ++t) {
+    // x-projection pre-activations of step t (independent of the recurrence: issue early)
+    float zx[4][4];
+    if (epi) {
+      const float* zrow = a.ids ? a.zx + (size_t)a.ids[(size_t)t * B + b] * a.zx_ld
+                                : a.zx + ((size_t)t * B + b) * a.zx_ld;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) ld4f(zrow + (size_t)g * H + u0, zx[g]);
+    }
+    if (t > 0) {
+      if (threadIdx.x == 0)
+        ok_flag = poll_counter(cnt + t, (unsigned)(H / 16), a.spin_limit, a.err, 1u);
+      __syncthreads();
+      if (!ok_flag) return;
+    }
+    // h_{t-1} fragments (handed off by other workgroups: sc1 loads only)
+    const __amdgpu_buffer_rsrc_t hsrc =
+        make_rsrc(a.hbuf + (size_t)t * B * H, sizeof(bf16) * (size_t)B * H);
+    bf16x8 hf[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) hf[s] = ld8_sc1(hsrc, hoff + s * 64);
+#pragma unroll
+    for (int ui = 0; ui < UB; ++ui) {
+      f32x4 acc[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g] = mfma16(wf[ui][g][s], hf[s], acc[g]);
+      float4* dst = reinterpret_cast<float4*>(&part[w][ui][lane][0]);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) dst[g] = make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
+    }
+    __syncthreads();
+    if (epi) {
+      float z[4][4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float4 s0 = reinterpret_cast<const float4*>(&part[0][w][lane][0])[g];
+        float4 s1 = reinterpret_cast<const float4*>(&part[1][w][lane][0])[g];
+        float4 s2 = reinterpret_cast<const float4*>(&part[2][w][lane][0])[g];
+        float4 s3 = reinterpret_cast<const float4*>(&part[3][w][lane][0])[g];
+        z[g][0] = s0.x + s1.x + s2.x + s3.x + zx[g][0];
+        z[g][1] = s0.y + s1.y + s2.y + s3.y + zx[g][1];
+        z[g][2] = s0.z + s1.z + s2.z + s3.z + zx[g][2];
+        z[g][3] = s0.w + s1.w + s2.w + s3.w + zx[g][3];
+      }
+      float gi[4], gj[4], gf[4], go[4], h[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        gi[r] = sigmoidf_(z[0][r]);
+        gj[r] = tanhf_(z[1][r]);
+        gf[r] = sigmoidf_(z[2][r] + a.forget_bias);
+        go[r] = sigmoidf_(z[3][r]);
+        c[r] = gf[r] * c[r] + gi[r] * gj[r];
+        h[r] = go[r] * tanhf_(c[r]);
+      }
+      const size_t o = (size_t)(t + 1) * B * H + bh;
+      st4bf_sc1(a.hbuf + o, h[0], h[1], h[2], h[3]);  // handed off: write-through
+      *reinterpret_cast<float4*>(a.cbuf + o) = make_float4(c[0], c[1], c[2], c[3]);
+      if (a.gates) {
+        bf16* gp = a.gates + ((size_t)t * B + b) * 4 * H + u0;
+        st4bf(gp, gi[0], gi[1], gi[2], gi[3]);
+        st4bf(gp + H, gj[0], gj[1], gj[2], gj[3]);
+        st4bf(gp + 2 * H, gf[0], gf[1], gf[2], gf[3]);
+        st4bf(gp + 3 * H, go[0], go[1], go[2], go[3]);
+      }
+      if (t == T - 1 && a.hlast32)
+        *reinterpret_cast<float4*>(a.hlast32 + bh) = make_float4(h[0], h[1], h[2], h[3]);
+      if (t + 1 < T) {
+        // each epilogue wave publishes its own 16-unit slab: drain its write-through stores,
+        // then one lane arrives (consumers wait for all H/16 slabs of the batch group)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+          __hip_atomic_fetch_add(cnt + t + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// backward (BPTT)
+// ------------------------------------------------------------------------------------------
+template <int KS, int UB>  // KS = k-steps per wave of the K = 4H reduction = H/32
+__global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a) {
+  __shared__ __attribute__((aligned(16))) float part[4][UB][64][4];
+  __shared__ int ok_flag;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int H = a.H, B = a.B, T = a.T;
+  const int nwg_u = H / (16 * UB);
+  const int ubk = blockIdx.x % nwg_u, bg = blockIdx.x / nwg_u;
+  const int ub0 = ubk * 16 * UB, b0 = bg * 16;
+  const int kq = 8 * (lane >> 4);
+  const int kbase = w * (KS * 32);  // == w * H
+  unsigned* cnt = a.cnt + (size_t)bg * (T + 1);
+  const int G4H = 4 * H;
+
+  bf16x8 wf[UB][KS];
+#pragma unroll
+  for (int ui = 0; ui < UB; ++ui)
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      wf[ui][s] = ld8(a.W + (size_t)(ub0 + ui * 16 + (lane & 15)) * G4H + kbase + s * 32 + kq);
+
+  const int b = b0 + (lane & 15);
+  const unsigned doff = (unsigned)(((size_t)b * G4H + kbase + kq) * sizeof(bf16));
+
+  const bool epi = w < UB;
+  const int u0 = ub0 + (epi ? w : 0) * 16 + 4 * (lane >> 4);
+  const size_t bh = (size_t)b * H + u0;
+  float dc[4] = {0.f, 0.f, 0.f, 0.f};
+
+  for (int t = T - 1; t >= 0; --t) {
+    // recurrence-independent epilogue operands, issued before the wait
+    float gi[4], gj[4], gf[4], go[4], cc[4], cp[4], dtop[4];
+    if (epi) {
+      const bf16* gp = a.gates + ((size_t)t * B + b) * G4H + u0;
+      ld4bf(gp, gi); ld4bf(gp + H, gj); ld4bf(gp + 2 * H, gf); ld4bf(gp + 3 * H, go);
+      ld4f(a.cbuf + (size_t)(t + 1) * B * H + bh, cc);
+      ld4f(a.cbuf + (size_t)t * B * H + bh, cp);
+      ld4f(a.dtop + (size_t)t * B * H + bh, dtop);
+    }
+    if (t < T - 1) {
+      if (threadIdx.x == 0)
+        ok_flag = poll_counter(cnt + t + 1, (unsigned)(H / 16), a.spin_limit, a.err, 2u);
+      __syncthreads();
+      if (!ok_flag) return;
+      const __amdgpu_buffer_rsrc_t dsrc =
+          make_rsrc(a.dz + (size_t)(t + 1) * B * G4H, sizeof(bf16) * (size_t)B * G4H);
+      bf16x8 df[KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) df[s] = ld8_sc1(dsrc, doff + s * 64);
+#pragma unroll
+      for (int ui = 0; ui < UB; ++ui) {
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) acc = mfma16(wf[ui][s], df[s], acc);
+        *reinterpret_cast<float4*>(&part[w][ui][lane][0]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      }
+      __syncthreads();
+    }
+    if (epi) {
+      float dh[4];
+      if (t < T - 1) {
+        const float4 s0 = *reinterpret_cast<const float4*>(&part[0][w][lane][0]);
+        const float4 s1 = *reinterpret_cast<const float4*>(&part[1][w][lane][0]);
+        const float4 s2 = *reinterpret_cast<const float4*>(&part[2][w][lane][0]);
+        const float4 s3 = *reinterpret_cast<const float4*>(&part[3][w][lane][0]);
+        dh[0] = s0.x + s1.x + s2.x + s3.x + dtop[0];
+        dh[1] = s0.y + s1.y + s2.y + s3.y + dtop[1];
+        dh[2] = s0.z + s1.z + s2.z + s3.z + dtop[2];
+        dh[3] = s0.w + s1.w + s2.w + s3.w + dtop[3];
+      } else {
+        dh[0] = dtop[0]; dh[1] = dtop[1]; dh[2] = dtop[2]; dh[3] = dtop[3];
+      }
+      float di[4], dj[4], df_[4], dO[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float th = tanhf_(cc[r]);
+        const float dcv = dc[r] + dh[r] * go[r] * (1.f - th * th);
+        dO[r] = dh[r] * th * go[r] * (1.f - go[r]);
+        di[r] = dcv * gj[r] * gi[r] * (1.f - gi[r]);
+        dj[r] = dcv * gi[r] * (1.f - gj[r] * gj[r]);
+        df_[r] = dcv * cp[r] * gf[r] * (1.f - gf[r]);
+        dc[r] = dcv * gf[r];
+      }
+      bf16* dz = a.dz + ((size_t)t * B + b) * G4H + u0;
+      st4bf_sc1(dz, di[0], di[1], di[2], di[3]);
+      st4bf_sc1(dz + H, dj[0], dj[1], dj[2], dj[3]);
+      st4bf_sc1(dz + 2 * H, df_[0], df_[1], df_[2], df_[3]);
+      st4bf_sc1(dz + 3 * H, dO[0], dO[1], dO[2], dO[3]);
+      if (t > 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+          __hip_atomic_fetch_add(cnt + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+template <int KS, int UB>
+static void fwd_inst(const PersistArgs& a, int grid, hipStream_t s) {
+  lstm_fwd_persist_kernel<KS, UB><<<grid, 256, 0, s>>>(a);
+}
+template <int KS, int UB>
+static void bwd_inst(const PersistArgs& a, int grid, hipStream_t s) {
+  lstm_bwd_persist_kernel<KS, UB><<<grid, 256, 0, s>>>(a);
+}
+
+static int ub_for(int H, int B, int cus) {
+  // one 16-unit block per workgroup unless that overfills the chip (<= 2 WGs per CU)
+  const int g1 = (H / 16) * (B / 16);
+  if (g1 <= 2 * cus) return 1;
+  return 2;
+}
+
+int lstm_persist_supported(int H, int B, int cus) {
+  if (H % 128 != 0 || B % 16 != 0 || H > 1024 || H < 128) return 0;
+  const int ub = ub_for(H, B, cus);
+  if ((H / 16) % ub) return 0;
+  const int grid = (H / (16 * ub)) * (B / 16);
+  return grid <= 2 * cus ? 1 : 0;
+}
+
+int lstm_persist_grid(int H, int B, int cus) {
+  return (H / (16 * ub_for(H, B, cus))) * (B / 16);
+}
+
+void launch_lstm_fwd_persist(const PersistArgs& a, int cus, hipStream_t s) {
+  const int ub = ub_for(a.H, a.B, cus);
+  const int grid = (a.H / (16 * ub)) * (a.B / 16);
+  (void)hipMemsetAsync(a.cnt, 0, sizeof(unsigned) * (size_t)(a.B / 16) * (a.T + 1), s);
+  const int ks = a.H / 128;
+#define FWD(K, U) \
+  if (ks == K && ub == U) { fwd_inst<K, U>(a, grid, s); return; }
+  FWD(1, 1) FWD(2, 1) FWD(3, 1) FWD(4, 1) FWD(6, 1) FWD(8, 1)
+  FWD(1, 2) FWD(2, 2) FWD(3, 2) FWD(4, 2) FWD(6, 2) FWD(8, 2)
+#undef FWD
+}
+
+void launch_lstm_bwd_persist(const PersistArgs& a, int cus, hipStream_t s) {
+  const int ub = ub_for(a.H, a.B, cus);
+  const int grid = (a.H / (16 * ub)) * (a.B / 16);
+  (void)hipMemsetAsync(a.cnt, 0, sizeof(unsigned) * (size_t)(a.B / 16) * (a.T + 1), s);
+  const int ks = a.H / 32;
+#define BWD(K, U) \
+  if (ks == K && ub == U) { bwd_inst<K, U>(a, grid, s); return; }
+  BWD(4, 1) BWD(8, 1) BWD(12, 1) BWD(16, 1) BWD(24, 1) BWD(32, 1)
+  BWD(4, 2) BWD(8, 2) BWD(12, 2) BWD(16, 2) BWD(24, 2) BWD(32, 2)
+#undef BWD
+}
+
+}  // namespace dcr

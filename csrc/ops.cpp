@@ -55,6 +55,339 @@ void adam_clip(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
                         (float)b1, (float)b2, (float)eps, (float)clip, cur_stream());
 }
 
+// ------------------------------------------------------------------------------------------
+// recurrent sequences: C++ time loop over the per-step kernels (rnn_step.hip)
+// ------------------------------------------------------------------------------------------
+template <typename T>
+T* optr(const c10::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+bool has(const c10::optional<at::Tensor>& t) { return t.has_value() && t->defined(); }
+
+void check_seq(const at::Tensor& t, at::ScalarType st, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(t.scalar_type() == st, name, " has the wrong dtype");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, name, " must be 16-B aligned");
+}
+void check_opt(const c10::optional<at::Tensor>& t, at::ScalarType st, const char* name) {
+  if (has(t)) check_seq(*t, st, name);
+}
+
+void rnn_fwd_seq(int64_t cell, const at::Tensor& WT, const c10::optional<at::Tensor>& WT2,
+                 const at::Tensor& zx, const c10::optional<at::Tensor>& ids, at::Tensor& hbuf,
+                 const c10::optional<at::Tensor>& h32, const c10::optional<at::Tensor>& cbuf,
+                 const c10::optional<at::Tensor>& gates, const c10::optional<at::Tensor>& pre,
+                 const c10::optional<at::Tensor>& aux, const c10::optional<at::Tensor>& rh,
+                 const c10::optional<at::Tensor>& hlast32, double forget_bias) {
+  check_seq(WT, at::kBFloat16, "WT");
+  check_seq(zx, at::kFloat, "zx");
+  check_seq(hbuf, at::kBFloat16, "hbuf");
+  check_opt(WT2, at::kBFloat16, "WT2");
+  check_opt(ids, at::kInt, "ids");
+  check_opt(h32, at::kFloat, "h32");
+  check_opt(cbuf, at::kFloat, "cbuf");
+  check_opt(gates, at::kBFloat16, "gates");
+  check_opt(pre, at::kFloat, "pre");
+  check_opt(aux, at::kFloat, "aux");
+  check_opt(rh, at::kBFloat16, "rh");
+  check_opt(hlast32, at::kFloat, "hlast32");
+  TORCH_CHECK(hbuf.dim() == 3, "hbuf must be [T+1, B, H]");
+  const int T = (int)hbuf.size(0) - 1, B = (int)hbuf.size(1), H = (int)hbuf.size(2);
+  TORCH_CHECK(T >= 1 && B >= 1, "empty sequence");
+  TORCH_CHECK(H % 32 == 0, "rnn_size must be a multiple of 32 on the GPU path");
+  const int GW = (int)zx.size(-1);
+  const bool gather = has(ids);
+  if (gather) {
+    TORCH_CHECK(ids->numel() == (int64_t)T * B, "ids must be [T, B]");
+  } else {
+    TORCH_CHECK(zx.numel() == (int64_t)T * B * GW, "zx must be [T, B, GW]");
+  }
+  TORCH_CHECK(GW % 4 == 0, "zx row must be a multiple of 4 floats");
+  const size_t BH = (size_t)B * H;
+  const int c = (int)cell;
+  const int G = c == dcr::CELL_LSTM ? 4 : c == dcr::CELL_NAS ? 8 : c == dcr::CELL_GRU_A ? 3 : 1;
+  TORCH_CHECK(WT.size(0) == (c == dcr::CELL_GRU_A ? 2 : G) * H && WT.size(1) == H, "WT shape");
+  if (c == dcr::CELL_LSTM || c == dcr::CELL_NAS) TORCH_CHECK(has(cbuf), "cbuf required");
+  if (c == dcr::CELL_GRU_A) TORCH_CHECK(has(h32) && has(rh) && has(gates) && has(WT2), "GRU buffers");
+  if (c == dcr::CELL_NAS) TORCH_CHECK(has(pre) && has(aux), "NAS buffers");
+  const int gld = has(gates) ? (int)gates->size(-1) : has(pre) ? (int)pre->size(-1) : 0;
+  auto st = cur_stream();
+  for (int t = 0; t < T; ++t) {
+    dcr::FwdStepArgs a{};
+    a.WT = ptr<bf16>(WT);
+    a.ids = gather ? ptr<int>(*ids) + (size_t)t * B : nullptr;
+    a.zx = gather ? ptr<float>(zx) : ptr<float>(zx) + (size_t)t * B * GW;
+    a.zx_ld = GW;
+    a.zx_off = 0;
+    a.hop = ptr<bf16>(hbuf) + t * BH;
+    a.hprev32 = has(h32) ? optr<float>(h32) + t * BH : nullptr;
+    a.cprev = has(cbuf) ? optr<float>(cbuf) + t * BH : nullptr;
+    a.hout = ptr<bf16>(hbuf) + (t + 1) * BH;
+    a.hout32 = has(h32) ? optr<float>(h32) + (t + 1) * BH
+                        : (t == T - 1 ? optr<float>(hlast32) : nullptr);
+    a.cout = has(cbuf) ? optr<float>(cbuf) + (t + 1) * BH : nullptr;
+    a.gates = has(gates) ? optr<bf16>(gates) + (size_t)t * B * gld : nullptr;
+    a.pre = has(pre) ? optr<float>(pre) + (size_t)t * B * gld : nullptr;
+    a.aux = has(aux) ? optr<float>(aux) + t * BH : nullptr;
+    a.rh = has(rh) ? optr<bf16>(rh) + t * BH : nullptr;
+    a.gates_ld = gld;
+    a.B = B;
+    a.H = H;
+    a.forget_bias = (float)forget_bias;
+    dcr::launch_fwd_step(c, a, st);
+    if (c == dcr::CELL_GRU_A) {
+      dcr::FwdStepArgs b2 = a;
+      b2.WT = optr<bf16>(WT2);
+      b2.zx_off = 2 * H;
+      b2.hop = a.rh;
+      dcr::launch_fwd_step(dcr::CELL_GRU_B, b2, st);
+    }
+  }
+}
+
+void rnn_bwd_seq(int64_t cell, const at::Tensor& W, const c10::optional<at::Tensor>& W2,
+                 const at::Tensor& dtop, at::Tensor& dz, const c10::optional<at::Tensor>& dzx,
+                 const c10::optional<at::Tensor>& gates, const c10::optional<at::Tensor>& pre,
+                 const c10::optional<at::Tensor>& aux, const c10::optional<at::Tensor>& zx,
+                 const c10::optional<at::Tensor>& cbuf, const c10::optional<at::Tensor>& h32,
+                 const c10::optional<at::Tensor>& hbuf, at::Tensor& dc,
+                 const c10::optional<at::Tensor>& partial) {
+  check_seq(W, at::kBFloat16, "W");
+  check_seq(dtop, at::kFloat, "dtop");
+  check_seq(dz, at::kBFloat16, "dz");
+  check_seq(dc, at::kFloat, "dc");
+  check_opt(W2, at::kBFloat16, "W2");
+  check_opt(dzx, at::kBFloat16, "dzx");
+  check_opt(gates, at::kBFloat16, "gates");
+  check_opt(pre, at::kFloat, "pre");
+  check_opt(aux, at::kFloat, "aux");
+  check_opt(zx, at::kFloat, "zx");
+  check_opt(cbuf, at::kFloat, "cbuf");
+  check_opt(h32, at::kFloat, "h32");
+  check_opt(hbuf, at::kBFloat16, "hbuf");
+  check_opt(partial, at::kFloat, "partial");
+  TORCH_CHECK(dtop.dim() == 3, "dtop must be [T, B, H]");
+  const int T = (int)dtop.size(0), B = (int)dtop.size(1), H = (int)dtop.size(2);
+  TORCH_CHECK(H % 32 == 0, "rnn_size must be a multiple of 32 on the GPU path");
+  const int GW = (int)dz.size(-1);
+  TORCH_CHECK(dz.numel() == (int64_t)T * B * GW, "dz must be [T, B, GW]");
+  TORCH_CHECK(dc.numel() == (int64_t)B * H, "dc must be [B, H]");
+  const size_t BH = (size_t)B * H;
+  const size_t BG = (size_t)B * GW;
+  auto st = cur_stream();
+  const int c = (int)cell;
+  (void)hipMemsetAsync(dc.data_ptr(), 0, sizeof(float) * BH, st);
+  if (c == dcr::CELL_GRU_A) {
+    TORCH_CHECK(has(W2) && has(gates) && has(h32) && has(partial), "GRU buffers");
+    TORCH_CHECK(GW == 3 * H, "GRU dz must be [T, B, 3H]");
+    const int gld = (int)gates->size(-1);
+    dcr::BwdStepArgs i{};
+    i.dtop = ptr<float>(dtop) + (T - 1) * BH;
+    i.gates = optr<bf16>(gates) + (size_t)(T - 1) * B * gld;
+    i.dc = ptr<float>(dc);
+    i.dz_out = ptr<bf16>(dz) + (T - 1) * BG + 2 * H;
+    i.dz_out_ld = GW;
+    i.gates_ld = gld;
+    i.B = B;
+    i.H = H;
+    dcr::launch_bwd_step(dcr::CELL_GRU_B, i, st);
+    for (int t = T - 1; t >= 0; --t) {
+      dcr::BwdStepArgs a{};
+      a.W = ptr<bf16>(W);
+      a.K = H;
+      a.dz_next = ptr<bf16>(dz) + t * BG + 2 * H;
+      a.dz_ld = GW;
+      a.gates = optr<bf16>(gates) + (size_t)t * B * gld;
+      a.gates_ld = gld;
+      a.hprev32 = optr<float>(h32) + t * BH;
+      a.dc = ptr<float>(dc);
+      a.partial = optr<float>(partial);
+      a.dz_out = ptr<bf16>(dz) + t * BG;
+      a.dz_out_ld = GW;
+      a.B = B;
+      a.H = H;
+      dcr::launch_bwd_step(dcr::CELL_GRU_A, a, st);
+      if (t > 0) {
+        dcr::BwdStepArgs b{};
+        b.W = optr<bf16>(W2);
+        b.K = 2 * H;
+        b.dz_next = ptr<bf16>(dz) + t * BG;
+        b.dz_ld = GW;
+        b.dtop = ptr<float>(dtop) + (t - 1) * BH;
+        b.partial = optr<float>(partial);
+        b.gates = optr<bf16>(gates) + (size_t)(t - 1) * B * gld;
+        b.gates_ld = gld;
+        b.dc = ptr<float>(dc);
+        b.dz_out = ptr<bf16>(dz) + (t - 1) * BG + 2 * H;
+        b.dz_out_ld = GW;
+        b.B = B;
+        b.H = H;
+        dcr::launch_bwd_step(dcr::CELL_GRU_B, b, st);
+      }
+    }
+    return;
+  }
+  const int K = GW;  // LSTM 4H, RNN H, NAS 8H
+  TORCH_CHECK(W.size(0) == H && W.size(1) == K, "W must be [H, G*H]");
+  if (c == dcr::CELL_LSTM) TORCH_CHECK(has(gates) && has(cbuf), "LSTM buffers");
+  if (c == dcr::CELL_RNN) TORCH_CHECK(has(hbuf), "RNN buffers");
+  if (c == dcr::CELL_NAS) TORCH_CHECK(has(pre) && has(aux) && has(zx) && has(cbuf) && has(dzx), "NAS buffers");
+  const int gld = has(gates) ? (int)gates->size(-1) : has(pre) ? (int)pre->size(-1) : 0;
+  for (int t = T - 1; t >= 0; --t) {
+    dcr::BwdStepArgs a{};
+    a.W = ptr<bf16>(W);
+    a.K = K;
+    a.dz_next = (t < T - 1) ? ptr<bf16>(dz) + (t + 1) * BG : nullptr;
+    a.dz_ld = GW;
+    a.dtop = ptr<float>(dtop) + t * BH;
+    a.gates = has(gates) ? optr<bf16>(gates) + (size_t)t * B * gld : nullptr;
+    a.pre = has(pre) ? optr<float>(pre) + (size_t)t * B * gld : nullptr;
+    a.aux = has(aux) ? optr<float>(aux) + t * BH : nullptr;
+    a.zx3 = has(zx) ? optr<float>(zx) + (size_t)t * B * GW + 3 * H : nullptr;
+    a.zx3_ld = GW;
+    a.c = has(cbuf) ? optr<float>(cbuf) + (t + 1) * BH : nullptr;
+    a.cprev = has(cbuf) ? optr<float>(cbuf) + t * BH : nullptr;
+    a.hcur = has(hbuf) ? optr<bf16>(hbuf) + (t + 1) * BH : nullptr;
+    a.dc = ptr<float>(dc);
+    a.dz_out = ptr<bf16>(dz) + t * BG;
+    a.dzx_out = has(dzx) ? optr<bf16>(dzx) + t * BG : nullptr;
+    a.dz_out_ld = GW;
+    a.gates_ld = gld;
+    a.B = B;
+    a.H = H;
+    dcr::launch_bwd_step(c, a, st);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// loss + segment sums
+// ------------------------------------------------------------------------------------------
+void xent(const at::Tensor& logits, const at::Tensor& targets, double grad_scale,
+          const c10::optional<at::Tensor>& row_loss, const c10::optional<at::Tensor>& dlogits,
+          at::Tensor& partial, at::Tensor& loss_out) {
+  check_seq(logits, at::kFloat, "logits");
+  check_seq(targets, at::kInt, "targets");
+  check_opt(row_loss, at::kFloat, "row_loss");
+  check_opt(dlogits, at::kBFloat16, "dlogits");
+  TORCH_CHECK(logits.dim() == 2, "logits must be [N, V]");
+  const int N = (int)logits.size(0), V = (int)logits.size(1);
+  TORCH_CHECK(targets.numel() == N, "targets must be [N]");
+  TORCH_CHECK(partial.numel() >= dcr::xent_num_partials(N), "partial too small");
+  dcr::launch_xent(ptr<float>(logits), ptr<int>(targets), N, V, (float)grad_scale,
+                   optr<float>(row_loss), optr<bf16>(dlogits), ptr<float>(partial),
+                   ptr<float>(loss_out), cur_stream());
+}
+
+void segsum(const at::Tensor& X, const c10::optional<at::Tensor>& ids, int64_t V, at::Tensor& out,
+            at::Tensor& workspace, bool accumulate) {
+  TORCH_CHECK(X.is_cuda() && X.dim() == 2 && X.stride(1) == 1, "X must be a row-major 2-D GPU tensor");
+  const int N = (int)X.size(0), W = (int)X.size(1), ldx = (int)X.stride(0);
+  check_opt(ids, at::kInt, "ids");
+  check_seq(out, at::kFloat, "out");
+  TORCH_CHECK(out.numel() == V * W, "out must be [V, W]");
+  TORCH_CHECK((size_t)workspace.numel() >= dcr::segsum_workspace_floats(N, W, (int)V), "workspace too small");
+  if (has(ids)) {
+    TORCH_CHECK(ids->numel() == N, "ids must be [N]");
+  } else {
+    TORCH_CHECK(V == 1, "without ids, V must be 1 (column sum)");
+  }
+  if (X.scalar_type() == at::kBFloat16) {
+    dcr::launch_segsum_bf16(ptr<bf16>(X), ldx, optr<int>(ids), N, W, (int)V, ptr<float>(out),
+                            ptr<float>(workspace), accumulate ? 1 : 0, cur_stream());
+  } else {
+    TORCH_CHECK(X.scalar_type() == at::kFloat, "X must be bf16 or fp32");
+    dcr::launch_segsum_f32(ptr<float>(X), ldx, optr<int>(ids), N, W, (int)V, ptr<float>(out),
+                           ptr<float>(workspace), accumulate ? 1 : 0, cur_stream());
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// persistent LSTM recurrence (lstm_persist.hip)
+// ------------------------------------------------------------------------------------------
+int num_cus() {
+  static int cus = -1;
+  if (cus < 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t prop;
+    cus = (hipGetDeviceProperties(&prop, dev) == hipSuccess) ? prop.multiProcessorCount : 0;
+  }
+  return cus;
+}
+
+int64_t lstm_persist_supported(int64_t H, int64_t B) {
+  return dcr::lstm_persist_supported((int)H, (int)B, num_cus());
+}
+
+void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::optional<at::Tensor>& ids,
+                      at::Tensor& hbuf, at::Tensor& cbuf, const c10::optional<at::Tensor>& gates,
+                      at::Tensor& hlast32, at::Tensor& cnt, at::Tensor& err, double forget_bias,
+                      int64_t spin_limit) {
+  check_seq(WT, at::kBFloat16, "WT");
+  check_seq(zx, at::kFloat, "zx");
+  check_seq(hbuf, at::kBFloat16, "hbuf");
+  check_seq(cbuf, at::kFloat, "cbuf");
+  check_seq(hlast32, at::kFloat, "hlast32");
+  check_opt(gates, at::kBFloat16, "gates");
+  check_opt(ids, at::kInt, "ids");
+  TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == at::kInt && err.scalar_type() == at::kInt,
+              "cnt/err must be int32 GPU tensors");
+  const int T = (int)hbuf.size(0) - 1, B = (int)hbuf.size(1), H = (int)hbuf.size(2);
+  TORCH_CHECK(dcr::lstm_persist_supported(H, B, num_cus()), "persistent LSTM unsupported for this shape");
+  TORCH_CHECK(WT.size(0) == 4 * H && WT.size(1) == H, "WT must be [4H, H]");
+  TORCH_CHECK(zx.size(-1) == 4 * H, "zx rows must be 4H wide");
+  if (has(ids)) {
+    TORCH_CHECK(ids->numel() == (int64_t)T * B, "ids must be [T, B]");
+  } else {
+    TORCH_CHECK(zx.numel() == (int64_t)T * B * 4 * H, "zx must be [T, B, 4H]");
+  }
+  if (has(gates)) TORCH_CHECK(gates->numel() == (int64_t)T * B * 4 * H, "gates must be [T, B, 4H]");
+  TORCH_CHECK(cnt.numel() >= (int64_t)(B / 16) * (T + 1), "counter buffer too small");
+  dcr::PersistArgs a{};
+  a.W = ptr<bf16>(WT);
+  a.zx = ptr<float>(zx);
+  a.ids = optr<int>(ids);
+  a.zx_ld = 4 * H;
+  a.hbuf = ptr<bf16>(hbuf);
+  a.cbuf = ptr<float>(cbuf);
+  a.gates = optr<bf16>(gates);
+  a.hlast32 = ptr<float>(hlast32);
+  a.cnt = reinterpret_cast<unsigned*>(cnt.data_ptr());
+  a.err = reinterpret_cast<unsigned*>(err.data_ptr());
+  a.B = B; a.H = H; a.T = T;
+  a.forget_bias = (float)forget_bias;
+  a.spin_limit = (unsigned)spin_limit;
+  dcr::launch_lstm_fwd_persist(a, num_cus(), cur_stream());
+}
+
+void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& dz,
+                      const at::Tensor& gates, const at::Tensor& cbuf, at::Tensor& cnt,
+                      at::Tensor& err, int64_t spin_limit) {
+  check_seq(W, at::kBFloat16, "W");
+  check_seq(dtop, at::kFloat, "dtop");
+  check_seq(dz, at::kBFloat16, "dz");
+  check_seq(gates, at::kBFloat16, "gates");
+  check_seq(cbuf, at::kFloat, "cbuf");
+  const int T = (int)dtop.size(0), B = (int)dtop.size(1), H = (int)dtop.size(2);
+  TORCH_CHECK(dcr::lstm_persist_supported(H, B, num_cus()), "persistent LSTM unsupported for this shape");
+  TORCH_CHECK(W.size(0) == H && W.size(1) == 4 * H, "W must be [H, 4H]");
+  TORCH_CHECK(dz.numel() == (int64_t)T * B * 4 * H && gates.numel() == (int64_t)T * B * 4 * H, "dz/gates shape");
+  TORCH_CHECK(cbuf.numel() == (int64_t)(T + 1) * B * H, "cbuf shape");
+  TORCH_CHECK(cnt.numel() >= (int64_t)(B / 16) * (T + 1), "counter buffer too small");
+  dcr::PersistArgs a{};
+  a.W = ptr<bf16>(W);
+  a.dtop = ptr<float>(dtop);
+  a.dz = ptr<bf16>(dz);
+  a.gates = ptr<bf16>(gates);
+  a.cbuf = ptr<float>(cbuf);
+  a.cnt = reinterpret_cast<unsigned*>(cnt.data_ptr());
+  a.err = reinterpret_cast<unsigned*>(err.data_ptr());
+  a.B = B; a.H = H; a.T = T;
+  a.spin_limit = (unsigned)spin_limit;
+  dcr::launch_lstm_bwd_persist(a, num_cus(), cur_stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(dcr, m) {
@@ -64,9 +397,40 @@ TORCH_LIBRARY(dcr, m) {
       "adam_clip(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? pbf, "
       "Tensor(e!) partials, Tensor(f!) norm_out, float lr_t, float b1, float b2, float eps, "
       "float clip) -> ()");
+  m.def(
+      "rnn_fwd_seq(int cell, Tensor WT, Tensor? WT2, Tensor zx, Tensor? ids, Tensor(a!) hbuf, "
+      "Tensor(b!)? h32, Tensor(c!)? cbuf, Tensor(d!)? gates, Tensor(e!)? pre, Tensor(f!)? aux, "
+      "Tensor(g!)? rh, Tensor(h!)? hlast32, float forget_bias) -> ()");
+  m.def(
+      "rnn_bwd_seq(int cell, Tensor W, Tensor? W2, Tensor dtop, Tensor(a!) dz, Tensor(b!)? dzx, "
+      "Tensor? gates, Tensor? pre, Tensor? aux, Tensor? zx, Tensor? cbuf, Tensor? h32, "
+      "Tensor? hbuf, Tensor(c!) dc, Tensor(d!)? partial) -> ()");
+  m.def(
+      "xent(Tensor logits, Tensor targets, float grad_scale, Tensor(a!)? row_loss, "
+      "Tensor(b!)? dlogits, Tensor(c!) partial, Tensor(d!) loss_out) -> ()");
+  m.def("xent_num_partials(int n) -> int",
+        [](int64_t n) -> int64_t { return dcr::xent_num_partials((int)n); });
+  m.def("lstm_persist_supported(int H, int B) -> int", &lstm_persist_supported);
+  m.def(
+      "lstm_persist_fwd(Tensor WT, Tensor zx, Tensor? ids, Tensor(a!) hbuf, Tensor(b!) cbuf, "
+      "Tensor(c!)? gates, Tensor(d!) hlast32, Tensor(e!) cnt, Tensor(f!) err, float forget_bias, "
+      "int spin_limit) -> ()");
+  m.def(
+      "lstm_persist_bwd(Tensor W, Tensor dtop, Tensor(a!) dz, Tensor gates, Tensor cbuf, "
+      "Tensor(b!) cnt, Tensor(c!) err, int spin_limit) -> ()");
+  m.def("segsum(Tensor X, Tensor? ids, int V, Tensor(a!) out, Tensor(b!) workspace, bool accumulate) -> ()");
+  m.def("segsum_workspace(int N, int W, int V) -> int", [](int64_t N, int64_t W, int64_t V) -> int64_t {
+    return (int64_t)dcr::segsum_workspace_floats((int)N, (int)W, (int)V);
+  });
 }
 
 TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("global_norm", &global_norm);
   m.impl("adam_clip", &adam_clip);
+  m.impl("rnn_fwd_seq", &rnn_fwd_seq);
+  m.impl("rnn_bwd_seq", &rnn_bwd_seq);
+  m.impl("xent", &xent);
+  m.impl("segsum", &segsum);
+  m.impl("lstm_persist_fwd", &lstm_persist_fwd);
+  m.impl("lstm_persist_bwd", &lstm_persist_bwd);
 }

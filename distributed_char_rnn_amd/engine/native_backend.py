@@ -1,0 +1,402 @@
+"""Native (gfx950 HIP) execution of one stateful-TBPTT training step.
+
+Replaces the reference's TF graph execution of one ``Session.run([summaries, cost,
+final_state, train_op])`` (train.py:199) -- T x L unrolled cell chains forward, tf.gradients
+backward -- with an explicit, hand-scheduled forward/backward over the kernels in ``csrc/``:
+
+forward, per layer l (time-major rows n = t*B + b):
+  * Zx = X_l · W_x + b  -- one MFMA library GEMM over all T steps (hipBLASLt, fp32 out); for
+    layer 0 without dropout the GEMM disappears: Zx_0 = (E·W_x0 + b0)[ids] is gathered from a
+    [V, G·H] table inside the recurrent kernel (V = 65 rows instead of B·T rows);
+  * ``dcr::rnn_fwd_seq``: the fused recurrent-GEMM + cell kernels, T launches from C++;
+head: logits = O·W_s + b_s (GEMM), ``dcr::xent`` = fused softmax-CE forward + dlogits;
+backward, top layer first:
+  * dO = dlogits·W_sᵀ, dW_s = Oᵀ·dlogits, db_s = colsum  -> head bucket ready for all-reduce
+  * ``dcr::rnn_bwd_seq``: fused recurrent-GEMM + cell-backward kernels (dZ per step)
+  * dW_h = H_prevᵀ·dZ, dW_x = X_lᵀ·dZ, db = colsum(dZ), dX = dZ·W_xᵀ  -> layer bucket ready
+  * layer 0 (gather mode): dEW = segsum(dZ_0 by id) [V, G·H]; dW_x0 = Eᵀ·dEW, db_0 = colsum(dEW),
+    dE = dEW·W_x0ᵀ  (three tiny GEMMs instead of two [B·T]-sized ones)
+
+All weights are refreshed from the fp32 master buffer into bf16 kernel layouts once per
+optimizer step (W_hᵀ for the forward's A operand, W_h in TF layout for the backward's).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from ..models.params import ParamStore, cell_specs
+from ..ops import native
+
+CELL_ID = {"lstm": 0, "gru": 1, "rnn": 3, "nas": 4}
+FORGET_BIAS = 1.0
+bf16 = torch.bfloat16
+f32 = torch.float32
+
+
+def _mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """bf16 x bf16 -> fp32 GEMM on the MFMA library path."""
+    return torch.mm(a, b, out_dtype=f32)
+
+
+@dataclass
+class LayerWeights:
+    Wx: torch.Tensor            # [D, GW] bf16 input projection
+    Wx32: Optional[torch.Tensor]  # [D, GW] fp32 (layer-0 table / dE)
+    bias: torch.Tensor          # [GW] fp32 (zeros for NAS)
+    Wh: torch.Tensor            # [H, GWr] bf16 TF layout (backward A operand); GRU: Wc_h
+    WhT: torch.Tensor           # [GWr, H] bf16 (forward A operand); GRU: Wg_hᵀ
+    W2: Optional[torch.Tensor] = None   # GRU: Wg_h [H, 2H]
+    WT2: Optional[torch.Tensor] = None  # GRU: Wc_hᵀ [H, H]
+
+
+@dataclass
+class LayerBufs:
+    hbuf: torch.Tensor
+    cbuf: Optional[torch.Tensor]
+    h32: Optional[torch.Tensor]
+    gates: Optional[torch.Tensor]
+    pre: Optional[torch.Tensor]
+    aux: Optional[torch.Tensor]
+    rh: Optional[torch.Tensor]
+    hlast32: torch.Tensor
+    zx: Optional[torch.Tensor]
+    dz: Optional[torch.Tensor]
+    dzx: Optional[torch.Tensor]
+    x_in: Optional[torch.Tensor] = None      # bf16 [N, D] layer input (dense mode)
+    masks: Dict[str, torch.Tensor] = field(default_factory=dict)
+
+
+class NativeBackend:
+    def __init__(self, store: ParamStore, dtype: str = "auto", seed: int = 0):
+        if dtype not in ("auto", "bf16"):
+            raise ValueError("the native GPU path computes in bf16 (use --dtype bf16/auto)")
+        self.ops = native.ops()
+        self.store = store
+        self.cfg = store.cfg
+        self.dev = store.device
+        self.cell = CELL_ID[self.cfg.model]
+        self.H = self.cfg.rnn_size
+        self.V = self.cfg.vocab_size
+        self.L = self.cfg.num_layers
+        if self.H % 32 != 0:
+            raise ValueError("the GPU path needs rnn_size % 32 == 0")
+        self.GW = {"lstm": 4, "gru": 3, "rnn": 1, "nas": 8}[self.cfg.model] * self.H
+        self._wver = None
+        self._w: List[LayerWeights] = []
+        self._head = None
+        self._bufs: Dict[Tuple[int, int, bool], dict] = {}
+        self.use_persist = os.environ.get("DCR_PERSIST", "1") != "0"
+        self.spin_limit = int(os.environ.get("DCR_SPIN_LIMIT", str(1 << 22)))
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self._steps = 0
+        self.gen = torch.Generator(device=self.dev)
+        self.gen.manual_seed(int(seed))
+
+    # ------------------------------------------------------------------ weights
+    def params_changed(self):
+        self._wver = None
+
+    def _prep(self):
+        ver = getattr(self.store, "version", 0)
+        if self._wver == ver and self._w:
+            return
+        s, H, D = self.store, self.H, self.H
+        self._w = []
+        for layer in range(self.L):
+            names = [sp.name for sp in cell_specs(self.cfg, layer)]
+            if self.cfg.model == "lstm" or self.cfg.model == "rnn":
+                k, b = s.view(names[0]), s.view(names[1])
+                Wh = k[D:].to(bf16).contiguous()
+                lw = LayerWeights(Wx=k[:D].to(bf16).contiguous(), Wx32=k[:D], bias=b,
+                                  Wh=Wh, WhT=Wh.t().contiguous())
+            elif self.cfg.model == "gru":
+                gk, gb, ck, cb = (s.view(n) for n in names)
+                Wx32 = torch.cat([gk[:D], ck[:D]], 1)
+                Wg = gk[D:].to(bf16).contiguous()
+                Wc = ck[D:].to(bf16).contiguous()
+                lw = LayerWeights(Wx=Wx32.to(bf16), Wx32=Wx32, bias=torch.cat([gb, cb]),
+                                  Wh=Wc, WhT=Wg.t().contiguous(), W2=Wg, WT2=Wc.t().contiguous())
+            else:  # nas
+                kx, km = s.view(names[0]), s.view(names[1])
+                Wh = km.to(bf16).contiguous()
+                lw = LayerWeights(Wx=kx.to(bf16).contiguous(), Wx32=kx,
+                                  bias=torch.zeros(8 * H, device=self.dev), Wh=Wh,
+                                  WhT=Wh.t().contiguous())
+            self._w.append(lw)
+        E = s.view("embedding")
+        w0 = self._w[0]
+        table = torch.addmm(w0.bias, E, w0.Wx32)  # [V, GW] fp32: (E·W_x0 + b0)
+        self._head = dict(E=E, table=table.contiguous(), Ws=s.view("rnnlm/softmax_w").to(bf16),
+                          bs=s.view("rnnlm/softmax_b"))
+        self._wver = ver
+
+    # ------------------------------------------------------------------ buffers
+    def _buffers(self, B: int, T: int, training: bool) -> dict:
+        key = (B, T, training)
+        if key in self._bufs:
+            return self._bufs[key]
+        H, GW, dev, m = self.H, self.GW, self.dev, self.cfg.model
+        N = B * T
+        layers = []
+        for layer in range(self.L):
+            dense = layer > 0 or self._dropout(training)
+            lb = LayerBufs(
+                hbuf=torch.empty(T + 1, B, H, dtype=bf16, device=dev),
+                cbuf=torch.empty(T + 1, B, H, dtype=f32, device=dev) if m in ("lstm", "nas") else None,
+                h32=torch.empty(T + 1, B, H, dtype=f32, device=dev) if m == "gru" else None,
+                gates=(torch.empty(T, B, GW, dtype=bf16, device=dev)
+                       if m == "gru" or (m == "lstm" and training) else None),
+                pre=torch.empty(T, B, GW, dtype=f32, device=dev) if m == "nas" else None,
+                aux=torch.empty(T, B, H, dtype=f32, device=dev) if m == "nas" else None,
+                rh=torch.empty(T, B, H, dtype=bf16, device=dev) if m == "gru" else None,
+                hlast32=torch.empty(B, H, dtype=f32, device=dev),
+                zx=torch.empty(T, B, GW, dtype=f32, device=dev) if (dense or m == "nas") else None,
+                dz=torch.empty(T, B, GW, dtype=bf16, device=dev) if training else None,
+                dzx=torch.empty(T, B, GW, dtype=bf16, device=dev) if (training and m == "nas") else None,
+            )
+            layers.append(lb)
+        ws = max(self.ops.segsum_workspace(N, GW, self.V), self.ops.segsum_workspace(N, H, self.V),
+                 self.ops.segsum_workspace(N, GW, 1), self.ops.segsum_workspace(N, self.V, 1), 1)
+        bufs = dict(
+            layers=layers,
+            logits=torch.empty(N, self.V, dtype=f32, device=dev),
+            dlogits=torch.empty(N, self.V, dtype=bf16, device=dev) if training else None,
+            row_loss=torch.empty(N, dtype=f32, device=dev),
+            xpart=torch.empty(self.ops.xent_num_partials(N), dtype=f32, device=dev),
+            loss=torch.empty(1, dtype=f32, device=dev),
+            dc=torch.empty(B, H, dtype=f32, device=dev),
+            gpart=torch.empty(B, H, dtype=f32, device=dev) if m == "gru" else None,
+            ws=torch.empty(ws, dtype=f32, device=dev),
+            colsum=torch.empty(1, max(GW, self.V), dtype=f32, device=dev),
+            persist=self._persist_ok(B),
+            cnt=torch.zeros((B // 16 + 1) * (T + 1), dtype=torch.int32, device=dev),
+        )
+        self._bufs[key] = bufs
+        return bufs
+
+    def _persist_ok(self, B: int) -> bool:
+        return (self.use_persist and self.cfg.model == "lstm"
+                and bool(self.ops.lstm_persist_supported(self.H, B)))
+
+    def check_errors(self):
+        """Raise if a persistent kernel hit its spin timeout (forces a device sync)."""
+        v = int(self.err.item())
+        if v:
+            self.err.zero_()
+            raise RuntimeError(f"persistent recurrent kernel timed out (code {v}); "
+                               "set DCR_PERSIST=0 to use the per-step kernels")
+
+    def _dropout(self, training: bool) -> bool:
+        c = self.cfg
+        return training and (c.input_keep_prob < 1.0 or c.output_keep_prob < 1.0)
+
+    def _mask(self, shape, keep: float) -> torch.Tensor:
+        return (torch.rand(shape, device=self.dev, generator=self.gen) < keep).to(bf16) * (1.0 / keep)
+
+    # ------------------------------------------------------------------ forward
+    def _forward(self, ids_tm: torch.Tensor, state, training: bool):
+        T, B = ids_tm.shape
+        H, N = self.H, T * B
+        self._prep()
+        bufs = self._buffers(B, T, training)
+        drop = self._dropout(training)
+        c = self.cfg
+        x_prev = None  # bf16 [T, B, H] input for the next layer
+        for layer in range(self.L):
+            lw, lb = self._w[layer], bufs["layers"][layer]
+            st = state[layer]
+            if self.cfg.model in ("lstm", "nas"):
+                lb.cbuf[0].copy_(st[0])
+                lb.hbuf[0].copy_(st[1])
+            else:
+                lb.hbuf[0].copy_(st[0])
+                if lb.h32 is not None:
+                    lb.h32[0].copy_(st[0])
+            gather = (layer == 0 and not drop and self.cfg.model != "nas")
+            ids_arg = None
+            if gather:
+                zx = self._head["table"]
+                ids_arg = ids_tm
+            else:
+                if layer == 0:
+                    X = self._head["E"][ids_tm.long()].to(bf16)  # [T, B, H]
+                    if training and c.output_keep_prob < 1.0:  # model.py:58-59 (A-13)
+                        lb.masks["emb"] = self._mask(X.shape, c.output_keep_prob)
+                        X = X * lb.masks["emb"]
+                else:
+                    X = x_prev
+                if drop and c.input_keep_prob < 1.0:
+                    lb.masks["in"] = self._mask(X.shape, c.input_keep_prob)
+                    X = X * lb.masks["in"]
+                lb.x_in = X.reshape(N, H).contiguous()
+                lb.zx.view(N, self.GW).copy_(torch.addmm(lw.bias, lb.x_in, lw.Wx, out_dtype=f32))
+                zx = lb.zx
+            if bufs["persist"]:
+                self.ops.lstm_persist_fwd(lw.WhT, zx, ids_arg, lb.hbuf, lb.cbuf, lb.gates,
+                                          lb.hlast32, bufs["cnt"], self.err, FORGET_BIAS,
+                                          self.spin_limit)
+            else:
+                self.ops.rnn_fwd_seq(self.cell, lw.WhT, lw.WT2, zx, ids_arg, lb.hbuf, lb.h32,
+                                     lb.cbuf, lb.gates, lb.pre, lb.aux, lb.rh, lb.hlast32,
+                                     FORGET_BIAS)
+            out = lb.hbuf[1:]
+            if drop and c.output_keep_prob < 1.0:
+                lb.masks["out"] = self._mask(out.shape, c.output_keep_prob)
+                out = out * lb.masks["out"]
+            x_prev = out
+        O = x_prev.reshape(N, H)
+        if not O.is_contiguous():
+            O = O.contiguous()
+        logits = bufs["logits"]
+        logits.copy_(torch.addmm(self._head["bs"], O, self._head["Ws"], out_dtype=f32))
+        new_state = []
+        for layer in range(self.L):
+            lb = bufs["layers"][layer]
+            if self.cfg.model in ("lstm", "nas"):
+                new_state.append((lb.cbuf[T].clone(), lb.hlast32.clone()))
+            elif self.cfg.model == "gru":
+                new_state.append((lb.h32[T].clone(),))
+            else:
+                new_state.append((lb.hlast32.clone(),))
+        return bufs, O, logits, new_state
+
+    # ------------------------------------------------------------------ training step
+    def train_step(self, x, y, state, on_ready=None, want_extras: bool = False):
+        ids_tm = x.t().contiguous()
+        tgt = y.t().contiguous().view(-1)
+        T, B = ids_tm.shape
+        H, V, N, GW = self.H, self.V, T * B, self.GW
+        bufs, O, logits, new_state = self._forward(ids_tm, state, True)
+        dlog = bufs["dlogits"]
+        self.ops.xent(logits, tgt, 1.0 / N, bufs["row_loss"], dlog, bufs["xpart"], bufs["loss"])
+        s, hd = self.store, self._head
+        # ---- head gradients
+        s.gview("rnnlm/softmax_w").copy_(_mm(O.t(), dlog))
+        self.ops.segsum(dlog, None, 1, bufs["colsum"][:, :V], bufs["ws"], False)
+        s.gview("rnnlm/softmax_b").copy_(bufs["colsum"][0, :V])
+        dtop = _mm(dlog, hd["Ws"].t()).view(T, B, H)
+        if on_ready is not None:
+            sb = s.by_name["rnnlm/softmax_b"]
+            on_ready(sb.offset + sb.numel)
+        drop = self._dropout(True)
+        c = self.cfg
+        for layer in reversed(range(self.L)):
+            lw, lb = self._w[layer], bufs["layers"][layer]
+            names = [sp.name for sp in cell_specs(self.cfg, layer)]
+            if "out" in lb.masks:
+                dtop = dtop * lb.masks["out"]
+            dtop = dtop.contiguous()
+            zx_nas = lb.zx if self.cfg.model == "nas" else None
+            if bufs["persist"]:
+                self.ops.lstm_persist_bwd(lw.Wh, dtop, lb.dz, lb.gates, lb.cbuf, bufs["cnt"],
+                                          self.err, self.spin_limit)
+            else:
+                self.ops.rnn_bwd_seq(self.cell, lw.Wh, lw.W2, dtop, lb.dz, lb.dzx, lb.gates,
+                                     lb.pre, lb.aux, zx_nas, lb.cbuf, lb.h32, lb.hbuf, bufs["dc"],
+                                     bufs["gpart"])
+            dZ = lb.dz.view(N, GW)
+            dZx = lb.dzx.view(N, GW) if lb.dzx is not None else dZ
+            Hprev = lb.hbuf[:T].reshape(N, H)
+            # recurrent-weight gradients
+            if self.cfg.model == "gru":
+                gk, gb, ck, cb = names
+                s.gview(gk)[H:].copy_(_mm(Hprev.t(), dZ[:, : 2 * H]))
+                s.gview(ck)[H:].copy_(_mm(lb.rh.view(N, H).t(), dZ[:, 2 * H:]))
+            elif self.cfg.model == "nas":
+                s.gview(names[1]).copy_(_mm(Hprev.t(), dZ))
+            else:
+                s.gview(names[0])[H:].copy_(_mm(Hprev.t(), dZ))
+            gather = (layer == 0 and not drop and self.cfg.model != "nas")
+            if gather:
+                dEW = torch.empty(V, GW, dtype=f32, device=self.dev)
+                self.ops.segsum(dZx, ids_tm.view(-1), V, dEW, bufs["ws"], False)
+                dWx = hd["E"].t() @ dEW                      # [H, GW] fp32
+                dbias = dEW.sum(0)
+                s.gview("embedding").copy_(dEW @ lw.Wx32.t())
+            else:
+                dWx = _mm(lb.x_in.t(), dZx)
+                self.ops.segsum(dZx, None, 1, bufs["colsum"][:, :GW], bufs["ws"], False)
+                dbias = bufs["colsum"][0, :GW]
+                dX = _mm(dZx, lw.Wx.t()).view(T, B, H)
+                if "in" in lb.masks:
+                    dX = dX * lb.masks["in"]
+                if layer > 0:
+                    dtop = dX
+                else:
+                    if "emb" in lb.masks:
+                        dX = dX * lb.masks["emb"]
+                    dXf = dX.reshape(N, H).float().contiguous()
+                    self.ops.segsum(dXf, ids_tm.view(-1), V, s.gview("embedding"), bufs["ws"], False)
+            self._write_input_grads(layer, names, dWx, dbias)
+            if on_ready is not None:
+                on_ready(None if layer == 0 else s.layer_range(layer)[1])
+        extras = {"logits": logits, "loss": bufs["row_loss"]} if want_extras else None
+        self._steps += 1
+        if bufs["persist"] and self._steps % 200 == 1:
+            self.check_errors()
+        return bufs["loss"][0], new_state, extras
+
+    def _write_input_grads(self, layer: int, names, dWx: torch.Tensor, dbias: torch.Tensor):
+        s, H = self.store, self.H
+        if self.cfg.model == "gru":
+            gk, gb, ck, cb = names
+            s.gview(gk)[:H].copy_(dWx[:, : 2 * H])
+            s.gview(ck)[:H].copy_(dWx[:, 2 * H:])
+            s.gview(gb).copy_(dbias[: 2 * H])
+            s.gview(cb).copy_(dbias[2 * H:])
+        elif self.cfg.model == "nas":
+            s.gview(names[0]).copy_(dWx)
+        else:
+            s.gview(names[0])[:H].copy_(dWx)
+            s.gview(names[1]).copy_(dbias)
+
+    # ------------------------------------------------------------------ inference
+    @torch.no_grad()
+    def step_logits(self, x_t: torch.Tensor, state):
+        ids_tm = x_t.t().contiguous()
+        bufs, O, logits, new_state = self._forward(ids_tm, state, False)
+        T, B = ids_tm.shape
+        lg = logits.view(T, B, self.V)[-1].clone()
+        return lg, new_state
+
+    @torch.no_grad()
+    def eval_loss(self, x, y, state):
+        ids_tm = x.t().contiguous()
+        tgt = y.t().contiguous().view(-1)
+        bufs, O, logits, new_state = self._forward(ids_tm, state, False)
+        self.ops.xent(logits, tgt, 1.0, None, None, bufs["xpart"], bufs["loss"])
+        return bufs["loss"][0].clone(), new_state
+
+    @torch.no_grad()
+    def sample_sequence(self, prime_ids, num: int, sampling_type: int, seed: int, num_samples: int,
+                        space_id: int = -1):
+        """Device-side autoregressive sampling; returns a [S, num] int tensor on the host."""
+        from ..models.reference import zero_state
+
+        S = num_samples
+        state = zero_state(self.cfg, S, self.dev)
+        g = torch.Generator(device=self.dev)
+        g.manual_seed(int(seed))
+        for cid in prime_ids[:-1]:
+            x = torch.full((S, 1), cid, dtype=torch.int32, device=self.dev)
+            _, state = self.step_logits(x, state)
+        cur = torch.full((S, 1), prime_ids[-1], dtype=torch.int32, device=self.dev)
+        out = torch.empty(S, num, dtype=torch.int32, device=self.dev)
+        for i in range(num):
+            logits, state = self.step_logits(cur, state)
+            p = torch.softmax(logits, -1)
+            cdf = torch.cumsum(p, -1)
+            r = torch.rand(S, 1, device=self.dev, generator=g) * cdf[:, -1:]
+            pick = torch.searchsorted(cdf, r).clamp_(max=self.V - 1).to(torch.int32)
+            if sampling_type == 0:
+                pick = p.argmax(-1, keepdim=True).to(torch.int32)
+            elif sampling_type == 2:
+                am = p.argmax(-1, keepdim=True).to(torch.int32)
+                pick = torch.where(cur == space_id, pick, am)
+            out[:, i: i + 1] = pick
+            cur = pick
+        return out.cpu().tolist()

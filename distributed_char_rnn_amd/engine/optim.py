@@ -69,6 +69,7 @@ class TFAdam:
             if self.mirror is not None:
                 self.mirror.copy_(p)
         self.t += 1
+        self.store.version += 1
         return self.last_norm
 
     # -- checkpoint support (TF slot names) ----------------------------------------------

@@ -36,7 +36,7 @@ def sample(model: CharRNN, chars: Sequence[str], vocab: Dict[str, int], num: int
     if native is not None and model.device.type == "cuda":
         ids = native([vocab[c] for c in prime], num, sampling_type,
                      seed if seed is not None else int(np.random.SeedSequence().entropy % (1 << 62)),
-                     num_samples)
+                     num_samples, vocab.get(" ", -1))
         return [prime + "".join(chars[int(i)] for i in row) for row in ids]
 
     rng = np.random.default_rng(seed)

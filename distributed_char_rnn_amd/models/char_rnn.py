@@ -39,7 +39,8 @@ class CharRNN:
         self.device = torch.device(device)
         self.store = ParamStore(cfg, self.device, seed)
         if backend == "auto":
-            backend = "native" if self.device.type == "cuda" else "reference"
+            # fp32 on the GPU runs the autograd oracle; the native kernels compute in bf16
+            backend = "native" if (self.device.type == "cuda" and dtype != "fp32") else "reference"
         self.backend_name = backend
         if backend == "native":
             from ..engine.native_backend import NativeBackend
@@ -69,6 +70,7 @@ class CharRNN:
 
     def params_changed(self):
         """Call after parameters were modified outside the optimizer (restore/broadcast)."""
+        self.store.version += 1
         hook = getattr(self.backend, "params_changed", None)
         if hook is not None:
             hook()

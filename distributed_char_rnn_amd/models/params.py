@@ -129,6 +129,7 @@ class ParamStore:
         self.flat = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
         self.grad = torch.zeros_like(self.flat)
         self.by_name: Dict[str, ParamSpec] = {s.name: s for s in self.specs}
+        self.version = 0  # bumped whenever `flat` changes (optimizer step, restore, broadcast)
         self.initialize(seed)
 
     # -- views ---------------------------------------------------------------------------
@@ -169,6 +170,7 @@ class ParamStore:
             else:
                 v.zero_()
         self.flat.copy_(host)
+        self.version = getattr(self, "version", 0) + 1
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
         return {s.name: self.view(s.name).detach().cpu().clone() for s in self.specs}
@@ -183,3 +185,4 @@ class ParamStore:
             if tuple(t.shape) != s.shape:
                 raise ValueError(f"{s.name}: shape {tuple(t.shape)} != {s.shape}")
             self.view(s.name).copy_(t.to(self.flat.dtype))
+        self.version += 1
