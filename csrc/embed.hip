@@ -38,17 +38,67 @@ __global__ void __launch_bounds__(kSegThreads) segsum_lds_kernel(
   const bool va = ca < W, vb = cb < W;
   const int r0 = chunk * rows_per_chunk;
   const int r1 = min(N, r0 + rows_per_chunk);
-  for (int n = r0 + wave; n < r1; n += kSegThreads / 64) {
-    const int v = ids ? ids[n] : 0;
-    const T* row = X + (size_t)n * ldx;
-    if (va) atomicAdd(&acc[v * kSegCols + lane], (float)row[ca]);
-    if (vb) atomicAdd(&acc[v * kSegCols + 64 + lane], (float)row[cb]);
+  constexpr int U = 8;  // rows in flight per wave (the loop is load-latency bound otherwise)
+  constexpr int WS = kSegThreads / 64;
+  for (int n = r0 + wave; n < r1; n += WS * U) {
+    int vv[U];
+    float xa[U], xb[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const int nn = n + WS * j;
+      const bool ok = nn < r1;
+      vv[j] = ok ? (ids ? ids[nn] : 0) : -1;
+      const T* row = X + (size_t)(ok ? nn : r0) * ldx;
+      xa[j] = (ok && va) ? (float)row[ca] : 0.f;
+      xb[j] = (ok && vb) ? (float)row[cb] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (vv[j] < 0) continue;
+      if (va) atomicAdd(&acc[vv[j] * kSegCols + lane], xa[j]);
+      if (vb) atomicAdd(&acc[vv[j] * kSegCols + 64 + lane], xb[j]);
+    }
   }
   __syncthreads();
   float* out = partial + (size_t)chunk * V * W;
   for (int i = threadIdx.x; i < V * kSegCols; i += kSegThreads) {
     const int v = i / kSegCols, cc = c0 + (i % kSegCols);
     if (cc < W) out[(size_t)v * W + cc] = acc[i];
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kSegThreads) colsum_kernel(const T* __restrict__ X, int ldx, int N,
+                                                            int W, int rows_per_chunk,
+                                                            float* __restrict__ partial) {
+  __shared__ float red[kSegThreads / 64][kSegCols];
+  const int c0 = blockIdx.x * kSegCols, chunk = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ca = c0 + lane, cb = c0 + 64 + lane;
+  const bool va = ca < W, vb = cb < W;
+  const int r0 = chunk * rows_per_chunk, r1 = min(N, r0 + rows_per_chunk);
+  constexpr int U = 8, WS = kSegThreads / 64;
+  float sa = 0.f, sb = 0.f;
+  for (int n = r0 + wave; n < r1; n += WS * U) {
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const int nn = n + WS * j;
+      if (nn < r1) {
+        const T* row = X + (size_t)nn * ldx;
+        if (va) sa += (float)row[ca];
+        if (vb) sb += (float)row[cb];
+      }
+    }
+  }
+  red[wave][lane] = sa;
+  red[wave][64 + lane] = sb;
+  __syncthreads();
+  if (wave == 0) {
+    float ta = 0.f, tb = 0.f;
+#pragma unroll
+    for (int k = 0; k < WS; ++k) { ta += red[k][lane]; tb += red[k][64 + lane]; }
+    if (va) partial[(size_t)chunk * W + ca] = ta;
+    if (vb) partial[(size_t)chunk * W + cb] = tb;
   }
 }
 
@@ -76,8 +126,9 @@ __global__ void __launch_bounds__(kSegThreads) segsum_atomic_kernel(const T* __r
 }
 
 int segsum_rows_per_chunk(int N) {
-  // ~16-32 chunks for large N: enough blocks to fill the chip with few partials
-  int r = (N + 31) / 32;
+  // ~64 chunks for large N: with the column strips this gives hundreds of workgroups, each
+  // keeping 8 rows of loads in flight per wave, while the partials stay a few MB
+  int r = (N + 63) / 64;
   r = ((r + 255) / 256) * 256;
   return r < 256 ? 256 : r;
 }
@@ -101,8 +152,12 @@ static void launch_segsum_t(const T* X, int ldx, const int* ids, int N, int W, i
   const int rpc = segsum_rows_per_chunk(N);
   const int nchunks = (N + rpc - 1) / rpc;
   dim3 grid((W + kSegCols - 1) / kSegCols, nchunks);
-  const size_t lds = sizeof(float) * V * kSegCols;
-  segsum_lds_kernel<T><<<grid, kSegThreads, lds, s>>>(X, ldx, ids, N, W, V, rpc, workspace);
+  if (ids == nullptr && V == 1) {
+    colsum_kernel<T><<<grid, kSegThreads, 0, s>>>(X, ldx, N, W, rpc, workspace);
+  } else {
+    const size_t lds = sizeof(float) * V * kSegCols;
+    segsum_lds_kernel<T><<<grid, kSegThreads, lds, s>>>(X, ldx, ids, N, W, V, rpc, workspace);
+  }
   const int64_t VW = (int64_t)V * W;
   int nb = (int)((VW + kSegThreads - 1) / kSegThreads);
   if (nb > 2048) nb = 2048;

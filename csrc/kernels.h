@@ -90,6 +90,10 @@ struct PersistArgs {
   float* hlast32;        // [B, H] fp32 final h
   const float* dtop;     // bwd: [T, B, H] fp32 gradient from above
   bf16* dz;              // bwd: [T, B, 4H] bf16 gate-pre-activation gradients
+  float* db_part;        // bwd: [B/16, 4H] per-batch-group bias-gradient partials (or nullptr)
+  const int* bids;       // (unused)
+  float* dew_part;       // bwd layer-0 gather mode: [B/16, V, 4H] dEW partials (or nullptr)
+  int V;
   unsigned* cnt;         // [B/16, T+1] arrival counters (zeroed by the launcher)
   unsigned* err;         // timeout / error word (0 = ok)
   int B, H, T;

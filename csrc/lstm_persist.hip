@@ -207,6 +207,8 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
 template <int KS, int UB>  // KS = k-steps per wave of the K = 4H reduction = H/32
 __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a) {
   __shared__ __attribute__((aligned(16))) float part[4][UB][64][4];
+  // optional fused dEW accumulator (layer-0 gather mode): [V][UB*64] fp32, dynamic
+  extern __shared__ __attribute__((aligned(16))) float dew_acc[];
   __shared__ int ok_flag;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -233,6 +235,18 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
   const int u0 = ub0 + (epi ? w : 0) * 16 + 4 * (lane >> 4);
   const size_t bh = (size_t)b * H + u0;
   float dc[4] = {0.f, 0.f, 0.f, 0.f};
+  // fused bias-gradient accumulation: sum over this lane's batch row and all steps
+  float dbacc[4][4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dbacc[g][r] = 0.f;
+  const bool fuse_dew = a.dew_part != nullptr;
+  const int DW = UB * 64;  // dEW columns owned by this workgroup: UB blocks x 4 gates x 16 units
+  if (fuse_dew) {
+    for (int i = threadIdx.x; i < a.V * DW; i += 256) dew_acc[i] = 0.f;
+    __syncthreads();
+  }
 
   for (int t = T - 1; t >= 0; --t) {
     // recurrence-independent epilogue operands, issued before the wait
@@ -298,6 +312,56 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
         if (lane == 0)
           __hip_atomic_fetch_add(cnt + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      // off the critical path (after the arrival): accumulate the bf16-rounded dz exactly as
+      // the dW GEMMs will see it
+      float q[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        q[0][r] = (float)f2bf(di[r]); q[1][r] = (float)f2bf(dj[r]);
+        q[2][r] = (float)f2bf(df_[r]); q[3][r] = (float)f2bf(dO[r]);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dbacc[g][r] += q[g][r];
+      if (fuse_dew) {
+        const int id = a.ids[(size_t)t * B + b];
+        float* row = dew_acc + (size_t)id * DW + w * 64 + 4 * (lane >> 4);
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) atomicAdd(row + g * 16 + r, q[g][r]);
+      }
+    }
+  }
+  // bias-gradient partial of this batch group: reduce the 16 batch lanes (lane bits 0..3)
+  if (epi && a.db_part) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = dbacc[g][r];
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        v += __shfl_xor(v, 4, 64);
+        v += __shfl_xor(v, 8, 64);
+        dbacc[g][r] = v;
+      }
+    if ((lane & 15) == 0) {
+      float* dst = a.db_part + (size_t)bg * G4H + u0;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(dst + g * H) =
+            make_float4(dbacc[g][0], dbacc[g][1], dbacc[g][2], dbacc[g][3]);
+    }
+  }
+  if (fuse_dew) {
+    __syncthreads();
+    // dew_part[bg][v][g*H + ub0 + ui*16 + j]
+    for (int i = threadIdx.x; i < a.V * DW; i += 256) {
+      const int v = i / DW, col = i % DW;
+      const int ui = col / 64, g = (col % 64) / 16, j = col % 16;
+      a.dew_part[((size_t)bg * a.V + v) * G4H + g * H + ub0 + ui * 16 + j] = dew_acc[i];
     }
   }
 }
@@ -311,7 +375,8 @@ static void fwd_inst(const PersistArgs& a, int grid, hipStream_t s) {
 }
 template <int KS, int UB>
 static void bwd_inst(const PersistArgs& a, int grid, hipStream_t s) {
-  lstm_bwd_persist_kernel<KS, UB><<<grid, 256, 0, s>>>(a);
+  const size_t lds = a.dew_part ? sizeof(float) * (size_t)a.V * UB * 64 : 0;
+  lstm_bwd_persist_kernel<KS, UB><<<grid, 256, lds, s>>>(a);
 }
 
 static int ub_for(int H, int B, int cus) {

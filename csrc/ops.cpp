@@ -363,7 +363,9 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
 
 void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& dz,
                       const at::Tensor& gates, const at::Tensor& cbuf, at::Tensor& cnt,
-                      at::Tensor& err, int64_t spin_limit) {
+                      at::Tensor& err, int64_t spin_limit, const c10::optional<at::Tensor>& db_part,
+                      const c10::optional<at::Tensor>& ids,
+                      const c10::optional<at::Tensor>& dew_part, int64_t V) {
   check_seq(W, at::kBFloat16, "W");
   check_seq(dtop, at::kFloat, "dtop");
   check_seq(dz, at::kBFloat16, "dz");
@@ -385,6 +387,19 @@ void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& d
   a.err = reinterpret_cast<unsigned*>(err.data_ptr());
   a.B = B; a.H = H; a.T = T;
   a.spin_limit = (unsigned)spin_limit;
+  check_opt(db_part, at::kFloat, "db_part");
+  check_opt(dew_part, at::kFloat, "dew_part");
+  check_opt(ids, at::kInt, "ids");
+  if (has(db_part)) TORCH_CHECK(db_part->numel() == (int64_t)(B / 16) * 4 * H, "db_part must be [B/16, 4H]");
+  a.db_part = optr<float>(db_part);
+  if (has(dew_part)) {
+    TORCH_CHECK(has(ids) && ids->numel() == (int64_t)T * B, "dew_part needs ids [T, B]");
+    TORCH_CHECK(V >= 1 && V <= 128, "fused dEW supports V <= 128");
+    TORCH_CHECK(dew_part->numel() == (int64_t)(B / 16) * V * 4 * H, "dew_part must be [B/16, V, 4H]");
+    a.dew_part = optr<float>(dew_part);
+    a.ids = optr<int>(ids);
+    a.V = (int)V;
+  }
   dcr::launch_lstm_bwd_persist(a, num_cus(), cur_stream());
 }
 
@@ -417,7 +432,8 @@ TORCH_LIBRARY(dcr, m) {
       "int spin_limit) -> ()");
   m.def(
       "lstm_persist_bwd(Tensor W, Tensor dtop, Tensor(a!) dz, Tensor gates, Tensor cbuf, "
-      "Tensor(b!) cnt, Tensor(c!) err, int spin_limit) -> ()");
+      "Tensor(b!) cnt, Tensor(c!) err, int spin_limit, Tensor(d!)? db_part, Tensor? ids, "
+      "Tensor(e!)? dew_part, int V) -> ()");
   m.def("segsum(Tensor X, Tensor? ids, int V, Tensor(a!) out, Tensor(b!) workspace, bool accumulate) -> ()");
   m.def("segsum_workspace(int N, int W, int V) -> int", [](int64_t N, int64_t W, int64_t V) -> int64_t {
     return (int64_t)dcr::segsum_workspace_floats((int)N, (int)W, (int)V);

@@ -42,6 +42,27 @@ def _mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return torch.mm(a, b, out_dtype=f32)
 
 
+_OUT_OK = [None]
+
+
+def _mm_into(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor,
+             bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """GEMM written straight into ``out`` (e.g. a gradient view of the flat buffer), avoiding
+    a temporary + copy; falls back to copy if this torch build lacks the out= overload."""
+    if _OUT_OK[0] is not False and out.is_contiguous():
+        try:
+            if bias is None:
+                torch.mm(a, b, out_dtype=f32, out=out)
+            else:
+                torch.addmm(bias, a, b, out_dtype=f32, out=out)
+            _OUT_OK[0] = True
+            return out
+        except (RuntimeError, TypeError):
+            _OUT_OK[0] = False
+    out.copy_(_mm(a, b) if bias is None else torch.addmm(bias, a, b, out_dtype=f32))
+    return out
+
+
 @dataclass
 class LayerWeights:
     Wx: torch.Tensor            # [D, GW] bf16 input projection
@@ -173,6 +194,12 @@ class NativeBackend:
             ws=torch.empty(ws, dtype=f32, device=dev),
             colsum=torch.empty(1, max(GW, self.V), dtype=f32, device=dev),
             persist=self._persist_ok(B),
+            dtop=torch.empty(T, B, H, dtype=f32, device=dev) if training else None,
+            dx=torch.empty(T, B, H, dtype=f32, device=dev) if training else None,
+            db_part=(torch.empty(max(B // 16, 1), GW, dtype=f32, device=dev)
+                     if training else None),
+            dew_part=(torch.empty(max(B // 16, 1), self.V, GW, dtype=f32, device=dev)
+                      if (training and self.V <= 128) else None),
             cnt=torch.zeros((B // 16 + 1) * (T + 1), dtype=torch.int32, device=dev),
         )
         self._bufs[key] = bufs
@@ -233,7 +260,7 @@ class NativeBackend:
                     lb.masks["in"] = self._mask(X.shape, c.input_keep_prob)
                     X = X * lb.masks["in"]
                 lb.x_in = X.reshape(N, H).contiguous()
-                lb.zx.view(N, self.GW).copy_(torch.addmm(lw.bias, lb.x_in, lw.Wx, out_dtype=f32))
+                _mm_into(lb.x_in, lw.Wx, lb.zx.view(N, self.GW), bias=lw.bias)
                 zx = lb.zx
             if bufs["persist"]:
                 self.ops.lstm_persist_fwd(lw.WhT, zx, ids_arg, lb.hbuf, lb.cbuf, lb.gates,
@@ -252,7 +279,7 @@ class NativeBackend:
         if not O.is_contiguous():
             O = O.contiguous()
         logits = bufs["logits"]
-        logits.copy_(torch.addmm(self._head["bs"], O, self._head["Ws"], out_dtype=f32))
+        _mm_into(O, self._head["Ws"], logits, bias=self._head["bs"])
         new_state = []
         for layer in range(self.L):
             lb = bufs["layers"][layer]
@@ -275,10 +302,10 @@ class NativeBackend:
         self.ops.xent(logits, tgt, 1.0 / N, bufs["row_loss"], dlog, bufs["xpart"], bufs["loss"])
         s, hd = self.store, self._head
         # ---- head gradients
-        s.gview("rnnlm/softmax_w").copy_(_mm(O.t(), dlog))
+        _mm_into(O.t(), dlog, s.gview("rnnlm/softmax_w"))
         self.ops.segsum(dlog, None, 1, bufs["colsum"][:, :V], bufs["ws"], False)
         s.gview("rnnlm/softmax_b").copy_(bufs["colsum"][0, :V])
-        dtop = _mm(dlog, hd["Ws"].t()).view(T, B, H)
+        dtop = _mm_into(dlog, hd["Ws"].t(), bufs["dtop"].view(N, H)).view(T, B, H)
         if on_ready is not None:
             sb = s.by_name["rnnlm/softmax_b"]
             on_ready(sb.offset + sb.numel)
@@ -291,9 +318,13 @@ class NativeBackend:
                 dtop = dtop * lb.masks["out"]
             dtop = dtop.contiguous()
             zx_nas = lb.zx if self.cfg.model == "nas" else None
+            gather = (layer == 0 and not drop and self.cfg.model != "nas")
+            fused_dew = bufs["persist"] and gather and V <= 128
             if bufs["persist"]:
                 self.ops.lstm_persist_bwd(lw.Wh, dtop, lb.dz, lb.gates, lb.cbuf, bufs["cnt"],
-                                          self.err, self.spin_limit)
+                                          self.err, self.spin_limit, bufs["db_part"],
+                                          ids_tm if fused_dew else None,
+                                          bufs["dew_part"] if fused_dew else None, V)
             else:
                 self.ops.rnn_bwd_seq(self.cell, lw.Wh, lw.W2, dtop, lb.dz, lb.dzx, lb.gates,
                                      lb.pre, lb.aux, zx_nas, lb.cbuf, lb.h32, lb.hbuf, bufs["dc"],
@@ -307,21 +338,26 @@ class NativeBackend:
                 s.gview(gk)[H:].copy_(_mm(Hprev.t(), dZ[:, : 2 * H]))
                 s.gview(ck)[H:].copy_(_mm(lb.rh.view(N, H).t(), dZ[:, 2 * H:]))
             elif self.cfg.model == "nas":
-                s.gview(names[1]).copy_(_mm(Hprev.t(), dZ))
+                _mm_into(Hprev.t(), dZ, s.gview(names[1]))
             else:
-                s.gview(names[0])[H:].copy_(_mm(Hprev.t(), dZ))
-            gather = (layer == 0 and not drop and self.cfg.model != "nas")
+                _mm_into(Hprev.t(), dZ, s.gview(names[0])[H:])
             if gather:
-                dEW = torch.empty(V, GW, dtype=f32, device=self.dev)
-                self.ops.segsum(dZx, ids_tm.view(-1), V, dEW, bufs["ws"], False)
+                if fused_dew:
+                    dEW = bufs["dew_part"].sum(0)            # [V, GW] fp32 (fused in BPTT)
+                else:
+                    dEW = torch.empty(V, GW, dtype=f32, device=self.dev)
+                    self.ops.segsum(dZx, ids_tm.view(-1), V, dEW, bufs["ws"], False)
                 dWx = hd["E"].t() @ dEW                      # [H, GW] fp32
                 dbias = dEW.sum(0)
-                s.gview("embedding").copy_(dEW @ lw.Wx32.t())
+                torch.mm(dEW, lw.Wx32.t(), out=s.gview("embedding"))
             else:
                 dWx = _mm(lb.x_in.t(), dZx)
-                self.ops.segsum(dZx, None, 1, bufs["colsum"][:, :GW], bufs["ws"], False)
-                dbias = bufs["colsum"][0, :GW]
-                dX = _mm(dZx, lw.Wx.t()).view(T, B, H)
+                if bufs["persist"]:
+                    dbias = bufs["db_part"].sum(0)           # fused in BPTT
+                else:
+                    self.ops.segsum(dZx, None, 1, bufs["colsum"][:, :GW], bufs["ws"], False)
+                    dbias = bufs["colsum"][0, :GW]
+                dX = _mm_into(dZx, lw.Wx.t(), bufs["dx"].view(N, H)).view(T, B, H)
                 if "in" in lb.masks:
                     dX = dX * lb.masks["in"]
                 if layer > 0:

@@ -48,7 +48,7 @@ def write_bundle(prefix: str, tensors: Dict[str, object]) -> None:
     off = 0
     with open(tmp, "wb") as f:
         for name in sorted(tensors):
-            a = np.ascontiguousarray(_to_numpy(tensors[name]))
+            a = np.require(_to_numpy(tensors[name]), requirements="C")  # keeps 0-d scalars
             if a.dtype.name not in _DT:
                 a = a.astype(np.float32)
             b = a.astype(a.dtype.newbyteorder("<"), copy=False).tobytes()
