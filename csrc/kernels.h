@@ -94,6 +94,7 @@ struct PersistArgs {
   const int* bids;       // (unused)
   float* dew_part;       // bwd layer-0 gather mode: [B/16, V, 4H] dEW partials (or nullptr)
   int V;
+  uint64_t* ring;        // fwd granule hand-off: [2, B, H/2] tagged granules (nullptr = counters)
   unsigned* cnt;         // [B/16, T+1] arrival counters (zeroed by the launcher)
   unsigned* err;         // timeout / error word (0 = ok)
   int B, H, T;

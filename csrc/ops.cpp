@@ -323,7 +323,7 @@ int64_t lstm_persist_supported(int64_t H, int64_t B) {
 void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::optional<at::Tensor>& ids,
                       at::Tensor& hbuf, at::Tensor& cbuf, const c10::optional<at::Tensor>& gates,
                       at::Tensor& hlast32, at::Tensor& cnt, at::Tensor& err, double forget_bias,
-                      int64_t spin_limit) {
+                      int64_t spin_limit, const c10::optional<at::Tensor>& ring) {
   check_seq(WT, at::kBFloat16, "WT");
   check_seq(zx, at::kFloat, "zx");
   check_seq(hbuf, at::kBFloat16, "hbuf");
@@ -343,7 +343,7 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
     TORCH_CHECK(zx.numel() == (int64_t)T * B * 4 * H, "zx must be [T, B, 4H]");
   }
   if (has(gates)) TORCH_CHECK(gates->numel() == (int64_t)T * B * 4 * H, "gates must be [T, B, 4H]");
-  TORCH_CHECK(cnt.numel() >= (int64_t)(B / 16) * (T + 1), "counter buffer too small");
+  TORCH_CHECK(cnt.numel() >= (int64_t)(B / 16) * (T + 1) * 4, "counter buffer too small");
   dcr::PersistArgs a{};
   a.W = ptr<bf16>(WT);
   a.zx = ptr<float>(zx);
@@ -358,6 +358,11 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
   a.B = B; a.H = H; a.T = T;
   a.forget_bias = (float)forget_bias;
   a.spin_limit = (unsigned)spin_limit;
+  if (has(ring)) {
+    TORCH_CHECK(ring->is_cuda() && ring->element_size() == 8 && ring->is_contiguous(), "ring must be a contiguous 8-byte GPU tensor");
+    TORCH_CHECK(ring->numel() >= (int64_t)2 * B * (H / 2), "ring must hold [2, B, H/2] granules");
+    a.ring = reinterpret_cast<uint64_t*>(ring->data_ptr());
+  }
   dcr::launch_lstm_fwd_persist(a, num_cus(), cur_stream());
 }
 
@@ -376,7 +381,7 @@ void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& d
   TORCH_CHECK(W.size(0) == H && W.size(1) == 4 * H, "W must be [H, 4H]");
   TORCH_CHECK(dz.numel() == (int64_t)T * B * 4 * H && gates.numel() == (int64_t)T * B * 4 * H, "dz/gates shape");
   TORCH_CHECK(cbuf.numel() == (int64_t)(T + 1) * B * H, "cbuf shape");
-  TORCH_CHECK(cnt.numel() >= (int64_t)(B / 16) * (T + 1), "counter buffer too small");
+  TORCH_CHECK(cnt.numel() >= (int64_t)(B / 16) * (T + 1) * 4, "counter buffer too small");
   dcr::PersistArgs a{};
   a.W = ptr<bf16>(W);
   a.dtop = ptr<float>(dtop);
@@ -429,7 +434,7 @@ TORCH_LIBRARY(dcr, m) {
   m.def(
       "lstm_persist_fwd(Tensor WT, Tensor zx, Tensor? ids, Tensor(a!) hbuf, Tensor(b!) cbuf, "
       "Tensor(c!)? gates, Tensor(d!) hlast32, Tensor(e!) cnt, Tensor(f!) err, float forget_bias, "
-      "int spin_limit) -> ()");
+      "int spin_limit, Tensor(g!)? ring) -> ()");
   m.def(
       "lstm_persist_bwd(Tensor W, Tensor dtop, Tensor(a!) dz, Tensor gates, Tensor cbuf, "
       "Tensor(b!) cnt, Tensor(c!) err, int spin_limit, Tensor(d!)? db_part, Tensor? ids, "

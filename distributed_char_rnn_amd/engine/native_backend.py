@@ -112,6 +112,8 @@ class NativeBackend:
         self._bufs: Dict[Tuple[int, int, bool], dict] = {}
         self.use_persist = os.environ.get("DCR_PERSIST", "1") != "0"
         self.spin_limit = int(os.environ.get("DCR_SPIN_LIMIT", str(1 << 22)))
+        # forward hand-off form: "granule" (tagged data, R2) or "counter" (sc1 data + counter)
+        self.handoff = os.environ.get("DCR_HANDOFF", "counter")
         self.err = torch.zeros(1, dtype=torch.int32, device=self.dev)
         self._steps = 0
         self.gen = torch.Generator(device=self.dev)
@@ -200,7 +202,8 @@ class NativeBackend:
                      if training else None),
             dew_part=(torch.empty(max(B // 16, 1), self.V, GW, dtype=f32, device=dev)
                       if (training and self.V <= 128) else None),
-            cnt=torch.zeros((B // 16 + 1) * (T + 1), dtype=torch.int32, device=dev),
+            cnt=torch.zeros((B // 16 + 1) * (T + 1) * 4, dtype=torch.int32, device=dev),
+            ring=torch.zeros(2 * B * (H // 2), dtype=torch.int64, device=dev),
         )
         self._bufs[key] = bufs
         return bufs
@@ -265,7 +268,8 @@ class NativeBackend:
             if bufs["persist"]:
                 self.ops.lstm_persist_fwd(lw.WhT, zx, ids_arg, lb.hbuf, lb.cbuf, lb.gates,
                                           lb.hlast32, bufs["cnt"], self.err, FORGET_BIAS,
-                                          self.spin_limit)
+                                          self.spin_limit,
+                                          bufs["ring"] if self.handoff == "granule" else None)
             else:
                 self.ops.rnn_fwd_seq(self.cell, lw.WhT, lw.WT2, zx, ids_arg, lb.hbuf, lb.h32,
                                      lb.cbuf, lb.gates, lb.pre, lb.aux, lb.rh, lb.hlast32,

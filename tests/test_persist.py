@@ -17,9 +17,10 @@ def rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
 
 
-@pytest.fixture(autouse=True)
-def _short_spins(monkeypatch):
+@pytest.fixture(autouse=True, params=["granule", "counter"])
+def _short_spins(monkeypatch, request):
     monkeypatch.setenv("DCR_SPIN_LIMIT", str(1 << 20))
+    monkeypatch.setenv("DCR_HANDOFF", request.param)
 
 
 @pytest.mark.parametrize("B,T,H,L", [(32, 5, 128, 2), (48, 7, 256, 1), (64, 9, 512, 2),
