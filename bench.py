@@ -43,6 +43,8 @@ def parse(argv=None):
     ap.add_argument("--bucket_mb", type=float, default=8.0)
     ap.add_argument("--allreduce_dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--profile", action="store_true", help="print a per-phase timing table")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu = plumbing check of the multi-rank contract (reference backend, gloo)")
     return ap.parse_args(argv)
 
 
@@ -61,8 +63,12 @@ def main(argv=None) -> int:
             print(f"--gpus {a.gpus} needs torch.distributed.run with {a.gpus} processes",
                   file=sys.stderr)
             return 2
-    device = process_group.pick_device(topo, "cuda")
+    device = process_group.pick_device(topo, a.device)
     ctx = process_group.init(topo, device, "nccl" if device.type == "cuda" else "gloo")
+
+    def sync_dev():
+        if device.type == "cuda":
+            torch.cuda.synchronize()
     rank, world = max(ctx.rank, 0), ctx.world_size
 
     cfg = ModelConfig(model=a.model, vocab_size=a.vocab, rnn_size=a.hidden, num_layers=a.layers)
@@ -107,18 +113,18 @@ def main(argv=None) -> int:
 
     for i in range(a.warmup):
         loss, state = step(i, state)
-    torch.cuda.synchronize()
+    sync_dev()
     if prof is not None:
         prof.collect()
         prof.totals.clear()
         prof.counts.clear()
     ctx.barrier()
-    torch.cuda.synchronize()
+    sync_dev()
     t0 = time.perf_counter()
     for i in range(a.steps):
         loss, state = step(a.warmup + i, state)
     ctx.barrier()
-    torch.cuda.synchronize()
+    sync_dev()
     dt = time.perf_counter() - t0
     dt = ctx.all_reduce_scalar(dt, dist.ReduceOp.MAX) if world > 1 else dt
     final_loss = float(loss)
@@ -131,7 +137,7 @@ def main(argv=None) -> int:
             "metric": METRIC, "value": cps, "unit": "chars/sec", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16", "data": "synthetic (Shakespeare-unigram token stream, random-init weights)",
+            "dtype": "bf16" if device.type == "cuda" else "fp32", "data": "synthetic (Shakespeare-unigram token stream, random-init weights)",
             "config": {"model": f"{a.layers}-layer {a.model.upper()}-{a.hidden} (vocab {a.vocab})",
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": T,
                        "parallelism": f"dp{world}"},

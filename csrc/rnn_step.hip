@@ -17,6 +17,8 @@
 //  * State (c) and the backward carry (dc) stay fp32; MFMA operands bf16 with fp32 accumulate.
 //  * Backward: dh_rec = dZ_{t+1}·W_hᵀ uses W_h in its TF layout [H, G·H] (k contiguous) as the
 //    A operand; the epilogue fuses the cell's pointwise backward and emits dZ_t (bf16).
+// Each workgroup owns one 16-unit x 16-batch output tile; its 4 waves split the K reduction
+// (interleaved 32-wide k-steps, next step's fragments prefetched) and combine through LDS.
 // The time loop runs in C++ (ops.cpp) so one op call launches all T steps of a layer without
 // touching Python; the whole sequence is hipGraph-capturable.  The persistent (weights-resident)
 // LSTM kernels in lstm_persist.hip replace these for the flagship config.
@@ -32,22 +34,57 @@ template <> struct CellG<CELL_GRU_B> { static constexpr int G = 1; };
 template <> struct CellG<CELL_RNN> { static constexpr int G = 1; };
 template <> struct CellG<CELL_NAS> { static constexpr int G = 8; };
 
-// acc[t] += sum_k A[arow_t][k] * Bm[brow][k]  over k in [0, K)  (16x16x32 MFMA tiles)
+// Block-cooperative tile GEMM: acc[t] = sum_k A[arow_t][k] * Bm[brow][k] over k in [0, K).
+// The 4 waves of the workgroup take interleaved 32-wide k-steps (wave w: s = w, w+4, ...), keep
+// the next step's fragments in flight while the current MFMAs run, and meet in LDS; on return
+// wave 0 holds the full sums (other waves return garbage and must not use them).
 template <int NT>
-__device__ __forceinline__ void mfma_rows(f32x4 (&acc)[NT], const bf16* __restrict__ A,
+__device__ __forceinline__ void tile_gemm(f32x4 (&acc)[NT], const bf16* __restrict__ A,
                                           const int (&arow)[NT], int lda,
                                           const bf16* __restrict__ Bm, int brow, int ldb, int K,
-                                          int lane) {
+                                          int lane, int w, float* part /* [4][NT][64][4] */) {
   const int kq = 8 * (lane >> 4);
   const bf16* bp = Bm + (size_t)brow * ldb + kq;
   const bf16* ap[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) ap[t] = A + (size_t)arow[t] * lda + kq;
-
-  for (int k0 = 0; k0 < K; k0 += 32) {
-    const bf16x8 b = ld8(bp + k0);
+  for (int t = 0; t < NT; ++t) {
+    ap[t] = A + (size_t)arow[t] * lda + kq;
+    acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int KS = K / 32;
+  int s = w;
+  if (s < KS) {
+    bf16x8 b = ld8(bp + s * 32);
+    bf16x8 a[NT];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = mfma16(ld8(ap[t] + k0), b, acc[t]);
+    for (int t = 0; t < NT; ++t) a[t] = ld8(ap[t] + s * 32);
+    for (; s < KS; s += 4) {
+      const int sn = s + 4 < KS ? s + 4 : s;  // prefetch (re-load the last step when done)
+      const bf16x8 bn = ld8(bp + sn * 32);
+      bf16x8 an[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) an[t] = ld8(ap[t] + sn * 32);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = mfma16(a[t], b, acc[t]);
+      b = bn;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) a[t] = an[t];
+    }
+  }
+  if (w != 0) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      *reinterpret_cast<f32x4*>(part + ((size_t)(w * NT + t) * 64 + lane) * 4) = acc[t];
+  }
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int ww = 1; ww < 4; ++ww)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const f32x4 p = *reinterpret_cast<const f32x4*>(part + ((size_t)(ww * NT + t) * 64 + lane) * 4);
+        acc[t] += p;
+      }
   }
 }
 
@@ -74,21 +111,20 @@ __device__ __forceinline__ void f4arr(const float4 v, float (&o)[4]) {
 template <int CELL>
 __global__ void __launch_bounds__(256) fwd_step_kernel(FwdStepArgs a) {
   constexpr int G = CellG<CELL>::G;
+  __shared__ __attribute__((aligned(16))) float part[4 * G * 64 * 4];
   const int lane = threadIdx.x & 63;
-  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B;
-  const int nub = H / 16, nbt = (B + 15) / 16;
-  if (wave >= nub * nbt) return;
-  const int ub = (wave % nub) * 16, b0 = (wave / nub) * 16;
+  const int nub = H / 16;
+  const int ub = (blockIdx.x % nub) * 16, b0 = (blockIdx.x / nub) * 16;
 
   f32x4 acc[G];
-#pragma unroll
-  for (int g = 0; g < G; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
   int arow[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) arow[g] = g * H + ub + (lane & 15);
   const int brow = min(b0 + (lane & 15), B - 1);
-  mfma_rows<G>(acc, a.WT, arow, H, a.hop, brow, H, H, lane);
+  tile_gemm<G>(acc, a.WT, arow, H, a.hop, brow, H, H, lane, w, part);
+  if (w != 0) return;
 
   const int b = b0 + (lane & 15);
   if (b >= B) return;
@@ -185,18 +221,19 @@ __global__ void __launch_bounds__(256) fwd_step_kernel(FwdStepArgs a) {
 // ------------------------------------------------------------------------------------------
 template <int CELL>
 __global__ void __launch_bounds__(256) bwd_step_kernel(BwdStepArgs a) {
+  __shared__ __attribute__((aligned(16))) float part[4 * 64 * 4];
   const int lane = threadIdx.x & 63;
-  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B;
-  const int nub = H / 16, nbt = (B + 15) / 16;
-  if (wave >= nub * nbt) return;
-  const int ub = (wave % nub) * 16, b0 = (wave / nub) * 16;
+  const int nub = H / 16;
+  const int ub = (blockIdx.x % nub) * 16, b0 = (blockIdx.x / nub) * 16;
   f32x4 acc[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
   if (a.dz_next) {
     const int arow[1] = {ub + (lane & 15)};
     const int brow = min(b0 + (lane & 15), B - 1);
-    mfma_rows<1>(acc, a.W, arow, a.K, a.dz_next, brow, a.dz_ld, a.K, lane);
+    tile_gemm<1>(acc, a.W, arow, a.K, a.dz_next, brow, a.dz_ld, a.K, lane, w, part);
   }
+  if (w != 0) return;
   const int b = b0 + (lane & 15);
   if (b >= B) return;
   const int u0 = ub + 4 * (lane >> 4);
@@ -329,8 +366,7 @@ __global__ void __launch_bounds__(256) bwd_step_kernel(BwdStepArgs a) {
 }
 
 static inline int step_blocks(int B, int H) {
-  const int waves = ((B + 15) / 16) * (H / 16);
-  return (waves + 3) / 4;
+  return ((B + 15) / 16) * (H / 16);  // one 16-unit x 16-batch output tile per workgroup
 }
 
 void launch_fwd_step(int cell, const FwdStepArgs& a, hipStream_t s) {
