@@ -97,6 +97,7 @@ struct PersistArgs {
   uint64_t* ring;        // fwd granule hand-off: [2, B, H/2] tagged granules (nullptr = counters)
   unsigned* cnt;         // [B/16, T+1] arrival counters (zeroed by the launcher)
   unsigned* err;         // timeout / error word (0 = ok)
+  unsigned long long* diag;  // optional [T, 8] s_memtime stamps of workgroup 0 (diagnostics)
   int B, H, T;
   float forget_bias;
   unsigned spin_limit;

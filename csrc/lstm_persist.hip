@@ -102,7 +102,14 @@ __device__ __forceinline__ void arrive(unsigned* cnt) {
 // ------------------------------------------------------------------------------------------
 // forward
 // ------------------------------------------------------------------------------------------
-template <int KS, int UB>  // KS = k-steps (of 32) per wave = H/128; UB = 16-unit blocks per WG
+// DIAG builds record s_memtime stamps of workgroup 0 per step (never used for timing claims,
+// only for the share of each phase; cdna_hip_programming.md §7 "In-kernel stamps")
+#define STAMP(i)                                                                    \
+  if constexpr (DIAG) {                                                             \
+    if (blockIdx.x == 0 && threadIdx.x == 0)                                        \
+      a.diag[(size_t)t * 8 + (i)] = __builtin_amdgcn_s_memtime();                   \
+  }
+template <int KS, int UB, bool DIAG = false>  // KS = k-steps (of 32) per wave = H/128
 __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a) {
   // partials double-buffered by step parity: without a workgroup barrier before the MFMAs a
   // wave may start step t+1 while the epilogue wave still reads step t's partials
@@ -140,6 +147,7 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
   if (epi) ld4f(a.cbuf + bh, c);
 
   for (int t = 0; t < T; ++t) {
+    STAMP(0)
     // x-projection pre-activations of step t (independent of the recurrence: issue early)
     float zx[4][4];
     if (epi) {
@@ -152,8 +160,10 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
       // ONE poller per workgroup (pollers cost chip bandwidth); the barrier releases the waves
       if (threadIdx.x == 0 && !dead)
         dead = !poll_quarters(cnt + (size_t)t * 4, (unsigned)(H / 64), a.spin_limit, a.err, 1u);
+      STAMP(1)
       __syncthreads();
     }
+    STAMP(2)
     // h_{t-1} fragments (handed off by other workgroups: sc1 loads only)
     const __amdgpu_buffer_rsrc_t hsrc =
         make_rsrc(a.hbuf + (size_t)t * B * H, sizeof(bf16) * (size_t)B * H);
@@ -173,7 +183,9 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
 #pragma unroll
       for (int g = 0; g < 4; ++g) dst[g] = make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
     }
+    STAMP(3)
     __syncthreads();
+    STAMP(4)
     if (epi) {
       float z[4][4];
 #pragma unroll
@@ -198,6 +210,7 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
         h[r] = go[r] * tanhf_(c[r]);
       }
       const size_t o = (size_t)(t + 1) * B * H + bh;
+      STAMP(5)
       st4bf_sc1(a.hbuf + o, h[0], h[1], h[2], h[3]);  // handed off: write-through
       *reinterpret_cast<float4*>(a.cbuf + o) = make_float4(c[0], c[1], c[2], c[3]);
       if (a.gates) {
@@ -213,6 +226,7 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
         // each epilogue wave publishes its own 16-unit slab: drain its write-through stores,
         // then one lane arrives on the counter of the K-quarter its units belong to
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        STAMP(6)
         if (lane == 0)
           __hip_atomic_fetch_add(cnt + (size_t)(t + 1) * 4 + (u0 / (H / 4)), 1u, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
@@ -287,6 +301,28 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_granule_kernel(PersistArgs a)
       const __amdgpu_buffer_rsrc_t rs =
           make_rsrc(a.ring + (size_t)(t & 1) * B * HG, sizeof(uint64_t) * (size_t)B * HG);
       const unsigned tag = (unsigned)t;
+      // probe: wave 0 watches ONE sentinel granule per producer slab (the last granule of batch
+      // row b0+15 of every 16-unit slab; lane l < H/16 watches slab l) so the payload is read
+      // ~once instead of being re-polled by every wave; stores are unordered, so the payload
+      // tags are still verified below (re-polled on the rare miss)
+      if (w == 0 && !dead) {
+        const int nslab = H / 16;
+        const unsigned soff = (unsigned)((((size_t)(b0 + 15) * HG) + (lane % nslab) * 8 + 7) *
+                                         sizeof(uint64_t));
+        unsigned sp = 0;
+        for (;;) {
+          typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+          const u32x2 gv = __builtin_amdgcn_raw_buffer_load_b64(rs, soff, 0, kAuxSc1);
+          if (__all(gv[1] == tag)) break;
+          if (++sp > a.spin_limit) {
+            __hip_atomic_store(a.err, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            dead = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __syncthreads();
       unsigned spins = 0;
       for (;;) {
         bool ok = true;
@@ -542,7 +578,8 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
 // ------------------------------------------------------------------------------------------
 template <int KS, int UB>
 static void fwd_inst(const PersistArgs& a, int grid, hipStream_t s) {
-  lstm_fwd_persist_kernel<KS, UB><<<grid, 256, 0, s>>>(a);
+  if (a.diag) lstm_fwd_persist_kernel<KS, UB, true><<<grid, 256, 0, s>>>(a);
+  else lstm_fwd_persist_kernel<KS, UB, false><<<grid, 256, 0, s>>>(a);
 }
 template <int KS, int UB>
 static void fwd_granule_inst(const PersistArgs& a, int grid, hipStream_t s) {

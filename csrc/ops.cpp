@@ -323,7 +323,8 @@ int64_t lstm_persist_supported(int64_t H, int64_t B) {
 void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::optional<at::Tensor>& ids,
                       at::Tensor& hbuf, at::Tensor& cbuf, const c10::optional<at::Tensor>& gates,
                       at::Tensor& hlast32, at::Tensor& cnt, at::Tensor& err, double forget_bias,
-                      int64_t spin_limit, const c10::optional<at::Tensor>& ring) {
+                      int64_t spin_limit, const c10::optional<at::Tensor>& ring,
+                      const c10::optional<at::Tensor>& diag) {
   check_seq(WT, at::kBFloat16, "WT");
   check_seq(zx, at::kFloat, "zx");
   check_seq(hbuf, at::kBFloat16, "hbuf");
@@ -362,6 +363,10 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
     TORCH_CHECK(ring->is_cuda() && ring->element_size() == 8 && ring->is_contiguous(), "ring must be a contiguous 8-byte GPU tensor");
     TORCH_CHECK(ring->numel() >= (int64_t)2 * B * (H / 2), "ring must hold [2, B, H/2] granules");
     a.ring = reinterpret_cast<uint64_t*>(ring->data_ptr());
+  }
+  if (has(diag)) {
+    TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)T * 8, "diag must hold [T, 8] int64");
+    a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());
   }
   dcr::launch_lstm_fwd_persist(a, num_cus(), cur_stream());
 }
@@ -434,7 +439,7 @@ TORCH_LIBRARY(dcr, m) {
   m.def(
       "lstm_persist_fwd(Tensor WT, Tensor zx, Tensor? ids, Tensor(a!) hbuf, Tensor(b!) cbuf, "
       "Tensor(c!)? gates, Tensor(d!) hlast32, Tensor(e!) cnt, Tensor(f!) err, float forget_bias, "
-      "int spin_limit, Tensor(g!)? ring) -> ()");
+      "int spin_limit, Tensor(g!)? ring, Tensor(h!)? diag=None) -> ()");
   m.def(
       "lstm_persist_bwd(Tensor W, Tensor dtop, Tensor(a!) dz, Tensor gates, Tensor cbuf, "
       "Tensor(b!) cnt, Tensor(c!) err, int spin_limit, Tensor(d!)? db_part, Tensor? ids, "

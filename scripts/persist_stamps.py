@@ -1,0 +1,34 @@
+"""Diagnostic: s_memtime phase shares of the persistent LSTM forward (workgroup 0)."""
+import torch
+from distributed_char_rnn_amd.ops import native
+
+ops = native.ops()
+B, T, H = 256, 128, 512
+dev = "cuda"
+WT = (torch.randn(4 * H, H, device=dev) * 0.05).to(torch.bfloat16)
+zx = torch.randn(T, B, 4 * H, device=dev) * 0.1
+hbuf = torch.zeros(T + 1, B, H, dtype=torch.bfloat16, device=dev)
+cbuf = torch.zeros(T + 1, B, H, device=dev)
+gates = torch.empty(T, B, 4 * H, dtype=torch.bfloat16, device=dev)
+hl = torch.empty(B, H, device=dev)
+cnt = torch.zeros((B // 16 + 1) * (T + 1) * 4, dtype=torch.int32, device=dev)
+err = torch.zeros(1, dtype=torch.int32, device=dev)
+diag = torch.zeros(T, 8, dtype=torch.int64, device=dev)
+for it in range(5):
+    ops.lstm_persist_fwd(WT, zx, None, hbuf, cbuf, gates, hl, cnt, err, 1.0, 1 << 22, None, diag)
+torch.cuda.synchronize()
+ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+ev0.record()
+ops.lstm_persist_fwd(WT, zx, None, hbuf, cbuf, gates, hl, cnt, err, 1.0, 1 << 22, None, diag)
+ev1.record()
+torch.cuda.synchronize()
+d = diag.cpu().numpy().astype("float64")
+ms = ev0.elapsed_time(ev1)
+tot = (d[-1, 0] - d[1, 0]) / (T - 2)
+names = ["top->poll done", "poll->barrierA", "barrierA->mfma done", "mfma->barrierB",
+         "barrierB->epilogue math", "epi->drain done", "drain->next top"]
+import numpy as np
+dd = np.diff(np.concatenate([d[1:-1, [0, 1, 2, 3, 4, 5, 6]], d[2:, [0]]], 1), axis=1)
+print(f"kernel {ms*1e3/T:.2f} us/step (event); stamps {tot:.0f} ticks/step; err={int(err.item())}")
+for n, v in zip(names, dd.mean(0)):
+    print(f"  {n:<26}{v:8.0f} ticks  {100*v/tot:5.1f}%")
