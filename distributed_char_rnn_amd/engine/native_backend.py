@@ -115,6 +115,8 @@ class NativeBackend:
         # forward hand-off form: "granule" (tagged data, R2) or "counter" (sc1 data + counter)
         self.handoff = os.environ.get("DCR_HANDOFF", "counter")
         self.err = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self._side = None
+        self._side_used = False
         self._steps = 0
         self.gen = torch.Generator(device=self.dev)
         self.gen.manual_seed(int(seed))
@@ -198,7 +200,7 @@ class NativeBackend:
             persist=self._persist_ok(B),
             dtop=torch.empty(T, B, H, dtype=f32, device=dev) if training else None,
             dx=torch.empty(T, B, H, dtype=f32, device=dev) if training else None,
-            db_part=(torch.empty(max(B // 16, 1), GW, dtype=f32, device=dev)
+            db_part=(torch.empty(self.L, max(B // 16, 1), GW, dtype=f32, device=dev)
                      if training else None),
             dew_part=(torch.empty(max(B // 16, 1), self.V, GW, dtype=f32, device=dev)
                       if (training and self.V <= 128) else None),
@@ -207,6 +209,11 @@ class NativeBackend:
         )
         self._bufs[key] = bufs
         return bufs
+
+    def _side_stream(self):
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.dev)
+        return self._side
 
     def _persist_ok(self, B: int) -> bool:
         return (self.use_persist and self.cfg.model == "lstm"
@@ -326,7 +333,7 @@ class NativeBackend:
             fused_dew = bufs["persist"] and gather and V <= 128
             if bufs["persist"]:
                 self.ops.lstm_persist_bwd(lw.Wh, dtop, lb.dz, lb.gates, lb.cbuf, bufs["cnt"],
-                                          self.err, self.spin_limit, bufs["db_part"],
+                                          self.err, self.spin_limit, bufs["db_part"][layer],
                                           ids_tm if fused_dew else None,
                                           bufs["dew_part"] if fused_dew else None, V)
             else:
@@ -336,6 +343,26 @@ class NativeBackend:
             dZ = lb.dz.view(N, GW)
             dZx = lb.dzx.view(N, GW) if lb.dzx is not None else dZ
             Hprev = lb.hbuf[:T].reshape(N, H)
+            if bufs["persist"] and layer > 0 and not drop:
+                # Off the critical path: this layer's weight gradients (two [H x N]·[N x 4H]
+                # GEMMs) run on a side stream concurrently with the latency-bound BPTT of the
+                # layer below; the layer's all-reduce bucket is launched from that stream, so
+                # RCCL orders itself after the GEMMs.  Only dX stays on the critical path.
+                dbias = bufs["db_part"][layer].sum(0)
+                ev = torch.cuda.Event()
+                ev.record()
+                side = self._side_stream()
+                with torch.cuda.stream(side):
+                    side.wait_event(ev)
+                    _mm_into(Hprev.t(), dZ, s.gview(names[0])[H:])
+                    _mm_into(lb.x_in.t(), dZx, s.gview(names[0])[:H])
+                    s.gview(names[1]).copy_(dbias)
+                    dbias.record_stream(side)
+                    if on_ready is not None:
+                        on_ready(s.layer_range(layer)[1])
+                dtop = _mm_into(dZx, lw.Wx.t(), bufs["dx"].view(N, H)).view(T, B, H)
+                self._side_used = True
+                continue
             # recurrent-weight gradients
             if self.cfg.model == "gru":
                 gk, gb, ck, cb = names
@@ -357,7 +384,7 @@ class NativeBackend:
             else:
                 dWx = _mm(lb.x_in.t(), dZx)
                 if bufs["persist"]:
-                    dbias = bufs["db_part"].sum(0)           # fused in BPTT
+                    dbias = bufs["db_part"][layer].sum(0)    # fused in BPTT
                 else:
                     self.ops.segsum(dZx, None, 1, bufs["colsum"][:, :GW], bufs["ws"], False)
                     dbias = bufs["colsum"][0, :GW]
@@ -374,6 +401,9 @@ class NativeBackend:
             self._write_input_grads(layer, names, dWx, dbias)
             if on_ready is not None:
                 on_ready(None if layer == 0 else s.layer_range(layer)[1])
+        if self._side_used:
+            torch.cuda.current_stream().wait_stream(self._side)
+            self._side_used = False
         extras = {"logits": logits, "loss": bufs["row_loss"]} if want_extras else None
         self._steps += 1
         if bufs["persist"] and self._steps % 200 == 1:
