@@ -94,6 +94,9 @@ struct PersistArgs {
   const int* bids;       // (unused)
   float* dew_part;       // bwd layer-0 gather mode: [B/16, V, 4H] dEW partials (or nullptr)
   int V;
+  const bf16* Wx;        // fwd fused input projection: W_xᵀ [4H, H] (or nullptr)
+  const bf16* xin;       // fwd fused input: [T, B, H] bf16 layer input
+  const float* bias;     // fwd fused input: [4H] fp32
   uint64_t* ring;        // fwd granule hand-off: [2, B, H/2] tagged granules (nullptr = counters)
   unsigned* cnt;         // [B/16, T+1] arrival counters (zeroed by the launcher)
   unsigned* err;         // timeout / error word (0 = ok)
@@ -104,6 +107,7 @@ struct PersistArgs {
 };
 int lstm_persist_supported(int H, int B, int cus);
 int lstm_persist_grid(int H, int B, int cus);
+int lstm_persist_xfuse_supported(int H, int B, int cus);
 void launch_lstm_fwd_persist(const PersistArgs& a, int cus, hipStream_t s);
 void launch_lstm_bwd_persist(const PersistArgs& a, int cus, hipStream_t s);
 

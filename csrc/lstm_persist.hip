@@ -109,7 +109,10 @@ __device__ __forceinline__ void arrive(unsigned* cnt) {
     if (blockIdx.x == 0 && threadIdx.x == 0)                                        \
       a.diag[(size_t)t * 8 + (i)] = __builtin_amdgcn_s_memtime();                   \
   }
-template <int KS, int UB, bool DIAG = false>  // KS = k-steps (of 32) per wave = H/128
+// XF: the layer's input projection x_t·W_x (+bias) is computed in-kernel from register-resident
+// W_xᵀ fragments while the workgroup waits for h_{t-1} (x_t comes from the layer below, already
+// complete) -- no separate GEMM, no [T,B,4H] fp32 Zx round trip through HBM.
+template <int KS, int UB, bool DIAG = false, bool XF = false>
 __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a) {
   // partials double-buffered by step parity: without a workgroup barrier before the MFMAs a
   // wave may start step t+1 while the epilogue wave still reads step t's partials
@@ -136,6 +139,18 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
         wf[ui][g][s] = ld8(a.W + (size_t)(g * H + ub0 + ui * 16 + (lane & 15)) * H + kbase +
                            s * 32 + kq);
 
+  bf16x8 xw[XF ? UB : 1][4][XF ? KS : 1];
+  if constexpr (XF) {
+#pragma unroll
+    for (int ui = 0; ui < UB; ++ui)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+          xw[ui][g][s] = ld8(a.Wx + (size_t)(g * H + ub0 + ui * 16 + (lane & 15)) * H + kbase +
+                             s * 32 + kq);
+  }
+
   const int b = b0 + (lane & 15);
   const unsigned hoff = (unsigned)(((size_t)b * H + kbase + kq) * sizeof(bf16));
 
@@ -145,12 +160,42 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
   const size_t bh = (size_t)b * H + u0;
   float c[4] = {0.f, 0.f, 0.f, 0.f};
   if (epi) ld4f(a.cbuf + bh, c);
+  float bias[4][4];
+  if constexpr (XF) {
+    if (epi) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) ld4f(a.bias + g * H + u0, bias[g]);
+    }
+  }
 
   for (int t = 0; t < T; ++t) {
     STAMP(0)
     // x-projection pre-activations of step t (independent of the recurrence: issue early)
     float zx[4][4];
-    if (epi) {
+    f32x4 acc[UB][4];
+#pragma unroll
+    for (int ui = 0; ui < UB; ++ui)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[ui][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (XF) {
+      // input projection of step t: independent of the recurrence, runs before the wait
+      const bf16* xp = a.xin + ((size_t)t * B + b) * H + kbase + kq;
+      bf16x8 xf[KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) xf[s] = ld8(xp + s * 32);
+#pragma unroll
+      for (int ui = 0; ui < UB; ++ui)
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) acc[ui][g] = mfma16(xw[ui][g][s], xf[s], acc[ui][g]);
+      if (epi) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) zx[g][r] = bias[g][r];
+      }
+    } else if (epi) {
       const float* zrow = a.ids ? a.zx + (size_t)a.ids[(size_t)t * B + b] * a.zx_ld
                                 : a.zx + ((size_t)t * B + b) * a.zx_ld;
 #pragma unroll
@@ -172,16 +217,14 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
     for (int s = 0; s < KS; ++s) hf[s] = ld8_sc1(hsrc, hoff + s * 64);
 #pragma unroll
     for (int ui = 0; ui < UB; ++ui) {
-      f32x4 acc[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < KS; ++s)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) acc[g] = mfma16(wf[ui][g][s], hf[s], acc[g]);
+        for (int g = 0; g < 4; ++g) acc[ui][g] = mfma16(wf[ui][g][s], hf[s], acc[ui][g]);
       float4* dst = reinterpret_cast<float4*>(&part[t & 1][w][ui][lane][0]);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) dst[g] = make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
+      for (int g = 0; g < 4; ++g)
+        dst[g] = make_float4(acc[ui][g][0], acc[ui][g][1], acc[ui][g][2], acc[ui][g][3]);
     }
     STAMP(3)
     __syncthreads();
@@ -578,8 +621,9 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
 // ------------------------------------------------------------------------------------------
 template <int KS, int UB>
 static void fwd_inst(const PersistArgs& a, int grid, hipStream_t s) {
-  if (a.diag) lstm_fwd_persist_kernel<KS, UB, true><<<grid, 256, 0, s>>>(a);
-  else lstm_fwd_persist_kernel<KS, UB, false><<<grid, 256, 0, s>>>(a);
+  if (a.Wx) lstm_fwd_persist_kernel<KS, UB, false, true><<<grid, 256, 0, s>>>(a);
+  else if (a.diag) lstm_fwd_persist_kernel<KS, UB, true, false><<<grid, 256, 0, s>>>(a);
+  else lstm_fwd_persist_kernel<KS, UB, false, false><<<grid, 256, 0, s>>>(a);
 }
 template <int KS, int UB>
 static void fwd_granule_inst(const PersistArgs& a, int grid, hipStream_t s) {
@@ -591,6 +635,7 @@ static void bwd_inst(const PersistArgs& a, int grid, hipStream_t s) {
   lstm_bwd_persist_kernel<KS, UB><<<grid, 256, lds, s>>>(a);
 }
 
+int lstm_persist_grid(int H, int B, int cus);
 static int ub_for(int H, int B, int cus) {
   // one 16-unit block per workgroup unless that overfills the chip (<= 2 WGs per CU);
   // DCR_PERSIST_UB=1 forces 16-unit workgroups
@@ -611,6 +656,12 @@ int lstm_persist_supported(int H, int B, int cus) {
   if ((H / 16) % ub) return 0;
   const int grid = (H / (16 * ub)) * (B / 16);
   return grid <= 2 * cus ? 1 : 0;
+}
+
+int lstm_persist_xfuse_supported(int H, int B, int cus) {
+  // the fused-input variant holds W_x and W_h in registers: one workgroup per CU at most
+  return lstm_persist_supported(H, B, cus) && lstm_persist_grid(H, B, cus) <= cus &&
+         H <= 512;
 }
 
 int lstm_persist_grid(int H, int B, int cus) {

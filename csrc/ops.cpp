@@ -324,7 +324,8 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
                       at::Tensor& hbuf, at::Tensor& cbuf, const c10::optional<at::Tensor>& gates,
                       at::Tensor& hlast32, at::Tensor& cnt, at::Tensor& err, double forget_bias,
                       int64_t spin_limit, const c10::optional<at::Tensor>& ring,
-                      const c10::optional<at::Tensor>& diag) {
+                      const c10::optional<at::Tensor>& diag, const c10::optional<at::Tensor>& WxT,
+                      const c10::optional<at::Tensor>& xin, const c10::optional<at::Tensor>& bias) {
   check_seq(WT, at::kBFloat16, "WT");
   check_seq(zx, at::kFloat, "zx");
   check_seq(hbuf, at::kBFloat16, "hbuf");
@@ -338,7 +339,16 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
   TORCH_CHECK(dcr::lstm_persist_supported(H, B, num_cus()), "persistent LSTM unsupported for this shape");
   TORCH_CHECK(WT.size(0) == 4 * H && WT.size(1) == H, "WT must be [4H, H]");
   TORCH_CHECK(zx.size(-1) == 4 * H, "zx rows must be 4H wide");
-  if (has(ids)) {
+  const bool xfuse = has(WxT);
+  if (xfuse) {
+    check_seq(*WxT, at::kBFloat16, "WxT");
+    TORCH_CHECK(has(xin) && has(bias), "fused input projection needs xin and bias");
+    check_seq(*xin, at::kBFloat16, "xin");
+    check_seq(*bias, at::kFloat, "bias");
+    TORCH_CHECK(WxT->size(0) == 4 * H && WxT->size(1) == H, "WxT must be [4H, H]");
+    TORCH_CHECK(xin->numel() == (int64_t)T * B * H && bias->numel() == 4 * H, "xin/bias shape");
+    TORCH_CHECK(dcr::lstm_persist_xfuse_supported(H, B, num_cus()), "fused-input persistent LSTM unsupported");
+  } else if (has(ids)) {
     TORCH_CHECK(ids->numel() == (int64_t)T * B, "ids must be [T, B]");
   } else {
     TORCH_CHECK(zx.numel() == (int64_t)T * B * 4 * H, "zx must be [T, B, 4H]");
@@ -363,6 +373,11 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
     TORCH_CHECK(ring->is_cuda() && ring->element_size() == 8 && ring->is_contiguous(), "ring must be a contiguous 8-byte GPU tensor");
     TORCH_CHECK(ring->numel() >= (int64_t)2 * B * (H / 2), "ring must hold [2, B, H/2] granules");
     a.ring = reinterpret_cast<uint64_t*>(ring->data_ptr());
+  }
+  if (xfuse) {
+    a.Wx = optr<bf16>(WxT);
+    a.xin = optr<bf16>(xin);
+    a.bias = optr<float>(bias);
   }
   if (has(diag)) {
     TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)T * 8, "diag must hold [T, 8] int64");
@@ -436,10 +451,14 @@ TORCH_LIBRARY(dcr, m) {
   m.def("xent_num_partials(int n) -> int",
         [](int64_t n) -> int64_t { return dcr::xent_num_partials((int)n); });
   m.def("lstm_persist_supported(int H, int B) -> int", &lstm_persist_supported);
+  m.def("lstm_persist_xfuse_supported(int H, int B) -> int", [](int64_t H, int64_t B) -> int64_t {
+    return dcr::lstm_persist_xfuse_supported((int)H, (int)B, num_cus());
+  });
   m.def(
       "lstm_persist_fwd(Tensor WT, Tensor zx, Tensor? ids, Tensor(a!) hbuf, Tensor(b!) cbuf, "
       "Tensor(c!)? gates, Tensor(d!) hlast32, Tensor(e!) cnt, Tensor(f!) err, float forget_bias, "
-      "int spin_limit, Tensor(g!)? ring, Tensor(h!)? diag=None) -> ()");
+      "int spin_limit, Tensor(g!)? ring, Tensor(h!)? diag=None, Tensor? WxT=None, Tensor? xin=None, "
+      "Tensor? bias=None) -> ()");
   m.def(
       "lstm_persist_bwd(Tensor W, Tensor dtop, Tensor(a!) dz, Tensor gates, Tensor cbuf, "
       "Tensor(b!) cnt, Tensor(c!) err, int spin_limit, Tensor(d!)? db_part, Tensor? ids, "

@@ -71,6 +71,7 @@ class LayerWeights:
     Wh: torch.Tensor            # [H, GWr] bf16 TF layout (backward A operand); GRU: Wc_h
     WhT: torch.Tensor           # [GWr, H] bf16 (forward A operand); GRU: Wg_hᵀ
     W2: Optional[torch.Tensor] = None   # GRU: Wg_h [H, 2H]
+    WxT: Optional[torch.Tensor] = None  # LSTM: W_xᵀ [4H, D] (fused-input persistent forward)
     WT2: Optional[torch.Tensor] = None  # GRU: Wc_hᵀ [H, H]
 
 
@@ -136,8 +137,9 @@ class NativeBackend:
             if self.cfg.model == "lstm" or self.cfg.model == "rnn":
                 k, b = s.view(names[0]), s.view(names[1])
                 Wh = k[D:].to(bf16).contiguous()
-                lw = LayerWeights(Wx=k[:D].to(bf16).contiguous(), Wx32=k[:D], bias=b,
-                                  Wh=Wh, WhT=Wh.t().contiguous())
+                Wx = k[:D].to(bf16).contiguous()
+                lw = LayerWeights(Wx=Wx, Wx32=k[:D], bias=b, Wh=Wh, WhT=Wh.t().contiguous(),
+                                  WxT=Wx.t().contiguous() if layer > 0 else None)
             elif self.cfg.model == "gru":
                 gk, gb, ck, cb = (s.view(n) for n in names)
                 Wx32 = torch.cat([gk[:D], ck[:D]], 1)
@@ -198,6 +200,8 @@ class NativeBackend:
             ws=torch.empty(ws, dtype=f32, device=dev),
             colsum=torch.empty(1, max(GW, self.V), dtype=f32, device=dev),
             persist=self._persist_ok(B),
+            xfuse=(self._persist_ok(B) and os.environ.get("DCR_XFUSE", "1") != "0"
+                   and bool(self.ops.lstm_persist_xfuse_supported(self.H, B))),
             dtop=torch.empty(T, B, H, dtype=f32, device=dev) if training else None,
             dx=torch.empty(T, B, H, dtype=f32, device=dev) if training else None,
             db_part=(torch.empty(self.L, max(B // 16, 1), GW, dtype=f32, device=dev)
@@ -255,6 +259,15 @@ class NativeBackend:
                     lb.h32[0].copy_(st[0])
             gather = (layer == 0 and not drop and self.cfg.model != "nas")
             ids_arg = None
+            xfuse = (bufs["persist"] and layer > 0 and not drop and lw.WxT is not None
+                     and bufs["xfuse"])
+            if xfuse:
+                lb.x_in = x_prev.reshape(N, H)
+                self.ops.lstm_persist_fwd(lw.WhT, lw.bias, None, lb.hbuf, lb.cbuf, lb.gates,
+                                          lb.hlast32, bufs["cnt"], self.err, FORGET_BIAS,
+                                          self.spin_limit, None, None, lw.WxT, x_prev, lw.bias)
+                x_prev = lb.hbuf[1:]
+                continue
             if gather:
                 zx = self._head["table"]
                 ids_arg = ids_tm
