@@ -33,6 +33,9 @@ namespace dcr {
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kAuxSc1 = 16;  // buffer-op cache-policy bits: sc1 (bypass L1, write-through)
+#ifndef XCD_GROUPING
+#define XCD_GROUPING 1
+#endif
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, size_t bytes) {
   const unsigned n = bytes > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (unsigned)bytes;
@@ -93,6 +96,22 @@ __device__ __forceinline__ bool poll_quarters(unsigned* cnt4, unsigned target, u
   }
 }
 
+// Block -> (unit block, batch group).  Speed only: place the unit-block workgroups of one batch
+// group on the same XCD under the observed round-robin dispatch (blocks b, b+8, ... share an
+// XCD; MI355X_MICROARCH.md "Workgroup dispatch"), so the batch group's hand-off payload is
+// fetched into one L2 and served to all its consumers from there.  Correctness never depends
+// on it: every hand-off is sc1 + counters regardless of placement.
+__device__ __forceinline__ void map_block(int bid, int nwg_u, int nbg, int& ubk, int& bg) {
+  if (nbg % 8 == 0 && XCD_GROUPING) {
+    const int xcd = bid % 8, j = bid / 8;  // j in [0, nwg_u * nbg / 8)
+    bg = xcd + 8 * (j / nwg_u);
+    ubk = j % nwg_u;
+  } else {
+    ubk = bid % nwg_u;
+    bg = bid / nwg_u;
+  }
+}
+
 __device__ __forceinline__ void arrive(unsigned* cnt) {
   // every store of this wave must be complete (write-through) before the counter moves
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -121,7 +140,8 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
   const int nwg_u = H / (16 * UB);
-  const int ubk = blockIdx.x % nwg_u, bg = blockIdx.x / nwg_u;
+  int ubk, bg;
+  map_block(blockIdx.x, nwg_u, B / 16, ubk, bg);
   const int ub0 = ubk * 16 * UB, b0 = bg * 16;
   const int kq = 8 * (lane >> 4);
   const int kbase = w * (KS * 32);
@@ -302,7 +322,8 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_granule_kernel(PersistArgs a)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
   const int nwg_u = H / (16 * UB);
-  const int ubk = blockIdx.x % nwg_u, bg = blockIdx.x / nwg_u;
+  int ubk, bg;
+  map_block(blockIdx.x, nwg_u, B / 16, ubk, bg);
   const int ub0 = ubk * 16 * UB, b0 = bg * 16;
   const int kq = 8 * (lane >> 4);
   const int kbase = w * (KS * 32);
@@ -450,7 +471,7 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_granule_kernel(PersistArgs a)
 // ------------------------------------------------------------------------------------------
 // backward (BPTT)
 // ------------------------------------------------------------------------------------------
-template <int KS, int UB>  // KS = k-steps per wave of the K = 4H reduction = H/32
+template <int KS, int UB, bool DIAG = false>  // KS = k-steps per wave of K = 4H = H/32
 __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a) {
   __shared__ __attribute__((aligned(16))) float part[2][4][UB][64][4];  // parity double buffer
   // optional fused dEW accumulator (layer-0 gather mode): [V][UB*64] fp32, dynamic
@@ -459,7 +480,8 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
   const int nwg_u = H / (16 * UB);
-  const int ubk = blockIdx.x % nwg_u, bg = blockIdx.x / nwg_u;
+  int ubk, bg;
+  map_block(blockIdx.x, nwg_u, B / 16, ubk, bg);
   const int ub0 = ubk * 16 * UB, b0 = bg * 16;
   const int kq = 8 * (lane >> 4);
   unsigned* cnt = a.cnt + (size_t)bg * (T + 1) * 4;
@@ -498,6 +520,7 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
   }
 
   for (int t = T - 1; t >= 0; --t) {
+    STAMP(0)
     // recurrence-independent epilogue operands, issued before the wait
     float gi[4], gj[4], gf[4], go[4], cc[4], cp[4], dtop[4];
     if (epi) {
@@ -510,7 +533,9 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
     if (t < T - 1) {
       if (threadIdx.x == 0 && !dead)
         dead = !poll_quarters(cnt + (size_t)(t + 1) * 4, (unsigned)(H / 64), a.spin_limit, a.err, 2u);
+      STAMP(1)
       __syncthreads();
+      STAMP(2)
       const __amdgpu_buffer_rsrc_t dsrc =
           make_rsrc(a.dz + (size_t)(t + 1) * B * G4H, sizeof(bf16) * (size_t)B * G4H);
       bf16x8 df[KS];
@@ -524,7 +549,9 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
         *reinterpret_cast<float4*>(&part[t & 1][w][ui][lane][0]) =
             make_float4(acc[0], acc[1], acc[2], acc[3]);
       }
+      STAMP(3)
       __syncthreads();
+      STAMP(4)
     }
     if (epi) {
       float dh[4];
@@ -552,12 +579,14 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
         dc[r] = dcv * gf[r];
       }
       bf16* dz = a.dz + ((size_t)t * B + b) * G4H + u0;
+      STAMP(5)
       st4bf_sc1(dz, di[0], di[1], di[2], di[3]);
       st4bf_sc1(dz + H, dj[0], dj[1], dj[2], dj[3]);
       st4bf_sc1(dz + 2 * H, df_[0], df_[1], df_[2], df_[3]);
       st4bf_sc1(dz + 3 * H, dO[0], dO[1], dO[2], dO[3]);
       if (t > 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        STAMP(6)
         if (lane == 0)
           __hip_atomic_fetch_add(cnt + (size_t)t * 4 + (u0 / (H / 4)), 1u, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
@@ -632,7 +661,8 @@ static void fwd_granule_inst(const PersistArgs& a, int grid, hipStream_t s) {
 template <int KS, int UB>
 static void bwd_inst(const PersistArgs& a, int grid, hipStream_t s) {
   const size_t lds = a.dew_part ? sizeof(float) * (size_t)a.V * UB * 64 : 0;
-  lstm_bwd_persist_kernel<KS, UB><<<grid, 256, lds, s>>>(a);
+  if (a.diag) lstm_bwd_persist_kernel<KS, UB, true><<<grid, 256, lds, s>>>(a);
+  else lstm_bwd_persist_kernel<KS, UB, false><<<grid, 256, lds, s>>>(a);
 }
 
 int lstm_persist_grid(int H, int B, int cus);

@@ -390,7 +390,8 @@ void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& d
                       const at::Tensor& gates, const at::Tensor& cbuf, at::Tensor& cnt,
                       at::Tensor& err, int64_t spin_limit, const c10::optional<at::Tensor>& db_part,
                       const c10::optional<at::Tensor>& ids,
-                      const c10::optional<at::Tensor>& dew_part, int64_t V) {
+                      const c10::optional<at::Tensor>& dew_part, int64_t V,
+                      const c10::optional<at::Tensor>& diag) {
   check_seq(W, at::kBFloat16, "W");
   check_seq(dtop, at::kFloat, "dtop");
   check_seq(dz, at::kBFloat16, "dz");
@@ -424,6 +425,10 @@ void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& d
     a.dew_part = optr<float>(dew_part);
     a.ids = optr<int>(ids);
     a.V = (int)V;
+  }
+  if (has(diag)) {
+    TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)T * 8, "diag must hold [T, 8] int64");
+    a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());
   }
   dcr::launch_lstm_bwd_persist(a, num_cus(), cur_stream());
 }
@@ -462,7 +467,7 @@ TORCH_LIBRARY(dcr, m) {
   m.def(
       "lstm_persist_bwd(Tensor W, Tensor dtop, Tensor(a!) dz, Tensor gates, Tensor cbuf, "
       "Tensor(b!) cnt, Tensor(c!) err, int spin_limit, Tensor(d!)? db_part, Tensor? ids, "
-      "Tensor(e!)? dew_part, int V) -> ()");
+      "Tensor(e!)? dew_part, int V, Tensor(f!)? diag=None) -> ()");
   m.def("segsum(Tensor X, Tensor? ids, int V, Tensor(a!) out, Tensor(b!) workspace, bool accumulate) -> ()");
   m.def("segsum_workspace(int N, int W, int V) -> int", [](int64_t N, int64_t W, int64_t V) -> int64_t {
     return (int64_t)dcr::segsum_workspace_floats((int)N, (int)W, (int)V);

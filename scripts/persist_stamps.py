@@ -32,3 +32,25 @@ dd = np.diff(np.concatenate([d[1:-1, [0, 1, 2, 3, 4, 5, 6]], d[2:, [0]]], 1), ax
 print(f"kernel {ms*1e3/T:.2f} us/step (event); stamps {tot:.0f} ticks/step; err={int(err.item())}")
 for n, v in zip(names, dd.mean(0)):
     print(f"  {n:<26}{v:8.0f} ticks  {100*v/tot:5.1f}%")
+
+# ---- backward
+W = (torch.randn(H, 4 * H, device=dev) * 0.05).to(torch.bfloat16)
+dtop = torch.randn(T, B, H, device=dev) * 0.01
+dz = torch.empty(T, B, 4 * H, dtype=torch.bfloat16, device=dev)
+dbp = torch.empty(B // 16, 4 * H, device=dev)
+for it in range(3):
+    ops.lstm_persist_bwd(W, dtop, dz, gates, cbuf, cnt, err, 1 << 22, dbp, None, None, 65, diag)
+torch.cuda.synchronize()
+ev0.record()
+ops.lstm_persist_bwd(W, dtop, dz, gates, cbuf, cnt, err, 1 << 22, dbp, None, None, 65, diag)
+ev1.record()
+torch.cuda.synchronize()
+d = diag.cpu().numpy().astype("float64")[::-1]  # reverse time order
+ms = ev0.elapsed_time(ev1)
+tot = (d[-1, 0] - d[1, 0]) / (T - 2)
+dd = np.diff(np.concatenate([d[1:-1, [0, 1, 2, 3, 4, 5, 6]], d[2:, [0]]], 1), axis=1)
+print(f"BWD kernel {ms*1e3/T:.2f} us/step (event); stamps {tot:.0f} ticks/step; err={int(err.item())}")
+names = ["top->poll done", "poll->barrierA", "barrierA->mfma done", "mfma->barrierB",
+         "barrierB->epilogue math", "epi->drain done", "drain->next top"]
+for n, v in zip(names, dd.mean(0)):
+    print(f"  {n:<26}{v:8.0f} ticks  {100*v/tot:5.1f}%")
