@@ -94,7 +94,9 @@ struct PersistArgs {
   const int* bids;       // (unused)
   float* dew_part;       // bwd layer-0 gather mode: [B/16, V, 4H] dEW partials (or nullptr)
   int V;
-  const bf16* Wx;        // fwd fused input projection: W_xᵀ [4H, H] (or nullptr)
+  const bf16* Wx;        // fwd: W_xᵀ [4H, H] fused input projection; bwd: W_x of the layer above
+                         //   [H, 4H] (TF layout) to fuse dtop = dZ_above · W_xᵀ (or nullptr)
+  const bf16* dzx;       // bwd fused dtop: dZ of the layer above [T, B, 4H] bf16
   const bf16* xin;       // fwd fused input: [T, B, H] bf16 layer input
   const float* bias;     // fwd fused input: [4H] fp32
   uint64_t* ring;        // fwd granule hand-off: [2, B, H/2] tagged granules (nullptr = counters)

@@ -471,7 +471,10 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_granule_kernel(PersistArgs a)
 // ------------------------------------------------------------------------------------------
 // backward (BPTT)
 // ------------------------------------------------------------------------------------------
-template <int KS, int UB, bool DIAG = false>  // KS = k-steps per wave of K = 4H = H/32
+// XB: the gradient arriving from the layer above, dtop_t = dZ^{l+1}_t · W_x^{l+1}ᵀ, is computed
+// in-kernel from register-resident W_x^{l+1} rows and the (already complete) dZ of the layer
+// above while the workgroup waits for the dZ_{t+1} hand-off -- no dX GEMM on the critical path.
+template <int KS, int UB, bool DIAG = false, bool XB = false>
 __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a) {
   __shared__ __attribute__((aligned(16))) float part[2][4][UB][64][4];  // parity double buffer
   // optional fused dEW accumulator (layer-0 gather mode): [V][UB*64] fp32, dynamic
@@ -498,6 +501,14 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
 #pragma unroll
     for (int s = 0; s < KS; ++s)
       wf[ui][s] = ld8(a.W + (size_t)(ub0 + ui * 16 + (lane & 15)) * G4H + kcol(s) + kq);
+  bf16x8 xw[XB ? UB : 1][XB ? KS : 1];
+  if constexpr (XB) {
+#pragma unroll
+    for (int ui = 0; ui < UB; ++ui)
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        xw[ui][s] = ld8(a.Wx + (size_t)(ub0 + ui * 16 + (lane & 15)) * G4H + kcol(s) + kq);
+  }
 
   const int b = b0 + (lane & 15);
   const unsigned doff = (unsigned)(((size_t)b * G4H + kq) * sizeof(bf16));
@@ -528,9 +539,24 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
       ld4bf(gp, gi); ld4bf(gp + H, gj); ld4bf(gp + 2 * H, gf); ld4bf(gp + 3 * H, go);
       ld4f(a.cbuf + (size_t)(t + 1) * B * H + bh, cc);
       ld4f(a.cbuf + (size_t)t * B * H + bh, cp);
-      ld4f(a.dtop + (size_t)t * B * H + bh, dtop);
+      if constexpr (!XB) ld4f(a.dtop + (size_t)t * B * H + bh, dtop);
     }
-    if (t < T - 1) {
+    // per-wave partial sums over this wave's K quarter: [x-part (XB)] + recurrent part
+    f32x4 pacc[UB];
+#pragma unroll
+    for (int ui = 0; ui < UB; ++ui) pacc[ui] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (XB) {
+      const bf16* zp = a.dzx + ((size_t)t * B + b) * G4H + kq;
+      bf16x8 zf[KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) zf[s] = ld8(zp + kcol(s));
+#pragma unroll
+      for (int ui = 0; ui < UB; ++ui)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) pacc[ui] = mfma16(xw[ui][s], zf[s], pacc[ui]);
+    }
+    if (t < T - 1 || XB) {
+     if (t < T - 1) {
       if (threadIdx.x == 0 && !dead)
         dead = !poll_quarters(cnt + (size_t)(t + 1) * 4, (unsigned)(H / 64), a.spin_limit, a.err, 2u);
       STAMP(1)
@@ -542,20 +568,25 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
 #pragma unroll
       for (int s = 0; s < KS; ++s) df[s] = ld8_sc1(dsrc, doff + kcol(s) * 2);
 #pragma unroll
-      for (int ui = 0; ui < UB; ++ui) {
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int ui = 0; ui < UB; ++ui)
 #pragma unroll
-        for (int s = 0; s < KS; ++s) acc = mfma16(wf[ui][s], df[s], acc);
+        for (int s = 0; s < KS; ++s) pacc[ui] = mfma16(wf[ui][s], df[s], pacc[ui]);
+     }
+#pragma unroll
+      for (int ui = 0; ui < UB; ++ui)
         *reinterpret_cast<float4*>(&part[t & 1][w][ui][lane][0]) =
-            make_float4(acc[0], acc[1], acc[2], acc[3]);
-      }
+            make_float4(pacc[ui][0], pacc[ui][1], pacc[ui][2], pacc[ui][3]);
       STAMP(3)
       __syncthreads();
       STAMP(4)
     }
     if (epi) {
       float dh[4];
-      if (t < T - 1) {
+      if constexpr (XB) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dtop[r] = 0.f;
+      }
+      if (t < T - 1 || XB) {
         const float4 s0 = *reinterpret_cast<const float4*>(&part[t & 1][0][w][lane][0]);
         const float4 s1 = *reinterpret_cast<const float4*>(&part[t & 1][1][w][lane][0]);
         const float4 s2 = *reinterpret_cast<const float4*>(&part[t & 1][2][w][lane][0]);
@@ -661,8 +692,9 @@ static void fwd_granule_inst(const PersistArgs& a, int grid, hipStream_t s) {
 template <int KS, int UB>
 static void bwd_inst(const PersistArgs& a, int grid, hipStream_t s) {
   const size_t lds = a.dew_part ? sizeof(float) * (size_t)a.V * UB * 64 : 0;
-  if (a.diag) lstm_bwd_persist_kernel<KS, UB, true><<<grid, 256, lds, s>>>(a);
-  else lstm_bwd_persist_kernel<KS, UB, false><<<grid, 256, lds, s>>>(a);
+  if (a.Wx) lstm_bwd_persist_kernel<KS, UB, false, true><<<grid, 256, lds, s>>>(a);
+  else if (a.diag) lstm_bwd_persist_kernel<KS, UB, true, false><<<grid, 256, lds, s>>>(a);
+  else lstm_bwd_persist_kernel<KS, UB, false, false><<<grid, 256, lds, s>>>(a);
 }
 
 int lstm_persist_grid(int H, int B, int cus);

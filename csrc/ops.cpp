@@ -391,7 +391,8 @@ void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& d
                       at::Tensor& err, int64_t spin_limit, const c10::optional<at::Tensor>& db_part,
                       const c10::optional<at::Tensor>& ids,
                       const c10::optional<at::Tensor>& dew_part, int64_t V,
-                      const c10::optional<at::Tensor>& diag) {
+                      const c10::optional<at::Tensor>& diag, const c10::optional<at::Tensor>& Wx_above,
+                      const c10::optional<at::Tensor>& dz_above) {
   check_seq(W, at::kBFloat16, "W");
   check_seq(dtop, at::kFloat, "dtop");
   check_seq(dz, at::kBFloat16, "dz");
@@ -430,6 +431,16 @@ void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& d
     TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)T * 8, "diag must hold [T, 8] int64");
     a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());
   }
+  if (has(Wx_above)) {
+    check_seq(*Wx_above, at::kBFloat16, "Wx_above");
+    TORCH_CHECK(has(dz_above), "dz_above required with Wx_above");
+    check_seq(*dz_above, at::kBFloat16, "dz_above");
+    TORCH_CHECK(Wx_above->size(0) == H && Wx_above->size(1) == 4 * H, "Wx_above must be [H, 4H]");
+    TORCH_CHECK(dz_above->numel() == (int64_t)T * B * 4 * H, "dz_above must be [T, B, 4H]");
+    TORCH_CHECK(dcr::lstm_persist_xfuse_supported(H, B, num_cus()), "fused-dtop persistent BPTT unsupported");
+    a.Wx = optr<bf16>(Wx_above);
+    a.dzx = optr<bf16>(dz_above);
+  }
   dcr::launch_lstm_bwd_persist(a, num_cus(), cur_stream());
 }
 
@@ -467,7 +478,8 @@ TORCH_LIBRARY(dcr, m) {
   m.def(
       "lstm_persist_bwd(Tensor W, Tensor dtop, Tensor(a!) dz, Tensor gates, Tensor cbuf, "
       "Tensor(b!) cnt, Tensor(c!) err, int spin_limit, Tensor(d!)? db_part, Tensor? ids, "
-      "Tensor(e!)? dew_part, int V, Tensor(f!)? diag=None) -> ()");
+      "Tensor(e!)? dew_part, int V, Tensor(f!)? diag=None, Tensor? Wx_above=None, "
+      "Tensor? dz_above=None) -> ()");
   m.def("segsum(Tensor X, Tensor? ids, int V, Tensor(a!) out, Tensor(b!) workspace, bool accumulate) -> ()");
   m.def("segsum_workspace(int N, int W, int V) -> int", [](int64_t N, int64_t W, int64_t V) -> int64_t {
     return (int64_t)dcr::segsum_workspace_floats((int)N, (int)W, (int)V);

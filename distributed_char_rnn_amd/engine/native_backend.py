@@ -115,6 +115,9 @@ class NativeBackend:
         self.spin_limit = int(os.environ.get("DCR_SPIN_LIMIT", str(1 << 22)))
         # forward hand-off form: "granule" (tagged data, R2) or "counter" (sc1 data + counter)
         self.handoff = os.environ.get("DCR_HANDOFF", "counter")
+        # fused dtop (dZ_above·W_xᵀ inside the lower layer's BPTT): measured slower (4.22 vs
+        # 3.47 ms/step: its extra dZ loads sit on the load-bound critical path), opt-in only
+        self.fused_dtop = os.environ.get("DCR_FUSED_DTOP", "0") == "1"
         self.err = torch.zeros(1, dtype=torch.int32, device=self.dev)
         self._side = None
         self._side_used = False
@@ -219,6 +222,15 @@ class NativeBackend:
             self._side = torch.cuda.Stream(device=self.dev)
         return self._side
 
+    def _exclusive_ok(self, bufs) -> bool:
+        """One-workgroup-per-CU persistent variants need the whole GPU to themselves: only when
+        no collective (RCCL) or side-stream kernel can run beside them."""
+        if not bufs["xfuse"] or os.environ.get("DCR_EXCLUSIVE", "1") == "0":
+            return False
+        import torch.distributed as dist
+
+        return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+
     def _persist_ok(self, B: int) -> bool:
         return (self.use_persist and self.cfg.model == "lstm"
                 and bool(self.ops.lstm_persist_supported(self.H, B)))
@@ -259,6 +271,8 @@ class NativeBackend:
                     lb.h32[0].copy_(st[0])
             gather = (layer == 0 and not drop and self.cfg.model != "nas")
             ids_arg = None
+            # the forward never has a concurrent kernel (the previous step's all-reduce is joined
+            # before the optimizer), so the one-workgroup-per-CU fused variant is safe here
             xfuse = (bufs["persist"] and layer > 0 and not drop and lw.WxT is not None
                      and bufs["xfuse"])
             if xfuse:
@@ -335,20 +349,28 @@ class NativeBackend:
             on_ready(sb.offset + sb.numel)
         drop = self._dropout(True)
         c = self.cfg
+        deferred = []
         for layer in reversed(range(self.L)):
             lw, lb = self._w[layer], bufs["layers"][layer]
             names = [sp.name for sp in cell_specs(self.cfg, layer)]
-            if "out" in lb.masks:
-                dtop = dtop * lb.masks["out"]
-            dtop = dtop.contiguous()
+            if dtop is not None:
+                if "out" in lb.masks:
+                    dtop = dtop * lb.masks["out"]
+                dtop = dtop.contiguous()
             zx_nas = lb.zx if self.cfg.model == "nas" else None
             gather = (layer == 0 and not drop and self.cfg.model != "nas")
             fused_dew = bufs["persist"] and gather and V <= 128
             if bufs["persist"]:
-                self.ops.lstm_persist_bwd(lw.Wh, dtop, lb.dz, lb.gates, lb.cbuf, bufs["cnt"],
+                above = None
+                if dtop is None:  # dtop of this layer is fused: dZ_above · W_x,aboveᵀ in-kernel
+                    above = (self._w[layer + 1].Wx, bufs["layers"][layer + 1].dz)
+                self.ops.lstm_persist_bwd(lw.Wh, dtop if dtop is not None else bufs["dtop"],
+                                          lb.dz, lb.gates, lb.cbuf, bufs["cnt"],
                                           self.err, self.spin_limit, bufs["db_part"][layer],
                                           ids_tm if fused_dew else None,
-                                          bufs["dew_part"] if fused_dew else None, V)
+                                          bufs["dew_part"] if fused_dew else None, V, None,
+                                          above[0] if above else None,
+                                          above[1] if above else None)
             else:
                 self.ops.rnn_bwd_seq(self.cell, lw.Wh, lw.W2, dtop, lb.dz, lb.dzx, lb.gates,
                                      lb.pre, lb.aux, zx_nas, lb.cbuf, lb.h32, lb.hbuf, bufs["dc"],
@@ -356,6 +378,24 @@ class NativeBackend:
             dZ = lb.dz.view(N, GW)
             dZx = lb.dzx.view(N, GW) if lb.dzx is not None else dZ
             Hprev = lb.hbuf[:T].reshape(N, H)
+            if (bufs["persist"] and layer > 0 and not drop and self.fused_dtop
+                    and self._exclusive_ok(bufs)):
+                # The layer below fuses dtop = dZ·W_xᵀ into its BPTT kernel.  That kernel holds
+                # W_h and W_x^{above} in registers (one workgroup per CU, grid = all CUs), so
+                # NOTHING may run beside it (a concurrent kernel holding CUs could deadlock the
+                # grid's residency): this layer's weight gradients are deferred until after it.
+                dbias = bufs["db_part"][layer].sum(0)
+
+                def _wgrads(names=names, Hprev=Hprev, dZ=dZ, dZx=dZx, lb=lb, dbias=dbias,
+                            layer=layer):
+                    _mm_into(Hprev.t(), dZ, s.gview(names[0])[H:])
+                    _mm_into(lb.x_in.t(), dZx, s.gview(names[0])[:H])
+                    s.gview(names[1]).copy_(dbias)
+                    if on_ready is not None:
+                        on_ready(s.layer_range(layer)[1])
+                deferred.append(_wgrads)
+                dtop = None
+                continue
             if bufs["persist"] and layer > 0 and not drop:
                 # Off the critical path: this layer's weight gradients (two [H x N]·[N x 4H]
                 # GEMMs) run on a side stream concurrently with the latency-bound BPTT of the
@@ -376,6 +416,9 @@ class NativeBackend:
                 dtop = _mm_into(dZx, lw.Wx.t(), bufs["dx"].view(N, H)).view(T, B, H)
                 self._side_used = True
                 continue
+            for fn in deferred:  # weight grads of the layers above (after the fused BPTT)
+                fn()
+            deferred.clear()
             # recurrent-weight gradients
             if self.cfg.model == "gru":
                 gk, gb, ck, cb = names
