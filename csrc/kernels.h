@@ -106,11 +106,16 @@ struct PersistArgs {
   int B, H, T;
   float forget_bias;
   unsigned spin_limit;
+  int excl;              // bwd: all-loads-in-flight variant (one WG per CU: nothing may run beside it)
 };
 int lstm_persist_supported(int H, int B, int cus);
 int lstm_persist_grid(int H, int B, int cus);
 int lstm_persist_xfuse_supported(int H, int B, int cus);
-void launch_lstm_fwd_persist(const PersistArgs& a, int cus, hipStream_t s);
-void launch_lstm_bwd_persist(const PersistArgs& a, int cus, hipStream_t s);
+// max co-resident workgroups per CU of the instantiation a launch with these flags would use
+// (flags: 1 fused input/dtop, 2 diag stamps, 4 exclusive bwd, 8 granule fwd; V>0: fused dEW LDS)
+int lstm_persist_occupancy(int bwd, int H, int B, int V, int flags, int cus);
+// return 0 on success, <0 if the grid cannot be co-resident or the shape is unsupported
+int launch_lstm_fwd_persist(const PersistArgs& a, int cus, hipStream_t s);
+int launch_lstm_bwd_persist(const PersistArgs& a, int cus, hipStream_t s);
 
 }  // namespace dcr

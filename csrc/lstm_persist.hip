@@ -235,6 +235,7 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
     bf16x8 hf[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s) hf[s] = ld8_sc1(hsrc, hoff + s * 64);
+    __builtin_amdgcn_sched_barrier(0);  // keep all KS hand-off loads in flight together
 #pragma unroll
     for (int ui = 0; ui < UB; ++ui) {
 #pragma unroll
@@ -275,6 +276,16 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
       const size_t o = (size_t)(t + 1) * B * H + bh;
       STAMP(5)
       st4bf_sc1(a.hbuf + o, h[0], h[1], h[2], h[3]);  // handed off: write-through
+      if (t + 1 < T) {
+        // each epilogue wave publishes its own 16-unit slab: drain ONLY the hand-off store
+        // (the activation-cache stores below are issued after the arrival, so the wait does
+        // not cover them), then one lane arrives on the counter of its K-quarter
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        STAMP(6)
+        if (lane == 0)
+          __hip_atomic_fetch_add(cnt + (size_t)(t + 1) * 4 + (u0 / (H / 4)), 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+      }
       *reinterpret_cast<float4*>(a.cbuf + o) = make_float4(c[0], c[1], c[2], c[3]);
       if (a.gates) {
         bf16* gp = a.gates + ((size_t)t * B + b) * 4 * H + u0;
@@ -285,15 +296,6 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
       }
       if (t == T - 1 && a.hlast32)
         *reinterpret_cast<float4*>(a.hlast32 + bh) = make_float4(h[0], h[1], h[2], h[3]);
-      if (t + 1 < T) {
-        // each epilogue wave publishes its own 16-unit slab: drain its write-through stores,
-        // then one lane arrives on the counter of the K-quarter its units belong to
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        STAMP(6)
-        if (lane == 0)
-          __hip_atomic_fetch_add(cnt + (size_t)(t + 1) * 4 + (u0 / (H / 4)), 1u, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-      }
     }
   }
 }
@@ -474,7 +476,12 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_granule_kernel(PersistArgs a)
 // XB: the gradient arriving from the layer above, dtop_t = dZ^{l+1}_t · W_x^{l+1}ᵀ, is computed
 // in-kernel from register-resident W_x^{l+1} rows and the (already complete) dZ of the layer
 // above while the workgroup waits for the dZ_{t+1} hand-off -- no dX GEMM on the critical path.
-template <int KS, int UB, bool DIAG = false, bool XB = false>
+//
+// EXCL: all KS payload loads of a step are forced in flight together (sched_barrier); the extra
+// 4*KS live VGPRs push KS=16/UB=2 past 256 registers, i.e. one workgroup per CU, so this variant
+// is only launched when nothing can run beside it (see lstm_persist_occupancy and the backend's
+// exclusive mode).  Measured at H=512, B=256: 4.32 vs 5.0 us per BPTT step.
+template <int KS, int UB, bool DIAG = false, bool XB = false, bool EXCL = false>
 __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a) {
   __shared__ __attribute__((aligned(16))) float part[2][4][UB][64][4];  // parity double buffer
   // optional fused dEW accumulator (layer-0 gather mode): [V][UB*64] fp32, dynamic
@@ -567,6 +574,7 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
       bf16x8 df[KS];
 #pragma unroll
       for (int s = 0; s < KS; ++s) df[s] = ld8_sc1(dsrc, doff + kcol(s) * 2);
+      if constexpr (EXCL) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int ui = 0; ui < UB; ++ui)
 #pragma unroll
@@ -609,8 +617,8 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
         df_[r] = dcv * cp[r] * gf[r] * (1.f - gf[r]);
         dc[r] = dcv * gf[r];
       }
-      bf16* dz = a.dz + ((size_t)t * B + b) * G4H + u0;
       STAMP(5)
+      bf16* dz = a.dz + ((size_t)t * B + b) * G4H + u0;
       st4bf_sc1(dz, di[0], di[1], di[2], di[3]);
       st4bf_sc1(dz + H, dj[0], dj[1], dj[2], dj[3]);
       st4bf_sc1(dz + 2 * H, df_[0], df_[1], df_[2], df_[3]);
@@ -679,87 +687,118 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
+// Kernel selection returns the exact instantiation so that launch and residency query agree.
+enum : int { PF_FUSED = 1, PF_DIAG = 2, PF_EXCL = 4, PF_GRANULE = 8 };
+
 template <int KS, int UB>
-static void fwd_inst(const PersistArgs& a, int grid, hipStream_t s) {
-  if (a.Wx) lstm_fwd_persist_kernel<KS, UB, false, true><<<grid, 256, 0, s>>>(a);
-  else if (a.diag) lstm_fwd_persist_kernel<KS, UB, true, false><<<grid, 256, 0, s>>>(a);
-  else lstm_fwd_persist_kernel<KS, UB, false, false><<<grid, 256, 0, s>>>(a);
+static const void* fwd_fn(int flags) {
+  if (flags & PF_GRANULE) return (const void*)lstm_fwd_granule_kernel<KS, UB>;
+  if (flags & PF_FUSED) return (const void*)lstm_fwd_persist_kernel<KS, UB, false, true>;
+  if (flags & PF_DIAG) return (const void*)lstm_fwd_persist_kernel<KS, UB, true, false>;
+  return (const void*)lstm_fwd_persist_kernel<KS, UB, false, false>;
 }
 template <int KS, int UB>
-static void fwd_granule_inst(const PersistArgs& a, int grid, hipStream_t s) {
-  lstm_fwd_granule_kernel<KS, UB><<<grid, 256, 0, s>>>(a);
-}
-template <int KS, int UB>
-static void bwd_inst(const PersistArgs& a, int grid, hipStream_t s) {
-  const size_t lds = a.dew_part ? sizeof(float) * (size_t)a.V * UB * 64 : 0;
-  if (a.Wx) lstm_bwd_persist_kernel<KS, UB, false, true><<<grid, 256, lds, s>>>(a);
-  else if (a.diag) lstm_bwd_persist_kernel<KS, UB, true, false><<<grid, 256, lds, s>>>(a);
-  else lstm_bwd_persist_kernel<KS, UB, false, false><<<grid, 256, lds, s>>>(a);
+static const void* bwd_fn(int flags) {
+  if (flags & PF_FUSED) return (const void*)lstm_bwd_persist_kernel<KS, UB, false, true>;
+  const bool d = flags & PF_DIAG, e = flags & PF_EXCL;
+  if (d && e) return (const void*)lstm_bwd_persist_kernel<KS, UB, true, false, true>;
+  if (d) return (const void*)lstm_bwd_persist_kernel<KS, UB, true, false, false>;
+  if (e) return (const void*)lstm_bwd_persist_kernel<KS, UB, false, false, true>;
+  return (const void*)lstm_bwd_persist_kernel<KS, UB, false, false, false>;
 }
 
-int lstm_persist_grid(int H, int B, int cus);
 static int ub_for(int H, int B, int cus) {
-  // one 16-unit block per workgroup unless that overfills the chip (<= 2 WGs per CU);
-  // DCR_PERSIST_UB=1 forces 16-unit workgroups
+  // DCR_PERSIST_UB=1 forces 16-unit workgroups; default: 32-unit workgroups (measured 3.84 vs
+  // 4.02 ms/step at B=256, H=512: half the pollers, half the backward hand-off traffic);
+  // 16-unit ones only when H/16 is odd
+  (void)B; (void)cus;
   static int forced = -1;
   if (forced < 0) {
     const char* e = getenv("DCR_PERSIST_UB");
     forced = (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
   }
   if (forced == 1) return 1;
-  // default: 32-unit workgroups (measured 3.84 vs 4.02 ms/step at B=256, H=512: half the
-  // pollers, half the backward hand-off traffic); 16-unit ones only when H/16 is odd
   return ((H / 16) % 2 == 0) ? 2 : 1;
 }
 
-int lstm_persist_supported(int H, int B, int cus) {
-  if (H % 128 != 0 || B % 16 != 0 || H > 1024 || H < 128) return 0;
+static const void* pick(int bwd, int H, int B, int flags, int cus) {
   const int ub = ub_for(H, B, cus);
-  if ((H / 16) % ub) return 0;
-  const int grid = (H / (16 * ub)) * (B / 16);
-  return grid <= 2 * cus ? 1 : 0;
+  if (!bwd) {
+    const int ks = H / 128;
+#define FWD(K, U) \
+  if (ks == K && ub == U) return fwd_fn<K, U>(flags);
+    FWD(1, 1) FWD(2, 1) FWD(3, 1) FWD(4, 1) FWD(6, 1) FWD(8, 1)
+    FWD(1, 2) FWD(2, 2) FWD(3, 2) FWD(4, 2) FWD(6, 2) FWD(8, 2)
+#undef FWD
+  } else {
+    const int ks = H / 32;
+#define BWD(K, U) \
+  if (ks == K && ub == U) return bwd_fn<K, U>(flags);
+    BWD(4, 1) BWD(8, 1) BWD(12, 1) BWD(16, 1) BWD(24, 1) BWD(32, 1)
+    BWD(4, 2) BWD(8, 2) BWD(12, 2) BWD(16, 2) BWD(24, 2) BWD(32, 2)
+#undef BWD
+  }
+  return nullptr;
 }
 
-int lstm_persist_xfuse_supported(int H, int B, int cus) {
-  // the fused-input variant holds W_x and W_h in registers: one workgroup per CU at most
-  return lstm_persist_supported(H, B, cus) && lstm_persist_grid(H, B, cus) <= cus &&
-         H <= 512;
+static size_t dyn_lds(int bwd, int H, int B, int V, int cus) {
+  return (bwd && V > 0) ? sizeof(float) * (size_t)V * ub_for(H, B, cus) * 64 : 0;
+}
+
+int lstm_persist_supported(int H, int B, int cus) {
+  // shape support only; whether a grid can be co-resident is lstm_persist_occupancy's job
+  (void)cus;
+  if (H % 128 != 0 || B % 16 != 0 || H > 1024 || H < 128) return 0;
+  return (H / 16) % ub_for(H, B, cus) == 0 ? 1 : 0;
 }
 
 int lstm_persist_grid(int H, int B, int cus) {
   return (H / (16 * ub_for(H, B, cus))) * (B / 16);
 }
 
-void launch_lstm_fwd_persist(const PersistArgs& a, int cus, hipStream_t s) {
-  const int ub = ub_for(a.H, a.B, cus);
-  const int grid = (a.H / (16 * ub)) * (a.B / 16);
-  (void)hipMemsetAsync(a.cnt, 0, sizeof(unsigned) * (size_t)(a.B / 16) * (a.T + 1) * 4, s);
-  const int ks = a.H / 128;
-  if (a.ring) {
-    (void)hipMemsetAsync(a.ring, 0, sizeof(uint64_t) * 2 * (size_t)a.B * (a.H / 2), s);
-#define FWDG(K, U) \
-  if (ks == K && ub == U) { fwd_granule_inst<K, U>(a, grid, s); return; }
-    FWDG(1, 1) FWDG(2, 1) FWDG(3, 1) FWDG(4, 1) FWDG(6, 1) FWDG(8, 1)
-    FWDG(1, 2) FWDG(2, 2) FWDG(3, 2) FWDG(4, 2) FWDG(6, 2) FWDG(8, 2)
-#undef FWDG
-  }
-#define FWD(K, U) \
-  if (ks == K && ub == U) { fwd_inst<K, U>(a, grid, s); return; }
-  FWD(1, 1) FWD(2, 1) FWD(3, 1) FWD(4, 1) FWD(6, 1) FWD(8, 1)
-  FWD(1, 2) FWD(2, 2) FWD(3, 2) FWD(4, 2) FWD(6, 2) FWD(8, 2)
-#undef FWD
+int lstm_persist_occupancy(int bwd, int H, int B, int V, int flags, int cus) {
+  if (!lstm_persist_supported(H, B, cus)) return 0;
+  const void* fn = pick(bwd, H, B, flags, cus);
+  if (!fn) return 0;
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 256, dyn_lds(bwd, H, B, V, cus)) !=
+      hipSuccess)
+    return 0;
+  return n;
 }
 
-void launch_lstm_bwd_persist(const PersistArgs& a, int cus, hipStream_t s) {
-  const int ub = ub_for(a.H, a.B, cus);
-  const int grid = (a.H / (16 * ub)) * (a.B / 16);
+int lstm_persist_xfuse_supported(int H, int B, int cus) {
+  // the fused-input variant holds W_x and W_h in registers: the whole grid must still be
+  // co-resident with the GPU to itself
+  return H <= 512 && lstm_persist_grid(H, B, cus) <=
+                         lstm_persist_occupancy(0, H, B, 0, PF_FUSED, cus) * cus;
+}
+
+// Every workgroup of a persistent grid spins on its neighbours, so the whole grid must be
+// resident at once: refuse (rather than hang or time out) a grid the CUs cannot hold.
+static int launch_persist(int bwd, const PersistArgs& a, int flags, int cus, hipStream_t s) {
+  const int grid = lstm_persist_grid(a.H, a.B, cus);
+  const void* fn = pick(bwd, a.H, a.B, flags, cus);
+  if (!fn) return -1;
+  const size_t lds = dyn_lds(bwd, a.H, a.B, a.dew_part ? a.V : 0, cus);
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 256, lds) != hipSuccess ||
+      grid > occ * cus)
+    return -2;
   (void)hipMemsetAsync(a.cnt, 0, sizeof(unsigned) * (size_t)(a.B / 16) * (a.T + 1) * 4, s);
-  const int ks = a.H / 32;
-#define BWD(K, U) \
-  if (ks == K && ub == U) { bwd_inst<K, U>(a, grid, s); return; }
-  BWD(4, 1) BWD(8, 1) BWD(12, 1) BWD(16, 1) BWD(24, 1) BWD(32, 1)
-  BWD(4, 2) BWD(8, 2) BWD(12, 2) BWD(16, 2) BWD(24, 2) BWD(32, 2)
-#undef BWD
+  if (a.ring) (void)hipMemsetAsync(a.ring, 0, sizeof(uint64_t) * 2 * (size_t)a.B * (a.H / 2), s);
+  void* args[] = {const_cast<PersistArgs*>(&a)};
+  return hipLaunchKernel(fn, dim3(grid), dim3(256), args, lds, s) == hipSuccess ? 0 : -3;
+}
+
+int launch_lstm_fwd_persist(const PersistArgs& a, int cus, hipStream_t s) {
+  const int flags = (a.ring ? PF_GRANULE : 0) | (a.Wx ? PF_FUSED : 0) | (a.diag ? PF_DIAG : 0);
+  return launch_persist(0, a, flags, cus, s);
+}
+
+int launch_lstm_bwd_persist(const PersistArgs& a, int cus, hipStream_t s) {
+  const int flags = (a.Wx ? PF_FUSED : 0) | (a.diag ? PF_DIAG : 0) | (a.excl ? PF_EXCL : 0);
+  return launch_persist(1, a, flags, cus, s);
 }
 
 }  // namespace dcr

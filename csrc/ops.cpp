@@ -383,7 +383,9 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
     TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)T * 8, "diag must hold [T, 8] int64");
     a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());
   }
-  dcr::launch_lstm_fwd_persist(a, num_cus(), cur_stream());
+  const int rc = dcr::launch_lstm_fwd_persist(a, num_cus(), cur_stream());
+  TORCH_CHECK(rc == 0, "persistent LSTM forward not launched (", rc,
+              "): grid cannot be co-resident on this GPU for H=", H, " B=", B);
 }
 
 void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& dz,
@@ -392,7 +394,7 @@ void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& d
                       const c10::optional<at::Tensor>& ids,
                       const c10::optional<at::Tensor>& dew_part, int64_t V,
                       const c10::optional<at::Tensor>& diag, const c10::optional<at::Tensor>& Wx_above,
-                      const c10::optional<at::Tensor>& dz_above) {
+                      const c10::optional<at::Tensor>& dz_above, bool exclusive) {
   check_seq(W, at::kBFloat16, "W");
   check_seq(dtop, at::kFloat, "dtop");
   check_seq(dz, at::kBFloat16, "dz");
@@ -441,7 +443,10 @@ void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& d
     a.Wx = optr<bf16>(Wx_above);
     a.dzx = optr<bf16>(dz_above);
   }
-  dcr::launch_lstm_bwd_persist(a, num_cus(), cur_stream());
+  a.excl = exclusive ? 1 : 0;
+  const int rc = dcr::launch_lstm_bwd_persist(a, num_cus(), cur_stream());
+  TORCH_CHECK(rc == 0, "persistent LSTM BPTT not launched (", rc,
+              "): grid cannot be co-resident on this GPU for H=", H, " B=", B);
 }
 
 }  // namespace
@@ -467,6 +472,14 @@ TORCH_LIBRARY(dcr, m) {
   m.def("xent_num_partials(int n) -> int",
         [](int64_t n) -> int64_t { return dcr::xent_num_partials((int)n); });
   m.def("lstm_persist_supported(int H, int B) -> int", &lstm_persist_supported);
+  m.def("num_cus() -> int", []() -> int64_t { return num_cus(); });
+  m.def("lstm_persist_grid(int H, int B) -> int", [](int64_t H, int64_t B) -> int64_t {
+    return dcr::lstm_persist_grid((int)H, (int)B, num_cus());
+  });
+  m.def("lstm_persist_occupancy(int bwd, int H, int B, int V, int flags) -> int",
+        [](int64_t bwd, int64_t H, int64_t B, int64_t V, int64_t flags) -> int64_t {
+          return dcr::lstm_persist_occupancy((int)bwd, (int)H, (int)B, (int)V, (int)flags, num_cus());
+        });
   m.def("lstm_persist_xfuse_supported(int H, int B) -> int", [](int64_t H, int64_t B) -> int64_t {
     return dcr::lstm_persist_xfuse_supported((int)H, (int)B, num_cus());
   });
@@ -479,7 +492,7 @@ TORCH_LIBRARY(dcr, m) {
       "lstm_persist_bwd(Tensor W, Tensor dtop, Tensor(a!) dz, Tensor gates, Tensor cbuf, "
       "Tensor(b!) cnt, Tensor(c!) err, int spin_limit, Tensor(d!)? db_part, Tensor? ids, "
       "Tensor(e!)? dew_part, int V, Tensor(f!)? diag=None, Tensor? Wx_above=None, "
-      "Tensor? dz_above=None) -> ()");
+      "Tensor? dz_above=None, bool exclusive=False) -> ()");
   m.def("segsum(Tensor X, Tensor? ids, int V, Tensor(a!) out, Tensor(b!) workspace, bool accumulate) -> ()");
   m.def("segsum_workspace(int N, int W, int V) -> int", [](int64_t N, int64_t W, int64_t V) -> int64_t {
     return (int64_t)dcr::segsum_workspace_floats((int)N, (int)W, (int)V);

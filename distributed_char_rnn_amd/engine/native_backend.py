@@ -33,6 +33,8 @@ from ..ops import native
 
 CELL_ID = {"lstm": 0, "gru": 1, "rnn": 3, "nas": 4}
 FORGET_BIAS = 1.0
+# lstm_persist_occupancy flags (csrc/lstm_persist.hip PF_*)
+PF_FUSED, PF_DIAG, PF_EXCL, PF_GRANULE = 1, 2, 4, 8
 bf16 = torch.bfloat16
 f32 = torch.float32
 
@@ -118,6 +120,7 @@ class NativeBackend:
         # fused dtop (dZ_above·W_xᵀ inside the lower layer's BPTT): measured slower (4.22 vs
         # 3.47 ms/step: its extra dZ loads sit on the load-bound critical path), opt-in only
         self.fused_dtop = os.environ.get("DCR_FUSED_DTOP", "0") == "1"
+        self.side_overlap = os.environ.get("DCR_SIDE", "1") == "1"
         self.err = torch.zeros(1, dtype=torch.int32, device=self.dev)
         self._side = None
         self._side_used = False
@@ -202,9 +205,7 @@ class NativeBackend:
             gpart=torch.empty(B, H, dtype=f32, device=dev) if m == "gru" else None,
             ws=torch.empty(ws, dtype=f32, device=dev),
             colsum=torch.empty(1, max(GW, self.V), dtype=f32, device=dev),
-            persist=self._persist_ok(B),
-            xfuse=(self._persist_ok(B) and os.environ.get("DCR_XFUSE", "1") != "0"
-                   and bool(self.ops.lstm_persist_xfuse_supported(self.H, B))),
+            **self._persist_plan(B, training),
             dtop=torch.empty(T, B, H, dtype=f32, device=dev) if training else None,
             dx=torch.empty(T, B, H, dtype=f32, device=dev) if training else None,
             db_part=(torch.empty(self.L, max(B // 16, 1), GW, dtype=f32, device=dev)
@@ -227,13 +228,69 @@ class NativeBackend:
         no collective (RCCL) or side-stream kernel can run beside them."""
         if not bufs["xfuse"] or os.environ.get("DCR_EXCLUSIVE", "1") == "0":
             return False
+        return self._world() == 1
+
+    @staticmethod
+    def _world() -> int:
         import torch.distributed as dist
 
-        return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+        return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
-    def _persist_ok(self, B: int) -> bool:
-        return (self.use_persist and self.cfg.model == "lstm"
-                and bool(self.ops.lstm_persist_supported(self.H, B)))
+    def _persist_plan(self, B: int, training: bool) -> dict:
+        """Residency plan for the persistent kernels at batch ``B``.
+
+        Every workgroup of a persistent grid spins on its neighbours, so the whole grid must be
+        co-resident.  ``lstm_persist_occupancy`` reports how many workgroups of the exact
+        instantiation fit on one CU (registers + LDS).  The kernels run in one of two modes:
+
+        * ``overlap``: RCCL buckets and the side-stream weight-gradient GEMMs run *beside* the
+          BPTT kernels, so every BPTT grid must leave a spare workgroup slot on each CU
+          (grid <= (occupancy - 1) * CUs);
+        * ``exclusive``: nothing runs beside the persistent kernels (weight GEMMs in stream order,
+          all-reduce buckets released after the last BPTT launch), which allows the faster
+          one-workgroup-per-CU BPTT variant (all hand-off loads in flight, PF_EXCL).
+
+        Overlap is preferred whenever it fits (H=512, B=256, 1 GPU: 3.32 ms/step vs 3.36 for
+        exclusive -- the side-stream weight GEMMs are worth more than the faster BPTT variant),
+        and on multi-GPU it also hides the gradient all-reduce behind BPTT.
+        ``DCR_MODE=overlap|exclusive`` forces a mode.
+        """
+        plan = dict(persist=False, xfuse=False, mode="exclusive", bwd_excl=False)
+        o = self.ops
+        if not (self.use_persist and self.cfg.model == "lstm"
+                and bool(o.lstm_persist_supported(self.H, B))):
+            return plan
+        H, cus, grid = self.H, int(o.num_cus()), int(o.lstm_persist_grid(self.H, B))
+        vdew = self.V if (training and self.V <= 128) else 0
+
+        def occ(bwd, flags, v=0):
+            return int(o.lstm_persist_occupancy(bwd, H, B, v, flags))
+
+        def fits(bwd, flags, margin=0):
+            return all(grid <= (occ(bwd, flags, v) - margin) * cus for v in {0, vdew})
+
+        fwd_flags = PF_GRANULE if self.handoff == "granule" else 0
+        if not (fits(0, fwd_flags) and (not training or fits(1, 0))):
+            return plan
+        plan["persist"] = True
+        plan["xfuse"] = (os.environ.get("DCR_XFUSE", "1") != "0"
+                         and bool(o.lstm_persist_xfuse_supported(H, B)))
+        if not training:
+            return plan
+        shared_ok = fits(1, 0, margin=1)
+        excl_ok = fits(1, PF_EXCL)
+        forced = os.environ.get("DCR_MODE", "")
+        if forced == "overlap" and shared_ok:
+            mode = "overlap"
+        elif forced == "exclusive":
+            mode = "exclusive"
+        elif self._world() > 1:
+            mode = "overlap" if shared_ok else "exclusive"
+        else:
+            mode = "overlap" if (shared_ok and self.side_overlap) else "exclusive"
+        plan["mode"] = mode
+        plan["bwd_excl"] = mode == "exclusive" and excl_ok
+        return plan
 
     def check_errors(self):
         """Raise if a persistent kernel hit its spin timeout (forces a device sync)."""
@@ -344,6 +401,13 @@ class NativeBackend:
         self.ops.segsum(dlog, None, 1, bufs["colsum"][:, :V], bufs["ws"], False)
         s.gview("rnnlm/softmax_b").copy_(bufs["colsum"][0, :V])
         dtop = _mm_into(dlog, hd["Ws"].t(), bufs["dtop"].view(N, H)).view(T, B, H)
+        overlap = bufs["mode"] == "overlap" or not bufs["persist"]
+        pending = []
+        if on_ready is not None and not overlap:
+            # exclusive mode: nothing may run beside the persistent BPTT grids, so the gradient
+            # buckets are released (in the same order) only after the last BPTT launch
+            user_ready = on_ready
+            on_ready = pending.append
         if on_ready is not None:
             sb = s.by_name["rnnlm/softmax_b"]
             on_ready(sb.offset + sb.numel)
@@ -370,7 +434,8 @@ class NativeBackend:
                                           ids_tm if fused_dew else None,
                                           bufs["dew_part"] if fused_dew else None, V, None,
                                           above[0] if above else None,
-                                          above[1] if above else None)
+                                          above[1] if above else None,
+                                          exclusive=bufs["bwd_excl"] and above is None)
             else:
                 self.ops.rnn_bwd_seq(self.cell, lw.Wh, lw.W2, dtop, lb.dz, lb.dzx, lb.gates,
                                      lb.pre, lb.aux, zx_nas, lb.cbuf, lb.h32, lb.hbuf, bufs["dc"],
@@ -396,7 +461,7 @@ class NativeBackend:
                 deferred.append(_wgrads)
                 dtop = None
                 continue
-            if bufs["persist"] and layer > 0 and not drop:
+            if bufs["persist"] and layer > 0 and not drop and self.side_overlap and overlap:
                 # Off the critical path: this layer's weight gradients (two [H x N]·[N x 4H]
                 # GEMMs) run on a side stream concurrently with the latency-bound BPTT of the
                 # layer below; the layer's all-reduce bucket is launched from that stream, so
@@ -460,6 +525,8 @@ class NativeBackend:
         if self._side_used:
             torch.cuda.current_stream().wait_stream(self._side)
             self._side_used = False
+        for off in pending:
+            user_ready(off)
         extras = {"logits": logits, "loss": bufs["row_loss"]} if want_extras else None
         self._steps += 1
         if bufs["persist"] and self._steps % 200 == 1:

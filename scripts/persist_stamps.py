@@ -1,8 +1,11 @@
 """Diagnostic: s_memtime phase shares of the persistent LSTM forward (workgroup 0)."""
+import os
+
 import torch
 from distributed_char_rnn_amd.ops import native
 
 ops = native.ops()
+EXCL = os.environ.get("DCR_MODE", "exclusive") == "exclusive"  # bwd variant to stamp
 B, T, H = 256, 128, 512
 dev = "cuda"
 WT = (torch.randn(4 * H, H, device=dev) * 0.05).to(torch.bfloat16)
@@ -39,10 +42,12 @@ dtop = torch.randn(T, B, H, device=dev) * 0.01
 dz = torch.empty(T, B, 4 * H, dtype=torch.bfloat16, device=dev)
 dbp = torch.empty(B // 16, 4 * H, device=dev)
 for it in range(3):
-    ops.lstm_persist_bwd(W, dtop, dz, gates, cbuf, cnt, err, 1 << 22, dbp, None, None, 65, diag)
+    ops.lstm_persist_bwd(W, dtop, dz, gates, cbuf, cnt, err, 1 << 22, dbp, None, None, 65, diag,
+                         exclusive=EXCL)
 torch.cuda.synchronize()
 ev0.record()
-ops.lstm_persist_bwd(W, dtop, dz, gates, cbuf, cnt, err, 1 << 22, dbp, None, None, 65, diag)
+ops.lstm_persist_bwd(W, dtop, dz, gates, cbuf, cnt, err, 1 << 22, dbp, None, None, 65, diag,
+                         exclusive=EXCL)
 ev1.record()
 torch.cuda.synchronize()
 d = diag.cpu().numpy().astype("float64")[::-1]  # reverse time order

@@ -23,14 +23,19 @@ def _short_spins(monkeypatch, request):
     monkeypatch.setenv("DCR_HANDOFF", request.param)
 
 
+def _persist(backend, B):
+    return backend._persist_plan(B, True)["persist"]
+
+
+@pytest.mark.parametrize("mode", ["exclusive", "overlap"])
 @pytest.mark.parametrize("B,T,H,L", [(32, 5, 128, 2), (48, 7, 256, 1), (64, 9, 512, 2),
-                                     (256, 4, 512, 1), (16, 3, 1024, 1)])
-def test_persist_matches_reference(B, T, H, L, dcr_ops):
-    if not dcr_ops.lstm_persist_supported(H, B):
-        pytest.skip("shape not supported by the persistent path")
+                                     (256, 4, 512, 2), (16, 3, 1024, 1), (128, 3, 1024, 2)])
+def test_persist_matches_reference(B, T, H, L, mode, dcr_ops, monkeypatch):
+    monkeypatch.setenv("DCR_MODE", mode)
     cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=L)
     nat = CharRNN(cfg, device="cuda", seed=3)
-    assert nat.backend._persist_ok(B)
+    if not _persist(nat.backend, B):
+        pytest.skip("grid not co-resident for this shape: per-step path")
     ref = ReferenceBackend(nat.store)
     torch.manual_seed(1)
     x = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
@@ -58,7 +63,7 @@ def test_persist_equals_per_step_kernels(monkeypatch):
     a = CharRNN(cfg, device="cuda", seed=5)
     monkeypatch.setenv("DCR_PERSIST", "0")
     b = CharRNN(cfg, device="cuda", seed=5)
-    assert a.backend._persist_ok(B) and not b.backend._persist_ok(B)
+    assert _persist(a.backend, B) and not _persist(b.backend, B)
     x = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
     la, sa, _ = a.backend.train_step(x, x, a.zero_state(B))
     lb, sb, _ = b.backend.train_step(x, x, b.zero_state(B))
@@ -86,3 +91,37 @@ def test_persist_repeated_calls_stable():
     m.backend.check_errors()
     assert abs(l0.item() - l1.item()) < 1e-5
     assert rel(m.store.grad, g0) < 1e-5
+
+
+def test_residency_plan_and_refusal(dcr_ops):
+    """A grid that cannot be co-resident is planned onto the per-step path, and the op itself
+    refuses to launch it (instead of spinning into a timeout)."""
+    cus = dcr_ops.num_cus()
+    assert cus > 0
+    # bench shape: 256 workgroups, the shared BPTT variant fits twice per CU (overlap-safe)
+    H, B = 512, 256
+    grid = dcr_ops.lstm_persist_grid(H, B)
+    assert grid <= cus * dcr_ops.lstm_persist_occupancy(0, H, B, 0, 0)
+    assert grid <= cus * (dcr_ops.lstm_persist_occupancy(1, H, B, 65, 0) - 1)
+    assert grid <= cus * dcr_ops.lstm_persist_occupancy(1, H, B, 65, 4)
+    # H=1024, B=256: 512 workgroups of a one-per-CU kernel can never all be resident
+    H, B, T = 1024, 256, 2
+    if dcr_ops.lstm_persist_grid(H, B) <= cus * dcr_ops.lstm_persist_occupancy(0, H, B, 0, 0):
+        pytest.skip("this GPU can hold the H=1024 grid")
+    cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=1)
+    m = CharRNN(cfg, device="cuda", seed=1)
+    assert not _persist(m.backend, B)
+    dev = "cuda"
+    WT = torch.zeros(4 * H, H, dtype=torch.bfloat16, device=dev)
+    zx = torch.zeros(T, B, 4 * H, device=dev)
+    hbuf = torch.zeros(T + 1, B, H, dtype=torch.bfloat16, device=dev)
+    cbuf = torch.zeros(T + 1, B, H, device=dev)
+    h32 = torch.zeros(B, H, device=dev)
+    cnt = torch.zeros((B // 16) * (T + 1) * 4, dtype=torch.int32, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    with pytest.raises(RuntimeError, match="co-resident"):
+        dcr_ops.lstm_persist_fwd(WT, zx, None, hbuf, cbuf, None, h32, cnt, err, 1.0, 1 << 16, None)
+    # the model still trains through the per-step kernels
+    x = torch.randint(0, 65, (B, T), device=dev, dtype=torch.int32)
+    loss, _, _ = m.backend.train_step(x, x, m.zero_state(B))
+    assert torch.isfinite(loss).item()
