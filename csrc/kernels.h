@@ -118,4 +118,26 @@ int lstm_persist_occupancy(int bwd, int H, int B, int V, int flags, int cus);
 int launch_lstm_fwd_persist(const PersistArgs& a, int cus, hipStream_t s);
 int launch_lstm_bwd_persist(const PersistArgs& a, int cus, hipStream_t s);
 
+// fused softmax head (head.hip)
+struct HeadArgs {
+  const bf16* O;        // [N, ldo] bf16 top-layer outputs
+  int ldo;
+  const bf16* WsT;      // [VP, H] bf16 softmax_wᵀ, rows >= V zero (VP = head_vpad(V))
+  const bf16* Wsk;      // [H, VK] bf16 softmax_w, columns >= V zero (VK = head_kpad(V))
+  const float* bias;    // [V]
+  const int* targets;   // [N] or nullptr (logits-only)
+  int N, H, V;
+  float grad_scale;     // d loss / d logit scale (1/N for cost = sum/B/T)
+  float* logits;        // [N, V] fp32 or nullptr
+  float* row_loss;      // [N] or nullptr
+  bf16* dlogits;        // [N, V] bf16 or nullptr
+  float* dtop;          // [N, H] fp32 or nullptr
+  float* part;          // [grid, VP+1] partials workspace
+};
+int head_vpad(int V);
+int head_kpad(int V);
+int head_supported(int V, int H);
+int head_num_partials(int N, int cus);
+int launch_head(const HeadArgs& a, int cus, float* db_out, float* loss_out, hipStream_t s);
+
 }  // namespace dcr

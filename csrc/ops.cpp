@@ -449,6 +449,64 @@ void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& d
               "): grid cannot be co-resident on this GPU for H=", H, " B=", B);
 }
 
+// ------------------------------------------------------------------------------------------
+// fused softmax head (head.hip)
+// ------------------------------------------------------------------------------------------
+void head(const at::Tensor& O, const at::Tensor& WsT, const c10::optional<at::Tensor>& Wsk,
+          const at::Tensor& bias, const c10::optional<at::Tensor>& targets, double grad_scale,
+          const c10::optional<at::Tensor>& logits, const c10::optional<at::Tensor>& row_loss,
+          const c10::optional<at::Tensor>& dlogits, const c10::optional<at::Tensor>& dtop,
+          const c10::optional<at::Tensor>& db, at::Tensor& part,
+          const c10::optional<at::Tensor>& loss) {
+  TORCH_CHECK(O.is_cuda() && O.dim() == 2 && O.scalar_type() == at::kBFloat16 && O.stride(1) == 1,
+              "O must be a row-major bf16 [N, H] GPU tensor");
+  const int N = (int)O.size(0), H = (int)O.size(1), V = (int)bias.numel();
+  TORCH_CHECK(dcr::head_supported(V, H), "fused head supports V <= 256 and H % 32 == 0");
+  const int VP = dcr::head_vpad(V), VK = dcr::head_kpad(V);
+  check_seq(WsT, at::kBFloat16, "WsT");
+  check_seq(bias, at::kFloat, "bias");
+  TORCH_CHECK(WsT.numel() == (int64_t)VP * H, "WsT must be [head_vpad(V), H]");
+  const bool train = has(dlogits) || has(dtop);
+  if (has(dtop)) {
+    TORCH_CHECK(has(Wsk), "dtop needs Wsk");
+    check_seq(*Wsk, at::kBFloat16, "Wsk");
+    TORCH_CHECK(Wsk->numel() == (int64_t)H * VK, "Wsk must be [H, head_kpad(V)]");
+    check_seq(*dtop, at::kFloat, "dtop");
+    TORCH_CHECK(dtop->numel() == (int64_t)N * H, "dtop must be [N, H]");
+  }
+  if (train || has(loss) || has(row_loss)) {
+    TORCH_CHECK(has(targets), "loss / gradients need targets");
+  }
+  if (has(targets)) {
+    check_seq(*targets, at::kInt, "targets");
+    TORCH_CHECK(targets->numel() == N, "targets must be [N]");
+  }
+  if (has(logits)) { check_seq(*logits, at::kFloat, "logits"); TORCH_CHECK(logits->numel() == (int64_t)N * V, "logits must be [N, V]"); }
+  if (has(row_loss)) { check_seq(*row_loss, at::kFloat, "row_loss"); TORCH_CHECK(row_loss->numel() == N, "row_loss must be [N]"); }
+  if (has(dlogits)) { check_seq(*dlogits, at::kBFloat16, "dlogits"); TORCH_CHECK(dlogits->numel() == (int64_t)N * V, "dlogits must be [N, V]"); }
+  if (has(db)) { check_seq(*db, at::kFloat, "db"); TORCH_CHECK(db->numel() == V, "db must be [V]"); }
+  if (has(loss)) { check_seq(*loss, at::kFloat, "loss"); TORCH_CHECK(loss->numel() >= 1, "loss must hold 1 float"); }
+  check_seq(part, at::kFloat, "part");
+  TORCH_CHECK(part.numel() >= (int64_t)dcr::head_num_partials(N, num_cus()) * (VP + 1),
+              "partials workspace too small (head_num_partials)");
+  dcr::HeadArgs a{};
+  a.O = ptr<bf16>(O);
+  a.ldo = (int)O.stride(0);
+  a.WsT = ptr<bf16>(WsT);
+  a.Wsk = optr<bf16>(Wsk);
+  a.bias = ptr<float>(bias);
+  a.targets = optr<int>(targets);
+  a.N = N; a.H = H; a.V = V;
+  a.grad_scale = (float)grad_scale;
+  a.logits = optr<float>(logits);
+  a.row_loss = optr<float>(row_loss);
+  a.dlogits = optr<bf16>(dlogits);
+  a.dtop = optr<float>(dtop);
+  a.part = ptr<float>(part);
+  TORCH_CHECK(dcr::launch_head(a, num_cus(), optr<float>(db), optr<float>(loss), cur_stream()) == 0,
+              "fused head launch failed");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(dcr, m) {
@@ -493,6 +551,19 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor(b!) cnt, Tensor(c!) err, int spin_limit, Tensor(d!)? db_part, Tensor? ids, "
       "Tensor(e!)? dew_part, int V, Tensor(f!)? diag=None, Tensor? Wx_above=None, "
       "Tensor? dz_above=None, bool exclusive=False) -> ()");
+  m.def("head_supported(int V, int H) -> int", [](int64_t V, int64_t H) -> int64_t {
+    return dcr::head_supported((int)V, (int)H);
+  });
+  m.def("head_pads(int V) -> int[]", [](int64_t V) -> std::vector<int64_t> {
+    return {dcr::head_vpad((int)V), dcr::head_kpad((int)V)};
+  });
+  m.def("head_workspace(int N, int V) -> int", [](int64_t N, int64_t V) -> int64_t {
+    return (int64_t)dcr::head_num_partials((int)N, num_cus()) * (dcr::head_vpad((int)V) + 1);
+  });
+  m.def(
+      "head(Tensor O, Tensor WsT, Tensor? Wsk, Tensor bias, Tensor? targets, float grad_scale, "
+      "Tensor(a!)? logits, Tensor(b!)? row_loss, Tensor(c!)? dlogits, Tensor(d!)? dtop, "
+      "Tensor(e!)? db, Tensor(f!) part, Tensor(g!)? loss) -> ()");
   m.def("segsum(Tensor X, Tensor? ids, int V, Tensor(a!) out, Tensor(b!) workspace, bool accumulate) -> ()");
   m.def("segsum_workspace(int N, int W, int V) -> int", [](int64_t N, int64_t W, int64_t V) -> int64_t {
     return (int64_t)dcr::segsum_workspace_floats((int)N, (int)W, (int)V);
@@ -508,4 +579,5 @@ TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("segsum", &segsum);
   m.impl("lstm_persist_fwd", &lstm_persist_fwd);
   m.impl("lstm_persist_bwd", &lstm_persist_bwd);
+  m.impl("head", &head);
 }

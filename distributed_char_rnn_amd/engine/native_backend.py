@@ -65,6 +65,39 @@ def _mm_into(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor,
     return out
 
 
+def _split_k(K: int, M: int, Nn: int) -> int:
+    """Split factor for a token-reduction GEMM with a small [M, Nn] output: the library tiles
+    such an output into a few dozen workgroups (the 512x2048, K=32768 weight gradient ran on 73
+    of 256 CUs at 335 TFLOP/s), so the reduction is split into S batched slices instead
+    (scripts/bench_gemms.py: 205 -> 97 us at S=8; the 512x65 head gradient 133 -> 27 us)."""
+    if K < 8192 or -(-M // 128) * -(-Nn // 256) >= 128:
+        return 1
+    S = 8 if M * Nn >= (1 << 18) else 16
+    while S > 1 and (K % S or K // S < 1024):
+        S //= 2
+    return S
+
+
+def _mm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
+           split: bool = True) -> torch.Tensor:
+    """fp32 ``aᵀ·b`` for token-major bf16 operands ``a`` [K, M] and ``b`` [K, Nn] (weight
+    gradients: K = T·B tokens), split-K over batched MFMA GEMMs + one fp32 sum when the output
+    is too small to fill the chip.  ``split=False`` for GEMMs that run beside a persistent
+    kernel on a side stream: there a chip-filling grid only steals the recurrence's CUs
+    (measured: 256-workgroup split-K beside BPTT stretched both)."""
+    K, M = a.shape
+    Nn = b.shape[1]
+    S = _split_k(K, M, Nn) if split else 1
+    if S == 1:
+        return _mm(a.t(), b) if out is None else _mm_into(a.t(), b, out)
+    part = torch.bmm(a.unflatten(0, (S, K // S)).transpose(1, 2), b.unflatten(0, (S, K // S)),
+                     out_dtype=f32)
+    if out is None:
+        return part.sum(0)
+    torch.sum(part, 0, out=out)
+    return out
+
+
 @dataclass
 class LayerWeights:
     Wx: torch.Tensor            # [D, GW] bf16 input projection
@@ -121,6 +154,9 @@ class NativeBackend:
         # 3.47 ms/step: its extra dZ loads sit on the load-bound critical path), opt-in only
         self.fused_dtop = os.environ.get("DCR_FUSED_DTOP", "0") == "1"
         self.side_overlap = os.environ.get("DCR_SIDE", "1") == "1"
+        # fused softmax head (csrc/head.hip): logits + CE + dlogits + d softmax_b + dtop
+        self.fused_head = (os.environ.get("DCR_FUSED_HEAD", "1") != "0"
+                           and bool(self.ops.head_supported(self.V, self.H)))
         self.err = torch.zeros(1, dtype=torch.int32, device=self.dev)
         self._side = None
         self._side_used = False
@@ -163,8 +199,16 @@ class NativeBackend:
         E = s.view("embedding")
         w0 = self._w[0]
         table = torch.addmm(w0.bias, E, w0.Wx32)  # [V, GW] fp32: (E·W_x0 + b0)
-        self._head = dict(E=E, table=table.contiguous(), Ws=s.view("rnnlm/softmax_w").to(bf16),
+        Ws32 = s.view("rnnlm/softmax_w")
+        self._head = dict(E=E, table=table.contiguous(), Ws=Ws32.to(bf16),
                           bs=s.view("rnnlm/softmax_b"))
+        if self.fused_head:
+            VP, VK = self.ops.head_pads(self.V)
+            WsT = torch.zeros(VP, H, dtype=bf16, device=self.dev)
+            WsT[: self.V].copy_(Ws32.t())
+            Wsk = torch.zeros(H, VK, dtype=bf16, device=self.dev)
+            Wsk[:, : self.V].copy_(Ws32)
+            self._head.update(WsT=WsT, Wsk=Wsk)
         self._wver = ver
 
     # ------------------------------------------------------------------ buffers
@@ -205,6 +249,8 @@ class NativeBackend:
             gpart=torch.empty(B, H, dtype=f32, device=dev) if m == "gru" else None,
             ws=torch.empty(ws, dtype=f32, device=dev),
             colsum=torch.empty(1, max(GW, self.V), dtype=f32, device=dev),
+            head_part=(torch.empty(self.ops.head_workspace(N, self.V), dtype=f32, device=dev)
+                       if self.fused_head else None),
             **self._persist_plan(B, training),
             dtop=torch.empty(T, B, H, dtype=f32, device=dev) if training else None,
             dx=torch.empty(T, B, H, dtype=f32, device=dev) if training else None,
@@ -308,7 +354,7 @@ class NativeBackend:
         return (torch.rand(shape, device=self.dev, generator=self.gen) < keep).to(bf16) * (1.0 / keep)
 
     # ------------------------------------------------------------------ forward
-    def _forward(self, ids_tm: torch.Tensor, state, training: bool):
+    def _forward(self, ids_tm: torch.Tensor, state, training: bool, want_logits: bool = True):
         T, B = ids_tm.shape
         H, N = self.H, T * B
         self._prep()
@@ -374,7 +420,8 @@ class NativeBackend:
         if not O.is_contiguous():
             O = O.contiguous()
         logits = bufs["logits"]
-        _mm_into(O, self._head["Ws"], logits, bias=self._head["bs"])
+        if want_logits:
+            _mm_into(O, self._head["Ws"], logits, bias=self._head["bs"])
         new_state = []
         for layer in range(self.L):
             lb = bufs["layers"][layer]
@@ -392,15 +439,26 @@ class NativeBackend:
         tgt = y.t().contiguous().view(-1)
         T, B = ids_tm.shape
         H, V, N, GW = self.H, self.V, T * B, self.GW
-        bufs, O, logits, new_state = self._forward(ids_tm, state, True)
+        bufs, O, logits, new_state = self._forward(ids_tm, state, True,
+                                                   want_logits=not self.fused_head)
         dlog = bufs["dlogits"]
-        self.ops.xent(logits, tgt, 1.0 / N, bufs["row_loss"], dlog, bufs["xpart"], bufs["loss"])
         s, hd = self.store, self._head
-        # ---- head gradients
-        _mm_into(O.t(), dlog, s.gview("rnnlm/softmax_w"))
-        self.ops.segsum(dlog, None, 1, bufs["colsum"][:, :V], bufs["ws"], False)
-        s.gview("rnnlm/softmax_b").copy_(bufs["colsum"][0, :V])
-        dtop = _mm_into(dlog, hd["Ws"].t(), bufs["dtop"].view(N, H)).view(T, B, H)
+        if self.fused_head:
+            # one launch: logits (only if asked for) -> CE -> bf16 dlogits, d softmax_b, dtop
+            self.ops.head(O, hd["WsT"], hd["Wsk"], hd["bs"], tgt, 1.0 / N,
+                          logits if want_extras else None, bufs["row_loss"], dlog,
+                          bufs["dtop"].view(N, H), s.gview("rnnlm/softmax_b"),
+                          bufs["head_part"], bufs["loss"])
+            _mm_tn(O, dlog, s.gview("rnnlm/softmax_w"))
+            dtop = bufs["dtop"].view(T, B, H)
+        else:
+            self.ops.xent(logits, tgt, 1.0 / N, bufs["row_loss"], dlog, bufs["xpart"],
+                          bufs["loss"])
+            # ---- head gradients
+            _mm_tn(O, dlog, s.gview("rnnlm/softmax_w"))
+            self.ops.segsum(dlog, None, 1, bufs["colsum"][:, :V], bufs["ws"], False)
+            s.gview("rnnlm/softmax_b").copy_(bufs["colsum"][0, :V])
+            dtop = _mm_into(dlog, hd["Ws"].t(), bufs["dtop"].view(N, H)).view(T, B, H)
         overlap = bufs["mode"] == "overlap" or not bufs["persist"]
         pending = []
         if on_ready is not None and not overlap:
@@ -453,8 +511,8 @@ class NativeBackend:
 
                 def _wgrads(names=names, Hprev=Hprev, dZ=dZ, dZx=dZx, lb=lb, dbias=dbias,
                             layer=layer):
-                    _mm_into(Hprev.t(), dZ, s.gview(names[0])[H:])
-                    _mm_into(lb.x_in.t(), dZx, s.gview(names[0])[:H])
+                    _mm_tn(Hprev, dZ, s.gview(names[0])[H:])
+                    _mm_tn(lb.x_in, dZx, s.gview(names[0])[:H])
                     s.gview(names[1]).copy_(dbias)
                     if on_ready is not None:
                         on_ready(s.layer_range(layer)[1])
@@ -472,8 +530,8 @@ class NativeBackend:
                 side = self._side_stream()
                 with torch.cuda.stream(side):
                     side.wait_event(ev)
-                    _mm_into(Hprev.t(), dZ, s.gview(names[0])[H:])
-                    _mm_into(lb.x_in.t(), dZx, s.gview(names[0])[:H])
+                    _mm_tn(Hprev, dZ, s.gview(names[0])[H:], split=False)
+                    _mm_tn(lb.x_in, dZx, s.gview(names[0])[:H], split=False)
                     s.gview(names[1]).copy_(dbias)
                     dbias.record_stream(side)
                     if on_ready is not None:
@@ -487,12 +545,12 @@ class NativeBackend:
             # recurrent-weight gradients
             if self.cfg.model == "gru":
                 gk, gb, ck, cb = names
-                s.gview(gk)[H:].copy_(_mm(Hprev.t(), dZ[:, : 2 * H]))
-                s.gview(ck)[H:].copy_(_mm(lb.rh.view(N, H).t(), dZ[:, 2 * H:]))
+                _mm_tn(Hprev, dZ[:, : 2 * H], s.gview(gk)[H:])
+                _mm_tn(lb.rh.view(N, H), dZ[:, 2 * H:], s.gview(ck)[H:])
             elif self.cfg.model == "nas":
-                _mm_into(Hprev.t(), dZ, s.gview(names[1]))
+                _mm_tn(Hprev, dZ, s.gview(names[1]))
             else:
-                _mm_into(Hprev.t(), dZ, s.gview(names[0])[H:])
+                _mm_tn(Hprev, dZ, s.gview(names[0])[H:])
             if gather:
                 if fused_dew:
                     dEW = bufs["dew_part"].sum(0)            # [V, GW] fp32 (fused in BPTT)
@@ -503,7 +561,7 @@ class NativeBackend:
                 dbias = dEW.sum(0)
                 torch.mm(dEW, lw.Wx32.t(), out=s.gview("embedding"))
             else:
-                dWx = _mm(lb.x_in.t(), dZx)
+                dWx = _mm_tn(lb.x_in, dZx)
                 if bufs["persist"]:
                     dbias = bufs["db_part"][layer].sum(0)    # fused in BPTT
                 else:
@@ -560,8 +618,14 @@ class NativeBackend:
     def eval_loss(self, x, y, state):
         ids_tm = x.t().contiguous()
         tgt = y.t().contiguous().view(-1)
-        bufs, O, logits, new_state = self._forward(ids_tm, state, False)
-        self.ops.xent(logits, tgt, 1.0, None, None, bufs["xpart"], bufs["loss"])
+        bufs, O, logits, new_state = self._forward(ids_tm, state, False,
+                                                   want_logits=not self.fused_head)
+        if self.fused_head:
+            hd = self._head
+            self.ops.head(O, hd["WsT"], None, hd["bs"], tgt, 1.0, None, None, None, None, None,
+                          bufs["head_part"], bufs["loss"])
+        else:
+            self.ops.xent(logits, tgt, 1.0, None, None, bufs["xpart"], bufs["loss"])
         return bufs["loss"][0].clone(), new_state
 
     @torch.no_grad()
