@@ -296,10 +296,12 @@ class NativeBackend:
           all-reduce buckets released after the last BPTT launch), which allows the faster
           one-workgroup-per-CU BPTT variant (all hand-off loads in flight, PF_EXCL).
 
-        Overlap is preferred whenever it fits (H=512, B=256, 1 GPU: 3.32 ms/step vs 3.36 for
-        exclusive -- the side-stream weight GEMMs are worth more than the faster BPTT variant),
-        and on multi-GPU it also hides the gradient all-reduce behind BPTT.
-        ``DCR_MODE=overlap|exclusive`` forces a mode.
+        Exclusive is preferred whenever its BPTT variant fits: with the weight GEMMs split-K in
+        stream order it measured 2.74-2.80 vs 3.03-3.06 ms/step for overlap (H=512, B=256, same
+        box) -- a chip-filling GEMM beside the latency-bound recurrence slows both.  Under data
+        parallelism the gradient buckets are released right after the last BPTT launch, so the
+        all-reduce still overlaps the layer-0 weight GEMMs.  ``DCR_MODE=overlap|exclusive``
+        forces a mode.
         """
         plan = dict(persist=False, xfuse=False, mode="exclusive", bwd_excl=False)
         o = self.ops
@@ -330,8 +332,8 @@ class NativeBackend:
             mode = "overlap"
         elif forced == "exclusive":
             mode = "exclusive"
-        elif self._world() > 1:
-            mode = "overlap" if shared_ok else "exclusive"
+        elif excl_ok:
+            mode = "exclusive"
         else:
             mode = "overlap" if (shared_ok and self.side_overlap) else "exclusive"
         plan["mode"] = mode
@@ -494,6 +496,12 @@ class NativeBackend:
                                           above[0] if above else None,
                                           above[1] if above else None,
                                           exclusive=bufs["bwd_excl"] and above is None)
+                if layer == 0 and pending:
+                    # the last persistent grid is queued: buckets may now run beside the
+                    # (non-persistent) layer-0 weight GEMMs
+                    for off in pending:
+                        user_ready(off)
+                    pending.clear()
             else:
                 self.ops.rnn_bwd_seq(self.cell, lw.Wh, lw.W2, dtop, lb.dz, lb.dzx, lb.gates,
                                      lb.pre, lb.aux, zx_nas, lb.cbuf, lb.h32, lb.hbuf, bufs["dc"],

@@ -6,7 +6,8 @@ from distributed_char_rnn_amd.ops import native
 
 ops = native.ops()
 EXCL = os.environ.get("DCR_MODE", "exclusive") == "exclusive"  # bwd variant to stamp
-B, T, H = 256, 128, 512
+B = int(os.environ.get("DCR_B", "256"))
+T, H = 128, int(os.environ.get("DCR_H", "512"))
 dev = "cuda"
 WT = (torch.randn(4 * H, H, device=dev) * 0.05).to(torch.bfloat16)
 zx = torch.randn(T, B, 4 * H, device=dev) * 0.1
