@@ -107,6 +107,7 @@ struct PersistArgs {
   float forget_bias;
   unsigned spin_limit;
   int excl;              // bwd: all-loads-in-flight variant (one WG per CU: nothing may run beside it)
+  int cnt_zeroed;        // counters already zeroed by the caller (batched prep launch)
 };
 int lstm_persist_supported(int H, int B, int cus);
 int lstm_persist_grid(int H, int B, int cus);
@@ -139,5 +140,23 @@ int head_kpad(int V);
 int head_supported(int V, int H);
 int head_num_partials(int N, int cus);
 int launch_head(const HeadArgs& a, int cus, float* db_out, float* loss_out, hipStream_t s);
+
+// batched per-step data movement (prep.hip)
+enum PrepMode : int { PREP_COPY = 0, PREP_TRANSPOSE = 1, PREP_ZERO = 2 };
+struct PrepTask {
+  const float* src;     // fp32 row-strided source (unused for ZERO)
+  void* dst;            // bf16 or fp32 (ZERO: any 4-byte element type)
+  int rows, cols;       // source shape (ZERO: destination shape)
+  int src_ld, dst_ld;   // row strides in elements
+  int mode;             // PrepMode
+  int dst_bf16;         // 1: bf16 destination
+  int tile0;            // first tile (set by launch_prep)
+};
+constexpr int kPrepMaxTasks = 48;
+struct PrepTable {
+  PrepTask t[kPrepMaxTasks];
+  int n;
+};
+void launch_prep(PrepTable& tab, hipStream_t s);
 
 }  // namespace dcr

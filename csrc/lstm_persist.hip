@@ -785,7 +785,8 @@ static int launch_persist(int bwd, const PersistArgs& a, int flags, int cus, hip
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 256, lds) != hipSuccess ||
       grid > occ * cus)
     return -2;
-  (void)hipMemsetAsync(a.cnt, 0, sizeof(unsigned) * (size_t)(a.B / 16) * (a.T + 1) * 4, s);
+  if (!a.cnt_zeroed)
+    (void)hipMemsetAsync(a.cnt, 0, sizeof(unsigned) * (size_t)(a.B / 16) * (a.T + 1) * 4, s);
   if (a.ring) (void)hipMemsetAsync(a.ring, 0, sizeof(uint64_t) * 2 * (size_t)a.B * (a.H / 2), s);
   void* args[] = {const_cast<PersistArgs*>(&a)};
   return hipLaunchKernel(fn, dim3(grid), dim3(256), args, lds, s) == hipSuccess ? 0 : -3;

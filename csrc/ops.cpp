@@ -325,7 +325,8 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
                       at::Tensor& hlast32, at::Tensor& cnt, at::Tensor& err, double forget_bias,
                       int64_t spin_limit, const c10::optional<at::Tensor>& ring,
                       const c10::optional<at::Tensor>& diag, const c10::optional<at::Tensor>& WxT,
-                      const c10::optional<at::Tensor>& xin, const c10::optional<at::Tensor>& bias) {
+                      const c10::optional<at::Tensor>& xin, const c10::optional<at::Tensor>& bias,
+                      bool cnt_zeroed) {
   check_seq(WT, at::kBFloat16, "WT");
   check_seq(zx, at::kFloat, "zx");
   check_seq(hbuf, at::kBFloat16, "hbuf");
@@ -383,6 +384,7 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
     TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)T * 8, "diag must hold [T, 8] int64");
     a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());
   }
+  a.cnt_zeroed = cnt_zeroed ? 1 : 0;
   const int rc = dcr::launch_lstm_fwd_persist(a, num_cus(), cur_stream());
   TORCH_CHECK(rc == 0, "persistent LSTM forward not launched (", rc,
               "): grid cannot be co-resident on this GPU for H=", H, " B=", B);
@@ -394,7 +396,7 @@ void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& d
                       const c10::optional<at::Tensor>& ids,
                       const c10::optional<at::Tensor>& dew_part, int64_t V,
                       const c10::optional<at::Tensor>& diag, const c10::optional<at::Tensor>& Wx_above,
-                      const c10::optional<at::Tensor>& dz_above, bool exclusive) {
+                      const c10::optional<at::Tensor>& dz_above, bool exclusive, bool cnt_zeroed) {
   check_seq(W, at::kBFloat16, "W");
   check_seq(dtop, at::kFloat, "dtop");
   check_seq(dz, at::kBFloat16, "dz");
@@ -444,6 +446,7 @@ void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& d
     a.dzx = optr<bf16>(dz_above);
   }
   a.excl = exclusive ? 1 : 0;
+  a.cnt_zeroed = cnt_zeroed ? 1 : 0;
   const int rc = dcr::launch_lstm_bwd_persist(a, num_cus(), cur_stream());
   TORCH_CHECK(rc == 0, "persistent LSTM BPTT not launched (", rc,
               "): grid cannot be co-resident on this GPU for H=", H, " B=", B);
@@ -507,6 +510,51 @@ void head(const at::Tensor& O, const at::Tensor& WsT, const c10::optional<at::Te
               "fused head launch failed");
 }
 
+// ------------------------------------------------------------------------------------------
+// batched per-step data movement (prep.hip)
+// ------------------------------------------------------------------------------------------
+void prep(at::TensorList src, at::TensorList dst, at::IntArrayRef mode) {
+  TORCH_CHECK(src.size() == dst.size() && dst.size() == mode.size(), "prep: list lengths differ");
+  TORCH_CHECK((int)dst.size() <= dcr::kPrepMaxTasks, "prep: too many tasks");
+  dcr::PrepTable tab{};
+  tab.n = (int)dst.size();
+  auto ld = [](const at::Tensor& t) -> int {
+    TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1, "prep: views must be 2-D with unit column stride");
+    return (int)t.stride(0);
+  };
+  for (int i = 0; i < tab.n; ++i) {
+    const at::Tensor& d = dst[i];
+    TORCH_CHECK(d.is_cuda(), "prep: destinations must be GPU tensors");
+    dcr::PrepTask& T = tab.t[i];
+    T.mode = (int)mode[i];
+    T.dst = d.data_ptr();
+    T.dst_ld = ld(d);
+    if (T.mode == dcr::PREP_ZERO) {
+      TORCH_CHECK(d.element_size() == 4, "prep: ZERO needs 4-byte elements");
+      T.rows = (int)d.size(0);
+      T.cols = (int)d.size(1);
+      continue;
+    }
+    const at::Tensor& s = src[i];
+    TORCH_CHECK(s.is_cuda() && s.scalar_type() == at::kFloat, "prep: sources must be fp32 GPU tensors");
+    TORCH_CHECK(d.scalar_type() == at::kBFloat16 || d.scalar_type() == at::kFloat,
+                "prep: destinations must be bf16 or fp32");
+    T.src = s.data_ptr<float>();
+    T.src_ld = ld(s);
+    T.rows = (int)s.size(0);
+    T.cols = (int)s.size(1);
+    T.dst_bf16 = d.scalar_type() == at::kBFloat16 ? 1 : 0;
+    if (T.mode == dcr::PREP_COPY) {
+      TORCH_CHECK(d.size(0) == s.size(0) && d.size(1) == s.size(1), "prep: copy shape mismatch");
+    } else if (T.mode == dcr::PREP_TRANSPOSE) {
+      TORCH_CHECK(d.size(0) == s.size(1) && d.size(1) == s.size(0), "prep: transpose shape mismatch");
+    } else {
+      TORCH_CHECK(false, "prep: unknown mode");
+    }
+  }
+  dcr::launch_prep(tab, cur_stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(dcr, m) {
@@ -545,12 +593,12 @@ TORCH_LIBRARY(dcr, m) {
       "lstm_persist_fwd(Tensor WT, Tensor zx, Tensor? ids, Tensor(a!) hbuf, Tensor(b!) cbuf, "
       "Tensor(c!)? gates, Tensor(d!) hlast32, Tensor(e!) cnt, Tensor(f!) err, float forget_bias, "
       "int spin_limit, Tensor(g!)? ring, Tensor(h!)? diag=None, Tensor? WxT=None, Tensor? xin=None, "
-      "Tensor? bias=None) -> ()");
+      "Tensor? bias=None, bool cnt_zeroed=False) -> ()");
   m.def(
       "lstm_persist_bwd(Tensor W, Tensor dtop, Tensor(a!) dz, Tensor gates, Tensor cbuf, "
       "Tensor(b!) cnt, Tensor(c!) err, int spin_limit, Tensor(d!)? db_part, Tensor? ids, "
       "Tensor(e!)? dew_part, int V, Tensor(f!)? diag=None, Tensor? Wx_above=None, "
-      "Tensor? dz_above=None, bool exclusive=False) -> ()");
+      "Tensor? dz_above=None, bool exclusive=False, bool cnt_zeroed=False) -> ()");
   m.def("head_supported(int V, int H) -> int", [](int64_t V, int64_t H) -> int64_t {
     return dcr::head_supported((int)V, (int)H);
   });
@@ -564,6 +612,7 @@ TORCH_LIBRARY(dcr, m) {
       "head(Tensor O, Tensor WsT, Tensor? Wsk, Tensor bias, Tensor? targets, float grad_scale, "
       "Tensor(a!)? logits, Tensor(b!)? row_loss, Tensor(c!)? dlogits, Tensor(d!)? dtop, "
       "Tensor(e!)? db, Tensor(f!) part, Tensor(g!)? loss) -> ()");
+  m.def("prep(Tensor[] src, Tensor(a!)[] dst, int[] mode) -> ()");
   m.def("segsum(Tensor X, Tensor? ids, int V, Tensor(a!) out, Tensor(b!) workspace, bool accumulate) -> ()");
   m.def("segsum_workspace(int N, int W, int V) -> int", [](int64_t N, int64_t W, int64_t V) -> int64_t {
     return (int64_t)dcr::segsum_workspace_floats((int)N, (int)W, (int)V);
@@ -580,4 +629,5 @@ TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("lstm_persist_fwd", &lstm_persist_fwd);
   m.impl("lstm_persist_bwd", &lstm_persist_bwd);
   m.impl("head", &head);
+  m.impl("prep", &prep);
 }

@@ -144,6 +144,7 @@ class NativeBackend:
         self.GW = {"lstm": 4, "gru": 3, "rnn": 1, "nas": 8}[self.cfg.model] * self.H
         self._wver = None
         self._w: List[LayerWeights] = []
+        self._table_dirty = False
         self._head = None
         self._bufs: Dict[Tuple[int, int, bool], dict] = {}
         self.use_persist = os.environ.get("DCR_PERSIST", "1") != "0"
@@ -168,48 +169,71 @@ class NativeBackend:
     def params_changed(self):
         self._wver = None
 
-    def _prep(self):
-        ver = getattr(self.store, "version", 0)
-        if self._wver == ver and self._w:
-            return
-        s, H, D = self.store, self.H, self.H
-        self._w = []
+    def _alloc_weights(self):
+        """bf16 (and padded / concatenated fp32) layouts of the master weights, allocated once
+        and refreshed by ``_weight_tasks`` through the batched prep kernel."""
+        s, H, D, dev = self.store, self.H, self.H, self.dev
+        self._w, self._wtasks = [], []
+        T = self._wtasks
+        e = lambda *shape, dt=bf16: torch.empty(*shape, dtype=dt, device=dev)  # noqa: E731
         for layer in range(self.L):
             names = [sp.name for sp in cell_specs(self.cfg, layer)]
-            if self.cfg.model == "lstm" or self.cfg.model == "rnn":
+            if self.cfg.model in ("lstm", "rnn"):
                 k, b = s.view(names[0]), s.view(names[1])
-                Wh = k[D:].to(bf16).contiguous()
-                Wx = k[:D].to(bf16).contiguous()
-                lw = LayerWeights(Wx=Wx, Wx32=k[:D], bias=b, Wh=Wh, WhT=Wh.t().contiguous(),
-                                  WxT=Wx.t().contiguous() if layer > 0 else None)
+                GW = k.shape[1]
+                lw = LayerWeights(Wx=e(D, GW), Wx32=k[:D], bias=b, Wh=e(H, GW), WhT=e(GW, H),
+                                  WxT=e(GW, D) if (layer > 0 and self.cfg.model == "lstm")
+                                  else None)
+                T += [(k[D:], lw.Wh, 0), (k[D:], lw.WhT, 1), (k[:D], lw.Wx, 0)]
+                if lw.WxT is not None:
+                    T.append((k[:D], lw.WxT, 1))
             elif self.cfg.model == "gru":
                 gk, gb, ck, cb = (s.view(n) for n in names)
-                Wx32 = torch.cat([gk[:D], ck[:D]], 1)
-                Wg = gk[D:].to(bf16).contiguous()
-                Wc = ck[D:].to(bf16).contiguous()
-                lw = LayerWeights(Wx=Wx32.to(bf16), Wx32=Wx32, bias=torch.cat([gb, cb]),
-                                  Wh=Wc, WhT=Wg.t().contiguous(), W2=Wg, WT2=Wc.t().contiguous())
+                Wx32, bias = e(D, 3 * H, dt=f32), e(3 * H, dt=f32)
+                lw = LayerWeights(Wx=e(D, 3 * H), Wx32=Wx32, bias=bias, Wh=e(H, H),
+                                  WhT=e(2 * H, H), W2=e(H, 2 * H), WT2=e(H, H))
+                T += [(gk[:D], Wx32[:, : 2 * H], 0), (ck[:D], Wx32[:, 2 * H:], 0),
+                      (gk[:D], lw.Wx[:, : 2 * H], 0), (ck[:D], lw.Wx[:, 2 * H:], 0),
+                      (gk[D:], lw.W2, 0), (gk[D:], lw.WhT, 1), (ck[D:], lw.Wh, 0),
+                      (ck[D:], lw.WT2, 1), (gb.view(1, -1), bias[: 2 * H].view(1, -1), 0),
+                      (cb.view(1, -1), bias[2 * H:].view(1, -1), 0)]
             else:  # nas
                 kx, km = s.view(names[0]), s.view(names[1])
-                Wh = km.to(bf16).contiguous()
-                lw = LayerWeights(Wx=kx.to(bf16).contiguous(), Wx32=kx,
-                                  bias=torch.zeros(8 * H, device=self.dev), Wh=Wh,
-                                  WhT=Wh.t().contiguous())
+                lw = LayerWeights(Wx=e(D, 8 * H), Wx32=kx, bias=torch.zeros(8 * H, device=dev),
+                                  Wh=e(H, 8 * H), WhT=e(8 * H, H))
+                T += [(km, lw.Wh, 0), (km, lw.WhT, 1), (kx, lw.Wx, 0)]
             self._w.append(lw)
-        E = s.view("embedding")
-        w0 = self._w[0]
-        table = torch.addmm(w0.bias, E, w0.Wx32)  # [V, GW] fp32: (E·W_x0 + b0)
         Ws32 = s.view("rnnlm/softmax_w")
-        self._head = dict(E=E, table=table.contiguous(), Ws=Ws32.to(bf16),
-                          bs=s.view("rnnlm/softmax_b"))
+        self._head = dict(E=s.view("embedding"), Ws=e(H, self.V), bs=s.view("rnnlm/softmax_b"))
+        T.append((Ws32, self._head["Ws"], 0))
         if self.fused_head:
             VP, VK = self.ops.head_pads(self.V)
-            WsT = torch.zeros(VP, H, dtype=bf16, device=self.dev)
-            WsT[: self.V].copy_(Ws32.t())
-            Wsk = torch.zeros(H, VK, dtype=bf16, device=self.dev)
-            Wsk[:, : self.V].copy_(Ws32)
-            self._head.update(WsT=WsT, Wsk=Wsk)
+            self._head["WsT"] = torch.zeros(VP, H, dtype=bf16, device=dev)   # pads stay zero
+            self._head["Wsk"] = torch.zeros(H, VK, dtype=bf16, device=dev)
+            T += [(Ws32, self._head["WsT"][: self.V], 1),
+                  (Ws32, self._head["Wsk"][:, : self.V], 0)]
+
+    def _prep(self) -> list:
+        """Prep-kernel tasks that refresh the weight layouts after a parameter change (empty
+        when the weights are current); the layer-0 ``E·W_x + b`` table is recomputed after
+        they ran (``_run_prep``)."""
+        ver = getattr(self.store, "version", 0)
+        if not self._w:
+            self._alloc_weights()
+        elif self._wver == ver:
+            return []
         self._wver = ver
+        self._table_dirty = True
+        return list(self._wtasks)
+
+    def _run_prep(self, tasks: list):
+        for i in range(0, len(tasks), 48):  # kPrepMaxTasks
+            chunk = tasks[i: i + 48]
+            self.ops.prep([t[0] for t in chunk], [t[1] for t in chunk], [t[2] for t in chunk])
+        if self._table_dirty:
+            w0 = self._w[0]
+            self._head["table"] = torch.addmm(w0.bias, self._head["E"], w0.Wx32)  # [V, GW]
+            self._table_dirty = False
 
     # ------------------------------------------------------------------ buffers
     def _buffers(self, B: int, T: int, training: bool) -> dict:
@@ -258,7 +282,9 @@ class NativeBackend:
                      if training else None),
             dew_part=(torch.empty(max(B // 16, 1), self.V, GW, dtype=f32, device=dev)
                       if (training and self.V <= 128) else None),
-            cnt=torch.zeros((B // 16 + 1) * (T + 1) * 4, dtype=torch.int32, device=dev),
+            # one hand-off counter region per persistent launch (fwd layers, then bwd layers),
+            # zeroed together by the step's prep launch
+            cnt=torch.zeros(2 * self.L, (B // 16 + 1) * (T + 1) * 4, dtype=torch.int32, device=dev),
             ring=torch.zeros(2 * B * (H // 2), dtype=torch.int64, device=dev),
         )
         self._bufs[key] = bufs
@@ -359,21 +385,27 @@ class NativeBackend:
     def _forward(self, ids_tm: torch.Tensor, state, training: bool, want_logits: bool = True):
         T, B = ids_tm.shape
         H, N = self.H, T * B
-        self._prep()
+        tasks = self._prep()
         bufs = self._buffers(B, T, training)
         drop = self._dropout(training)
         c = self.cfg
+        # initial state into slot 0 of the sequence buffers, hand-off counters zeroed: all in
+        # the same prep launch as the weight layouts
+        for layer in range(self.L):
+            lb, st = bufs["layers"][layer], state[layer]
+            pairs = ([(st[0], lb.cbuf[0]), (st[1], lb.hbuf[0])] if self.cfg.model in ("lstm", "nas")
+                     else [(st[0], lb.hbuf[0])] + ([(st[0], lb.h32[0])] if lb.h32 is not None else []))
+            for src, dst in pairs:
+                if src.dtype == f32 and src.dim() == 2 and src.stride(1) == 1:
+                    tasks.append((src, dst, 0))
+                else:
+                    dst.copy_(src)
+        if bufs["persist"]:
+            tasks.append((bufs["cnt"], bufs["cnt"], 2))
+        self._run_prep(tasks)
         x_prev = None  # bf16 [T, B, H] input for the next layer
         for layer in range(self.L):
             lw, lb = self._w[layer], bufs["layers"][layer]
-            st = state[layer]
-            if self.cfg.model in ("lstm", "nas"):
-                lb.cbuf[0].copy_(st[0])
-                lb.hbuf[0].copy_(st[1])
-            else:
-                lb.hbuf[0].copy_(st[0])
-                if lb.h32 is not None:
-                    lb.h32[0].copy_(st[0])
             gather = (layer == 0 and not drop and self.cfg.model != "nas")
             ids_arg = None
             # the forward never has a concurrent kernel (the previous step's all-reduce is joined
@@ -383,8 +415,9 @@ class NativeBackend:
             if xfuse:
                 lb.x_in = x_prev.reshape(N, H)
                 self.ops.lstm_persist_fwd(lw.WhT, lw.bias, None, lb.hbuf, lb.cbuf, lb.gates,
-                                          lb.hlast32, bufs["cnt"], self.err, FORGET_BIAS,
-                                          self.spin_limit, None, None, lw.WxT, x_prev, lw.bias)
+                                          lb.hlast32, bufs["cnt"][layer], self.err, FORGET_BIAS,
+                                          self.spin_limit, None, None, lw.WxT, x_prev, lw.bias,
+                                          cnt_zeroed=True)
                 x_prev = lb.hbuf[1:]
                 continue
             if gather:
@@ -406,9 +439,10 @@ class NativeBackend:
                 zx = lb.zx
             if bufs["persist"]:
                 self.ops.lstm_persist_fwd(lw.WhT, zx, ids_arg, lb.hbuf, lb.cbuf, lb.gates,
-                                          lb.hlast32, bufs["cnt"], self.err, FORGET_BIAS,
+                                          lb.hlast32, bufs["cnt"][layer], self.err, FORGET_BIAS,
                                           self.spin_limit,
-                                          bufs["ring"] if self.handoff == "granule" else None)
+                                          bufs["ring"] if self.handoff == "granule" else None,
+                                          cnt_zeroed=True)
             else:
                 self.ops.rnn_fwd_seq(self.cell, lw.WhT, lw.WT2, zx, ids_arg, lb.hbuf, lb.h32,
                                      lb.cbuf, lb.gates, lb.pre, lb.aux, lb.rh, lb.hlast32,
@@ -489,13 +523,14 @@ class NativeBackend:
                 if dtop is None:  # dtop of this layer is fused: dZ_above · W_x,aboveᵀ in-kernel
                     above = (self._w[layer + 1].Wx, bufs["layers"][layer + 1].dz)
                 self.ops.lstm_persist_bwd(lw.Wh, dtop if dtop is not None else bufs["dtop"],
-                                          lb.dz, lb.gates, lb.cbuf, bufs["cnt"],
+                                          lb.dz, lb.gates, lb.cbuf, bufs["cnt"][self.L + layer],
                                           self.err, self.spin_limit, bufs["db_part"][layer],
                                           ids_tm if fused_dew else None,
                                           bufs["dew_part"] if fused_dew else None, V, None,
                                           above[0] if above else None,
                                           above[1] if above else None,
-                                          exclusive=bufs["bwd_excl"] and above is None)
+                                          exclusive=bufs["bwd_excl"] and above is None,
+                                          cnt_zeroed=True)
                 if layer == 0 and pending:
                     # the last persistent grid is queued: buckets may now run beside the
                     # (non-persistent) layer-0 weight GEMMs
