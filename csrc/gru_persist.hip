@@ -1,0 +1,396 @@
+// Persistent, weights-resident GRU recurrence (forward and BPTT) for gfx950 -- the "GRU 3-gate
+// fused-GEMM path" of BASELINE.json's 3-layer GRU-1024 config.
+//
+// Reference semantics: TF 1.8 GRUCell as wired by model.py:15-25 (cell_fn = GRUCell):
+//   [r, u] = sigmoid([x, h_{t-1}]·W_g + b_g)                 (gates/gates kernel+bias)
+//   c~     = tanh([x, r ⊙ h_{t-1}]·W_c + b_c)                (candidate/candidate kernel+bias)
+//   h_t    = u ⊙ h_{t-1} + (1 - u) ⊙ c~
+// The reset gate multiplies h BEFORE the candidate matmul, so every step has two dependent
+// all-units exchanges: r⊙h_{t-1} after phase A and h_t after phase B.  The per-step kernels
+// (rnn_step.hip, CELL_GRU_A/B) paid two launches per step and re-read W_h from L2 each time;
+// here one launch runs the whole sequence of one layer, with the recurrent weight slices
+// resident in VGPRs as MFMA A fragments and the two exchanges done in-kernel with the same
+// placement-independent hand-off as the LSTM (persist_common.h, Guideline 16 row 1).
+//
+// Work split (swapped-operand mfma_f32_16x16x32_bf16, as lstm_persist.hip): workgroup (ubk, bg)
+// owns UB*16 hidden units x 16 batch rows; its 4 waves split K in quarters and keep
+//   fwd: W_gᵀ rows (r and u gates of its units, K = H) and W_cᵀ rows (K = H)
+//   bwd: W_c rows (d(r⊙h) = dZc·W_cᵀ, K = H) and W_g rows (dh = dZg·W_gᵀ, K = 2H)
+// Wave w < UB runs the cell epilogue of unit block w with h_{t-1} / the dh carry in registers.
+// Counters: two sets per launch (phase A and phase B), one per (batch group, step, K quarter).
+#include "common.h"
+#include "kernels.h"
+#include "persist_common.h"
+
+namespace dcr {
+
+// ------------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------------
+template <int KS, int UB>
+__global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs a) {
+  // single-buffered partials: every write of partA (partB) is separated from the previous
+  // epilogue read by the phase-B (next phase-A) barrier, which the epilogue wave joins last
+  __shared__ __attribute__((aligned(16))) float partA[4][UB][64][8];
+  __shared__ __attribute__((aligned(16))) float partB[4][UB][64][4];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int H = a.H, B = a.B, T = a.T;
+  const int nwg_u = H / (16 * UB);
+  int ubk, bg;
+  map_block(blockIdx.x, nwg_u, B / 16, ubk, bg);
+  const int ub0 = ubk * 16 * UB, b0 = bg * 16;
+  const int kq = 8 * (lane >> 4);
+  const int kbase = w * (KS * 32);
+  const size_t cset = (size_t)(B / 16) * (T + 1) * 4;
+  unsigned* cntH = a.cnt + (size_t)bg * (T + 1) * 4;         // slot t: h_t published
+  unsigned* cntR = a.cnt + cset + (size_t)bg * (T + 1) * 4;  // slot t: r⊙h_{t-1} published
+  const unsigned quarter_target = (unsigned)(H / 64);
+  bool dead = false;
+
+  bf16x8 wg[UB][2][KS], wc[UB][KS];
+#pragma unroll
+  for (int ui = 0; ui < UB; ++ui)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int row = ub0 + ui * 16 + (lane & 15);
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+        wg[ui][g][s] = ld8(a.WgT + (size_t)(g * H + row) * H + kbase + s * 32 + kq);
+      wc[ui][s] = ld8(a.WcT + (size_t)row * H + kbase + s * 32 + kq);
+    }
+
+  const int b = b0 + (lane & 15);
+  const unsigned hoff = (unsigned)(((size_t)b * H + kbase + kq) * sizeof(bf16));
+  const bool epi = w < UB;
+  const int u0 = ub0 + (epi ? w : 0) * 16 + 4 * (lane >> 4);
+  const size_t bh = (size_t)b * H + u0;
+  const int G3 = 3 * H;
+  float hp[4] = {0.f, 0.f, 0.f, 0.f};
+  if (epi) ld4f(a.h32 + bh, hp);  // h_0, fp32
+
+  for (int t = 0; t < T; ++t) {
+    float zx[3][4];
+    if (epi) {
+      const float* zrow = a.ids ? a.zx + (size_t)a.ids[(size_t)t * B + b] * a.zx_ld
+                                : a.zx + ((size_t)t * B + b) * a.zx_ld;
+#pragma unroll
+      for (int g = 0; g < 3; ++g) ld4f(zrow + (size_t)g * H + u0, zx[g]);
+    }
+    // ---- phase A: [r, u] from h_{t-1}
+    if (t > 0) {
+      if (threadIdx.x == 0 && !dead)
+        dead = !poll_quarters(cntH + (size_t)t * 4, quarter_target, a.spin_limit, a.err, 5u);
+      __syncthreads();
+    }
+    {
+      const __amdgpu_buffer_rsrc_t src =
+          make_rsrc(a.hbuf + (size_t)t * B * H, sizeof(bf16) * (size_t)B * H);
+      bf16x8 hf[KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) hf[s] = ld8_sc1(src, hoff + s * 64);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ui = 0; ui < UB; ++ui) {
+        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int g = 0; g < 2; ++g) acc[g] = mfma16(wg[ui][g][s], hf[s], acc[g]);
+        float4* dst = reinterpret_cast<float4*>(&partA[w][ui][lane][0]);
+        dst[0] = make_float4(acc[0][0], acc[0][1], acc[0][2], acc[0][3]);
+        dst[1] = make_float4(acc[1][0], acc[1][1], acc[1][2], acc[1][3]);
+      }
+    }
+    __syncthreads();
+    float uu[4];
+    if (epi) {
+      float rr[4];
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const float4 s0 = reinterpret_cast<const float4*>(&partA[0][w][lane][0])[g];
+        const float4 s1 = reinterpret_cast<const float4*>(&partA[1][w][lane][0])[g];
+        const float4 s2 = reinterpret_cast<const float4*>(&partA[2][w][lane][0])[g];
+        const float4 s3 = reinterpret_cast<const float4*>(&partA[3][w][lane][0])[g];
+        float* o = g == 0 ? rr : uu;
+        o[0] = sigmoidf_(s0.x + s1.x + s2.x + s3.x + zx[g][0]);
+        o[1] = sigmoidf_(s0.y + s1.y + s2.y + s3.y + zx[g][1]);
+        o[2] = sigmoidf_(s0.z + s1.z + s2.z + s3.z + zx[g][2]);
+        o[3] = sigmoidf_(s0.w + s1.w + s2.w + s3.w + zx[g][3]);
+      }
+      st4bf_sc1(a.rh + (size_t)t * B * H + bh, rr[0] * hp[0], rr[1] * hp[1], rr[2] * hp[2],
+                rr[3] * hp[3]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0)
+        __hip_atomic_fetch_add(cntR + (size_t)t * 4 + (u0 / (H / 4)), 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      bf16* gp = a.gates + ((size_t)t * B + b) * G3 + u0;
+      st4bf(gp, rr[0], rr[1], rr[2], rr[3]);
+      st4bf(gp + H, uu[0], uu[1], uu[2], uu[3]);
+    }
+    // ---- phase B: c~ from r⊙h_{t-1}
+    if (threadIdx.x == 0 && !dead)
+      dead = !poll_quarters(cntR + (size_t)t * 4, quarter_target, a.spin_limit, a.err, 6u);
+    __syncthreads();
+    {
+      const __amdgpu_buffer_rsrc_t src =
+          make_rsrc(a.rh + (size_t)t * B * H, sizeof(bf16) * (size_t)B * H);
+      bf16x8 rf[KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) rf[s] = ld8_sc1(src, hoff + s * 64);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ui = 0; ui < UB; ++ui) {
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) acc = mfma16(wc[ui][s], rf[s], acc);
+        *reinterpret_cast<float4*>(&partB[w][ui][lane][0]) =
+            make_float4(acc[0], acc[1], acc[2], acc[3]);
+      }
+    }
+    __syncthreads();
+    if (epi) {
+      const float4 s0 = *reinterpret_cast<const float4*>(&partB[0][w][lane][0]);
+      const float4 s1 = *reinterpret_cast<const float4*>(&partB[1][w][lane][0]);
+      const float4 s2 = *reinterpret_cast<const float4*>(&partB[2][w][lane][0]);
+      const float4 s3 = *reinterpret_cast<const float4*>(&partB[3][w][lane][0]);
+      float cc[4], h[4];
+      cc[0] = tanhf_(s0.x + s1.x + s2.x + s3.x + zx[2][0]);
+      cc[1] = tanhf_(s0.y + s1.y + s2.y + s3.y + zx[2][1]);
+      cc[2] = tanhf_(s0.z + s1.z + s2.z + s3.z + zx[2][2]);
+      cc[3] = tanhf_(s0.w + s1.w + s2.w + s3.w + zx[2][3]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h[r] = uu[r] * hp[r] + (1.f - uu[r]) * cc[r];
+      const size_t o = (size_t)(t + 1) * B * H + bh;
+      st4bf_sc1(a.hbuf + o, h[0], h[1], h[2], h[3]);
+      if (t + 1 < T) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+          __hip_atomic_fetch_add(cntH + (size_t)(t + 1) * 4 + (u0 / (H / 4)), 1u,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      *reinterpret_cast<float4*>(a.h32 + o) = make_float4(h[0], h[1], h[2], h[3]);
+      st4bf(a.gates + ((size_t)t * B + b) * G3 + 2 * H + u0, cc[0], cc[1], cc[2], cc[3]);
+      if (t == T - 1 && a.hlast32)
+        *reinterpret_cast<float4*>(a.hlast32 + bh) = make_float4(h[0], h[1], h[2], h[3]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hp[r] = h[r];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// backward (BPTT); same recurrences as rnn_step.hip's CELL_GRU_A / CELL_GRU_B steps:
+//   phase A (step t):   d(r⊙h) = dZc_t · W_cᵀ;  dZr_t, dZu_t;  P = dh'_t·u + d(r⊙h)·r
+//   phase B (t -> t-1): dh'_{t-1} = dtop_{t-1} + P + dZg_t · W_gᵀ;  dZc_{t-1}
+// dh' and P never leave the epilogue lane's registers.
+// ------------------------------------------------------------------------------------------
+template <int KA, int UB>
+__global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs a) {
+  constexpr int KB = 2 * KA;  // phase B reduces over K = 2H
+  __shared__ __attribute__((aligned(16))) float partA[4][UB][64][4];
+  __shared__ __attribute__((aligned(16))) float partB[4][UB][64][4];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int H = a.H, B = a.B, T = a.T;
+  const int nwg_u = H / (16 * UB);
+  int ubk, bg;
+  map_block(blockIdx.x, nwg_u, B / 16, ubk, bg);
+  const int ub0 = ubk * 16 * UB, b0 = bg * 16;
+  const int kq = 8 * (lane >> 4);
+  const int kA = w * (KA * 32), kB = w * (KB * 32);
+  const size_t cset = (size_t)(B / 16) * (T + 1) * 4;
+  unsigned* cntC = a.cnt + (size_t)bg * (T + 1) * 4;         // slot t: dZc_t published
+  unsigned* cntG = a.cnt + cset + (size_t)bg * (T + 1) * 4;  // slot t: dZg_t published
+  const unsigned quarter_target = (unsigned)(H / 64);
+  const int G3 = 3 * H;
+  bool dead = false;
+
+  bf16x8 wc[UB][KA], wg[UB][KB];
+#pragma unroll
+  for (int ui = 0; ui < UB; ++ui) {
+    const int row = ub0 + ui * 16 + (lane & 15);
+#pragma unroll
+    for (int s = 0; s < KA; ++s) wc[ui][s] = ld8(a.Wc + (size_t)row * H + kA + s * 32 + kq);
+#pragma unroll
+    for (int s = 0; s < KB; ++s) wg[ui][s] = ld8(a.Wg + (size_t)row * 2 * H + kB + s * 32 + kq);
+  }
+
+  const int b = b0 + (lane & 15);
+  const bool epi = w < UB;
+  const int u0 = ub0 + (epi ? w : 0) * 16 + 4 * (lane >> 4);
+  const size_t bh = (size_t)b * H + u0;
+  const unsigned offA = (unsigned)(((size_t)b * G3 + 2 * H + kA + kq) * sizeof(bf16));
+  const unsigned offB = (unsigned)(((size_t)b * G3 + kB + kq) * sizeof(bf16));
+  float dhp[4] = {0.f, 0.f, 0.f, 0.f};
+
+  // dZc_{T-1} from the top gradient alone
+  if (epi) {
+    float uu[4], cc[4];
+    ld4f(a.dtop + (size_t)(T - 1) * B * H + bh, dhp);
+    const bf16* gp = a.gates + ((size_t)(T - 1) * B + b) * G3 + u0;
+    ld4bf(gp + H, uu);
+    ld4bf(gp + 2 * H, cc);
+    st4bf_sc1(a.dz + ((size_t)(T - 1) * B + b) * G3 + 2 * H + u0,
+              dhp[0] * (1.f - uu[0]) * (1.f - cc[0] * cc[0]),
+              dhp[1] * (1.f - uu[1]) * (1.f - cc[1] * cc[1]),
+              dhp[2] * (1.f - uu[2]) * (1.f - cc[2] * cc[2]),
+              dhp[3] * (1.f - uu[3]) * (1.f - cc[3] * cc[3]));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0)
+      __hip_atomic_fetch_add(cntC + (size_t)(T - 1) * 4 + (u0 / (H / 4)), 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  }
+
+  for (int t = T - 1; t >= 0; --t) {
+    // recurrence-independent epilogue operands, issued before the waits
+    float rr[4], uu[4], cc[4], hp[4], dt[4], up[4], cp[4];
+    if (epi) {
+      const bf16* gp = a.gates + ((size_t)t * B + b) * G3 + u0;
+      ld4bf(gp, rr); ld4bf(gp + H, uu); ld4bf(gp + 2 * H, cc);
+      ld4f(a.h32 + (size_t)t * B * H + bh, hp);
+      if (t > 0) {
+        ld4f(a.dtop + (size_t)(t - 1) * B * H + bh, dt);
+        const bf16* gq = a.gates + ((size_t)(t - 1) * B + b) * G3 + u0;
+        ld4bf(gq + H, up); ld4bf(gq + 2 * H, cp);
+      }
+    }
+    const __amdgpu_buffer_rsrc_t zsrc =
+        make_rsrc(a.dz + (size_t)t * B * G3, sizeof(bf16) * (size_t)B * G3);
+    // ---- phase A: d(r⊙h_{t-1}) = dZc_t · W_cᵀ
+    if (threadIdx.x == 0 && !dead)
+      dead = !poll_quarters(cntC + (size_t)t * 4, quarter_target, a.spin_limit, a.err, 7u);
+    __syncthreads();
+    {
+      bf16x8 zf[KA];
+#pragma unroll
+      for (int s = 0; s < KA; ++s) zf[s] = ld8_sc1(zsrc, offA + s * 64);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ui = 0; ui < UB; ++ui) {
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KA; ++s) acc = mfma16(wc[ui][s], zf[s], acc);
+        *reinterpret_cast<float4*>(&partA[w][ui][lane][0]) =
+            make_float4(acc[0], acc[1], acc[2], acc[3]);
+      }
+    }
+    __syncthreads();
+    float P[4];
+    if (epi) {
+      const float4 s0 = *reinterpret_cast<const float4*>(&partA[0][w][lane][0]);
+      const float4 s1 = *reinterpret_cast<const float4*>(&partA[1][w][lane][0]);
+      const float4 s2 = *reinterpret_cast<const float4*>(&partA[2][w][lane][0]);
+      const float4 s3 = *reinterpret_cast<const float4*>(&partA[3][w][lane][0]);
+      const float drh[4] = {s0.x + s1.x + s2.x + s3.x, s0.y + s1.y + s2.y + s3.y,
+                            s0.z + s1.z + s2.z + s3.z, s0.w + s1.w + s2.w + s3.w};
+      float dzr[4], dzu[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float du = dhp[r] * (hp[r] - cc[r]);
+        dzu[r] = du * uu[r] * (1.f - uu[r]);
+        dzr[r] = drh[r] * hp[r] * rr[r] * (1.f - rr[r]);
+        P[r] = dhp[r] * uu[r] + drh[r] * rr[r];
+      }
+      bf16* dz = a.dz + ((size_t)t * B + b) * G3 + u0;
+      st4bf_sc1(dz, dzr[0], dzr[1], dzr[2], dzr[3]);
+      st4bf_sc1(dz + H, dzu[0], dzu[1], dzu[2], dzu[3]);
+      if (t > 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+          __hip_atomic_fetch_add(cntG + (size_t)t * 4 + (u0 / (H / 4)), 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (t == 0) break;  // dh'_{-1} (the initial state's gradient) is not needed
+    // ---- phase B: dh'_{t-1} = dtop_{t-1} + P + dZg_t · W_gᵀ
+    if (threadIdx.x == 0 && !dead)
+      dead = !poll_quarters(cntG + (size_t)t * 4, quarter_target, a.spin_limit, a.err, 8u);
+    __syncthreads();
+    {
+      bf16x8 zf[KB];
+#pragma unroll
+      for (int s = 0; s < KB; ++s) zf[s] = ld8_sc1(zsrc, offB + s * 64);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ui = 0; ui < UB; ++ui) {
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KB; ++s) acc = mfma16(wg[ui][s], zf[s], acc);
+        *reinterpret_cast<float4*>(&partB[w][ui][lane][0]) =
+            make_float4(acc[0], acc[1], acc[2], acc[3]);
+      }
+    }
+    __syncthreads();
+    if (epi) {
+      const float4 s0 = *reinterpret_cast<const float4*>(&partB[0][w][lane][0]);
+      const float4 s1 = *reinterpret_cast<const float4*>(&partB[1][w][lane][0]);
+      const float4 s2 = *reinterpret_cast<const float4*>(&partB[2][w][lane][0]);
+      const float4 s3 = *reinterpret_cast<const float4*>(&partB[3][w][lane][0]);
+      dhp[0] = dt[0] + P[0] + s0.x + s1.x + s2.x + s3.x;
+      dhp[1] = dt[1] + P[1] + s0.y + s1.y + s2.y + s3.y;
+      dhp[2] = dt[2] + P[2] + s0.z + s1.z + s2.z + s3.z;
+      dhp[3] = dt[3] + P[3] + s0.w + s1.w + s2.w + s3.w;
+      float dzc[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dzc[r] = dhp[r] * (1.f - up[r]) * (1.f - cp[r] * cp[r]);
+      st4bf_sc1(a.dz + ((size_t)(t - 1) * B + b) * G3 + 2 * H + u0, dzc[0], dzc[1], dzc[2],
+                dzc[3]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0)
+        __hip_atomic_fetch_add(cntC + (size_t)(t - 1) * 4 + (u0 / (H / 4)), 1u,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+template <int K, int U>
+static const void* gru_fn(int bwd) {
+  return bwd ? (const void*)gru_bwd_persist_kernel<K, U> : (const void*)gru_fwd_persist_kernel<K, U>;
+}
+
+static const void* gru_pick(int bwd, int H, int ub) {
+  const int ks = H / 128;
+#define GP(K, U) \
+  if (ks == K && ub == U) return gru_fn<K, U>(bwd);
+  GP(1, 1) GP(2, 1) GP(3, 1) GP(4, 1) GP(6, 1) GP(8, 1)
+  GP(1, 2) GP(2, 2) GP(3, 2) GP(4, 2) GP(6, 2) GP(8, 2)
+#undef GP
+  return nullptr;
+}
+
+static int gru_grid(int H, int B, int ub) { return (H / (16 * ub)) * (B / 16); }
+
+// Largest unit block (32 then 16 units per workgroup) whose forward AND backward grids can be
+// co-resident with the GPU to themselves; 0 = not supported (per-step kernels instead).
+int gru_persist_ub(int H, int B, int cus) {
+  if (H % 128 != 0 || H < 128 || H > 1024 || B % 16 != 0 || B < 16 || cus <= 0) return 0;
+  for (int ub = 2; ub >= 1; --ub) {
+    bool ok = true;
+    for (int bwd = 0; bwd < 2 && ok; ++bwd) {
+      const void* fn = gru_pick(bwd, H, ub);
+      int occ = 0;
+      ok = fn && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 256, 0) == hipSuccess &&
+           gru_grid(H, B, ub) <= occ * cus;
+    }
+    if (ok) return ub;
+  }
+  return 0;
+}
+
+int launch_gru_persist(int bwd, const GruPersistArgs& a, int cus, hipStream_t s) {
+  const int ub = gru_persist_ub(a.H, a.B, cus);
+  if (!ub) return -2;
+  const void* fn = gru_pick(bwd, a.H, ub);
+  if (!fn) return -1;
+  if (!a.cnt_zeroed)
+    (void)hipMemsetAsync(a.cnt, 0, sizeof(unsigned) * 2 * (size_t)(a.B / 16) * (a.T + 1) * 4, s);
+  void* args[] = {const_cast<GruPersistArgs*>(&a)};
+  return hipLaunchKernel(fn, dim3(gru_grid(a.H, a.B, ub)), dim3(256), args, 0, s) == hipSuccess
+             ? 0 : -3;
+}
+
+}  // namespace dcr

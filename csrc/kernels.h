@@ -119,6 +119,31 @@ int lstm_persist_occupancy(int bwd, int H, int B, int V, int flags, int cus);
 int launch_lstm_fwd_persist(const PersistArgs& a, int cus, hipStream_t s);
 int launch_lstm_bwd_persist(const PersistArgs& a, int cus, hipStream_t s);
 
+// persistent GRU recurrence (gru_persist.hip)
+struct GruPersistArgs {
+  const bf16* WgT;      // fwd: W_g,hᵀ [2H, H] (r rows, then u rows)
+  const bf16* WcT;      // fwd: W_c,hᵀ [H, H]
+  const float* zx;      // fwd: [T, B, zx_ld] input projections (+bias) or [V, zx_ld] table
+  const int* ids;       // fwd gather mode: [T, B]
+  int zx_ld;            // 3H
+  bf16* hbuf;           // [T+1, B, H] bf16 (slot 0 = h_0)
+  float* h32;           // [T+1, B, H] fp32 (slot 0 = h_0)
+  bf16* rh;             // fwd: [T, B, H] r ⊙ h_{t-1}
+  bf16* gates;          // [T, B, 3H] r, u, c~
+  float* hlast32;       // fwd: [B, H] (optional)
+  const bf16* Wg;       // bwd: W_g,h [H, 2H] (TF layout)
+  const bf16* Wc;       // bwd: W_c,h [H, H]
+  const float* dtop;    // bwd: [T, B, H]
+  bf16* dz;             // bwd: [T, B, 3H] dZr, dZu, dZc
+  unsigned* cnt;        // 2 sets x [B/16, T+1, 4] counters
+  unsigned* err;
+  int B, H, T;
+  unsigned spin_limit;
+  int cnt_zeroed;
+};
+int gru_persist_ub(int H, int B, int cus);
+int launch_gru_persist(int bwd, const GruPersistArgs& a, int cus, hipStream_t s);
+
 // fused softmax head (head.hip)
 struct HeadArgs {
   const bf16* O;        // [N, ldo] bf16 top-layer outputs

@@ -27,96 +27,10 @@
 // otherwise falls back to the per-step kernels.
 #include "common.h"
 #include "kernels.h"
+#include "persist_common.h"
 #include <stdlib.h>
 
 namespace dcr {
-
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-constexpr int kAuxSc1 = 16;  // buffer-op cache-policy bits: sc1 (bypass L1, write-through)
-#ifndef XCD_GROUPING
-#define XCD_GROUPING 1
-#endif
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, size_t bytes) {
-  const unsigned n = bytes > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (unsigned)bytes;
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, n, 0x00020000);
-}
-__device__ __forceinline__ bf16x8 ld8_sc1(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
-  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, kAuxSc1);
-  return __builtin_bit_cast(bf16x8, v);
-}
-__device__ __forceinline__ void st4bf_sc1(bf16* p, float a, float b, float c, float d) {
-  bf16x4 v;
-  v[0] = f2bf(a); v[1] = f2bf(b); v[2] = f2bf(c); v[3] = f2bf(d);
-  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), __builtin_bit_cast(uint64_t, v),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st4bf(bf16* p, float a, float b, float c, float d) {
-  bf16x4 v;
-  v[0] = f2bf(a); v[1] = f2bf(b); v[2] = f2bf(c); v[3] = f2bf(d);
-  *reinterpret_cast<bf16x4*>(p) = v;
-}
-__device__ __forceinline__ void ld4bf(const bf16* p, float (&o)[4]) {
-  const bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
-  o[0] = (float)v[0]; o[1] = (float)v[1]; o[2] = (float)v[2]; o[3] = (float)v[3];
-}
-__device__ __forceinline__ void ld4f(const float* p, float (&o)[4]) {
-  const float4 v = *reinterpret_cast<const float4*>(p);
-  o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
-}
-
-// One lane of the workgroup polls `*cnt >= target` (relaxed agent-scope = sc1 loads); the
-// result is broadcast through LDS by the barrier that follows.  Returns false on timeout.
-__device__ __forceinline__ bool poll_counter(unsigned* cnt, unsigned target, unsigned limit,
-                                             unsigned* err, unsigned code) {
-  unsigned spins = 0;
-  while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-    if (++spins > limit) {
-      __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  return true;
-}
-
-// Poll the 4 per-quarter counters of one step (one 16-B sc1 load) until all reach `target`.
-__device__ __forceinline__ bool poll_quarters(unsigned* cnt4, unsigned target, unsigned limit,
-                                              unsigned* err, unsigned code) {
-  const __amdgpu_buffer_rsrc_t r = make_rsrc(cnt4, 16);
-  unsigned spins = 0;
-  for (;;) {
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, kAuxSc1);
-    if (v[0] >= target && v[1] >= target && v[2] >= target && v[3] >= target) return true;
-    if (++spins > limit) {
-      __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-// Block -> (unit block, batch group).  Speed only: place the unit-block workgroups of one batch
-// group on the same XCD under the observed round-robin dispatch (blocks b, b+8, ... share an
-// XCD; MI355X_MICROARCH.md "Workgroup dispatch"), so the batch group's hand-off payload is
-// fetched into one L2 and served to all its consumers from there.  Correctness never depends
-// on it: every hand-off is sc1 + counters regardless of placement.
-__device__ __forceinline__ void map_block(int bid, int nwg_u, int nbg, int& ubk, int& bg) {
-  if (nbg % 8 == 0 && XCD_GROUPING) {
-    const int xcd = bid % 8, j = bid / 8;  // j in [0, nwg_u * nbg / 8)
-    bg = xcd + 8 * (j / nwg_u);
-    ubk = j % nwg_u;
-  } else {
-    ubk = bid % nwg_u;
-    bg = bid / nwg_u;
-  }
-}
-
-__device__ __forceinline__ void arrive(unsigned* cnt) {
-  // every store of this wave must be complete (write-through) before the counter moves
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // ------------------------------------------------------------------------------------------
 // forward

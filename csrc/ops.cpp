@@ -453,6 +453,88 @@ void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& d
 }
 
 // ------------------------------------------------------------------------------------------
+// persistent GRU recurrence (gru_persist.hip)
+// ------------------------------------------------------------------------------------------
+static void gru_common(dcr::GruPersistArgs& a, const at::Tensor& gates, const at::Tensor& h32,
+                       at::Tensor& cnt, at::Tensor& err, int64_t spin_limit, bool cnt_zeroed,
+                       int T, int B, int H) {
+  check_seq(gates, at::kBFloat16, "gates");
+  check_seq(h32, at::kFloat, "h32");
+  TORCH_CHECK(gates.numel() == (int64_t)T * B * 3 * H, "gates must be [T, B, 3H]");
+  TORCH_CHECK(h32.numel() == (int64_t)(T + 1) * B * H, "h32 must be [T+1, B, H]");
+  TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == at::kInt && err.scalar_type() == at::kInt,
+              "cnt/err must be int32 GPU tensors");
+  TORCH_CHECK(cnt.numel() >= (int64_t)2 * (B / 16) * (T + 1) * 4, "counter buffer too small");
+  TORCH_CHECK(dcr::gru_persist_ub(H, B, num_cus()) > 0, "persistent GRU unsupported for H=", H,
+              " B=", B, " (grid cannot be co-resident)");
+  a.gates = ptr<bf16>(gates);
+  a.h32 = ptr<float>(h32);
+  a.cnt = reinterpret_cast<unsigned*>(cnt.data_ptr());
+  a.err = reinterpret_cast<unsigned*>(err.data_ptr());
+  a.B = B; a.H = H; a.T = T;
+  a.spin_limit = (unsigned)spin_limit;
+  a.cnt_zeroed = cnt_zeroed ? 1 : 0;
+}
+
+void gru_persist_fwd(const at::Tensor& WgT, const at::Tensor& WcT, const at::Tensor& zx,
+                     const c10::optional<at::Tensor>& ids, at::Tensor& hbuf, at::Tensor& h32,
+                     at::Tensor& rh, at::Tensor& gates, const c10::optional<at::Tensor>& hlast32,
+                     at::Tensor& cnt, at::Tensor& err, int64_t spin_limit, bool cnt_zeroed) {
+  check_seq(WgT, at::kBFloat16, "WgT");
+  check_seq(WcT, at::kBFloat16, "WcT");
+  check_seq(zx, at::kFloat, "zx");
+  check_seq(hbuf, at::kBFloat16, "hbuf");
+  check_seq(rh, at::kBFloat16, "rh");
+  check_opt(ids, at::kInt, "ids");
+  check_opt(hlast32, at::kFloat, "hlast32");
+  const int T = (int)hbuf.size(0) - 1, B = (int)hbuf.size(1), H = (int)hbuf.size(2);
+  TORCH_CHECK(WgT.size(0) == 2 * H && WgT.size(1) == H, "WgT must be [2H, H]");
+  TORCH_CHECK(WcT.size(0) == H && WcT.size(1) == H, "WcT must be [H, H]");
+  TORCH_CHECK(zx.size(-1) == 3 * H, "zx rows must be 3H wide");
+  if (has(ids)) {
+    TORCH_CHECK(ids->numel() == (int64_t)T * B, "ids must be [T, B]");
+  } else {
+    TORCH_CHECK(zx.numel() == (int64_t)T * B * 3 * H, "zx must be [T, B, 3H]");
+  }
+  TORCH_CHECK(rh.numel() == (int64_t)T * B * H, "rh must be [T, B, H]");
+  if (has(hlast32)) TORCH_CHECK(hlast32->numel() == (int64_t)B * H, "hlast32 must be [B, H]");
+  dcr::GruPersistArgs a{};
+  gru_common(a, gates, h32, cnt, err, spin_limit, cnt_zeroed, T, B, H);
+  a.WgT = ptr<bf16>(WgT);
+  a.WcT = ptr<bf16>(WcT);
+  a.zx = ptr<float>(zx);
+  a.ids = optr<int>(ids);
+  a.zx_ld = 3 * H;
+  a.hbuf = ptr<bf16>(hbuf);
+  a.rh = ptr<bf16>(rh);
+  a.hlast32 = optr<float>(hlast32);
+  const int rc = dcr::launch_gru_persist(0, a, num_cus(), cur_stream());
+  TORCH_CHECK(rc == 0, "persistent GRU forward not launched (", rc, ")");
+}
+
+void gru_persist_bwd(const at::Tensor& Wg, const at::Tensor& Wc, const at::Tensor& dtop,
+                     at::Tensor& dz, const at::Tensor& gates, const at::Tensor& h32,
+                     at::Tensor& cnt, at::Tensor& err, int64_t spin_limit, bool cnt_zeroed) {
+  check_seq(Wg, at::kBFloat16, "Wg");
+  check_seq(Wc, at::kBFloat16, "Wc");
+  check_seq(dtop, at::kFloat, "dtop");
+  check_seq(dz, at::kBFloat16, "dz");
+  TORCH_CHECK(dtop.dim() == 3, "dtop must be [T, B, H]");
+  const int T = (int)dtop.size(0), B = (int)dtop.size(1), H = (int)dtop.size(2);
+  TORCH_CHECK(Wg.size(0) == H && Wg.size(1) == 2 * H, "Wg must be [H, 2H]");
+  TORCH_CHECK(Wc.size(0) == H && Wc.size(1) == H, "Wc must be [H, H]");
+  TORCH_CHECK(dz.numel() == (int64_t)T * B * 3 * H, "dz must be [T, B, 3H]");
+  dcr::GruPersistArgs a{};
+  gru_common(a, gates, h32, cnt, err, spin_limit, cnt_zeroed, T, B, H);
+  a.Wg = ptr<bf16>(Wg);
+  a.Wc = ptr<bf16>(Wc);
+  a.dtop = ptr<float>(dtop);
+  a.dz = ptr<bf16>(dz);
+  const int rc = dcr::launch_gru_persist(1, a, num_cus(), cur_stream());
+  TORCH_CHECK(rc == 0, "persistent GRU BPTT not launched (", rc, ")");
+}
+
+// ------------------------------------------------------------------------------------------
 // fused softmax head (head.hip)
 // ------------------------------------------------------------------------------------------
 void head(const at::Tensor& O, const at::Tensor& WsT, const c10::optional<at::Tensor>& Wsk,
@@ -613,6 +695,16 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor(a!)? logits, Tensor(b!)? row_loss, Tensor(c!)? dlogits, Tensor(d!)? dtop, "
       "Tensor(e!)? db, Tensor(f!) part, Tensor(g!)? loss) -> ()");
   m.def("prep(Tensor[] src, Tensor(a!)[] dst, int[] mode) -> ()");
+  m.def("gru_persist_ub(int H, int B) -> int", [](int64_t H, int64_t B) -> int64_t {
+    return dcr::gru_persist_ub((int)H, (int)B, num_cus());
+  });
+  m.def(
+      "gru_persist_fwd(Tensor WgT, Tensor WcT, Tensor zx, Tensor? ids, Tensor(a!) hbuf, "
+      "Tensor(b!) h32, Tensor(c!) rh, Tensor(d!) gates, Tensor(e!)? hlast32, Tensor(f!) cnt, "
+      "Tensor(g!) err, int spin_limit, bool cnt_zeroed=False) -> ()");
+  m.def(
+      "gru_persist_bwd(Tensor Wg, Tensor Wc, Tensor dtop, Tensor(a!) dz, Tensor gates, "
+      "Tensor h32, Tensor(b!) cnt, Tensor(c!) err, int spin_limit, bool cnt_zeroed=False) -> ()");
   m.def("segsum(Tensor X, Tensor? ids, int V, Tensor(a!) out, Tensor(b!) workspace, bool accumulate) -> ()");
   m.def("segsum_workspace(int N, int W, int V) -> int", [](int64_t N, int64_t W, int64_t V) -> int64_t {
     return (int64_t)dcr::segsum_workspace_floats((int)N, (int)W, (int)V);
@@ -630,4 +722,6 @@ TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("lstm_persist_bwd", &lstm_persist_bwd);
   m.impl("head", &head);
   m.impl("prep", &prep);
+  m.impl("gru_persist_fwd", &gru_persist_fwd);
+  m.impl("gru_persist_bwd", &gru_persist_bwd);
 }

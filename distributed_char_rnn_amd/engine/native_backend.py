@@ -284,7 +284,8 @@ class NativeBackend:
                       if (training and self.V <= 128) else None),
             # one hand-off counter region per persistent launch (fwd layers, then bwd layers),
             # zeroed together by the step's prep launch
-            cnt=torch.zeros(2 * self.L, (B // 16 + 1) * (T + 1) * 4, dtype=torch.int32, device=dev),
+            cnt=torch.zeros(2 * self.L, 2 * (B // 16 + 1) * (T + 1) * 4, dtype=torch.int32,
+                            device=dev),
             ring=torch.zeros(2 * B * (H // 2), dtype=torch.int64, device=dev),
         )
         self._bufs[key] = bufs
@@ -329,8 +330,14 @@ class NativeBackend:
         all-reduce still overlaps the layer-0 weight GEMMs.  ``DCR_MODE=overlap|exclusive``
         forces a mode.
         """
-        plan = dict(persist=False, xfuse=False, mode="exclusive", bwd_excl=False)
+        plan = dict(persist=False, xfuse=False, mode="exclusive", bwd_excl=False,
+                    gru_persist=False)
         o = self.ops
+        if self.use_persist and self.cfg.model == "gru":
+            # persistent GRU (gru_persist.hip): the C++ side picks the unit block whose fwd and
+            # bwd grids are co-resident; always exclusive (nothing beside it)
+            plan["gru_persist"] = bool(o.gru_persist_ub(self.H, B))
+            return plan
         if not (self.use_persist and self.cfg.model == "lstm"
                 and bool(o.lstm_persist_supported(self.H, B))):
             return plan
@@ -400,7 +407,7 @@ class NativeBackend:
                     tasks.append((src, dst, 0))
                 else:
                     dst.copy_(src)
-        if bufs["persist"]:
+        if bufs["persist"] or bufs["gru_persist"]:
             tasks.append((bufs["cnt"], bufs["cnt"], 2))
         self._run_prep(tasks)
         x_prev = None  # bf16 [T, B, H] input for the next layer
@@ -443,6 +450,10 @@ class NativeBackend:
                                           self.spin_limit,
                                           bufs["ring"] if self.handoff == "granule" else None,
                                           cnt_zeroed=True)
+            elif bufs["gru_persist"]:
+                self.ops.gru_persist_fwd(lw.WhT, lw.WT2, zx, ids_arg, lb.hbuf, lb.h32, lb.rh,
+                                         lb.gates, None, bufs["cnt"][layer], self.err,
+                                         self.spin_limit, cnt_zeroed=True)
             else:
                 self.ops.rnn_fwd_seq(self.cell, lw.WhT, lw.WT2, zx, ids_arg, lb.hbuf, lb.h32,
                                      lb.cbuf, lb.gates, lb.pre, lb.aux, lb.rh, lb.hlast32,
@@ -495,7 +506,8 @@ class NativeBackend:
             self.ops.segsum(dlog, None, 1, bufs["colsum"][:, :V], bufs["ws"], False)
             s.gview("rnnlm/softmax_b").copy_(bufs["colsum"][0, :V])
             dtop = _mm_into(dlog, hd["Ws"].t(), bufs["dtop"].view(N, H)).view(T, B, H)
-        overlap = bufs["mode"] == "overlap" or not bufs["persist"]
+        persistent = bufs["persist"] or bufs["gru_persist"]
+        overlap = bufs["mode"] == "overlap" or not persistent
         pending = []
         if on_ready is not None and not overlap:
             # exclusive mode: nothing may run beside the persistent BPTT grids, so the gradient
@@ -534,6 +546,14 @@ class NativeBackend:
                 if layer == 0 and pending:
                     # the last persistent grid is queued: buckets may now run beside the
                     # (non-persistent) layer-0 weight GEMMs
+                    for off in pending:
+                        user_ready(off)
+                    pending.clear()
+            elif bufs["gru_persist"]:
+                self.ops.gru_persist_bwd(lw.W2, lw.Wh, dtop, lb.dz, lb.gates, lb.h32,
+                                         bufs["cnt"][self.L + layer], self.err, self.spin_limit,
+                                         cnt_zeroed=True)
+                if layer == 0 and pending:
                     for off in pending:
                         user_ready(off)
                     pending.clear()
@@ -630,7 +650,7 @@ class NativeBackend:
             user_ready(off)
         extras = {"logits": logits, "loss": bufs["row_loss"]} if want_extras else None
         self._steps += 1
-        if bufs["persist"] and self._steps % 200 == 1:
+        if persistent and self._steps % 200 == 1:
             self.check_errors()
         return bufs["loss"][0], new_state, extras
 
