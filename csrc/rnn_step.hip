@@ -24,6 +24,7 @@
 // LSTM kernels in lstm_persist.hip replace these for the flagship config.
 #include "common.h"
 #include "kernels.h"
+#include <stdlib.h>
 
 namespace dcr {
 
@@ -34,57 +35,70 @@ template <> struct CellG<CELL_GRU_B> { static constexpr int G = 1; };
 template <> struct CellG<CELL_RNN> { static constexpr int G = 1; };
 template <> struct CellG<CELL_NAS> { static constexpr int G = 8; };
 
-// Block-cooperative tile GEMM: acc[t] = sum_k A[arow_t][k] * Bm[brow][k] over k in [0, K).
-// The 4 waves of the workgroup take interleaved 32-wide k-steps (wave w: s = w, w+4, ...), keep
-// the next step's fragments in flight while the current MFMAs run, and meet in LDS; on return
-// wave 0 holds the full sums (other waves return garbage and must not use them).
-template <int NT>
+// Block-cooperative tile GEMM over NBT batch tiles:
+//   acc_j[t] = sum_k A[arow_t][k] * Bm[brow_j][k]   over k in [0, K), j < NBT.
+// The 4 waves take interleaved 32-wide k-steps (wave w: s = w, w+4, ...), keep the next step's
+// fragments in flight while the current MFMAs run, and meet in LDS; each A fragment feeds NBT
+// MFMAs, so a workgroup reads its weight slice once per NBT x 16 batch rows (the per-step
+// kernels are L2/MALL-bandwidth bound at large H).  On return wave w < NBT holds the full sums
+// of batch tile w; the other waves return garbage and must not use them.
+template <int NT, int NBT>
 __device__ __forceinline__ void tile_gemm(f32x4 (&acc)[NT], const bf16* __restrict__ A,
                                           const int (&arow)[NT], int lda,
-                                          const bf16* __restrict__ Bm, int brow, int ldb, int K,
-                                          int lane, int w, float* part /* [4][NT][64][4] */) {
+                                          const bf16* __restrict__ Bm, const int (&brow)[NBT],
+                                          int ldb, int K, int lane, int w,
+                                          float* part /* [4][NT][NBT][64][4] */) {
   const int kq = 8 * (lane >> 4);
-  const bf16* bp = Bm + (size_t)brow * ldb + kq;
+  const bf16* bp[NBT];
+#pragma unroll
+  for (int j = 0; j < NBT; ++j) bp[j] = Bm + (size_t)brow[j] * ldb + kq;
   const bf16* ap[NT];
+  f32x4 c[NT][NBT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     ap[t] = A + (size_t)arow[t] * lda + kq;
-    acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < NBT; ++j) c[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   const int KS = K / 32;
   int s = w;
   if (s < KS) {
-    bf16x8 b = ld8(bp + s * 32);
-    bf16x8 a[NT];
+    bf16x8 b[NBT], a[NT];
+#pragma unroll
+    for (int j = 0; j < NBT; ++j) b[j] = ld8(bp[j] + s * 32);
 #pragma unroll
     for (int t = 0; t < NT; ++t) a[t] = ld8(ap[t] + s * 32);
     for (; s < KS; s += 4) {
       const int sn = s + 4 < KS ? s + 4 : s;  // prefetch (re-load the last step when done)
-      const bf16x8 bn = ld8(bp + sn * 32);
-      bf16x8 an[NT];
+      bf16x8 bn[NBT], an[NT];
+#pragma unroll
+      for (int j = 0; j < NBT; ++j) bn[j] = ld8(bp[j] + sn * 32);
 #pragma unroll
       for (int t = 0; t < NT; ++t) an[t] = ld8(ap[t] + sn * 32);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = mfma16(a[t], b, acc[t]);
-      b = bn;
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int j = 0; j < NBT; ++j) c[t][j] = mfma16(a[t], b[j], c[t][j]);
+#pragma unroll
+      for (int j = 0; j < NBT; ++j) b[j] = bn[j];
 #pragma unroll
       for (int t = 0; t < NT; ++t) a[t] = an[t];
     }
   }
-  if (w != 0) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
-      *reinterpret_cast<f32x4*>(part + ((size_t)(w * NT + t) * 64 + lane) * 4) = acc[t];
-  }
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int j = 0; j < NBT; ++j)
+      *reinterpret_cast<f32x4*>(part + (((size_t)(w * NT + t) * NBT + j) * 64 + lane) * 4) = c[t][j];
   __syncthreads();
-  if (w == 0) {
+  if (w < NBT) {
 #pragma unroll
-    for (int ww = 1; ww < 4; ++ww)
+    for (int t = 0; t < NT; ++t) {
+      acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const f32x4 p = *reinterpret_cast<const f32x4*>(part + ((size_t)(ww * NT + t) * 64 + lane) * 4);
-        acc[t] += p;
-      }
+      for (int ww = 0; ww < 4; ++ww)
+        acc[t] += *reinterpret_cast<const f32x4*>(part + (((size_t)(ww * NT + t) * NBT + w) * 64 + lane) * 4);
+    }
   }
 }
 
@@ -108,23 +122,26 @@ __device__ __forceinline__ void f4arr(const float4 v, float (&o)[4]) {
 // ------------------------------------------------------------------------------------------
 // forward step
 // ------------------------------------------------------------------------------------------
-template <int CELL>
+template <int CELL, int NBT>
 __global__ void __launch_bounds__(256) fwd_step_kernel(FwdStepArgs a) {
   constexpr int G = CellG<CELL>::G;
-  __shared__ __attribute__((aligned(16))) float part[4 * G * 64 * 4];
+  static_assert(G * NBT <= 16, "partials must fit in 64 KB of LDS");
+  __shared__ __attribute__((aligned(16))) float part[4 * G * NBT * 64 * 4];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B;
   const int nub = H / 16;
-  const int ub = (blockIdx.x % nub) * 16, b0 = (blockIdx.x / nub) * 16;
+  const int ub = (blockIdx.x % nub) * 16, bgrp = (blockIdx.x / nub) * 16 * NBT;
 
   f32x4 acc[G];
-  int arow[G];
+  int arow[G], brow[NBT];
 #pragma unroll
   for (int g = 0; g < G; ++g) arow[g] = g * H + ub + (lane & 15);
-  const int brow = min(b0 + (lane & 15), B - 1);
-  tile_gemm<G>(acc, a.WT, arow, H, a.hop, brow, H, H, lane, w, part);
-  if (w != 0) return;
+#pragma unroll
+  for (int j = 0; j < NBT; ++j) brow[j] = min(bgrp + 16 * j + (lane & 15), B - 1);
+  tile_gemm<G, NBT>(acc, a.WT, arow, H, a.hop, brow, H, H, lane, w, part);
+  if (w >= NBT) return;
+  const int b0 = bgrp + 16 * w;
 
   const int b = b0 + (lane & 15);
   if (b >= B) return;
@@ -219,21 +236,24 @@ __global__ void __launch_bounds__(256) fwd_step_kernel(FwdStepArgs a) {
 // ------------------------------------------------------------------------------------------
 // backward step:  acc[u][b] = sum_k W[u][k] * dz_next[b][k]   (K = a.K), then cell backward
 // ------------------------------------------------------------------------------------------
-template <int CELL>
+template <int CELL, int NBT>
 __global__ void __launch_bounds__(256) bwd_step_kernel(BwdStepArgs a) {
-  __shared__ __attribute__((aligned(16))) float part[4 * 64 * 4];
+  __shared__ __attribute__((aligned(16))) float part[4 * NBT * 64 * 4];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B;
   const int nub = H / 16;
-  const int ub = (blockIdx.x % nub) * 16, b0 = (blockIdx.x / nub) * 16;
+  const int ub = (blockIdx.x % nub) * 16, bgrp = (blockIdx.x / nub) * 16 * NBT;
   f32x4 acc[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
   if (a.dz_next) {
     const int arow[1] = {ub + (lane & 15)};
-    const int brow = min(b0 + (lane & 15), B - 1);
-    tile_gemm<1>(acc, a.W, arow, a.K, a.dz_next, brow, a.dz_ld, a.K, lane, w, part);
+    int brow[NBT];
+#pragma unroll
+    for (int j = 0; j < NBT; ++j) brow[j] = min(bgrp + 16 * j + (lane & 15), B - 1);
+    tile_gemm<1, NBT>(acc, a.W, arow, a.K, a.dz_next, brow, a.dz_ld, a.K, lane, w, part);
   }
-  if (w != 0) return;
+  if (w >= NBT) return;
+  const int b0 = bgrp + 16 * w;
   const int b = b0 + (lane & 15);
   if (b >= B) return;
   const int u0 = ub + 4 * (lane >> 4);
@@ -365,29 +385,70 @@ __global__ void __launch_bounds__(256) bwd_step_kernel(BwdStepArgs a) {
   }
 }
 
-static inline int step_blocks(int B, int H) {
-  return ((B + 15) / 16) * (H / 16);  // one 16-unit x 16-batch output tile per workgroup
+// Batch tiles per workgroup: each workgroup reads its 16-unit weight slice once per NBT x 16
+// batch rows.  Larger NBT cuts weight traffic (which dominates at large H) but shrinks the grid.
+// Measured on 1x MI355X (4-layer LSTM-2048, T=512, B=64): NBT 1/2/4 -> 129/108/141 ms per
+// training step; the 3-layer GRU-1024 per-step path lost 20 % at NBT=4 (128 workgroups).  So
+// NBT=2 when that still leaves >= 256 workgroups (one per CU), else 1; DCR_STEP_NBT=1/2/4
+// overrides.
+static int step_nbt(int G, int B, int H) {
+  const char* e = getenv("DCR_STEP_NBT");
+  const int forced = (e && (e[0] == '1' || e[0] == '2' || e[0] == '4')) ? e[0] - '0' : 0;
+  const int nbt_tiles = (B + 15) / 16;
+  for (int c : {4, 2}) {
+    if (G * c > 16 || nbt_tiles < c) continue;
+    if (forced) {
+      if (c <= forced) return c;
+      continue;
+    }
+    if (c == 2 && (H / 16) * ((nbt_tiles + c - 1) / c) >= 256) return c;
+  }
+  return 1;
+}
+
+static inline int step_blocks(int B, int H, int nbt) {
+  return ((B + 16 * nbt - 1) / (16 * nbt)) * (H / 16);
+}
+
+template <int CELL>
+static void fwd_launch(const FwdStepArgs& a, hipStream_t s) {
+  const int nbt = step_nbt(CellG<CELL>::G, a.B, a.H);
+  const int nb = step_blocks(a.B, a.H, nbt);
+  if constexpr (CellG<CELL>::G * 4 <= 16) {
+    if (nbt == 4) { fwd_step_kernel<CELL, 4><<<nb, 256, 0, s>>>(a); return; }
+  }
+  if constexpr (CellG<CELL>::G * 2 <= 16) {
+    if (nbt == 2) { fwd_step_kernel<CELL, 2><<<nb, 256, 0, s>>>(a); return; }
+  }
+  fwd_step_kernel<CELL, 1><<<nb, 256, 0, s>>>(a);
+}
+
+template <int CELL>
+static void bwd_launch(const BwdStepArgs& a, hipStream_t s) {
+  const int nbt = step_nbt(1, a.B, a.H);
+  const int nb = step_blocks(a.B, a.H, nbt);
+  if (nbt == 4) bwd_step_kernel<CELL, 4><<<nb, 256, 0, s>>>(a);
+  else if (nbt == 2) bwd_step_kernel<CELL, 2><<<nb, 256, 0, s>>>(a);
+  else bwd_step_kernel<CELL, 1><<<nb, 256, 0, s>>>(a);
 }
 
 void launch_fwd_step(int cell, const FwdStepArgs& a, hipStream_t s) {
-  const int nb = step_blocks(a.B, a.H);
   switch (cell) {
-    case CELL_LSTM: fwd_step_kernel<CELL_LSTM><<<nb, 256, 0, s>>>(a); break;
-    case CELL_GRU_A: fwd_step_kernel<CELL_GRU_A><<<nb, 256, 0, s>>>(a); break;
-    case CELL_GRU_B: fwd_step_kernel<CELL_GRU_B><<<nb, 256, 0, s>>>(a); break;
-    case CELL_RNN: fwd_step_kernel<CELL_RNN><<<nb, 256, 0, s>>>(a); break;
-    case CELL_NAS: fwd_step_kernel<CELL_NAS><<<nb, 256, 0, s>>>(a); break;
+    case CELL_LSTM: fwd_launch<CELL_LSTM>(a, s); break;
+    case CELL_GRU_A: fwd_launch<CELL_GRU_A>(a, s); break;
+    case CELL_GRU_B: fwd_launch<CELL_GRU_B>(a, s); break;
+    case CELL_RNN: fwd_launch<CELL_RNN>(a, s); break;
+    case CELL_NAS: fwd_launch<CELL_NAS>(a, s); break;
   }
 }
 
 void launch_bwd_step(int cell, const BwdStepArgs& a, hipStream_t s) {
-  const int nb = step_blocks(a.B, a.H);
   switch (cell) {
-    case CELL_LSTM: bwd_step_kernel<CELL_LSTM><<<nb, 256, 0, s>>>(a); break;
-    case CELL_GRU_A: bwd_step_kernel<CELL_GRU_A><<<nb, 256, 0, s>>>(a); break;
-    case CELL_GRU_B: bwd_step_kernel<CELL_GRU_B><<<nb, 256, 0, s>>>(a); break;
-    case CELL_RNN: bwd_step_kernel<CELL_RNN><<<nb, 256, 0, s>>>(a); break;
-    case CELL_NAS: bwd_step_kernel<CELL_NAS><<<nb, 256, 0, s>>>(a); break;
+    case CELL_LSTM: bwd_launch<CELL_LSTM>(a, s); break;
+    case CELL_GRU_A: bwd_launch<CELL_GRU_A>(a, s); break;
+    case CELL_GRU_B: bwd_launch<CELL_GRU_B>(a, s); break;
+    case CELL_RNN: bwd_launch<CELL_RNN>(a, s); break;
+    case CELL_NAS: bwd_launch<CELL_NAS>(a, s); break;
   }
 }
 

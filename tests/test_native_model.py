@@ -100,3 +100,27 @@ def test_segsum_kernel(dcr_ops, V, W, N):
     ref.index_add_(0, (ids if ids is not None else torch.zeros(N, device="cuda", dtype=torch.int32)).long(),
                    X.double())
     torch.testing.assert_close(out.double(), ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("nbt", ["2", "4"])
+@pytest.mark.parametrize("model", ["lstm", "gru", "rnn", "nas"])
+def test_per_step_batch_tiles_match_reference(model, nbt, monkeypatch):
+    """Per-step kernels with several batch tiles per workgroup (weight slice read once per
+    NBT x 16 rows; ragged last group) against the fp32 oracle."""
+    monkeypatch.setenv("DCR_PERSIST", "0")
+    monkeypatch.setenv("DCR_STEP_NBT", nbt)
+    B, T, H, L = 56, 5, 64, 2
+    torch.manual_seed(2)
+    cfg, nat, ref = _pair(model, B, T, H, L)
+    x = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
+    y = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
+    st0 = [tuple(torch.randn(B, H, device="cuda") * 0.5 for _ in range(cfg.state_arity))
+           for _ in range(L)]
+    loss_r, _, _ = ref.train_step(x, y, [tuple(s.clone() for s in t) for t in st0])
+    g_ref = nat.store.grad.clone()
+    nat.store.grad.zero_()
+    loss_n, _, _ = nat.backend.train_step(x, y, [tuple(s.clone() for s in t) for t in st0])
+    torch.cuda.synchronize()
+    assert abs(loss_n.item() - loss_r.item()) < 2e-2 * max(1.0, abs(loss_r.item()))
+    for s in nat.store.specs:
+        assert rel(nat.store.gview(s.name), nat.store.view(s.name, g_ref)) < 6e-2, s.name
