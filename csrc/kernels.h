@@ -119,6 +119,15 @@ int lstm_persist_occupancy(int bwd, int H, int B, int V, int flags, int cus);
 int launch_lstm_fwd_persist(const PersistArgs& a, int cus, hipStream_t s);
 int launch_lstm_bwd_persist(const PersistArgs& a, int cus, hipStream_t s);
 
+// wide-vocabulary softmax CE (xent.hip): bias added in-kernel, fused d softmax_b, V % 4 == 0,
+// V <= 8192
+int xent_wide_waves(int N);
+int xent_wide_blocks(int N);
+int xent_wide_supported(int V);
+void launch_xent_wide(const float* logits, const float* bias, const int* targets, int N, int V,
+                      float grad_scale, float* row_loss, bf16* dlogits, float* colpart, float* db,
+                      float* partial, float* loss_out, hipStream_t s);
+
 // persistent GRU recurrence (gru_persist.hip)
 struct GruPersistArgs {
   const bf16* WgT;      // fwd: W_g,hᵀ [2H, H] (r rows, then u rows)

@@ -279,6 +279,38 @@ void xent(const at::Tensor& logits, const at::Tensor& targets, double grad_scale
                    ptr<float>(loss_out), cur_stream());
 }
 
+// wide-vocabulary CE with fused d softmax_b (workspace: [xent_wide_waves(N), V] column partials)
+void xent_wide(const at::Tensor& logits, const c10::optional<at::Tensor>& bias,
+               const at::Tensor& targets, double grad_scale,
+               const c10::optional<at::Tensor>& row_loss, const c10::optional<at::Tensor>& dlogits,
+               const c10::optional<at::Tensor>& colpart, const c10::optional<at::Tensor>& db,
+               at::Tensor& partial, at::Tensor& loss_out) {
+  check_seq(logits, at::kFloat, "logits");
+  check_seq(targets, at::kInt, "targets");
+  check_opt(row_loss, at::kFloat, "row_loss");
+  check_opt(dlogits, at::kBFloat16, "dlogits");
+  check_opt(colpart, at::kFloat, "colpart");
+  check_opt(db, at::kFloat, "db");
+  TORCH_CHECK(logits.dim() == 2, "logits must be [N, V]");
+  const int N = (int)logits.size(0), V = (int)logits.size(1);
+  TORCH_CHECK(dcr::xent_wide_supported(V), "xent_wide needs V % 4 == 0 and V <= 8192");
+  check_opt(bias, at::kFloat, "bias");
+  if (has(bias)) TORCH_CHECK(bias->numel() == V, "bias must be [V]");
+  TORCH_CHECK(targets.numel() == N, "targets must be [N]");
+  if (has(dlogits)) TORCH_CHECK(dlogits->numel() == (int64_t)N * V, "dlogits must be [N, V]");
+  if (has(db)) {
+    TORCH_CHECK(has(colpart) && has(dlogits), "db needs dlogits and colpart");
+    TORCH_CHECK(db->numel() == V, "db must be [V]");
+  }
+  if (has(colpart))
+    TORCH_CHECK(colpart->numel() >= (int64_t)dcr::xent_wide_waves(N) * V, "colpart too small");
+  TORCH_CHECK(partial.numel() >= dcr::xent_wide_blocks(N), "partial too small");
+  dcr::launch_xent_wide(ptr<float>(logits), optr<float>(bias), ptr<int>(targets), N, V,
+                        (float)grad_scale,
+                        optr<float>(row_loss), optr<bf16>(dlogits), optr<float>(colpart),
+                        optr<float>(db), ptr<float>(partial), ptr<float>(loss_out), cur_stream());
+}
+
 void segsum(const at::Tensor& X, const c10::optional<at::Tensor>& ids, int64_t V, at::Tensor& out,
             at::Tensor& workspace, bool accumulate) {
   TORCH_CHECK(X.is_cuda() && X.dim() == 2 && X.stride(1) == 1, "X must be a row-major 2-D GPU tensor");
@@ -657,6 +689,14 @@ TORCH_LIBRARY(dcr, m) {
   m.def(
       "xent(Tensor logits, Tensor targets, float grad_scale, Tensor(a!)? row_loss, "
       "Tensor(b!)? dlogits, Tensor(c!) partial, Tensor(d!) loss_out) -> ()");
+  m.def(
+      "xent_wide(Tensor logits, Tensor? bias, Tensor targets, float grad_scale, Tensor(a!)? row_loss, "
+      "Tensor(b!)? dlogits, Tensor(c!)? colpart, Tensor(d!)? db, Tensor(e!) partial, "
+      "Tensor(f!) loss_out) -> ()");
+  m.def("xent_wide_supported(int V) -> int",
+        [](int64_t V) -> int64_t { return dcr::xent_wide_supported((int)V); });
+  m.def("xent_wide_waves(int n) -> int",
+        [](int64_t n) -> int64_t { return dcr::xent_wide_waves((int)n); });
   m.def("xent_num_partials(int n) -> int",
         [](int64_t n) -> int64_t { return dcr::xent_num_partials((int)n); });
   m.def("lstm_persist_supported(int H, int B) -> int", &lstm_persist_supported);
@@ -717,6 +757,7 @@ TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("rnn_fwd_seq", &rnn_fwd_seq);
   m.impl("rnn_bwd_seq", &rnn_bwd_seq);
   m.impl("xent", &xent);
+  m.impl("xent_wide", &xent_wide);
   m.impl("segsum", &segsum);
   m.impl("lstm_persist_fwd", &lstm_persist_fwd);
   m.impl("lstm_persist_bwd", &lstm_persist_bwd);

@@ -33,6 +33,7 @@ from ..ops import native
 
 CELL_ID = {"lstm": 0, "gru": 1, "rnn": 3, "nas": 4}
 FORGET_BIAS = 1.0
+SEG_LDS_MAX_V = 96  # csrc/embed.hip kSegLdsMaxV: larger vocabularies take the atomic scatter
 # lstm_persist_occupancy flags (csrc/lstm_persist.hip PF_*)
 PF_FUSED, PF_DIAG, PF_EXCL, PF_GRANULE = 1, 2, 4, 8
 bf16 = torch.bfloat16
@@ -275,6 +276,8 @@ class NativeBackend:
             colsum=torch.empty(1, max(GW, self.V), dtype=f32, device=dev),
             head_part=(torch.empty(self.ops.head_workspace(N, self.V), dtype=f32, device=dev)
                        if self.fused_head else None),
+            colpart=(torch.empty(self.ops.xent_wide_waves(N) * self.V, dtype=f32, device=dev)
+                     if (training and self._wide_xent(N)) else None),
             **self._persist_plan(B, training),
             dtop=torch.empty(T, B, H, dtype=f32, device=dev) if training else None,
             dx=torch.empty(T, B, H, dtype=f32, device=dev) if training else None,
@@ -290,6 +293,12 @@ class NativeBackend:
         )
         self._bufs[key] = bufs
         return bufs
+
+    def _wide_xent(self, N: int) -> bool:
+        """Library logits GEMM + one-read CE kernel (xent_wide) for vocabularies the fused head
+        does not cover (V > 256)."""
+        return (not self.fused_head and self.V >= 256 and os.environ.get("DCR_WIDE_XENT", "1") != "0"
+                and bool(self.ops.xent_wide_supported(self.V)))
 
     def _side_stream(self):
         if self._side is None:
@@ -389,7 +398,8 @@ class NativeBackend:
         return (torch.rand(shape, device=self.dev, generator=self.gen) < keep).to(bf16) * (1.0 / keep)
 
     # ------------------------------------------------------------------ forward
-    def _forward(self, ids_tm: torch.Tensor, state, training: bool, want_logits: bool = True):
+    def _forward(self, ids_tm: torch.Tensor, state, training: bool, want_logits: bool = True,
+                 logits_bias: bool = True):
         T, B = ids_tm.shape
         H, N = self.H, T * B
         tasks = self._prep()
@@ -468,7 +478,9 @@ class NativeBackend:
             O = O.contiguous()
         logits = bufs["logits"]
         if want_logits:
-            _mm_into(O, self._head["Ws"], logits, bias=self._head["bs"])
+            # the wide-vocabulary CE adds the bias itself: a bias-initialised GEMM output would
+            # cost an extra [N, V] fp32 broadcast copy (1 GB at V = 8192)
+            _mm_into(O, self._head["Ws"], logits, bias=self._head["bs"] if logits_bias else None)
         new_state = []
         for layer in range(self.L):
             lb = bufs["layers"][layer]
@@ -486,8 +498,10 @@ class NativeBackend:
         tgt = y.t().contiguous().view(-1)
         T, B = ids_tm.shape
         H, V, N, GW = self.H, self.V, T * B, self.GW
+        wide = self._wide_xent(T * B)
         bufs, O, logits, new_state = self._forward(ids_tm, state, True,
-                                                   want_logits=not self.fused_head)
+                                                   want_logits=not self.fused_head,
+                                                   logits_bias=not wide)
         dlog = bufs["dlogits"]
         s, hd = self.store, self._head
         if self.fused_head:
@@ -498,6 +512,15 @@ class NativeBackend:
                           bufs["head_part"], bufs["loss"])
             _mm_tn(O, dlog, s.gview("rnnlm/softmax_w"))
             dtop = bufs["dtop"].view(T, B, H)
+        elif wide:
+            # wide vocabulary: one-read CE (bias added in-kernel), d softmax_b fused (xent_wide)
+            self.ops.xent_wide(logits, hd["bs"], tgt, 1.0 / N, bufs["row_loss"], dlog,
+                               bufs["colpart"], s.gview("rnnlm/softmax_b"), bufs["xpart"],
+                               bufs["loss"])
+            if want_extras:
+                logits += hd["bs"]
+            _mm_tn(O, dlog, s.gview("rnnlm/softmax_w"))
+            dtop = _mm_into(dlog, hd["Ws"].t(), bufs["dtop"].view(N, H)).view(T, B, H)
         else:
             self.ops.xent(logits, tgt, 1.0 / N, bufs["row_loss"], dlog, bufs["xpart"],
                           bufs["loss"])
@@ -614,7 +637,20 @@ class NativeBackend:
                 _mm_tn(Hprev, dZ, s.gview(names[1]))
             else:
                 _mm_tn(Hprev, dZ, s.gview(names[0])[H:])
-            if gather:
+            if gather and V > SEG_LDS_MAX_V and not fused_dew:
+                # wide vocabulary: the [V, GW] dEW segment sum would be an atomic scatter of
+                # N x GW values plus two fp32 [V, GW] GEMMs; the dense route scatters N x H
+                # instead: dW_x0 = E[ids]ᵀ·dZ0 (split-K), dE = segsum(dZ0·W_x0ᵀ)
+                X0 = hd["E"][ids_tm.view(-1).long()].to(bf16)      # [N, H]
+                dWx = _mm_tn(X0, dZx)
+                if bufs["persist"]:
+                    dbias = bufs["db_part"][layer].sum(0)
+                else:
+                    self.ops.segsum(dZx, None, 1, bufs["colsum"][:, :GW], bufs["ws"], False)
+                    dbias = bufs["colsum"][0, :GW]
+                dXf = _mm_into(dZx, lw.Wx.t(), bufs["dx"].view(N, H))
+                self.ops.segsum(dXf, ids_tm.view(-1), V, s.gview("embedding"), bufs["ws"], False)
+            elif gather:
                 if fused_dew:
                     dEW = bufs["dew_part"].sum(0)            # [V, GW] fp32 (fused in BPTT)
                 else:
