@@ -79,7 +79,7 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
     }
     // ---- phase A: [r, u] from h_{t-1}
     if (t > 0) {
-      if (threadIdx.x == 0 && !dead)
+      if (threadIdx.x == kPollerThread && !dead)
         dead = !poll_quarters(cntH + (size_t)t * 4, quarter_target, a.spin_limit, a.err, 5u);
       __syncthreads();
     }
@@ -129,7 +129,7 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
       st4bf(gp + H, uu[0], uu[1], uu[2], uu[3]);
     }
     // ---- phase B: c~ from r⊙h_{t-1}
-    if (threadIdx.x == 0 && !dead)
+    if (threadIdx.x == kPollerThread && !dead)
       dead = !poll_quarters(cntR + (size_t)t * 4, quarter_target, a.spin_limit, a.err, 6u);
     __syncthreads();
     {
@@ -258,7 +258,7 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
     const __amdgpu_buffer_rsrc_t zsrc =
         make_rsrc(a.dz + (size_t)t * B * G3, sizeof(bf16) * (size_t)B * G3);
     // ---- phase A: d(r⊙h_{t-1}) = dZc_t · W_cᵀ
-    if (threadIdx.x == 0 && !dead)
+    if (threadIdx.x == kPollerThread && !dead)
       dead = !poll_quarters(cntC + (size_t)t * 4, quarter_target, a.spin_limit, a.err, 7u);
     __syncthreads();
     {
@@ -304,7 +304,7 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
     }
     if (t == 0) break;  // dh'_{-1} (the initial state's gradient) is not needed
     // ---- phase B: dh'_{t-1} = dtop_{t-1} + P + dZg_t · W_gᵀ
-    if (threadIdx.x == 0 && !dead)
+    if (threadIdx.x == kPollerThread && !dead)
       dead = !poll_quarters(cntG + (size_t)t * 4, quarter_target, a.spin_limit, a.err, 8u);
     __syncthreads();
     {

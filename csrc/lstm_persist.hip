@@ -137,7 +137,7 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
     }
     if (t > 0) {
       // ONE poller per workgroup (pollers cost chip bandwidth); the barrier releases the waves
-      if (threadIdx.x == 0 && !dead)
+      if (threadIdx.x == kLstmPollerThread && !dead)
         dead = !poll_quarters(cnt + (size_t)t * 4, (unsigned)(H / 64), a.spin_limit, a.err, 1u);
       STAMP(1)
       __syncthreads();
@@ -446,8 +446,11 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
     for (int r = 0; r < 4; ++r) dbacc[g][r] = 0.f;
   const bool fuse_dew = a.dew_part != nullptr;
   const int DW = UB * 64;  // dEW columns owned by this workgroup: UB blocks x 4 gates x 16 units
+  // LDS row stride DW + 1: with DW (a multiple of 64 floats) every batch lane's row id*DW fell
+  // on the same bank; the odd stride spreads ids over banks
+  const int DWP = DW + 1;
   if (fuse_dew) {
-    for (int i = threadIdx.x; i < a.V * DW; i += 256) dew_acc[i] = 0.f;
+    for (int i = threadIdx.x; i < a.V * DWP; i += 256) dew_acc[i] = 0.f;
     __syncthreads();
   }
 
@@ -455,7 +458,9 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
     STAMP(0)
     // recurrence-independent epilogue operands, issued before the wait
     float gi[4], gj[4], gf[4], go[4], cc[4], cp[4], dtop[4];
+    int tok = 0;  // fused dEW row (issued with the other recurrence-independent operands)
     if (epi) {
+      if (fuse_dew) tok = a.ids[(size_t)t * B + b];
       const bf16* gp = a.gates + ((size_t)t * B + b) * G4H + u0;
       ld4bf(gp, gi); ld4bf(gp + H, gj); ld4bf(gp + 2 * H, gf); ld4bf(gp + 3 * H, go);
       ld4f(a.cbuf + (size_t)(t + 1) * B * H + bh, cc);
@@ -478,7 +483,7 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
     }
     if (t < T - 1 || XB) {
      if (t < T - 1) {
-      if (threadIdx.x == 0 && !dead)
+      if (threadIdx.x == kLstmPollerThread && !dead)
         dead = !poll_quarters(cnt + (size_t)(t + 1) * 4, (unsigned)(H / 64), a.spin_limit, a.err, 2u);
       STAMP(1)
       __syncthreads();
@@ -557,8 +562,8 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
 #pragma unroll
         for (int r = 0; r < 4; ++r) dbacc[g][r] += q[g][r];
       if (fuse_dew) {
-        const int id = a.ids[(size_t)t * B + b];
-        float* row = dew_acc + (size_t)id * DW + w * 64 + 4 * (lane >> 4);
+        const int id = tok;
+        float* row = dew_acc + (size_t)id * DWP + w * 64 + 4 * (lane >> 4);
 #pragma unroll
         for (int g = 0; g < 4; ++g)
 #pragma unroll
@@ -593,7 +598,7 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
     for (int i = threadIdx.x; i < a.V * DW; i += 256) {
       const int v = i / DW, col = i % DW;
       const int ui = col / 64, g = (col % 64) / 16, j = col % 16;
-      a.dew_part[((size_t)bg * a.V + v) * G4H + g * H + ub0 + ui * 16 + j] = dew_acc[i];
+      a.dew_part[((size_t)bg * a.V + v) * G4H + g * H + ub0 + ui * 16 + j] = dew_acc[v * DWP + col];
     }
   }
 }
@@ -656,7 +661,7 @@ static const void* pick(int bwd, int H, int B, int flags, int cus) {
 }
 
 static size_t dyn_lds(int bwd, int H, int B, int V, int cus) {
-  return (bwd && V > 0) ? sizeof(float) * (size_t)V * ub_for(H, B, cus) * 64 : 0;
+  return (bwd && V > 0) ? sizeof(float) * (size_t)V * (ub_for(H, B, cus) * 64 + 1) : 0;
 }
 
 int lstm_persist_supported(int H, int B, int cus) {

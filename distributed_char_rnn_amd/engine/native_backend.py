@@ -156,6 +156,11 @@ class NativeBackend:
         # 3.47 ms/step: its extra dZ loads sit on the load-bound critical path), opt-in only
         self.fused_dtop = os.environ.get("DCR_FUSED_DTOP", "0") == "1"
         self.side_overlap = os.environ.get("DCR_SIDE", "1") == "1"
+        # layer-0 embedding-table gradient dEW = onehot(ids)ᵀ·dZ0 [V, 4H]:
+        #   "gemm"  split-K MFMA GEMM against a bf16 one-hot matrix after the BPTT;
+        #   "fused" LDS atomics inside the BPTT epilogue;  "segsum" the segment-sum kernel
+        self.dew_mode = os.environ.get("DCR_DEW", "gemm")
+        self.fused_dew = self.dew_mode == "fused"
         # fused softmax head (csrc/head.hip): logits + CE + dlogits + d softmax_b + dtop
         self.fused_head = (os.environ.get("DCR_FUSED_HEAD", "1") != "0"
                            and bool(self.ops.head_supported(self.V, self.H)))
@@ -276,6 +281,8 @@ class NativeBackend:
             colsum=torch.empty(1, max(GW, self.V), dtype=f32, device=dev),
             head_part=(torch.empty(self.ops.head_workspace(N, self.V), dtype=f32, device=dev)
                        if self.fused_head else None),
+            onehot=(torch.empty(N, 8 * ((self.V + 7) // 8), dtype=bf16, device=dev)
+                    if (training and self.V <= SEG_LDS_MAX_V) else None),
             colpart=(torch.empty(self.ops.xent_wide_waves(N) * self.V, dtype=f32, device=dev)
                      if (training and self._wide_xent(N)) else None),
             **self._persist_plan(B, training),
@@ -552,7 +559,7 @@ class NativeBackend:
                 dtop = dtop.contiguous()
             zx_nas = lb.zx if self.cfg.model == "nas" else None
             gather = (layer == 0 and not drop and self.cfg.model != "nas")
-            fused_dew = bufs["persist"] and gather and V <= 128
+            fused_dew = bufs["persist"] and gather and V <= 128 and self.fused_dew
             if bufs["persist"]:
                 above = None
                 if dtop is None:  # dtop of this layer is fused: dZ_above · W_x,aboveᵀ in-kernel
@@ -653,6 +660,13 @@ class NativeBackend:
             elif gather:
                 if fused_dew:
                     dEW = bufs["dew_part"].sum(0)            # [V, GW] fp32 (fused in BPTT)
+                elif self.dew_mode == "gemm" and bufs["onehot"] is not None:
+                    # exact 1.0 one-hot entries: the same fp32 sums of the bf16 dZ values as a
+                    # scatter, as one split-K MFMA GEMM (K = T·B tokens)
+                    oh = bufs["onehot"]
+                    oh.zero_()
+                    oh.scatter_(1, ids_tm.view(-1, 1).long(), 1.0)
+                    dEW = _mm_tn(oh, dZx)[:V]                 # rows >= V are zero padding
                 else:
                     dEW = torch.empty(V, GW, dtype=f32, device=self.dev)
                     self.ops.segsum(dZx, ids_tm.view(-1), V, dEW, bufs["ws"], False)

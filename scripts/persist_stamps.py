@@ -42,12 +42,16 @@ W = (torch.randn(H, 4 * H, device=dev) * 0.05).to(torch.bfloat16)
 dtop = torch.randn(T, B, H, device=dev) * 0.01
 dz = torch.empty(T, B, 4 * H, dtype=torch.bfloat16, device=dev)
 dbp = torch.empty(B // 16, 4 * H, device=dev)
+# DCR_STAMP_DEW=1: layer-0 variant with the embedding-table gradient fused (ids + LDS atomics)
+DEW = os.environ.get("DCR_STAMP_DEW", "0") == "1"
+ids = torch.randint(0, 65, (T, B), device=dev, dtype=torch.int32) if DEW else None
+dewp = torch.empty(B // 16, 65, 4 * H, device=dev) if DEW else None
 for it in range(3):
-    ops.lstm_persist_bwd(W, dtop, dz, gates, cbuf, cnt, err, 1 << 22, dbp, None, None, 65, diag,
+    ops.lstm_persist_bwd(W, dtop, dz, gates, cbuf, cnt, err, 1 << 22, dbp, ids, dewp, 65, diag,
                          exclusive=EXCL)
 torch.cuda.synchronize()
 ev0.record()
-ops.lstm_persist_bwd(W, dtop, dz, gates, cbuf, cnt, err, 1 << 22, dbp, None, None, 65, diag,
+ops.lstm_persist_bwd(W, dtop, dz, gates, cbuf, cnt, err, 1 << 22, dbp, ids, dewp, 65, diag,
                          exclusive=EXCL)
 ev1.record()
 torch.cuda.synchronize()
