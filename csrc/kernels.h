@@ -128,6 +128,27 @@ void launch_xent_wide(const float* logits, const float* bias, const int* targets
                       float grad_scale, float* row_loss, bf16* dlogits, float* colpart, float* db,
                       float* partial, float* loss_out, hipStream_t s);
 
+// two-layer wavefront LSTM forward (lstm2_persist.hip)
+struct Lstm2Args {
+  const bf16* W0T;      // layer l   W_hᵀ [4H, H]
+  const bf16* W1T;      // layer l+1 W_hᵀ [4H, H]
+  const bf16* X1T;      // layer l+1 W_xᵀ [4H, H]
+  const float* zx0;     // layer l input projections (+bias): [T, B, zx_ld] or [V, zx_ld] table
+  const int* ids;       // gather mode: [T, B]
+  int zx_ld;
+  const float* bias1;   // layer l+1 bias [4H]
+  bf16* hbuf0; float* cbuf0; bf16* gates0; float* hlast0;   // layer l   [T+1,B,H] ...
+  bf16* hbuf1; float* cbuf1; bf16* gates1; float* hlast1;   // layer l+1
+  unsigned* cnt0;       // [B/32, T+1, 4] arrivals of layer l   (zeroed by the caller)
+  unsigned* cnt1;       // [B/32, T+1, 4] arrivals of layer l+1
+  unsigned* err;
+  int B, H, T;
+  float forget_bias;
+  unsigned spin_limit;
+};
+int lstm2_persist_supported(int H, int B, int cus);
+int launch_lstm2_fwd_persist(const Lstm2Args& a, int cus, hipStream_t s);
+
 // persistent GRU recurrence (gru_persist.hip)
 struct GruPersistArgs {
   const bf16* WgT;      // fwd: W_g,hᵀ [2H, H] (r rows, then u rows)

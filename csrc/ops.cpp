@@ -485,6 +485,63 @@ void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& d
 }
 
 // ------------------------------------------------------------------------------------------
+// two-layer wavefront LSTM forward (lstm2_persist.hip)
+// ------------------------------------------------------------------------------------------
+void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::Tensor& X1T,
+                       const at::Tensor& zx0, const c10::optional<at::Tensor>& ids,
+                       const at::Tensor& bias1, at::Tensor& hbuf0, at::Tensor& cbuf0,
+                       const c10::optional<at::Tensor>& gates0, at::Tensor& hlast0,
+                       at::Tensor& hbuf1, at::Tensor& cbuf1,
+                       const c10::optional<at::Tensor>& gates1, at::Tensor& hlast1,
+                       at::Tensor& cnt0, at::Tensor& cnt1, at::Tensor& err, double forget_bias,
+                       int64_t spin_limit) {
+  for (auto* t : {&W0T, &W1T, &X1T}) check_seq(*t, at::kBFloat16, "W");
+  check_seq(zx0, at::kFloat, "zx0");
+  check_seq(bias1, at::kFloat, "bias1");
+  for (auto* t : {&hbuf0, &hbuf1}) check_seq(*t, at::kBFloat16, "hbuf");
+  for (auto* t : {&cbuf0, &cbuf1, &hlast0, &hlast1}) check_seq(*t, at::kFloat, "state");
+  check_opt(gates0, at::kBFloat16, "gates0");
+  check_opt(gates1, at::kBFloat16, "gates1");
+  check_opt(ids, at::kInt, "ids");
+  const int T = (int)hbuf0.size(0) - 1, B = (int)hbuf0.size(1), H = (int)hbuf0.size(2);
+  TORCH_CHECK(hbuf1.sizes() == hbuf0.sizes(), "hbuf1 must match hbuf0");
+  TORCH_CHECK(cbuf0.numel() == hbuf0.numel() && cbuf1.numel() == hbuf0.numel(), "cbuf shape");
+  TORCH_CHECK(hlast0.numel() == (int64_t)B * H && hlast1.numel() == (int64_t)B * H, "hlast shape");
+  for (auto* t : {&W0T, &W1T, &X1T})
+    TORCH_CHECK(t->size(0) == 4 * H && t->size(1) == H, "weights must be [4H, H]");
+  TORCH_CHECK(bias1.numel() == 4 * H, "bias1 must be [4H]");
+  TORCH_CHECK(zx0.size(-1) == 4 * H, "zx0 rows must be 4H wide");
+  if (has(ids)) {
+    TORCH_CHECK(ids->numel() == (int64_t)T * B, "ids must be [T, B]");
+  } else {
+    TORCH_CHECK(zx0.numel() == (int64_t)T * B * 4 * H, "zx0 must be [T, B, 4H]");
+  }
+  for (auto* g : {&gates0, &gates1})
+    if (has(*g)) TORCH_CHECK((*g)->numel() == (int64_t)T * B * 4 * H, "gates must be [T, B, 4H]");
+  for (auto* c : {&cnt0, &cnt1})
+    TORCH_CHECK(c->is_cuda() && c->scalar_type() == at::kInt &&
+                    c->numel() >= (int64_t)(B / 32) * (T + 1) * 4, "counter buffer too small");
+  TORCH_CHECK(dcr::lstm2_persist_supported(H, B, num_cus()),
+              "two-layer persistent LSTM unsupported for H=", H, " B=", B);
+  dcr::Lstm2Args a{};
+  a.W0T = ptr<bf16>(W0T); a.W1T = ptr<bf16>(W1T); a.X1T = ptr<bf16>(X1T);
+  a.zx0 = ptr<float>(zx0); a.ids = optr<int>(ids); a.zx_ld = 4 * H;
+  a.bias1 = ptr<float>(bias1);
+  a.hbuf0 = ptr<bf16>(hbuf0); a.cbuf0 = ptr<float>(cbuf0); a.gates0 = optr<bf16>(gates0);
+  a.hlast0 = ptr<float>(hlast0);
+  a.hbuf1 = ptr<bf16>(hbuf1); a.cbuf1 = ptr<float>(cbuf1); a.gates1 = optr<bf16>(gates1);
+  a.hlast1 = ptr<float>(hlast1);
+  a.cnt0 = reinterpret_cast<unsigned*>(cnt0.data_ptr());
+  a.cnt1 = reinterpret_cast<unsigned*>(cnt1.data_ptr());
+  a.err = reinterpret_cast<unsigned*>(err.data_ptr());
+  a.B = B; a.H = H; a.T = T;
+  a.forget_bias = (float)forget_bias;
+  a.spin_limit = (unsigned)spin_limit;
+  const int rc = dcr::launch_lstm2_fwd_persist(a, num_cus(), cur_stream());
+  TORCH_CHECK(rc == 0, "two-layer persistent LSTM forward not launched (", rc, ")");
+}
+
+// ------------------------------------------------------------------------------------------
 // persistent GRU recurrence (gru_persist.hip)
 // ------------------------------------------------------------------------------------------
 static void gru_common(dcr::GruPersistArgs& a, const at::Tensor& gates, const at::Tensor& h32,
@@ -735,6 +792,14 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor(a!)? logits, Tensor(b!)? row_loss, Tensor(c!)? dlogits, Tensor(d!)? dtop, "
       "Tensor(e!)? db, Tensor(f!) part, Tensor(g!)? loss) -> ()");
   m.def("prep(Tensor[] src, Tensor(a!)[] dst, int[] mode) -> ()");
+  m.def("lstm2_persist_supported(int H, int B) -> int", [](int64_t H, int64_t B) -> int64_t {
+    return dcr::lstm2_persist_supported((int)H, (int)B, num_cus());
+  });
+  m.def(
+      "lstm2_persist_fwd(Tensor W0T, Tensor W1T, Tensor X1T, Tensor zx0, Tensor? ids, "
+      "Tensor bias1, Tensor(a!) hbuf0, Tensor(b!) cbuf0, Tensor(c!)? gates0, Tensor(d!) hlast0, "
+      "Tensor(e!) hbuf1, Tensor(f!) cbuf1, Tensor(g!)? gates1, Tensor(h!) hlast1, "
+      "Tensor(i!) cnt0, Tensor(j!) cnt1, Tensor(k!) err, float forget_bias, int spin_limit) -> ()");
   m.def("gru_persist_ub(int H, int B) -> int", [](int64_t H, int64_t B) -> int64_t {
     return dcr::gru_persist_ub((int)H, (int)B, num_cus());
   });
@@ -764,5 +829,6 @@ TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("head", &head);
   m.impl("prep", &prep);
   m.impl("gru_persist_fwd", &gru_persist_fwd);
+  m.impl("lstm2_persist_fwd", &lstm2_persist_fwd);
   m.impl("gru_persist_bwd", &gru_persist_bwd);
 }

@@ -149,6 +149,8 @@ class NativeBackend:
         self._head = None
         self._bufs: Dict[Tuple[int, int, bool], dict] = {}
         self.use_persist = os.environ.get("DCR_PERSIST", "1") != "0"
+        # two-layer wavefront forward (lstm2_persist.hip) for layers (0, 1)
+        self.use_pair = os.environ.get("DCR_PAIR", "1") != "0"
         self.spin_limit = int(os.environ.get("DCR_SPIN_LIMIT", str(1 << 22)))
         # forward hand-off form: "granule" (tagged data, R2) or "counter" (sc1 data + counter)
         self.handoff = os.environ.get("DCR_HANDOFF", "counter")
@@ -347,7 +349,7 @@ class NativeBackend:
         forces a mode.
         """
         plan = dict(persist=False, xfuse=False, mode="exclusive", bwd_excl=False,
-                    gru_persist=False)
+                    gru_persist=False, pair=False)
         o = self.ops
         if self.use_persist and self.cfg.model == "gru":
             # persistent GRU (gru_persist.hip): the C++ side picks the unit block whose fwd and
@@ -372,6 +374,8 @@ class NativeBackend:
         plan["persist"] = True
         plan["xfuse"] = (os.environ.get("DCR_XFUSE", "1") != "0"
                          and bool(o.lstm_persist_xfuse_supported(H, B)))
+        # two-layer wavefront forward (lstm2_persist.hip): layers (0,1), (2,3), ...
+        plan["pair"] = (self.L >= 2 and self.use_pair and bool(o.lstm2_persist_supported(H, B)))
         if not training:
             return plan
         shared_ok = fits(1, 0, margin=1)
@@ -428,7 +432,10 @@ class NativeBackend:
             tasks.append((bufs["cnt"], bufs["cnt"], 2))
         self._run_prep(tasks)
         x_prev = None  # bf16 [T, B, H] input for the next layer
+        paired = -1  # layer already computed by the previous layer's two-layer wavefront
         for layer in range(self.L):
+            if layer == paired:
+                continue
             lw, lb = self._w[layer], bufs["layers"][layer]
             gather = (layer == 0 and not drop and self.cfg.model != "nas")
             ids_arg = None
@@ -461,6 +468,18 @@ class NativeBackend:
                 lb.x_in = X.reshape(N, H).contiguous()
                 _mm_into(lb.x_in, lw.Wx, lb.zx.view(N, self.GW), bias=lw.bias)
                 zx = lb.zx
+            if bufs["pair"] and layer + 1 < self.L and not drop:
+                # layers (l, l+1) as one wavefront launch (lstm2_persist.hip): T+1 ticks
+                lw1, lb1 = self._w[layer + 1], bufs["layers"][layer + 1]
+                self.ops.lstm2_persist_fwd(lw.WhT, lw1.WhT, lw1.WxT, zx, ids_arg, lw1.bias,
+                                           lb.hbuf, lb.cbuf, lb.gates, lb.hlast32,
+                                           lb1.hbuf, lb1.cbuf, lb1.gates, lb1.hlast32,
+                                           bufs["cnt"][layer], bufs["cnt"][layer + 1], self.err,
+                                           FORGET_BIAS, self.spin_limit)
+                lb1.x_in = lb.hbuf[1:].reshape(N, H)
+                x_prev = lb1.hbuf[1:]
+                paired = layer + 1
+                continue
             if bufs["persist"]:
                 self.ops.lstm_persist_fwd(lw.WhT, zx, ids_arg, lb.hbuf, lb.cbuf, lb.gates,
                                           lb.hlast32, bufs["cnt"][layer], self.err, FORGET_BIAS,

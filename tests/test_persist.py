@@ -125,3 +125,30 @@ def test_residency_plan_and_refusal(dcr_ops):
     x = torch.randint(0, 65, (B, T), device=dev, dtype=torch.int32)
     loss, _, _ = m.backend.train_step(x, x, m.zero_state(B))
     assert torch.isfinite(loss).item()
+
+
+@pytest.mark.parametrize("B,T,H", [(32, 7, 128), (256, 12, 512), (64, 5, 384)])
+def test_two_layer_wavefront_equals_single_layer_kernels(B, T, H, monkeypatch):
+    """lstm2_persist.hip (layers 0 and 1 as one wavefront launch) vs two single-layer
+    persistent launches: identical bf16 math, so agreement to accumulation-order noise."""
+    cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=2)
+    a = CharRNN(cfg, device="cuda", seed=9)
+    monkeypatch.setenv("DCR_PAIR", "0")
+    b = CharRNN(cfg, device="cuda", seed=9)
+    assert a.backend._persist_plan(B, True)["pair"]
+    assert not b.backend._persist_plan(B, True)["pair"]
+    x = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
+    sa, sb = a.zero_state(B), b.zero_state(B)
+    for _ in range(2):  # carried state across steps
+        la, sa, _ = a.backend.train_step(x, x, sa)
+        lb, sb, _ = b.backend.train_step(x, x, sb)
+    torch.cuda.synchronize()
+    a.backend.check_errors()
+    assert abs(la.item() - lb.item()) < 1e-4
+    assert rel(a.store.grad, b.store.grad) < 1e-3
+    for u, v in zip(sa, sb):
+        for p, q in zip(u, v):
+            assert rel(p, q) < 1e-3
+    ea, _ = a.backend.eval_loss(x, x, a.zero_state(B))
+    eb, _ = b.backend.eval_loss(x, x, b.zero_state(B))
+    assert abs(ea.item() - eb.item()) < 1e-4
