@@ -83,9 +83,11 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     }
     if (tau >= 1) {
       if (threadIdx.x == kLstmPollerThread && !dead) {
-        dead = !poll_quarters(cnt0 + (size_t)tau * 4, target, a.spin_limit, a.err, 9u);
-        if (!dead && tau >= 2)
-          dead = !poll_quarters(cnt1 + (size_t)(tau - 1) * 4, target, a.spin_limit, a.err, 10u);
+        // layer l+1's slot tau-1 exists from tick 2 on; before that poll layer l's twice
+        dead = tau >= 2 ? !poll_quarters2(cnt0 + (size_t)tau * 4, target,
+                                          cnt1 + (size_t)(tau - 1) * 4, target, a.spin_limit,
+                                          a.err, 9u)
+                        : !poll_quarters(cnt0 + (size_t)tau * 4, target, a.spin_limit, a.err, 9u);
       }
       __syncthreads();
     }

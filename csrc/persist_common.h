@@ -73,6 +73,27 @@ __device__ __forceinline__ bool poll_quarters(unsigned* cnt4, unsigned target, u
   }
 }
 
+// Two counter sets polled together (one sc1 load each per iteration, both in flight): the
+// two-layer wavefront waits for both layers' previous tick without a second round trip.
+__device__ __forceinline__ bool poll_quarters2(unsigned* c0, unsigned t0, unsigned* c1,
+                                               unsigned t1, unsigned limit, unsigned* err,
+                                               unsigned code) {
+  const __amdgpu_buffer_rsrc_t r0 = make_rsrc(c0, 16), r1 = make_rsrc(c1, 16);
+  unsigned spins = 0;
+  for (;;) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r0, 0, 0, kAuxSc1);
+    const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(r1, 0, 0, kAuxSc1);
+    if (v[0] >= t0 && v[1] >= t0 && v[2] >= t0 && v[3] >= t0 && u[0] >= t1 && u[1] >= t1 &&
+        u[2] >= t1 && u[3] >= t1)
+      return true;
+    if (++spins > limit) {
+      __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 // Block -> (unit block, batch group).  Speed only: place the unit-block workgroups of one batch
 // group on the same XCD under the observed round-robin dispatch (blocks b, b+8, ... share an
 // XCD; MI355X_MICROARCH.md "Workgroup dispatch"), so the batch group's hand-off payload is
