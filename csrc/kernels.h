@@ -142,6 +142,7 @@ struct Lstm2Args {
   unsigned* cnt0;       // [B/32, T+1, 4] arrivals of layer l   (zeroed by the caller)
   unsigned* cnt1;       // [B/32, T+1, 4] arrivals of layer l+1
   unsigned* err;
+  unsigned long long* diag;  // optional [T+1, 8] s_memtime stamps of workgroup 0 (diagnostics)
   int B, H, T;
   float forget_bias;
   unsigned spin_limit;

@@ -21,7 +21,13 @@
 
 namespace dcr {
 
-template <int KS>
+#define STAMP2(i)                                                                   \
+  if constexpr (DIAG) {                                                             \
+    if (blockIdx.x == 0 && threadIdx.x == 0)                                        \
+      a.diag[(size_t)tau * 8 + (i)] = __builtin_amdgcn_s_memtime();                 \
+  }
+
+template <int KS, bool DIAG = false>
 __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) {
   // partials [wave][layer][tile][lane][gate*4 + r]: single-buffered -- every tick after the
   // first starts with the poll barrier, which each epilogue wave joins after its reads
@@ -73,6 +79,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
 
   for (int tau = 0; tau <= T; ++tau) {
     const bool on0 = tau < T, on1 = tau >= 1;
+    STAMP2(0)
     // layer-l input projections of step tau (recurrence independent: issued before the wait)
     float zx[4][4];
     if (L == 0 && on0) {
@@ -89,8 +96,10 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
                                           a.err, 9u)
                         : !poll_quarters(cnt0 + (size_t)tau * 4, target, a.spin_limit, a.err, 9u);
       }
+      STAMP2(1)
       __syncthreads();
     }
+    STAMP2(2)
     // payloads: h_l[tau] (both layers' input) and h_{l+1}[tau-1]
     bf16x8 hf0[2][KS], hf1[2][KS];
     {
@@ -140,7 +149,9 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
         for (int g = 0; g < 4; ++g) dst[g] = make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
       }
     }
+    STAMP2(3)
     __syncthreads();
+    STAMP2(4)
     if (L == 0 ? on0 : on1) {
       const int t = L == 0 ? tau : tau - 1;  // this layer's step
       float z[4][4];
@@ -167,10 +178,12 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
         h[r] = go[r] * tanhf_(c[r]);
       }
       const size_t o = (size_t)(t + 1) * B * H + bh;
+      STAMP2(5)
       st4bf_sc1(hbL + o, h[0], h[1], h[2], h[3]);
       // layer l's slot t+1 feeds both layers (up to slot T); layer l+1's slot t+1 only itself
       if (L == 0 || t + 1 < T) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        STAMP2(6)
         if (lane == 0)
           __hip_atomic_fetch_add(cntL + (size_t)(t + 1) * 4 + (u0 / (H / 4)), 1u,
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -190,14 +203,17 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
 }
 
 template <int KS>
-static const void* lstm2_fn() { return (const void*)lstm2_fwd_persist_kernel<KS>; }
+static const void* lstm2_fn(bool diag) {
+  return diag ? (const void*)lstm2_fwd_persist_kernel<KS, true>
+              : (const void*)lstm2_fwd_persist_kernel<KS, false>;
+}
 
-static const void* lstm2_pick(int H) {
+static const void* lstm2_pick(int H, bool diag = false) {
   switch (H / 128) {
-    case 1: return lstm2_fn<1>();
-    case 2: return lstm2_fn<2>();
-    case 3: return lstm2_fn<3>();
-    case 4: return lstm2_fn<4>();
+    case 1: return lstm2_fn<1>(diag);
+    case 2: return lstm2_fn<2>(diag);
+    case 3: return lstm2_fn<3>(diag);
+    case 4: return lstm2_fn<4>(diag);
   }
   return nullptr;
 }
@@ -216,7 +232,8 @@ int lstm2_persist_supported(int H, int B, int cus) {
 int launch_lstm2_fwd_persist(const Lstm2Args& a, int cus, hipStream_t s) {
   if (!lstm2_persist_supported(a.H, a.B, cus)) return -2;
   void* args[] = {const_cast<Lstm2Args*>(&a)};
-  return hipLaunchKernel(lstm2_pick(a.H), dim3(lstm2_grid(a.H, a.B)), dim3(256), args, 0, s) ==
+  return hipLaunchKernel(lstm2_pick(a.H, a.diag != nullptr), dim3(lstm2_grid(a.H, a.B)),
+                         dim3(256), args, 0, s) ==
                  hipSuccess ? 0 : -3;
 }
 

@@ -494,7 +494,7 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
                        at::Tensor& hbuf1, at::Tensor& cbuf1,
                        const c10::optional<at::Tensor>& gates1, at::Tensor& hlast1,
                        at::Tensor& cnt0, at::Tensor& cnt1, at::Tensor& err, double forget_bias,
-                       int64_t spin_limit) {
+                       int64_t spin_limit, const c10::optional<at::Tensor>& diag) {
   for (auto* t : {&W0T, &W1T, &X1T}) check_seq(*t, at::kBFloat16, "W");
   check_seq(zx0, at::kFloat, "zx0");
   check_seq(bias1, at::kFloat, "bias1");
@@ -537,6 +537,11 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
   a.B = B; a.H = H; a.T = T;
   a.forget_bias = (float)forget_bias;
   a.spin_limit = (unsigned)spin_limit;
+  if (has(diag)) {
+    TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)(T + 1) * 8,
+                "diag must hold [T+1, 8] int64");
+    a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());
+  }
   const int rc = dcr::launch_lstm2_fwd_persist(a, num_cus(), cur_stream());
   TORCH_CHECK(rc == 0, "two-layer persistent LSTM forward not launched (", rc, ")");
 }
@@ -799,7 +804,8 @@ TORCH_LIBRARY(dcr, m) {
       "lstm2_persist_fwd(Tensor W0T, Tensor W1T, Tensor X1T, Tensor zx0, Tensor? ids, "
       "Tensor bias1, Tensor(a!) hbuf0, Tensor(b!) cbuf0, Tensor(c!)? gates0, Tensor(d!) hlast0, "
       "Tensor(e!) hbuf1, Tensor(f!) cbuf1, Tensor(g!)? gates1, Tensor(h!) hlast1, "
-      "Tensor(i!) cnt0, Tensor(j!) cnt1, Tensor(k!) err, float forget_bias, int spin_limit) -> ()");
+      "Tensor(i!) cnt0, Tensor(j!) cnt1, Tensor(k!) err, float forget_bias, int spin_limit, "
+      "Tensor(l!)? diag=None) -> ()");
   m.def("gru_persist_ub(int H, int B) -> int", [](int64_t H, int64_t B) -> int64_t {
     return dcr::gru_persist_ub((int)H, (int)B, num_cus());
   });

@@ -64,3 +64,39 @@ names = ["top->poll done", "poll->barrierA", "barrierA->mfma done", "mfma->barri
          "barrierB->epilogue math", "epi->drain done", "drain->next top"]
 for n, v in zip(names, dd.mean(0)):
     print(f"  {n:<26}{v:8.0f} ticks  {100*v/tot:5.1f}%")
+
+# ---- two-layer wavefront forward (lstm2_persist.hip)
+if ops.lstm2_persist_supported(H, B):
+    W1T = (torch.randn(4 * H, H, device=dev) * 0.05).to(torch.bfloat16)
+    X1T = (torch.randn(4 * H, H, device=dev) * 0.05).to(torch.bfloat16)
+    b1 = torch.zeros(4 * H, device=dev)
+    hb1 = torch.zeros_like(hbuf)
+    cb1 = torch.zeros_like(cbuf)
+    g1 = torch.empty_like(gates)
+    hl1 = torch.empty_like(hl)
+    c0 = torch.zeros(B // 32 * (T + 1) * 4, dtype=torch.int32, device=dev)
+    c1 = torch.zeros_like(c0)
+    diag2 = torch.zeros(T + 1, 8, dtype=torch.int64, device=dev)
+
+    def run2():
+        c0.zero_()
+        c1.zero_()
+        ops.lstm2_persist_fwd(WT, W1T, X1T, zx, None, b1, hbuf, cbuf, gates, hl, hb1, cb1, g1,
+                              hl1, c0, c1, err, 1.0, 1 << 22, diag2)
+    for _ in range(3):
+        run2()
+    torch.cuda.synchronize()
+    ev0.record()
+    run2()
+    ev1.record()
+    torch.cuda.synchronize()
+    d = diag2.cpu().numpy().astype("float64")
+    ms = ev0.elapsed_time(ev1)
+    tot = (d[-2, 0] - d[2, 0]) / (T - 4)
+    names2 = ["top->poll done", "poll->barrierA", "barrierA->mfma done", "mfma->barrierB",
+              "barrierB->epilogue math", "epi->drain done", "drain->next top"]
+    dd = np.diff(np.concatenate([d[2:-2, [0, 1, 2, 3, 4, 5, 6]], d[3:-1, [0]]], 1), axis=1)
+    print(f"PAIR kernel {ms*1e3/(T+1):.2f} us/tick (event); stamps {tot:.0f} ticks/tick; "
+          f"err={int(err.item())}")
+    for n, v in zip(names2, dd.mean(0)):
+        print(f"  {n:<26}{v:8.0f} ticks  {100*v/tot:5.1f}%")
