@@ -108,6 +108,8 @@ struct PersistArgs {
   unsigned spin_limit;
   int excl;              // bwd: all-loads-in-flight variant (one WG per CU: nothing may run beside it)
   int cnt_zeroed;        // counters already zeroed by the caller (batched prep launch)
+  bf16* zring;           // bwd: optional [2, B, 4H] fragment-tiled dZ hand-off ring
+                         //   (persist_common.h frag_index); dz stays row-major for the GEMMs
 };
 int lstm_persist_supported(int H, int B, int cus);
 int lstm_persist_grid(int H, int B, int cus);

@@ -488,11 +488,18 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
       STAMP(1)
       __syncthreads();
       STAMP(2)
-      const __amdgpu_buffer_rsrc_t dsrc =
-          make_rsrc(a.dz + (size_t)(t + 1) * B * G4H, sizeof(bf16) * (size_t)B * G4H);
       bf16x8 df[KS];
+      if (a.zring) {  // fragment-tiled ring: one contiguous 1 KB load per k-step
+        const __amdgpu_buffer_rsrc_t zsrc =
+            make_rsrc(a.zring + (size_t)((t + 1) & 1) * B * G4H, sizeof(bf16) * (size_t)B * G4H);
 #pragma unroll
-      for (int s = 0; s < KS; ++s) df[s] = ld8_sc1(dsrc, doff + kcol(s) * 2);
+        for (int s = 0; s < KS; ++s) df[s] = ld8_sc1(zsrc, frag_load_off(bg, kcol(s) >> 5, G4H, lane));
+      } else {
+        const __amdgpu_buffer_rsrc_t dsrc =
+            make_rsrc(a.dz + (size_t)(t + 1) * B * G4H, sizeof(bf16) * (size_t)B * G4H);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) df[s] = ld8_sc1(dsrc, doff + kcol(s) * 2);
+      }
       if constexpr (EXCL) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int ui = 0; ui < UB; ++ui)
@@ -538,16 +545,30 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
       }
       STAMP(5)
       bf16* dz = a.dz + ((size_t)t * B + b) * G4H + u0;
-      st4bf_sc1(dz, di[0], di[1], di[2], di[3]);
-      st4bf_sc1(dz + H, dj[0], dj[1], dj[2], dj[3]);
-      st4bf_sc1(dz + 2 * H, df_[0], df_[1], df_[2], df_[3]);
-      st4bf_sc1(dz + 3 * H, dO[0], dO[1], dO[2], dO[3]);
+      bf16* const zr = a.zring ? a.zring + (size_t)(t & 1) * B * G4H : nullptr;
+      if (zr) {  // handed-off copy in fragment order; row-major dz after the arrival
+        st4bf_sc1(zr + frag_index(b, u0, G4H), di[0], di[1], di[2], di[3]);
+        st4bf_sc1(zr + frag_index(b, H + u0, G4H), dj[0], dj[1], dj[2], dj[3]);
+        st4bf_sc1(zr + frag_index(b, 2 * H + u0, G4H), df_[0], df_[1], df_[2], df_[3]);
+        st4bf_sc1(zr + frag_index(b, 3 * H + u0, G4H), dO[0], dO[1], dO[2], dO[3]);
+      } else {
+        st4bf_sc1(dz, di[0], di[1], di[2], di[3]);
+        st4bf_sc1(dz + H, dj[0], dj[1], dj[2], dj[3]);
+        st4bf_sc1(dz + 2 * H, df_[0], df_[1], df_[2], df_[3]);
+        st4bf_sc1(dz + 3 * H, dO[0], dO[1], dO[2], dO[3]);
+      }
       if (t > 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         STAMP(6)
         if (lane == 0)
           __hip_atomic_fetch_add(cnt + (size_t)t * 4 + (u0 / (H / 4)), 1u, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (zr) {
+        st4bf(dz, di[0], di[1], di[2], di[3]);
+        st4bf(dz + H, dj[0], dj[1], dj[2], dj[3]);
+        st4bf(dz + 2 * H, df_[0], df_[1], df_[2], df_[3]);
+        st4bf(dz + 3 * H, dO[0], dO[1], dO[2], dO[3]);
       }
       // off the critical path (after the arrival): accumulate the bf16-rounded dz exactly as
       // the dW GEMMs will see it

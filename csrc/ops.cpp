@@ -428,7 +428,8 @@ void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& d
                       const c10::optional<at::Tensor>& ids,
                       const c10::optional<at::Tensor>& dew_part, int64_t V,
                       const c10::optional<at::Tensor>& diag, const c10::optional<at::Tensor>& Wx_above,
-                      const c10::optional<at::Tensor>& dz_above, bool exclusive, bool cnt_zeroed) {
+                      const c10::optional<at::Tensor>& dz_above, bool exclusive, bool cnt_zeroed,
+                      const c10::optional<at::Tensor>& zring) {
   check_seq(W, at::kBFloat16, "W");
   check_seq(dtop, at::kFloat, "dtop");
   check_seq(dz, at::kBFloat16, "dz");
@@ -479,6 +480,11 @@ void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& d
   }
   a.excl = exclusive ? 1 : 0;
   a.cnt_zeroed = cnt_zeroed ? 1 : 0;
+  if (has(zring)) {
+    check_seq(*zring, at::kBFloat16, "zring");
+    TORCH_CHECK(zring->numel() >= (int64_t)2 * B * 4 * H, "zring must hold [2, B, 4H]");
+    a.zring = ptr<bf16>(*zring);
+  }
   const int rc = dcr::launch_lstm_bwd_persist(a, num_cus(), cur_stream());
   TORCH_CHECK(rc == 0, "persistent LSTM BPTT not launched (", rc,
               "): grid cannot be co-resident on this GPU for H=", H, " B=", B);
@@ -782,7 +788,8 @@ TORCH_LIBRARY(dcr, m) {
       "lstm_persist_bwd(Tensor W, Tensor dtop, Tensor(a!) dz, Tensor gates, Tensor cbuf, "
       "Tensor(b!) cnt, Tensor(c!) err, int spin_limit, Tensor(d!)? db_part, Tensor? ids, "
       "Tensor(e!)? dew_part, int V, Tensor(f!)? diag=None, Tensor? Wx_above=None, "
-      "Tensor? dz_above=None, bool exclusive=False, bool cnt_zeroed=False) -> ()");
+      "Tensor? dz_above=None, bool exclusive=False, bool cnt_zeroed=False, "
+      "Tensor(g!)? zring=None) -> ()");
   m.def("head_supported(int V, int H) -> int", [](int64_t V, int64_t H) -> int64_t {
     return dcr::head_supported((int)V, (int)H);
   });

@@ -94,6 +94,21 @@ __device__ __forceinline__ bool poll_quarters2(unsigned* c0, unsigned t0, unsign
   }
 }
 
+// Fragment-tiled hand-off layout.  Element (b, k) of a [B, K] bf16 slab lives at
+//   ((b/16 * K/32 + k/32) * 64 + ((k%32)/8)*16 + b%16) * 8 + k%8        (bf16 elements)
+// i.e. exactly where mfma_f32_16x16x32_bf16's B fragment of (batch tile b/16, k-step k/32)
+// wants it: a consumer wave's load of one k-step is ONE contiguous 1 KB buffer_load (lane l at
+// byte 16*l), instead of 16 rows x 64 B of a row-major slab.  Measured with sc1 loads, 64 KB per
+// workgroup, 256 workgroups: 0.60 vs 1.74 us (half the L2 requests;
+// scripts/micro/payload_pattern.hip).  Producers' 4-unit (8 B) stores land 8-B aligned.
+__device__ __forceinline__ size_t frag_index(int b, int k, int K) {
+  return ((size_t)((b >> 4) * (K >> 5) + (k >> 5)) * 64 + ((k & 31) >> 3) * 16 + (b & 15)) * 8 +
+         (k & 7);
+}
+__device__ __forceinline__ unsigned frag_load_off(int bg, int kstep, int K, int lane) {
+  return (unsigned)((((size_t)bg * (K >> 5) + kstep) * 64 + lane) * 16);
+}
+
 // Block -> (unit block, batch group).  Speed only: place the unit-block workgroups of one batch
 // group on the same XCD under the observed round-robin dispatch (blocks b, b+8, ... share an
 // XCD; MI355X_MICROARCH.md "Workgroup dispatch"), so the batch group's hand-off payload is

@@ -299,6 +299,9 @@ class NativeBackend:
             cnt=torch.zeros(2 * self.L, 2 * (B // 16 + 1) * (T + 1) * 4, dtype=torch.int32,
                             device=dev),
             ring=torch.zeros(2 * B * (H // 2), dtype=torch.int64, device=dev),
+            # fragment-tiled dZ hand-off ring of the persistent BPTT (persist_common.h)
+            zring=(torch.empty(2 * B * GW, dtype=bf16, device=dev)
+                   if (training and os.environ.get("DCR_FRAG", "1") != "0") else None),
         )
         self._bufs[key] = bufs
         return bufs
@@ -591,7 +594,7 @@ class NativeBackend:
                                           above[0] if above else None,
                                           above[1] if above else None,
                                           exclusive=bufs["bwd_excl"] and above is None,
-                                          cnt_zeroed=True)
+                                          cnt_zeroed=True, zring=bufs["zring"])
                 if layer == 0 and pending:
                     # the last persistent grid is queued: buckets may now run beside the
                     # (non-persistent) layer-0 weight GEMMs
