@@ -145,6 +145,8 @@ struct Lstm2Args {
   unsigned* cnt1;       // [B/32, T+1, 4] arrivals of layer l+1
   unsigned* err;
   unsigned long long* diag;  // optional [T+1, 8] s_memtime stamps of workgroup 0 (diagnostics)
+  bf16* hring0;         // optional [2, B, H] fragment-tiled h hand-off rings (persist_common.h);
+  bf16* hring1;         //   the row-major hbufs are then written after the arrival
   int B, H, T;
   float forget_bias;
   unsigned spin_limit;

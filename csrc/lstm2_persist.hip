@@ -103,19 +103,28 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     // payloads: h_l[tau] (both layers' input) and h_{l+1}[tau-1]
     bf16x8 hf0[2][KS], hf1[2][KS];
     {
+      // slot 0 (initial state, written by the prep launch) is row-major; later slots come from
+      // the fragment-tiled rings: one contiguous 1 KB load per (tile, k-step)
+      const bool ring0 = a.hring0 && tau > 0, ring1 = a.hring1 && tau > 1;
       const __amdgpu_buffer_rsrc_t r0 =
-          make_rsrc(a.hbuf0 + (size_t)tau * B * H, sizeof(bf16) * (size_t)B * H);
+          ring0 ? make_rsrc(a.hring0 + (size_t)(tau & 1) * B * H, sizeof(bf16) * (size_t)B * H)
+                : make_rsrc(a.hbuf0 + (size_t)tau * B * H, sizeof(bf16) * (size_t)B * H);
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int s = 0; s < KS; ++s) hf0[j][s] = ld8_sc1(r0, hoff[j] + s * 64);
+        for (int s = 0; s < KS; ++s)
+          hf0[j][s] = ld8_sc1(r0, ring0 ? frag_load_off(2 * bg + j, w * KS + s, H, lane)
+                                        : hoff[j] + s * 64);
       if (on1) {
         const __amdgpu_buffer_rsrc_t r1 =
-            make_rsrc(a.hbuf1 + (size_t)(tau - 1) * B * H, sizeof(bf16) * (size_t)B * H);
+            ring1 ? make_rsrc(a.hring1 + (size_t)((tau - 1) & 1) * B * H, sizeof(bf16) * (size_t)B * H)
+                  : make_rsrc(a.hbuf1 + (size_t)(tau - 1) * B * H, sizeof(bf16) * (size_t)B * H);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-          for (int s = 0; s < KS; ++s) hf1[j][s] = ld8_sc1(r1, hoff[j] + s * 64);
+          for (int s = 0; s < KS; ++s)
+            hf1[j][s] = ld8_sc1(r1, ring1 ? frag_load_off(2 * bg + j, w * KS + s, H, lane)
+                                          : hoff[j] + s * 64);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -179,7 +188,11 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
       }
       const size_t o = (size_t)(t + 1) * B * H + bh;
       STAMP2(5)
-      st4bf_sc1(hbL + o, h[0], h[1], h[2], h[3]);
+      bf16* const ringL = L ? a.hring1 : a.hring0;
+      if (ringL)
+        st4bf_sc1(ringL + (size_t)((t + 1) & 1) * B * H + frag_index(b, u0, H), h[0], h[1], h[2], h[3]);
+      else
+        st4bf_sc1(hbL + o, h[0], h[1], h[2], h[3]);
       // layer l's slot t+1 feeds both layers (up to slot T); layer l+1's slot t+1 only itself
       if (L == 0 || t + 1 < T) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -188,6 +201,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
           __hip_atomic_fetch_add(cntL + (size_t)(t + 1) * 4 + (u0 / (H / 4)), 1u,
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      if (ringL) st4bf(hbL + o, h[0], h[1], h[2], h[3]);  // row-major copy for the GEMMs
       *reinterpret_cast<float4*>(cbL + o) = make_float4(c[0], c[1], c[2], c[3]);
       if (gtL) {
         bf16* gp = gtL + ((size_t)t * B + b) * 4 * H + u0;

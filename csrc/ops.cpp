@@ -500,7 +500,9 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
                        at::Tensor& hbuf1, at::Tensor& cbuf1,
                        const c10::optional<at::Tensor>& gates1, at::Tensor& hlast1,
                        at::Tensor& cnt0, at::Tensor& cnt1, at::Tensor& err, double forget_bias,
-                       int64_t spin_limit, const c10::optional<at::Tensor>& diag) {
+                       int64_t spin_limit, const c10::optional<at::Tensor>& diag,
+                       const c10::optional<at::Tensor>& hring0,
+                       const c10::optional<at::Tensor>& hring1) {
   for (auto* t : {&W0T, &W1T, &X1T}) check_seq(*t, at::kBFloat16, "W");
   check_seq(zx0, at::kFloat, "zx0");
   check_seq(bias1, at::kFloat, "bias1");
@@ -548,6 +550,14 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
                 "diag must hold [T+1, 8] int64");
     a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());
   }
+  for (auto* r : {&hring0, &hring1})
+    if (has(*r)) {
+      check_seq(**r, at::kBFloat16, "hring");
+      TORCH_CHECK((*r)->numel() >= (int64_t)2 * B * H, "hring must hold [2, B, H]");
+    }
+  TORCH_CHECK(has(hring0) == has(hring1), "pass both hand-off rings or neither");
+  a.hring0 = optr<bf16>(hring0);
+  a.hring1 = optr<bf16>(hring1);
   const int rc = dcr::launch_lstm2_fwd_persist(a, num_cus(), cur_stream());
   TORCH_CHECK(rc == 0, "two-layer persistent LSTM forward not launched (", rc, ")");
 }
@@ -812,7 +822,7 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor bias1, Tensor(a!) hbuf0, Tensor(b!) cbuf0, Tensor(c!)? gates0, Tensor(d!) hlast0, "
       "Tensor(e!) hbuf1, Tensor(f!) cbuf1, Tensor(g!)? gates1, Tensor(h!) hlast1, "
       "Tensor(i!) cnt0, Tensor(j!) cnt1, Tensor(k!) err, float forget_bias, int spin_limit, "
-      "Tensor(l!)? diag=None) -> ()");
+      "Tensor(l!)? diag=None, Tensor(m!)? hring0=None, Tensor(n!)? hring1=None) -> ()");
   m.def("gru_persist_ub(int H, int B) -> int", [](int64_t H, int64_t B) -> int64_t {
     return dcr::gru_persist_ub((int)H, (int)B, num_cus());
   });

@@ -299,6 +299,10 @@ class NativeBackend:
             cnt=torch.zeros(2 * self.L, 2 * (B // 16 + 1) * (T + 1) * 4, dtype=torch.int32,
                             device=dev),
             ring=torch.zeros(2 * B * (H // 2), dtype=torch.int64, device=dev),
+            # fragment-tiled h hand-off rings of the wavefront forward (persist_common.h)
+            hrings=((torch.empty(2 * B * H, dtype=bf16, device=dev),
+                     torch.empty(2 * B * H, dtype=bf16, device=dev))
+                    if os.environ.get("DCR_FRAG", "1") != "0" else None),
             # fragment-tiled dZ hand-off ring of the persistent BPTT (persist_common.h)
             zring=(torch.empty(2 * B * GW, dtype=bf16, device=dev)
                    if (training and os.environ.get("DCR_FRAG", "1") != "0") else None),
@@ -478,7 +482,8 @@ class NativeBackend:
                                            lb.hbuf, lb.cbuf, lb.gates, lb.hlast32,
                                            lb1.hbuf, lb1.cbuf, lb1.gates, lb1.hlast32,
                                            bufs["cnt"][layer], bufs["cnt"][layer + 1], self.err,
-                                           FORGET_BIAS, self.spin_limit)
+                                           FORGET_BIAS, self.spin_limit, None,
+                                           *(bufs["hrings"] or (None, None)))
                 lb1.x_in = lb.hbuf[1:].reshape(N, H)
                 x_prev = lb1.hbuf[1:]
                 paired = layer + 1
