@@ -84,11 +84,14 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
       __syncthreads();
     }
     {
+      const bool fr = a.ring0 && t > 0;  // slot 0 (initial state) is row-major
       const __amdgpu_buffer_rsrc_t src =
-          make_rsrc(a.hbuf + (size_t)t * B * H, sizeof(bf16) * (size_t)B * H);
+          fr ? make_rsrc(a.ring0 + (size_t)(t & 1) * B * H, sizeof(bf16) * (size_t)B * H)
+             : make_rsrc(a.hbuf + (size_t)t * B * H, sizeof(bf16) * (size_t)B * H);
       bf16x8 hf[KS];
 #pragma unroll
-      for (int s = 0; s < KS; ++s) hf[s] = ld8_sc1(src, hoff + s * 64);
+      for (int s = 0; s < KS; ++s)
+        hf[s] = ld8_sc1(src, fr ? frag_load_off(bg, w * KS + s, H, lane) : hoff + s * 64);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int ui = 0; ui < UB; ++ui) {
@@ -118,12 +121,16 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
         o[2] = sigmoidf_(s0.z + s1.z + s2.z + s3.z + zx[g][2]);
         o[3] = sigmoidf_(s0.w + s1.w + s2.w + s3.w + zx[g][3]);
       }
-      st4bf_sc1(a.rh + (size_t)t * B * H + bh, rr[0] * hp[0], rr[1] * hp[1], rr[2] * hp[2],
-                rr[3] * hp[3]);
+      const float rh0 = rr[0] * hp[0], rh1 = rr[1] * hp[1], rh2 = rr[2] * hp[2], rh3 = rr[3] * hp[3];
+      if (a.ring1)
+        st4bf_sc1(a.ring1 + (size_t)(t & 1) * B * H + frag_index(b, u0, H), rh0, rh1, rh2, rh3);
+      else
+        st4bf_sc1(a.rh + (size_t)t * B * H + bh, rh0, rh1, rh2, rh3);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0)
         __hip_atomic_fetch_add(cntR + (size_t)t * 4 + (u0 / (H / 4)), 1u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+      if (a.ring1) st4bf(a.rh + (size_t)t * B * H + bh, rh0, rh1, rh2, rh3);
       bf16* gp = a.gates + ((size_t)t * B + b) * G3 + u0;
       st4bf(gp, rr[0], rr[1], rr[2], rr[3]);
       st4bf(gp + H, uu[0], uu[1], uu[2], uu[3]);
@@ -134,10 +141,12 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
     __syncthreads();
     {
       const __amdgpu_buffer_rsrc_t src =
-          make_rsrc(a.rh + (size_t)t * B * H, sizeof(bf16) * (size_t)B * H);
+          a.ring1 ? make_rsrc(a.ring1 + (size_t)(t & 1) * B * H, sizeof(bf16) * (size_t)B * H)
+                  : make_rsrc(a.rh + (size_t)t * B * H, sizeof(bf16) * (size_t)B * H);
       bf16x8 rf[KS];
 #pragma unroll
-      for (int s = 0; s < KS; ++s) rf[s] = ld8_sc1(src, hoff + s * 64);
+      for (int s = 0; s < KS; ++s)
+        rf[s] = ld8_sc1(src, a.ring1 ? frag_load_off(bg, w * KS + s, H, lane) : hoff + s * 64);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int ui = 0; ui < UB; ++ui) {
@@ -162,13 +171,18 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
 #pragma unroll
       for (int r = 0; r < 4; ++r) h[r] = uu[r] * hp[r] + (1.f - uu[r]) * cc[r];
       const size_t o = (size_t)(t + 1) * B * H + bh;
-      st4bf_sc1(a.hbuf + o, h[0], h[1], h[2], h[3]);
+      if (a.ring0)
+        st4bf_sc1(a.ring0 + (size_t)((t + 1) & 1) * B * H + frag_index(b, u0, H), h[0], h[1],
+                  h[2], h[3]);
+      else
+        st4bf_sc1(a.hbuf + o, h[0], h[1], h[2], h[3]);
       if (t + 1 < T) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0)
           __hip_atomic_fetch_add(cntH + (size_t)(t + 1) * 4 + (u0 / (H / 4)), 1u,
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      if (a.ring0) st4bf(a.hbuf + o, h[0], h[1], h[2], h[3]);
       *reinterpret_cast<float4*>(a.h32 + o) = make_float4(h[0], h[1], h[2], h[3]);
       st4bf(a.gates + ((size_t)t * B + b) * G3 + 2 * H + u0, cc[0], cc[1], cc[2], cc[3]);
       if (t == T - 1 && a.hlast32)
@@ -231,15 +245,19 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
     const bf16* gp = a.gates + ((size_t)(T - 1) * B + b) * G3 + u0;
     ld4bf(gp + H, uu);
     ld4bf(gp + 2 * H, cc);
-    st4bf_sc1(a.dz + ((size_t)(T - 1) * B + b) * G3 + 2 * H + u0,
-              dhp[0] * (1.f - uu[0]) * (1.f - cc[0] * cc[0]),
-              dhp[1] * (1.f - uu[1]) * (1.f - cc[1] * cc[1]),
-              dhp[2] * (1.f - uu[2]) * (1.f - cc[2] * cc[2]),
-              dhp[3] * (1.f - uu[3]) * (1.f - cc[3] * cc[3]));
+    float z0[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) z0[r] = dhp[r] * (1.f - uu[r]) * (1.f - cc[r] * cc[r]);
+    bf16* const zrow = a.dz + ((size_t)(T - 1) * B + b) * G3 + 2 * H + u0;
+    if (a.ring0)
+      st4bf_sc1(a.ring0 + (size_t)((T - 1) & 1) * B * H + frag_index(b, u0, H), z0[0], z0[1], z0[2], z0[3]);
+    else
+      st4bf_sc1(zrow, z0[0], z0[1], z0[2], z0[3]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0)
       __hip_atomic_fetch_add(cntC + (size_t)(T - 1) * 4 + (u0 / (H / 4)), 1u, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
+    if (a.ring0) st4bf(zrow, z0[0], z0[1], z0[2], z0[3]);
   }
 
   for (int t = T - 1; t >= 0; --t) {
@@ -263,8 +281,15 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
     __syncthreads();
     {
       bf16x8 zf[KA];
+      if (a.ring0) {
+        const __amdgpu_buffer_rsrc_t rc =
+            make_rsrc(a.ring0 + (size_t)(t & 1) * B * H, sizeof(bf16) * (size_t)B * H);
 #pragma unroll
-      for (int s = 0; s < KA; ++s) zf[s] = ld8_sc1(zsrc, offA + s * 64);
+        for (int s = 0; s < KA; ++s) zf[s] = ld8_sc1(rc, frag_load_off(bg, w * KA + s, H, lane));
+      } else {
+#pragma unroll
+        for (int s = 0; s < KA; ++s) zf[s] = ld8_sc1(zsrc, offA + s * 64);
+      }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int ui = 0; ui < UB; ++ui) {
@@ -293,13 +318,23 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
         P[r] = dhp[r] * uu[r] + drh[r] * rr[r];
       }
       bf16* dz = a.dz + ((size_t)t * B + b) * G3 + u0;
-      st4bf_sc1(dz, dzr[0], dzr[1], dzr[2], dzr[3]);
-      st4bf_sc1(dz + H, dzu[0], dzu[1], dzu[2], dzu[3]);
+      if (a.ring1) {
+        bf16* gr = a.ring1 + (size_t)(t & 1) * B * 2 * H;
+        st4bf_sc1(gr + frag_index(b, u0, 2 * H), dzr[0], dzr[1], dzr[2], dzr[3]);
+        st4bf_sc1(gr + frag_index(b, H + u0, 2 * H), dzu[0], dzu[1], dzu[2], dzu[3]);
+      } else {
+        st4bf_sc1(dz, dzr[0], dzr[1], dzr[2], dzr[3]);
+        st4bf_sc1(dz + H, dzu[0], dzu[1], dzu[2], dzu[3]);
+      }
       if (t > 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0)
           __hip_atomic_fetch_add(cntG + (size_t)t * 4 + (u0 / (H / 4)), 1u, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (a.ring1) {
+        st4bf(dz, dzr[0], dzr[1], dzr[2], dzr[3]);
+        st4bf(dz + H, dzu[0], dzu[1], dzu[2], dzu[3]);
       }
     }
     if (t == 0) break;  // dh'_{-1} (the initial state's gradient) is not needed
@@ -309,8 +344,15 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
     __syncthreads();
     {
       bf16x8 zf[KB];
+      if (a.ring1) {
+        const __amdgpu_buffer_rsrc_t rg =
+            make_rsrc(a.ring1 + (size_t)(t & 1) * B * 2 * H, sizeof(bf16) * (size_t)B * 2 * H);
 #pragma unroll
-      for (int s = 0; s < KB; ++s) zf[s] = ld8_sc1(zsrc, offB + s * 64);
+        for (int s = 0; s < KB; ++s) zf[s] = ld8_sc1(rg, frag_load_off(bg, w * KB + s, 2 * H, lane));
+      } else {
+#pragma unroll
+        for (int s = 0; s < KB; ++s) zf[s] = ld8_sc1(zsrc, offB + s * 64);
+      }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int ui = 0; ui < UB; ++ui) {
@@ -334,12 +376,17 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
       float dzc[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) dzc[r] = dhp[r] * (1.f - up[r]) * (1.f - cp[r] * cp[r]);
-      st4bf_sc1(a.dz + ((size_t)(t - 1) * B + b) * G3 + 2 * H + u0, dzc[0], dzc[1], dzc[2],
-                dzc[3]);
+      bf16* const crow = a.dz + ((size_t)(t - 1) * B + b) * G3 + 2 * H + u0;
+      if (a.ring0)
+        st4bf_sc1(a.ring0 + (size_t)((t - 1) & 1) * B * H + frag_index(b, u0, H), dzc[0], dzc[1],
+                  dzc[2], dzc[3]);
+      else
+        st4bf_sc1(crow, dzc[0], dzc[1], dzc[2], dzc[3]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0)
         __hip_atomic_fetch_add(cntC + (size_t)(t - 1) * 4 + (u0 / (H / 4)), 1u,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (a.ring0) st4bf(crow, dzc[0], dzc[1], dzc[2], dzc[3]);
     }
   }
 }

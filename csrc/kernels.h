@@ -108,6 +108,7 @@ struct PersistArgs {
   unsigned spin_limit;
   int excl;              // bwd: all-loads-in-flight variant (one WG per CU: nothing may run beside it)
   int cnt_zeroed;        // counters already zeroed by the caller (batched prep launch)
+  bf16* hring;           // fwd: optional [2, B, H] fragment-tiled h hand-off ring
   bf16* zring;           // bwd: optional [2, B, 4H] fragment-tiled dZ hand-off ring
                          //   (persist_common.h frag_index); dz stays row-major for the GEMMs
 };
@@ -172,6 +173,8 @@ struct GruPersistArgs {
   bf16* dz;             // bwd: [T, B, 3H] dZr, dZu, dZc
   unsigned* cnt;        // 2 sets x [B/16, T+1, 4] counters
   unsigned* err;
+  bf16* ring0;          // optional fragment-tiled hand-off rings (persist_common.h):
+  bf16* ring1;          //   fwd: h [2,B,H], r⊙h [2,B,H];  bwd: dZc [2,B,H], dZg [2,B,2H]
   int B, H, T;
   unsigned spin_limit;
   int cnt_zeroed;

@@ -144,11 +144,14 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
     }
     STAMP(2)
     // h_{t-1} fragments (handed off by other workgroups: sc1 loads only)
+    const bool fring = a.hring && t > 0;  // slot 0 (initial state) is row-major
     const __amdgpu_buffer_rsrc_t hsrc =
-        make_rsrc(a.hbuf + (size_t)t * B * H, sizeof(bf16) * (size_t)B * H);
+        fring ? make_rsrc(a.hring + (size_t)(t & 1) * B * H, sizeof(bf16) * (size_t)B * H)
+              : make_rsrc(a.hbuf + (size_t)t * B * H, sizeof(bf16) * (size_t)B * H);
     bf16x8 hf[KS];
 #pragma unroll
-    for (int s = 0; s < KS; ++s) hf[s] = ld8_sc1(hsrc, hoff + s * 64);
+    for (int s = 0; s < KS; ++s)
+      hf[s] = ld8_sc1(hsrc, fring ? frag_load_off(bg, w * KS + s, H, lane) : hoff + s * 64);
     __builtin_amdgcn_sched_barrier(0);  // keep all KS hand-off loads in flight together
 #pragma unroll
     for (int ui = 0; ui < UB; ++ui) {
@@ -189,7 +192,11 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
       }
       const size_t o = (size_t)(t + 1) * B * H + bh;
       STAMP(5)
-      st4bf_sc1(a.hbuf + o, h[0], h[1], h[2], h[3]);  // handed off: write-through
+      if (a.hring)  // handed off in fragment order (write-through); row-major copy below
+        st4bf_sc1(a.hring + (size_t)((t + 1) & 1) * B * H + frag_index(b, u0, H), h[0], h[1],
+                  h[2], h[3]);
+      else
+        st4bf_sc1(a.hbuf + o, h[0], h[1], h[2], h[3]);  // handed off: write-through
       if (t + 1 < T) {
         // each epilogue wave publishes its own 16-unit slab: drain ONLY the hand-off store
         // (the activation-cache stores below are issued after the arrival, so the wait does
@@ -200,6 +207,7 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
           __hip_atomic_fetch_add(cnt + (size_t)(t + 1) * 4 + (u0 / (H / 4)), 1u, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
       }
+      if (a.hring) st4bf(a.hbuf + o, h[0], h[1], h[2], h[3]);
       *reinterpret_cast<float4*>(a.cbuf + o) = make_float4(c[0], c[1], c[2], c[3]);
       if (a.gates) {
         bf16* gp = a.gates + ((size_t)t * B + b) * 4 * H + u0;

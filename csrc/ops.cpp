@@ -358,7 +358,7 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
                       int64_t spin_limit, const c10::optional<at::Tensor>& ring,
                       const c10::optional<at::Tensor>& diag, const c10::optional<at::Tensor>& WxT,
                       const c10::optional<at::Tensor>& xin, const c10::optional<at::Tensor>& bias,
-                      bool cnt_zeroed) {
+                      bool cnt_zeroed, const c10::optional<at::Tensor>& hring) {
   check_seq(WT, at::kBFloat16, "WT");
   check_seq(zx, at::kFloat, "zx");
   check_seq(hbuf, at::kBFloat16, "hbuf");
@@ -417,6 +417,12 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
     a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());
   }
   a.cnt_zeroed = cnt_zeroed ? 1 : 0;
+  if (has(hring)) {
+    TORCH_CHECK(!has(ring), "the fragment ring and the granule hand-off are exclusive");
+    check_seq(*hring, at::kBFloat16, "hring");
+    TORCH_CHECK(hring->numel() >= (int64_t)2 * B * H, "hring must hold [2, B, H]");
+    a.hring = ptr<bf16>(*hring);
+  }
   const int rc = dcr::launch_lstm_fwd_persist(a, num_cus(), cur_stream());
   TORCH_CHECK(rc == 0, "persistent LSTM forward not launched (", rc,
               "): grid cannot be co-resident on this GPU for H=", H, " B=", B);
@@ -567,7 +573,17 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
 // ------------------------------------------------------------------------------------------
 static void gru_common(dcr::GruPersistArgs& a, const at::Tensor& gates, const at::Tensor& h32,
                        at::Tensor& cnt, at::Tensor& err, int64_t spin_limit, bool cnt_zeroed,
-                       int T, int B, int H) {
+                       int T, int B, int H, const c10::optional<at::Tensor>& ring0,
+                       const c10::optional<at::Tensor>& ring1, int64_t w1) {
+  TORCH_CHECK(has(ring0) == has(ring1), "pass both hand-off rings or neither");
+  if (has(ring0)) {
+    check_seq(*ring0, at::kBFloat16, "ring0");
+    check_seq(*ring1, at::kBFloat16, "ring1");
+    TORCH_CHECK(ring0->numel() >= (int64_t)2 * B * H && ring1->numel() >= 2 * B * w1,
+                "hand-off rings too small");
+    a.ring0 = ptr<bf16>(*ring0);
+    a.ring1 = ptr<bf16>(*ring1);
+  }
   check_seq(gates, at::kBFloat16, "gates");
   check_seq(h32, at::kFloat, "h32");
   TORCH_CHECK(gates.numel() == (int64_t)T * B * 3 * H, "gates must be [T, B, 3H]");
@@ -589,7 +605,8 @@ static void gru_common(dcr::GruPersistArgs& a, const at::Tensor& gates, const at
 void gru_persist_fwd(const at::Tensor& WgT, const at::Tensor& WcT, const at::Tensor& zx,
                      const c10::optional<at::Tensor>& ids, at::Tensor& hbuf, at::Tensor& h32,
                      at::Tensor& rh, at::Tensor& gates, const c10::optional<at::Tensor>& hlast32,
-                     at::Tensor& cnt, at::Tensor& err, int64_t spin_limit, bool cnt_zeroed) {
+                     at::Tensor& cnt, at::Tensor& err, int64_t spin_limit, bool cnt_zeroed,
+                     const c10::optional<at::Tensor>& ring0, const c10::optional<at::Tensor>& ring1) {
   check_seq(WgT, at::kBFloat16, "WgT");
   check_seq(WcT, at::kBFloat16, "WcT");
   check_seq(zx, at::kFloat, "zx");
@@ -609,7 +626,7 @@ void gru_persist_fwd(const at::Tensor& WgT, const at::Tensor& WcT, const at::Ten
   TORCH_CHECK(rh.numel() == (int64_t)T * B * H, "rh must be [T, B, H]");
   if (has(hlast32)) TORCH_CHECK(hlast32->numel() == (int64_t)B * H, "hlast32 must be [B, H]");
   dcr::GruPersistArgs a{};
-  gru_common(a, gates, h32, cnt, err, spin_limit, cnt_zeroed, T, B, H);
+  gru_common(a, gates, h32, cnt, err, spin_limit, cnt_zeroed, T, B, H, ring0, ring1, H);
   a.WgT = ptr<bf16>(WgT);
   a.WcT = ptr<bf16>(WcT);
   a.zx = ptr<float>(zx);
@@ -624,7 +641,8 @@ void gru_persist_fwd(const at::Tensor& WgT, const at::Tensor& WcT, const at::Ten
 
 void gru_persist_bwd(const at::Tensor& Wg, const at::Tensor& Wc, const at::Tensor& dtop,
                      at::Tensor& dz, const at::Tensor& gates, const at::Tensor& h32,
-                     at::Tensor& cnt, at::Tensor& err, int64_t spin_limit, bool cnt_zeroed) {
+                     at::Tensor& cnt, at::Tensor& err, int64_t spin_limit, bool cnt_zeroed,
+                     const c10::optional<at::Tensor>& ring0, const c10::optional<at::Tensor>& ring1) {
   check_seq(Wg, at::kBFloat16, "Wg");
   check_seq(Wc, at::kBFloat16, "Wc");
   check_seq(dtop, at::kFloat, "dtop");
@@ -635,7 +653,7 @@ void gru_persist_bwd(const at::Tensor& Wg, const at::Tensor& Wc, const at::Tenso
   TORCH_CHECK(Wc.size(0) == H && Wc.size(1) == H, "Wc must be [H, H]");
   TORCH_CHECK(dz.numel() == (int64_t)T * B * 3 * H, "dz must be [T, B, 3H]");
   dcr::GruPersistArgs a{};
-  gru_common(a, gates, h32, cnt, err, spin_limit, cnt_zeroed, T, B, H);
+  gru_common(a, gates, h32, cnt, err, spin_limit, cnt_zeroed, T, B, H, ring0, ring1, 2 * H);
   a.Wg = ptr<bf16>(Wg);
   a.Wc = ptr<bf16>(Wc);
   a.dtop = ptr<float>(dtop);
@@ -793,7 +811,7 @@ TORCH_LIBRARY(dcr, m) {
       "lstm_persist_fwd(Tensor WT, Tensor zx, Tensor? ids, Tensor(a!) hbuf, Tensor(b!) cbuf, "
       "Tensor(c!)? gates, Tensor(d!) hlast32, Tensor(e!) cnt, Tensor(f!) err, float forget_bias, "
       "int spin_limit, Tensor(g!)? ring, Tensor(h!)? diag=None, Tensor? WxT=None, Tensor? xin=None, "
-      "Tensor? bias=None, bool cnt_zeroed=False) -> ()");
+      "Tensor? bias=None, bool cnt_zeroed=False, Tensor(i!)? hring=None) -> ()");
   m.def(
       "lstm_persist_bwd(Tensor W, Tensor dtop, Tensor(a!) dz, Tensor gates, Tensor cbuf, "
       "Tensor(b!) cnt, Tensor(c!) err, int spin_limit, Tensor(d!)? db_part, Tensor? ids, "
@@ -829,10 +847,12 @@ TORCH_LIBRARY(dcr, m) {
   m.def(
       "gru_persist_fwd(Tensor WgT, Tensor WcT, Tensor zx, Tensor? ids, Tensor(a!) hbuf, "
       "Tensor(b!) h32, Tensor(c!) rh, Tensor(d!) gates, Tensor(e!)? hlast32, Tensor(f!) cnt, "
-      "Tensor(g!) err, int spin_limit, bool cnt_zeroed=False) -> ()");
+      "Tensor(g!) err, int spin_limit, bool cnt_zeroed=False, Tensor(h!)? ring0=None, "
+      "Tensor(i!)? ring1=None) -> ()");
   m.def(
       "gru_persist_bwd(Tensor Wg, Tensor Wc, Tensor dtop, Tensor(a!) dz, Tensor gates, "
-      "Tensor h32, Tensor(b!) cnt, Tensor(c!) err, int spin_limit, bool cnt_zeroed=False) -> ()");
+      "Tensor h32, Tensor(b!) cnt, Tensor(c!) err, int spin_limit, bool cnt_zeroed=False, "
+      "Tensor(d!)? ring0=None, Tensor(e!)? ring1=None) -> ()");
   m.def("segsum(Tensor X, Tensor? ids, int V, Tensor(a!) out, Tensor(b!) workspace, bool accumulate) -> ()");
   m.def("segsum_workspace(int N, int W, int V) -> int", [](int64_t N, int64_t W, int64_t V) -> int64_t {
     return (int64_t)dcr::segsum_workspace_floats((int)N, (int)W, (int)V);

@@ -299,6 +299,11 @@ class NativeBackend:
             cnt=torch.zeros(2 * self.L, 2 * (B // 16 + 1) * (T + 1) * 4, dtype=torch.int32,
                             device=dev),
             ring=torch.zeros(2 * B * (H // 2), dtype=torch.int64, device=dev),
+            # fragment-tiled hand-off rings of the persistent GRU: [h or dZc, r⊙h, dZg]
+            grings=((torch.empty(2 * B * H, dtype=bf16, device=dev),
+                     torch.empty(2 * B * H, dtype=bf16, device=dev),
+                     torch.empty(2 * B * 2 * H, dtype=bf16, device=dev))
+                    if (m == "gru" and os.environ.get("DCR_FRAG", "1") != "0") else None),
             # fragment-tiled h hand-off rings of the wavefront forward (persist_common.h)
             hrings=((torch.empty(2 * B * H, dtype=bf16, device=dev),
                      torch.empty(2 * B * H, dtype=bf16, device=dev))
@@ -455,7 +460,8 @@ class NativeBackend:
                 self.ops.lstm_persist_fwd(lw.WhT, lw.bias, None, lb.hbuf, lb.cbuf, lb.gates,
                                           lb.hlast32, bufs["cnt"][layer], self.err, FORGET_BIAS,
                                           self.spin_limit, None, None, lw.WxT, x_prev, lw.bias,
-                                          cnt_zeroed=True)
+                                          cnt_zeroed=True,
+                                          hring=bufs["hrings"][0] if bufs["hrings"] else None)
                 x_prev = lb.hbuf[1:]
                 continue
             if gather:
@@ -493,11 +499,15 @@ class NativeBackend:
                                           lb.hlast32, bufs["cnt"][layer], self.err, FORGET_BIAS,
                                           self.spin_limit,
                                           bufs["ring"] if self.handoff == "granule" else None,
-                                          cnt_zeroed=True)
+                                          cnt_zeroed=True,
+                                          hring=(bufs["hrings"][0] if bufs["hrings"]
+                                                 and self.handoff != "granule" else None))
             elif bufs["gru_persist"]:
+                gr = bufs["grings"]
                 self.ops.gru_persist_fwd(lw.WhT, lw.WT2, zx, ids_arg, lb.hbuf, lb.h32, lb.rh,
                                          lb.gates, None, bufs["cnt"][layer], self.err,
-                                         self.spin_limit, cnt_zeroed=True)
+                                         self.spin_limit, cnt_zeroed=True,
+                                         ring0=gr[0] if gr else None, ring1=gr[1] if gr else None)
             else:
                 self.ops.rnn_fwd_seq(self.cell, lw.WhT, lw.WT2, zx, ids_arg, lb.hbuf, lb.h32,
                                      lb.cbuf, lb.gates, lb.pre, lb.aux, lb.rh, lb.hlast32,
@@ -607,9 +617,11 @@ class NativeBackend:
                         user_ready(off)
                     pending.clear()
             elif bufs["gru_persist"]:
+                gr = bufs["grings"]
                 self.ops.gru_persist_bwd(lw.W2, lw.Wh, dtop, lb.dz, lb.gates, lb.h32,
                                          bufs["cnt"][self.L + layer], self.err, self.spin_limit,
-                                         cnt_zeroed=True)
+                                         cnt_zeroed=True, ring0=gr[0] if gr else None,
+                                         ring1=gr[2] if gr else None)
                 if layer == 0 and pending:
                     for off in pending:
                         user_ready(off)
