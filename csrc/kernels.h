@@ -88,6 +88,7 @@ struct PersistArgs {
   float* cbuf;           // [T+1, B, H] fp32 (slot 0 = c_0)
   bf16* gates;           // [T, B, 4H] bf16 activation cache (sigma(i), tanh(j), sigma(f), sigma(o))
   float* hlast32;        // [B, H] fp32 final h
+  float* clast32;        // optional [B, H] fp32 final c (the new TBPTT state without a copy)
   const float* dtop;     // bwd: [T, B, H] fp32 gradient from above
   bf16* dz;              // bwd: [T, B, 4H] bf16 gate-pre-activation gradients
   float* db_part;        // bwd: [B/16, 4H] per-batch-group bias-gradient partials (or nullptr)
@@ -146,6 +147,8 @@ struct Lstm2Args {
   unsigned* cnt1;       // [B/32, T+1, 4] arrivals of layer l+1
   unsigned* err;
   unsigned long long* diag;  // optional [T+1, 8] s_memtime stamps of workgroup 0 (diagnostics)
+  float* clast0;        // optional [B, H] final c of layers l and l+1
+  float* clast1;
   bf16* hring0;         // optional [2, B, H] fragment-tiled h hand-off rings (persist_common.h);
   bf16* hring1;         //   the row-major hbufs are then written after the arrival
   int B, H, T;

@@ -70,6 +70,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
   float* const cbL = L ? a.cbuf1 : a.cbuf0;
   bf16* const gtL = L ? a.gates1 : a.gates0;
   float* const hlL = L ? a.hlast1 : a.hlast0;
+  float* const clL = L ? a.clast1 : a.clast0;
   unsigned* const cntL = L ? cnt1 : cnt0;
   float c[4];
   ld4f(cbL + bh, c);
@@ -212,6 +213,8 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
       }
       if (t == T - 1 && hlL)
         *reinterpret_cast<float4*>(hlL + bh) = make_float4(h[0], h[1], h[2], h[3]);
+      if (t == T - 1 && clL)
+        *reinterpret_cast<float4*>(clL + bh) = make_float4(c[0], c[1], c[2], c[3]);
     }
   }
 }

@@ -218,6 +218,8 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
       }
       if (t == T - 1 && a.hlast32)
         *reinterpret_cast<float4*>(a.hlast32 + bh) = make_float4(h[0], h[1], h[2], h[3]);
+      if (t == T - 1 && a.clast32)
+        *reinterpret_cast<float4*>(a.clast32 + bh) = make_float4(c[0], c[1], c[2], c[3]);
     }
   }
 }
@@ -388,6 +390,8 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_granule_kernel(PersistArgs a)
       }
       if (t == T - 1 && a.hlast32)
         *reinterpret_cast<float4*>(a.hlast32 + bh) = make_float4(h[0], h[1], h[2], h[3]);
+      if (t == T - 1 && a.clast32)
+        *reinterpret_cast<float4*>(a.clast32 + bh) = make_float4(c[0], c[1], c[2], c[3]);
     }
   }
 }

@@ -358,7 +358,8 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
                       int64_t spin_limit, const c10::optional<at::Tensor>& ring,
                       const c10::optional<at::Tensor>& diag, const c10::optional<at::Tensor>& WxT,
                       const c10::optional<at::Tensor>& xin, const c10::optional<at::Tensor>& bias,
-                      bool cnt_zeroed, const c10::optional<at::Tensor>& hring) {
+                      bool cnt_zeroed, const c10::optional<at::Tensor>& hring,
+                      const c10::optional<at::Tensor>& clast32) {
   check_seq(WT, at::kBFloat16, "WT");
   check_seq(zx, at::kFloat, "zx");
   check_seq(hbuf, at::kBFloat16, "hbuf");
@@ -417,6 +418,11 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
     a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());
   }
   a.cnt_zeroed = cnt_zeroed ? 1 : 0;
+  if (has(clast32)) {
+    check_seq(*clast32, at::kFloat, "clast32");
+    TORCH_CHECK(clast32->numel() == (int64_t)B * H, "clast32 must be [B, H]");
+    a.clast32 = ptr<float>(*clast32);
+  }
   if (has(hring)) {
     TORCH_CHECK(!has(ring), "the fragment ring and the granule hand-off are exclusive");
     check_seq(*hring, at::kBFloat16, "hring");
@@ -508,7 +514,9 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
                        at::Tensor& cnt0, at::Tensor& cnt1, at::Tensor& err, double forget_bias,
                        int64_t spin_limit, const c10::optional<at::Tensor>& diag,
                        const c10::optional<at::Tensor>& hring0,
-                       const c10::optional<at::Tensor>& hring1) {
+                       const c10::optional<at::Tensor>& hring1,
+                       const c10::optional<at::Tensor>& clast0,
+                       const c10::optional<at::Tensor>& clast1) {
   for (auto* t : {&W0T, &W1T, &X1T}) check_seq(*t, at::kBFloat16, "W");
   check_seq(zx0, at::kFloat, "zx0");
   check_seq(bias1, at::kFloat, "bias1");
@@ -564,6 +572,13 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
   TORCH_CHECK(has(hring0) == has(hring1), "pass both hand-off rings or neither");
   a.hring0 = optr<bf16>(hring0);
   a.hring1 = optr<bf16>(hring1);
+  for (auto* c : {&clast0, &clast1})
+    if (has(*c)) {
+      check_seq(**c, at::kFloat, "clast");
+      TORCH_CHECK((*c)->numel() == (int64_t)B * H, "clast must be [B, H]");
+    }
+  a.clast0 = optr<float>(clast0);
+  a.clast1 = optr<float>(clast1);
   const int rc = dcr::launch_lstm2_fwd_persist(a, num_cus(), cur_stream());
   TORCH_CHECK(rc == 0, "two-layer persistent LSTM forward not launched (", rc, ")");
 }
@@ -811,7 +826,8 @@ TORCH_LIBRARY(dcr, m) {
       "lstm_persist_fwd(Tensor WT, Tensor zx, Tensor? ids, Tensor(a!) hbuf, Tensor(b!) cbuf, "
       "Tensor(c!)? gates, Tensor(d!) hlast32, Tensor(e!) cnt, Tensor(f!) err, float forget_bias, "
       "int spin_limit, Tensor(g!)? ring, Tensor(h!)? diag=None, Tensor? WxT=None, Tensor? xin=None, "
-      "Tensor? bias=None, bool cnt_zeroed=False, Tensor(i!)? hring=None) -> ()");
+      "Tensor? bias=None, bool cnt_zeroed=False, Tensor(i!)? hring=None, "
+      "Tensor(j!)? clast32=None) -> ()");
   m.def(
       "lstm_persist_bwd(Tensor W, Tensor dtop, Tensor(a!) dz, Tensor gates, Tensor cbuf, "
       "Tensor(b!) cnt, Tensor(c!) err, int spin_limit, Tensor(d!)? db_part, Tensor? ids, "
@@ -840,7 +856,8 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor bias1, Tensor(a!) hbuf0, Tensor(b!) cbuf0, Tensor(c!)? gates0, Tensor(d!) hlast0, "
       "Tensor(e!) hbuf1, Tensor(f!) cbuf1, Tensor(g!)? gates1, Tensor(h!) hlast1, "
       "Tensor(i!) cnt0, Tensor(j!) cnt1, Tensor(k!) err, float forget_bias, int spin_limit, "
-      "Tensor(l!)? diag=None, Tensor(m!)? hring0=None, Tensor(n!)? hring1=None) -> ()");
+      "Tensor(l!)? diag=None, Tensor(m!)? hring0=None, Tensor(n!)? hring1=None, "
+      "Tensor(o!)? clast0=None, Tensor(p!)? clast1=None) -> ()");
   m.def("gru_persist_ub(int H, int B) -> int", [](int64_t H, int64_t B) -> int64_t {
     return dcr::gru_persist_ub((int)H, (int)B, num_cus());
   });

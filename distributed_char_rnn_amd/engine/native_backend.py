@@ -99,6 +99,13 @@ def _mm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
     return out
 
 
+def _put(dst: torch.Tensor, src: torch.Tensor):
+    """dst.copy_(src) unless src already is dst's memory (results written in place)."""
+    if not (src.data_ptr() == dst.data_ptr() and src.shape == dst.shape
+            and src.stride() == dst.stride()):
+        dst.copy_(src)
+
+
 @dataclass
 class LayerWeights:
     Wx: torch.Tensor            # [D, GW] bf16 input projection
@@ -125,6 +132,7 @@ class LayerBufs:
     dz: Optional[torch.Tensor]
     dzx: Optional[torch.Tensor]
     x_in: Optional[torch.Tensor] = None      # bf16 [N, D] layer input (dense mode)
+    clast32: Optional[torch.Tensor] = None   # fp32 [B, H] final c (persistent LSTM)
     masks: Dict[str, torch.Tensor] = field(default_factory=dict)
 
 
@@ -443,6 +451,13 @@ class NativeBackend:
         if bufs["persist"] or bufs["gru_persist"]:
             tasks.append((bufs["cnt"], bufs["cnt"], 2))
         self._run_prep(tasks)
+        # the persistent LSTM kernels write the final (c, h) straight into fresh tensors that
+        # become the returned TBPTT state (no copies of cbuf[T] / hlast32 afterwards)
+        fresh = bufs["persist"] and self.cfg.model == "lstm"
+        if fresh:
+            for lb in bufs["layers"]:
+                lb.hlast32 = torch.empty(B, H, dtype=f32, device=self.dev)
+                lb.clast32 = torch.empty(B, H, dtype=f32, device=self.dev)
         x_prev = None  # bf16 [T, B, H] input for the next layer
         paired = -1  # layer already computed by the previous layer's two-layer wavefront
         for layer in range(self.L):
@@ -461,7 +476,8 @@ class NativeBackend:
                                           lb.hlast32, bufs["cnt"][layer], self.err, FORGET_BIAS,
                                           self.spin_limit, None, None, lw.WxT, x_prev, lw.bias,
                                           cnt_zeroed=True,
-                                          hring=bufs["hrings"][0] if bufs["hrings"] else None)
+                                          hring=bufs["hrings"][0] if bufs["hrings"] else None,
+                                          clast32=lb.clast32)
                 x_prev = lb.hbuf[1:]
                 continue
             if gather:
@@ -489,7 +505,8 @@ class NativeBackend:
                                            lb1.hbuf, lb1.cbuf, lb1.gates, lb1.hlast32,
                                            bufs["cnt"][layer], bufs["cnt"][layer + 1], self.err,
                                            FORGET_BIAS, self.spin_limit, None,
-                                           *(bufs["hrings"] or (None, None)))
+                                           *(bufs["hrings"] or (None, None)), lb.clast32,
+                                           lb1.clast32)
                 lb1.x_in = lb.hbuf[1:].reshape(N, H)
                 x_prev = lb1.hbuf[1:]
                 paired = layer + 1
@@ -501,7 +518,8 @@ class NativeBackend:
                                           bufs["ring"] if self.handoff == "granule" else None,
                                           cnt_zeroed=True,
                                           hring=(bufs["hrings"][0] if bufs["hrings"]
-                                                 and self.handoff != "granule" else None))
+                                                 and self.handoff != "granule" else None),
+                                          clast32=lb.clast32)
             elif bufs["gru_persist"]:
                 gr = bufs["grings"]
                 self.ops.gru_persist_fwd(lw.WhT, lw.WT2, zx, ids_arg, lb.hbuf, lb.h32, lb.rh,
@@ -529,7 +547,8 @@ class NativeBackend:
         for layer in range(self.L):
             lb = bufs["layers"][layer]
             if self.cfg.model in ("lstm", "nas"):
-                new_state.append((lb.cbuf[T].clone(), lb.hlast32.clone()))
+                new_state.append((lb.clast32, lb.hlast32) if fresh
+                                 else (lb.cbuf[T].clone(), lb.hlast32.clone()))
             elif self.cfg.model == "gru":
                 new_state.append((lb.h32[T].clone(),))
             else:
@@ -639,7 +658,7 @@ class NativeBackend:
                 # W_h and W_x^{above} in registers (one workgroup per CU, grid = all CUs), so
                 # NOTHING may run beside it (a concurrent kernel holding CUs could deadlock the
                 # grid's residency): this layer's weight gradients are deferred until after it.
-                dbias = bufs["db_part"][layer].sum(0)
+                dbias = self._bias_sum(bufs["db_part"][layer], names)
 
                 def _wgrads(names=names, Hprev=Hprev, dZ=dZ, dZx=dZx, lb=lb, dbias=dbias,
                             layer=layer):
@@ -656,7 +675,7 @@ class NativeBackend:
                 # GEMMs) run on a side stream concurrently with the latency-bound BPTT of the
                 # layer below; the layer's all-reduce bucket is launched from that stream, so
                 # RCCL orders itself after the GEMMs.  Only dX stays on the critical path.
-                dbias = bufs["db_part"][layer].sum(0)
+                dbias = self._bias_sum(bufs["db_part"][layer], names)
                 ev = torch.cuda.Event()
                 ev.record()
                 side = self._side_stream()
@@ -690,7 +709,7 @@ class NativeBackend:
                 X0 = hd["E"][ids_tm.view(-1).long()].to(bf16)      # [N, H]
                 dWx = _mm_tn(X0, dZx)
                 if bufs["persist"]:
-                    dbias = bufs["db_part"][layer].sum(0)
+                    dbias = self._bias_sum(bufs["db_part"][layer], names)
                 else:
                     self.ops.segsum(dZx, None, 1, bufs["colsum"][:, :GW], bufs["ws"], False)
                     dbias = bufs["colsum"][0, :GW]
@@ -713,9 +732,10 @@ class NativeBackend:
                 dbias = dEW.sum(0)
                 torch.mm(dEW, lw.Wx32.t(), out=s.gview("embedding"))
             else:
-                dWx = _mm_tn(lb.x_in, dZx)
+                dWx = (_mm_tn(lb.x_in, dZx, s.gview(names[0])[:H])
+                       if self.cfg.model in ("lstm", "rnn") else _mm_tn(lb.x_in, dZx))
                 if bufs["persist"]:
-                    dbias = bufs["db_part"][layer].sum(0)    # fused in BPTT
+                    dbias = self._bias_sum(bufs["db_part"][layer], names)  # fused in BPTT
                 else:
                     self.ops.segsum(dZx, None, 1, bufs["colsum"][:, :GW], bufs["ws"], False)
                     dbias = bufs["colsum"][0, :GW]
@@ -743,6 +763,13 @@ class NativeBackend:
             self.check_errors()
         return bufs["loss"][0], new_state, extras
 
+    def _bias_sum(self, part: torch.Tensor, names) -> torch.Tensor:
+        """Sum the per-batch-group bias partials; for cells with one [GW] bias the sum is
+        written straight into its gradient slice (the later copy_ is then a no-op)."""
+        if self.cfg.model in ("lstm", "rnn"):
+            return torch.sum(part, 0, out=self.store.gview(names[1]))
+        return part.sum(0)
+
     def _write_input_grads(self, layer: int, names, dWx: torch.Tensor, dbias: torch.Tensor):
         s, H = self.store, self.H
         if self.cfg.model == "gru":
@@ -754,8 +781,8 @@ class NativeBackend:
         elif self.cfg.model == "nas":
             s.gview(names[0]).copy_(dWx)
         else:
-            s.gview(names[0])[:H].copy_(dWx)
-            s.gview(names[1]).copy_(dbias)
+            _put(s.gview(names[0])[:H], dWx)
+            _put(s.gview(names[1]), dbias)
 
     # ------------------------------------------------------------------ inference
     @torch.no_grad()

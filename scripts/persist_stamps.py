@@ -18,12 +18,19 @@ hl = torch.empty(B, H, device=dev)
 cnt = torch.zeros((B // 16 + 1) * (T + 1) * 4, dtype=torch.int32, device=dev)
 err = torch.zeros(1, dtype=torch.int32, device=dev)
 diag = torch.zeros(T, 8, dtype=torch.int64, device=dev)
+# fragment-order hand-off rings as the backend uses them (DCR_FRAG=0: row-major hand-off)
+FRAG = os.environ.get("DCR_FRAG", "1") != "0"
+hring = torch.empty(2 * B * H, dtype=torch.bfloat16, device=dev) if FRAG else None
+zring = torch.empty(2 * B * 4 * H, dtype=torch.bfloat16, device=dev) if FRAG else None
+hring1 = torch.empty(2 * B * H, dtype=torch.bfloat16, device=dev) if FRAG else None
 for it in range(5):
-    ops.lstm_persist_fwd(WT, zx, None, hbuf, cbuf, gates, hl, cnt, err, 1.0, 1 << 22, None, diag)
+    ops.lstm_persist_fwd(WT, zx, None, hbuf, cbuf, gates, hl, cnt, err, 1.0, 1 << 22, None, diag,
+                         hring=hring)
 torch.cuda.synchronize()
 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 ev0.record()
-ops.lstm_persist_fwd(WT, zx, None, hbuf, cbuf, gates, hl, cnt, err, 1.0, 1 << 22, None, diag)
+ops.lstm_persist_fwd(WT, zx, None, hbuf, cbuf, gates, hl, cnt, err, 1.0, 1 << 22, None, diag,
+                     hring=hring)
 ev1.record()
 torch.cuda.synchronize()
 d = diag.cpu().numpy().astype("float64")
@@ -48,11 +55,11 @@ ids = torch.randint(0, 65, (T, B), device=dev, dtype=torch.int32) if DEW else No
 dewp = torch.empty(B // 16, 65, 4 * H, device=dev) if DEW else None
 for it in range(3):
     ops.lstm_persist_bwd(W, dtop, dz, gates, cbuf, cnt, err, 1 << 22, dbp, ids, dewp, 65, diag,
-                         exclusive=EXCL)
+                         exclusive=EXCL, zring=zring)
 torch.cuda.synchronize()
 ev0.record()
 ops.lstm_persist_bwd(W, dtop, dz, gates, cbuf, cnt, err, 1 << 22, dbp, ids, dewp, 65, diag,
-                         exclusive=EXCL)
+                     exclusive=EXCL, zring=zring)
 ev1.record()
 torch.cuda.synchronize()
 d = diag.cpu().numpy().astype("float64")[::-1]  # reverse time order
@@ -82,7 +89,7 @@ if ops.lstm2_persist_supported(H, B):
         c0.zero_()
         c1.zero_()
         ops.lstm2_persist_fwd(WT, W1T, X1T, zx, None, b1, hbuf, cbuf, gates, hl, hb1, cb1, g1,
-                              hl1, c0, c1, err, 1.0, 1 << 22, diag2)
+                              hl1, c0, c1, err, 1.0, 1 << 22, diag2, hring, hring1)
     for _ in range(3):
         run2()
     torch.cuda.synchronize()
