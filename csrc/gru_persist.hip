@@ -21,6 +21,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "persist_common.h"
+#include <stdlib.h>
 
 namespace dcr {
 
@@ -45,7 +46,10 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
   const size_t cset = (size_t)(B / 16) * (T + 1) * 4;
   unsigned* cntH = a.cnt + (size_t)bg * (T + 1) * 4;         // slot t: h_t published
   unsigned* cntR = a.cnt + cset + (size_t)bg * (T + 1) * 4;  // slot t: r⊙h_{t-1} published
-  const unsigned quarter_target = (unsigned)(H / 64);
+  const unsigned target = (unsigned)(H / (64 * UB));  // workgroups per K-quarter shard
+  __shared__ unsigned wg_cnt[2];  // LDS last-arriver counters (phase A / phase B)
+  if (threadIdx.x < 2) wg_cnt[threadIdx.x] = 0;
+  __syncthreads();
   bool dead = false;
 
   bf16x8 wg[UB][2][KS], wc[UB][KS];
@@ -80,7 +84,7 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
     // ---- phase A: [r, u] from h_{t-1}
     if (t > 0) {
       if (threadIdx.x == kPollerThread && !dead)
-        dead = !poll_quarters(cntH + (size_t)t * 4, quarter_target, a.spin_limit, a.err, 5u);
+        dead = !poll_shards4(cntH + (size_t)t * 4, target, a.spin_limit, a.err, 5u);
       __syncthreads();
     }
     {
@@ -128,8 +132,7 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
         st4bf_sc1(a.rh + (size_t)t * B * H + bh, rh0, rh1, rh2, rh3);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0)
-        __hip_atomic_fetch_add(cntR + (size_t)t * 4 + (u0 / (H / 4)), 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        wg_arrive(&wg_cnt[0], UB, cntR + (size_t)t * 4 + (u0 / (H / 4)));
       if (a.ring1) st4bf(a.rh + (size_t)t * B * H + bh, rh0, rh1, rh2, rh3);
       bf16* gp = a.gates + ((size_t)t * B + b) * G3 + u0;
       st4bf(gp, rr[0], rr[1], rr[2], rr[3]);
@@ -137,7 +140,7 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
     }
     // ---- phase B: c~ from r⊙h_{t-1}
     if (threadIdx.x == kPollerThread && !dead)
-      dead = !poll_quarters(cntR + (size_t)t * 4, quarter_target, a.spin_limit, a.err, 6u);
+      dead = !poll_shards4(cntR + (size_t)t * 4, target, a.spin_limit, a.err, 6u);
     __syncthreads();
     {
       const __amdgpu_buffer_rsrc_t src =
@@ -179,8 +182,7 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
       if (t + 1 < T) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0)
-          __hip_atomic_fetch_add(cntH + (size_t)(t + 1) * 4 + (u0 / (H / 4)), 1u,
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          wg_arrive(&wg_cnt[1], UB, cntH + (size_t)(t + 1) * 4 + (u0 / (H / 4)));
       }
       if (a.ring0) st4bf(a.hbuf + o, h[0], h[1], h[2], h[3]);
       *reinterpret_cast<float4*>(a.h32 + o) = make_float4(h[0], h[1], h[2], h[3]);
@@ -216,7 +218,10 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
   const size_t cset = (size_t)(B / 16) * (T + 1) * 4;
   unsigned* cntC = a.cnt + (size_t)bg * (T + 1) * 4;         // slot t: dZc_t published
   unsigned* cntG = a.cnt + cset + (size_t)bg * (T + 1) * 4;  // slot t: dZg_t published
-  const unsigned quarter_target = (unsigned)(H / 64);
+  const unsigned target = (unsigned)(H / (64 * UB));  // workgroups per K-quarter shard
+  __shared__ unsigned wg_cnt[2];  // LDS last-arriver counters (phase A / phase B)
+  if (threadIdx.x < 2) wg_cnt[threadIdx.x] = 0;
+  __syncthreads();
   const int G3 = 3 * H;
   bool dead = false;
 
@@ -255,8 +260,7 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
       st4bf_sc1(zrow, z0[0], z0[1], z0[2], z0[3]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0)
-      __hip_atomic_fetch_add(cntC + (size_t)(T - 1) * 4 + (u0 / (H / 4)), 1u, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
+      wg_arrive(&wg_cnt[1], UB, cntC + (size_t)(T - 1) * 4 + (u0 / (H / 4)));
     if (a.ring0) st4bf(zrow, z0[0], z0[1], z0[2], z0[3]);
   }
 
@@ -277,7 +281,7 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
         make_rsrc(a.dz + (size_t)t * B * G3, sizeof(bf16) * (size_t)B * G3);
     // ---- phase A: d(r⊙h_{t-1}) = dZc_t · W_cᵀ
     if (threadIdx.x == kPollerThread && !dead)
-      dead = !poll_quarters(cntC + (size_t)t * 4, quarter_target, a.spin_limit, a.err, 7u);
+      dead = !poll_shards4(cntC + (size_t)t * 4, target, a.spin_limit, a.err, 7u);
     __syncthreads();
     {
       bf16x8 zf[KA];
@@ -329,8 +333,7 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
       if (t > 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0)
-          __hip_atomic_fetch_add(cntG + (size_t)t * 4 + (u0 / (H / 4)), 1u, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+          wg_arrive(&wg_cnt[0], UB, cntG + (size_t)t * 4 + (u0 / (H / 4)));
       }
       if (a.ring1) {
         st4bf(dz, dzr[0], dzr[1], dzr[2], dzr[3]);
@@ -340,7 +343,7 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
     if (t == 0) break;  // dh'_{-1} (the initial state's gradient) is not needed
     // ---- phase B: dh'_{t-1} = dtop_{t-1} + P + dZg_t · W_gᵀ
     if (threadIdx.x == kPollerThread && !dead)
-      dead = !poll_quarters(cntG + (size_t)t * 4, quarter_target, a.spin_limit, a.err, 8u);
+      dead = !poll_shards4(cntG + (size_t)t * 4, target, a.spin_limit, a.err, 8u);
     __syncthreads();
     {
       bf16x8 zf[KB];
@@ -384,8 +387,7 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
         st4bf_sc1(crow, dzc[0], dzc[1], dzc[2], dzc[3]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0)
-        __hip_atomic_fetch_add(cntC + (size_t)(t - 1) * 4 + (u0 / (H / 4)), 1u,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        wg_arrive(&wg_cnt[1], UB, cntC + (size_t)(t - 1) * 4 + (u0 / (H / 4)));
       if (a.ring0) st4bf(crow, dzc[0], dzc[1], dzc[2], dzc[3]);
     }
   }
@@ -415,7 +417,9 @@ static int gru_grid(int H, int B, int ub) { return (H / (16 * ub)) * (B / 16); }
 // co-resident with the GPU to themselves; 0 = not supported (per-step kernels instead).
 int gru_persist_ub(int H, int B, int cus) {
   if (H % 128 != 0 || H < 128 || H > 1024 || B % 16 != 0 || B < 16 || cus <= 0) return 0;
-  for (int ub = 2; ub >= 1; --ub) {
+  const char* e = getenv("DCR_GRU_UB");
+  const int first = (e && e[0] == '1') ? 1 : 2;
+  for (int ub = first; ub >= 1; --ub) {
     bool ok = true;
     for (int bwd = 0; bwd < 2 && ok; ++bwd) {
       const void* fn = gru_pick(bwd, H, ub);

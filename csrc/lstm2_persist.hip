@@ -43,7 +43,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
   const int kbase = w * (KS * 32);
   unsigned* cnt0 = a.cnt0 + (size_t)bg * (T + 1) * 4;
   unsigned* cnt1 = a.cnt1 + (size_t)bg * (T + 1) * 4;
-  const unsigned target = (unsigned)(H / 32);  // (H/4)/16 unit blocks x 2 batch tiles
+  const unsigned target = (unsigned)(H / 8);  // H/16 unit blocks x 2 batch tiles
   bool dead = false;
 
   bf16x8 w0[4][KS], w1[4][KS], x1[4][KS];
@@ -92,10 +92,10 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     if (tau >= 1) {
       if (threadIdx.x == kLstmPollerThread && !dead) {
         // layer l+1's slot tau-1 exists from tick 2 on; before that poll layer l's twice
-        dead = tau >= 2 ? !poll_quarters2(cnt0 + (size_t)tau * 4, target,
-                                          cnt1 + (size_t)(tau - 1) * 4, target, a.spin_limit,
-                                          a.err, 9u)
-                        : !poll_quarters(cnt0 + (size_t)tau * 4, target, a.spin_limit, a.err, 9u);
+        dead = tau >= 2 ? !poll_counter2(cnt0 + (size_t)tau * 4, target,
+                                         cnt1 + (size_t)(tau - 1) * 4, target, a.spin_limit,
+                                         a.err, 9u)
+                        : !poll_counter(cnt0 + (size_t)tau * 4, target, a.spin_limit, a.err, 9u);
       }
       STAMP2(1)
       __syncthreads();
@@ -199,7 +199,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         STAMP2(6)
         if (lane == 0)
-          __hip_atomic_fetch_add(cntL + (size_t)(t + 1) * 4 + (u0 / (H / 4)), 1u,
+          __hip_atomic_fetch_add(cntL + (size_t)(t + 1) * 4, 1u,
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       if (ringL) st4bf(hbL + o, h[0], h[1], h[2], h[3]);  // row-major copy for the GEMMs

@@ -138,7 +138,7 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
     if (t > 0) {
       // ONE poller per workgroup (pollers cost chip bandwidth); the barrier releases the waves
       if (threadIdx.x == kLstmPollerThread && !dead)
-        dead = !poll_quarters(cnt + (size_t)t * 4, (unsigned)(H / 64), a.spin_limit, a.err, 1u);
+        dead = !poll_counter(cnt + (size_t)t * 4, (unsigned)(H / 16), a.spin_limit, a.err, 1u);
       STAMP(1)
       __syncthreads();
     }
@@ -204,7 +204,7 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         STAMP(6)
         if (lane == 0)
-          __hip_atomic_fetch_add(cnt + (size_t)(t + 1) * 4 + (u0 / (H / 4)), 1u, __ATOMIC_RELAXED,
+          __hip_atomic_fetch_add(cnt + (size_t)(t + 1) * 4, 1u, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
       }
       if (a.hring) st4bf(a.hbuf + o, h[0], h[1], h[2], h[3]);
@@ -496,7 +496,7 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
     if (t < T - 1 || XB) {
      if (t < T - 1) {
       if (threadIdx.x == kLstmPollerThread && !dead)
-        dead = !poll_quarters(cnt + (size_t)(t + 1) * 4, (unsigned)(H / 64), a.spin_limit, a.err, 2u);
+        dead = !poll_counter(cnt + (size_t)(t + 1) * 4, (unsigned)(H / 16), a.spin_limit, a.err, 2u);
       STAMP(1)
       __syncthreads();
       STAMP(2)
@@ -573,7 +573,7 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         STAMP(6)
         if (lane == 0)
-          __hip_atomic_fetch_add(cnt + (size_t)t * 4 + (u0 / (H / 4)), 1u, __ATOMIC_RELAXED,
+          __hip_atomic_fetch_add(cnt + (size_t)t * 4, 1u, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
       }
       if (zr) {

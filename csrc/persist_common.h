@@ -42,8 +42,16 @@ __device__ __forceinline__ void ld4f(const float* p, float (&o)[4]) {
   o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
 }
 
-// One lane of the workgroup polls `*cnt >= target` (relaxed agent-scope = sc1 loads); the
-// result is broadcast through LDS by the barrier that follows.  Returns false on timeout.
+// Hand-off protocol (MI355X_MICROARCH.md "Valid forms", third row, matched in every cell):
+//   producer: every handed-off byte stored sc1 (global_store_dwordx2 sc1; every 128-B line
+//             written whole by one store instruction of one wave: the fragment-order rings
+//             below), the storing wave's s_waitcnt vmcnt(0), then ONE lane of that wave adds 1
+//             to the (batch group, step) counter (agent-scope atomic);
+//   consumer: ONE lane polls that counter with global_load_dword sc1 (+ s_sleep), a workgroup
+//             barrier, then every load of the bytes is buffer_load_dwordx4 sc1.
+// One unsharded counter per (batch group, step): a single dword poll per iteration (polling
+// four quarter shards with four dword loads cost 13 % on the GRU).  Returns false on timeout
+// after setting the error word; the caller keeps going so the grid always drains.
 __device__ __forceinline__ bool poll_counter(unsigned* cnt, unsigned target, unsigned limit,
                                              unsigned* err, unsigned code) {
   unsigned spins = 0;
@@ -57,9 +65,14 @@ __device__ __forceinline__ bool poll_counter(unsigned* cnt, unsigned target, uns
   return true;
 }
 
-// Poll the 4 per-quarter counters of one step (one 16-B sc1 load) until all reach `target`.
-__device__ __forceinline__ bool poll_quarters(unsigned* cnt4, unsigned target, unsigned limit,
-                                              unsigned* err, unsigned code) {
+// Sharded form (the same table's FIRST row): ONE lane of each storing workgroup signals for ALL
+// that workgroup's stores -- every epilogue wave drains (vmcnt(0)) and then adds to an LDS
+// counter, and the wave whose add comes last does the agent-scope add -- on one of four shards
+// (the workgroup's K quarter); the consumer polls every shard with one 16-B sc1 load.  Used by
+// the GRU, whose H/16 = 64 epilogue waves per counter (H = 1024) made a single counter's atomics
+// the bottleneck (21.7 vs 14.4 ms per step).
+__device__ __forceinline__ bool poll_shards4(unsigned* cnt4, unsigned target, unsigned limit,
+                                             unsigned* err, unsigned code) {
   const __amdgpu_buffer_rsrc_t r = make_rsrc(cnt4, 16);
   unsigned spins = 0;
   for (;;) {
@@ -73,19 +86,31 @@ __device__ __forceinline__ bool poll_quarters(unsigned* cnt4, unsigned target, u
   }
 }
 
-// Two counter sets polled together (one sc1 load each per iteration, both in flight): the
-// two-layer wavefront waits for both layers' previous tick without a second round trip.
-__device__ __forceinline__ bool poll_quarters2(unsigned* c0, unsigned t0, unsigned* c1,
-                                               unsigned t1, unsigned limit, unsigned* err,
-                                               unsigned code) {
-  const __amdgpu_buffer_rsrc_t r0 = make_rsrc(c0, 16), r1 = make_rsrc(c1, 16);
+// Workgroup-level arrival (first-row form): call from lane 0 of each of the `nwaves` storing
+// waves AFTER that wave's s_waitcnt vmcnt(0); the last of them adds 1 to `shard`.
+__device__ __forceinline__ void wg_arrive(unsigned* lds_cnt, unsigned nwaves, unsigned* shard) {
+  if (nwaves == 1) {  // the workgroup's only storing wave signals for itself
+    __hip_atomic_fetch_add(shard, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  const unsigned old = __hip_atomic_fetch_add(lds_cnt, 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (old == nwaves - 1) {
+    __hip_atomic_store(lds_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add(shard, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Two counters polled together (both dword loads in flight per iteration): the two-layer
+// wavefront waits for both layers' previous tick without a second round trip.
+__device__ __forceinline__ bool poll_counter2(unsigned* c0, unsigned t0, unsigned* c1,
+                                              unsigned t1, unsigned limit, unsigned* err,
+                                              unsigned code) {
   unsigned spins = 0;
   for (;;) {
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r0, 0, 0, kAuxSc1);
-    const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(r1, 0, 0, kAuxSc1);
-    if (v[0] >= t0 && v[1] >= t0 && v[2] >= t0 && v[3] >= t0 && u[0] >= t1 && u[1] >= t1 &&
-        u[2] >= t1 && u[3] >= t1)
-      return true;
+    const unsigned v0 = __hip_atomic_load(c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned v1 = __hip_atomic_load(c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v0 >= t0 && v1 >= t1) return true;
     if (++spins > limit) {
       __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
