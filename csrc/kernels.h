@@ -158,6 +158,28 @@ struct Lstm2Args {
 int lstm2_persist_supported(int H, int B, int cus);
 int launch_lstm2_fwd_persist(const Lstm2Args& a, int cus, hipStream_t s);
 
+// two-layer wavefront LSTM BPTT (lstm2_persist.hip): layers l and l+1 in one launch, layer l
+// one step behind layer l+1; layer l's dtop = dZ_{l+1}·W_x,l+1ᵀ is computed in-kernel
+struct Lstm2BwdArgs {
+  const bf16* Wh0;      // layer l   W_h [H, 4H] (TF layout)
+  const bf16* Wh1;      // layer l+1 W_h [H, 4H]
+  const bf16* Wx1;      // layer l+1 W_x [H, 4H] (input rows of its kernel)
+  const float* dtop1;   // [T, B, H] gradient arriving at layer l+1's output
+  const bf16* gates0; const float* cbuf0;   // layer l   activation cache [T,B,4H], c [T+1,B,H]
+  const bf16* gates1; const float* cbuf1;   // layer l+1
+  bf16* dz0; bf16* dz1;                     // [T, B, 4H] row-major dZ (weight GEMM operands)
+  bf16* zring0; bf16* zring1;               // [2, B, 4H] fragment-tiled dZ hand-off rings
+  float* db_part0; float* db_part1;         // [B/16, 4H] bias-gradient partials (or nullptr)
+  unsigned* cnt0;       // [B/32, T+1, 4] arrivals of layer l   (zeroed by the caller)
+  unsigned* cnt1;       // [B/32, T+1, 4] arrivals of layer l+1
+  unsigned* err;
+  unsigned long long* diag;  // optional [T+1, 8] s_memtime stamps of workgroup 0
+  int B, H, T;
+  unsigned spin_limit;
+};
+int lstm2_bwd_persist_supported(int H, int B, int cus);
+int launch_lstm2_bwd_persist(const Lstm2BwdArgs& a, int cus, hipStream_t s);
+
 // persistent GRU recurrence (gru_persist.hip)
 struct GruPersistArgs {
   const bf16* WgT;      // fwd: W_g,hᵀ [2H, H] (r rows, then u rows)

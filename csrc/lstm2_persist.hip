@@ -254,4 +254,256 @@ int launch_lstm2_fwd_persist(const Lstm2Args& a, int cus, hipStream_t s) {
                  hipSuccess ? 0 : -3;
 }
 
+// ------------------------------------------------------------------------------------------
+// two-layer wavefront BPTT
+// ------------------------------------------------------------------------------------------
+// Reference: tf.gradients through the unrolled two-layer stack (model.py:72, 91).  The
+// single-layer persistent BPTT (lstm_persist.hip) runs layer l+1's T steps, a dX GEMM
+// (dZ_{l+1}·W_x,l+1ᵀ), then layer l's T steps: 2T hand-off-latency-bound steps.  Layer l's
+// step t needs only layer l+1's dZ_t (its dtop) and its own dZ_{t+1}, so here one launch runs
+// both as a reverse wavefront: at tick tau layer l+1 computes step T-1-tau and layer l step
+// T-tau.  Both consume the slot dZ_{l+1}[T-tau] (layer l+1's recurrent operand and, through the
+// register-resident W_x,l+1 rows, layer l's dtop), so the dX GEMM disappears and T+1 ticks
+// replace 2T steps.
+//
+// Workgroup (ubk, bg) owns 16 hidden units x 32 batch rows (two 16-row MFMA tiles) of BOTH
+// layers.  K = 4H is split by hidden-unit quarter exactly as in lstm_bwd_persist_kernel: wave w
+// reduces over the columns g*H + [w*H/4, (w+1)*H/4) of every gate g and keeps the W_h,l,
+// W_h,l+1 and W_x,l+1 rows of its units for that K quarter resident (3 x KS fragments).
+// Wave w runs the cell-backward epilogue of layer w>>1 (0 = l, 1 = l+1), batch tile w&1.
+// Hand-off: as the forward above (sc1 fragment-order ring stores, the storing wave's
+// vmcnt(0), one agent-scope add per storing wave; ONE poller per workgroup watches both
+// layers' counters; every load of handed-off dZ is buffer_load sc1).
+template <int KS, bool DIAG = false>
+__global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs a) {
+  // partials [wave][layer][tile][lane][unit r]: single-buffered -- every tick that writes them
+  // starts with the poll barrier, which each epilogue wave joins after its reads
+  __shared__ __attribute__((aligned(16))) float part[4][2][2][64][4];
+  // bias-gradient accumulators of each epilogue lane, kept in LDS (registers are the limit:
+  // 3 x KS weight and 3 x KS payload fragments live across the MFMA phase)
+  __shared__ float dbl[4][16][64];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int H = a.H, B = a.B, T = a.T;
+  const int G4H = 4 * H;
+  int ubk, bg;
+  map_block(blockIdx.x, H / 16, B / 32, ubk, bg);
+  const int ub0 = ubk * 16, b0 = bg * 32;
+  const int kq = 8 * (lane >> 4);
+  unsigned* cnt0 = a.cnt0 + (size_t)bg * (T + 1) * 4;
+  unsigned* cnt1 = a.cnt1 + (size_t)bg * (T + 1) * 4;
+  const unsigned target = (unsigned)(H / 8);  // H/16 unit blocks x 2 batch tiles
+  bool dead = false;
+
+  constexpr int KSG = KS / 4;  // k-steps per gate segment
+  auto kcol = [&](int s) { return (s / KSG) * H + w * (H / 4) + (s % KSG) * 32; };
+  bf16x8 wh0[KS], wh1[KS], wx1[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const size_t row = (size_t)(ub0 + (lane & 15)) * G4H + kcol(s) + kq;
+    wh0[s] = ld8(a.Wh0 + row);
+    wh1[s] = ld8(a.Wh1 + row);
+    wx1[s] = ld8(a.Wx1 + row);
+  }
+
+  // epilogue role: layer L, batch tile J
+  const int L = w >> 1, J = w & 1;
+  const int b = b0 + 16 * J + (lane & 15);
+  const int u0 = ub0 + 4 * (lane >> 4);
+  const size_t bh = (size_t)b * H + u0;
+  const bf16* const gtL = L ? a.gates1 : a.gates0;
+  const float* const cbL = L ? a.cbuf1 : a.cbuf0;
+  bf16* const dzL = L ? a.dz1 : a.dz0;
+  bf16* const zrL = L ? a.zring1 : a.zring0;
+  unsigned* const cntL = L ? cnt1 : cnt0;
+  float dc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dbl[w][i][lane] = 0.f;
+
+  for (int tau = 0; tau <= T; ++tau) {
+    const bool on1 = tau < T, on0 = tau >= 1;
+    const int t = L ? T - 1 - tau : T - tau;  // this role's step
+    const bool act = L ? on1 : on0;
+    STAMP2(0)
+    // recurrence-independent epilogue operands, issued before the wait
+    float gi[4], gj[4], gf[4], go[4], cc[4], cp[4], dtop[4];
+    if (act) {
+      const bf16* gp = gtL + ((size_t)t * B + b) * G4H + u0;
+      ld4bf(gp, gi); ld4bf(gp + H, gj); ld4bf(gp + 2 * H, gf); ld4bf(gp + 3 * H, go);
+      ld4f(cbL + (size_t)(t + 1) * B * H + bh, cc);
+      ld4f(cbL + (size_t)t * B * H + bh, cp);
+      if (L) {
+        ld4f(a.dtop1 + (size_t)t * B * H + bh, dtop);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dtop[r] = 0.f;
+      }
+    }
+    if (tau >= 1) {
+      // slot s1 = T - tau of layer l+1 (both layers' operand), slot s1 + 1 of layer l
+      const int s1 = T - tau;
+      const bool has0 = tau >= 2;
+      if (threadIdx.x == kLstmPollerThread && !dead) {
+        dead = has0 ? !poll_counter2(cnt1 + (size_t)s1 * 4, target, cnt0 + (size_t)(s1 + 1) * 4,
+                                     target, a.spin_limit, a.err, 10u)
+                    : !poll_counter(cnt1 + (size_t)s1 * 4, target, a.spin_limit, a.err, 10u);
+      }
+      STAMP2(1)
+      __syncthreads();
+      STAMP2(2)
+      const size_t slab = sizeof(bf16) * (size_t)B * G4H;
+      const __amdgpu_buffer_rsrc_t r1 = make_rsrc(a.zring1 + (size_t)(s1 & 1) * B * G4H, slab);
+      const __amdgpu_buffer_rsrc_t r0 =
+          make_rsrc(a.zring0 + (size_t)((s1 + 1) & 1) * B * G4H, slab);
+      // register budget (one wave per SIMD, <= ~450 VGPR+AGPR without spills): 3 x KS weight
+      // fragments + 3 x KS payload fragments in flight (both tiles of dZ_{l+1}, tile 0 of
+      // dZ_l); tile 1 of dZ_l is issued once tile 0's dZ_{l+1} fragments are consumed
+      bf16x8 p1[2][KS], p0[KS];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+          p1[j][s] = ld8_sc1(r1, frag_load_off(2 * bg + j, kcol(s) >> 5, G4H, lane));
+      if (has0) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+          p0[s] = ld8_sc1(r0, frag_load_off(2 * bg, kcol(s) >> 5, G4H, lane));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x4 acc1 = f32x4{0.f, 0.f, 0.f, 0.f}, acc0 = f32x4{0.f, 0.f, 0.f, 0.f};
+        // layer l+1: dh partial = dZ_{l+1}[t+1] · W_h,l+1ᵀ;  layer l: dtop = dZ_{l+1}[t] · W_x,l+1ᵀ
+        if (on1) {
+#pragma unroll
+          for (int s = 0; s < KS; ++s) acc1 = mfma16(wh1[s], p1[j][s], acc1);
+        }
+#pragma unroll
+        for (int s = 0; s < KS; ++s) acc0 = mfma16(wx1[s], p1[j][s], acc0);
+        if (has0) {
+          // + dZ_l[t+1] · W_h,lᵀ
+#pragma unroll
+          for (int s = 0; s < KS; ++s) acc0 = mfma16(wh0[s], p0[s], acc0);
+          if (j == 0) {
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+              p0[s] = ld8_sc1(r0, frag_load_off(2 * bg + 1, kcol(s) >> 5, G4H, lane));
+          }
+        }
+        if (on1)
+          *reinterpret_cast<float4*>(&part[w][1][j][lane][0]) =
+              make_float4(acc1[0], acc1[1], acc1[2], acc1[3]);
+        *reinterpret_cast<float4*>(&part[w][0][j][lane][0]) =
+            make_float4(acc0[0], acc0[1], acc0[2], acc0[3]);
+      }
+      STAMP2(3)
+      __syncthreads();
+      STAMP2(4)
+    }
+    if (act) {
+      float dh[4];
+      if (tau >= 1) {
+        const float4 s0 = *reinterpret_cast<const float4*>(&part[0][L][J][lane][0]);
+        const float4 s1 = *reinterpret_cast<const float4*>(&part[1][L][J][lane][0]);
+        const float4 s2 = *reinterpret_cast<const float4*>(&part[2][L][J][lane][0]);
+        const float4 s3 = *reinterpret_cast<const float4*>(&part[3][L][J][lane][0]);
+        dh[0] = s0.x + s1.x + s2.x + s3.x + dtop[0];
+        dh[1] = s0.y + s1.y + s2.y + s3.y + dtop[1];
+        dh[2] = s0.z + s1.z + s2.z + s3.z + dtop[2];
+        dh[3] = s0.w + s1.w + s2.w + s3.w + dtop[3];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dh[r] = dtop[r];
+      }
+      float di[4], dj[4], df_[4], dO[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float th = tanhf_(cc[r]);
+        const float dcv = dc[r] + dh[r] * go[r] * (1.f - th * th);
+        dO[r] = dh[r] * th * go[r] * (1.f - go[r]);
+        di[r] = dcv * gj[r] * gi[r] * (1.f - gi[r]);
+        dj[r] = dcv * gi[r] * (1.f - gj[r] * gj[r]);
+        df_[r] = dcv * cp[r] * gf[r] * (1.f - gf[r]);
+        dc[r] = dcv * gf[r];
+      }
+      STAMP2(5)
+      // layer l+1's dZ_t feeds both layers at the next tick (t >= 0); layer l's only itself
+      if (L || t >= 1) {
+        bf16* const zr = zrL + (size_t)(t & 1) * B * G4H;
+        st4bf_sc1(zr + frag_index(b, u0, G4H), di[0], di[1], di[2], di[3]);
+        st4bf_sc1(zr + frag_index(b, H + u0, G4H), dj[0], dj[1], dj[2], dj[3]);
+        st4bf_sc1(zr + frag_index(b, 2 * H + u0, G4H), df_[0], df_[1], df_[2], df_[3]);
+        st4bf_sc1(zr + frag_index(b, 3 * H + u0, G4H), dO[0], dO[1], dO[2], dO[3]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        STAMP2(6)
+        if (lane == 0)
+          __hip_atomic_fetch_add(cntL + (size_t)t * 4, 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+      }
+      // row-major copy for the weight GEMMs, after the arrival (off the critical path)
+      bf16* dz = dzL + ((size_t)t * B + b) * G4H + u0;
+      st4bf(dz, di[0], di[1], di[2], di[3]);
+      st4bf(dz + H, dj[0], dj[1], dj[2], dj[3]);
+      st4bf(dz + 2 * H, df_[0], df_[1], df_[2], df_[3]);
+      st4bf(dz + 3 * H, dO[0], dO[1], dO[2], dO[3]);
+      // bias gradient of the bf16-rounded dz, exactly as the weight GEMMs see it
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        dbl[w][r][lane] += (float)f2bf(di[r]);
+        dbl[w][4 + r][lane] += (float)f2bf(dj[r]);
+        dbl[w][8 + r][lane] += (float)f2bf(df_[r]);
+        dbl[w][12 + r][lane] += (float)f2bf(dO[r]);
+      }
+    }
+  }
+  // bias-gradient partial of this role's 16-row tile: reduce the 16 batch lanes
+  float* const dbp = L ? a.db_part1 : a.db_part0;
+  if (dbp) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = dbl[w][g * 4 + r][lane];
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        v += __shfl_xor(v, 4, 64);
+        v += __shfl_xor(v, 8, 64);
+        if ((lane & 15) == 0) dbp[(size_t)(2 * bg + J) * G4H + g * H + u0 + r] = v;
+      }
+  }
+}
+
+template <int KS>
+static const void* lstm2_bwd_fn(bool diag) {
+  return diag ? (const void*)lstm2_bwd_persist_kernel<KS, true>
+              : (const void*)lstm2_bwd_persist_kernel<KS, false>;
+}
+
+static const void* lstm2_bwd_pick(int H, bool diag = false) {
+  switch (H / 32) {  // KS = 4H / 4 waves / 32
+    case 4: return lstm2_bwd_fn<4>(diag);
+    case 8: return lstm2_bwd_fn<8>(diag);
+    case 12: return lstm2_bwd_fn<12>(diag);
+    case 16: return lstm2_bwd_fn<16>(diag);
+  }
+  return nullptr;
+}
+
+int lstm2_bwd_persist_supported(int H, int B, int cus) {
+  if (H % 128 != 0 || H < 128 || H > 512 || B % 32 != 0 || B < 32 || cus <= 0) return 0;
+  const void* fn = lstm2_bwd_pick(H);
+  int occ = 0;
+  if (!fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 256, 0) != hipSuccess)
+    return 0;
+  return lstm2_grid(H, B) <= occ * cus ? 1 : 0;
+}
+
+int launch_lstm2_bwd_persist(const Lstm2BwdArgs& a, int cus, hipStream_t s) {
+  if (!lstm2_bwd_persist_supported(a.H, a.B, cus)) return -2;
+  void* args[] = {const_cast<Lstm2BwdArgs*>(&a)};
+  return hipLaunchKernel(lstm2_bwd_pick(a.H, a.diag != nullptr), dim3(lstm2_grid(a.H, a.B)),
+                         dim3(256), args, 0, s) == hipSuccess ? 0 : -3;
+}
+
 }  // namespace dcr

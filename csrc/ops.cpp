@@ -583,6 +583,57 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
   TORCH_CHECK(rc == 0, "two-layer persistent LSTM forward not launched (", rc, ")");
 }
 
+// two-layer wavefront LSTM BPTT (lstm2_persist.hip)
+void lstm2_persist_bwd(const at::Tensor& Wh0, const at::Tensor& Wh1, const at::Tensor& Wx1,
+                       const at::Tensor& dtop1, const at::Tensor& gates0, const at::Tensor& cbuf0,
+                       const at::Tensor& gates1, const at::Tensor& cbuf1, at::Tensor& dz0,
+                       at::Tensor& dz1, at::Tensor& zring0, at::Tensor& zring1,
+                       const c10::optional<at::Tensor>& db_part0,
+                       const c10::optional<at::Tensor>& db_part1, at::Tensor& cnt0,
+                       at::Tensor& cnt1, at::Tensor& err, int64_t spin_limit,
+                       const c10::optional<at::Tensor>& diag) {
+  for (auto* t : {&Wh0, &Wh1, &Wx1}) check_seq(*t, at::kBFloat16, "W");
+  check_seq(dtop1, at::kFloat, "dtop1");
+  for (const at::Tensor* t : {&gates0, &gates1, (const at::Tensor*)&dz0, (const at::Tensor*)&dz1, (const at::Tensor*)&zring0, (const at::Tensor*)&zring1}) check_seq(*t, at::kBFloat16, "bf16 buffer");
+  for (auto* t : {&cbuf0, &cbuf1}) check_seq(*t, at::kFloat, "cbuf");
+  const int T = (int)dtop1.size(0), B = (int)dtop1.size(1), H = (int)dtop1.size(2);
+  for (auto* t : {&Wh0, &Wh1, &Wx1})
+    TORCH_CHECK(t->size(0) == H && t->size(1) == 4 * H, "weights must be [H, 4H]");
+  const int64_t n4 = (int64_t)T * B * 4 * H;
+  for (const at::Tensor* t : {&gates0, &gates1, (const at::Tensor*)&dz0, (const at::Tensor*)&dz1}) TORCH_CHECK(t->numel() == n4, "gates/dz must be [T, B, 4H]");
+  for (auto* t : {&cbuf0, &cbuf1}) TORCH_CHECK(t->numel() == (int64_t)(T + 1) * B * H, "cbuf must be [T+1, B, H]");
+  for (auto* t : {&zring0, &zring1}) TORCH_CHECK(t->numel() >= (int64_t)2 * B * 4 * H, "zring must hold [2, B, 4H]");
+  for (auto* c : {&cnt0, &cnt1})
+    TORCH_CHECK(c->is_cuda() && c->scalar_type() == at::kInt &&
+                    c->numel() >= (int64_t)(B / 32) * (T + 1) * 4, "counter buffer too small");
+  for (auto* d : {&db_part0, &db_part1}) {
+    check_opt(*d, at::kFloat, "db_part");
+    if (has(*d)) TORCH_CHECK((*d)->numel() == (int64_t)(B / 16) * 4 * H, "db_part must be [B/16, 4H]");
+  }
+  TORCH_CHECK(dcr::lstm2_bwd_persist_supported(H, B, num_cus()),
+              "two-layer persistent LSTM BPTT unsupported for H=", H, " B=", B);
+  dcr::Lstm2BwdArgs a{};
+  a.Wh0 = ptr<bf16>(Wh0); a.Wh1 = ptr<bf16>(Wh1); a.Wx1 = ptr<bf16>(Wx1);
+  a.dtop1 = ptr<float>(dtop1);
+  a.gates0 = ptr<bf16>(gates0); a.cbuf0 = ptr<float>(cbuf0);
+  a.gates1 = ptr<bf16>(gates1); a.cbuf1 = ptr<float>(cbuf1);
+  a.dz0 = ptr<bf16>(dz0); a.dz1 = ptr<bf16>(dz1);
+  a.zring0 = ptr<bf16>(zring0); a.zring1 = ptr<bf16>(zring1);
+  a.db_part0 = optr<float>(db_part0); a.db_part1 = optr<float>(db_part1);
+  a.cnt0 = reinterpret_cast<unsigned*>(cnt0.data_ptr());
+  a.cnt1 = reinterpret_cast<unsigned*>(cnt1.data_ptr());
+  a.err = reinterpret_cast<unsigned*>(err.data_ptr());
+  a.B = B; a.H = H; a.T = T;
+  a.spin_limit = (unsigned)spin_limit;
+  if (has(diag)) {
+    TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)(T + 1) * 8,
+                "diag must hold [T+1, 8] int64");
+    a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());
+  }
+  const int rc = dcr::launch_lstm2_bwd_persist(a, num_cus(), cur_stream());
+  TORCH_CHECK(rc == 0, "two-layer persistent LSTM BPTT not launched (", rc, ")");
+}
+
 // ------------------------------------------------------------------------------------------
 // persistent GRU recurrence (gru_persist.hip)
 // ------------------------------------------------------------------------------------------
@@ -858,6 +909,15 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor(i!) cnt0, Tensor(j!) cnt1, Tensor(k!) err, float forget_bias, int spin_limit, "
       "Tensor(l!)? diag=None, Tensor(m!)? hring0=None, Tensor(n!)? hring1=None, "
       "Tensor(o!)? clast0=None, Tensor(p!)? clast1=None) -> ()");
+  m.def("lstm2_bwd_persist_supported(int H, int B) -> int", [](int64_t H, int64_t B) -> int64_t {
+    return dcr::lstm2_bwd_persist_supported((int)H, (int)B, num_cus());
+  });
+  m.def(
+      "lstm2_persist_bwd(Tensor Wh0, Tensor Wh1, Tensor Wx1, Tensor dtop1, Tensor gates0, "
+      "Tensor cbuf0, Tensor gates1, Tensor cbuf1, Tensor(a!) dz0, Tensor(b!) dz1, "
+      "Tensor(c!) zring0, Tensor(d!) zring1, Tensor(e!)? db_part0, Tensor(f!)? db_part1, "
+      "Tensor(g!) cnt0, Tensor(h!) cnt1, Tensor(i!) err, int spin_limit, "
+      "Tensor(j!)? diag=None) -> ()");
   m.def("gru_persist_ub(int H, int B) -> int", [](int64_t H, int64_t B) -> int64_t {
     return dcr::gru_persist_ub((int)H, (int)B, num_cus());
   });
@@ -890,5 +950,6 @@ TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("prep", &prep);
   m.impl("gru_persist_fwd", &gru_persist_fwd);
   m.impl("lstm2_persist_fwd", &lstm2_persist_fwd);
+  m.impl("lstm2_persist_bwd", &lstm2_persist_bwd);
   m.impl("gru_persist_bwd", &gru_persist_bwd);
 }

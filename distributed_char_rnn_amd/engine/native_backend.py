@@ -159,6 +159,8 @@ class NativeBackend:
         self.use_persist = os.environ.get("DCR_PERSIST", "1") != "0"
         # two-layer wavefront forward (lstm2_persist.hip) for layers (0, 1)
         self.use_pair = os.environ.get("DCR_PAIR", "1") != "0"
+        # two-layer wavefront BPTT (lstm2_persist.hip) for the same pairs
+        self.use_pair_bwd = os.environ.get("DCR_PAIR_BWD", "1") != "0"
         self.spin_limit = int(os.environ.get("DCR_SPIN_LIMIT", str(1 << 22)))
         # forward hand-off form: "granule" (tagged data, R2) or "counter" (sc1 data + counter)
         self.handoff = os.environ.get("DCR_HANDOFF", "counter")
@@ -320,6 +322,9 @@ class NativeBackend:
             zring=(torch.empty(2 * B * GW, dtype=bf16, device=dev)
                    if (training and os.environ.get("DCR_FRAG", "1") != "0") else None),
         )
+        # second dZ ring for the two-layer wavefront BPTT (one ring per layer)
+        bufs["zring2"] = (torch.empty(2 * B * GW, dtype=bf16, device=dev)
+                          if bufs["pair_bwd"] else None)
         self._bufs[key] = bufs
         return bufs
 
@@ -369,7 +374,7 @@ class NativeBackend:
         forces a mode.
         """
         plan = dict(persist=False, xfuse=False, mode="exclusive", bwd_excl=False,
-                    gru_persist=False, pair=False)
+                    gru_persist=False, pair=False, pair_bwd=False)
         o = self.ops
         if self.use_persist and self.cfg.model == "gru":
             # persistent GRU (gru_persist.hip): the C++ side picks the unit block whose fwd and
@@ -398,6 +403,10 @@ class NativeBackend:
         plan["pair"] = (self.L >= 2 and self.use_pair and bool(o.lstm2_persist_supported(H, B)))
         if not training:
             return plan
+        # two-layer wavefront BPTT (needs the fragment-order dZ rings)
+        plan["pair_bwd"] = (plan["pair"] and self.use_pair_bwd
+                            and os.environ.get("DCR_FRAG", "1") != "0"
+                            and bool(o.lstm2_bwd_persist_supported(H, B)))
         shared_ok = fits(1, 0, margin=1)
         excl_ok = fits(1, PF_EXCL)
         forced = os.environ.get("DCR_MODE", "")
@@ -409,6 +418,8 @@ class NativeBackend:
             mode = "exclusive"
         else:
             mode = "overlap" if (shared_ok and self.side_overlap) else "exclusive"
+        if plan["pair_bwd"]:
+            mode = "exclusive"  # one workgroup per CU (register-bound): nothing runs beside it
         plan["mode"] = mode
         plan["bwd_excl"] = mode == "exclusive" and excl_ok
         return plan
@@ -606,6 +617,7 @@ class NativeBackend:
         drop = self._dropout(True)
         c = self.cfg
         deferred = []
+        paired_done = -1  # lower layer whose BPTT already ran inside a two-layer wavefront
         for layer in reversed(range(self.L)):
             lw, lb = self._w[layer], bufs["layers"][layer]
             names = [sp.name for sp in cell_specs(self.cfg, layer)]
@@ -616,7 +628,26 @@ class NativeBackend:
             zx_nas = lb.zx if self.cfg.model == "nas" else None
             gather = (layer == 0 and not drop and self.cfg.model != "nas")
             fused_dew = bufs["persist"] and gather and V <= 128 and self.fused_dew
-            if bufs["persist"]:
+            pair_hi = bufs["pair_bwd"] and layer % 2 == 1 and not drop and dtop is not None
+            if pair_hi:
+                # layers (layer-1, layer) as one reverse wavefront (lstm2_persist.hip): T+1
+                # ticks, the lower layer's dtop = dZ·W_xᵀ of this layer computed in-kernel
+                lo = layer - 1
+                lw0, lb0 = self._w[lo], bufs["layers"][lo]
+                self.ops.lstm2_persist_bwd(lw0.Wh, lw.Wh, lw.Wx, dtop, lb0.gates, lb0.cbuf,
+                                           lb.gates, lb.cbuf, lb0.dz, lb.dz, bufs["zring"],
+                                           bufs["zring2"], bufs["db_part"][lo],
+                                           bufs["db_part"][layer], bufs["cnt"][self.L + lo],
+                                           bufs["cnt"][self.L + layer], self.err,
+                                           self.spin_limit)
+                paired_done = lo
+                if lo == 0 and pending:
+                    for off in pending:
+                        user_ready(off)
+                    pending.clear()
+            elif layer == paired_done:
+                pass
+            elif bufs["persist"]:
                 above = None
                 if dtop is None:  # dtop of this layer is fused: dZ_above · W_x,aboveᵀ in-kernel
                     above = (self._w[layer + 1].Wx, bufs["layers"][layer + 1].dz)
@@ -652,8 +683,8 @@ class NativeBackend:
             dZ = lb.dz.view(N, GW)
             dZx = lb.dzx.view(N, GW) if lb.dzx is not None else dZ
             Hprev = lb.hbuf[:T].reshape(N, H)
-            if (bufs["persist"] and layer > 0 and not drop and self.fused_dtop
-                    and self._exclusive_ok(bufs)):
+            if (bufs["persist"] and layer > 0 and not drop and self.fused_dtop and not pair_hi
+                    and layer != paired_done and self._exclusive_ok(bufs)):
                 # The layer below fuses dtop = dZ·W_xᵀ into its BPTT kernel.  That kernel holds
                 # W_h and W_x^{above} in registers (one workgroup per CU, grid = all CUs), so
                 # NOTHING may run beside it (a concurrent kernel holding CUs could deadlock the
@@ -670,7 +701,8 @@ class NativeBackend:
                 deferred.append(_wgrads)
                 dtop = None
                 continue
-            if bufs["persist"] and layer > 0 and not drop and self.side_overlap and overlap:
+            if (bufs["persist"] and layer > 0 and not drop and self.side_overlap and overlap
+                    and not pair_hi):
                 # Off the critical path: this layer's weight gradients (two [H x N]·[N x 4H]
                 # GEMMs) run on a side stream concurrently with the latency-bound BPTT of the
                 # layer below; the layer's all-reduce bucket is launched from that stream, so
@@ -739,6 +771,12 @@ class NativeBackend:
                 else:
                     self.ops.segsum(dZx, None, 1, bufs["colsum"][:, :GW], bufs["ws"], False)
                     dbias = bufs["colsum"][0, :GW]
+                if pair_hi:  # the lower layer's dtop was fused into the wavefront BPTT
+                    self._write_input_grads(layer, names, dWx, dbias)
+                    if on_ready is not None:
+                        on_ready(s.layer_range(layer)[1])
+                    dtop = None
+                    continue
                 dX = _mm_into(dZx, lw.Wx.t(), bufs["dx"].view(N, H)).view(T, B, H)
                 if "in" in lb.masks:
                     dX = dX * lb.masks["in"]

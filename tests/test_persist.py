@@ -153,3 +153,29 @@ def test_two_layer_wavefront_equals_single_layer_kernels(B, T, H, monkeypatch):
     ea, _ = a.backend.eval_loss(x, x, a.zero_state(B))
     eb, _ = b.backend.eval_loss(x, x, b.zero_state(B))
     assert abs(ea.item() - eb.item()) < 1e-4
+
+
+@pytest.mark.parametrize("B,T,H,L", [(32, 6, 128, 2), (256, 10, 512, 2), (64, 5, 384, 4),
+                                     (96, 4, 256, 3)])
+def test_two_layer_wavefront_bptt_equals_single_layer_kernels(B, T, H, L, monkeypatch):
+    """lstm2_bwd_persist_kernel (layers l and l+1 in one reverse wavefront, layer l's dtop
+    fused in-kernel) vs single-layer persistent BPTT launches + the dX GEMM."""
+    cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=L)
+    a = CharRNN(cfg, device="cuda", seed=5)
+    monkeypatch.setenv("DCR_PAIR_BWD", "0")
+    b = CharRNN(cfg, device="cuda", seed=5)
+    assert a.backend._persist_plan(B, True)["pair_bwd"]
+    assert not b.backend._persist_plan(B, True)["pair_bwd"]
+    torch.manual_seed(2)
+    x = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
+    y = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
+    sa, sb = a.zero_state(B), b.zero_state(B)
+    for _ in range(2):
+        la, sa, _ = a.backend.train_step(x, y, sa)
+        lb, sb, _ = b.backend.train_step(x, y, sb)
+    torch.cuda.synchronize()
+    a.backend.check_errors()
+    assert abs(la.item() - lb.item()) < 1e-4
+    for s in a.store.specs:
+        e = rel(a.store.gview(s.name), b.store.gview(s.name))
+        assert e < 2e-3, (s.name, e)
