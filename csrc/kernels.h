@@ -247,4 +247,22 @@ struct PrepTable {
 };
 void launch_prep(PrepTable& tab, hipStream_t s);
 
+
+// on-device sampling step (sample.hip): softmax head + categorical draw, one workgroup per stream
+struct SampleArgs {
+  const bf16* O;          // [S, H] top-layer output of this step
+  const bf16* WsT;        // [V, H] softmax_wᵀ (bf16)
+  const float* bs;        // [V] softmax_b
+  int* cur;               // [S] in: previous ids (sampling_type 2); out: the picks
+  int* out;               // [S, ld] generated ids; row s written at pos[s]
+  int* pos;               // [S] write positions (incremented)
+  unsigned* ctr;          // [S] RNG counters (incremented)
+  const float* u;         // optional [S] explicit uniforms in [0, 1) (tests)
+  float* logits_out;      // optional [S, V] fp32 logits (tests)
+  int S, H, V, ld, mode, space_id;
+  unsigned long long seed;
+};
+int sample_supported(int V, int H);
+void launch_sample_step(const SampleArgs& a, hipStream_t s);
+
 }  // namespace dcr

@@ -634,6 +634,42 @@ void lstm2_persist_bwd(const at::Tensor& Wh0, const at::Tensor& Wh1, const at::T
   TORCH_CHECK(rc == 0, "two-layer persistent LSTM BPTT not launched (", rc, ")");
 }
 
+// on-device sampling step (sample.hip)
+void sample_step(const at::Tensor& O, const at::Tensor& WsT, const at::Tensor& bs, at::Tensor& cur,
+                 at::Tensor& out, at::Tensor& pos, at::Tensor& ctr,
+                 const c10::optional<at::Tensor>& u, const c10::optional<at::Tensor>& logits,
+                 int64_t mode, int64_t space_id, int64_t seed) {
+  check_seq(O, at::kBFloat16, "O");
+  check_seq(WsT, at::kBFloat16, "WsT");
+  check_seq(bs, at::kFloat, "bs");
+  for (auto* t : {&cur, &out, &pos, &ctr}) check_seq(*t, at::kInt, "sampling state");
+  const int S = (int)O.size(0), H = (int)O.size(1), V = (int)WsT.size(0);
+  TORCH_CHECK(O.dim() == 2 && WsT.dim() == 2 && WsT.size(1) == H, "O [S, H], WsT [V, H]");
+  TORCH_CHECK(bs.numel() == V, "bs must be [V]");
+  TORCH_CHECK(dcr::sample_supported(V, H), "sampling kernel: V <= 8192, H % 8 == 0, H <= 4096");
+  TORCH_CHECK(cur.numel() == S && pos.numel() == S && ctr.numel() == S, "per-stream state must be [S]");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == S, "out must be [S, n]");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "sampling_type must be 0, 1 or 2");
+  dcr::SampleArgs a{};
+  a.O = ptr<bf16>(O); a.WsT = ptr<bf16>(WsT); a.bs = ptr<float>(bs);
+  a.cur = ptr<int>(cur); a.out = ptr<int>(out); a.pos = ptr<int>(pos);
+  a.ctr = reinterpret_cast<unsigned*>(ctr.data_ptr());
+  if (has(u)) {
+    check_seq(*u, at::kFloat, "u");
+    TORCH_CHECK(u->numel() == S, "u must be [S]");
+    a.u = ptr<float>(*u);
+  }
+  if (has(logits)) {
+    check_seq(*logits, at::kFloat, "logits");
+    TORCH_CHECK(logits->numel() == (int64_t)S * V, "logits must be [S, V]");
+    a.logits_out = ptr<float>(*logits);
+  }
+  a.S = S; a.H = H; a.V = V; a.ld = (int)out.size(1);
+  a.mode = (int)mode; a.space_id = (int)space_id;
+  a.seed = (unsigned long long)seed;
+  dcr::launch_sample_step(a, cur_stream());
+}
+
 // ------------------------------------------------------------------------------------------
 // persistent GRU recurrence (gru_persist.hip)
 // ------------------------------------------------------------------------------------------
@@ -918,6 +954,13 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor(c!) zring0, Tensor(d!) zring1, Tensor(e!)? db_part0, Tensor(f!)? db_part1, "
       "Tensor(g!) cnt0, Tensor(h!) cnt1, Tensor(i!) err, int spin_limit, "
       "Tensor(j!)? diag=None) -> ()");
+  m.def("sample_supported(int V, int H) -> int", [](int64_t V, int64_t H) -> int64_t {
+    return dcr::sample_supported((int)V, (int)H);
+  });
+  m.def(
+      "sample_step(Tensor O, Tensor WsT, Tensor bs, Tensor(a!) cur, Tensor(b!) out, "
+      "Tensor(c!) pos, Tensor(d!) ctr, Tensor? u, Tensor(e!)? logits, int mode, int space_id, "
+      "int seed) -> ()");
   m.def("gru_persist_ub(int H, int B) -> int", [](int64_t H, int64_t B) -> int64_t {
     return dcr::gru_persist_ub((int)H, (int)B, num_cus());
   });
@@ -951,5 +994,6 @@ TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("gru_persist_fwd", &gru_persist_fwd);
   m.impl("lstm2_persist_fwd", &lstm2_persist_fwd);
   m.impl("lstm2_persist_bwd", &lstm2_persist_bwd);
+  m.impl("sample_step", &sample_step);
   m.impl("gru_persist_bwd", &gru_persist_bwd);
 }

@@ -1,0 +1,26 @@
+"""Generation throughput of the device-side sampling loop (csrc/sample.hip + hipGraph replay)
+vs the eager loop, 2-layer LSTM-512, vocab 65 (random init).
+
+    PYTHONPATH=. python scripts/bench_sample.py
+"""
+import json
+import time
+
+import torch
+
+from distributed_char_rnn_amd.models.char_rnn import CharRNN
+from distributed_char_rnn_amd.models.params import ModelConfig
+
+cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=512, num_layers=2)
+m = CharRNN(cfg, device="cuda", seed=0)
+be = m.backend
+n = 500
+for S in (1, 64):
+    for graph in (True, False):
+        be.sample_sequence([1, 2], 20, 1, 0, S, 0, use_graph=graph)  # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        be.sample_sequence([1, 2], n, 1, 0, S, 0, use_graph=graph)
+        dt = time.perf_counter() - t0
+        print(json.dumps({"streams": S, "graph": graph, "chars": n, "us_per_step": dt / n * 1e6,
+                          "chars_per_sec": S * n / dt}))

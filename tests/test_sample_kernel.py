@@ -1,0 +1,104 @@
+"""On-device sampling step (csrc/sample.hip) vs a float64 PyTorch oracle, and the hipGraph
+generation loop (NativeBackend.sample_sequence) vs the eager loop.
+
+Reference semantics: Model.sample (model.py:105-140): argmax (0), inverse-CDF weighted pick
+``searchsorted(cumsum(p), rand * sum(p))`` (1), weighted only after a space else argmax (2)."""
+import pytest
+import torch
+
+from distributed_char_rnn_amd.models.char_rnn import CharRNN
+from distributed_char_rnn_amd.models.params import ModelConfig
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(S, H, V, seed=0, scale=1.0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    O = (torch.randn(S, H, device="cuda", generator=g) * scale).to(torch.bfloat16)
+    WsT = (torch.randn(V, H, device="cuda", generator=g) * 0.1).to(torch.bfloat16)
+    bs = torch.randn(V, device="cuda", generator=g) * 0.1
+    return O, WsT, bs
+
+
+def _state(S, n, prev):
+    i32 = dict(dtype=torch.int32, device="cuda")
+    return (torch.full((S,), prev, **i32), torch.full((S, n), -1, **i32),
+            torch.zeros(S, **i32), torch.zeros(S, **i32))
+
+
+@pytest.mark.parametrize("S,H,V", [(4, 64, 65), (33, 512, 65), (8, 256, 8192), (2, 128, 300)])
+def test_sample_step_matches_oracle(dcr_ops, S, H, V):
+    O, WsT, bs = _inputs(S, H, V)
+    ref_logits = O.double() @ WsT.double().t() + bs.double()
+    p = torch.softmax(ref_logits, -1)
+    cdf = torch.cumsum(p, -1)
+    # argmax
+    cur, out, pos, ctr = _state(S, 3, 0)
+    lg = torch.empty(S, V, device="cuda")
+    dcr_ops.sample_step(O, WsT, bs, cur, out, pos, ctr, None, lg, 0, -1, 1)
+    torch.cuda.synchronize()
+    assert torch.allclose(lg.double(), ref_logits, atol=1e-4, rtol=1e-4)
+    top2 = ref_logits.topk(2, -1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 1e-4
+    assert (out[:, 0].long() == ref_logits.argmax(-1))[clear].all()
+    assert (cur == out[:, 0]).all() and (pos == 1).all() and (ctr == 1).all()
+    # weighted pick with explicit uniforms
+    u = torch.rand(S, device="cuda")
+    cur, out, pos, ctr = _state(S, 2, 0)
+    dcr_ops.sample_step(O, WsT, bs, cur, out, pos, ctr, u, None, 1, -1, 1)
+    torch.cuda.synchronize()
+    want = torch.searchsorted(cdf, (u.double() * cdf[:, -1]).unsqueeze(1)).squeeze(1).clamp(max=V - 1)
+    # skip draws that land within rounding distance of a bucket edge
+    r = u.double() * cdf[:, -1]
+    near = (cdf - r.unsqueeze(1)).abs().min(-1).values < 1e-5
+    assert (out[:, 0].long() == want)[~near].all()
+
+
+def test_sample_step_mode2_space_rule(dcr_ops):
+    S, H, V, space = 16, 128, 65, 0
+    O, WsT, bs = _inputs(S, H, V, seed=3, scale=0.2)
+    prev = torch.tensor([space if i % 2 == 0 else 5 for i in range(S)], dtype=torch.int32,
+                        device="cuda")
+    u = torch.rand(S, device="cuda")
+    cur, out, pos, ctr = _state(S, 1, 0)
+    cur.copy_(prev)
+    dcr_ops.sample_step(O, WsT, bs, cur, out, pos, ctr, u, None, 2, space, 1)
+    cw, ow, pw, kw = _state(S, 1, 0)
+    dcr_ops.sample_step(O, WsT, bs, cw, ow, pw, kw, u, None, 1, space, 1)
+    ca, oa, pa, ka = _state(S, 1, 0)
+    dcr_ops.sample_step(O, WsT, bs, ca, oa, pa, ka, u, None, 0, space, 1)
+    torch.cuda.synchronize()
+    even = torch.arange(S, device="cuda") % 2 == 0
+    assert (out[even, 0] == ow[even, 0]).all()       # after a space: weighted pick
+    assert (out[~even, 0] == oa[~even, 0]).all()     # otherwise: argmax
+
+
+def test_sample_step_distribution(dcr_ops):
+    """Hash-RNG draws follow softmax(logits): 16k streams of one distribution."""
+    S, H, V = 16384, 64, 65
+    O1, WsT, bs = _inputs(1, H, V, seed=7, scale=2.0)
+    O = O1.expand(S, H).contiguous()
+    cur, out, pos, ctr = _state(S, 1, 0)
+    dcr_ops.sample_step(O, WsT, bs, cur, out, pos, ctr, None, None, 1, -1, 12345)
+    torch.cuda.synchronize()
+    p = torch.softmax(O1.double() @ WsT.double().t() + bs.double(), -1)[0]
+    freq = torch.bincount(out[:, 0].long(), minlength=V).double() / S
+    assert (freq - p).abs().max().item() < 0.015
+    # the counter advanced: a second draw differs from the first for most streams
+    dcr_ops.sample_step(O, WsT, bs, cur, torch.zeros_like(out), torch.zeros_like(pos), ctr, None,
+                        None, 1, -1, 12345)
+    assert (ctr == 2).all()
+
+
+@pytest.mark.parametrize("model,S", [("lstm", 1), ("lstm", 32), ("gru", 4)])
+def test_sample_sequence_graph_equals_eager(model, S):
+    cfg = ModelConfig(model=model, vocab_size=65, rnn_size=128, num_layers=2)
+    m = CharRNN(cfg, device="cuda", seed=1)
+    be = m.backend
+    a = be.sample_sequence([3, 7, 1], 40, 1, seed=99, num_samples=S, space_id=0, use_graph=True)
+    b = be.sample_sequence([3, 7, 1], 40, 1, seed=99, num_samples=S, space_id=0, use_graph=False)
+    assert a == b
+    assert len(a) == S and all(len(r) == 40 for r in a)
+    assert all(0 <= c < 65 for r in a for c in r)
+    c = be.sample_sequence([3, 7, 1], 40, 1, seed=100, num_samples=S, space_id=0)
+    assert c != a  # a different seed draws a different sequence
