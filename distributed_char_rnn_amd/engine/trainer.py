@@ -218,6 +218,7 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
                 opt.step(lr)
             global_step += 1
             steps_done += 1
+            process_group.maybe_inject_fault(rank, global_step)
             if pending is not None:
                 flush(pending, t0)
             pending = (global_step, e, loss_t, t0)

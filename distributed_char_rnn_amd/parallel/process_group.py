@@ -5,10 +5,15 @@ train.py:117-135) and the chief/non-chief session logic of ``MonitoredTrainingSe
 (train.py:157-163).  One process drives one GPU; collectives go through ``torch.distributed``
 with the ``nccl`` backend, which is RCCL over xGMI on ROCm, or ``gloo`` for CPU tests.
 
-Failure detection: every collective carries ``--dist_timeout``; with
-``--heartbeat S`` each rank refreshes ``hb/<rank>`` in the store every S seconds and rank 0 logs
-ranks whose heartbeat is older than 3·S.  Recovery is checkpoint based: relaunch all ranks with
-``--init_from <save_dir>``.
+Failure detection (the reference has none -- a dead PS or worker leaves the
+others blocked in gRPC, train.py:129-130): every collective carries ``--dist_timeout``; with
+``--heartbeat S`` each rank refreshes ``hb/<rank>`` in the store every S seconds, rank 0 marks
+a rank whose heartbeat is older than 3·S as lost by setting ``abort`` in the store, and every
+rank's heartbeat thread that sees ``abort`` (or loses the store, i.e. rank 0 died) ends its
+process with ``EXIT_PEER_LOST`` instead of waiting out the collective timeout.  Recovery is
+checkpoint based: relaunch all ranks with ``--init_from <save_dir>`` (``--resume_exact``
+continues at the saved epoch/batch).  ``DCR_FAULT=<rank>:<step>`` kills that rank at that global
+step (fault injection for the tests).
 """
 from __future__ import annotations
 
@@ -22,6 +27,20 @@ import torch
 import torch.distributed as dist
 
 from .topology import Topology
+
+
+EXIT_PEER_LOST = 75  # EX_TEMPFAIL: a peer died; relaunch every rank with --init_from
+
+
+def maybe_inject_fault(rank: int, global_step: int, log=print):
+    """``DCR_FAULT=<rank>:<step>``: simulate a crash of ``rank`` at ``global_step``."""
+    spec = os.environ.get("DCR_FAULT", "")
+    if not spec:
+        return
+    r, _, st = spec.partition(":")
+    if int(r) == rank and int(st) == global_step:
+        log(f"[fault] injected crash of rank {rank} at step {global_step}")
+        os._exit(17)
 
 
 class DistContext:
@@ -79,10 +98,18 @@ class DistContext:
         if period <= 0 or self.store is None or not self.enabled:
             return
 
+        def lost(msg):
+            log(f"[heartbeat] rank {self.rank}: {msg}; exiting with {EXIT_PEER_LOST} "
+                "(relaunch all ranks with --init_from)")
+            os._exit(EXIT_PEER_LOST)
+
         def run():
+            failures = 0
             while not self._hb_stop.wait(period):
                 try:
                     self.store.set(f"hb/{self.rank}", str(time.time()))
+                    if self.store.check(["abort"]):
+                        lost("abort: " + self.store.get("abort").decode())
                     if self.rank == 0:
                         now = time.time()
                         for r in range(self.world_size):
@@ -91,9 +118,15 @@ class DistContext:
                             except Exception:
                                 continue
                             if now - ts > 3 * period:
-                                log(f"[heartbeat] rank {r} silent for {now - ts:.1f}s")
+                                self.store.set("abort", f"rank {r} silent for {now - ts:.1f}s")
+                                lost(f"rank {r} silent for {now - ts:.1f}s")
+                    failures = 0
                 except Exception:
-                    return
+                    if self._hb_stop.is_set():
+                        return
+                    failures += 1
+                    if failures >= 3:  # the store (rank 0 / ps) is gone
+                        lost("rendezvous store unreachable")
 
         self.store.set(f"hb/{self.rank}", str(time.time()))
         self._hb_thread = threading.Thread(target=run, daemon=True, name="dcr-heartbeat")
@@ -137,7 +170,11 @@ def init(topo: Topology, device: torch.device, backend: str = "auto",
     if topo.from_env:
         dist.init_process_group(backend=backend, timeout=timeout,
                                 device_id=device if device.type == "cuda" else None)
-        return DistContext(topo, device, backend)
+        try:  # torchrun's rendezvous store, for heartbeats
+            store = dist.distributed_c10d._get_default_store()
+        except Exception:
+            store = None
+        return DistContext(topo, device, backend, store=store)
     is_master = (topo.rank == 0 and not topo.store_host_is_ps)
     store = dist.TCPStore(topo.master_addr, topo.master_port, world_size=None,
                           is_master=is_master, timeout=timeout, wait_for_workers=False)
