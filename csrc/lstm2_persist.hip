@@ -29,9 +29,10 @@ namespace dcr {
 
 template <int KS, bool DIAG = false>
 __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) {
-  // partials [wave][layer][tile][lane][gate*4 + r]: single-buffered -- every tick after the
-  // first starts with the poll barrier, which each epilogue wave joins after its reads
-  __shared__ __attribute__((aligned(16))) float part[4][2][2][64][16];
+  // partials [wave][layer][tile][gate][lane][r] (16-B lane stride: conflict-free b128 LDS
+  // access), single-buffered -- every tick after the first starts with the poll barrier, which
+  // each epilogue wave joins after its reads
+  __shared__ __attribute__((aligned(16))) float part[4][2][2][4][64][4];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
@@ -139,9 +140,10 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
         for (int s = 0; s < KS; ++s)
 #pragma unroll
           for (int g = 0; g < 4; ++g) acc[g] = mfma16(w0[g][s], hf0[j][s], acc[g]);
-        float4* dst = reinterpret_cast<float4*>(&part[w][0][j][lane][0]);
+        float* dst = &part[w][0][j][0][lane][0];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) dst[g] = make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<float4*>(dst + g * 256) = make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
       }
       if (on1) {
         f32x4 acc[4];
@@ -154,9 +156,10 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
             acc[g] = mfma16(x1[g][s], hf0[j][s], acc[g]);
             acc[g] = mfma16(w1[g][s], hf1[j][s], acc[g]);
           }
-        float4* dst = reinterpret_cast<float4*>(&part[w][1][j][lane][0]);
+        float* dst = &part[w][1][j][0][lane][0];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) dst[g] = make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<float4*>(dst + g * 256) = make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
       }
     }
     STAMP2(3)
@@ -167,10 +170,10 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
       float z[4][4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const float4 s0 = reinterpret_cast<const float4*>(&part[0][L][J][lane][0])[g];
-        const float4 s1 = reinterpret_cast<const float4*>(&part[1][L][J][lane][0])[g];
-        const float4 s2 = reinterpret_cast<const float4*>(&part[2][L][J][lane][0])[g];
-        const float4 s3 = reinterpret_cast<const float4*>(&part[3][L][J][lane][0])[g];
+        const float4 s0 = *reinterpret_cast<const float4*>(&part[0][L][J][g][lane][0]);
+        const float4 s1 = *reinterpret_cast<const float4*>(&part[1][L][J][g][lane][0]);
+        const float4 s2 = *reinterpret_cast<const float4*>(&part[2][L][J][g][lane][0]);
+        const float4 s3 = *reinterpret_cast<const float4*>(&part[3][L][J][g][lane][0]);
         const float* add = L == 0 ? zx[g] : bias1[g];
         z[g][0] = s0.x + s1.x + s2.x + s3.x + add[0];
         z[g][1] = s0.y + s1.y + s2.y + s3.y + add[1];

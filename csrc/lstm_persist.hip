@@ -49,7 +49,7 @@ template <int KS, int UB, bool DIAG = false, bool XF = false>
 __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a) {
   // partials double-buffered by step parity: without a workgroup barrier before the MFMAs a
   // wave may start step t+1 while the epilogue wave still reads step t's partials
-  __shared__ __attribute__((aligned(16))) float part[2][4][UB][64][16];
+  __shared__ __attribute__((aligned(16))) float part[2][4][UB][4][64][4];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
@@ -159,10 +159,11 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
       for (int s = 0; s < KS; ++s)
 #pragma unroll
         for (int g = 0; g < 4; ++g) acc[ui][g] = mfma16(wf[ui][g][s], hf[s], acc[ui][g]);
-      float4* dst = reinterpret_cast<float4*>(&part[t & 1][w][ui][lane][0]);
+      float* dst = &part[t & 1][w][ui][0][lane][0];
 #pragma unroll
       for (int g = 0; g < 4; ++g)
-        dst[g] = make_float4(acc[ui][g][0], acc[ui][g][1], acc[ui][g][2], acc[ui][g][3]);
+        *reinterpret_cast<float4*>(dst + g * 256) =
+            make_float4(acc[ui][g][0], acc[ui][g][1], acc[ui][g][2], acc[ui][g][3]);
     }
     STAMP(3)
     __syncthreads();
@@ -171,10 +172,10 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
       float z[4][4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        float4 s0 = reinterpret_cast<const float4*>(&part[t & 1][0][w][lane][0])[g];
-        float4 s1 = reinterpret_cast<const float4*>(&part[t & 1][1][w][lane][0])[g];
-        float4 s2 = reinterpret_cast<const float4*>(&part[t & 1][2][w][lane][0])[g];
-        float4 s3 = reinterpret_cast<const float4*>(&part[t & 1][3][w][lane][0])[g];
+        float4 s0 = *reinterpret_cast<const float4*>(&part[t & 1][0][w][g][lane][0]);
+        float4 s1 = *reinterpret_cast<const float4*>(&part[t & 1][1][w][g][lane][0]);
+        float4 s2 = *reinterpret_cast<const float4*>(&part[t & 1][2][w][g][lane][0]);
+        float4 s3 = *reinterpret_cast<const float4*>(&part[t & 1][3][w][g][lane][0]);
         z[g][0] = s0.x + s1.x + s2.x + s3.x + zx[g][0];
         z[g][1] = s0.y + s1.y + s2.y + s3.y + zx[g][1];
         z[g][2] = s0.z + s1.z + s2.z + s3.z + zx[g][2];
@@ -243,7 +244,7 @@ __device__ __forceinline__ uint64_t granule(float a, float b, unsigned tag) {
 
 template <int KS, int UB>
 __global__ void __launch_bounds__(256, 1) lstm_fwd_granule_kernel(PersistArgs a) {
-  __shared__ __attribute__((aligned(16))) float part[2][4][UB][64][16];  // parity double buffer
+  __shared__ __attribute__((aligned(16))) float part[2][4][UB][4][64][4];  // parity double buffer
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
@@ -343,19 +344,20 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_granule_kernel(PersistArgs a)
       for (int s = 0; s < KS; ++s)
 #pragma unroll
         for (int g = 0; g < 4; ++g) acc[g] = mfma16(wf[ui][g][s], hf[s], acc[g]);
-      float4* dst = reinterpret_cast<float4*>(&part[t & 1][w][ui][lane][0]);
+      float* dst = &part[t & 1][w][ui][0][lane][0];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) dst[g] = make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(dst + g * 256) = make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
     }
     __syncthreads();
     if (epi) {
       float z[4][4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        float4 s0 = reinterpret_cast<const float4*>(&part[t & 1][0][w][lane][0])[g];
-        float4 s1 = reinterpret_cast<const float4*>(&part[t & 1][1][w][lane][0])[g];
-        float4 s2 = reinterpret_cast<const float4*>(&part[t & 1][2][w][lane][0])[g];
-        float4 s3 = reinterpret_cast<const float4*>(&part[t & 1][3][w][lane][0])[g];
+        float4 s0 = *reinterpret_cast<const float4*>(&part[t & 1][0][w][g][lane][0]);
+        float4 s1 = *reinterpret_cast<const float4*>(&part[t & 1][1][w][g][lane][0]);
+        float4 s2 = *reinterpret_cast<const float4*>(&part[t & 1][2][w][g][lane][0]);
+        float4 s3 = *reinterpret_cast<const float4*>(&part[t & 1][3][w][g][lane][0]);
         z[g][0] = s0.x + s1.x + s2.x + s3.x + zx[g][0];
         z[g][1] = s0.y + s1.y + s2.y + s3.y + zx[g][1];
         z[g][2] = s0.z + s1.z + s2.z + s3.z + zx[g][2];

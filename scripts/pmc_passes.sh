@@ -1,0 +1,19 @@
+#!/bin/bash
+# rocprofv3 PMC passes over a short headline bench run (one counter group per run, each under
+# its own time limit; the slot limits of MI355X_MICROARCH.md "rocprofv3 PMC slots").
+set -o pipefail
+export TMPDIR=/tmp PYTHONPATH=$PWD
+mkdir -p gpurun_out/pmc
+i=0
+for pass in \
+  "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES" \
+  "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT" \
+  "TCC_HIT TCC_MISS TCC_REQ" \
+  "FETCH_SIZE" \
+  "WRITE_SIZE"; do
+  i=$((i+1))
+  echo "== pass $i: $pass"
+  timeout -s KILL 90 rocprofv3 --pmc $pass -d gpurun_out/pmc/p$i -o run --output-format csv -- \
+    python3 bench.py --steps 5 --warmup 2 > gpurun_out/pmc/p$i.log 2>&1 || { tail -5 gpurun_out/pmc/p$i.log; exit 1; }
+done
+echo done
