@@ -33,6 +33,7 @@ from ..ops import native
 
 CELL_ID = {"lstm": 0, "gru": 1, "rnn": 3, "nas": 4}
 FORGET_BIAS = 1.0
+PERSIST_MIN_T = 8  # shortest sequence that takes the persistent (weights-resident) kernels
 SEG_LDS_MAX_V = 96  # csrc/embed.hip kSegLdsMaxV: larger vocabularies take the atomic scatter
 # lstm_persist_occupancy flags (csrc/lstm_persist.hip PF_*)
 PF_FUSED, PF_DIAG, PF_EXCL, PF_GRANULE = 1, 2, 4, 8
@@ -157,6 +158,7 @@ class NativeBackend:
         self._head = None
         self._bufs: Dict[Tuple[int, int, bool], dict] = {}
         self.use_persist = os.environ.get("DCR_PERSIST", "1") != "0"
+        self.persist_min_t = int(os.environ.get("DCR_PERSIST_MIN_T", str(PERSIST_MIN_T)))
         # two-layer wavefront forward (lstm2_persist.hip) for layers (0, 1)
         self.use_pair = os.environ.get("DCR_PAIR", "1") != "0"
         # two-layer wavefront BPTT (lstm2_persist.hip) for the same pairs
@@ -297,7 +299,7 @@ class NativeBackend:
                     if (training and self.V <= SEG_LDS_MAX_V) else None),
             colpart=(torch.empty(self.ops.xent_wide_waves(N) * self.V, dtype=f32, device=dev)
                      if (training and self._wide_xent(N)) else None),
-            **self._persist_plan(B, training),
+            **self._persist_plan(B, training, T),
             dtop=torch.empty(T, B, H, dtype=f32, device=dev) if training else None,
             dx=torch.empty(T, B, H, dtype=f32, device=dev) if training else None,
             db_part=(torch.empty(self.L, max(B // 16, 1), GW, dtype=f32, device=dev)
@@ -352,7 +354,7 @@ class NativeBackend:
 
         return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
-    def _persist_plan(self, B: int, training: bool) -> dict:
+    def _persist_plan(self, B: int, training: bool, T: int = 1 << 30) -> dict:
         """Residency plan for the persistent kernels at batch ``B``.
 
         Every workgroup of a persistent grid spins on its neighbours, so the whole grid must be
@@ -376,6 +378,11 @@ class NativeBackend:
         plan = dict(persist=False, xfuse=False, mode="exclusive", bwd_excl=False,
                     gru_persist=False, pair=False, pair_bwd=False)
         o = self.ops
+        if T < self.persist_min_t:
+            # a persistent grid first loads every weight slice into registers (~6 MB for the
+            # 2-layer H=512 pair); for a handful of steps (sampling: T = 1) the per-step kernels,
+            # which stream W_h from L2, are faster (sampling 50 -> see scripts/bench_sample.py)
+            return plan
         if self.use_persist and self.cfg.model == "gru":
             # persistent GRU (gru_persist.hip): the C++ side picks the unit block whose fwd and
             # bwd grids are co-resident; always exclusive (nothing beside it)

@@ -18,6 +18,7 @@ def rel(a, b):
 @pytest.fixture(autouse=True)
 def _short_spins(monkeypatch):
     monkeypatch.setenv("DCR_SPIN_LIMIT", str(1 << 20))
+    monkeypatch.setenv("DCR_PERSIST_MIN_T", "1")  # short test sequences still take these kernels
 
 
 def _model(B, H, L, seed=3, **kw):

@@ -20,6 +20,7 @@ def rel(a, b):
 @pytest.fixture(autouse=True, params=["granule", "counter"])
 def _short_spins(monkeypatch, request):
     monkeypatch.setenv("DCR_SPIN_LIMIT", str(1 << 20))
+    monkeypatch.setenv("DCR_PERSIST_MIN_T", "1")  # short test sequences still take these kernels
     monkeypatch.setenv("DCR_HANDOFF", request.param)
 
 
