@@ -37,17 +37,21 @@ template <> struct CellG<CELL_NAS> { static constexpr int G = 8; };
 
 // Block-cooperative tile GEMM over NBT batch tiles:
 //   acc_j[t] = sum_k A[arow_t][k] * Bm[brow_j][k]   over k in [0, K), j < NBT.
-// The 4 waves take interleaved 32-wide k-steps (wave w: s = w, w+4, ...), keep the next step's
-// fragments in flight while the current MFMAs run, and meet in LDS; each A fragment feeds NBT
-// MFMAs, so a workgroup reads its weight slice once per NBT x 16 batch rows (the per-step
-// kernels are L2/MALL-bandwidth bound at large H).  On return wave w < NBT holds the full sums
-// of batch tile w; the other waves return garbage and must not use them.
+// The 4 waves take interleaved 32-wide k-steps (wave w: s = w, w+4, ...) and meet in LDS; each
+// A fragment feeds NBT MFMAs, so a workgroup reads its weight slice once per NBT x 16 batch rows.
+// At large H these kernels stream their weight slice from L2/MALL every step and are bound by
+// loads in flight (one 256-workgroup grid, one workgroup per CU: ~23 GB/s per CU with two stages
+// in flight at H = 2048), so the k loop is software-pipelined PD stages deep: PD-1 k-steps of
+// fragments (~24 16-B loads per lane) are in flight while the MFMAs of the current one run.
+// On return wave w < NBT holds the full sums of batch tile w; the other waves return garbage and
+// must not use them.
 template <int NT, int NBT>
 __device__ __forceinline__ void tile_gemm(f32x4 (&acc)[NT], const bf16* __restrict__ A,
                                           const int (&arow)[NT], int lda,
                                           const bf16* __restrict__ Bm, const int (&brow)[NBT],
                                           int ldb, int K, int lane, int w,
                                           float* part /* [4][NT][NBT][64][4] */) {
+  constexpr int PD = (24 / (NT + NBT)) < 2 ? 2 : ((24 / (NT + NBT)) > 8 ? 8 : 24 / (NT + NBT));
   const int kq = 8 * (lane >> 4);
   const bf16* bp[NBT];
 #pragma unroll
@@ -61,28 +65,35 @@ __device__ __forceinline__ void tile_gemm(f32x4 (&acc)[NT], const bf16* __restri
     for (int j = 0; j < NBT; ++j) c[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   const int KS = K / 32;
-  int s = w;
-  if (s < KS) {
-    bf16x8 b[NBT], a[NT];
+  const int n = w < KS ? (KS - w + 3) / 4 : 0;  // this wave's k-steps: s = w + 4 i, i < n
+  bf16x8 ra[PD][NT], rb[PD][NBT];
 #pragma unroll
-    for (int j = 0; j < NBT; ++j) b[j] = ld8(bp[j] + s * 32);
+  for (int p = 0; p < PD - 1; ++p)
+    if (p < n) {
+      const int s = w + 4 * p;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) a[t] = ld8(ap[t] + s * 32);
-    for (; s < KS; s += 4) {
-      const int sn = s + 4 < KS ? s + 4 : s;  // prefetch (re-load the last step when done)
-      bf16x8 bn[NBT], an[NT];
+      for (int j = 0; j < NBT; ++j) rb[p][j] = ld8(bp[j] + s * 32);
 #pragma unroll
-      for (int j = 0; j < NBT; ++j) bn[j] = ld8(bp[j] + sn * 32);
+      for (int t = 0; t < NT; ++t) ra[p][t] = ld8(ap[t] + s * 32);
+    }
+  for (int i0 = 0; i0 < n; i0 += PD) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) an[t] = ld8(ap[t] + sn * 32);
+    for (int q = 0; q < PD; ++q) {
+      const int i = i0 + q;
+      if (i < n) {
+        if (i + PD - 1 < n) {  // refill the slot freed one step ago
+          const int s = w + 4 * (i + PD - 1);
+          const int slot = (q + PD - 1) % PD;
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
+          for (int j = 0; j < NBT; ++j) rb[slot][j] = ld8(bp[j] + s * 32);
 #pragma unroll
-        for (int j = 0; j < NBT; ++j) c[t][j] = mfma16(a[t], b[j], c[t][j]);
+          for (int t = 0; t < NT; ++t) ra[slot][t] = ld8(ap[t] + s * 32);
+        }
 #pragma unroll
-      for (int j = 0; j < NBT; ++j) b[j] = bn[j];
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int t = 0; t < NT; ++t) a[t] = an[t];
+          for (int j = 0; j < NBT; ++j) c[t][j] = mfma16(ra[q][t], rb[q][j], c[t][j]);
+      }
     }
   }
 #pragma unroll
