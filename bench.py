@@ -43,6 +43,10 @@ def parse(argv=None):
     ap.add_argument("--bucket_mb", type=float, default=8.0)
     ap.add_argument("--allreduce_dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--profile", action="store_true", help="print a per-phase timing table")
+    ap.add_argument("--dist_backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="auto = nccl (RCCL over xGMI) on GPUs; gloo = multi-rank rehearsal on "
+                         "one GPU (with DCR_PERSIST=0: persistent grids of two processes cannot "
+                         "share the CUs)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu = plumbing check of the multi-rank contract (reference backend, gloo)")
     return ap.parse_args(argv)
@@ -64,7 +68,9 @@ def main(argv=None) -> int:
                   file=sys.stderr)
             return 2
     device = process_group.pick_device(topo, a.device)
-    ctx = process_group.init(topo, device, "nccl" if device.type == "cuda" else "gloo")
+    backend = a.dist_backend if a.dist_backend != "auto" else (
+        "nccl" if device.type == "cuda" else "gloo")
+    ctx = process_group.init(topo, device, backend)
 
     def sync_dev():
         if device.type == "cuda":
