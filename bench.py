@@ -106,15 +106,15 @@ def main(argv=None) -> int:
         sync.reset()
         if prof is None:
             loss, state, _ = model.train_step(x, y, state, sync)
-            sync.finish()
-            opt.step(2e-3)
+            gs = sync.finish(defer_scale=True)
+            opt.step(2e-3, grad_scale=gs)
         else:
             with prof.phase("fwd_bwd"):
                 loss, state, _ = model.train_step(x, y, state, sync)
             with prof.phase("grad_sync"):
-                sync.finish()
+                gs = sync.finish(defer_scale=True)
             with prof.phase("optimizer"):
-                opt.step(2e-3)
+                opt.step(2e-3, grad_scale=gs)
         return loss, state
 
     for i in range(a.warmup):

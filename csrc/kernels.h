@@ -14,7 +14,7 @@ void launch_global_norm(const float* g, int64_t n, float* partials, float* norm_
                         hipStream_t stream);
 void launch_adam_clip(float* p, const float* g, float* m, float* v, bf16* pbf, int64_t n,
                       float* partials, float* norm_out, float lr_t, float b1, float b2, float eps,
-                      float clip, hipStream_t stream);
+                      float clip, float gscale, hipStream_t stream);
 
 // ---- rnn_step.hip -----------------------------------------------------------------------
 enum CellKind { CELL_LSTM = 0, CELL_GRU_A = 1, CELL_GRU_B = 2, CELL_RNN = 3, CELL_NAS = 4 };

@@ -38,7 +38,7 @@ void global_norm(const at::Tensor& g, at::Tensor& partials, at::Tensor& norm_out
 
 void adam_clip(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
                const c10::optional<at::Tensor>& pbf, at::Tensor& partials, at::Tensor& norm_out,
-               double lr_t, double b1, double b2, double eps, double clip) {
+               double lr_t, double b1, double b2, double eps, double clip, double gscale) {
   for (const at::Tensor* t : {(const at::Tensor*)&p, &g, (const at::Tensor*)&m, (const at::Tensor*)&v}) {
     CHECK_DEV(*t); CHECK_CONTIG(*t); CHECK_F32(*t); CHECK_ALIGN16(*t);
     TORCH_CHECK(t->numel() == p.numel(), "adam buffers must have equal numel");
@@ -52,7 +52,7 @@ void adam_clip(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
   TORCH_CHECK(partials.numel() >= dcr::opt_num_partials(p.numel()), "partials too small");
   dcr::launch_adam_clip(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), pb,
                         p.numel(), ptr<float>(partials), ptr<float>(norm_out), (float)lr_t,
-                        (float)b1, (float)b2, (float)eps, (float)clip, cur_stream());
+                        (float)b1, (float)b2, (float)eps, (float)clip, (float)gscale, cur_stream());
 }
 
 // ------------------------------------------------------------------------------------------
@@ -875,7 +875,7 @@ TORCH_LIBRARY(dcr, m) {
   m.def(
       "adam_clip(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? pbf, "
       "Tensor(e!) partials, Tensor(f!) norm_out, float lr_t, float b1, float b2, float eps, "
-      "float clip) -> ()");
+      "float clip, float gscale=1.0) -> ()");
   m.def(
       "rnn_fwd_seq(int cell, Tensor WT, Tensor? WT2, Tensor zx, Tensor? ids, Tensor(a!) hbuf, "
       "Tensor(b!)? h32, Tensor(c!)? cbuf, Tensor(d!)? gates, Tensor(e!)? pre, Tensor(f!)? aux, "

@@ -6,7 +6,7 @@
 //   1. sumsq_partials: grid-stride float4 sum of g^2, one partial per block (fixed grid =>
 //      deterministic order).
 //   2. adam_apply: every block re-reduces the (<=1024) partials in LDS, derives
-//      scale = clip / max(||g||, clip) and applies
+//      scale = clip / max(||g||, clip) (g optionally pre-scaled by 1/world) and applies
 //        m = b1 m + (1-b1) g s ;  v = b2 v + (1-b2) (g s)^2 ;  p -= lr_t m / (sqrt(v) + eps)
 //      with TF's lr_t = lr * sqrt(1-b2^t) / (1-b1^t) computed on the host (TF "epsilon-hat").
 //      Optionally refreshes a bf16 mirror of the parameters in the same pass.
@@ -47,14 +47,17 @@ __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, 
 __global__ void __launch_bounds__(kOptThreads) adam_apply_kernel(
     float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
     bf16* __restrict__ pbf, int64_t n, const float* __restrict__ partials, int nparts,
-    float* __restrict__ norm_out, float lr_t, float b1, float b2, float eps, float clip) {
+    float* __restrict__ norm_out, float lr_t, float b1, float b2, float eps, float clip,
+    float gscale) {
   __shared__ float red[kOptThreads / 64];
   float acc = 0.f;
   for (int i = threadIdx.x; i < nparts; i += kOptThreads) acc += partials[i];
   const float sumsq = block_sum<kOptThreads>(acc, red);
-  const float norm = sqrtf(sumsq);
+  // gscale folds the data-parallel 1/world average into this pass (the gradient buffer holds
+  // the all-reduced SUM): the norm and the update see g * gscale
+  const float norm = sqrtf(sumsq) * gscale;
   // TF clip_by_global_norm: t * clip / max(norm, clip); clip <= 0 disables clipping.
-  const float s = (clip > 0.f) ? clip / fmaxf(norm, clip) : 1.f;
+  const float s = ((clip > 0.f) ? clip / fmaxf(norm, clip) : 1.f) * gscale;
   if (blockIdx.x == 0 && threadIdx.x == 0 && norm_out) norm_out[0] = norm;
 
   const int64_t n4 = n >> 2;
@@ -115,11 +118,11 @@ void launch_global_norm(const float* g, int64_t n, float* partials, float* norm_
 
 void launch_adam_clip(float* p, const float* g, float* m, float* v, bf16* pbf, int64_t n,
                       float* partials, float* norm_out, float lr_t, float b1, float b2, float eps,
-                      float clip, hipStream_t stream) {
+                      float clip, float gscale, hipStream_t stream) {
   const int nb = opt_num_partials(n);
   sumsq_partials_kernel<<<nb, kOptThreads, 0, stream>>>(g, n, partials);
   adam_apply_kernel<<<nb, kOptThreads, 0, stream>>>(p, g, m, v, pbf, n, partials, nb, norm_out,
-                                                    lr_t, b1, b2, eps, clip);
+                                                    lr_t, b1, b2, eps, clip, gscale);
 }
 
 }  // namespace dcr

@@ -50,18 +50,20 @@ class TFAdam:
         return lr * math.sqrt(1.0 - self.b2 ** t) / (1.0 - self.b1 ** t)
 
     @torch.no_grad()
-    def step(self, lr: float) -> torch.Tensor:
-        """Clip the (already averaged) flat gradient by global norm and apply one update.
-        Returns the pre-clip global norm as a 1-element device tensor (no host sync)."""
+    def step(self, lr: float, grad_scale: float = 1.0) -> torch.Tensor:
+        """Clip the flat gradient (times ``grad_scale``: 1/world when the data-parallel average
+        is folded in here, see ``GradSync.finish(defer_scale=True)``) by global norm and apply
+        one update.  Returns the pre-clip global norm as a 1-element device tensor (no host
+        sync)."""
         lr_t = self.lr_t(lr)
         p, g = self.store.flat, self.store.grad
         if self.native:
             self._ops.adam_clip(p, g, self.m, self.v, self.mirror, self._partials, self.last_norm,
-                                lr_t, self.b1, self.b2, self.eps, self.clip)
+                                lr_t, self.b1, self.b2, self.eps, self.clip, float(grad_scale))
         else:
-            norm = torch.sqrt((g.double() * g.double()).sum()).float()
+            norm = torch.sqrt((g.double() * g.double()).sum()).float() * grad_scale
             s = self.clip / torch.clamp(norm, min=self.clip) if self.clip > 0 else torch.ones(())
-            gs = g * s
+            gs = g * (s * grad_scale)
             self.m.mul_(self.b1).add_(gs, alpha=1 - self.b1)
             self.v.mul_(self.b2).addcmul_(gs, gs, value=1 - self.b2)
             p.sub_(lr_t * self.m / (self.v.sqrt() + self.eps))

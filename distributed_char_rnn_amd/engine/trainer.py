@@ -213,9 +213,9 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
             with prof.phase("fwd_bwd"):
                 loss_t, state, extras = _step(model, x, y, state, sync, want)
             with prof.phase("grad_sync"):
-                sync.finish()
+                gs = sync.finish(defer_scale=True)
             with prof.phase("optimizer"):
-                opt.step(lr)
+                opt.step(lr, grad_scale=gs)
             global_step += 1
             steps_done += 1
             process_group.maybe_inject_fault(rank, global_step)

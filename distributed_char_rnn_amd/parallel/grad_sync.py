@@ -79,10 +79,13 @@ class GradSync:
                 self._work.append((w, lo, hi, None))
             self._next += 1
 
-    def finish(self):
-        """Wait for all buckets and average (sum / world)."""
+    def finish(self, defer_scale: bool = False) -> float:
+        """Wait for all buckets and average (sum / world).  With ``defer_scale`` the buffer is
+        left holding the sum and the returned factor (1/world) is meant for
+        ``TFAdam.step(lr, grad_scale=...)``, which folds it into its clip/update pass (one fewer
+        pass over the gradient buffer)."""
         if not self.enabled:
-            return
+            return 1.0
         self.ready(None)
         for w, lo, hi, wire in self._work:
             w.wait()
@@ -90,7 +93,10 @@ class GradSync:
                 self.store.grad[lo:hi].copy_(wire)
         self._work.clear()
         self._next = 0
+        if defer_scale:
+            return 1.0 / self.world
         self.store.grad.mul_(1.0 / self.world)
+        return 1.0
 
     def broadcast_params(self, src: int = 0):
         if self.enabled:

@@ -41,3 +41,23 @@ def test_adam_clip_matches_reference(dcr_ops, n, clip):
     torch.testing.assert_close(v, rv, rtol=1e-5, atol=1e-9)
     torch.testing.assert_close(p, rp, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(pbf.float(), p.to(torch.bfloat16).float(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_adam_clip_folds_data_parallel_average(dcr_ops, world):
+    """gscale = 1/world on the all-reduced SUM == the kernel on the averaged gradient."""
+    torch.manual_seed(1)
+    n, dev = 100003, "cuda"
+    p = torch.randn(n, device=dev)
+    gsum = torch.randn(n, device=dev) * world
+    m = torch.zeros(n, device=dev)
+    v = torch.zeros(n, device=dev)
+    parts = torch.empty(dcr_ops.opt_num_partials(n), device=dev)
+    na, nb = torch.empty(1, device=dev), torch.empty(1, device=dev)
+    pa, ma, va = p.clone(), m.clone(), v.clone()
+    dcr_ops.adam_clip(pa, gsum / world, ma, va, None, parts, na, 1e-3, 0.9, 0.999, 1e-8, 5.0)
+    dcr_ops.adam_clip(p, gsum, m, v, None, parts, nb, 1e-3, 0.9, 0.999, 1e-8, 5.0, 1.0 / world)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(nb, na, rtol=1e-5, atol=0)
+    torch.testing.assert_close(p, pa, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(m, ma, rtol=1e-5, atol=1e-7)

@@ -168,3 +168,18 @@ def test_adam_slot_checkpoint_roundtrip():
     for s in st.specs:
         torch.testing.assert_close(st2.view(s.name, opt2.m), st.view(s.name, opt.m))
         torch.testing.assert_close(st2.view(s.name, opt2.v), st.view(s.name, opt.v))
+
+
+def test_tf_adam_grad_scale_equals_averaged_gradient():
+    from distributed_char_rnn_amd.engine.optim import TFAdam
+    cfg = ModelConfig(model="lstm", vocab_size=11, rnn_size=8, num_layers=1)
+    a = CharRNN(cfg, device="cpu", seed=0)
+    b = CharRNN(cfg, device="cpu", seed=0)
+    g = torch.randn(a.store.numel) * 3.0
+    a.store.grad.copy_(g / 4)
+    b.store.grad.copy_(g)
+    oa, ob = TFAdam(a.store, clip=1.0), TFAdam(b.store, clip=1.0)
+    na = oa.step(1e-2)
+    nb = ob.step(1e-2, grad_scale=0.25)
+    torch.testing.assert_close(nb, na)
+    torch.testing.assert_close(b.store.flat, a.store.flat)
