@@ -285,6 +285,12 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
   // bias-gradient accumulators of each epilogue lane, kept in LDS (registers are the limit:
   // 3 x KS weight and 3 x KS payload fragments live across the MFMA phase)
   __shared__ float dbl[4][16][64];
+  // layer l's dtop partial (this wave's K quarter, both tiles) for its NEXT tick, computed off
+  // the critical path after this tick's epilogue from the dZ_{l+1} fragments this tick loaded
+  __shared__ __attribute__((aligned(16))) float xsl[4][2][64][4];
+  // W_x,l+1 fragments [wave][k-step][lane] (64 KB): only the off-critical-path stash product
+  // reads them, so they live in LDS and leave the registers to W_h,l / W_h,l+1 and the payload
+  __shared__ __attribute__((aligned(16))) bf16x8 wx1l[4][KS][64];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
@@ -300,13 +306,13 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
 
   constexpr int KSG = KS / 4;  // k-steps per gate segment
   auto kcol = [&](int s) { return (s / KSG) * H + w * (H / 4) + (s % KSG) * 32; };
-  bf16x8 wh0[KS], wh1[KS], wx1[KS];
+  bf16x8 wh0[KS], wh1[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     const size_t row = (size_t)(ub0 + (lane & 15)) * G4H + kcol(s) + kq;
     wh0[s] = ld8(a.Wh0 + row);
     wh1[s] = ld8(a.Wh1 + row);
-    wx1[s] = ld8(a.Wx1 + row);
+    wx1l[w][s][lane] = ld8(a.Wx1 + row);  // read back only by this wave
   }
 
   // epilogue role: layer L, batch tile J
@@ -323,16 +329,22 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
 #pragma unroll
   for (int i = 0; i < 16; ++i) dbl[w][i][lane] = 0.f;
 
-  for (int tau = 0; tau <= T; ++tau) {
-    const bool on1 = tau < T, on0 = tau >= 1;
-    const int t = L ? T - 1 - tau : T - tau;  // this role's step
+  for (int tau = 0; tau <= T + 1; ++tau) {
+    const bool on1 = tau < T;                 // layer l+1 computes step T-1-tau
+    const bool on0 = tau >= 2;                // layer l computes step T+1-tau (two ticks behind)
+    const bool ld1 = tau >= 1 && tau <= T;    // dZ_{l+1}[T-tau] (published at tick tau-1)
+    const bool ld0 = tau >= 3;                // dZ_l[T+2-tau]   (published at tick tau-1)
+    const int t = L ? T - 1 - tau : T + 1 - tau;  // this role's step
     const bool act = L ? on1 : on0;
     STAMP2(0)
     // recurrence-independent epilogue operands, issued before the wait
-    float gi[4], gj[4], gf[4], go[4], cc[4], cp[4], dtop[4];
+    // (gates stay packed bf16 until the epilogue: registers are the limit here)
+    bf16x4 g4[4];
+    float cc[4], cp[4], dtop[4];
     if (act) {
       const bf16* gp = gtL + ((size_t)t * B + b) * G4H + u0;
-      ld4bf(gp, gi); ld4bf(gp + H, gj); ld4bf(gp + 2 * H, gf); ld4bf(gp + 3 * H, go);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) g4[g] = *reinterpret_cast<const bf16x4*>(gp + g * H);
       ld4f(cbL + (size_t)(t + 1) * B * H + bh, cc);
       ld4f(cbL + (size_t)t * B * H + bh, cp);
       if (L) {
@@ -342,32 +354,95 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
         for (int r = 0; r < 4; ++r) dtop[r] = 0.f;
       }
     }
+    auto epilogue = [&]() {
+        float dh[4];
+        if (tau >= 1) {
+          const float4 s0 = *reinterpret_cast<const float4*>(&part[0][L][J][lane][0]);
+          const float4 s1 = *reinterpret_cast<const float4*>(&part[1][L][J][lane][0]);
+          const float4 s2 = *reinterpret_cast<const float4*>(&part[2][L][J][lane][0]);
+          const float4 s3 = *reinterpret_cast<const float4*>(&part[3][L][J][lane][0]);
+          dh[0] = s0.x + s1.x + s2.x + s3.x + dtop[0];
+          dh[1] = s0.y + s1.y + s2.y + s3.y + dtop[1];
+          dh[2] = s0.z + s1.z + s2.z + s3.z + dtop[2];
+          dh[3] = s0.w + s1.w + s2.w + s3.w + dtop[3];
+        } else {
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) dh[r] = dtop[r];
+        }
+        float gi[4], gj[4], gf[4], go[4];
+  #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          gi[r] = (float)g4[0][r]; gj[r] = (float)g4[1][r];
+          gf[r] = (float)g4[2][r]; go[r] = (float)g4[3][r];
+        }
+        float di[4], dj[4], df_[4], dO[4];
+  #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float th = tanhf_(cc[r]);
+          const float dcv = dc[r] + dh[r] * go[r] * (1.f - th * th);
+          dO[r] = dh[r] * th * go[r] * (1.f - go[r]);
+          di[r] = dcv * gj[r] * gi[r] * (1.f - gi[r]);
+          dj[r] = dcv * gi[r] * (1.f - gj[r] * gj[r]);
+          df_[r] = dcv * cp[r] * gf[r] * (1.f - gf[r]);
+          dc[r] = dcv * gf[r];
+        }
+        STAMP2(5)
+        // layer l+1's dZ_t feeds both layers at the next tick (t >= 0); layer l's only itself
+        if (L || t >= 1) {
+          bf16* const zr = zrL + (size_t)(t & 1) * B * G4H;
+          st4bf_sc1(zr + frag_index(b, u0, G4H), di[0], di[1], di[2], di[3]);
+          st4bf_sc1(zr + frag_index(b, H + u0, G4H), dj[0], dj[1], dj[2], dj[3]);
+          st4bf_sc1(zr + frag_index(b, 2 * H + u0, G4H), df_[0], df_[1], df_[2], df_[3]);
+          st4bf_sc1(zr + frag_index(b, 3 * H + u0, G4H), dO[0], dO[1], dO[2], dO[3]);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          STAMP2(6)
+          if (lane == 0)
+            __hip_atomic_fetch_add(cntL + (size_t)t * 4, 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // row-major copy for the weight GEMMs, after the arrival (off the critical path)
+        bf16* dz = dzL + ((size_t)t * B + b) * G4H + u0;
+        st4bf(dz, di[0], di[1], di[2], di[3]);
+        st4bf(dz + H, dj[0], dj[1], dj[2], dj[3]);
+        st4bf(dz + 2 * H, df_[0], df_[1], df_[2], df_[3]);
+        st4bf(dz + 3 * H, dO[0], dO[1], dO[2], dO[3]);
+        // bias gradient of the bf16-rounded dz, exactly as the weight GEMMs see it
+  #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          dbl[w][r][lane] += (float)f2bf(di[r]);
+          dbl[w][4 + r][lane] += (float)f2bf(dj[r]);
+          dbl[w][8 + r][lane] += (float)f2bf(df_[r]);
+          dbl[w][12 + r][lane] += (float)f2bf(dO[r]);
+        }
+    };
     if (tau >= 1) {
-      // slot s1 = T - tau of layer l+1 (both layers' operand), slot s1 + 1 of layer l
-      const int s1 = T - tau;
-      const bool has0 = tau >= 2;
-      if (threadIdx.x == kLstmPollerThread && !dead) {
-        dead = has0 ? !poll_counter2(cnt1 + (size_t)s1 * 4, target, cnt0 + (size_t)(s1 + 1) * 4,
-                                     target, a.spin_limit, a.err, 10u)
-                    : !poll_counter(cnt1 + (size_t)s1 * 4, target, a.spin_limit, a.err, 10u);
+      bf16x8 p1[2][KS];
+      const int s1 = T - tau, s0 = T + 2 - tau;  // ring slots of dZ_{l+1} and dZ_l
+      if (threadIdx.x == kLstmPollerThread && !dead && (ld1 || ld0)) {
+        dead = (ld1 && ld0)
+                   ? !poll_counter2(cnt1 + (size_t)s1 * 4, target, cnt0 + (size_t)s0 * 4, target,
+                                    a.spin_limit, a.err, 10u)
+                   : !poll_counter(ld1 ? cnt1 + (size_t)s1 * 4 : cnt0 + (size_t)s0 * 4, target,
+                                   a.spin_limit, a.err, 10u);
       }
       STAMP2(1)
       __syncthreads();
       STAMP2(2)
       const size_t slab = sizeof(bf16) * (size_t)B * G4H;
       const __amdgpu_buffer_rsrc_t r1 = make_rsrc(a.zring1 + (size_t)(s1 & 1) * B * G4H, slab);
-      const __amdgpu_buffer_rsrc_t r0 =
-          make_rsrc(a.zring0 + (size_t)((s1 + 1) & 1) * B * G4H, slab);
+      const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.zring0 + (size_t)(s0 & 1) * B * G4H, slab);
       // register budget (one wave per SIMD, <= ~450 VGPR+AGPR without spills): 3 x KS weight
       // fragments + 3 x KS payload fragments in flight (both tiles of dZ_{l+1}, tile 0 of
-      // dZ_l); tile 1 of dZ_l is issued once tile 0's dZ_{l+1} fragments are consumed
-      bf16x8 p1[2][KS], p0[KS];
+      // dZ_l); tile 1 of dZ_l is issued once tile 0's fragments are consumed
+      bf16x8 p0[KS];
+      if (ld1) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int s = 0; s < KS; ++s)
-          p1[j][s] = ld8_sc1(r1, frag_load_off(2 * bg + j, kcol(s) >> 5, G4H, lane));
-      if (has0) {
+          for (int s = 0; s < KS; ++s)
+            p1[j][s] = ld8_sc1(r1, frag_load_off(2 * bg + j, kcol(s) >> 5, G4H, lane));
+      }
+      if (ld0) {
 #pragma unroll
         for (int s = 0; s < KS; ++s)
           p0[s] = ld8_sc1(r0, frag_load_off(2 * bg, kcol(s) >> 5, G4H, lane));
@@ -375,89 +450,45 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        f32x4 acc1 = f32x4{0.f, 0.f, 0.f, 0.f}, acc0 = f32x4{0.f, 0.f, 0.f, 0.f};
-        // layer l+1: dh partial = dZ_{l+1}[t+1] · W_h,l+1ᵀ;  layer l: dtop = dZ_{l+1}[t] · W_x,l+1ᵀ
-        if (on1) {
+        if (on1) {  // layer l+1: dh partial = dZ_{l+1}[t+1] · W_h,l+1ᵀ
+          f32x4 acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int s = 0; s < KS; ++s) acc1 = mfma16(wh1[s], p1[j][s], acc1);
-        }
-#pragma unroll
-        for (int s = 0; s < KS; ++s) acc0 = mfma16(wx1[s], p1[j][s], acc0);
-        if (has0) {
-          // + dZ_l[t+1] · W_h,lᵀ
-#pragma unroll
-          for (int s = 0; s < KS; ++s) acc0 = mfma16(wh0[s], p0[s], acc0);
-          if (j == 0) {
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int s = 0; s < KS; ++s)
-              p0[s] = ld8_sc1(r0, frag_load_off(2 * bg + 1, kcol(s) >> 5, G4H, lane));
-          }
-        }
-        if (on1)
           *reinterpret_cast<float4*>(&part[w][1][j][lane][0]) =
               make_float4(acc1[0], acc1[1], acc1[2], acc1[3]);
-        *reinterpret_cast<float4*>(&part[w][0][j][lane][0]) =
-            make_float4(acc0[0], acc0[1], acc0[2], acc0[3]);
+        }
+        if (on0) {  // layer l: dtop (stashed last tick) + dZ_l[t+1] · W_h,lᵀ
+          const float4 x0 = *reinterpret_cast<const float4*>(&xsl[w][j][lane][0]);
+          f32x4 acc0 = f32x4{x0.x, x0.y, x0.z, x0.w};
+          if (ld0) {
+#pragma unroll
+            for (int s = 0; s < KS; ++s) acc0 = mfma16(wh0[s], p0[s], acc0);
+            if (j == 0) {
+              __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+              for (int s = 0; s < KS; ++s)
+                p0[s] = ld8_sc1(r0, frag_load_off(2 * bg + 1, kcol(s) >> 5, G4H, lane));
+            }
+          }
+          *reinterpret_cast<float4*>(&part[w][0][j][lane][0]) =
+              make_float4(acc0[0], acc0[1], acc0[2], acc0[3]);
+        }
       }
       STAMP2(3)
       __syncthreads();
       STAMP2(4)
-    }
-    if (act) {
-      float dh[4];
-      if (tau >= 1) {
-        const float4 s0 = *reinterpret_cast<const float4*>(&part[0][L][J][lane][0]);
-        const float4 s1 = *reinterpret_cast<const float4*>(&part[1][L][J][lane][0]);
-        const float4 s2 = *reinterpret_cast<const float4*>(&part[2][L][J][lane][0]);
-        const float4 s3 = *reinterpret_cast<const float4*>(&part[3][L][J][lane][0]);
-        dh[0] = s0.x + s1.x + s2.x + s3.x + dtop[0];
-        dh[1] = s0.y + s1.y + s2.y + s3.y + dtop[1];
-        dh[2] = s0.z + s1.z + s2.z + s3.z + dtop[2];
-        dh[3] = s0.w + s1.w + s2.w + s3.w + dtop[3];
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dh[r] = dtop[r];
+      if (act) epilogue();
+      if (ld1) {  // layer l's dtop for its next tick, off the critical path (see xsl)
+  #pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+          for (int s = 0; s < KS; ++s) x = mfma16(wx1l[w][s][lane], p1[j][s], x);
+          *reinterpret_cast<float4*>(&xsl[w][j][lane][0]) = make_float4(x[0], x[1], x[2], x[3]);
+        }
       }
-      float di[4], dj[4], df_[4], dO[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float th = tanhf_(cc[r]);
-        const float dcv = dc[r] + dh[r] * go[r] * (1.f - th * th);
-        dO[r] = dh[r] * th * go[r] * (1.f - go[r]);
-        di[r] = dcv * gj[r] * gi[r] * (1.f - gi[r]);
-        dj[r] = dcv * gi[r] * (1.f - gj[r] * gj[r]);
-        df_[r] = dcv * cp[r] * gf[r] * (1.f - gf[r]);
-        dc[r] = dcv * gf[r];
-      }
-      STAMP2(5)
-      // layer l+1's dZ_t feeds both layers at the next tick (t >= 0); layer l's only itself
-      if (L || t >= 1) {
-        bf16* const zr = zrL + (size_t)(t & 1) * B * G4H;
-        st4bf_sc1(zr + frag_index(b, u0, G4H), di[0], di[1], di[2], di[3]);
-        st4bf_sc1(zr + frag_index(b, H + u0, G4H), dj[0], dj[1], dj[2], dj[3]);
-        st4bf_sc1(zr + frag_index(b, 2 * H + u0, G4H), df_[0], df_[1], df_[2], df_[3]);
-        st4bf_sc1(zr + frag_index(b, 3 * H + u0, G4H), dO[0], dO[1], dO[2], dO[3]);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        STAMP2(6)
-        if (lane == 0)
-          __hip_atomic_fetch_add(cntL + (size_t)t * 4, 1u, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-      }
-      // row-major copy for the weight GEMMs, after the arrival (off the critical path)
-      bf16* dz = dzL + ((size_t)t * B + b) * G4H + u0;
-      st4bf(dz, di[0], di[1], di[2], di[3]);
-      st4bf(dz + H, dj[0], dj[1], dj[2], dj[3]);
-      st4bf(dz + 2 * H, df_[0], df_[1], df_[2], df_[3]);
-      st4bf(dz + 3 * H, dO[0], dO[1], dO[2], dO[3]);
-      // bias gradient of the bf16-rounded dz, exactly as the weight GEMMs see it
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        dbl[w][r][lane] += (float)f2bf(di[r]);
-        dbl[w][4 + r][lane] += (float)f2bf(dj[r]);
-        dbl[w][8 + r][lane] += (float)f2bf(df_[r]);
-        dbl[w][12 + r][lane] += (float)f2bf(dO[r]);
-      }
+    } else if (act) {
+      epilogue();
     }
   }
   // bias-gradient partial of this role's 16-row tile: reduce the 16 batch lanes
