@@ -146,7 +146,7 @@ struct Lstm2Args {
   unsigned* cnt0;       // [B/32, T+1, 4] arrivals of layer l   (zeroed by the caller)
   unsigned* cnt1;       // [B/32, T+1, 4] arrivals of layer l+1
   unsigned* err;
-  unsigned long long* diag;  // optional [T+1, 8] s_memtime stamps of workgroup 0 (diagnostics)
+  unsigned long long* diag;  // optional [T+2, 8] s_memtime stamps of workgroup 0 (diagnostics)
   float* clast0;        // optional [B, H] final c of layers l and l+1
   float* clast1;
   bf16* hring0;         // optional [2, B, H] fragment-tiled h hand-off rings (persist_common.h);
@@ -173,7 +173,7 @@ struct Lstm2BwdArgs {
   unsigned* cnt0;       // [B/32, T+1, 4] arrivals of layer l   (zeroed by the caller)
   unsigned* cnt1;       // [B/32, T+1, 4] arrivals of layer l+1
   unsigned* err;
-  unsigned long long* diag;  // optional [T+1, 8] s_memtime stamps of workgroup 0
+  unsigned long long* diag;  // optional [T+2, 8] s_memtime stamps of workgroup 0
   int B, H, T;
   unsigned spin_limit;
 };

@@ -4,9 +4,11 @@
 // single-layer persistent kernels (lstm_persist.hip) therefore run 2T hand-off-latency-bound
 // steps for two layers, although layer l+1's step t-1 and layer l's step t are independent.
 // One launch here runs both layers as a wavefront: at tick tau layer l computes step tau and
-// layer l+1 computes step tau-1.  Both consume the same published slot h_l[tau] (layer l's
-// recurrent input and layer l+1's input x), so a tick loads one extra payload (h_{l+1}) and
-// T+1 ticks replace 2T steps.  Per-step latency, not bandwidth, bounds these kernels
+// layer l+1 computes step tau-2.  Layer l's recurrent operand h_l[tau-1] (slot tau) is also
+// layer l+1's input at step tau-1: its input-projection MFMAs h_l·W_x,l+1 run right after this
+// tick's epilogue (while the workgroup waits for the next hand-off) and are added at the next
+// tick, so the critical path of a tick carries only the two recurrent products.  T+2 ticks
+// replace 2T steps.  Per-step latency, not bandwidth, bounds these kernels
 // (profiles/r1_persist_stamps_vs_batch.txt), which is what makes the wider tick pay.
 //
 // Workgroup (ubk, bg) owns 16 hidden units x 32 batch rows (two 16-row MFMA tiles) of BOTH
@@ -79,8 +81,21 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
 #pragma unroll
   for (int g = 0; g < 4; ++g) ld4f(a.bias1 + g * H + u0, bias1[g]);
 
-  for (int tau = 0; tau <= T; ++tau) {
-    const bool on0 = tau < T, on1 = tau >= 1;
+  // layer l+1's input-projection partials (this wave's K quarter, [tile][gate]) for its NEXT
+  // tick: layer l+1 runs two ticks behind layer l, so x_t·W_x = h_l[t]·W_x is computed right
+  // after the epilogue of the tick that loaded h_l[t] for layer l's own recurrence -- off the
+  // critical path (the MFMAs run while the workgroup waits for the next hand-off)
+  f32x4 xs[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) xs[j][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int tau = 0; tau <= T + 1; ++tau) {
+    const bool on0 = tau < T;                  // layer l   computes step tau
+    const bool on1 = tau >= 2;                 // layer l+1 computes step tau-2
+    const bool ld0 = tau <= T;                 // slot tau of h_l (layer l's h_{tau-1})
+    const bool ld1 = on1;                      // slot tau-2 of h_{l+1}
     STAMP2(0)
     // layer-l input projections of step tau (recurrence independent: issued before the wait)
     float zx[4][4];
@@ -90,37 +105,43 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
 #pragma unroll
       for (int g = 0; g < 4; ++g) ld4f(zrow + (size_t)g * H + u0, zx[g]);
     }
-    if (tau >= 1) {
+    // hand-offs: layer l's slot tau (from tick tau-1; slot 0 is the prep-written initial state)
+    // and layer l+1's slot tau-2 (from tick tau-1; slot 0 likewise)
+    const bool pw0 = ld0 && tau >= 1, pw1 = ld1 && tau >= 3;
+    if (pw0 || pw1) {
       if (threadIdx.x == kLstmPollerThread && !dead) {
-        // layer l+1's slot tau-1 exists from tick 2 on; before that poll layer l's twice
-        dead = tau >= 2 ? !poll_counter2(cnt0 + (size_t)tau * 4, target,
-                                         cnt1 + (size_t)(tau - 1) * 4, target, a.spin_limit,
-                                         a.err, 9u)
-                        : !poll_counter(cnt0 + (size_t)tau * 4, target, a.spin_limit, a.err, 9u);
+        dead = (pw0 && pw1) ? !poll_counter2(cnt0 + (size_t)tau * 4, target,
+                                           cnt1 + (size_t)(tau - 2) * 4, target, a.spin_limit,
+                                           a.err, 9u)
+                          : !poll_counter(pw0 ? cnt0 + (size_t)tau * 4 : cnt1 + (size_t)(tau - 2) * 4,
+                                          target, a.spin_limit, a.err, 9u);
       }
       STAMP2(1)
       __syncthreads();
     }
     STAMP2(2)
-    // payloads: h_l[tau] (both layers' input) and h_{l+1}[tau-1]
     bf16x8 hf0[2][KS], hf1[2][KS];
     {
       // slot 0 (initial state, written by the prep launch) is row-major; later slots come from
       // the fragment-tiled rings: one contiguous 1 KB load per (tile, k-step)
-      const bool ring0 = a.hring0 && tau > 0, ring1 = a.hring1 && tau > 1;
-      const __amdgpu_buffer_rsrc_t r0 =
-          ring0 ? make_rsrc(a.hring0 + (size_t)(tau & 1) * B * H, sizeof(bf16) * (size_t)B * H)
-                : make_rsrc(a.hbuf0 + (size_t)tau * B * H, sizeof(bf16) * (size_t)B * H);
+      if (ld0) {
+        const bool ring0 = a.hring0 && tau > 0;
+        const __amdgpu_buffer_rsrc_t r0 =
+            ring0 ? make_rsrc(a.hring0 + (size_t)(tau & 1) * B * H, sizeof(bf16) * (size_t)B * H)
+                  : make_rsrc(a.hbuf0 + (size_t)tau * B * H, sizeof(bf16) * (size_t)B * H);
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int s = 0; s < KS; ++s)
-          hf0[j][s] = ld8_sc1(r0, ring0 ? frag_load_off(2 * bg + j, w * KS + s, H, lane)
-                                        : hoff[j] + s * 64);
-      if (on1) {
+          for (int s = 0; s < KS; ++s)
+            hf0[j][s] = ld8_sc1(r0, ring0 ? frag_load_off(2 * bg + j, w * KS + s, H, lane)
+                                          : hoff[j] + s * 64);
+      }
+      if (ld1) {
+        const int s1 = tau - 2;
+        const bool ring1 = a.hring1 && s1 > 0;
         const __amdgpu_buffer_rsrc_t r1 =
-            ring1 ? make_rsrc(a.hring1 + (size_t)((tau - 1) & 1) * B * H, sizeof(bf16) * (size_t)B * H)
-                  : make_rsrc(a.hbuf1 + (size_t)(tau - 1) * B * H, sizeof(bf16) * (size_t)B * H);
+            ring1 ? make_rsrc(a.hring1 + (size_t)(s1 & 1) * B * H, sizeof(bf16) * (size_t)B * H)
+                  : make_rsrc(a.hbuf1 + (size_t)s1 * B * H, sizeof(bf16) * (size_t)B * H);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -145,17 +166,14 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
         for (int g = 0; g < 4; ++g)
           *reinterpret_cast<float4*>(dst + g * 256) = make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
       }
-      if (on1) {
+      if (on1) {  // stashed x-part + recurrent part
         f32x4 acc[4];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int g = 0; g < 4; ++g) acc[g] = xs[j][g];
 #pragma unroll
         for (int s = 0; s < KS; ++s)
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            acc[g] = mfma16(x1[g][s], hf0[j][s], acc[g]);
-            acc[g] = mfma16(w1[g][s], hf1[j][s], acc[g]);
-          }
+          for (int g = 0; g < 4; ++g) acc[g] = mfma16(w1[g][s], hf1[j][s], acc[g]);
         float* dst = &part[w][1][j][0][lane][0];
 #pragma unroll
         for (int g = 0; g < 4; ++g)
@@ -165,8 +183,26 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     STAMP2(3)
     __syncthreads();
     STAMP2(4)
+    // layer l+1's x-part of its step tau-1 (next tick) from h_l[tau-1] = slot tau.  Issued
+    // right after this wave's hand-off arrival (nothing in flight then but the counter add):
+    // placed after the row-major stores, the compiler's conservative vmcnt waits made these
+    // MFMAs wait for the write-through of those stores
+    const bool stash = ld0 && tau >= 1;
+    bool stashed = false;
+    auto do_stash = [&]() {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) xs[j][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) xs[j][g] = mfma16(x1[g][s], hf0[j][s], xs[j][g]);
+      }
+      stashed = true;
+    };
     if (L == 0 ? on0 : on1) {
-      const int t = L == 0 ? tau : tau - 1;  // this layer's step
+      const int t = L == 0 ? tau : tau - 2;  // this layer's step
       float z[4][4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -205,6 +241,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
           __hip_atomic_fetch_add(cntL + (size_t)(t + 1) * 4, 1u,
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      if (stash) do_stash();
       if (ringL) st4bf(hbL + o, h[0], h[1], h[2], h[3]);  // row-major copy for the GEMMs
       *reinterpret_cast<float4*>(cbL + o) = make_float4(c[0], c[1], c[2], c[3]);
       if (gtL) {
@@ -219,6 +256,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
       if (t == T - 1 && clL)
         *reinterpret_cast<float4*>(clL + bh) = make_float4(c[0], c[1], c[2], c[3]);
     }
+    if (stash && !stashed) do_stash();  // waves without an epilogue this tick
   }
 }
 
@@ -265,9 +303,10 @@ int launch_lstm2_fwd_persist(const Lstm2Args& a, int cus, hipStream_t s) {
 // (dZ_{l+1}·W_x,l+1ᵀ), then layer l's T steps: 2T hand-off-latency-bound steps.  Layer l's
 // step t needs only layer l+1's dZ_t (its dtop) and its own dZ_{t+1}, so here one launch runs
 // both as a reverse wavefront: at tick tau layer l+1 computes step T-1-tau and layer l step
-// T-tau.  Both consume the slot dZ_{l+1}[T-tau] (layer l+1's recurrent operand and, through the
-// register-resident W_x,l+1 rows, layer l's dtop), so the dX GEMM disappears and T+1 ticks
-// replace 2T steps.
+// T+1-tau (two ticks behind).  The slot dZ_{l+1}[T-tau] loaded for layer l+1's recurrence is
+// also layer l's dtop operand one tick later: its W_x,l+1 product (fragments in LDS) runs after
+// this tick's epilogue, off the critical path, so the dX GEMM disappears and T+2 ticks replace
+// 2T steps.
 //
 // Workgroup (ubk, bg) owns 16 hidden units x 32 batch rows (two 16-row MFMA tiles) of BOTH
 // layers.  K = 4H is split by hidden-unit quarter exactly as in lstm_bwd_persist_kernel: wave w
@@ -354,7 +393,8 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
         for (int r = 0; r < 4; ++r) dtop[r] = 0.f;
       }
     }
-    auto epilogue = [&]() {
+    // after_arrive runs right after the wave's hand-off arrival, before its other stores
+    auto epilogue = [&](auto&& after_arrive) {
         float dh[4];
         if (tau >= 1) {
           const float4 s0 = *reinterpret_cast<const float4*>(&part[0][L][J][lane][0]);
@@ -400,6 +440,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
             __hip_atomic_fetch_add(cntL + (size_t)t * 4, 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
         }
+        after_arrive();
         // row-major copy for the weight GEMMs, after the arrival (off the critical path)
         bf16* dz = dzL + ((size_t)t * B + b) * G4H + u0;
         st4bf(dz, di[0], di[1], di[2], di[3]);
@@ -477,18 +518,26 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
       STAMP2(3)
       __syncthreads();
       STAMP2(4)
-      if (act) epilogue();
-      if (ld1) {  // layer l's dtop for its next tick, off the critical path (see xsl)
-  #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
-  #pragma unroll
-          for (int s = 0; s < KS; ++s) x = mfma16(wx1l[w][s][lane], p1[j][s], x);
-          *reinterpret_cast<float4*>(&xsl[w][j][lane][0]) = make_float4(x[0], x[1], x[2], x[3]);
+      // layer l's dtop for its next tick, off the critical path (see xsl), issued right after
+      // this wave's arrival: behind its row-major stores the compiler's conservative vmcnt waits
+      // would make the MFMAs wait for their write-through
+      bool stashed = false;
+      auto do_stash = [&]() {
+        if (ld1) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < KS; ++s) x = mfma16(wx1l[w][s][lane], p1[j][s], x);
+            *reinterpret_cast<float4*>(&xsl[w][j][lane][0]) = make_float4(x[0], x[1], x[2], x[3]);
+          }
         }
-      }
+        stashed = true;
+      };
+      if (act) epilogue(do_stash);
+      if (!stashed) do_stash();
     } else if (act) {
-      epilogue();
+      epilogue([] {});
     }
   }
   // bias-gradient partial of this role's 16-row tile: reduce the 16 batch lanes

@@ -560,8 +560,8 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
   a.forget_bias = (float)forget_bias;
   a.spin_limit = (unsigned)spin_limit;
   if (has(diag)) {
-    TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)(T + 1) * 8,
-                "diag must hold [T+1, 8] int64");
+    TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)(T + 2) * 8,
+                "diag must hold [T+2, 8] int64 (ticks 0..T+1)");
     a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());
   }
   for (auto* r : {&hring0, &hring1})
@@ -626,8 +626,8 @@ void lstm2_persist_bwd(const at::Tensor& Wh0, const at::Tensor& Wh1, const at::T
   a.B = B; a.H = H; a.T = T;
   a.spin_limit = (unsigned)spin_limit;
   if (has(diag)) {
-    TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)(T + 1) * 8,
-                "diag must hold [T+1, 8] int64");
+    TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)(T + 2) * 8,
+                "diag must hold [T+2, 8] int64 (ticks 0..T+1)");
     a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());
   }
   const int rc = dcr::launch_lstm2_bwd_persist(a, num_cus(), cur_stream());

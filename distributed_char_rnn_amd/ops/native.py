@@ -12,7 +12,9 @@ import threading
 
 import torch
 
-_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_C.so")
+# DCR_NATIVE_LIB selects another build of the library (same-box A/B runs: scripts/ab_bench.sh)
+_LIB = os.environ.get("DCR_NATIVE_LIB") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_C.so")
 _lock = threading.Lock()
 _loaded = False
 _err: str | None = None

@@ -83,7 +83,7 @@ if ops.lstm2_persist_supported(H, B):
     hl1 = torch.empty_like(hl)
     c0 = torch.zeros(B // 32 * (T + 1) * 4, dtype=torch.int32, device=dev)
     c1 = torch.zeros_like(c0)
-    diag2 = torch.zeros(T + 1, 8, dtype=torch.int64, device=dev)
+    diag2 = torch.zeros(T + 2, 8, dtype=torch.int64, device=dev)
 
     def run2():
         c0.zero_()
@@ -103,7 +103,7 @@ if ops.lstm2_persist_supported(H, B):
     names2 = ["top->poll done", "poll->barrierA", "barrierA->mfma done", "mfma->barrierB",
               "barrierB->epilogue math", "epi->drain done", "drain->next top"]
     dd = np.diff(np.concatenate([d[2:-2, [0, 1, 2, 3, 4, 5, 6]], d[3:-1, [0]]], 1), axis=1)
-    print(f"PAIR kernel {ms*1e3/(T+1):.2f} us/tick (event); stamps {tot:.0f} ticks/tick; "
+    print(f"PAIR kernel {ms*1e3/(T+2):.2f} us/tick (event); stamps {tot:.0f} ticks/tick; "
           f"err={int(err.item())}")
     for n, v in zip(names2, dd.mean(0)):
         print(f"  {n:<26}{v:8.0f} ticks  {100*v/tot:5.1f}%")
@@ -125,7 +125,7 @@ if ops.lstm2_bwd_persist_supported(H, B):
     db1 = torch.empty_like(db0)
     c0 = torch.zeros(B // 32 * (T + 1) * 4, dtype=torch.int32, device=dev)
     c1 = torch.zeros_like(c0)
-    diag3 = torch.zeros(T + 1, 8, dtype=torch.int64, device=dev)
+    diag3 = torch.zeros(T + 2, 8, dtype=torch.int64, device=dev)
 
     def run3(dg):
         c0.zero_()
@@ -140,7 +140,7 @@ if ops.lstm2_bwd_persist_supported(H, B):
         run3(dg)
         ev1.record()
         torch.cuda.synchronize()
-        print(f"PAIR BWD ({'diag' if dg is not None else 'plain'}) {ev0.elapsed_time(ev1)*1e3/(T+1):.2f} us/tick")
+        print(f"PAIR BWD ({'diag' if dg is not None else 'plain'}) {ev0.elapsed_time(ev1)*1e3/(T+2):.2f} us/tick")
     d = diag3.cpu().numpy().astype("float64")
     tot = (d[-2, 0] - d[2, 0]) / (T - 4)
     dd = np.diff(np.concatenate([d[2:-2, [0, 1, 2, 3, 4, 5, 6]], d[3:-1, [0]]], 1), axis=1)
