@@ -60,3 +60,25 @@ dt = torch.empty(N, H, device=dev)
 rows.append(("dtop = dlog Ws^T [32768x512, K=65]", timeit(lambda: torch.mm(D, Ws.t(), out_dtype=f32, out=dt)), 2 * N * H * V))
 for name, us, fl in rows:
     print(f"{name:<48} {us:9.1f} us  {fl / us / 1e6:8.1f} TFLOP/s")
+
+# NT form of the weight gradient: activations stored transposed ([H, N], K contiguous)
+XT = X.t().contiguous()
+ZT = Z.t().contiguous()
+ref = torch.mm(X.t(), Z, out_dtype=f32)
+
+
+def splitk_nt(AT, BT, S):
+    M, K = AT.shape
+    Nn = BT.shape[0]
+    a = AT.view(M, S, K // S).transpose(0, 1)          # [S, M, K/S], lda = K
+    b = BT.view(Nn, S, K // S).transpose(0, 1)         # [S, Nn, K/S]
+    return torch.bmm(a, b.transpose(1, 2), out_dtype=f32).sum(0)
+
+
+extra = [("dW NT  = XT ZT^T mm", timeit(lambda: torch.mm(XT, ZT.t(), out_dtype=f32, out=out)), 2 * N * H * G)]
+for S in (4, 8, 16):
+    r = splitk_nt(XT, ZT, S)
+    err = ((r - ref).norm() / ref.norm()).item()
+    extra.append((f"dW NT split-K S={S} err={err:.1e}", timeit(lambda: splitk_nt(XT, ZT, S)), 2 * N * H * G))
+for name, us, fl in extra:
+    print(f"{name:<52} {us:8.1f} us  {fl / us / 1e6:8.1f} TFLOP/s")
