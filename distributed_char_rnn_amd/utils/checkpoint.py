@@ -10,11 +10,14 @@ Reference artefacts (train.py:109-115, 145, 209-217; TF Saver V
 
 We keep every filename and the TF variable names/layouts (``rnnlm/multi_rnn_cell/cell_l/
 lstm_cell/kernel`` [D+H, 4H] in i,j,f,o order, ``<var>/Adam``, ``<var>/Adam_1``,
-``beta1_power``, ``beta2_power``, ``global_step``, ``Variable`` = the lr variable).  The bundle
-itself is our own container (decision recorded in SURVEY.md §5.4): the ``.index`` file is JSON
-(name -> dtype/shape/offset/crc32) and the ``.data`` shard is the raw little-endian tensor
-bytes, 64-byte aligned.  Nothing is pickled inside a bundle, so loading executes nothing.
-Extra entries (``dcr/epoch``, ``dcr/batch_pointer``, optional TBPTT state) make resume exact.
+``beta1_power``, ``beta2_power``, ``global_step``, ``Variable`` = the lr variable), and the
+bundle itself is TF's V2 tensor-bundle format (``utils/tf_bundle.py``: SSTable ``.index`` of
+BundleEntryProtos + raw ``.data`` shard), so checkpoints move both ways between this framework
+and a TF 1.x run of the reference (decision recorded in SURVEY.md §5.4).  ``DCR_CKPT_FORMAT=json``
+writes the older self-describing JSON container instead (``.index`` = JSON name ->
+dtype/shape/offset/crc32); reading detects either.  Nothing in a bundle is pickled, so loading
+executes nothing.  Extra entries (``dcr/epoch``, ``dcr/batch_pointer``, optional TBPTT state)
+make resume exact; TF ignores keys it has no variable for.
 """
 from __future__ import annotations
 
@@ -26,6 +29,8 @@ from typing import Dict, List, Optional
 
 import numpy as np
 import torch
+
+from . import tf_bundle
 
 FORMAT = "dcr-bundle-v1"
 _DT = {"float32": np.float32, "float64": np.float64, "int64": np.int64, "int32": np.int32,
@@ -41,7 +46,11 @@ def _to_numpy(t) -> np.ndarray:
     return np.asarray(t)
 
 
-def write_bundle(prefix: str, tensors: Dict[str, object]) -> None:
+def write_bundle(prefix: str, tensors: Dict[str, object], fmt: Optional[str] = None) -> None:
+    fmt = fmt or os.environ.get("DCR_CKPT_FORMAT", "tf")
+    if fmt == "tf":
+        tf_bundle.write_bundle(prefix, {k: _to_numpy(v) for k, v in tensors.items()})
+        return
     index = {"format": FORMAT, "tensors": {}}
     data_path = prefix + ".data-00000-of-00001"
     tmp = data_path + ".tmp"
@@ -69,6 +78,8 @@ def write_bundle(prefix: str, tensors: Dict[str, object]) -> None:
 
 
 def read_bundle(prefix: str, verify: bool = True) -> Dict[str, np.ndarray]:
+    if tf_bundle.is_tf_bundle(prefix):
+        return tf_bundle.read_bundle(prefix, verify)
     with open(prefix + ".index") as f:
         index = json.load(f)
     if index.get("format") != FORMAT:
