@@ -19,10 +19,12 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp16"])
+    ap.add_argument("--model", default="lstm", choices=["lstm", "gru"])
     a = ap.parse_args()
     dev = "cuda"
     emb = nn.Embedding(a.vocab, a.hidden).to(dev)
-    lstm = nn.LSTM(a.hidden, a.hidden, a.layers, batch_first=True).to(dev)
+    rnn_cls = nn.LSTM if a.model == "lstm" else nn.GRU
+    lstm = rnn_cls(a.hidden, a.hidden, a.layers, batch_first=True).to(dev)
     head = nn.Linear(a.hidden, a.vocab).to(dev)
     params = list(emb.parameters()) + list(lstm.parameters()) + list(head.parameters())
     opt = torch.optim.Adam(params, lr=2e-3)
@@ -34,7 +36,11 @@ def main():
 
     def step(h, c):
         with torch.autocast("cuda", dtype=dt, enabled=a.dtype != "fp32"):
-            out, (h2, c2) = lstm(emb(x), (h, c))
+            if a.model == "lstm":
+                out, (h2, c2) = lstm(emb(x), (h, c))
+            else:
+                out, h2 = lstm(emb(x), h)
+                c2 = c
             logits = head(out)
             loss = nn.functional.cross_entropy(logits.float().reshape(-1, a.vocab), y.reshape(-1))
         opt.zero_grad(set_to_none=True)
@@ -51,7 +57,7 @@ def main():
         h, c, loss = step(h, c)
     torch.cuda.synchronize()
     t = (time.perf_counter() - t0) / a.steps
-    print(json.dumps({"impl": "torch.nn.LSTM(MIOpen)", "dtype": a.dtype, "batch": a.batch,
+    print(json.dumps({"impl": f"torch.nn.{rnn_cls.__name__}(MIOpen)", "dtype": a.dtype, "batch": a.batch,
                       "seq": a.seq, "hidden": a.hidden, "layers": a.layers,
                       "ms_per_step": t * 1e3, "chars_per_sec": a.batch * a.seq / t,
                       "loss": float(loss)}))
