@@ -134,6 +134,9 @@ def main(argv=None) -> int:
     dt = time.perf_counter() - t0
     dt = ctx.all_reduce_scalar(dt, dist.ReduceOp.MAX) if world > 1 else dt
     final_loss = float(loss)
+    check = getattr(model.backend, "check_errors", None)
+    if check is not None:  # a persistent kernel that timed out would have produced garbage
+        check()
     ms = dt / a.steps * 1e3
     cps = world * B * T * a.steps / dt
     if rank == 0:

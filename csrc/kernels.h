@@ -121,6 +121,10 @@ int lstm_persist_xfuse_supported(int H, int B, int cus);
 int lstm_persist_occupancy(int bwd, int H, int B, int V, int flags, int cus);
 // return 0 on success, <0 if the grid cannot be co-resident or the shape is unsupported
 int launch_lstm_fwd_persist(const PersistArgs& a, int cus, hipStream_t s);
+// large-H (1024 < H <= 2048) persistent forward, 8-unit weight shards (lstm_big.hip); needs the
+// fragment-order ring a.hring
+int lstm_big_supported(int H, int B, int cus);
+int launch_lstm_big_fwd(const PersistArgs& a, int cus, hipStream_t s);
 int launch_lstm_bwd_persist(const PersistArgs& a, int cus, hipStream_t s);
 
 // wide-vocabulary softmax CE (xent.hip): bias added in-kernel, fused d softmax_b, V % 4 == 0,

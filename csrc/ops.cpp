@@ -503,6 +503,67 @@ void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& d
 }
 
 // ------------------------------------------------------------------------------------------
+// large-H persistent LSTM forward (lstm_big.hip)
+void lstm_big_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::optional<at::Tensor>& ids,
+                  at::Tensor& hbuf, at::Tensor& cbuf, const c10::optional<at::Tensor>& gates,
+                  at::Tensor& hlast32, at::Tensor& cnt, at::Tensor& err, double forget_bias,
+                  int64_t spin_limit, at::Tensor& hring, bool cnt_zeroed,
+                  const c10::optional<at::Tensor>& clast32,
+                  const c10::optional<at::Tensor>& diag) {
+  check_seq(WT, at::kBFloat16, "WT");
+  check_seq(zx, at::kFloat, "zx");
+  check_seq(hbuf, at::kBFloat16, "hbuf");
+  check_seq(cbuf, at::kFloat, "cbuf");
+  check_seq(hlast32, at::kFloat, "hlast32");
+  check_seq(hring, at::kBFloat16, "hring");
+  check_opt(gates, at::kBFloat16, "gates");
+  check_opt(ids, at::kInt, "ids");
+  TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == at::kInt && err.scalar_type() == at::kInt,
+              "cnt/err must be int32 GPU tensors");
+  const int T = (int)hbuf.size(0) - 1, B = (int)hbuf.size(1), H = (int)hbuf.size(2);
+  TORCH_CHECK(dcr::lstm_big_supported(H, B, num_cus()), "large-H persistent LSTM unsupported for H=",
+              H, " B=", B);
+  TORCH_CHECK(WT.size(0) == 4 * H && WT.size(1) == H, "WT must be [4H, H]");
+  TORCH_CHECK(zx.size(-1) == 4 * H, "zx rows must be 4H wide");
+  if (has(ids)) {
+    TORCH_CHECK(ids->numel() == (int64_t)T * B, "ids must be [T, B]");
+  } else {
+    TORCH_CHECK(zx.numel() == (int64_t)T * B * 4 * H, "zx must be [T, B, 4H]");
+  }
+  TORCH_CHECK(cbuf.numel() == (int64_t)(T + 1) * B * H, "cbuf must be [T+1, B, H]");
+  TORCH_CHECK(hlast32.numel() == (int64_t)B * H, "hlast32 must be [B, H]");
+  if (has(gates)) TORCH_CHECK(gates->numel() == (int64_t)T * B * 4 * H, "gates must be [T, B, 4H]");
+  TORCH_CHECK(hring.numel() >= (int64_t)2 * B * H, "hring must hold [2, B, H]");
+  TORCH_CHECK(cnt.numel() >= (int64_t)(B / 16) * (T + 1) * 4, "counter buffer too small");
+  dcr::PersistArgs a{};
+  a.W = ptr<bf16>(WT);
+  a.zx = ptr<float>(zx);
+  a.ids = optr<int>(ids);
+  a.zx_ld = 4 * H;
+  a.hbuf = ptr<bf16>(hbuf);
+  a.cbuf = ptr<float>(cbuf);
+  a.gates = optr<bf16>(gates);
+  a.hlast32 = ptr<float>(hlast32);
+  a.cnt = reinterpret_cast<unsigned*>(cnt.data_ptr());
+  a.err = reinterpret_cast<unsigned*>(err.data_ptr());
+  a.B = B; a.H = H; a.T = T;
+  a.forget_bias = (float)forget_bias;
+  a.spin_limit = (unsigned)spin_limit;
+  a.cnt_zeroed = cnt_zeroed ? 1 : 0;
+  a.hring = ptr<bf16>(hring);
+  if (has(clast32)) {
+    check_seq(*clast32, at::kFloat, "clast32");
+    TORCH_CHECK(clast32->numel() == (int64_t)B * H, "clast32 must be [B, H]");
+    a.clast32 = ptr<float>(*clast32);
+  }
+  if (has(diag)) {
+    TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)T * 8, "diag must hold [T, 8] int64");
+    a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());
+  }
+  const int rc = dcr::launch_lstm_big_fwd(a, num_cus(), cur_stream());
+  TORCH_CHECK(rc == 0, "large-H persistent LSTM forward not launched (", rc, ")");
+}
+
 // two-layer wavefront LSTM forward (lstm2_persist.hip)
 // ------------------------------------------------------------------------------------------
 void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::Tensor& X1T,
@@ -961,6 +1022,14 @@ TORCH_LIBRARY(dcr, m) {
       "sample_step(Tensor O, Tensor WsT, Tensor bs, Tensor(a!) cur, Tensor(b!) out, "
       "Tensor(c!) pos, Tensor(d!) ctr, Tensor? u, Tensor(e!)? logits, int mode, int space_id, "
       "int seed) -> ()");
+  m.def("lstm_big_supported(int H, int B) -> int", [](int64_t H, int64_t B) -> int64_t {
+    return dcr::lstm_big_supported((int)H, (int)B, num_cus());
+  });
+  m.def(
+      "lstm_big_fwd(Tensor WT, Tensor zx, Tensor? ids, Tensor(a!) hbuf, Tensor(b!) cbuf, "
+      "Tensor(c!)? gates, Tensor(d!) hlast32, Tensor(e!) cnt, Tensor(f!) err, float forget_bias, "
+      "int spin_limit, Tensor(g!) hring, bool cnt_zeroed=False, Tensor(h!)? clast32=None, "
+      "Tensor(i!)? diag=None) -> ()");
   m.def("gru_persist_ub(int H, int B) -> int", [](int64_t H, int64_t B) -> int64_t {
     return dcr::gru_persist_ub((int)H, (int)B, num_cus());
   });
@@ -994,6 +1063,7 @@ TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("gru_persist_fwd", &gru_persist_fwd);
   m.impl("lstm2_persist_fwd", &lstm2_persist_fwd);
   m.impl("lstm2_persist_bwd", &lstm2_persist_bwd);
+  m.impl("lstm_big_fwd", &lstm_big_fwd);
   m.impl("sample_step", &sample_step);
   m.impl("gru_persist_bwd", &gru_persist_bwd);
 }

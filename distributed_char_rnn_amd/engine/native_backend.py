@@ -163,6 +163,11 @@ class NativeBackend:
         self.use_pair = os.environ.get("DCR_PAIR", "1") != "0"
         # two-layer wavefront BPTT (lstm2_persist.hip) for the same pairs
         self.use_pair_bwd = os.environ.get("DCR_PAIR_BWD", "1") != "0"
+        # large-H weights-resident forward (lstm_big.hip) for 1024 < H <= 2048: opt-in.  Its
+        # every-step all-to-all hand-off spans all 8 XCDs and the payload phase measured ~15 us
+        # per step (scripts/big_stamps.py) vs 16.4 us for a whole per-step kernel, so the
+        # per-step kernels stay the default there (open gap)
+        self.use_big_fwd = os.environ.get("DCR_BIG_FWD", "0") == "1"
         self.spin_limit = int(os.environ.get("DCR_SPIN_LIMIT", str(1 << 22)))
         # forward hand-off form: "granule" (tagged data, R2) or "counter" (sc1 data + counter)
         self.handoff = os.environ.get("DCR_HANDOFF", "counter")
@@ -376,7 +381,7 @@ class NativeBackend:
         forces a mode.
         """
         plan = dict(persist=False, xfuse=False, mode="exclusive", bwd_excl=False,
-                    gru_persist=False, pair=False, pair_bwd=False)
+                    gru_persist=False, pair=False, pair_bwd=False, big_fwd=False)
         o = self.ops
         if T < self.persist_min_t:
             # a persistent grid first loads every weight slice into registers (~6 MB for the
@@ -387,6 +392,13 @@ class NativeBackend:
             # persistent GRU (gru_persist.hip): the C++ side picks the unit block whose fwd and
             # bwd grids are co-resident; always exclusive (nothing beside it)
             plan["gru_persist"] = bool(o.gru_persist_ub(self.H, B))
+            return plan
+        if (self.use_persist and self.cfg.model == "lstm" and self.H > 1024
+                and os.environ.get("DCR_FRAG", "1") != "0"
+                and self.use_big_fwd and bool(o.lstm_big_supported(self.H, B))):
+            # large H (lstm_big.hip): weights-resident forward with 8-unit shards; the BPTT
+            # stays on the per-step kernels
+            plan["big_fwd"] = True
             return plan
         if not (self.use_persist and self.cfg.model == "lstm"
                 and bool(o.lstm_persist_supported(self.H, B))):
@@ -466,7 +478,7 @@ class NativeBackend:
                     tasks.append((src, dst, 0))
                 else:
                     dst.copy_(src)
-        if bufs["persist"] or bufs["gru_persist"]:
+        if bufs["persist"] or bufs["gru_persist"] or bufs["big_fwd"]:
             tasks.append((bufs["cnt"], bufs["cnt"], 2))
         self._run_prep(tasks)
         # the persistent LSTM kernels write the final (c, h) straight into fresh tensors that
@@ -538,6 +550,10 @@ class NativeBackend:
                                           hring=(bufs["hrings"][0] if bufs["hrings"]
                                                  and self.handoff != "granule" else None),
                                           clast32=lb.clast32)
+            elif bufs["big_fwd"]:
+                self.ops.lstm_big_fwd(lw.WhT, zx, ids_arg, lb.hbuf, lb.cbuf, lb.gates,
+                                      lb.hlast32, bufs["cnt"][layer], self.err, FORGET_BIAS,
+                                      self.spin_limit, bufs["hrings"][0], cnt_zeroed=True)
             elif bufs["gru_persist"]:
                 gr = bufs["grings"]
                 self.ops.gru_persist_fwd(lw.WhT, lw.WT2, zx, ids_arg, lb.hbuf, lb.h32, lb.rh,
@@ -804,7 +820,7 @@ class NativeBackend:
             user_ready(off)
         extras = {"logits": logits, "loss": bufs["row_loss"]} if want_extras else None
         self._steps += 1
-        if persistent and self._steps % 200 == 1:
+        if (persistent or bufs["big_fwd"]) and self._steps % 200 == 1:
             self.check_errors()
         return bufs["loss"][0], new_state, extras
 

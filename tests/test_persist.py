@@ -180,3 +180,33 @@ def test_two_layer_wavefront_bptt_equals_single_layer_kernels(B, T, H, L, monkey
     for s in a.store.specs:
         e = rel(a.store.gview(s.name), b.store.gview(s.name))
         assert e < 2e-3, (s.name, e)
+
+
+@pytest.mark.parametrize("B,T,H,L", [(64, 5, 2048, 2), (32, 4, 1152, 1), (32, 6, 1536, 2)])
+def test_large_h_forward_equals_per_step_kernels(B, T, H, L, monkeypatch):
+    """lstm_big.hip (weights-resident forward with 8-unit shards, 1024 < H <= 2048) vs the
+    per-step kernels: the same bf16 math, so agreement to accumulation-order noise."""
+    cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=L)
+    monkeypatch.setenv("DCR_BIG_FWD", "1")  # opt-in path
+    a = CharRNN(cfg, device="cuda", seed=4)
+    if not a.backend._persist_plan(B, True)["big_fwd"]:
+        pytest.skip("large-H persistent forward not co-resident for this shape")
+    monkeypatch.setenv("DCR_BIG_FWD", "0")
+    b = CharRNN(cfg, device="cuda", seed=4)
+    assert not b.backend._persist_plan(B, True)["big_fwd"]
+    torch.manual_seed(3)
+    x = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
+    y = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
+    st = [tuple(torch.randn(B, H, device="cuda") * 0.5 for _ in range(2)) for _ in range(L)]
+    la, sa, _ = a.backend.train_step(x, y, [tuple(s.clone() for s in t) for t in st])
+    lb, sb, _ = b.backend.train_step(x, y, [tuple(s.clone() for s in t) for t in st])
+    torch.cuda.synchronize()
+    a.backend.check_errors()
+    assert abs(la.item() - lb.item()) < 1e-3
+    for u, v in zip(sa, sb):
+        for p, q in zip(u, v):
+            assert rel(p, q) < 2e-3
+    assert rel(a.store.grad, b.store.grad) < 5e-3
+    ref = ReferenceBackend(a.store)
+    lr, _, _ = ref.train_step(x, y, [tuple(s.clone() for s in t) for t in st])
+    assert abs(la.item() - lr.item()) < 2e-2 * max(1.0, abs(lr.item()))
