@@ -629,11 +629,19 @@ class NativeBackend:
         persistent = bufs["persist"] or bufs["gru_persist"]
         overlap = bufs["mode"] == "overlap" or not persistent
         pending = []
+        user_ready = None
         if on_ready is not None and not overlap:
             # exclusive mode: nothing may run beside the persistent BPTT grids, so the gradient
-            # buckets are released (in the same order) only after the last BPTT launch
+            # buckets are released (in the same order) only after the last BPTT launch; from
+            # then on readiness is forwarded directly (the remaining weight GEMMs overlap RCCL)
             user_ready = on_ready
             on_ready = pending.append
+
+        def _release():
+            for off in pending:
+                user_ready(off)
+            pending.clear()
+            return user_ready
         if on_ready is not None:
             sb = s.by_name["rnnlm/softmax_b"]
             on_ready(sb.offset + sb.numel)
@@ -664,10 +672,8 @@ class NativeBackend:
                                            bufs["cnt"][self.L + layer], self.err,
                                            self.spin_limit)
                 paired_done = lo
-                if lo == 0 and pending:
-                    for off in pending:
-                        user_ready(off)
-                    pending.clear()
+                if lo == 0 and user_ready is not None:
+                    on_ready = _release()
             elif layer == paired_done:
                 pass
             elif bufs["persist"]:
@@ -683,22 +689,18 @@ class NativeBackend:
                                           above[1] if above else None,
                                           exclusive=bufs["bwd_excl"] and above is None,
                                           cnt_zeroed=True, zring=bufs["zring"])
-                if layer == 0 and pending:
+                if layer == 0 and user_ready is not None:
                     # the last persistent grid is queued: buckets may now run beside the
                     # (non-persistent) layer-0 weight GEMMs
-                    for off in pending:
-                        user_ready(off)
-                    pending.clear()
+                    on_ready = _release()
             elif bufs["gru_persist"]:
                 gr = bufs["grings"]
                 self.ops.gru_persist_bwd(lw.W2, lw.Wh, dtop, lb.dz, lb.gates, lb.h32,
                                          bufs["cnt"][self.L + layer], self.err, self.spin_limit,
                                          cnt_zeroed=True, ring0=gr[0] if gr else None,
                                          ring1=gr[2] if gr else None)
-                if layer == 0 and pending:
-                    for off in pending:
-                        user_ready(off)
-                    pending.clear()
+                if layer == 0 and user_ready is not None:
+                    on_ready = _release()
             else:
                 self.ops.rnn_bwd_seq(self.cell, lw.Wh, lw.W2, dtop, lb.dz, lb.dzx, lb.gates,
                                      lb.pre, lb.aux, zx_nas, lb.cbuf, lb.h32, lb.hbuf, bufs["dc"],
@@ -816,8 +818,8 @@ class NativeBackend:
         if self._side_used:
             torch.cuda.current_stream().wait_stream(self._side)
             self._side_used = False
-        for off in pending:
-            user_ready(off)
+        if pending:
+            _release()
         extras = {"logits": logits, "loss": bufs["row_loss"]} if want_extras else None
         self._steps += 1
         if (persistent or bufs["big_fwd"]) and self._steps % 200 == 1:
