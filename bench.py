@@ -42,6 +42,8 @@ def parse(argv=None):
     ap.add_argument("--model", default="lstm")
     ap.add_argument("--bucket_mb", type=float, default=8.0)
     ap.add_argument("--allreduce_dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--clip_norm", default="tf", choices=["tf", "dense"],
+                    help="embedding term of the clip norm (default: TF per-token semantics)")
     ap.add_argument("--profile", action="store_true", help="print a per-phase timing table")
     ap.add_argument("--dist_backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="auto = nccl (RCCL over xGMI) on GPUs; gloo = multi-rank rehearsal on "
@@ -77,7 +79,8 @@ def main(argv=None) -> int:
             torch.cuda.synchronize()
     rank, world = max(ctx.rank, 0), ctx.world_size
 
-    cfg = ModelConfig(model=a.model, vocab_size=a.vocab, rnn_size=a.hidden, num_layers=a.layers)
+    cfg = ModelConfig(model=a.model, vocab_size=a.vocab, rnn_size=a.hidden, num_layers=a.layers,
+                      clip_norm=a.clip_norm)
     model = CharRNN(cfg, device=device, seed=1234)
     opt = TFAdam(model.store, clip=5.0)
     sync = GradSync(model.store, world, a.bucket_mb, a.allreduce_dtype)

@@ -12,9 +12,16 @@ typedef __bf16 bf16;
 int opt_num_partials(int64_t n);
 void launch_global_norm(const float* g, int64_t n, float* partials, float* norm_out,
                         hipStream_t stream);
+void launch_sumsq(const void* x, bool is_bf16, int64_t n, float* partials, float* out,
+                  hipStream_t stream);
+bool tok_norm_supported(int64_t N, int H, int K);
+int tok_norm_num_partials(int64_t N, int H);
+void launch_tok_norm(const bf16* dz, const bf16* w, int64_t N, int H, int K, float* partials,
+                     float* out, hipStream_t stream);
 void launch_adam_clip(float* p, const float* g, float* m, float* v, bf16* pbf, int64_t n,
                       float* partials, float* norm_out, float lr_t, float b1, float b2, float eps,
-                      float clip, float gscale, hipStream_t stream);
+                      float clip, float gscale, int64_t n_norm, const float* extra_sq,
+                      hipStream_t stream);
 
 // ---- rnn_step.hip -----------------------------------------------------------------------
 enum CellKind { CELL_LSTM = 0, CELL_GRU_A = 1, CELL_GRU_B = 2, CELL_RNN = 3, CELL_NAS = 4 };

@@ -36,9 +36,35 @@ void global_norm(const at::Tensor& g, at::Tensor& partials, at::Tensor& norm_out
                           cur_stream());
 }
 
+// out[0] = sum(x^2) with fp32 accumulation; x fp32 or bf16
+void sumsq(const at::Tensor& x, at::Tensor& partials, at::Tensor& out) {
+  CHECK_DEV(x); CHECK_CONTIG(x); CHECK_ALIGN16(x);
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16,
+              "sumsq: fp32 or bf16");
+  CHECK_F32(partials); CHECK_F32(out);
+  TORCH_CHECK(partials.numel() >= dcr::opt_num_partials(x.numel()), "partials too small");
+  dcr::launch_sumsq(x.data_ptr(), x.scalar_type() == at::kBFloat16, x.numel(),
+                    ptr<float>(partials), ptr<float>(out), cur_stream());
+}
+
+// out[0] = sum over rows of ||dz[n, :] · wᵀ||^2  (dz [N, K] bf16, w [H, K] bf16), fused
+void tok_norm(const at::Tensor& dz, const at::Tensor& w, at::Tensor& partials, at::Tensor& out) {
+  CHECK_DEV(dz); CHECK_CONTIG(dz); CHECK_BF16(dz); CHECK_ALIGN16(dz);
+  CHECK_DEV(w); CHECK_CONTIG(w); CHECK_BF16(w); CHECK_ALIGN16(w);
+  CHECK_F32(partials); CHECK_F32(out);
+  TORCH_CHECK(dz.dim() == 2 && w.dim() == 2 && dz.size(1) == w.size(1), "tok_norm: shapes");
+  const int64_t N = dz.size(0);
+  const int H = (int)w.size(0), K = (int)w.size(1);
+  TORCH_CHECK(dcr::tok_norm_supported(N, H, K), "tok_norm: unsupported shape");
+  TORCH_CHECK(partials.numel() >= dcr::tok_norm_num_partials(N, H), "partials too small");
+  dcr::launch_tok_norm(ptr<bf16>(dz), ptr<bf16>(w), N, H, K, ptr<float>(partials),
+                       ptr<float>(out), cur_stream());
+}
+
 void adam_clip(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
                const c10::optional<at::Tensor>& pbf, at::Tensor& partials, at::Tensor& norm_out,
-               double lr_t, double b1, double b2, double eps, double clip, double gscale) {
+               double lr_t, double b1, double b2, double eps, double clip, double gscale,
+               int64_t n_norm, const c10::optional<at::Tensor>& extra_sq) {
   for (const at::Tensor* t : {(const at::Tensor*)&p, &g, (const at::Tensor*)&m, (const at::Tensor*)&v}) {
     CHECK_DEV(*t); CHECK_CONTIG(*t); CHECK_F32(*t); CHECK_ALIGN16(*t);
     TORCH_CHECK(t->numel() == p.numel(), "adam buffers must have equal numel");
@@ -50,9 +76,18 @@ void adam_clip(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
     pb = ptr<bf16>(*pbf);
   }
   TORCH_CHECK(partials.numel() >= dcr::opt_num_partials(p.numel()), "partials too small");
+  if (n_norm < 0) n_norm = p.numel();
+  TORCH_CHECK(n_norm <= p.numel(), "adam_clip: n_norm must be <= numel");
+  const float* ex = nullptr;
+  if (extra_sq.has_value() && extra_sq->defined()) {
+    CHECK_DEV(*extra_sq); CHECK_F32(*extra_sq);
+    TORCH_CHECK(extra_sq->numel() >= 1, "extra_sq: one element");
+    ex = ptr<float>(*extra_sq);
+  }
   dcr::launch_adam_clip(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), pb,
                         p.numel(), ptr<float>(partials), ptr<float>(norm_out), (float)lr_t,
-                        (float)b1, (float)b2, (float)eps, (float)clip, (float)gscale, cur_stream());
+                        (float)b1, (float)b2, (float)eps, (float)clip, (float)gscale, n_norm, ex,
+                        cur_stream());
 }
 
 // ------------------------------------------------------------------------------------------
@@ -936,7 +971,13 @@ TORCH_LIBRARY(dcr, m) {
   m.def(
       "adam_clip(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? pbf, "
       "Tensor(e!) partials, Tensor(f!) norm_out, float lr_t, float b1, float b2, float eps, "
-      "float clip, float gscale=1.0) -> ()");
+      "float clip, float gscale=1.0, int n_norm=-1, Tensor? extra_sq=None) -> ()");
+  m.def("sumsq(Tensor x, Tensor(a!) partials, Tensor(b!) out) -> ()");
+  m.def("tok_norm(Tensor dz, Tensor w, Tensor(a!) partials, Tensor(b!) out) -> ()");
+  m.def("tok_norm_supported(int N, int H, int K) -> bool",
+        [](int64_t N, int64_t H, int64_t K) -> bool {
+          return dcr::tok_norm_supported(N, (int)H, (int)K);
+        });
   m.def(
       "rnn_fwd_seq(int cell, Tensor WT, Tensor? WT2, Tensor zx, Tensor? ids, Tensor(a!) hbuf, "
       "Tensor(b!)? h32, Tensor(c!)? cbuf, Tensor(d!)? gates, Tensor(e!)? pre, Tensor(f!)? aux, "
@@ -1050,6 +1091,8 @@ TORCH_LIBRARY(dcr, m) {
 
 TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("global_norm", &global_norm);
+  m.impl("sumsq", &sumsq);
+  m.impl("tok_norm", &tok_norm);
   m.impl("adam_clip", &adam_clip);
   m.impl("rnn_fwd_seq", &rnn_fwd_seq);
   m.impl("rnn_bwd_seq", &rnn_bwd_seq);

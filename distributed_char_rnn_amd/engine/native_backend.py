@@ -187,6 +187,11 @@ class NativeBackend:
         self._side = None
         self._side_used = False
         self._steps = 0
+        # TF clip-norm semantics for the embedding gradient (models/params.py: clip_norm)
+        self.tf_norm = self.cfg.clip_norm == "tf"
+        self._npart: Optional[torch.Tensor] = None
+        self._tpart: Optional[torch.Tensor] = None
+        self.tok_norm_fused = os.environ.get("DCR_TOK_NORM", "library") == "fused"
         self.gen = torch.Generator(device=self.dev)
         self.gen.manual_seed(int(seed))
 
@@ -649,6 +654,11 @@ class NativeBackend:
         c = self.cfg
         deferred = []
         paired_done = -1  # lower layer whose BPTT already ran inside a two-layer wavefront
+        # TF clip-norm term from dx_tok = dZ0·W_x0ᵀ: needed as an extra GEMM only on the layer-0
+        # gather route (every other route materialises dx_tok anyway)
+        gather0 = not drop and self.cfg.model != "nas"
+        fused_dew0 = bufs["persist"] and gather0 and V <= 128 and self.fused_dew
+        tok_gemm = self.tf_norm and gather0 and not (V > SEG_LDS_MAX_V and not fused_dew0)
         for layer in reversed(range(self.L)):
             lw, lb = self._w[layer], bufs["layers"][layer]
             names = [sp.name for sp in cell_specs(self.cfg, layer)]
@@ -772,6 +782,7 @@ class NativeBackend:
                     dbias = bufs["colsum"][0, :GW]
                 dXf = _mm_into(dZx, lw.Wx.t(), bufs["dx"].view(N, H))
                 self.ops.segsum(dXf, ids_tm.view(-1), V, s.gview("embedding"), bufs["ws"], False)
+                self._token_norm(dXf)
             elif gather:
                 if fused_dew:
                     dEW = bufs["dew_part"].sum(0)            # [V, GW] fp32 (fused in BPTT)
@@ -788,6 +799,8 @@ class NativeBackend:
                 dWx = hd["E"].t() @ dEW                      # [H, GW] fp32
                 dbias = dEW.sum(0)
                 torch.mm(dEW, lw.Wx32.t(), out=s.gview("embedding"))
+                if tok_gemm:
+                    self._token_norm_gemm(dZx, lw.Wx)
             else:
                 dWx = (_mm_tn(lb.x_in, dZx, s.gview(names[0])[:H])
                        if self.cfg.model in ("lstm", "rnn") else _mm_tn(lb.x_in, dZx))
@@ -812,7 +825,13 @@ class NativeBackend:
                         dX = dX * lb.masks["emb"]
                     dXf = dX.reshape(N, H).float().contiguous()
                     self.ops.segsum(dXf, ids_tm.view(-1), V, s.gview("embedding"), bufs["ws"], False)
+                    self._token_norm(dXf)
             self._write_input_grads(layer, names, dWx, dbias)
+            if layer == 0 and self._side_used:
+                # side-stream work (token-norm slot, overlapped weight GEMMs) is part of the
+                # last bucket: join before reporting it ready
+                torch.cuda.current_stream().wait_stream(self._side)
+                self._side_used = False
             if on_ready is not None:
                 on_ready(None if layer == 0 else s.layer_range(layer)[1])
         if self._side_used:
@@ -825,6 +844,33 @@ class NativeBackend:
         if (persistent or bufs["big_fwd"]) and self._steps % 200 == 1:
             self.check_errors()
         return bufs["loss"][0], new_state, extras
+
+    def _token_norm(self, dx_tok: torch.Tensor) -> None:
+        """TF clip-norm term of the embedding (ModelConfig.clip_norm == "tf"): the sum of
+        squares of the per-token input gradients (the IndexedSlices values), written into the
+        gradient buffer's norm slot (all-reduced with the last bucket, read by adam_clip)."""
+        if not self.tf_norm:
+            return
+        n = dx_tok.numel()
+        if self._npart is None or self._npart.numel() < self.ops.opt_num_partials(n):
+            self._npart = torch.empty(self.ops.opt_num_partials(n), dtype=f32, device=self.dev)
+        self.ops.sumsq(dx_tok.contiguous(), self._npart, self.store.norm_slot_view())
+
+    def _token_norm_gemm(self, dz0: torch.Tensor, wx0: torch.Tensor) -> None:
+        """sum_tok ||dZ0_tok·W_x0ᵀ||² into the norm slot.  Default: the library GEMM to bf16
+        rows + the sumsq kernel (66 us at the headline shape, scripts/bench_tok_norm.py);
+        DCR_TOK_NORM=fused: the fused MFMA kernel (optim.hip tok_norm, the [N, H] product never
+        materialised) -- correct, but at 470-530 TFLOP/s it does not reach the library GEMM's
+        ~1 PFLOP/s yet (128-145 us).  A side-stream overlap with the weight GEMMs was measured
+        slower than running in line: both are chip-filling."""
+        N, K = dz0.shape
+        if self.tok_norm_fused and self.ops.tok_norm_supported(N, wx0.shape[0], K):
+            n = (N // 128) * (wx0.shape[0] // 64)  # >= workgroups of any tile choice
+            if self._tpart is None or self._tpart.numel() < n:
+                self._tpart = torch.empty(n, dtype=f32, device=self.dev)
+            self.ops.tok_norm(dz0, wx0, self._tpart, self.store.norm_slot_view())
+        else:
+            self._token_norm(torch.mm(dz0, wx0.t()))
 
     def _bias_sum(self, part: torch.Tensor, names) -> torch.Tensor:
         """Sum the per-batch-group bias partials; for cells with one [GW] bias the sum is

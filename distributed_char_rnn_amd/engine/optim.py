@@ -6,7 +6,11 @@ Reference: ``grads, _ = clip_by_global_norm(tf.gradients(cost, tvars), grad_clip
 "epsilon-hat" form: ``lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t)``,
 ``theta -= lr_t * m / (sqrt(v) + eps)`` with ``b1 = .9, b2 = .999, eps = 1e-8`` [TF-ext].
 The embedding's IndexedSlices update in TF decays m/v densely and updates every row, which is
-exactly dense Adam with a zero gradient for unseen rows, so one dense kernel matches it.
+exactly dense Adam with a zero gradient for unseen rows, so one dense kernel matches it.  The
+global norm, however, sees the IndexedSlices *values* (one row per token, duplicates not yet
+summed), so with ``ModelConfig.clip_norm == "tf"`` the dense embedding gradient is left out of
+the norm and the per-token sum of squares in ``ParamStore.norm_slot`` (written by the backend's
+backward) is added instead.
 
 On the GPU the whole update is the two-launch fused kernel in ``csrc/optim.hip``; on CPU the
 same math runs as torch ops.
@@ -56,20 +60,28 @@ class TFAdam:
         one update.  Returns the pre-clip global norm as a 1-element device tensor (no host
         sync)."""
         lr_t = self.lr_t(lr)
-        p, g = self.store.flat, self.store.grad
+        st = self.store
+        n = st.norm_slot  # every parameter; the norm slot and the padding after it are not
+        p, g, m, v = (b.narrow(0, 0, n) for b in (st.flat, st.grad, self.m, self.v))
+        n_norm, use_slot = st.norm_terms()
+        slot = st.norm_slot_view() if use_slot else None
         if self.native:
-            self._ops.adam_clip(p, g, self.m, self.v, self.mirror, self._partials, self.last_norm,
-                                lr_t, self.b1, self.b2, self.eps, self.clip, float(grad_scale))
+            mirror = self.mirror.narrow(0, 0, n) if self.mirror is not None else None
+            self._ops.adam_clip(p, g, m, v, mirror, self._partials, self.last_norm, lr_t,
+                                self.b1, self.b2, self.eps, self.clip, float(grad_scale), n_norm,
+                                slot)
         else:
-            norm = torch.sqrt((g.double() * g.double()).sum()).float() * grad_scale
+            gn = g.narrow(0, 0, n_norm).double()
+            sq = (gn * gn).sum() + (slot.double().sum() if slot is not None else 0.0)
+            norm = torch.sqrt(sq).float() * grad_scale
             s = self.clip / torch.clamp(norm, min=self.clip) if self.clip > 0 else torch.ones(())
             gs = g * (s * grad_scale)
-            self.m.mul_(self.b1).add_(gs, alpha=1 - self.b1)
-            self.v.mul_(self.b2).addcmul_(gs, gs, value=1 - self.b2)
-            p.sub_(lr_t * self.m / (self.v.sqrt() + self.eps))
+            m.mul_(self.b1).add_(gs, alpha=1 - self.b1)
+            v.mul_(self.b2).addcmul_(gs, gs, value=1 - self.b2)
+            p.sub_(lr_t * m / (v.sqrt() + self.eps))
             self.last_norm.copy_(norm.reshape(1))
             if self.mirror is not None:
-                self.mirror.copy_(p)
+                self.mirror.copy_(st.flat)
         self.t += 1
         self.store.version += 1
         return self.last_norm

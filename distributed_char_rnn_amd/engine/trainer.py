@@ -115,7 +115,8 @@ def restore(model: CharRNN, opt: TFAdam, prefix: str):
 def build_model(args, vocab_size: int, device) -> CharRNN:
     cfg = ModelConfig(model=args.model, vocab_size=vocab_size, rnn_size=args.rnn_size,
                       num_layers=args.num_layers, input_keep_prob=args.input_keep_prob,
-                      output_keep_prob=args.output_keep_prob)
+                      output_keep_prob=args.output_keep_prob,
+                      clip_norm=getattr(args, "clip_norm", "tf"))
     return CharRNN(cfg, device=device, seed=args.seed, dtype=getattr(args, "dtype", "auto"))
 
 

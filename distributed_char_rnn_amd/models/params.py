@@ -46,10 +46,16 @@ class ModelConfig:
     num_layers: int = 2
     input_keep_prob: float = 1.0
     output_keep_prob: float = 1.0
+    # What the global-norm clip measures for the embedding gradient: "tf" = TF 1.x semantics,
+    # the IndexedSlices values (one [H] row per token, before duplicates are summed;
+    # model.py:55,91-92 [TF-ext]); "dense" = the norm of the summed [V, H] gradient.
+    clip_norm: str = "tf"
 
     def __post_init__(self):
         if self.model not in CELL_SCOPES:
             raise ValueError(f"model type not supported: {self.model}")
+        if self.clip_norm not in ("tf", "dense"):
+            raise ValueError(f"clip_norm must be 'tf' or 'dense', got {self.clip_norm!r}")
 
     @property
     def gates(self) -> int:
@@ -124,7 +130,13 @@ class ParamStore:
         self.cfg = cfg
         self.specs = model_specs(cfg)
         last = self.specs[-1]
-        self.numel = last.offset + (last.numel + ALIGN - 1) // ALIGN * ALIGN
+        # After the last tensor (the embedding): one aligned block whose first element is the
+        # "norm slot" -- the per-token sum of squares of the embedding gradient that TF's
+        # clip_by_global_norm sees (ModelConfig.clip_norm == "tf").  It lives in the gradient
+        # buffer so data-parallel all-reduce sums it with everything else for free; the
+        # optimizer never updates it.
+        self.norm_slot = last.offset + (last.numel + ALIGN - 1) // ALIGN * ALIGN
+        self.numel = self.norm_slot + ALIGN
         self.device = torch.device(device)
         self.flat = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
         self.grad = torch.zeros_like(self.flat)
@@ -143,6 +155,18 @@ class ParamStore:
 
     def names(self) -> List[str]:
         return [s.name for s in self.specs]
+
+    def norm_terms(self) -> Tuple[int, bool]:
+        """(n_norm, use_slot): the clip norm is sum(grad[:n_norm]^2) (+ grad[norm_slot] when
+        use_slot).  In "tf" mode the dense embedding gradient (the last tensor) is replaced
+        by the per-token term in the slot."""
+        if self.cfg.clip_norm == "tf":
+            return self.by_name["embedding"].offset, True
+        return self.norm_slot, False
+
+    def norm_slot_view(self, buf: Optional[torch.Tensor] = None) -> torch.Tensor:
+        b = self.grad if buf is None else buf
+        return b.narrow(0, self.norm_slot, 1)
 
     def layer_names(self, layer: int) -> List[str]:
         return [s.name for s in cell_specs(self.cfg, layer)]

@@ -117,10 +117,14 @@ def _dropout(x, keep: float, gen: Optional[torch.Generator]):
 
 
 def forward(cfg: ModelConfig, params: dict, x: torch.Tensor, state: State, training: bool = True,
-            gen: Optional[torch.Generator] = None):
-    """x: int [B, T].  Returns (logits [B*T, V] batch-major, final_state, outputs [B, T, H])."""
+            gen: Optional[torch.Generator] = None, taps: Optional[dict] = None):
+    """x: int [B, T].  Returns (logits [B*T, V] batch-major, final_state, outputs [B, T, H]).
+    ``taps["emb"]`` receives the embedding_lookup output (the tensor whose gradient TF
+    represents as IndexedSlices)."""
     B, T = x.shape
     emb = params["embedding"][x.long()]  # [B, T, H]
+    if taps is not None:
+        taps["emb"] = emb
     if training and cfg.output_keep_prob:
         emb = _dropout(emb, cfg.output_keep_prob, gen)
     wrap = training and (cfg.output_keep_prob < 1.0 or cfg.input_keep_prob < 1.0)
@@ -174,16 +178,26 @@ class ReferenceBackend:
     def train_step(self, x, y, state: State, on_bucket_ready=None, want_extras: bool = False):
         params = self.params(True)
         gen = self.gen if self.store.device.type == "cpu" else None
-        logits, new_state, _ = forward(self.cfg, params, x, state, training=True, gen=gen)
+        taps = {}
+        logits, new_state, _ = forward(self.cfg, params, x, state, training=True, gen=gen,
+                                       taps=taps)
         cost, per = loss_fn(logits, y)
         names = self.store.names()
-        grads = torch.autograd.grad(cost, [params[n] for n in names], allow_unused=True)
+        grads = torch.autograd.grad(cost, [params[n] for n in names] + [taps["emb"]],
+                                    allow_unused=True)
         for n, g in zip(names, grads):
             gv = self.store.gview(n)
             if g is None:
                 gv.zero_()
             else:
                 gv.copy_(g)
+        # TF's clip norm term for the embedding: the per-token IndexedSlices values
+        g_tok = grads[-1]
+        slot = self.store.norm_slot_view()
+        if self.cfg.clip_norm == "tf" and g_tok is not None:
+            slot.copy_((g_tok.double() ** 2).sum().reshape(1))
+        else:
+            slot.zero_()
         if on_bucket_ready is not None:
             on_bucket_ready(None)  # everything is ready at once on this path
         detached = [tuple(s.detach() for s in st) for st in new_state]

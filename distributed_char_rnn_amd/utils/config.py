@@ -36,6 +36,9 @@ def train_parser() -> argparse.ArgumentParser:
                    help="minibatch size per worker (sequences propagated in parallel)")
     p.add_argument("--num_epochs", type=int, default=50, help="number of epochs")
     p.add_argument("--grad_clip", type=float, default=5.0, help="clip gradients at this global norm")
+    p.add_argument("--clip_norm", choices=["tf", "dense"], default="tf",
+                   help="embedding term of the clip norm: 'tf' = per-token IndexedSlices values "
+                        "(TF 1.x, the reference), 'dense' = the summed [V, H] gradient")
     p.add_argument("--learning_rate", type=float, default=0.002, help="learning rate")
     p.add_argument("--decay_rate", type=float, default=0.97,
                    help="per-epoch exponential learning-rate decay (Adam)")

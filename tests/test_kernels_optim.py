@@ -43,6 +43,69 @@ def test_adam_clip_matches_reference(dcr_ops, n, clip):
     torch.testing.assert_close(pbf.float(), p.to(torch.bfloat16).float(), rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("n,n_norm", [(4096, 4096), (100000, 60000), (4265088, 4265024)])
+def test_adam_clip_partial_norm_plus_extra(dcr_ops, n, n_norm):
+    """norm = sqrt(sum(g[:n_norm]^2) + extra) (TF IndexedSlices embedding term); the update
+    still covers all n elements."""
+    torch.manual_seed(2)
+    dev = "cuda"
+    p = torch.randn(n, device=dev)
+    g = torch.randn(n, device=dev) * 0.1
+    m = torch.zeros(n, device=dev)
+    v = torch.zeros(n, device=dev)
+    extra = torch.tensor([3.25], device=dev)
+    parts = torch.empty(dcr_ops.opt_num_partials(n), device=dev)
+    norm = torch.empty(1, device=dev)
+    want = math.sqrt(float((g[:n_norm].double() ** 2).sum()) + 3.25)
+    s = 1.0 / max(want, 1.0)
+    lr, b1, b2, eps = 1e-3, 0.9, 0.999, 1e-8
+    gs = g * s
+    rm = (1 - b1) * gs
+    rv = (1 - b2) * gs * gs
+    rp = p - lr * rm / (rv.sqrt() + eps)
+    dcr_ops.adam_clip(p, g, m, v, None, parts, norm, lr, b1, b2, eps, 1.0, 1.0, n_norm, extra)
+    torch.cuda.synchronize()
+    assert norm.item() == pytest.approx(want, rel=1e-5)
+    torch.testing.assert_close(m, rm, rtol=1e-5, atol=1e-9)
+    torch.testing.assert_close(p, rp, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n", [3, 4097, 32768 * 512])
+def test_sumsq_kernel(dcr_ops, dtype, n):
+    torch.manual_seed(3)
+    x = (torch.randn(n, device="cuda") * 0.01).to(dtype)
+    parts = torch.empty(dcr_ops.opt_num_partials(n), device="cuda")
+    out = torch.empty(1, device="cuda")
+    dcr_ops.sumsq(x, parts, out)
+    torch.cuda.synchronize()
+    assert out.item() == pytest.approx(float((x.double() ** 2).sum()), rel=1e-5)
+
+
+@pytest.mark.parametrize("N,H,K", [(128, 64, 256), (1024, 512, 2048), (384, 256, 768),
+                                   (256, 128, 128), (32768, 512, 2048), (256, 192, 768),
+                                   (256, 1024, 4096), (128, 2048, 2048)])
+def test_tok_norm_kernel(dcr_ops, N, H, K):
+    """Fused sum_n ||dz[n]·wᵀ||² (TF per-token embedding norm term) vs an fp64 reference of
+    the same bf16 operands."""
+    torch.manual_seed(4)
+    dz = (torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16)
+    w = (torch.randn(H, K, device="cuda") * 0.05).to(torch.bfloat16)
+    assert dcr_ops.tok_norm_supported(N, H, K)
+    parts = torch.empty((N // 128) * (H // 64), device="cuda")
+    out = torch.empty(1, device="cuda")
+    dcr_ops.tok_norm(dz, w, parts, out)
+    torch.cuda.synchronize()
+    want = float(((dz.double() @ w.double().t()) ** 2).sum())
+    assert out.item() == pytest.approx(want, rel=1e-4)
+
+
+def test_tok_norm_unsupported_shapes(dcr_ops):
+    assert not dcr_ops.tok_norm_supported(100, 512, 2048)   # N % 128
+    assert not dcr_ops.tok_norm_supported(128, 512, 96)     # K % 64
+    assert not dcr_ops.tok_norm_supported(128, 96, 384)     # H % 64
+
+
 @pytest.mark.parametrize("world", [2, 8])
 def test_adam_clip_folds_data_parallel_average(dcr_ops, world):
     """gscale = 1/world on the all-reduced SUM == the kernel on the averaged gradient."""

@@ -95,19 +95,22 @@ def test_reference_gradients_finite_difference(model):
 
 
 def test_tf_adam_matches_formula_and_clips():
-    cfg = ModelConfig(model="rnn", vocab_size=5, rnn_size=4, num_layers=1)
+    cfg = ModelConfig(model="rnn", vocab_size=5, rnn_size=4, num_layers=1, clip_norm="dense")
     st = ParamStore(cfg, seed=0)
     opt = TFAdam(st, clip=0.5)
     p0 = st.flat.clone()
     st.grad.normal_()
-    g = st.grad.clone()
+    n = st.norm_slot  # parameters end here; the norm slot block is neither measured nor updated
+    g = st.grad[:n].clone()
     norm = g.norm().item()
     opt.step(0.01)
     gs = g * (0.5 / max(norm, 0.5))
     m = 0.1 * gs
     v = 0.001 * gs * gs
     lr_t = 0.01 * math.sqrt(1 - 0.999) / (1 - 0.9)
-    torch.testing.assert_close(st.flat, p0 - lr_t * m / (v.sqrt() + 1e-8), rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(st.flat[:n], p0[:n] - lr_t * m / (v.sqrt() + 1e-8), rtol=1e-5,
+                               atol=1e-7)
+    assert torch.equal(st.flat[n:], p0[n:])
     assert abs(opt.last_norm.item() - norm) < 1e-4
     assert opt.t == 1
     assert lr_for_epoch(0.002, 0.97, 3) == pytest.approx(0.002 * 0.97 ** 3)
@@ -178,6 +181,13 @@ def test_tf_adam_grad_scale_equals_averaged_gradient():
     g = torch.randn(a.store.numel) * 3.0
     a.store.grad.copy_(g / 4)
     b.store.grad.copy_(g)
+    # the norm slot holds a SUM OF SQUARES (TF per-token embedding term): the all-reduced
+    # slot of 4 ranks is averaged by 1/4^2, exactly what the folded grad_scale does to it
+    slot = a.store.norm_slot
+    a.store.grad[slot:] = 0.0
+    b.store.grad[slot:] = 0.0
+    a.store.grad[slot] = 7.0 / 16
+    b.store.grad[slot] = 7.0
     oa, ob = TFAdam(a.store, clip=1.0), TFAdam(b.store, clip=1.0)
     na = oa.step(1e-2)
     nb = ob.step(1e-2, grad_scale=0.25)

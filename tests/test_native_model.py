@@ -48,6 +48,10 @@ def test_train_step_matches_reference(model, B, T, H, L):
         gr = nat.store.view(s.name, g_ref)
         gn = nat.store.gview(s.name)
         assert rel(gn, gr) < 6e-2, (s.name, rel(gn, gr))
+    # TF clip-norm term: per-token sum of squares of the embedding-lookup gradient
+    slot_r = nat.store.norm_slot_view(g_ref)
+    slot_n = nat.store.norm_slot_view()
+    assert slot_r.item() > 0 and rel(slot_n, slot_r) < 6e-2, (slot_n, slot_r)
 
 
 @pytest.mark.parametrize("model", ["lstm", "gru"])
@@ -124,3 +128,21 @@ def test_per_step_batch_tiles_match_reference(model, nbt, monkeypatch):
     assert abs(loss_n.item() - loss_r.item()) < 2e-2 * max(1.0, abs(loss_r.item()))
     for s in nat.store.specs:
         assert rel(nat.store.gview(s.name), nat.store.view(s.name, g_ref)) < 6e-2, s.name
+
+
+def test_tf_norm_slot_fused_kernel_matches_library_route(monkeypatch):
+    """DCR_TOK_NORM=fused (optim.hip tok_norm) and the default library GEMM + sumsq route
+    write the same per-token embedding norm term on the persistent headline path."""
+    torch.manual_seed(0)
+    B, T, H = 64, 16, 128
+    x = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
+    y = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
+    slots = []
+    for mode in ("library", "fused"):
+        monkeypatch.setenv("DCR_TOK_NORM", mode)
+        cfg, nat, _ = _pair("lstm", B, T, H, 2)
+        nat.backend.train_step(x, y, nat.zero_state(B))
+        torch.cuda.synchronize()
+        slots.append(nat.store.norm_slot_view().item())
+    assert slots[0] > 0
+    assert slots[1] == pytest.approx(slots[0], rel=2e-3)
