@@ -119,6 +119,8 @@ __device__ __forceinline__ bool poll_counter2(unsigned* c0, unsigned t0, unsigne
   }
 }
 
+// Index helpers below are __host__ __device__ so tests/native/layout_check.hip can verify them
+// on the host under ASan/UBSan (tests/test_native_host.py).
 // Fragment-tiled hand-off layout.  Element (b, k) of a [B, K] bf16 slab lives at
 //   ((b/16 * K/32 + k/32) * 64 + ((k%32)/8)*16 + b%16) * 8 + k%8        (bf16 elements)
 // i.e. exactly where mfma_f32_16x16x32_bf16's B fragment of (batch tile b/16, k-step k/32)
@@ -126,11 +128,11 @@ __device__ __forceinline__ bool poll_counter2(unsigned* c0, unsigned t0, unsigne
 // byte 16*l), instead of 16 rows x 64 B of a row-major slab.  Measured with sc1 loads, 64 KB per
 // workgroup, 256 workgroups: 0.60 vs 1.74 us (half the L2 requests;
 // scripts/micro/payload_pattern.hip).  Producers' 4-unit (8 B) stores land 8-B aligned.
-__device__ __forceinline__ size_t frag_index(int b, int k, int K) {
+__host__ __device__ __forceinline__ size_t frag_index(int b, int k, int K) {
   return ((size_t)((b >> 4) * (K >> 5) + (k >> 5)) * 64 + ((k & 31) >> 3) * 16 + (b & 15)) * 8 +
          (k & 7);
 }
-__device__ __forceinline__ unsigned frag_load_off(int bg, int kstep, int K, int lane) {
+__host__ __device__ __forceinline__ unsigned frag_load_off(int bg, int kstep, int K, int lane) {
   return (unsigned)((((size_t)bg * (K >> 5) + kstep) * 64 + lane) * 16);
 }
 
@@ -139,7 +141,8 @@ __device__ __forceinline__ unsigned frag_load_off(int bg, int kstep, int K, int 
 // XCD; MI355X_MICROARCH.md "Workgroup dispatch"), so the batch group's hand-off payload is
 // fetched into one L2 and served to all its consumers from there.  Correctness never depends
 // on it: every hand-off is sc1 + counters regardless of placement.
-__device__ __forceinline__ void map_block(int bid, int nwg_u, int nbg, int& ubk, int& bg) {
+__host__ __device__ __forceinline__ void map_block(int bid, int nwg_u, int nbg, int& ubk,
+                                                    int& bg) {
   if (nbg % 8 == 0 && XCD_GROUPING) {
     const int xcd = bid % 8, j = bid / 8;  // j in [0, nwg_u * nbg / 8)
     bg = xcd + 8 * (j / nwg_u);
