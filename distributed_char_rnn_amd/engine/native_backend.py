@@ -860,9 +860,9 @@ class NativeBackend:
         """sum_tok ||dZ0_tok·W_x0ᵀ||² into the norm slot.  Default: the library GEMM to bf16
         rows + the sumsq kernel (66 us at the headline shape, scripts/bench_tok_norm.py);
         DCR_TOK_NORM=fused: the fused MFMA kernel (optim.hip tok_norm, the [N, H] product never
-        materialised) -- correct, but at 470-530 TFLOP/s it does not reach the library GEMM's
-        ~1 PFLOP/s yet (128-145 us).  A side-stream overlap with the weight GEMMs was measured
-        slower than running in line: both are chip-filling."""
+        materialised, LDS-DMA ring) -- correct, 92 us at 745 TFLOP/s, not yet at the library
+        GEMM's ~1 PFLOP/s.  A side-stream overlap with the weight GEMMs was measured slower
+        than running in line: both are chip-filling."""
         N, K = dz0.shape
         if self.tok_norm_fused and self.ops.tok_norm_supported(N, wx0.shape[0], K):
             n = (N // 128) * (wx0.shape[0] // 64)  # >= workgroups of any tile choice
