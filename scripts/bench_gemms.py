@@ -82,3 +82,15 @@ for S in (4, 8, 16):
     extra.append((f"dW NT split-K S={S} err={err:.1e}", timeit(lambda: splitk_nt(XT, ZT, S)), 2 * N * H * G))
 for name, us, fl in extra:
     print(f"{name:<52} {us:8.1f} us  {fl / us / 1e6:8.1f} TFLOP/s")
+
+# output-precision / orientation variants of the weight gradient (the library picks stream-K
+# kernels for some of them)
+outT = torch.empty(G, H, device=dev)
+more = [
+    ("dW  mm bf16 out", timeit(lambda: torch.mm(X.t(), Z)), 2 * N * H * G),
+    ("dW^T = Z^T X mm fp32 out [2048x512]", timeit(lambda: torch.mm(Z.t(), X, out_dtype=f32, out=outT)), 2 * N * H * G),
+    ("dW^T mm fp32 + transpose copy", timeit(lambda: out.copy_(torch.mm(Z.t(), X, out_dtype=f32).t())), 2 * N * H * G),
+    ("dW^T = Z^T X mm bf16 out", timeit(lambda: torch.mm(Z.t(), X)), 2 * N * H * G),
+]
+for name, us, fl in more:
+    print(f"{name:<52} {us:8.1f} us  {fl / us / 1e6:8.1f} TFLOP/s")
