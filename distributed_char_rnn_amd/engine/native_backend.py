@@ -667,6 +667,7 @@ class NativeBackend:
                     dtop = dtop * lb.masks["out"]
                 dtop = dtop.contiguous()
             zx_nas = lb.zx if self.cfg.model == "nas" else None
+            written = False  # this layer's kernel/bias gradients already in the flat buffer
             gather = (layer == 0 and not drop and self.cfg.model != "nas")
             fused_dew = bufs["persist"] and gather and V <= 128 and self.fused_dew
             pair_hi = bufs["pair_bwd"] and layer % 2 == 1 and not drop and dtop is not None
@@ -798,6 +799,15 @@ class NativeBackend:
                     self.ops.segsum(dZx, ids_tm.view(-1), V, dEW, bufs["ws"], False)
                 dWx = hd["E"].t() @ dEW                      # [H, GW] fp32
                 dbias = dEW.sum(0)
+                # layer 0's own gradients are final here: report them before the embedding
+                # gradient and the token-norm GEMM, so that under data parallelism the
+                # layer-0 bucket's all-reduce overlaps that work and the last bucket is only
+                # the embedding + norm slot
+                self._write_input_grads(layer, names, dWx, dbias)
+                written = True
+                if on_ready is not None:
+                    self._join_side()
+                    on_ready(s.layer_range(0)[1])
                 torch.mm(dEW, lw.Wx32.t(), out=s.gview("embedding"))
                 if tok_gemm:
                     self._token_norm_gemm(dZx, lw.Wx)
@@ -826,17 +836,15 @@ class NativeBackend:
                     dXf = dX.reshape(N, H).float().contiguous()
                     self.ops.segsum(dXf, ids_tm.view(-1), V, s.gview("embedding"), bufs["ws"], False)
                     self._token_norm(dXf)
-            self._write_input_grads(layer, names, dWx, dbias)
-            if layer == 0 and self._side_used:
-                # side-stream work (token-norm slot, overlapped weight GEMMs) is part of the
-                # last bucket: join before reporting it ready
-                torch.cuda.current_stream().wait_stream(self._side)
-                self._side_used = False
+            if not written:
+                self._write_input_grads(layer, names, dWx, dbias)
+            if layer == 0:
+                # side-stream work (overlapped weight GEMMs of the layers above) may share the
+                # remaining buckets: join before reporting them ready
+                self._join_side()
             if on_ready is not None:
                 on_ready(None if layer == 0 else s.layer_range(layer)[1])
-        if self._side_used:
-            torch.cuda.current_stream().wait_stream(self._side)
-            self._side_used = False
+        self._join_side()
         if pending:
             _release()
         extras = {"logits": logits, "loss": bufs["row_loss"]} if want_extras else None
@@ -855,6 +863,11 @@ class NativeBackend:
         if self._npart is None or self._npart.numel() < self.ops.opt_num_partials(n):
             self._npart = torch.empty(self.ops.opt_num_partials(n), dtype=f32, device=self.dev)
         self.ops.sumsq(dx_tok.contiguous(), self._npart, self.store.norm_slot_view())
+
+    def _join_side(self) -> None:
+        if self._side_used:
+            torch.cuda.current_stream().wait_stream(self._side)
+            self._side_used = False
 
     def _token_norm_gemm(self, dz0: torch.Tensor, wx0: torch.Tensor) -> None:
         """sum_tok ||dZ0_tok·W_x0ᵀ||² into the norm slot.  Default: the library GEMM to bf16
