@@ -83,3 +83,15 @@ def test_norm_slot_is_never_updated_and_outside_every_tensor():
     before = store.flat[store.norm_slot:].clone()
     TFAdam(store).step(1e-2)
     assert torch.equal(store.flat[store.norm_slot:], before)
+
+
+def test_cli_flag_reaches_the_model_config():
+    from distributed_char_rnn_amd.engine.trainer import build_model
+    from distributed_char_rnn_amd.utils.config import train_parser
+
+    for flag, want in (([], "tf"), (["--clip_norm", "dense"], "dense")):
+        args = train_parser().parse_args(["--rnn_size", "16", "--num_layers", "1"] + flag)
+        model = build_model(args, 7, "cpu")
+        assert model.store.cfg.clip_norm == want
+    with pytest.raises(SystemExit):
+        train_parser().parse_args(["--clip_norm", "bogus"])
