@@ -21,15 +21,16 @@ namespace dcr {
 
 constexpr int kOptThreads = 256;
 
-__device__ __forceinline__ float sq4(const float* g, int64_t i) {
+// sum of squares of the i-th 16-byte vector (4 fp32 or 8 bf16 elements)
+__device__ __forceinline__ float sqv(const float* g, int64_t i) {
   const float4 x = reinterpret_cast<const float4*>(g)[i];
   return x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
 }
-__device__ __forceinline__ float sq4(const bf16* g, int64_t i) {
-  const bf16x4 x = reinterpret_cast<const bf16x4*>(g)[i];
+__device__ __forceinline__ float sqv(const bf16* g, int64_t i) {
+  const bf16x8 x = reinterpret_cast<const bf16x8*>(g)[i];
   float a = 0.f;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < 8; ++k) {
     const float f = bf2f(x[k]);
     a += f * f;
   }
@@ -46,13 +47,14 @@ __global__ void __launch_bounds__(kOptThreads) sumsq_partials_kernel(
     const T* __restrict__ g, int64_t n, float* __restrict__ partials,
     const float* __restrict__ extra) {
   __shared__ float red[kOptThreads / 64];
+  constexpr int kVec = 16 / (int)sizeof(T);
   float acc = 0.f;
-  const int64_t n4 = n >> 2;
-  for (int64_t i = blockIdx.x * (int64_t)kOptThreads + threadIdx.x; i < n4;
+  const int64_t nv = n / kVec;
+  for (int64_t i = blockIdx.x * (int64_t)kOptThreads + threadIdx.x; i < nv;
        i += (int64_t)gridDim.x * kOptThreads)
-    acc += sq4(g, i);
+    acc += sqv(g, i);
   if (blockIdx.x == 0) {  // tail (+ the extra term, once)
-    for (int64_t i = (n4 << 2) + threadIdx.x; i < n; i += kOptThreads) acc += sq1(g, i);
+    for (int64_t i = nv * kVec + threadIdx.x; i < n; i += kOptThreads) acc += sq1(g, i);
     if (extra && threadIdx.x == 0) acc += extra[0];
   }
   const float t = block_sum<kOptThreads>(acc, red);
