@@ -45,6 +45,10 @@ struct FwdStepArgs {
   int gates_ld;
   int B, H;
   float forget_bias;
+  // no-GEMM mode (WT == nullptr; LSTM / RNN): the recurrent pre-activation h_{t-1}·W_h was
+  // computed elsewhere (library GEMM, large H) into zrec [B, zrec_ld] fp32; epilogue only
+  const float* zrec;
+  int zrec_ld;
 };
 
 struct BwdStepArgs {

@@ -181,6 +181,79 @@ void rnn_fwd_seq(int64_t cell, const at::Tensor& WT, const c10::optional<at::Ten
   }
 }
 
+// One epilogue-only LSTM step (large-H library path, native_backend._lstm_seq_lib): the
+// recurrent GEMM zrec = h_{t-1}·W_h ran as a library GEMM; this applies the cell forward
+// (zx = input projection + bias rows, or the [V, 4H] table gathered by ids).
+void lstm_step_ew_fwd(const at::Tensor& zrec, const at::Tensor& zx,
+                      const c10::optional<at::Tensor>& ids, const at::Tensor& cprev,
+                      at::Tensor& hout, const c10::optional<at::Tensor>& hout32, at::Tensor& cout,
+                      at::Tensor& gates, double forget_bias) {
+  check_seq(zrec, at::kFloat, "zrec");
+  check_seq(zx, at::kFloat, "zx");
+  check_seq(cprev, at::kFloat, "cprev");
+  check_seq(hout, at::kBFloat16, "hout");
+  check_seq(cout, at::kFloat, "cout");
+  check_seq(gates, at::kBFloat16, "gates");
+  check_opt(ids, at::kInt, "ids");
+  check_opt(hout32, at::kFloat, "hout32");
+  const int B = (int)hout.size(0), H = (int)hout.size(1);
+  TORCH_CHECK(H % 32 == 0 && zrec.numel() == (int64_t)B * 4 * H && gates.numel() == zrec.numel(),
+              "lstm_step_ew_fwd: shapes");
+  TORCH_CHECK(cprev.numel() == (int64_t)B * H && cout.numel() == cprev.numel(), "c shapes");
+  TORCH_CHECK(zx.size(-1) == 4 * H, "zx row must be 4H");
+  if (has(ids)) {
+    TORCH_CHECK(ids->numel() == B, "ids must be [B]");
+  } else {
+    TORCH_CHECK(zx.numel() == (int64_t)B * 4 * H, "zx must be [B, 4H]");
+  }
+  dcr::FwdStepArgs a{};
+  a.WT = nullptr;
+  a.zrec = ptr<float>(zrec);
+  a.zrec_ld = 4 * H;
+  a.zx = ptr<float>(zx);
+  a.ids = has(ids) ? ptr<int>(*ids) : nullptr;
+  a.zx_ld = 4 * H;
+  a.cprev = ptr<float>(cprev);
+  a.hout = ptr<bf16>(hout);
+  a.hout32 = optr<float>(hout32);
+  a.cout = ptr<float>(cout);
+  a.gates = ptr<bf16>(gates);
+  a.gates_ld = 4 * H;
+  a.B = B;
+  a.H = H;
+  a.forget_bias = (float)forget_bias;
+  dcr::launch_fwd_step(dcr::CELL_LSTM, a, cur_stream());
+}
+
+// One epilogue-only LSTM BPTT step: dh = dtop_t + dZ_{t+1}·W_hᵀ (library GEMM) -> dZ_t, dc.
+void lstm_step_ew_bwd(const at::Tensor& dh, const at::Tensor& gates, const at::Tensor& c,
+                      const at::Tensor& cprev, at::Tensor& dc, at::Tensor& dz_out) {
+  check_seq(dh, at::kFloat, "dh");
+  check_seq(gates, at::kBFloat16, "gates");
+  check_seq(c, at::kFloat, "c");
+  check_seq(cprev, at::kFloat, "cprev");
+  check_seq(dc, at::kFloat, "dc");
+  check_seq(dz_out, at::kBFloat16, "dz_out");
+  const int B = (int)dh.size(0), H = (int)dh.size(1);
+  TORCH_CHECK(H % 32 == 0 && gates.numel() == (int64_t)B * 4 * H &&
+                  dz_out.numel() == gates.numel(), "lstm_step_ew_bwd: shapes");
+  TORCH_CHECK(c.numel() == (int64_t)B * H && cprev.numel() == c.numel() && dc.numel() == c.numel(),
+              "lstm_step_ew_bwd: state shapes");
+  dcr::BwdStepArgs a{};
+  a.dz_next = nullptr;
+  a.dtop = ptr<float>(dh);
+  a.gates = ptr<bf16>(gates);
+  a.gates_ld = 4 * H;
+  a.c = ptr<float>(c);
+  a.cprev = ptr<float>(cprev);
+  a.dc = ptr<float>(dc);
+  a.dz_out = ptr<bf16>(dz_out);
+  a.dz_out_ld = 4 * H;
+  a.B = B;
+  a.H = H;
+  dcr::launch_bwd_step(dcr::CELL_LSTM, a, cur_stream());
+}
+
 void rnn_bwd_seq(int64_t cell, const at::Tensor& W, const c10::optional<at::Tensor>& W2,
                  const at::Tensor& dtop, at::Tensor& dz, const c10::optional<at::Tensor>& dzx,
                  const c10::optional<at::Tensor>& gates, const c10::optional<at::Tensor>& pre,
@@ -973,6 +1046,12 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor(e!) partials, Tensor(f!) norm_out, float lr_t, float b1, float b2, float eps, "
       "float clip, float gscale=1.0, int n_norm=-1, Tensor? extra_sq=None) -> ()");
   m.def("sumsq(Tensor x, Tensor(a!) partials, Tensor(b!) out) -> ()");
+  m.def(
+      "lstm_step_ew_fwd(Tensor zrec, Tensor zx, Tensor? ids, Tensor cprev, Tensor(a!) hout, "
+      "Tensor(b!)? hout32, Tensor(c!) cout, Tensor(d!) gates, float forget_bias) -> ()");
+  m.def(
+      "lstm_step_ew_bwd(Tensor dh, Tensor gates, Tensor c, Tensor cprev, Tensor(a!) dc, "
+      "Tensor(b!) dz_out) -> ()");
   m.def("tok_norm(Tensor dz, Tensor w, Tensor(a!) partials, Tensor(b!) out) -> ()");
   m.def("tok_norm_supported(int N, int H, int K) -> bool",
         [](int64_t N, int64_t H, int64_t K) -> bool {
@@ -1092,6 +1171,8 @@ TORCH_LIBRARY(dcr, m) {
 TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("global_norm", &global_norm);
   m.impl("sumsq", &sumsq);
+  m.impl("lstm_step_ew_fwd", &lstm_step_ew_fwd);
+  m.impl("lstm_step_ew_bwd", &lstm_step_ew_bwd);
   m.impl("tok_norm", &tok_norm);
   m.impl("adam_clip", &adam_clip);
   m.impl("rnn_fwd_seq", &rnn_fwd_seq);

@@ -150,7 +150,7 @@ __global__ void __launch_bounds__(256) fwd_step_kernel(FwdStepArgs a) {
   for (int g = 0; g < G; ++g) arow[g] = g * H + ub + (lane & 15);
 #pragma unroll
   for (int j = 0; j < NBT; ++j) brow[j] = min(bgrp + 16 * j + (lane & 15), B - 1);
-  tile_gemm<G, NBT>(acc, a.WT, arow, H, a.hop, brow, H, H, lane, w, part);
+  if (a.WT) tile_gemm<G, NBT>(acc, a.WT, arow, H, a.hop, brow, H, H, lane, w, part);
   if (w >= NBT) return;
   const int b0 = bgrp + 16 * w;
 
@@ -158,6 +158,13 @@ __global__ void __launch_bounds__(256) fwd_step_kernel(FwdStepArgs a) {
   if (b >= B) return;
   const int u0 = ub + 4 * (lane >> 4);
   const size_t bh = (size_t)b * H + u0;
+  if (!a.WT) {  // epilogue-only step: the recurrent GEMM ran on the library path
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const float4 v = ld4f(a.zrec + (size_t)b * a.zrec_ld + (size_t)g * H + u0);
+      acc[g] = f32x4{v.x, v.y, v.z, v.w};
+    }
+  }
   const float* zrow = (a.ids ? a.zx + (size_t)a.ids[b] * a.zx_ld : a.zx + (size_t)b * a.zx_ld) +
                       a.zx_off + u0;
   float zx[G][4];
@@ -421,9 +428,12 @@ static inline int step_blocks(int B, int H, int nbt) {
   return ((B + 16 * nbt - 1) / (16 * nbt)) * (H / 16);
 }
 
+// epilogue-only steps (no GEMM): every wave of a workgroup takes a batch tile
+static int ew_nbt(int G, int B) { return (G * 4 <= 16 && B >= 64) ? 4 : (G * 2 <= 16 && B >= 32) ? 2 : 1; }
+
 template <int CELL>
 static void fwd_launch(const FwdStepArgs& a, hipStream_t s) {
-  const int nbt = step_nbt(CellG<CELL>::G, a.B, a.H);
+  const int nbt = a.WT ? step_nbt(CellG<CELL>::G, a.B, a.H) : ew_nbt(CellG<CELL>::G, a.B);
   const int nb = step_blocks(a.B, a.H, nbt);
   if constexpr (CellG<CELL>::G * 4 <= 16) {
     if (nbt == 4) { fwd_step_kernel<CELL, 4><<<nb, 256, 0, s>>>(a); return; }
@@ -436,7 +446,7 @@ static void fwd_launch(const FwdStepArgs& a, hipStream_t s) {
 
 template <int CELL>
 static void bwd_launch(const BwdStepArgs& a, hipStream_t s) {
-  const int nbt = step_nbt(1, a.B, a.H);
+  const int nbt = a.dz_next ? step_nbt(1, a.B, a.H) : ew_nbt(1, a.B);
   const int nb = step_blocks(a.B, a.H, nbt);
   if (nbt == 4) bwd_step_kernel<CELL, 4><<<nb, 256, 0, s>>>(a);
   else if (nbt == 2) bwd_step_kernel<CELL, 2><<<nb, 256, 0, s>>>(a);

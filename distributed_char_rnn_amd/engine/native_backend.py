@@ -192,6 +192,9 @@ class NativeBackend:
         self._npart: Optional[torch.Tensor] = None
         self._tpart: Optional[torch.Tensor] = None
         self.tok_norm_fused = os.environ.get("DCR_TOK_NORM", "library") == "fused"
+        self.libstep = os.environ.get("DCR_LIBSTEP", "auto")
+        self._addmm2d: Optional[bool] = None
+        self._lib_graphs: Dict[tuple, tuple] = {}
         self.gen = torch.Generator(device=self.dev)
         self.gen.manual_seed(int(seed))
 
@@ -565,6 +568,8 @@ class NativeBackend:
                                          lb.gates, None, bufs["cnt"][layer], self.err,
                                          self.spin_limit, cnt_zeroed=True,
                                          ring0=gr[0] if gr else None, ring1=gr[1] if gr else None)
+            elif self._lib_step("fwd", B):
+                self._lstm_fwd_lib(lw, lb, zx, ids_arg, bufs)
             else:
                 self.ops.rnn_fwd_seq(self.cell, lw.WhT, lw.WT2, zx, ids_arg, lb.hbuf, lb.h32,
                                      lb.cbuf, lb.gates, lb.pre, lb.aux, lb.rh, lb.hlast32,
@@ -712,6 +717,8 @@ class NativeBackend:
                                          ring1=gr[2] if gr else None)
                 if layer == 0 and user_ready is not None:
                     on_ready = _release()
+            elif self._lib_step("bwd", B):
+                self._lstm_bwd_lib(lw, lb, dtop, bufs)
             else:
                 self.ops.rnn_bwd_seq(self.cell, lw.Wh, lw.W2, dtop, lb.dz, lb.dzx, lb.gates,
                                      lb.pre, lb.aux, zx_nas, lb.cbuf, lb.h32, lb.hbuf, bufs["dc"],
@@ -863,6 +870,115 @@ class NativeBackend:
         if self._npart is None or self._npart.numel() < self.ops.opt_num_partials(n):
             self._npart = torch.empty(self.ops.opt_num_partials(n), dtype=f32, device=self.dev)
         self.ops.sumsq(dx_tok.contiguous(), self._npart, self.store.norm_slot_view())
+
+    # ------------------------------------------------------------------ large-H library steps
+    def _lib_step(self, direction: str, B: int) -> bool:
+        """Per-time-step recurrent GEMM on the library path + epilogue-only cell kernel, for
+        LSTM with H > 1024 (no weights-resident kernel there).  The fused per-step kernels
+        re-read the whole step payload once per 16-unit block (128 x at H = 2048), so their
+        step time grows linearly with the batch; a library GEMM reads W_h once per step
+        (scripts/bench_step_gemms.py: 17-25 us for B = 64-256).  auto: BPTT always, forward
+        from B >= 128 (at B = 64 the fused forward step, 16.7 us, beats GEMM + epilogue).
+        DCR_LIBSTEP=0 / 1 forces either way."""
+        if self.cfg.model != "lstm":
+            return False
+        if self.libstep == "0":
+            return False
+        if self.libstep == "1":
+            return True
+        if self.H <= 1024:
+            return False
+        return direction == "bwd" or B >= 128
+
+    def _lstm_fwd_lib(self, lw, lb, zx, ids, bufs) -> None:
+        T, B = lb.gates.shape[0], lb.gates.shape[1]
+        zrec = bufs.get("zrec")
+        if zrec is None:
+            zrec = bufs["zrec"] = torch.empty(B, self.GW, dtype=f32, device=self.dev)
+
+        def body(zx, ids):
+            for t in range(T):
+                torch.mm(lb.hbuf[t], lw.Wh, out_dtype=f32, out=zrec)
+                self.ops.lstm_step_ew_fwd(zrec, zx if ids is not None else zx[t],
+                                          ids[t] if ids is not None else None, lb.cbuf[t],
+                                          lb.hbuf[t + 1], lb.hlast32 if t == T - 1 else None,
+                                          lb.cbuf[t + 1], lb.gates[t], FORGET_BIAS)
+
+        self._run_lib_loop(("fwd", id(lb)), body, zx, ids,
+                           a_static=lb.zx is not None and zx.data_ptr() == lb.zx.data_ptr())
+
+    def _lstm_bwd_lib(self, lw, lb, dtop, bufs) -> None:
+        T, B = dtop.shape[0], dtop.shape[1]
+        dh = bufs.get("dhrec")
+        if dh is None:
+            dh = bufs["dhrec"] = torch.empty(B, self.H, dtype=f32, device=self.dev)
+        dc = bufs["dc"]
+        WhT = lw.Wh.t()
+
+        def body(dtop, _unused):
+            dc.zero_()
+            for t in reversed(range(T)):
+                if t == T - 1:
+                    src = dtop[t]
+                else:  # dh = dtop_t + dZ_{t+1}·W_hᵀ (the add in the GEMM's epilogue if supported)
+                    self._addmm_rows(dtop[t], lb.dz[t + 1], WhT, dh)
+                    src = dh
+                self.ops.lstm_step_ew_bwd(src, lb.gates[t], lb.cbuf[t + 1], lb.cbuf[t], dc,
+                                          lb.dz[t])
+
+        static = any(buf is not None and dtop.data_ptr() == buf.data_ptr()
+                     for buf in (bufs["dtop"], bufs["dx"]))
+        self._run_lib_loop(("bwd", id(lb)), body, dtop, None, a_static=static)
+
+    def _run_lib_loop(self, key, body, a, b, a_static: bool = False) -> None:
+        """Run a T-step library loop (2 launches per step) as a replayed hipGraph: eager,
+        the per-step host launch cost (~15 us) is as long as the GPU's step at B = 64.  The
+        graph is captured on the first call with static copies of the loop's varying inputs
+        (a: zx / table / dtop, b: ids) and replayed afterwards; everything else it touches
+        (h, c, gates, dZ buffers, the bf16 weights refreshed in place) is persistent.
+        ``a_static``: ``a`` is itself a persistent buffer (dense zx, the dtop / dx buffers),
+        captured directly instead of through a copy.  DCR_LIB_GRAPH=0 runs eagerly."""
+        if os.environ.get("DCR_LIB_GRAPH", "1") == "0":
+            body(a, b)
+            return
+        ent = self._lib_graphs.get(key)
+        if ent is None or ent[1].shape != a.shape or (b is not None and ent[2].shape != b.shape):
+            sa = a if a_static else a.clone()
+            sb = b.clone() if b is not None else None
+            body(sa, sb)  # warm-up outside capture (library handles, workspaces)
+            g = torch.cuda.CUDAGraph()
+            try:
+                s = torch.cuda.Stream(device=self.dev)
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    with torch.cuda.graph(g, stream=s):
+                        body(sa, sb)
+                torch.cuda.current_stream().wait_stream(s)
+            except RuntimeError:
+                self._lib_graphs[key] = ("eager", None, None)
+                body(a, b)
+                return
+            self._lib_graphs[key] = ent = (g, sa, sb)
+        if ent[0] == "eager":
+            body(a, b)
+            return
+        g, sa, sb = ent
+        if sa.data_ptr() != a.data_ptr():
+            sa.copy_(a)
+        if sb is not None and sb.data_ptr() != b.data_ptr():
+            sb.copy_(b)
+        g.replay()
+
+    def _addmm_rows(self, c, a, b, out) -> None:
+        if self._addmm2d is not False:
+            try:
+                torch.addmm(c, a, b, out_dtype=f32, out=out)
+                self._addmm2d = True
+                return
+            except (RuntimeError, TypeError):
+                self._addmm2d = False
+        torch.mm(a, b, out_dtype=f32, out=out)
+        out.add_(c)
 
     def _join_side(self) -> None:
         if self._side_used:
