@@ -17,7 +17,6 @@ from __future__ import annotations
 
 import argparse
 import json
-import os
 import sys
 import time
 
@@ -149,7 +148,8 @@ def main(argv=None) -> int:
             "metric": METRIC, "value": cps, "unit": "chars/sec", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16" if device.type == "cuda" else "fp32", "data": "synthetic (Shakespeare-unigram token stream, random-init weights)",
+            "dtype": "bf16" if device.type == "cuda" else "fp32",
+            "data": "synthetic (Shakespeare-unigram token stream, random-init weights)",
             "config": {"model": f"{a.layers}-layer {a.model.upper()}-{a.hidden} (vocab {a.vocab})",
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": T,
                        "parallelism": f"dp{world}"},

@@ -29,7 +29,7 @@ boundary so fp32 and bf16 views are 16-byte aligned for vector loads.
 from __future__ import annotations
 
 import math
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
 import torch

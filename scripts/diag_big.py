@@ -1,6 +1,5 @@
 """Diagnostic: large-H persistent forward vs per-step kernels vs fp32 reference at long T."""
 import os
-import sys
 
 import torch
 

@@ -1,4 +1,3 @@
-import torch
 from distributed_char_rnn_amd.ops import native
 o = native.ops()
 for H, B in [(128, 32), (512, 256), (384, 64), (256, 96)]:

@@ -1,7 +1,5 @@
 """Persistent weights-resident LSTM kernels (csrc/lstm_persist.hip) vs the fp32 autograd oracle
 and vs the per-step kernels; also checks that no hand-off ever timed out."""
-import os
-
 import pytest
 import torch
 
