@@ -225,23 +225,28 @@ void lstm_step_ew_fwd(const at::Tensor& zrec, const at::Tensor& zx,
   dcr::launch_fwd_step(dcr::CELL_LSTM, a, cur_stream());
 }
 
-// One epilogue-only LSTM BPTT step: dh = dtop_t + dZ_{t+1}·W_hᵀ (library GEMM) -> dZ_t, dc.
-void lstm_step_ew_bwd(const at::Tensor& dh, const at::Tensor& gates, const at::Tensor& c,
-                      const at::Tensor& cprev, at::Tensor& dc, at::Tensor& dz_out) {
-  check_seq(dh, at::kFloat, "dh");
+// One epilogue-only LSTM BPTT step: dh = dtop_t + dhrec (dhrec = dZ_{t+1}·W_hᵀ from a library
+// GEMM, absent at the last step) -> dZ_t, dc.
+void lstm_step_ew_bwd(const at::Tensor& dtop, const c10::optional<at::Tensor>& dhrec,
+                      const at::Tensor& gates, const at::Tensor& c, const at::Tensor& cprev,
+                      at::Tensor& dc, at::Tensor& dz_out) {
+  check_seq(dtop, at::kFloat, "dtop");
+  check_opt(dhrec, at::kFloat, "dhrec");
+  if (has(dhrec)) TORCH_CHECK(dhrec->numel() == dtop.numel(), "dhrec must be [B, H]");
   check_seq(gates, at::kBFloat16, "gates");
   check_seq(c, at::kFloat, "c");
   check_seq(cprev, at::kFloat, "cprev");
   check_seq(dc, at::kFloat, "dc");
   check_seq(dz_out, at::kBFloat16, "dz_out");
-  const int B = (int)dh.size(0), H = (int)dh.size(1);
+  const int B = (int)dtop.size(0), H = (int)dtop.size(1);
   TORCH_CHECK(H % 32 == 0 && gates.numel() == (int64_t)B * 4 * H &&
                   dz_out.numel() == gates.numel(), "lstm_step_ew_bwd: shapes");
   TORCH_CHECK(c.numel() == (int64_t)B * H && cprev.numel() == c.numel() && dc.numel() == c.numel(),
               "lstm_step_ew_bwd: state shapes");
   dcr::BwdStepArgs a{};
   a.dz_next = nullptr;
-  a.dtop = ptr<float>(dh);
+  a.dtop = ptr<float>(dtop);
+  a.partial = optr<float>(dhrec);
   a.gates = ptr<bf16>(gates);
   a.gates_ld = 4 * H;
   a.c = ptr<float>(c);
@@ -1050,8 +1055,8 @@ TORCH_LIBRARY(dcr, m) {
       "lstm_step_ew_fwd(Tensor zrec, Tensor zx, Tensor? ids, Tensor cprev, Tensor(a!) hout, "
       "Tensor(b!)? hout32, Tensor(c!) cout, Tensor(d!) gates, float forget_bias) -> ()");
   m.def(
-      "lstm_step_ew_bwd(Tensor dh, Tensor gates, Tensor c, Tensor cprev, Tensor(a!) dc, "
-      "Tensor(b!) dz_out) -> ()");
+      "lstm_step_ew_bwd(Tensor dtop, Tensor? dhrec, Tensor gates, Tensor c, Tensor cprev, "
+      "Tensor(a!) dc, Tensor(b!) dz_out) -> ()");
   m.def("tok_norm(Tensor dz, Tensor w, Tensor(a!) partials, Tensor(b!) out) -> ()");
   m.def("tok_norm_supported(int N, int H, int K) -> bool",
         [](int64_t N, int64_t H, int64_t K) -> bool {

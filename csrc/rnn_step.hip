@@ -280,6 +280,10 @@ __global__ void __launch_bounds__(256) bwd_step_kernel(BwdStepArgs a) {
   if (a.dtop) f4arr(ld4f(a.dtop + bh), dtop);
 
   if constexpr (CELL == CELL_LSTM) {
+    if (!a.dz_next && a.partial) {  // epilogue-only step: recurrent dh from a library GEMM
+      const float4 v = ld4f(a.partial + bh);
+      acc[0] = f32x4{v.x, v.y, v.z, v.w};
+    }
     float gi[4], gj[4], gf[4], go[4], c[4], cp[4], dc[4];
     const bf16* gp = a.gates + (size_t)b * a.gates_ld + u0;
     ld4bf(gp, gi); ld4bf(gp + H, gj); ld4bf(gp + 2 * H, gf); ld4bf(gp + 3 * H, go);

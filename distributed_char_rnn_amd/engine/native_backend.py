@@ -193,7 +193,6 @@ class NativeBackend:
         self._tpart: Optional[torch.Tensor] = None
         self.tok_norm_fused = os.environ.get("DCR_TOK_NORM", "library") == "fused"
         self.libstep = os.environ.get("DCR_LIBSTEP", "auto")
-        self._addmm2d: Optional[bool] = None
         self._lib_graphs: Dict[tuple, tuple] = {}
         self.gen = torch.Generator(device=self.dev)
         self.gen.manual_seed(int(seed))
@@ -918,13 +917,12 @@ class NativeBackend:
         def body(dtop, _unused):
             dc.zero_()
             for t in reversed(range(T)):
-                if t == T - 1:
-                    src = dtop[t]
-                else:  # dh = dtop_t + dZ_{t+1}·W_hᵀ (the add in the GEMM's epilogue if supported)
-                    self._addmm_rows(dtop[t], lb.dz[t + 1], WhT, dh)
-                    src = dh
-                self.ops.lstm_step_ew_bwd(src, lb.gates[t], lb.cbuf[t + 1], lb.cbuf[t], dc,
-                                          lb.dz[t])
+                # dh = dtop_t + dZ_{t+1}·W_hᵀ: the GEMM writes the recurrent part, the cell
+                # kernel adds dtop_t (an addmm with a 2-D input costs a separate copy launch)
+                if t < T - 1:
+                    torch.mm(lb.dz[t + 1], WhT, out_dtype=f32, out=dh)
+                self.ops.lstm_step_ew_bwd(dtop[t], dh if t < T - 1 else None, lb.gates[t],
+                                          lb.cbuf[t + 1], lb.cbuf[t], dc, lb.dz[t])
 
         static = any(buf is not None and dtop.data_ptr() == buf.data_ptr()
                      for buf in (bufs["dtop"], bufs["dx"]))
@@ -968,17 +966,6 @@ class NativeBackend:
         if sb is not None and sb.data_ptr() != b.data_ptr():
             sb.copy_(b)
         g.replay()
-
-    def _addmm_rows(self, c, a, b, out) -> None:
-        if self._addmm2d is not False:
-            try:
-                torch.addmm(c, a, b, out_dtype=f32, out=out)
-                self._addmm2d = True
-                return
-            except (RuntimeError, TypeError):
-                self._addmm2d = False
-        torch.mm(a, b, out_dtype=f32, out=out)
-        out.add_(c)
 
     def _join_side(self) -> None:
         if self._side_used:
