@@ -193,7 +193,6 @@ class NativeBackend:
         self._tpart: Optional[torch.Tensor] = None
         self.tok_norm_fused = os.environ.get("DCR_TOK_NORM", "library") == "fused"
         self.libstep = os.environ.get("DCR_LIBSTEP", "auto")
-        self._lib_graphs: Dict[tuple, tuple] = {}
         self.gen = torch.Generator(device=self.dev)
         self.gen.manual_seed(int(seed))
 
@@ -903,7 +902,7 @@ class NativeBackend:
                                           lb.hbuf[t + 1], lb.hlast32 if t == T - 1 else None,
                                           lb.cbuf[t + 1], lb.gates[t], FORGET_BIAS)
 
-        self._run_lib_loop(("fwd", id(lb)), body, zx, ids,
+        self._run_lib_loop(bufs, ("fwd", id(lb)), body, zx, ids,
                            a_static=lb.zx is not None and zx.data_ptr() == lb.zx.data_ptr())
 
     def _lstm_bwd_lib(self, lw, lb, dtop, bufs) -> None:
@@ -926,9 +925,9 @@ class NativeBackend:
 
         static = any(buf is not None and dtop.data_ptr() == buf.data_ptr()
                      for buf in (bufs["dtop"], bufs["dx"]))
-        self._run_lib_loop(("bwd", id(lb)), body, dtop, None, a_static=static)
+        self._run_lib_loop(bufs, ("bwd", id(lb)), body, dtop, None, a_static=static)
 
-    def _run_lib_loop(self, key, body, a, b, a_static: bool = False) -> None:
+    def _run_lib_loop(self, bufs, key, body, a, b, a_static: bool = False) -> None:
         """Run a T-step library loop (2 launches per step) as a replayed hipGraph: eager,
         the per-step host launch cost (~15 us) is as long as the GPU's step at B = 64.  The
         graph is captured on the first call with static copies of the loop's varying inputs
@@ -939,7 +938,9 @@ class NativeBackend:
         if os.environ.get("DCR_LIB_GRAPH", "1") == "0":
             body(a, b)
             return
-        ent = self._lib_graphs.get(key)
+        # the graphs live with the buffers they were captured on (and die with them)
+        graphs = bufs.setdefault("lib_graphs", {})
+        ent = graphs.get(key)
         if ent is None or ent[1].shape != a.shape or (b is not None and ent[2].shape != b.shape):
             sa = a if a_static else a.clone()
             sb = b.clone() if b is not None else None
@@ -953,10 +954,10 @@ class NativeBackend:
                         body(sa, sb)
                 torch.cuda.current_stream().wait_stream(s)
             except RuntimeError:
-                self._lib_graphs[key] = ("eager", None, None)
+                graphs[key] = ("eager", None, None)
                 body(a, b)
                 return
-            self._lib_graphs[key] = ent = (g, sa, sb)
+            graphs[key] = ent = (g, sa, sb)
         if ent[0] == "eager":
             body(a, b)
             return
