@@ -49,6 +49,7 @@ struct FwdStepArgs {
   // computed elsewhere (library GEMM, large H) into zrec [B, zrec_ld] fp32; epilogue only
   const float* zrec;
   int zrec_ld;
+  int nsplit;            // zrec holds nsplit split-K partial slabs of [B, zrec_ld] (0 = 1)
 };
 
 struct BwdStepArgs {
@@ -71,7 +72,14 @@ struct BwdStepArgs {
   bf16* dzx_out;         // NAS: input-branch dZx
   int dz_out_ld, gates_ld;
   int B, H;
+  int nsplit;            // LSTM epilogue-only: `partial` = nsplit [B, H] slabs (0 = 1)
 };
+
+// ---- step_gemm.hip ----------------------------------------------------------------------
+bool step_gemm_supported(int B, int N, int K);
+int step_gemm_splits(int B, int N, int K);
+void launch_step_gemm(const bf16* X, const bf16* W, int B, int N, int K, int splits, float* part,
+                      hipStream_t stream);
 
 void launch_fwd_step(int cell, const FwdStepArgs& a, hipStream_t s);
 void launch_bwd_step(int cell, const BwdStepArgs& a, hipStream_t s);

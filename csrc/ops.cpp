@@ -197,8 +197,8 @@ void lstm_step_ew_fwd(const at::Tensor& zrec, const at::Tensor& zx,
   check_opt(ids, at::kInt, "ids");
   check_opt(hout32, at::kFloat, "hout32");
   const int B = (int)hout.size(0), H = (int)hout.size(1);
-  TORCH_CHECK(H % 32 == 0 && zrec.numel() == (int64_t)B * 4 * H && gates.numel() == zrec.numel(),
-              "lstm_step_ew_fwd: shapes");
+  TORCH_CHECK(H % 32 == 0 && zrec.numel() % ((int64_t)B * 4 * H) == 0 &&
+                  gates.numel() == (int64_t)B * 4 * H, "lstm_step_ew_fwd: shapes");
   TORCH_CHECK(cprev.numel() == (int64_t)B * H && cout.numel() == cprev.numel(), "c shapes");
   TORCH_CHECK(zx.size(-1) == 4 * H, "zx row must be 4H");
   if (has(ids)) {
@@ -210,6 +210,7 @@ void lstm_step_ew_fwd(const at::Tensor& zrec, const at::Tensor& zx,
   a.WT = nullptr;
   a.zrec = ptr<float>(zrec);
   a.zrec_ld = 4 * H;
+  a.nsplit = (int)(zrec.numel() / ((int64_t)B * 4 * H));  // split-K slabs (step_gemm)
   a.zx = ptr<float>(zx);
   a.ids = has(ids) ? ptr<int>(*ids) : nullptr;
   a.zx_ld = 4 * H;
@@ -232,7 +233,9 @@ void lstm_step_ew_bwd(const at::Tensor& dtop, const c10::optional<at::Tensor>& d
                       at::Tensor& dc, at::Tensor& dz_out) {
   check_seq(dtop, at::kFloat, "dtop");
   check_opt(dhrec, at::kFloat, "dhrec");
-  if (has(dhrec)) TORCH_CHECK(dhrec->numel() == dtop.numel(), "dhrec must be [B, H]");
+  if (has(dhrec)) {
+    TORCH_CHECK(dhrec->numel() % dtop.numel() == 0, "dhrec must be [S, B, H]");
+  }
   check_seq(gates, at::kBFloat16, "gates");
   check_seq(c, at::kFloat, "c");
   check_seq(cprev, at::kFloat, "cprev");
@@ -247,6 +250,7 @@ void lstm_step_ew_bwd(const at::Tensor& dtop, const c10::optional<at::Tensor>& d
   a.dz_next = nullptr;
   a.dtop = ptr<float>(dtop);
   a.partial = optr<float>(dhrec);
+  a.nsplit = has(dhrec) ? (int)(dhrec->numel() / dtop.numel()) : 0;
   a.gates = ptr<bf16>(gates);
   a.gates_ld = 4 * H;
   a.c = ptr<float>(c);
@@ -257,6 +261,20 @@ void lstm_step_ew_bwd(const at::Tensor& dtop, const c10::optional<at::Tensor>& d
   a.B = B;
   a.H = H;
   dcr::launch_bwd_step(dcr::CELL_LSTM, a, cur_stream());
+}
+
+// partial[z] = X[:, z-th K slice] · W[:, same]ᵀ for z < S (step_gemm.hip); part [S, B, N] fp32
+void step_gemm(const at::Tensor& X, const at::Tensor& W, at::Tensor& part) {
+  check_seq(X, at::kBFloat16, "X");
+  check_seq(W, at::kBFloat16, "W");
+  check_seq(part, at::kFloat, "part");
+  TORCH_CHECK(X.dim() == 2 && W.dim() == 2 && X.size(1) == W.size(1), "step_gemm: shapes");
+  const int B = (int)X.size(0), K = (int)X.size(1), N = (int)W.size(0);
+  TORCH_CHECK(dcr::step_gemm_supported(B, N, K), "step_gemm: unsupported shape");
+  TORCH_CHECK(part.numel() % ((int64_t)B * N) == 0, "part must be [S, B, N]");
+  const int S = (int)(part.numel() / ((int64_t)B * N));
+  TORCH_CHECK(S >= 1 && K % (32 * S) == 0, "step_gemm: K must split into S 32-multiples");
+  dcr::launch_step_gemm(ptr<bf16>(X), ptr<bf16>(W), B, N, K, S, ptr<float>(part), cur_stream());
 }
 
 void rnn_bwd_seq(int64_t cell, const at::Tensor& W, const c10::optional<at::Tensor>& W2,
@@ -1051,6 +1069,12 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor(e!) partials, Tensor(f!) norm_out, float lr_t, float b1, float b2, float eps, "
       "float clip, float gscale=1.0, int n_norm=-1, Tensor? extra_sq=None) -> ()");
   m.def("sumsq(Tensor x, Tensor(a!) partials, Tensor(b!) out) -> ()");
+  m.def("step_gemm(Tensor X, Tensor W, Tensor(a!) part) -> ()");
+  m.def("step_gemm_splits(int B, int N, int K) -> int",
+        [](int64_t B, int64_t N, int64_t K) -> int64_t {
+          return dcr::step_gemm_supported((int)B, (int)N, (int)K)
+                     ? dcr::step_gemm_splits((int)B, (int)N, (int)K) : 0;
+        });
   m.def(
       "lstm_step_ew_fwd(Tensor zrec, Tensor zx, Tensor? ids, Tensor cprev, Tensor(a!) hout, "
       "Tensor(b!)? hout32, Tensor(c!) cout, Tensor(d!) gates, float forget_bias) -> ()");
@@ -1176,6 +1200,7 @@ TORCH_LIBRARY(dcr, m) {
 TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("global_norm", &global_norm);
   m.impl("sumsq", &sumsq);
+  m.impl("step_gemm", &step_gemm);
   m.impl("lstm_step_ew_fwd", &lstm_step_ew_fwd);
   m.impl("lstm_step_ew_bwd", &lstm_step_ew_bwd);
   m.impl("tok_norm", &tok_norm);

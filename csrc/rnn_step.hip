@@ -158,11 +158,17 @@ __global__ void __launch_bounds__(256) fwd_step_kernel(FwdStepArgs a) {
   if (b >= B) return;
   const int u0 = ub + 4 * (lane >> 4);
   const size_t bh = (size_t)b * H + u0;
-  if (!a.WT) {  // epilogue-only step: the recurrent GEMM ran on the library path
+  if (!a.WT) {  // epilogue-only step: the recurrent GEMM ran elsewhere (split-K slabs)
+    const int ns = a.nsplit > 0 ? a.nsplit : 1;
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const float4 v = ld4f(a.zrec + (size_t)b * a.zrec_ld + (size_t)g * H + u0);
-      acc[g] = f32x4{v.x, v.y, v.z, v.w};
+    for (int g = 0; g < G; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int sp = 0; sp < ns; ++sp) {
+      const float* zr = a.zrec + (size_t)sp * B * a.zrec_ld + (size_t)b * a.zrec_ld + u0;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const float4 v = ld4f(zr + (size_t)g * H);
+        acc[g] += f32x4{v.x, v.y, v.z, v.w};
+      }
     }
   }
   const float* zrow = (a.ids ? a.zx + (size_t)a.ids[b] * a.zx_ld : a.zx + (size_t)b * a.zx_ld) +
@@ -280,9 +286,12 @@ __global__ void __launch_bounds__(256) bwd_step_kernel(BwdStepArgs a) {
   if (a.dtop) f4arr(ld4f(a.dtop + bh), dtop);
 
   if constexpr (CELL == CELL_LSTM) {
-    if (!a.dz_next && a.partial) {  // epilogue-only step: recurrent dh from a library GEMM
-      const float4 v = ld4f(a.partial + bh);
-      acc[0] = f32x4{v.x, v.y, v.z, v.w};
+    if (!a.dz_next && a.partial) {  // epilogue-only step: recurrent dh (split-K slabs)
+      const int ns = a.nsplit > 0 ? a.nsplit : 1;
+      for (int sp = 0; sp < ns; ++sp) {
+        const float4 v = ld4f(a.partial + (size_t)sp * B * H + bh);
+        acc[0] += f32x4{v.x, v.y, v.z, v.w};
+      }
     }
     float gi[4], gj[4], gf[4], go[4], c[4], cp[4], dc[4];
     const bf16* gp = a.gates + (size_t)b * a.gates_ld + u0;

@@ -193,6 +193,10 @@ class NativeBackend:
         self._tpart: Optional[torch.Tensor] = None
         self.tok_norm_fused = os.environ.get("DCR_TOK_NORM", "library") == "fused"
         self.libstep = os.environ.get("DCR_LIBSTEP", "auto")
+        # per-step recurrent GEMM of the library-step path: "library" (hipBLASLt) or "native"
+        # (csrc/step_gemm.hip split-K; correct, but its fp32 split slabs cost more than they
+        # save: LSTM-2048 108.5 vs 96.0 ms at B = 64, 216 vs 199 at B = 256)
+        self.step_gemm_mode = os.environ.get("DCR_STEP_GEMM", "library")
         self.gen = torch.Generator(device=self.dev)
         self.gen.manual_seed(int(seed))
 
@@ -890,13 +894,17 @@ class NativeBackend:
 
     def _lstm_fwd_lib(self, lw, lb, zx, ids, bufs) -> None:
         T, B = lb.gates.shape[0], lb.gates.shape[1]
+        S = self._step_gemm_splits(B, self.GW, self.H)
         zrec = bufs.get("zrec")
         if zrec is None:
-            zrec = bufs["zrec"] = torch.empty(B, self.GW, dtype=f32, device=self.dev)
+            zrec = bufs["zrec"] = torch.empty(max(S, 1), B, self.GW, dtype=f32, device=self.dev)
 
         def body(zx, ids):
             for t in range(T):
-                torch.mm(lb.hbuf[t], lw.Wh, out_dtype=f32, out=zrec)
+                if S:  # split-K step GEMM (step_gemm.hip) into S slabs, summed by the cell kernel
+                    self.ops.step_gemm(lb.hbuf[t], lw.WhT, zrec)
+                else:
+                    torch.mm(lb.hbuf[t], lw.Wh, out_dtype=f32, out=zrec[0])
                 self.ops.lstm_step_ew_fwd(zrec, zx if ids is not None else zx[t],
                                           ids[t] if ids is not None else None, lb.cbuf[t],
                                           lb.hbuf[t + 1], lb.hlast32 if t == T - 1 else None,
@@ -907,9 +915,10 @@ class NativeBackend:
 
     def _lstm_bwd_lib(self, lw, lb, dtop, bufs) -> None:
         T, B = dtop.shape[0], dtop.shape[1]
+        S = self._step_gemm_splits(B, self.H, self.GW)
         dh = bufs.get("dhrec")
         if dh is None:
-            dh = bufs["dhrec"] = torch.empty(B, self.H, dtype=f32, device=self.dev)
+            dh = bufs["dhrec"] = torch.empty(max(S, 1), B, self.H, dtype=f32, device=self.dev)
         dc = bufs["dc"]
         WhT = lw.Wh.t()
 
@@ -918,8 +927,10 @@ class NativeBackend:
             for t in reversed(range(T)):
                 # dh = dtop_t + dZ_{t+1}·W_hᵀ: the GEMM writes the recurrent part, the cell
                 # kernel adds dtop_t (an addmm with a 2-D input costs a separate copy launch)
-                if t < T - 1:
-                    torch.mm(lb.dz[t + 1], WhT, out_dtype=f32, out=dh)
+                if t < T - 1 and S:
+                    self.ops.step_gemm(lb.dz[t + 1], lw.Wh, dh)
+                elif t < T - 1:
+                    torch.mm(lb.dz[t + 1], WhT, out_dtype=f32, out=dh[0])
                 self.ops.lstm_step_ew_bwd(dtop[t], dh if t < T - 1 else None, lb.gates[t],
                                           lb.cbuf[t + 1], lb.cbuf[t], dc, lb.dz[t])
 
@@ -967,6 +978,14 @@ class NativeBackend:
         if sb is not None and sb.data_ptr() != b.data_ptr():
             sb.copy_(b)
         g.replay()
+
+    def _step_gemm_splits(self, B: int, N: int, K: int) -> int:
+        """Split count of the native split-K step GEMM (csrc/step_gemm.hip) for an [B, K] x
+        [N, K]ᵀ step product, or 0 to use the library GEMM (the default; DCR_STEP_GEMM=native
+        selects the kernel where the shape allows)."""
+        if self.step_gemm_mode != "native":
+            return 0
+        return int(self.ops.step_gemm_splits(B, N, K))
 
     def _join_side(self) -> None:
         if self._side_used:

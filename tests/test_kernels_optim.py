@@ -124,3 +124,19 @@ def test_adam_clip_folds_data_parallel_average(dcr_ops, world):
     torch.testing.assert_close(nb, na, rtol=1e-5, atol=0)
     torch.testing.assert_close(p, pa, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(m, ma, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("B,N,K", [(64, 8192, 2048), (64, 2048, 8192), (128, 512, 256),
+                                   (64, 64, 96)])
+def test_step_gemm_split_k(dcr_ops, B, N, K):
+    """Split-K step GEMM (csrc/step_gemm.hip): the S fp32 slabs sum to X·Wᵀ."""
+    torch.manual_seed(6)
+    X = (torch.randn(B, K, device="cuda") * 0.1).to(torch.bfloat16)
+    W = (torch.randn(N, K, device="cuda") * 0.05).to(torch.bfloat16)
+    S = dcr_ops.step_gemm_splits(B, N, K)
+    assert S >= 1
+    part = torch.full((S, B, N), float("nan"), device="cuda")
+    dcr_ops.step_gemm(X, W, part)
+    torch.cuda.synchronize()
+    want = X.double() @ W.double().t()
+    torch.testing.assert_close(part.sum(0).double(), want, rtol=1e-4, atol=1e-4)

@@ -148,12 +148,14 @@ def test_tf_norm_slot_fused_kernel_matches_library_route(monkeypatch):
     assert slots[1] == pytest.approx(slots[0], rel=2e-3)
 
 
+@pytest.mark.parametrize("gemm", ["library", "native"])
 @pytest.mark.parametrize("B,T,H,L", [(32, 5, 64, 2), (64, 4, 128, 1)])
-def test_library_step_lstm_path_matches_reference(B, T, H, L, monkeypatch):
+def test_library_step_lstm_path_matches_reference(B, T, H, L, gemm, monkeypatch):
     """DCR_LIBSTEP=1: per-step library GEMM (h·W_h / dZ·W_hᵀ) + epilogue-only cell kernels
     (the H > 1024 LSTM path) against the fp32 oracle, persistent kernels off."""
     monkeypatch.setenv("DCR_PERSIST", "0")
     monkeypatch.setenv("DCR_LIBSTEP", "1")
+    monkeypatch.setenv("DCR_STEP_GEMM", gemm)
     torch.manual_seed(5)
     cfg, nat, ref = _pair("lstm", B, T, H, L)
     assert nat.backend._lib_step("fwd", B) and nat.backend._lib_step("bwd", B)
