@@ -75,6 +75,29 @@ struct BwdStepArgs {
   int nsplit;            // LSTM epilogue-only: `partial` = nsplit [B, H] slabs (0 = 1)
 };
 
+// ---- lstm_ew.hip: epilogue-only LSTM cell steps (large-H library-step path) -------------
+struct LstmEwArgs {
+  int B, H, nsplit;        // nsplit: zrec / dhrec slabs ([nsplit, B, 4H] / [nsplit, B, H])
+  float forget_bias;
+  // forward
+  const float* zrec;       // recurrent pre-activation slabs
+  const float* zx;         // [B, 4H] input projection + bias, or the [V, 4H] table with ids
+  const int* ids;          // [B] or nullptr
+  const float* cprev;      // [B, H]
+  bf16* hout;              // [B, H]
+  float* hout32;           // optional [B, H]
+  float* cout;             // [B, H]
+  bf16* gates;             // [B, 4H] (sigma i, tanh j, sigma f, sigma o)
+  // backward
+  const float* dtop;       // [B, H]
+  const float* dhrec;      // recurrent dh slabs (nsplit may be 0)
+  const bf16* gates_in;    // [B, 4H]
+  const float* c;          // [B, H] c_t
+  float* dc;               // [B, H] carry (in/out)
+  bf16* dz_out;            // [B, 4H]
+};
+void launch_lstm_ew(bool bwd, const LstmEwArgs& a, hipStream_t s);
+
 // ---- step_gemm.hip ----------------------------------------------------------------------
 bool step_gemm_supported(int B, int N, int K);
 int step_gemm_splits(int B, int N, int K);

@@ -206,24 +206,20 @@ void lstm_step_ew_fwd(const at::Tensor& zrec, const at::Tensor& zx,
   } else {
     TORCH_CHECK(zx.numel() == (int64_t)B * 4 * H, "zx must be [B, 4H]");
   }
-  dcr::FwdStepArgs a{};
-  a.WT = nullptr;
-  a.zrec = ptr<float>(zrec);
-  a.zrec_ld = 4 * H;
+  dcr::LstmEwArgs a{};
+  a.B = B;
+  a.H = H;
   a.nsplit = (int)(zrec.numel() / ((int64_t)B * 4 * H));  // split-K slabs (step_gemm)
+  a.forget_bias = (float)forget_bias;
+  a.zrec = ptr<float>(zrec);
   a.zx = ptr<float>(zx);
   a.ids = has(ids) ? ptr<int>(*ids) : nullptr;
-  a.zx_ld = 4 * H;
   a.cprev = ptr<float>(cprev);
   a.hout = ptr<bf16>(hout);
   a.hout32 = optr<float>(hout32);
   a.cout = ptr<float>(cout);
   a.gates = ptr<bf16>(gates);
-  a.gates_ld = 4 * H;
-  a.B = B;
-  a.H = H;
-  a.forget_bias = (float)forget_bias;
-  dcr::launch_fwd_step(dcr::CELL_LSTM, a, cur_stream());
+  dcr::launch_lstm_ew(false, a, cur_stream());
 }
 
 // One epilogue-only LSTM BPTT step: dh = dtop_t + dhrec (dhrec = dZ_{t+1}·W_hᵀ from a library
@@ -246,21 +242,18 @@ void lstm_step_ew_bwd(const at::Tensor& dtop, const c10::optional<at::Tensor>& d
                   dz_out.numel() == gates.numel(), "lstm_step_ew_bwd: shapes");
   TORCH_CHECK(c.numel() == (int64_t)B * H && cprev.numel() == c.numel() && dc.numel() == c.numel(),
               "lstm_step_ew_bwd: state shapes");
-  dcr::BwdStepArgs a{};
-  a.dz_next = nullptr;
-  a.dtop = ptr<float>(dtop);
-  a.partial = optr<float>(dhrec);
+  dcr::LstmEwArgs a{};
+  a.B = B;
+  a.H = H;
   a.nsplit = has(dhrec) ? (int)(dhrec->numel() / dtop.numel()) : 0;
-  a.gates = ptr<bf16>(gates);
-  a.gates_ld = 4 * H;
+  a.dtop = ptr<float>(dtop);
+  a.dhrec = optr<float>(dhrec);
+  a.gates_in = ptr<bf16>(gates);
   a.c = ptr<float>(c);
   a.cprev = ptr<float>(cprev);
   a.dc = ptr<float>(dc);
   a.dz_out = ptr<bf16>(dz_out);
-  a.dz_out_ld = 4 * H;
-  a.B = B;
-  a.H = H;
-  dcr::launch_bwd_step(dcr::CELL_LSTM, a, cur_stream());
+  dcr::launch_lstm_ew(true, a, cur_stream());
 }
 
 // partial[z] = X[:, z-th K slice] · W[:, same]ᵀ for z < S (step_gemm.hip); part [S, B, N] fp32
