@@ -114,15 +114,42 @@ __global__ void __launch_bounds__(kSegThreads) segsum_reduce_kernel(const float*
   }
 }
 
+// Wide vocabularies: each workgroup owns kAtomicRows consecutive rows x one 256-column strip
+// (one workgroup per row was dispatch-bound: 65536 one-atomic-per-thread workgroups took
+// 141 us at N = 32768, W = 512); runs of equal ids inside the chunk are summed in registers
+// and flushed with one fp32 atomic.  With ``perm`` the caller passes the ids sorted and perm[n]
+// = source row of sorted position n: a frequent id then costs one atomic per chunk instead of
+// one per occurrence (hot rows serialise the atomics; the synthetic 8k stream is unigram-skewed).
+constexpr int kAtomicRows = 32;
+
 template <typename T>
 __global__ void __launch_bounds__(kSegThreads) segsum_atomic_kernel(const T* __restrict__ X, int ldx,
                                                                    const int* __restrict__ ids,
+                                                                   const int* __restrict__ perm,
                                                                    int N, int W,
                                                                    float* __restrict__ out) {
-  const int n = blockIdx.y;
-  const int v = ids ? ids[n] : 0;
-  for (int c = blockIdx.x * kSegThreads + threadIdx.x; c < W; c += gridDim.x * kSegThreads)
-    atomicAdd(out + (size_t)v * W + c, (float)X[(size_t)n * ldx + c]);
+  const int c = blockIdx.x * kSegThreads + threadIdx.x;
+  const int n0 = blockIdx.y * kAtomicRows;
+  const int n1 = n0 + kAtomicRows < N ? n0 + kAtomicRows : N;
+  if (c >= W) return;
+  float x[kAtomicRows];
+#pragma unroll
+  for (int i = 0; i < kAtomicRows; ++i)  // all loads in flight before the first atomic
+    x[i] = n0 + i < n1 ? (float)X[(size_t)(perm ? perm[n0 + i] : n0 + i) * ldx + c] : 0.f;
+  int cur = ids ? ids[n0] : 0;
+  float acc = 0.f;
+#pragma unroll
+  for (int i = 0; i < kAtomicRows; ++i) {
+    if (n0 + i >= n1) break;
+    const int v = ids ? ids[n0 + i] : 0;
+    if (v != cur) {
+      atomicAdd(out + (size_t)cur * W + c, acc);
+      acc = 0.f;
+      cur = v;
+    }
+    acc += x[i];
+  }
+  atomicAdd(out + (size_t)cur * W + c, acc);
 }
 
 int segsum_rows_per_chunk(int N) {
@@ -142,11 +169,11 @@ size_t segsum_workspace_floats(int N, int W, int V) {
 
 template <typename T>
 static void launch_segsum_t(const T* X, int ldx, const int* ids, int N, int W, int V, float* out,
-                            float* workspace, int accumulate, hipStream_t s) {
-  if (V > kSegLdsMaxV) {
+                            float* workspace, int accumulate, const int* perm, hipStream_t s) {
+  if (V > kSegLdsMaxV || perm) {
     if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float) * (size_t)V * W, s);
-    dim3 grid((W + kSegThreads - 1) / kSegThreads, N);
-    segsum_atomic_kernel<T><<<grid, kSegThreads, 0, s>>>(X, ldx, ids, N, W, out);
+    dim3 grid((W + kSegThreads - 1) / kSegThreads, (N + kAtomicRows - 1) / kAtomicRows);
+    segsum_atomic_kernel<T><<<grid, kSegThreads, 0, s>>>(X, ldx, ids, perm, N, W, out);
     return;
   }
   const int rpc = segsum_rows_per_chunk(N);
@@ -165,12 +192,12 @@ static void launch_segsum_t(const T* X, int ldx, const int* ids, int N, int W, i
 }
 
 void launch_segsum_bf16(const bf16* X, int ldx, const int* ids, int N, int W, int V, float* out,
-                        float* workspace, int accumulate, hipStream_t s) {
-  launch_segsum_t<bf16>(X, ldx, ids, N, W, V, out, workspace, accumulate, s);
+                        float* workspace, int accumulate, hipStream_t s, const int* perm) {
+  launch_segsum_t<bf16>(X, ldx, ids, N, W, V, out, workspace, accumulate, perm, s);
 }
 void launch_segsum_f32(const float* X, int ldx, const int* ids, int N, int W, int V, float* out,
-                       float* workspace, int accumulate, hipStream_t s) {
-  launch_segsum_t<float>(X, ldx, ids, N, W, V, out, workspace, accumulate, s);
+                       float* workspace, int accumulate, hipStream_t s, const int* perm) {
+  launch_segsum_t<float>(X, ldx, ids, N, W, V, out, workspace, accumulate, perm, s);
 }
 
 }  // namespace dcr

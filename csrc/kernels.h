@@ -115,10 +115,13 @@ void launch_xent(const float* logits, const int* targets, int N, int V, float gr
 // ---- embed.hip --------------------------------------------------------------------------
 int segsum_rows_per_chunk(int N);
 size_t segsum_workspace_floats(int N, int W, int V);
+// perm (atomic route only): ids are sorted and perm[n] is the source row of position n
 void launch_segsum_bf16(const bf16* X, int ldx, const int* ids, int N, int W, int V, float* out,
-                        float* workspace, int accumulate, hipStream_t s);
+                        float* workspace, int accumulate, hipStream_t s,
+                        const int* perm = nullptr);
 void launch_segsum_f32(const float* X, int ldx, const int* ids, int N, int W, int V, float* out,
-                       float* workspace, int accumulate, hipStream_t s);
+                       float* workspace, int accumulate, hipStream_t s,
+                       const int* perm = nullptr);
 
 // ---- lstm_persist.hip -------------------------------------------------------------------
 struct PersistArgs {

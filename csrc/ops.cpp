@@ -417,7 +417,7 @@ void xent_wide(const at::Tensor& logits, const c10::optional<at::Tensor>& bias,
   check_opt(db, at::kFloat, "db");
   TORCH_CHECK(logits.dim() == 2, "logits must be [N, V]");
   const int N = (int)logits.size(0), V = (int)logits.size(1);
-  TORCH_CHECK(dcr::xent_wide_supported(V), "xent_wide needs V % 4 == 0 and V <= 8192");
+  TORCH_CHECK(dcr::xent_wide_supported(V), "xent_wide needs V % 4 == 0 and V <= 16384");
   check_opt(bias, at::kFloat, "bias");
   if (has(bias)) TORCH_CHECK(bias->numel() == V, "bias must be [V]");
   TORCH_CHECK(targets.numel() == N, "targets must be [N]");
@@ -436,7 +436,7 @@ void xent_wide(const at::Tensor& logits, const c10::optional<at::Tensor>& bias,
 }
 
 void segsum(const at::Tensor& X, const c10::optional<at::Tensor>& ids, int64_t V, at::Tensor& out,
-            at::Tensor& workspace, bool accumulate) {
+            at::Tensor& workspace, bool accumulate, const c10::optional<at::Tensor>& perm) {
   TORCH_CHECK(X.is_cuda() && X.dim() == 2 && X.stride(1) == 1, "X must be a row-major 2-D GPU tensor");
   const int N = (int)X.size(0), W = (int)X.size(1), ldx = (int)X.stride(0);
   check_opt(ids, at::kInt, "ids");
@@ -448,13 +448,18 @@ void segsum(const at::Tensor& X, const c10::optional<at::Tensor>& ids, int64_t V
   } else {
     TORCH_CHECK(V == 1, "without ids, V must be 1 (column sum)");
   }
+  check_opt(perm, at::kInt, "perm");
+  if (has(perm))
+    TORCH_CHECK(has(ids) && perm->numel() == N, "perm needs (sorted) ids and must be [N]");
   if (X.scalar_type() == at::kBFloat16) {
     dcr::launch_segsum_bf16(ptr<bf16>(X), ldx, optr<int>(ids), N, W, (int)V, ptr<float>(out),
-                            ptr<float>(workspace), accumulate ? 1 : 0, cur_stream());
+                            ptr<float>(workspace), accumulate ? 1 : 0, cur_stream(),
+                            optr<int>(perm));
   } else {
     TORCH_CHECK(X.scalar_type() == at::kFloat, "X must be bf16 or fp32");
     dcr::launch_segsum_f32(ptr<float>(X), ldx, optr<int>(ids), N, W, (int)V, ptr<float>(out),
-                           ptr<float>(workspace), accumulate ? 1 : 0, cur_stream());
+                           ptr<float>(workspace), accumulate ? 1 : 0, cur_stream(),
+                           optr<int>(perm));
   }
 }
 
@@ -1184,7 +1189,8 @@ TORCH_LIBRARY(dcr, m) {
       "gru_persist_bwd(Tensor Wg, Tensor Wc, Tensor dtop, Tensor(a!) dz, Tensor gates, "
       "Tensor h32, Tensor(b!) cnt, Tensor(c!) err, int spin_limit, bool cnt_zeroed=False, "
       "Tensor(d!)? ring0=None, Tensor(e!)? ring1=None) -> ()");
-  m.def("segsum(Tensor X, Tensor? ids, int V, Tensor(a!) out, Tensor(b!) workspace, bool accumulate) -> ()");
+  m.def("segsum(Tensor X, Tensor? ids, int V, Tensor(a!) out, Tensor(b!) workspace, bool accumulate, "
+        "Tensor? perm=None) -> ()");
   m.def("segsum_workspace(int N, int W, int V) -> int", [](int64_t N, int64_t W, int64_t V) -> int64_t {
     return (int64_t)dcr::segsum_workspace_floats((int)N, (int)W, (int)V);
   });

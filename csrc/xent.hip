@@ -79,48 +79,64 @@ void launch_xent(const float* logits, const int* targets, int N, int V, float gr
 
 
 // ------------------------------------------------------------------------------------------
-// Wide vocabularies (BASELINE.json's 8k-token config).  The row-per-wave kernel above reads a
-// V = 8192 fp32 row three times, d softmax_b needed a separate column sum over the bf16
-// dlogits, and the logits GEMM's bias broadcast cost a 1 GB copy (864 + 255 + 155 us per step
-// at N = 32768).  Here a wave owns kWideRPW rows and holds ONE row at a time in registers
-// (NC float4 per lane), so the logits are read exactly once:
-//   online (max, sum-exp) over the row's registers -> lse, row loss
+// Wide vocabularies (BASELINE.json's 8k-token config).  A row-per-wave kernel reads a V = 8192
+// fp32 row three times, d softmax_b needed a separate column sum over the bf16 dlogits, and
+// the logits GEMM's bias broadcast cost a 1 GB copy (864 + 255 + 155 us per step at
+// N = 32768).  Here the logits are read exactly once:
+//   a WORKGROUP owns kWideRPB consecutive rows and holds one row at a time in registers,
+//   thread t holding float4 columns t, t + 256, ... (NC of them, so NC float4 per lane and
+//   every load / store of a wave is one contiguous 1 KB / 512 B segment);
+//   row max and sum-exp: wave reduction + a 4-entry LDS exchange (2 barriers per row);
 //   dlogits = (softmax - onehot) * scale written as bf16x4, and the bf16-rounded values
 //   accumulated per column in registers (d softmax_b, exactly what the weight GEMM sees);
-// the softmax bias is added here (the GEMM runs without it).  The 4 waves' column partials are
-// reduced through LDS in 1 KB chunks -> one [V] partial per block -> xent_colsum_kernel.
+//   the row loss comes from the thread that owns column y (no dependent global load).
+// The softmax bias is added here (the GEMM runs without it).  Each thread's column sums are
+// the block's [V] partial directly -> xent_colsum_kernel.
+// (The previous row-per-wave layout held 2 x 128 fp32 per lane at V = 8192: 256 VGPRs + 226
+// AGPRs, one wave per SIMD, 456-465 us per step = 3.5 TB/s.)
 // ------------------------------------------------------------------------------------------
-constexpr int kWideRPW = 32;  // rows per wave
+constexpr int kWideRPB = 32;  // rows per workgroup
 
 template <int NC>
 __global__ void __launch_bounds__(256) xent_wide_kernel(
     const float* __restrict__ logits, const float* __restrict__ bias,
     const int* __restrict__ targets, int N, int V, float scale, float* __restrict__ row_loss,
     bf16* __restrict__ dlogits, float* __restrict__ colpart, float* __restrict__ partial) {
-  __shared__ float4 red[3][64];
+  __shared__ float red[2][4];
   __shared__ float lred[4];
-  __shared__ float4 bz[64 * NC];  // the softmax bias, staged once (registers hold the row)
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int r0 = (blockIdx.x * 4 + w) * kWideRPW;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int V4 = V / 4;
-  for (int f = threadIdx.x; f < 64 * NC; f += 256)
-    bz[f] = (bias && f < V4) ? reinterpret_cast<const float4*>(bias)[f] : make_float4(0.f, 0.f, 0.f, 0.f);
-  __syncthreads();
+  const int r0 = blockIdx.x * kWideRPB;
+  __shared__ float4 bb[NC][256];  // the softmax bias (each thread reads only its own columns)
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    const int f = tid + 256 * j;
+    bb[j][tid] = (bias && f < V4) ? reinterpret_cast<const float4*>(bias)[f]
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   float acc[NC][4];
 #pragma unroll
   for (int j = 0; j < NC; ++j) acc[j][0] = acc[j][1] = acc[j][2] = acc[j][3] = 0.f;
   float lacc = 0.f;
-  for (int i = 0; i < kWideRPW; ++i) {
+  for (int i = 0; i < kWideRPB; ++i) {
     const int n = r0 + i;
-    if (n >= N) break;
+    if (n >= N) break;  // uniform across the workgroup
+    const int y = targets[n];
+    const int fy = y >> 2, qy = y & 3;
     const float4* xr = reinterpret_cast<const float4*>(logits + (size_t)n * V);
     float x[NC][4];
+    float zy = 0.f;
+    bool own = false;
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
-      const int f = lane + 64 * j;
+      const int f = tid + 256 * j;
       const float4 v = f < V4 ? xr[f] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
-      const float4 bb = bz[f];
-      x[j][0] = v.x + bb.x; x[j][1] = v.y + bb.y; x[j][2] = v.z + bb.z; x[j][3] = v.w + bb.w;
+      const float4 bv = bb[j][tid];
+      x[j][0] = v.x + bv.x; x[j][1] = v.y + bv.y; x[j][2] = v.z + bv.z; x[j][3] = v.w + bv.w;
+      if (f == fy) {
+        own = true;
+        zy = qy == 0 ? x[j][0] : qy == 1 ? x[j][1] : qy == 2 ? x[j][2] : x[j][3];
+      }
     }
     float m = -INFINITY;
 #pragma unroll
@@ -128,15 +144,23 @@ __global__ void __launch_bounds__(256) xent_wide_kernel(
 #pragma unroll
       for (int q = 0; q < 4; ++q) m = fmaxf(m, x[j][q]);
     m = wave_max(m);
-    float sm = 0.f;
+    if (lane == 0) red[0][w] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+    float sm = 0.f;  // x becomes exp(x - m): reused for dlogits (one exp per element)
 #pragma unroll
     for (int j = 0; j < NC; ++j)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) sm += __expf(x[j][q] - m);
+      for (int q = 0; q < 4; ++q) {
+        x[j][q] = __expf(x[j][q] - m);
+        sm += x[j][q];
+      }
     sm = wave_sum(sm);
-    const int y = targets[n];
-    if (lane == 0) {
-      const float loss = m + __logf(sm) - (logits[(size_t)n * V + y] + (bias ? bias[y] : 0.f));
+    if (lane == 0) red[1][w] = sm;
+    __syncthreads();
+    sm = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    if (own) {
+      const float loss = m + __logf(sm) - zy;
       if (row_loss) row_loss[n] = loss;
       lacc += loss;
     }
@@ -145,12 +169,12 @@ __global__ void __launch_bounds__(256) xent_wide_kernel(
       bf16x4* d = reinterpret_cast<bf16x4*>(dlogits + (size_t)n * V);
 #pragma unroll
       for (int j = 0; j < NC; ++j) {
-        const int f = lane + 64 * j;
+        const int f = tid + 256 * j;
         if (f < V4) {
           bf16x4 o;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            o[q] = f2bf((__expf(x[j][q] - m) * inv - (4 * f + q == y ? 1.f : 0.f)) * scale);
+            o[q] = f2bf((x[j][q] * inv - (f == fy && q == qy ? 1.f : 0.f)) * scale);
             acc[j][q] += (float)o[q];
           }
           d[f] = o;
@@ -164,59 +188,68 @@ __global__ void __launch_bounds__(256) xent_wide_kernel(
     float4* out = reinterpret_cast<float4*>(colpart + (size_t)blockIdx.x * V);
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
-      if (w > 0) red[w - 1][lane] = make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
-      __syncthreads();
-      const int f = lane + 64 * j;
-      if (w == 0 && f < V4) {
-        float4 t = make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          t.x += red[k][lane].x; t.y += red[k][lane].y; t.z += red[k][lane].z; t.w += red[k][lane].w;
-        }
-        out[f] = t;
-      }
-      __syncthreads();
+      const int f = tid + 256 * j;
+      if (f < V4) out[f] = make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
     }
-  } else {
-    __syncthreads();
   }
-  if (threadIdx.x == 0) partial[blockIdx.x] = lred[0] + lred[1] + lred[2] + lred[3];
+  __syncthreads();
+  if (tid == 0) partial[blockIdx.x] = lred[0] + lred[1] + lred[2] + lred[3];
 }
 
-// d softmax_b[v] = sum of the per-block partial rows: 64 columns x 4 row-interleaved groups per
-// block, fixed order per thread and a fixed LDS combine (deterministic)
+// d softmax_b = column sums of the per-block partials [nrows, V].  A workgroup owns 4 float4
+// columns x 64 row groups (16 independent float4 loads per thread at nrows = 1024, all in flight;
+// 512 workgroups at V = 8192), reduced in a fixed order through LDS (bitwise reproducible).
+// (One column per thread over 256 serial rows took 62 us at V = 8192 with 1024 partials.)
 __global__ void __launch_bounds__(256) xent_colsum_kernel(const float* __restrict__ colpart,
                                                           int nrows, int V,
                                                           float* __restrict__ out) {
-  __shared__ float red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
-  float s = 0.f;
-  if (c < V)
-    for (int k = rg; k < nrows; k += 4) s += colpart[(size_t)k * V + c];
-  red[rg][threadIdx.x & 63] = s;
+  __shared__ float4 red[64][4];
+  const int cl = threadIdx.x & 3, rg = threadIdx.x >> 2;
+  const int f = blockIdx.x * 4 + cl, V4 = V / 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (f < V4) {
+    const float4* p = reinterpret_cast<const float4*>(colpart) + f;
+#pragma unroll 16
+    for (int k = rg; k < nrows; k += 64) {
+      const float4 v = p[(size_t)k * V4];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  }
+  red[rg][cl] = s;
   __syncthreads();
-  if (rg == 0 && c < V) out[c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+#pragma unroll
+  for (int h = 32; h > 0; h >>= 1) {
+    if (rg < h) {
+      const float4 o = red[rg + h][cl];
+      s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
+      red[rg][cl] = s;
+    }
+    __syncthreads();
+  }
+  if (rg == 0 && f < V4) {  // scalar stores: out is a gradient view of unknown alignment
+    out[4 * f] = s.x; out[4 * f + 1] = s.y; out[4 * f + 2] = s.z; out[4 * f + 3] = s.w;
+  }
 }
 
-int xent_wide_blocks(int N) { return ((N + kWideRPW - 1) / kWideRPW + 3) / 4; }
+int xent_wide_blocks(int N) { return (N + kWideRPB - 1) / kWideRPB; }
 int xent_wide_waves(int N) { return xent_wide_blocks(N); }  // partial rows: one per block
-int xent_wide_supported(int V) { return V % 4 == 0 && V <= 64 * 4 * 32 ? 1 : 0; }
+int xent_wide_supported(int V) { return V % 4 == 0 && V <= 256 * 4 * 16 ? 1 : 0; }
 
 void launch_xent_wide(const float* logits, const float* bias, const int* targets, int N, int V,
                       float grad_scale, float* row_loss, bf16* dlogits, float* colpart, float* db,
                       float* partial, float* loss_out, hipStream_t s) {
   const int nb = xent_wide_blocks(N);
-  const int nc = (V / 4 + 63) / 64;
+  const int nc = (V / 4 + 255) / 256;
 #define XW(K)                                                                                \
   if (nc <= K) {                                                                             \
     xent_wide_kernel<K><<<nb, 256, 0, s>>>(logits, bias, targets, N, V, grad_scale, row_loss, \
                                            dlogits, colpart, partial);                       \
   } else
-  XW(1) XW(2) XW(4) XW(8) XW(16) XW(32) {}
+  XW(1) XW(2) XW(4) XW(8) XW(16) {}
 #undef XW
   sum_partials_kernel<<<1, kXentThreads, 0, s>>>(partial, nb, 1.0f / (float)N, loss_out);
   if (dlogits && colpart && db)
-    xent_colsum_kernel<<<(V + 63) / 64, 256, 0, s>>>(colpart, nb, V, db);
+    xent_colsum_kernel<<<(V / 4 + 3) / 4, 256, 0, s>>>(colpart, nb, V, db);
 }
 
 }  // namespace dcr

@@ -267,7 +267,18 @@ class NativeBackend:
             self.ops.prep([t[0] for t in chunk], [t[1] for t in chunk], [t[2] for t in chunk])
         if self._table_dirty:
             w0 = self._w[0]
-            self._head["table"] = torch.addmm(w0.bias, self._head["E"], w0.Wx32)  # [V, GW]
+            if self.V > SEG_LDS_MAX_V:
+                # wide vocabulary: the [V, H] x [H, GW] table product on bf16 MFMA operands
+                # (the fp32 GEMM took 139 us per step at V = 8192), i.e. the same operand
+                # precision as a bf16 layer-0 input projection; the bf16 E copy is also the
+                # row source of the dense backward route's X0 gather
+                Eb = self._head.get("Ebf")
+                if Eb is None or Eb.shape != self._head["E"].shape:
+                    Eb = self._head["Ebf"] = torch.empty_like(self._head["E"], dtype=bf16)
+                Eb.copy_(self._head["E"])
+                self._head["table"] = torch.addmm(w0.bias, Eb, w0.Wx, out_dtype=f32)
+            else:
+                self._head["table"] = torch.addmm(w0.bias, self._head["E"], w0.Wx32)  # [V, GW]
             self._table_dirty = False
 
     # ------------------------------------------------------------------ buffers
@@ -783,7 +794,9 @@ class NativeBackend:
                 # wide vocabulary: the [V, GW] dEW segment sum would be an atomic scatter of
                 # N x GW values plus two fp32 [V, GW] GEMMs; the dense route scatters N x H
                 # instead: dW_x0 = E[ids]ᵀ·dZ0 (split-K), dE = segsum(dZ0·W_x0ᵀ)
-                X0 = hd["E"][ids_tm.view(-1).long()].to(bf16)      # [N, H]
+                Eb = hd.get("Ebf")                                  # refreshed with the table
+                X0 = (Eb[ids_tm.view(-1).long()] if Eb is not None
+                      else hd["E"][ids_tm.view(-1).long()].to(bf16))    # [N, H]
                 dWx = _mm_tn(X0, dZx)
                 if bufs["persist"]:
                     dbias = self._bias_sum(bufs["db_part"][layer], names)
@@ -791,7 +804,7 @@ class NativeBackend:
                     self.ops.segsum(dZx, None, 1, bufs["colsum"][:, :GW], bufs["ws"], False)
                     dbias = bufs["colsum"][0, :GW]
                 dXf = _mm_into(dZx, lw.Wx.t(), bufs["dx"].view(N, H))
-                self.ops.segsum(dXf, ids_tm.view(-1), V, s.gview("embedding"), bufs["ws"], False)
+                self._embed_grad(dXf, ids_tm, bufs)
                 self._token_norm(dXf)
             elif gather:
                 if fused_dew:
@@ -843,7 +856,7 @@ class NativeBackend:
                     if "emb" in lb.masks:
                         dX = dX * lb.masks["emb"]
                     dXf = dX.reshape(N, H).float().contiguous()
-                    self.ops.segsum(dXf, ids_tm.view(-1), V, s.gview("embedding"), bufs["ws"], False)
+                    self._embed_grad(dXf, ids_tm, bufs)
                     self._token_norm(dXf)
             if not written:
                 self._write_input_grads(layer, names, dWx, dbias)
@@ -861,6 +874,18 @@ class NativeBackend:
         if (persistent or bufs["big_fwd"]) and self._steps % 200 == 1:
             self.check_errors()
         return bufs["loss"][0], new_state, extras
+
+    def _embed_grad(self, dXf: torch.Tensor, ids_tm: torch.Tensor, bufs) -> None:
+        """dE = segsum(dX_tok, ids) into the gradient buffer.  Wide vocabularies take the
+        fp32-atomic route; there the ids are sorted first (a frequent id is then one register
+        run per 32-row chunk instead of one atomic per occurrence: 127 -> see BASELINE.md)."""
+        ids = ids_tm.view(-1)
+        out = self.store.gview("embedding")
+        if self.V > SEG_LDS_MAX_V and os.environ.get("DCR_SEG_SORT", "1") != "0":
+            sid, perm = torch.sort(ids)
+            self.ops.segsum(dXf, sid, self.V, out, bufs["ws"], False, perm.int())
+        else:
+            self.ops.segsum(dXf, ids, self.V, out, bufs["ws"], False)
 
     def _token_norm(self, dx_tok: torch.Tensor) -> None:
         """TF clip-norm term of the embedding (ModelConfig.clip_norm == "tf"): the sum of

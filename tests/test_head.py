@@ -100,7 +100,7 @@ def test_model_fused_head_equals_library_head(monkeypatch):
     assert abs(ev_a.item() - ev_c.item()) < 1e-3
 
 
-@pytest.mark.parametrize("N,V", [(1000, 8192), (333, 256), (70, 1028)])
+@pytest.mark.parametrize("N,V", [(1000, 8192), (333, 256), (70, 1028), (4100, 12288)])
 def test_xent_wide_matches_torch(N, V, dcr_ops):
     torch.manual_seed(3)
     logits = torch.randn(N, V, device="cuda") * 4

@@ -106,6 +106,28 @@ def test_segsum_kernel(dcr_ops, V, W, N):
     torch.testing.assert_close(out.double(), ref, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("N", [4100, 32768])
+def test_segsum_atomic_wide_vocab_runs(dcr_ops, N):
+    """Wide-vocabulary atomic route (V > 96) with fp32 rows and long runs of equal ids (the
+    kernel sums a run in registers and flushes it with one atomic), ragged last chunk."""
+    V, W = 8192, 512
+    X = torch.randn(N, W, device="cuda")
+    ids = torch.randint(0, V, (N,), device="cuda", dtype=torch.int32)
+    ids[100:180] = 7        # a run crossing a 32-row chunk boundary
+    ids[-5:] = ids[0]
+    out = torch.empty(V, W, device="cuda")
+    ws = torch.empty(max(1, dcr_ops.segsum_workspace(N, W, V)), device="cuda")
+    dcr_ops.segsum(X, ids, V, out, ws, False)
+    ref = torch.zeros(V, W, device="cuda", dtype=torch.float64)
+    ref.index_add_(0, ids.long(), X.double())
+    torch.testing.assert_close(out.double(), ref, rtol=1e-4, atol=1e-4)
+    # sorted route: ids sorted + source-row permutation (native_backend._embed_grad)
+    sid, perm = torch.sort(ids)
+    out2 = torch.empty(V, W, device="cuda")
+    dcr_ops.segsum(X, sid, V, out2, ws, False, perm.int())
+    torch.testing.assert_close(out2.double(), ref, rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.parametrize("nbt", ["2", "4"])
 @pytest.mark.parametrize("model", ["lstm", "gru", "rnn", "nas"])
 def test_per_step_batch_tiles_match_reference(model, nbt, monkeypatch):
