@@ -928,8 +928,8 @@ class NativeBackend:
             for t in range(T):
                 if S:  # split-K step GEMM (step_gemm.hip) into S slabs, summed by the cell kernel
                     self.ops.step_gemm(lb.hbuf[t], lw.WhT, zrec)
-                else:
-                    torch.mm(lb.hbuf[t], lw.Wh, out_dtype=f32, out=zrec[0])
+                else:  # B operand as W_hᵀ-transposed (NT form): 20.7 vs 25.6 us at B = 256
+                    torch.mm(lb.hbuf[t], lw.WhT.t(), out_dtype=f32, out=zrec[0])
                 self.ops.lstm_step_ew_fwd(zrec, zx if ids is not None else zx[t],
                                           ids[t] if ids is not None else None, lb.cbuf[t],
                                           lb.hbuf[t + 1], lb.hlast32 if t == T - 1 else None,
