@@ -102,6 +102,57 @@ __global__ void __launch_bounds__(kSegThreads) colsum_kernel(const T* __restrict
   }
 }
 
+// Column sums (bias gradients) of a bf16 [N, W] matrix with 16-byte rows: each lane reads 8
+// consecutive columns (one 1 KB access per wave and row instead of 128 B), 8 rows in flight
+// per wave; a workgroup owns 512 columns x one row chunk.  (The scalar colsum_kernel read the
+// GRU-1024 [32768, 3072] dZ at 1.7 TB/s: 122 us.)
+constexpr int kVecCols = 512;
+
+__global__ void __launch_bounds__(kSegThreads) colsum_vec_kernel(const bf16* __restrict__ X, int ldx,
+                                                                int N, int W, int rows_per_chunk,
+                                                                float* __restrict__ partial) {
+  __shared__ float red[kSegThreads / 64][kVecCols];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * kVecCols + lane * 8, chunk = blockIdx.y;
+  const bool ok = c < W;  // W % 8 == 0: a lane's 8 columns are all in or all out
+  const int r0 = chunk * rows_per_chunk, r1 = min(N, r0 + rows_per_chunk);
+  constexpr int U = 8, WS = kSegThreads / 64;
+  float acc[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+  if (ok) {
+    for (int n = r0 + wave; n < r1; n += WS * U) {
+      bf16x8 v[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const int nn = n + WS * j;
+        if (nn < r1) {
+          v[j] = *reinterpret_cast<const bf16x8*>(X + (size_t)nn * ldx + c);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[j][q] = f2bf(0.f);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] += bf2f(v[j][q]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) red[wave][lane * 8 + q] = acc[q];
+  __syncthreads();
+  for (int i = threadIdx.x; i < kVecCols; i += kSegThreads) {
+    const int cc = blockIdx.x * kVecCols + i;
+    if (cc < W) {
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < WS; ++k) t += red[k][i];
+      partial[(size_t)chunk * W + cc] = t;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(kSegThreads) segsum_reduce_kernel(const float* __restrict__ partial,
                                                                    int nchunks, int64_t VW,
                                                                    float* __restrict__ out,
@@ -179,7 +230,12 @@ static void launch_segsum_t(const T* X, int ldx, const int* ids, int N, int W, i
   const int rpc = segsum_rows_per_chunk(N);
   const int nchunks = (N + rpc - 1) / rpc;
   dim3 grid((W + kSegCols - 1) / kSegCols, nchunks);
-  if (ids == nullptr && V == 1) {
+  if (ids == nullptr && V == 1 && sizeof(T) == 2 && W % 8 == 0 && ldx % 8 == 0 &&
+      (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
+    dim3 vgrid((W + kVecCols - 1) / kVecCols, nchunks);
+    colsum_vec_kernel<<<vgrid, kSegThreads, 0, s>>>(reinterpret_cast<const bf16*>(X), ldx, N, W,
+                                                    rpc, workspace);
+  } else if (ids == nullptr && V == 1) {
     colsum_kernel<T><<<grid, kSegThreads, 0, s>>>(X, ldx, N, W, rpc, workspace);
   } else {
     const size_t lds = sizeof(float) * V * kSegCols;
