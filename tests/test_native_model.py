@@ -93,7 +93,8 @@ def test_xent_kernel(dcr_ops):
     torch.testing.assert_close(dl.float(), lt.grad, rtol=1e-2, atol=1e-5)
 
 
-@pytest.mark.parametrize("V,W,N", [(65, 256, 5000), (1, 130, 777), (200, 64, 300), (1, 3072, 5000), (1, 520, 777)])
+@pytest.mark.parametrize("V,W,N", [(65, 256, 5000), (1, 130, 777), (200, 64, 300),
+                                   (1, 3072, 5000), (1, 520, 777)])
 def test_segsum_kernel(dcr_ops, V, W, N):
     X = torch.randn(N, W, device="cuda").to(torch.bfloat16)
     ids = torch.randint(0, V, (N,), device="cuda", dtype=torch.int32) if V > 1 else None
