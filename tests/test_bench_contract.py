@@ -2,10 +2,13 @@
 must run warmup + timed steps, take the max time over ranks and print exactly ONE JSON line
 (rank 0) with the required keys."""
 import json
+import math
 import os
 import socket
 import subprocess
 import sys
+
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
@@ -53,3 +56,25 @@ def test_bench_single_cpu():
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json_lines(r.stdout)[0]
     assert d["n_gpus"] == 1 and d["config"]["parallelism"] == "dp1"
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_one_gpu():
+    """The DP path on real GPU tensors: two ranks share cuda:0 (the GPU box has one card), so
+    RCCL refuses them (duplicate GPU) and gloo carries the bucketed all-reduce; the per-step
+    kernels run because two processes' persistent grids cannot both be co-resident on one chip
+    (the spin timeout reports that instead of hanging, see native_backend.check_errors)."""
+    env = dict(os.environ, PYTHONPATH=ROOT, DCR_PERSIST="0")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--dist_backend", "gloo", "--batch", "64", "--seq", "32"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert d["value"] > 0 and math.isfinite(d["final_loss"])
