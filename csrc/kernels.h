@@ -192,19 +192,22 @@ struct Lstm2Args {
   const float* bias1;   // layer l+1 bias [4H]
   bf16* hbuf0; float* cbuf0; bf16* gates0; float* hlast0;   // layer l   [T+1,B,H] ...
   bf16* hbuf1; float* cbuf1; bf16* gates1; float* hlast1;   // layer l+1
-  unsigned* cnt0;       // [B/32, T+1, 4] arrivals of layer l   (zeroed by the caller)
-  unsigned* cnt1;       // [B/32, T+1, 4] arrivals of layer l+1
+  unsigned* cnt0;       // [nbg, T+1, 4] arrivals of layer l   (zeroed by the caller)
+  unsigned* cnt1;       // [nbg, T+1, 4] arrivals of layer l+1
   unsigned* err;
-  unsigned long long* diag;  // optional [T+2, 8] s_memtime stamps of workgroup 0 (diagnostics)
+  unsigned long long* diag;  // optional [T+1, 8] s_memtime stamps of workgroup 0 (diagnostics)
   float* clast0;        // optional [B, H] final c of layers l and l+1
   float* clast1;
-  bf16* hring0;         // optional [2, B, H] fragment-tiled h hand-off rings (persist_common.h);
-  bf16* hring1;         //   the row-major hbufs are then written after the arrival
-  int B, H, T;
+  bf16* hring0;         // [2, nbg*32, H] fragment-tiled h hand-off rings (persist_common.h)
+  bf16* hring1;
+  int B, H, T;          // B: real batch rows (row-major buffers); rows up to nbg*32 are padding
+  int G, nbg;           // batch groups per workgroup; 32-row batch groups (multiple of G)
   float forget_bias;
   unsigned spin_limit;
 };
-int lstm2_persist_supported(int H, int B, int cus);
+// batch groups per workgroup for the two-layer kernels at (H, B) (force > 0: only that value),
+// 0 = unsupported
+int lstm2_plan_g(int H, int B, int cus, int force);
 int launch_lstm2_fwd_persist(const Lstm2Args& a, int cus, hipStream_t s);
 
 // two-layer wavefront LSTM BPTT (lstm2_persist.hip): layers l and l+1 in one launch, layer l
@@ -218,15 +221,15 @@ struct Lstm2BwdArgs {
   const bf16* gates1; const float* cbuf1;   // layer l+1
   bf16* dz0; bf16* dz1;                     // [T, B, 4H] row-major dZ (weight GEMM operands)
   bf16* zring0; bf16* zring1;               // [2, B, 4H] fragment-tiled dZ hand-off rings
-  float* db_part0; float* db_part1;         // [B/16, 4H] bias-gradient partials (or nullptr)
-  unsigned* cnt0;       // [B/32, T+1, 4] arrivals of layer l   (zeroed by the caller)
-  unsigned* cnt1;       // [B/32, T+1, 4] arrivals of layer l+1
+  float* db_part0; float* db_part1;         // [2*nbg/G, 4H] bias-gradient partials (or nullptr)
+  unsigned* cnt0;       // [nbg, T+1, 4] arrivals of layer l   (zeroed by the caller)
+  unsigned* cnt1;       // [nbg, T+1, 4] arrivals of layer l+1
   unsigned* err;
   unsigned long long* diag;  // optional [T+2, 8] s_memtime stamps of workgroup 0
   int B, H, T;
+  int G, nbg;           // as Lstm2Args; zring0/1 hold [2, nbg*32, 4H]
   unsigned spin_limit;
 };
-int lstm2_bwd_persist_supported(int H, int B, int cus);
 int launch_lstm2_bwd_persist(const Lstm2BwdArgs& a, int cus, hipStream_t s);
 
 // persistent GRU recurrence (gru_persist.hip)

@@ -695,6 +695,13 @@ void lstm_big_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::optiona
 
 // two-layer wavefront LSTM forward (lstm2_persist.hip)
 // ------------------------------------------------------------------------------------------
+static int lstm2_nbg(int B, int G) { return ((B + 31) / 32 + G - 1) / G * G; }
+
+static void check_lstm2_counters(const at::Tensor& c, int nbg, int T) {
+  TORCH_CHECK(c.is_cuda() && c.scalar_type() == at::kInt && c.is_contiguous() &&
+                  c.numel() >= (int64_t)nbg * (T + 1) * 4, "counter buffer too small");
+}
+
 void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::Tensor& X1T,
                        const at::Tensor& zx0, const c10::optional<at::Tensor>& ids,
                        const at::Tensor& bias1, at::Tensor& hbuf0, at::Tensor& cbuf0,
@@ -702,20 +709,22 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
                        at::Tensor& hbuf1, at::Tensor& cbuf1,
                        const c10::optional<at::Tensor>& gates1, at::Tensor& hlast1,
                        at::Tensor& cnt0, at::Tensor& cnt1, at::Tensor& err, double forget_bias,
-                       int64_t spin_limit, const c10::optional<at::Tensor>& diag,
-                       const c10::optional<at::Tensor>& hring0,
-                       const c10::optional<at::Tensor>& hring1,
+                       int64_t spin_limit, at::Tensor& hring0, at::Tensor& hring1, int64_t G,
                        const c10::optional<at::Tensor>& clast0,
-                       const c10::optional<at::Tensor>& clast1) {
+                       const c10::optional<at::Tensor>& clast1,
+                       const c10::optional<at::Tensor>& diag) {
   for (auto* t : {&W0T, &W1T, &X1T}) check_seq(*t, at::kBFloat16, "W");
   check_seq(zx0, at::kFloat, "zx0");
   check_seq(bias1, at::kFloat, "bias1");
-  for (auto* t : {&hbuf0, &hbuf1}) check_seq(*t, at::kBFloat16, "hbuf");
+  for (auto* t : {&hbuf0, &hbuf1, &hring0, &hring1}) check_seq(*t, at::kBFloat16, "hbuf/hring");
   for (auto* t : {&cbuf0, &cbuf1, &hlast0, &hlast1}) check_seq(*t, at::kFloat, "state");
   check_opt(gates0, at::kBFloat16, "gates0");
   check_opt(gates1, at::kBFloat16, "gates1");
   check_opt(ids, at::kInt, "ids");
   const int T = (int)hbuf0.size(0) - 1, B = (int)hbuf0.size(1), H = (int)hbuf0.size(2);
+  TORCH_CHECK(G >= 1 && dcr::lstm2_plan_g(H, B, num_cus(), (int)G) == G,
+              "two-layer persistent LSTM: no co-resident grid for H=", H, " B=", B, " G=", G);
+  const int nbg = lstm2_nbg(B, (int)G);
   TORCH_CHECK(hbuf1.sizes() == hbuf0.sizes(), "hbuf1 must match hbuf0");
   TORCH_CHECK(cbuf0.numel() == hbuf0.numel() && cbuf1.numel() == hbuf0.numel(), "cbuf shape");
   TORCH_CHECK(hlast0.numel() == (int64_t)B * H && hlast1.numel() == (int64_t)B * H, "hlast shape");
@@ -730,11 +739,9 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
   }
   for (auto* g : {&gates0, &gates1})
     if (has(*g)) TORCH_CHECK((*g)->numel() == (int64_t)T * B * 4 * H, "gates must be [T, B, 4H]");
-  for (auto* c : {&cnt0, &cnt1})
-    TORCH_CHECK(c->is_cuda() && c->scalar_type() == at::kInt &&
-                    c->numel() >= (int64_t)(B / 32) * (T + 1) * 4, "counter buffer too small");
-  TORCH_CHECK(dcr::lstm2_persist_supported(H, B, num_cus()),
-              "two-layer persistent LSTM unsupported for H=", H, " B=", B);
+  for (auto* c : {&cnt0, &cnt1}) check_lstm2_counters(*c, nbg, T);
+  for (auto* r : {&hring0, &hring1})
+    TORCH_CHECK(r->numel() >= (int64_t)2 * nbg * 32 * H, "hring must hold [2, ", nbg * 32, ", H]");
   dcr::Lstm2Args a{};
   a.W0T = ptr<bf16>(W0T); a.W1T = ptr<bf16>(W1T); a.X1T = ptr<bf16>(X1T);
   a.zx0 = ptr<float>(zx0); a.ids = optr<int>(ids); a.zx_ld = 4 * H;
@@ -746,7 +753,7 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
   a.cnt0 = reinterpret_cast<unsigned*>(cnt0.data_ptr());
   a.cnt1 = reinterpret_cast<unsigned*>(cnt1.data_ptr());
   a.err = reinterpret_cast<unsigned*>(err.data_ptr());
-  a.B = B; a.H = H; a.T = T;
+  a.B = B; a.H = H; a.T = T; a.G = (int)G; a.nbg = nbg;
   a.forget_bias = (float)forget_bias;
   a.spin_limit = (unsigned)spin_limit;
   if (has(diag)) {
@@ -754,14 +761,8 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
                 "diag must hold [T+2, 8] int64 (ticks 0..T+1)");
     a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());
   }
-  for (auto* r : {&hring0, &hring1})
-    if (has(*r)) {
-      check_seq(**r, at::kBFloat16, "hring");
-      TORCH_CHECK((*r)->numel() >= (int64_t)2 * B * H, "hring must hold [2, B, H]");
-    }
-  TORCH_CHECK(has(hring0) == has(hring1), "pass both hand-off rings or neither");
-  a.hring0 = optr<bf16>(hring0);
-  a.hring1 = optr<bf16>(hring1);
+  a.hring0 = ptr<bf16>(hring0);
+  a.hring1 = ptr<bf16>(hring1);
   for (auto* c : {&clast0, &clast1})
     if (has(*c)) {
       check_seq(**c, at::kFloat, "clast");
@@ -780,28 +781,34 @@ void lstm2_persist_bwd(const at::Tensor& Wh0, const at::Tensor& Wh1, const at::T
                        at::Tensor& dz1, at::Tensor& zring0, at::Tensor& zring1,
                        const c10::optional<at::Tensor>& db_part0,
                        const c10::optional<at::Tensor>& db_part1, at::Tensor& cnt0,
-                       at::Tensor& cnt1, at::Tensor& err, int64_t spin_limit,
+                       at::Tensor& cnt1, at::Tensor& err, int64_t spin_limit, int64_t G,
                        const c10::optional<at::Tensor>& diag) {
   for (auto* t : {&Wh0, &Wh1, &Wx1}) check_seq(*t, at::kBFloat16, "W");
   check_seq(dtop1, at::kFloat, "dtop1");
-  for (const at::Tensor* t : {&gates0, &gates1, (const at::Tensor*)&dz0, (const at::Tensor*)&dz1, (const at::Tensor*)&zring0, (const at::Tensor*)&zring1}) check_seq(*t, at::kBFloat16, "bf16 buffer");
+  for (const at::Tensor* t : {&gates0, &gates1, (const at::Tensor*)&dz0, (const at::Tensor*)&dz1,
+                              (const at::Tensor*)&zring0, (const at::Tensor*)&zring1})
+    check_seq(*t, at::kBFloat16, "bf16 buffer");
   for (auto* t : {&cbuf0, &cbuf1}) check_seq(*t, at::kFloat, "cbuf");
   const int T = (int)dtop1.size(0), B = (int)dtop1.size(1), H = (int)dtop1.size(2);
+  TORCH_CHECK(G >= 1 && dcr::lstm2_plan_g(H, B, num_cus(), (int)G) == G,
+              "two-layer persistent LSTM BPTT: no co-resident grid for H=", H, " B=", B, " G=", G);
+  const int nbg = lstm2_nbg(B, (int)G);
   for (auto* t : {&Wh0, &Wh1, &Wx1})
     TORCH_CHECK(t->size(0) == H && t->size(1) == 4 * H, "weights must be [H, 4H]");
   const int64_t n4 = (int64_t)T * B * 4 * H;
-  for (const at::Tensor* t : {&gates0, &gates1, (const at::Tensor*)&dz0, (const at::Tensor*)&dz1}) TORCH_CHECK(t->numel() == n4, "gates/dz must be [T, B, 4H]");
-  for (auto* t : {&cbuf0, &cbuf1}) TORCH_CHECK(t->numel() == (int64_t)(T + 1) * B * H, "cbuf must be [T+1, B, H]");
-  for (auto* t : {&zring0, &zring1}) TORCH_CHECK(t->numel() >= (int64_t)2 * B * 4 * H, "zring must hold [2, B, 4H]");
-  for (auto* c : {&cnt0, &cnt1})
-    TORCH_CHECK(c->is_cuda() && c->scalar_type() == at::kInt &&
-                    c->numel() >= (int64_t)(B / 32) * (T + 1) * 4, "counter buffer too small");
+  for (const at::Tensor* t : {&gates0, &gates1, (const at::Tensor*)&dz0, (const at::Tensor*)&dz1})
+    TORCH_CHECK(t->numel() == n4, "gates/dz must be [T, B, 4H]");
+  for (auto* t : {&cbuf0, &cbuf1})
+    TORCH_CHECK(t->numel() == (int64_t)(T + 1) * B * H, "cbuf must be [T+1, B, H]");
+  for (auto* t : {&zring0, &zring1})
+    TORCH_CHECK(t->numel() >= (int64_t)2 * nbg * 32 * 4 * H, "zring must hold [2, ", nbg * 32, ", 4H]");
+  for (auto* c : {&cnt0, &cnt1}) check_lstm2_counters(*c, nbg, T);
   for (auto* d : {&db_part0, &db_part1}) {
     check_opt(*d, at::kFloat, "db_part");
-    if (has(*d)) TORCH_CHECK((*d)->numel() == (int64_t)(B / 16) * 4 * H, "db_part must be [B/16, 4H]");
+    if (has(*d))
+      TORCH_CHECK((*d)->numel() == (int64_t)(2 * nbg / G) * 4 * H,
+                  "db_part must be [2*nbg/G, 4H] = [", 2 * nbg / G, ", ", 4 * H, "]");
   }
-  TORCH_CHECK(dcr::lstm2_bwd_persist_supported(H, B, num_cus()),
-              "two-layer persistent LSTM BPTT unsupported for H=", H, " B=", B);
   dcr::Lstm2BwdArgs a{};
   a.Wh0 = ptr<bf16>(Wh0); a.Wh1 = ptr<bf16>(Wh1); a.Wx1 = ptr<bf16>(Wx1);
   a.dtop1 = ptr<float>(dtop1);
@@ -813,7 +820,7 @@ void lstm2_persist_bwd(const at::Tensor& Wh0, const at::Tensor& Wh1, const at::T
   a.cnt0 = reinterpret_cast<unsigned*>(cnt0.data_ptr());
   a.cnt1 = reinterpret_cast<unsigned*>(cnt1.data_ptr());
   a.err = reinterpret_cast<unsigned*>(err.data_ptr());
-  a.B = B; a.H = H; a.T = T;
+  a.B = B; a.H = H; a.T = T; a.G = (int)G; a.nbg = nbg;
   a.spin_limit = (unsigned)spin_limit;
   if (has(diag)) {
     TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)(T + 2) * 8,
@@ -1143,24 +1150,24 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor(a!)? logits, Tensor(b!)? row_loss, Tensor(c!)? dlogits, Tensor(d!)? dtop, "
       "Tensor(e!)? db, Tensor(f!) part, Tensor(g!)? loss) -> ()");
   m.def("prep(Tensor[] src, Tensor(a!)[] dst, int[] mode) -> ()");
-  m.def("lstm2_persist_supported(int H, int B) -> int", [](int64_t H, int64_t B) -> int64_t {
-    return dcr::lstm2_persist_supported((int)H, (int)B, num_cus());
-  });
+  m.def("lstm2_plan(int H, int B, int force=0) -> int",
+        [](int64_t H, int64_t B, int64_t force) -> int64_t {
+          return dcr::lstm2_plan_g((int)H, (int)B, num_cus(), (int)force);
+        });
+  m.def("lstm2_nbg(int B, int G) -> int",
+        [](int64_t B, int64_t G) -> int64_t { return lstm2_nbg((int)B, (int)G); });
   m.def(
       "lstm2_persist_fwd(Tensor W0T, Tensor W1T, Tensor X1T, Tensor zx0, Tensor? ids, "
       "Tensor bias1, Tensor(a!) hbuf0, Tensor(b!) cbuf0, Tensor(c!)? gates0, Tensor(d!) hlast0, "
       "Tensor(e!) hbuf1, Tensor(f!) cbuf1, Tensor(g!)? gates1, Tensor(h!) hlast1, "
       "Tensor(i!) cnt0, Tensor(j!) cnt1, Tensor(k!) err, float forget_bias, int spin_limit, "
-      "Tensor(l!)? diag=None, Tensor(m!)? hring0=None, Tensor(n!)? hring1=None, "
-      "Tensor(o!)? clast0=None, Tensor(p!)? clast1=None) -> ()");
-  m.def("lstm2_bwd_persist_supported(int H, int B) -> int", [](int64_t H, int64_t B) -> int64_t {
-    return dcr::lstm2_bwd_persist_supported((int)H, (int)B, num_cus());
-  });
+      "Tensor(l!) hring0, Tensor(m!) hring1, int G, Tensor(o!)? clast0=None, "
+      "Tensor(p!)? clast1=None, Tensor(q!)? diag=None) -> ()");
   m.def(
       "lstm2_persist_bwd(Tensor Wh0, Tensor Wh1, Tensor Wx1, Tensor dtop1, Tensor gates0, "
       "Tensor cbuf0, Tensor gates1, Tensor cbuf1, Tensor(a!) dz0, Tensor(b!) dz1, "
       "Tensor(c!) zring0, Tensor(d!) zring1, Tensor(e!)? db_part0, Tensor(f!)? db_part1, "
-      "Tensor(g!) cnt0, Tensor(h!) cnt1, Tensor(i!) err, int spin_limit, "
+      "Tensor(g!) cnt0, Tensor(h!) cnt1, Tensor(i!) err, int spin_limit, int G, "
       "Tensor(j!)? diag=None) -> ()");
   m.def("sample_supported(int V, int H) -> int", [](int64_t V, int64_t H) -> int64_t {
     return dcr::sample_supported((int)V, (int)H);

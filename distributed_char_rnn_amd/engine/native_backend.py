@@ -288,6 +288,9 @@ class NativeBackend:
             return self._bufs[key]
         H, GW, dev, m = self.H, self.GW, self.dev, self.cfg.model
         N = B * T
+        plan = self._persist_plan(B, training, T)
+        Bp = max(B, 32 * plan["pair_nbg"])  # hand-off rings of the pair kernels: padded batch
+        nrow = max(B // 16, 2 * plan["pair_nbg"] // max(plan["pair_g"], 1), 1)
         layers = []
         for layer in range(self.L):
             dense = layer > 0 or self._dropout(training)
@@ -325,17 +328,17 @@ class NativeBackend:
                     if (training and self.V <= SEG_LDS_MAX_V) else None),
             colpart=(torch.empty(self.ops.xent_wide_waves(N) * self.V, dtype=f32, device=dev)
                      if (training and self._wide_xent(N)) else None),
-            **self._persist_plan(B, training, T),
+            **plan,
             dtop=torch.empty(T, B, H, dtype=f32, device=dev) if training else None,
             dx=torch.empty(T, B, H, dtype=f32, device=dev) if training else None,
-            db_part=(torch.empty(self.L, max(B // 16, 1), GW, dtype=f32, device=dev)
+            db_part=(torch.empty(self.L, nrow, GW, dtype=f32, device=dev)
                      if training else None),
             dew_part=(torch.empty(max(B // 16, 1), self.V, GW, dtype=f32, device=dev)
                       if (training and self.V <= 128) else None),
             # one hand-off counter region per persistent launch (fwd layers, then bwd layers),
             # zeroed together by the step's prep launch
-            cnt=torch.zeros(2 * self.L, 2 * (B // 16 + 1) * (T + 1) * 4, dtype=torch.int32,
-                            device=dev),
+            cnt=torch.zeros(2 * self.L, max(2 * (B // 16 + 1), plan["pair_nbg"]) * (T + 1) * 4,
+                            dtype=torch.int32, device=dev),
             ring=torch.zeros(2 * B * (H // 2), dtype=torch.int64, device=dev),
             # fragment-tiled hand-off rings of the persistent GRU: [h or dZc, r⊙h, dZg]
             grings=((torch.empty(2 * B * H, dtype=bf16, device=dev),
@@ -343,16 +346,23 @@ class NativeBackend:
                      torch.empty(2 * B * 2 * H, dtype=bf16, device=dev))
                     if (m == "gru" and os.environ.get("DCR_FRAG", "1") != "0") else None),
             # fragment-tiled h hand-off rings of the wavefront forward (persist_common.h)
-            hrings=((torch.empty(2 * B * H, dtype=bf16, device=dev),
-                     torch.empty(2 * B * H, dtype=bf16, device=dev))
-                    if os.environ.get("DCR_FRAG", "1") != "0" else None),
+            hrings=((torch.empty(2 * Bp * H, dtype=bf16, device=dev),
+                     torch.empty(2 * Bp * H, dtype=bf16, device=dev))
+                    if (os.environ.get("DCR_FRAG", "1") != "0" or plan["pair"]) else None),
             # fragment-tiled dZ hand-off ring of the persistent BPTT (persist_common.h)
-            zring=(torch.empty(2 * B * GW, dtype=bf16, device=dev)
-                   if (training and os.environ.get("DCR_FRAG", "1") != "0") else None),
+            zring=(torch.empty(2 * Bp * GW, dtype=bf16, device=dev)
+                   if (training and (os.environ.get("DCR_FRAG", "1") != "0" or plan["pair_bwd"]))
+                   else None),
         )
         # second dZ ring for the two-layer wavefront BPTT (one ring per layer)
-        bufs["zring2"] = (torch.empty(2 * B * GW, dtype=bf16, device=dev)
+        bufs["zring2"] = (torch.empty(2 * Bp * GW, dtype=bf16, device=dev)
                           if bufs["pair_bwd"] else None)
+        # layers run by the persistent LSTM kernels (their final state is written into fresh
+        # tensors, their bias gradients come from the kernels' db_part partials)
+        npair = 2 * (self.L // 2) if bufs["pair"] else 0
+        bufs["pers_layers"] = set(range(npair)) | (set(range(npair, self.L)) if bufs["persist"]
+                                                   else set())
+        bufs["pair_rows"] = 2 * bufs["pair_nbg"] // max(bufs["pair_g"], 1)
         self._bufs[key] = bufs
         return bufs
 
@@ -402,7 +412,8 @@ class NativeBackend:
         forces a mode.
         """
         plan = dict(persist=False, xfuse=False, mode="exclusive", bwd_excl=False,
-                    gru_persist=False, pair=False, pair_bwd=False, big_fwd=False)
+                    gru_persist=False, pair=False, pair_bwd=False, big_fwd=False, pair_g=0,
+                    pair_nbg=0)
         o = self.ops
         if T < self.persist_min_t:
             # a persistent grid first loads every weight slice into registers (~6 MB for the
@@ -421,8 +432,18 @@ class NativeBackend:
             # stays on the per-step kernels
             plan["big_fwd"] = True
             return plan
-        if not (self.use_persist and self.cfg.model == "lstm"
-                and bool(o.lstm_persist_supported(self.H, B))):
+        if not (self.use_persist and self.cfg.model == "lstm"):
+            return plan
+        # two-layer wavefront kernels (lstm2_persist.hip) for layers (0,1), (2,3), ...: any
+        # batch (padded to 32-row groups, G groups per workgroup), H in {128..512}
+        if self.L >= 2 and self.use_pair and not self._dropout(training):
+            G = int(o.lstm2_plan(self.H, B, int(os.environ.get("DCR_PAIR_G", "0"))))
+            if G:
+                plan.update(pair=True, pair_g=G, pair_nbg=int(o.lstm2_nbg(B, G)),
+                            pair_bwd=training and self.use_pair_bwd)
+                if training:
+                    plan["mode"] = "exclusive"  # one workgroup per CU: nothing runs beside it
+        if not bool(o.lstm_persist_supported(self.H, B)):
             return plan
         H, cus, grid = self.H, int(o.num_cus()), int(o.lstm_persist_grid(self.H, B))
         vdew = self.V if (training and self.V <= 128) else 0
@@ -439,14 +460,8 @@ class NativeBackend:
         plan["persist"] = True
         plan["xfuse"] = (os.environ.get("DCR_XFUSE", "1") != "0"
                          and bool(o.lstm_persist_xfuse_supported(H, B)))
-        # two-layer wavefront forward (lstm2_persist.hip): layers (0,1), (2,3), ...
-        plan["pair"] = (self.L >= 2 and self.use_pair and bool(o.lstm2_persist_supported(H, B)))
         if not training:
             return plan
-        # two-layer wavefront BPTT (needs the fragment-order dZ rings)
-        plan["pair_bwd"] = (plan["pair"] and self.use_pair_bwd
-                            and os.environ.get("DCR_FRAG", "1") != "0"
-                            and bool(o.lstm2_bwd_persist_supported(H, B)))
         shared_ok = fits(1, 0, margin=1)
         excl_ok = fits(1, PF_EXCL)
         forced = os.environ.get("DCR_MODE", "")
@@ -499,16 +514,16 @@ class NativeBackend:
                     tasks.append((src, dst, 0))
                 else:
                     dst.copy_(src)
-        if bufs["persist"] or bufs["gru_persist"] or bufs["big_fwd"]:
+        if bufs["persist"] or bufs["pair"] or bufs["gru_persist"] or bufs["big_fwd"]:
             tasks.append((bufs["cnt"], bufs["cnt"], 2))
         self._run_prep(tasks)
         # the persistent LSTM kernels write the final (c, h) straight into fresh tensors that
         # become the returned TBPTT state (no copies of cbuf[T] / hlast32 afterwards)
-        fresh = bufs["persist"] and self.cfg.model == "lstm"
-        if fresh:
-            for lb in bufs["layers"]:
-                lb.hlast32 = torch.empty(B, H, dtype=f32, device=self.dev)
-                lb.clast32 = torch.empty(B, H, dtype=f32, device=self.dev)
+        fresh = bufs["pers_layers"] if self.cfg.model == "lstm" else set()
+        for layer in fresh:
+            lb = bufs["layers"][layer]
+            lb.hlast32 = torch.empty(B, H, dtype=f32, device=self.dev)
+            lb.clast32 = torch.empty(B, H, dtype=f32, device=self.dev)
         x_prev = None  # bf16 [T, B, H] input for the next layer
         paired = -1  # layer already computed by the previous layer's two-layer wavefront
         for layer in range(self.L):
@@ -555,9 +570,8 @@ class NativeBackend:
                                            lb.hbuf, lb.cbuf, lb.gates, lb.hlast32,
                                            lb1.hbuf, lb1.cbuf, lb1.gates, lb1.hlast32,
                                            bufs["cnt"][layer], bufs["cnt"][layer + 1], self.err,
-                                           FORGET_BIAS, self.spin_limit, None,
-                                           *(bufs["hrings"] or (None, None)), lb.clast32,
-                                           lb1.clast32)
+                                           FORGET_BIAS, self.spin_limit, *bufs["hrings"],
+                                           bufs["pair_g"], lb.clast32, lb1.clast32)
                 lb1.x_in = lb.hbuf[1:].reshape(N, H)
                 x_prev = lb1.hbuf[1:]
                 paired = layer + 1
@@ -604,7 +618,7 @@ class NativeBackend:
         for layer in range(self.L):
             lb = bufs["layers"][layer]
             if self.cfg.model in ("lstm", "nas"):
-                new_state.append((lb.clast32, lb.hlast32) if fresh
+                new_state.append((lb.clast32, lb.hlast32) if layer in fresh
                                  else (lb.cbuf[T].clone(), lb.hlast32.clone()))
             elif self.cfg.model == "gru":
                 new_state.append((lb.h32[T].clone(),))
@@ -649,7 +663,7 @@ class NativeBackend:
             self.ops.segsum(dlog, None, 1, bufs["colsum"][:, :V], bufs["ws"], False)
             s.gview("rnnlm/softmax_b").copy_(bufs["colsum"][0, :V])
             dtop = _mm_into(dlog, hd["Ws"].t(), bufs["dtop"].view(N, H)).view(T, B, H)
-        persistent = bufs["persist"] or bufs["gru_persist"]
+        persistent = bufs["persist"] or bufs["pair"] or bufs["gru_persist"]
         overlap = bufs["mode"] == "overlap" or not persistent
         pending = []
         user_ready = None
@@ -694,12 +708,13 @@ class NativeBackend:
                 # ticks, the lower layer's dtop = dZ·W_xᵀ of this layer computed in-kernel
                 lo = layer - 1
                 lw0, lb0 = self._w[lo], bufs["layers"][lo]
+                nr = bufs["pair_rows"]
                 self.ops.lstm2_persist_bwd(lw0.Wh, lw.Wh, lw.Wx, dtop, lb0.gates, lb0.cbuf,
                                            lb.gates, lb.cbuf, lb0.dz, lb.dz, bufs["zring"],
-                                           bufs["zring2"], bufs["db_part"][lo],
-                                           bufs["db_part"][layer], bufs["cnt"][self.L + lo],
+                                           bufs["zring2"], bufs["db_part"][lo][:nr],
+                                           bufs["db_part"][layer][:nr], bufs["cnt"][self.L + lo],
                                            bufs["cnt"][self.L + layer], self.err,
-                                           self.spin_limit)
+                                           self.spin_limit, bufs["pair_g"])
                 paired_done = lo
                 if lo == 0 and user_ready is not None:
                     on_ready = _release()
@@ -745,7 +760,7 @@ class NativeBackend:
                 # W_h and W_x^{above} in registers (one workgroup per CU, grid = all CUs), so
                 # NOTHING may run beside it (a concurrent kernel holding CUs could deadlock the
                 # grid's residency): this layer's weight gradients are deferred until after it.
-                dbias = self._bias_sum(bufs["db_part"][layer], names)
+                dbias = self._bias_sum(self._db_part(bufs, layer), names)
 
                 def _wgrads(names=names, Hprev=Hprev, dZ=dZ, dZx=dZx, lb=lb, dbias=dbias,
                             layer=layer):
@@ -763,7 +778,7 @@ class NativeBackend:
                 # GEMMs) run on a side stream concurrently with the latency-bound BPTT of the
                 # layer below; the layer's all-reduce bucket is launched from that stream, so
                 # RCCL orders itself after the GEMMs.  Only dX stays on the critical path.
-                dbias = self._bias_sum(bufs["db_part"][layer], names)
+                dbias = self._bias_sum(self._db_part(bufs, layer), names)
                 ev = torch.cuda.Event()
                 ev.record()
                 side = self._side_stream()
@@ -798,8 +813,8 @@ class NativeBackend:
                 X0 = (Eb[ids_tm.view(-1).long()] if Eb is not None
                       else hd["E"][ids_tm.view(-1).long()].to(bf16))    # [N, H]
                 dWx = _mm_tn(X0, dZx)
-                if bufs["persist"]:
-                    dbias = self._bias_sum(bufs["db_part"][layer], names)
+                if layer in bufs["pers_layers"]:
+                    dbias = self._bias_sum(self._db_part(bufs, layer), names)
                 else:
                     self.ops.segsum(dZx, None, 1, bufs["colsum"][:, :GW], bufs["ws"], False)
                     dbias = bufs["colsum"][0, :GW]
@@ -836,8 +851,8 @@ class NativeBackend:
             else:
                 dWx = (_mm_tn(lb.x_in, dZx, s.gview(names[0])[:H])
                        if self.cfg.model in ("lstm", "rnn") else _mm_tn(lb.x_in, dZx))
-                if bufs["persist"]:
-                    dbias = self._bias_sum(bufs["db_part"][layer], names)  # fused in BPTT
+                if layer in bufs["pers_layers"]:
+                    dbias = self._bias_sum(self._db_part(bufs, layer), names)  # fused in BPTT
                 else:
                     self.ops.segsum(dZx, None, 1, bufs["colsum"][:, :GW], bufs["ws"], False)
                     dbias = bufs["colsum"][0, :GW]
@@ -1032,6 +1047,13 @@ class NativeBackend:
             self.ops.tok_norm(dz0, wx0, self._tpart, self.store.norm_slot_view())
         else:
             self._token_norm(torch.mm(dz0, wx0.t()))
+
+    @staticmethod
+    def _db_part(bufs, layer: int) -> torch.Tensor:
+        """The rows of the bias-gradient partials the layer's persistent BPTT kernel wrote."""
+        if bufs["pair_bwd"] and layer < 2 * (len(bufs["layers"]) // 2):
+            return bufs["db_part"][layer][: bufs["pair_rows"]]
+        return bufs["db_part"][layer][: max(bufs["layers"][0].hbuf.shape[1] // 16, 1)]
 
     def _bias_sum(self, part: torch.Tensor, names) -> torch.Tensor:
         """Sum the per-batch-group bias partials; for cells with one [GW] bias the sum is

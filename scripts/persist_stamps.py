@@ -72,78 +72,4 @@ names = ["top->poll done", "poll->barrierA", "barrierA->mfma done", "mfma->barri
 for n, v in zip(names, dd.mean(0)):
     print(f"  {n:<26}{v:8.0f} ticks  {100*v/tot:5.1f}%")
 
-# ---- two-layer wavefront forward (lstm2_persist.hip)
-if ops.lstm2_persist_supported(H, B):
-    W1T = (torch.randn(4 * H, H, device=dev) * 0.05).to(torch.bfloat16)
-    X1T = (torch.randn(4 * H, H, device=dev) * 0.05).to(torch.bfloat16)
-    b1 = torch.zeros(4 * H, device=dev)
-    hb1 = torch.zeros_like(hbuf)
-    cb1 = torch.zeros_like(cbuf)
-    g1 = torch.empty_like(gates)
-    hl1 = torch.empty_like(hl)
-    c0 = torch.zeros(B // 32 * (T + 1) * 4, dtype=torch.int32, device=dev)
-    c1 = torch.zeros_like(c0)
-    diag2 = torch.zeros(T + 2, 8, dtype=torch.int64, device=dev)
-
-    def run2():
-        c0.zero_()
-        c1.zero_()
-        ops.lstm2_persist_fwd(WT, W1T, X1T, zx, None, b1, hbuf, cbuf, gates, hl, hb1, cb1, g1,
-                              hl1, c0, c1, err, 1.0, 1 << 22, diag2, hring, hring1)
-    for _ in range(3):
-        run2()
-    torch.cuda.synchronize()
-    ev0.record()
-    run2()
-    ev1.record()
-    torch.cuda.synchronize()
-    d = diag2.cpu().numpy().astype("float64")
-    ms = ev0.elapsed_time(ev1)
-    tot = (d[-2, 0] - d[2, 0]) / (T - 4)
-    names2 = ["top->poll done", "poll->barrierA", "barrierA->mfma done", "mfma->barrierB",
-              "barrierB->epilogue math", "epi->drain done", "drain->next top"]
-    dd = np.diff(np.concatenate([d[2:-2, [0, 1, 2, 3, 4, 5, 6]], d[3:-1, [0]]], 1), axis=1)
-    print(f"PAIR kernel {ms*1e3/(T+2):.2f} us/tick (event); stamps {tot:.0f} ticks/tick; "
-          f"err={int(err.item())}")
-    for n, v in zip(names2, dd.mean(0)):
-        print(f"  {n:<26}{v:8.0f} ticks  {100*v/tot:5.1f}%")
-
-# ---- two-layer wavefront BPTT (lstm2_bwd_persist_kernel)
-if ops.lstm2_bwd_persist_supported(H, B):
-    Wh0 = (torch.randn(H, 4 * H, device=dev) * 0.05).to(torch.bfloat16)
-    Wh1 = (torch.randn(H, 4 * H, device=dev) * 0.05).to(torch.bfloat16)
-    Wx1 = (torch.randn(H, 4 * H, device=dev) * 0.05).to(torch.bfloat16)
-    g0 = torch.rand(T, B, 4 * H, device=dev).to(torch.bfloat16)
-    g1 = torch.rand(T, B, 4 * H, device=dev).to(torch.bfloat16)
-    cb0 = torch.randn(T + 1, B, H, device=dev) * 0.5
-    cb1 = torch.randn(T + 1, B, H, device=dev) * 0.5
-    dz0 = torch.empty(T, B, 4 * H, dtype=torch.bfloat16, device=dev)
-    dz1 = torch.empty_like(dz0)
-    zr0 = torch.empty(2 * B * 4 * H, dtype=torch.bfloat16, device=dev)
-    zr1 = torch.empty_like(zr0)
-    db0 = torch.empty(B // 16, 4 * H, device=dev)
-    db1 = torch.empty_like(db0)
-    c0 = torch.zeros(B // 32 * (T + 1) * 4, dtype=torch.int32, device=dev)
-    c1 = torch.zeros_like(c0)
-    diag3 = torch.zeros(T + 2, 8, dtype=torch.int64, device=dev)
-
-    def run3(dg):
-        c0.zero_()
-        c1.zero_()
-        ops.lstm2_persist_bwd(Wh0, Wh1, Wx1, dtop, g0, cb0, g1, cb1, dz0, dz1, zr0, zr1, db0, db1,
-                              c0, c1, err, 1 << 22, dg)
-    for dg in (None, diag3):
-        for _ in range(3):
-            run3(dg)
-        torch.cuda.synchronize()
-        ev0.record()
-        run3(dg)
-        ev1.record()
-        torch.cuda.synchronize()
-        print(f"PAIR BWD ({'diag' if dg is not None else 'plain'}) {ev0.elapsed_time(ev1)*1e3/(T+2):.2f} us/tick")
-    d = diag3.cpu().numpy().astype("float64")
-    tot = (d[-2, 0] - d[2, 0]) / (T - 4)
-    dd = np.diff(np.concatenate([d[2:-2, [0, 1, 2, 3, 4, 5, 6]], d[3:-1, [0]]], 1), axis=1)
-    print(f"PAIR BWD stamps {tot:.0f} ticks/tick; err={int(err.item())}")
-    for n, v in zip(names2, dd.mean(0)):
-        print(f"  {n:<26}{v:8.0f} ticks  {100*v/tot:5.1f}%")
+# the two-layer wavefront kernels: scripts/pair_bench.py

@@ -1,0 +1,123 @@
+"""Two-layer wavefront kernels (csrc/lstm2_persist.hip) at any batch size: ragged batches padded
+to 32-row groups, and G batch groups per workgroup for batches beyond one group per CU column.
+
+Numerics are checked against the fp32 autograd oracle (ReferenceBackend, TF cell semantics) and
+against themselves across G (the per-group math is identical, so results are bitwise equal)."""
+import pytest
+import torch
+
+from distributed_char_rnn_amd.models.char_rnn import CharRNN
+from distributed_char_rnn_amd.models.params import ModelConfig
+from distributed_char_rnn_amd.models.reference import ReferenceBackend
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+@pytest.fixture(autouse=True)
+def _env(monkeypatch):
+    monkeypatch.setenv("DCR_SPIN_LIMIT", str(1 << 20))
+    monkeypatch.setenv("DCR_PERSIST_MIN_T", "1")
+
+
+def _batch(B, T, V=65, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randint(0, V, (B, T), generator=g, dtype=torch.int32).cuda()
+    y = torch.randint(0, V, (B, T), generator=g, dtype=torch.int32).cuda()
+    return x, y
+
+
+@pytest.mark.parametrize("B,T,H,L,G", [(50, 6, 128, 2, 0), (384, 5, 512, 2, 0),
+                                       (512, 4, 512, 2, 0), (100, 5, 256, 2, 2),
+                                       (70, 4, 128, 4, 3), (1024, 3, 512, 2, 0)])
+def test_pair_matches_oracle(B, T, H, L, G, monkeypatch):
+    monkeypatch.setenv("DCR_PAIR_G", str(G))
+    cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=L)
+    nat = CharRNN(cfg, device="cuda", seed=3)
+    plan = nat.backend._persist_plan(B, True, T)
+    assert plan["pair"] and plan["pair_bwd"], plan
+    assert G == 0 or plan["pair_g"] == G
+    ref = ReferenceBackend(nat.store)
+    x, y = _batch(B, T, seed=B)
+    torch.manual_seed(1)
+    st0 = [tuple(torch.randn(B, H, device="cuda") * 0.5 for _ in range(2)) for _ in range(L)]
+    loss_r, st_r, _ = ref.train_step(x, y, [tuple(s.clone() for s in t) for t in st0])
+    g_ref = nat.store.grad.clone()
+    nat.store.grad.zero_()
+    loss_n, st_n, _ = nat.backend.train_step(x, y, [tuple(s.clone() for s in t) for t in st0])
+    torch.cuda.synchronize()
+    nat.backend.check_errors()
+    assert abs(loss_n.item() - loss_r.item()) < 2e-2 * max(1.0, abs(loss_r.item()))
+    for a_r, a_n in zip(st_r, st_n):
+        for s_r, s_n in zip(a_r, a_n):
+            assert rel(s_n, s_r) < 3e-2
+    for s in nat.store.specs:
+        e = rel(nat.store.gview(s.name), nat.store.view(s.name, g_ref))
+        assert e < 6e-2, (s.name, e)
+
+
+@pytest.mark.parametrize("B,H,Gs", [(256, 512, (1, 2, 4)), (96, 256, (1, 3)), (200, 128, (1, 2, 7))])
+def test_pair_groups_bitwise_equal(B, H, Gs, monkeypatch):
+    """The same batch run with G = 1, 2, 4 ... groups per workgroup: every (row, unit) is
+    computed by the same instructions in the same order, so losses and states are bitwise
+    equal; the gradients agree to the summation order of the in-kernel bias partials."""
+    T = 6
+    cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=2)
+    x, y = _batch(B, T, seed=7)
+    outs = []
+    for G in Gs:
+        monkeypatch.setenv("DCR_PAIR_G", str(G))
+        m = CharRNN(cfg, device="cuda", seed=11)
+        plan = m.backend._persist_plan(B, True, T)
+        if plan["pair_g"] != G:
+            pytest.skip(f"G={G} not co-resident on this GPU")
+        st = m.zero_state(B)
+        for _ in range(2):  # carried state across steps
+            loss, st, _ = m.backend.train_step(x, y, st)
+        torch.cuda.synchronize()
+        m.backend.check_errors()
+        outs.append((loss.item(), m.store.grad.clone(), [s.clone() for t in st for s in t]))
+    for loss, grad, st in outs[1:]:
+        assert loss == outs[0][0]
+        assert rel(grad, outs[0][1]) < 1e-6
+        for a, b in zip(st, outs[0][2]):
+            assert torch.equal(a, b)
+
+
+def test_pair_ragged_batch_equals_per_step_kernels(monkeypatch):
+    """B = 50 (the reference default, train.py:46) through the padded pair kernels vs the
+    per-step kernels: the same bf16 math, agreement to accumulation-order noise."""
+    B, T, H = 50, 12, 128
+    cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=2)
+    a = CharRNN(cfg, device="cuda", seed=5)
+    monkeypatch.setenv("DCR_PERSIST", "0")
+    b = CharRNN(cfg, device="cuda", seed=5)
+    assert a.backend._persist_plan(B, True, T)["pair"]
+    assert not b.backend._persist_plan(B, True, T)["pair"]
+    x, y = _batch(B, T, seed=3)
+    sa, sb = a.zero_state(B), b.zero_state(B)
+    for _ in range(3):
+        la, sa, _ = a.backend.train_step(x, y, sa)
+        lb, sb, _ = b.backend.train_step(x, y, sb)
+    torch.cuda.synchronize()
+    a.backend.check_errors()
+    assert abs(la.item() - lb.item()) < 1e-3
+    assert rel(a.store.grad, b.store.grad) < 1e-2
+    for u, v in zip(sa, sb):
+        for p, q in zip(u, v):
+            assert rel(p, q) < 1e-2
+
+
+def test_pair_plan_covers_large_batches(dcr_ops):
+    """Batches up to G_max x 256 rows (H = 512) plan onto the pair kernels: no cliff to the
+    per-step kernels above B = 256."""
+    for B in (1, 17, 50, 256, 257, 384, 512, 768, 1024):
+        G = int(dcr_ops.lstm2_plan(512, B, 0))
+        assert G >= 1, B
+        nbg = int(dcr_ops.lstm2_nbg(B, G))
+        assert nbg * 32 >= B and nbg % G == 0
+        assert (512 // 16) * (nbg // G) <= dcr_ops.num_cus()

@@ -135,8 +135,8 @@ def test_two_layer_wavefront_equals_single_layer_kernels(B, T, H, monkeypatch):
     a = CharRNN(cfg, device="cuda", seed=9)
     monkeypatch.setenv("DCR_PAIR", "0")
     b = CharRNN(cfg, device="cuda", seed=9)
-    assert a.backend._persist_plan(B, True)["pair"]
-    assert not b.backend._persist_plan(B, True)["pair"]
+    assert a.backend._persist_plan(B, True, T)["pair"]
+    assert not b.backend._persist_plan(B, True, T)["pair"]
     x = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
     sa, sb = a.zero_state(B), b.zero_state(B)
     for _ in range(2):  # carried state across steps
@@ -163,8 +163,8 @@ def test_two_layer_wavefront_bptt_equals_single_layer_kernels(B, T, H, L, monkey
     a = CharRNN(cfg, device="cuda", seed=5)
     monkeypatch.setenv("DCR_PAIR_BWD", "0")
     b = CharRNN(cfg, device="cuda", seed=5)
-    assert a.backend._persist_plan(B, True)["pair_bwd"]
-    assert not b.backend._persist_plan(B, True)["pair_bwd"]
+    assert a.backend._persist_plan(B, True, T)["pair_bwd"]
+    assert not b.backend._persist_plan(B, True, T)["pair_bwd"]
     torch.manual_seed(2)
     x = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
     y = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
