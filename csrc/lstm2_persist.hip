@@ -122,6 +122,23 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     // slot T-1 (by itself)
     const bool signal = act && (L == 0 || t + 1 < T);
     STAMP2(0)
+    // layer-l input projections of step tau (independent of the hand-off): group 0's rows are
+    // loaded before the poll, group g+1's right behind group g's payload (a gathered row needs
+    // its id first; loaded for all groups here, the wait overlaps the poll)
+    auto zx_row = [&](int g) -> const float* {
+      const int b = (col * G + g) * 32 + 16 * J + (lane & 15);
+      if (!(L == 0 && on0 && b < B)) return nullptr;
+      return a.ids ? a.zx0 + (size_t)a.ids[(size_t)tau * B + b] * a.zx_ld
+                   : a.zx0 + ((size_t)tau * B + b) * a.zx_ld;
+    };
+    const float* zrows[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) zrows[g] = zx_row(g);
+    float zxn[4][4] = {};
+    if (zrows[0]) {
+#pragma unroll
+      for (int gt = 0; gt < 4; ++gt) ld4f(zrows[0] + (size_t)gt * H + u0, zxn[gt]);
+    }
     // hand-offs of the previous tick: layer l's slot tau, layer l+1's slot tau-LAG (slot 0 of
     // either is the prep-written initial state)
     const bool pw0 = ld0 && tau >= 1, pw1 = ld1 && tau >= LAG + 1;
@@ -143,14 +160,11 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
       const int b = bg * 32 + 16 * J + (lane & 15);
       const bool live = b < B;
       const size_t bh = (size_t)b * H + u0;
-      // layer-l input projections of step tau (independent of the hand-off)
-      float zx[4][4] = {};
-      if (L == 0 && on0 && live) {
-        const float* zrow = a.ids ? a.zx0 + (size_t)a.ids[(size_t)tau * B + b] * a.zx_ld
-                                  : a.zx0 + ((size_t)tau * B + b) * a.zx_ld;
+      float zx[4][4];
 #pragma unroll
-        for (int gt = 0; gt < 4; ++gt) ld4f(zrow + (size_t)gt * H + u0, zx[gt]);
-      }
+      for (int gt = 0; gt < 4; ++gt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) zx[gt][r] = zxn[gt][r];
       bf16x8 hf0[2][KS], hf1[2][KS];
       {
         // slot 0 is row-major [B, H] (rows >= B read as zero: buffer bounds); later slots come
@@ -184,6 +198,10 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
                             : (unsigned)(((size_t)(bg * 32 + 16 * j + (lane & 15)) * H + kbase +
                                           s * 32 + kq) * sizeof(bf16)));
         }
+      }
+      if (g + 1 < G && zrows[g + 1]) {
+#pragma unroll
+        for (int gt = 0; gt < 4; ++gt) ld4f(zrows[g + 1] + (size_t)gt * H + u0, zxn[gt]);
       }
       if (g > 0) __syncthreads();  // the previous group's epilogue has read the partials
       __builtin_amdgcn_sched_barrier(0);

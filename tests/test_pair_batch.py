@@ -60,15 +60,18 @@ def test_pair_matches_oracle(B, T, H, L, G, monkeypatch):
         assert e < 6e-2, (s.name, e)
 
 
-@pytest.mark.parametrize("B,H,Gs", [(256, 512, (1, 2, 4)), (96, 256, (1, 3)), (200, 128, (1, 2, 7))])
-def test_pair_groups_bitwise_equal(B, H, Gs, monkeypatch):
-    """The same batch run with G = 1, 2, 4 ... groups per workgroup: every (row, unit) is
-    computed by the same instructions in the same order, so losses and states are bitwise
-    equal; the gradients agree to the summation order of the in-kernel bias partials."""
+@pytest.mark.parametrize("B,H,Gs", [(256, 512, (1, 2, 4)), (96, 256, (1, 2, 3)),
+                                    (200, 128, (1, 2, 4))])
+def test_pair_groups_agree(B, H, Gs, monkeypatch):
+    """The same batch run with G = 1, 2, 4 ... groups per workgroup.  For G >= 2 every (row,
+    unit) is computed by the same instructions in the same order, so losses and states are
+    bitwise equal; G = 1 runs the forward's layer l+1 two ticks behind (its input product summed
+    separately), so it agrees to bf16 rounding; gradients also differ in the summation order of
+    the in-kernel bias partials."""
     T = 6
     cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=2)
     x, y = _batch(B, T, seed=7)
-    outs = []
+    outs = {}
     for G in Gs:
         monkeypatch.setenv("DCR_PAIR_G", str(G))
         m = CharRNN(cfg, device="cuda", seed=11)
@@ -80,11 +83,18 @@ def test_pair_groups_bitwise_equal(B, H, Gs, monkeypatch):
             loss, st, _ = m.backend.train_step(x, y, st)
         torch.cuda.synchronize()
         m.backend.check_errors()
-        outs.append((loss.item(), m.store.grad.clone(), [s.clone() for t in st for s in t]))
-    for loss, grad, st in outs[1:]:
-        assert loss == outs[0][0]
-        assert rel(grad, outs[0][1]) < 1e-6
-        for a, b in zip(st, outs[0][2]):
+        outs[G] = (loss.item(), m.store.grad.clone(), [s.clone() for t in st for s in t])
+    ref = outs[Gs[0]]
+    for G, (loss, grad, st) in outs.items():
+        assert abs(loss - ref[0]) < 1e-4
+        assert rel(grad, ref[1]) < 2e-3
+        for a, b in zip(st, ref[2]):
+            assert rel(a, b) < 2e-3
+    multi = [outs[G] for G in Gs if G >= 2]
+    for loss, grad, st in multi[1:]:
+        assert loss == multi[0][0]
+        assert rel(grad, multi[0][1]) < 1e-6
+        for a, b in zip(st, multi[0][2]):
             assert torch.equal(a, b)
 
 
