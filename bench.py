@@ -81,7 +81,7 @@ def main(argv=None) -> int:
     cfg = ModelConfig(model=a.model, vocab_size=a.vocab, rnn_size=a.hidden, num_layers=a.layers,
                       clip_norm=a.clip_norm)
     model = CharRNN(cfg, device=device, seed=1234)
-    opt = TFAdam(model.store, clip=5.0)
+    opt = TFAdam(model.store, clip=5.0, guard=model.error_word())
     sync = GradSync(model.store, world, a.bucket_mb, a.allreduce_dtype)
     sync.broadcast_params(0)
     model.params_changed()

@@ -184,6 +184,7 @@ class NativeBackend:
         self.fused_head = (os.environ.get("DCR_FUSED_HEAD", "1") != "0"
                            and bool(self.ops.head_supported(self.V, self.H)))
         self.err = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self._err_host: Optional[torch.Tensor] = None
         self._side = None
         self._side_used = False
         self._steps = 0
@@ -480,12 +481,17 @@ class NativeBackend:
         return plan
 
     def check_errors(self):
-        """Raise if a persistent kernel hit its spin timeout (forces a device sync)."""
+        """Raise if a persistent kernel hit its spin timeout (forces a device sync).  The word
+        is cleared so the caller may recover (e.g. restore a checkpoint and continue)."""
         v = int(self.err.item())
         if v:
             self.err.zero_()
-            raise RuntimeError(f"persistent recurrent kernel timed out (code {v}); "
-                               "set DCR_PERSIST=0 to use the per-step kernels")
+            if self._err_host is not None:
+                self._err_host.zero_()
+            raise RuntimeError(f"persistent recurrent kernel timed out (code {v}); the "
+                               "optimizer skipped the step's update.  Another process sharing "
+                               "this GPU can cause this (one rank per GPU); DCR_PERSIST=0 "
+                               "selects the per-step kernels")
 
     def _dropout(self, training: bool) -> bool:
         c = self.cfg
@@ -886,9 +892,21 @@ class NativeBackend:
             _release()
         extras = {"logits": logits, "loss": bufs["row_loss"]} if want_extras else None
         self._steps += 1
-        if (persistent or bufs["big_fwd"]) and self._steps % 200 == 1:
-            self.check_errors()
+        if persistent or bufs["big_fwd"]:
+            self._poll_errors()
         return bufs["loss"][0], new_state, extras
+
+    def _poll_errors(self) -> None:
+        """Non-blocking check of the persistent kernels' error word: each step copies it into
+        pinned host memory behind its own work and reads the copy of an earlier step, so a
+        spin timeout raises within a step or two without a device sync.  (The optimizer skips
+        its update on device while the word is set: TFAdam(guard=err).)"""
+        if self._err_host is None:
+            self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        v = int(self._err_host[0])
+        if v:
+            self.check_errors()
+        self._err_host.copy_(self.err, non_blocking=True)
 
     def _embed_grad(self, dXf: torch.Tensor, ids_tm: torch.Tensor, bufs) -> None:
         """dE = segsum(dX_tok, ids) into the gradient buffer.  Wide vocabularies take the

@@ -31,8 +31,13 @@ def lr_for_epoch(learning_rate: float, decay_rate: float, epoch: int) -> float:
 
 class TFAdam:
     def __init__(self, store: ParamStore, beta1: float = 0.9, beta2: float = 0.999,
-                 eps: float = 1e-8, clip: float = 5.0, bf16_mirror: bool = False):
+                 eps: float = 1e-8, clip: float = 5.0, bf16_mirror: bool = False,
+                 guard: Optional[torch.Tensor] = None):
+        """``guard``: a device error word (the persistent kernels' timeout word); while it is
+        non-zero the fused kernel skips the update on device, so a timed-out step never
+        corrupts the weights or the Adam slots."""
         self.store = store
+        self.guard = guard
         self.b1, self.b2, self.eps, self.clip = beta1, beta2, eps, clip
         self.m = torch.zeros_like(store.flat)
         self.v = torch.zeros_like(store.flat)
@@ -69,7 +74,7 @@ class TFAdam:
             mirror = self.mirror.narrow(0, 0, n) if self.mirror is not None else None
             self._ops.adam_clip(p, g, m, v, mirror, self._partials, self.last_norm, lr_t,
                                 self.b1, self.b2, self.eps, self.clip, float(grad_scale), n_norm,
-                                slot)
+                                slot, self.guard)
         else:
             gn = g.narrow(0, 0, n_norm).double()
             sq = (gn * gn).sum() + (slot.double().sum() if slot is not None else 0.0)

@@ -89,6 +89,9 @@ def check_init_from(args, loader) -> str:
 
 def checkpoint_tensors(model: CharRNN, opt: TFAdam, global_step: int, lr: float, epoch: int,
                        batch: int, state=None):
+    """Every tensor of a checkpoint.  ``state`` (``--save_state``): the TBPTT carry after
+    ``batch``, as [world, B, H] per (layer, component) -- each data-parallel rank carries its own
+    rows (see ``gather_state``) -- so ``--resume_exact`` continues bit-for-bit."""
     t = {}
     t.update(model.store.state_dict())
     t.update(opt.slot_state())
@@ -101,6 +104,47 @@ def checkpoint_tensors(model: CharRNN, opt: TFAdam, global_step: int, lr: float,
             for si, s in enumerate(st):
                 t[f"dcr/state/{li}/{si}"] = s.detach().float().cpu()
     return t
+
+
+def gather_state(ctx, state):
+    """[world, B, H] copies of every state tensor (all ranks' carries), on every rank."""
+    out = []
+    for st in state:
+        comps = []
+        for s in st:
+            s = s.detach().float().contiguous()
+            if ctx.enabled:
+                parts = [torch.empty_like(s) for _ in range(ctx.world_size)]
+                torch.distributed.all_gather(parts, s)
+                full = torch.stack(parts)
+            else:
+                full = s.unsqueeze(0)
+            comps.append(full)
+        out.append(tuple(comps))
+    return out
+
+
+def restore_state(model: CharRNN, sd, rank: int, batch: int):
+    """The TBPTT carry saved with the checkpoint (``--save_state``), this rank's rows; None if
+    the checkpoint has none or it does not match the batch shape."""
+    ref = model.zero_state(batch)
+    out = []
+    for li, st in enumerate(ref):
+        comps = []
+        for si, z in enumerate(st):
+            v = sd.get(f"dcr/state/{li}/{si}")
+            if v is None:
+                return None
+            v = torch.as_tensor(np.asarray(v))
+            if v.dim() == z.dim() + 1:  # [world, B, H]
+                if rank >= v.shape[0]:
+                    return None
+                v = v[rank]
+            if tuple(v.shape) != tuple(z.shape):
+                return None
+            comps.append(v.to(device=z.device, dtype=z.dtype))
+        out.append(tuple(comps))
+    return out
 
 
 def restore(model: CharRNN, opt: TFAdam, prefix: str):
@@ -139,11 +183,15 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
     loader = make_loader(args, ctx)
     args.vocab_size = loader.vocab_size
     prefix: Optional[str] = None
-    if args.init_from is not None:
-        prefix = check_init_from(args, loader)
-    elif ctx.world_size > 1 and ckpt.latest_checkpoint(args.save_dir):
-        # MonitoredTrainingSession's chief auto-restores from checkpoint_dir (train.py:157-163)
-        prefix = ckpt.latest_checkpoint(args.save_dir)
+    # Only the chief resolves and reads the checkpoint (save_dir need not be on a shared
+    # filesystem); the restored step counters, Adam slots and TBPTT carries are broadcast below
+    if chief:
+        if args.init_from is not None:
+            prefix = check_init_from(args, loader)
+        elif ctx.world_size > 1 and ckpt.latest_checkpoint(args.save_dir):
+            # MonitoredTrainingSession's chief auto-restores from checkpoint_dir
+            # (train.py:157-163)
+            prefix = ckpt.latest_checkpoint(args.save_dir)
 
     if chief:
         os.makedirs(args.save_dir, exist_ok=True)
@@ -152,9 +200,11 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
                          os.path.join(args.save_dir, "chars_vocab.pkl"))
 
     model = build_model(args, loader.vocab_size, device)
-    opt = TFAdam(model.store, clip=args.grad_clip)
+    # a persistent-kernel timeout makes the optimizer skip its update on device
+    opt = TFAdam(model.store, clip=args.grad_clip, guard=model.error_word())
     global_step = 0
     start_epoch, start_batch = 0, 0
+    sd = None
     if prefix is not None:
         sd = restore(model, opt, prefix)
         global_step = int(sd.get("global_step", 0))
@@ -165,11 +215,26 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
 
     sync = GradSync(model.store, ctx.world_size, getattr(args, "bucket_mb", 8.0),
                     getattr(args, "allreduce_dtype", "fp32"))
+    saved_state = None
     if ctx.world_size > 1:
+        # rank 0's restore -> every rank: parameters, Adam slots, step counters (a rank that
+        # kept opt.t = 0 would use a different lr_t and diverge; one that kept the batch
+        # pointer 0 would run a different number of steps and hang the last all-reduce)
         sync.broadcast_params(0)
         ctx.broadcast_(opt.m)
         ctx.broadcast_(opt.v)
+        meta = torch.tensor([global_step, opt.t, start_epoch, start_batch], dtype=torch.int64,
+                            device=device if ctx.backend == "nccl" else "cpu")
+        ctx.broadcast_(meta)
+        global_step, opt.t, start_epoch, start_batch = (int(v) for v in meta.tolist())
         model.params_changed()
+        if start_batch > 0:
+            saved_state = _broadcast_state(ctx, model, sd, args.batch_size, device)
+    elif sd is not None and start_batch > 0:
+        saved_state = restore_state(model, sd, 0, args.batch_size)
+    if start_batch > 0 and saved_state is None:
+        _log("warning: the checkpoint holds no TBPTT state for this batch shape (train with "
+             "--save_state): the resumed epoch continues from a zero state", rank)
     ctx.start_heartbeat(getattr(args, "heartbeat", 0.0))
 
     nb = ctx.min_int(loader.num_batches)
@@ -207,6 +272,8 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
         b0 = start_batch if e == start_epoch else 0
         if b0:
             loader.pointer = b0
+            if saved_state is not None:  # the carry of the interrupted run's batch b0 - 1
+                state = saved_state
         for b in range(b0, nb):
             t0 = time.time()
             x, y = loader.next_batch()
@@ -236,9 +303,12 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
                 if pending is not None:
                     flush(pending, time.time())
                     pending = None
+                model.check_errors()  # never checkpoint weights of a timed-out step
+                save_st = None
+                if getattr(args, "save_state", False):
+                    save_st = gather_state(ctx, state)  # collective: every rank
                 if chief:
-                    tensors = checkpoint_tensors(model, opt, global_step, lr, e, b,
-                                                 state if getattr(args, "save_state", False) else None)
+                    tensors = checkpoint_tensors(model, opt, global_step, lr, e, b, save_st)
                     path = saver.save(args.save_dir, tensors, step_idx)
                     print("model saved to {}".format(os.path.join(args.save_dir, "model.ckpt")),
                           flush=True)
@@ -249,10 +319,40 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
             break
     if pending is not None:
         flush(pending, time.time())
+    model.check_errors()
     if prof.enabled and chief:
         print(prof.table(), flush=True)
     logger.close()
     return 0
+
+
+def _broadcast_state(ctx, model: CharRNN, sd, batch: int, device):
+    """Rank 0 holds the checkpoint's [world, B, H] carries: broadcast them, each rank keeps its
+    own rows.  None (on every rank) when the checkpoint has none."""
+    ref = model.zero_state(batch)
+    have = torch.zeros(1, dtype=torch.int64, device=device if ctx.backend == "nccl" else "cpu")
+    full = None
+    if ctx.rank == 0 and sd is not None:
+        full = restore_state(model, sd, 0, batch)  # shape check on rank 0's rows
+        if full is not None and all(np.asarray(sd[f"dcr/state/{li}/{si}"]).ndim == 3 and
+                                    np.asarray(sd[f"dcr/state/{li}/{si}"]).shape[0] == ctx.world_size
+                                    for li, st in enumerate(ref) for si in range(len(st))):
+            have.fill_(1)
+    ctx.broadcast_(have)
+    if not int(have.item()):
+        return None
+    out = []
+    for li, st in enumerate(ref):
+        comps = []
+        for si, z in enumerate(st):
+            buf = torch.empty((ctx.world_size,) + tuple(z.shape), dtype=torch.float32,
+                              device=z.device if ctx.backend == "nccl" else "cpu")
+            if ctx.rank == 0:
+                buf.copy_(torch.as_tensor(np.asarray(sd[f"dcr/state/{li}/{si}"])))
+            ctx.broadcast_(buf)
+            comps.append(buf[ctx.rank].to(device=z.device, dtype=z.dtype).clone())
+        out.append(tuple(comps))
+    return out
 
 
 def _step(model: CharRNN, x, y, state, sync: GradSync, want_extras: bool):

@@ -68,6 +68,17 @@ class CharRNN:
     def eval_loss(self, x, y, state: State):
         return self.backend.eval_loss(_as_ids(x, self.device), _as_ids(y, self.device), state)
 
+    def error_word(self) -> Optional[torch.Tensor]:
+        """The native backend's device error word (persistent-kernel spin timeouts), for
+        ``TFAdam(guard=...)``; None on the reference backend."""
+        return getattr(self.backend, "err", None)
+
+    def check_errors(self) -> None:
+        """Raise if a persistent kernel timed out (synchronises the device)."""
+        check = getattr(self.backend, "check_errors", None)
+        if check is not None:
+            check()
+
     def params_changed(self):
         """Call after parameters were modified outside the optimizer (restore/broadcast)."""
         self.store.version += 1

@@ -96,6 +96,9 @@ class GradSync:
         if defer_scale:
             return 1.0 / self.world
         self.store.grad.mul_(1.0 / self.world)
+        # the clip-norm slot holds a SUM OF SQUARES (TF's per-token embedding term, summed over
+        # ranks): averaging the gradients scales it by 1/world^2, not 1/world
+        self.store.norm_slot_view().mul_(1.0 / self.world)
         return 1.0
 
     def broadcast_params(self, src: int = 0):

@@ -147,11 +147,20 @@ class DistContext:
             dist.destroy_process_group()
 
 
-def pick_device(topo: Topology, requested: str = "auto") -> torch.device:
+def pick_device(topo: Topology, requested: str = "auto", log=print) -> torch.device:
     if requested == "cpu":
         return torch.device("cpu")
     if requested in ("auto", "cuda") and torch.cuda.is_available():
         n = torch.cuda.device_count()
+        local_world = topo.local_world_size
+        if local_world > n:
+            # more local ranks than GPUs: ranks share a device.  The persistent recurrent
+            # kernels need every CU of the chip (one workgroup per CU, co-resident grids), so two
+            # processes' grids on one GPU spin into the timeout: use the per-step kernels.
+            if os.environ.get("DCR_PERSIST", "1") != "0":
+                log(f"[rank {topo.rank}] {local_world} local ranks share {n} GPU(s): persistent "
+                    "kernels disabled (DCR_PERSIST=0); run one rank per GPU for speed")
+                os.environ["DCR_PERSIST"] = "0"
         dev = torch.device("cuda", topo.local_rank % max(n, 1))
         torch.cuda.set_device(dev)
         return dev

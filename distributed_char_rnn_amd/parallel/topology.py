@@ -28,6 +28,7 @@ class Topology:
     role: str = "worker"  # worker | ps
     store_host_is_ps: bool = False
     from_env: bool = False
+    local_world_size: int = 1  # ranks on this host (more than its GPUs => shared devices)
 
     @property
     def distributed(self) -> bool:
@@ -51,7 +52,9 @@ def from_env() -> Optional[Topology]:
         return Topology(rank=int(os.environ["RANK"]), world_size=int(os.environ["WORLD_SIZE"]),
                         local_rank=int(os.environ.get("LOCAL_RANK", os.environ["RANK"])),
                         master_addr=os.environ.get("MASTER_ADDR", "127.0.0.1"),
-                        master_port=int(os.environ.get("MASTER_PORT", 29500)), from_env=True)
+                        master_port=int(os.environ.get("MASTER_PORT", 29500)), from_env=True,
+                        local_world_size=int(os.environ.get("LOCAL_WORLD_SIZE",
+                                                            os.environ["WORLD_SIZE"])))
     return None
 
 
@@ -79,5 +82,9 @@ def from_args(args) -> Topology:
                         master_port=port, role="ps", store_host_is_ps=True)
     if not 0 <= args.task_index < len(workers):
         raise ValueError(f"task_index {args.task_index} out of range for {len(workers)} workers")
-    return Topology(rank=args.task_index, world_size=len(workers), local_rank=args.task_index,
-                    master_addr=host, master_port=port, role="worker", store_host_is_ps=ps)
+    hosts = [_split_hostport(w)[0] for w in workers]
+    mine = hosts[args.task_index]
+    local = [i for i, h in enumerate(hosts) if h == mine]
+    return Topology(rank=args.task_index, world_size=len(workers),
+                    local_rank=local.index(args.task_index), master_addr=host, master_port=port,
+                    role="worker", store_host_is_ps=ps, local_world_size=len(local))

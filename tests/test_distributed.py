@@ -33,28 +33,32 @@ def _data(B, T, steps):
     return rng.integers(0, 11, size=(steps, B, T + 1)).astype(np.int32)
 
 
-def _worker(rank, world, port, B, T, steps, out_q, bucket_mb, wire):
+CLIP = 0.05  # small enough that every step clips (the clip norm itself is then under test)
+
+
+def _worker(rank, world, port, B, T, steps, out_q, bucket_mb, wire, defer=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         cfg = ModelConfig(**CFG)
         m = CharRNN(cfg, device="cpu", seed=123)
-        opt = TFAdam(m.store, clip=1.0)
+        opt = TFAdam(m.store, clip=CLIP)
         sync = GradSync(m.store, world, bucket_mb, wire)
         sync.broadcast_params(0)
         data = _data(B * world, T, steps)
         state = m.zero_state(B)
-        losses = []
+        losses, norms = [], []
         for s in range(steps):
             blk = data[s, rank * B:(rank + 1) * B]
             sync.reset()
             loss, state, _ = m.train_step(blk[:, :-1], blk[:, 1:], state, sync)
-            sync.finish()
-            opt.step(0.01)
+            gs = sync.finish(defer_scale=defer)
+            opt.step(0.01, grad_scale=gs)
             losses.append(loss.item())
+            norms.append(float(opt.last_norm))
         if rank == 0:
-            out_q.put((m.store.flat.clone().numpy(), losses))
+            out_q.put((m.store.flat.clone().numpy(), losses, norms))
     finally:
         dist.destroy_process_group()
 
@@ -62,30 +66,39 @@ def _worker(rank, world, port, B, T, steps, out_q, bucket_mb, wire):
 def _single(B, T, steps):
     cfg = ModelConfig(**CFG)
     m = CharRNN(cfg, device="cpu", seed=123)
-    opt = TFAdam(m.store, clip=1.0)
+    opt = TFAdam(m.store, clip=CLIP)
     data = _data(B, T, steps)
     state = m.zero_state(B)
+    norms = []
     for s in range(steps):
         loss, state, _ = m.train_step(data[s, :, :-1], data[s, :, 1:], state)
         opt.step(0.01)
-    return m.store.flat.clone().numpy()
+        norms.append(float(opt.last_norm))
+    return m.store.flat.clone().numpy(), norms
 
 
-@pytest.mark.parametrize("bucket_mb,wire", [(8.0, "fp32"), (0.0005, "fp32")])
-def test_dp_two_ranks_equals_single_process_double_batch(bucket_mb, wire):
+@pytest.mark.parametrize("bucket_mb,wire,defer", [(8.0, "fp32", False), (0.0005, "fp32", False),
+                                                  (8.0, "fp32", True)])
+def test_dp_two_ranks_equals_single_process_double_batch(bucket_mb, wire, defer):
+    """Both averaging paths of GradSync.finish (scale in place / folded into the optimizer),
+    with clipping active every step: the TF clip norm (per-token embedding term, a sum of
+    squares that averages with 1/world^2) must equal the single-process one."""
     B, T, steps, world = 3, 5, 3, 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, B, T, steps, q, bucket_mb, wire))
+    procs = [ctx.Process(target=_worker,
+                         args=(r, world, port, B, T, steps, q, bucket_mb, wire, defer))
              for r in range(world)]
     for p in procs:
         p.start()
-    flat, losses = q.get(timeout=240)
+    flat, losses, norms = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    ref = _single(B * world, T, steps)
+    ref, ref_norms = _single(B * world, T, steps)
+    assert all(n > CLIP for n in ref_norms)  # clipping was active
+    np.testing.assert_allclose(norms, ref_norms, rtol=1e-4)
     np.testing.assert_allclose(flat, ref, rtol=2e-4, atol=2e-6)
     assert all(np.isfinite(losses))
 
@@ -131,3 +144,13 @@ def test_topology_env_wins(monkeypatch):
     monkeypatch.setenv("LOCAL_RANK", "3")
     t = topology.from_args(_ns(worker_hosts="a:1", job_name="worker", task_index=0))
     assert (t.rank, t.world_size, t.local_rank, t.from_env) == (3, 8, 3, True)
+
+
+def test_topology_local_world_from_worker_hosts():
+    """Ranks that share a host share its GPUs: the local rank/world drive the device choice
+    and the shared-device check (process_group.pick_device)."""
+    hosts = "10.0.0.1:9000,10.0.0.1:9001,10.0.0.2:9000,10.0.0.1:9002"
+    t = topology.from_args(_ns(worker_hosts=hosts, job_name="worker", task_index=3))
+    assert (t.rank, t.local_rank, t.local_world_size) == (3, 2, 3)
+    t = topology.from_args(_ns(worker_hosts=hosts, job_name="worker", task_index=2))
+    assert (t.local_rank, t.local_world_size) == (0, 1)

@@ -1,0 +1,114 @@
+"""Exact resume: ``--save_state`` checkpoints the TBPTT carry with the step
+counters, and ``--init_from <dir> --resume_exact`` continues mid-epoch from it, so an
+interrupted run ends with exactly the weights of an uninterrupted one.  The reference restarts
+at epoch 0 with a zero state (train.py:185-190).
+
+Also the data-parallel form with the checkpoint visible to rank 0 only (save_dir on a
+node-local disk): the step counters, Adam slots and every rank's carry come from rank 0.
+CPU, deterministic, so the comparisons are bitwise."""
+import os
+import shutil
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from distributed_char_rnn_amd.utils import checkpoint as ckpt
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+COMMON = ["--synthetic_text", "6000", "--num_epochs", "2", "--batch_size", "4",
+          "--seq_length", "16", "--rnn_size", "16", "--num_layers", "2", "--device", "cpu",
+          "--log_dir", "logs", "--save_every", "4", "--save_state", "--seed", "3"]
+
+
+def _env():
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def _train(cwd, extra):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "train.py")] + COMMON + extra,
+                       cwd=cwd, env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+def _final(save_dir):
+    sd = ckpt.Saver.restore(ckpt.latest_checkpoint(save_dir))
+    return {k: np.asarray(v) for k, v in sd.items()}
+
+
+def _assert_same(a, b):
+    keys = [k for k in a if not k.startswith("dcr/")]
+    assert set(keys) <= set(b)
+    for k in keys:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+def test_kill_and_resume_equals_uninterrupted_run(tmp_path):
+    w = str(tmp_path)
+    _train(w, ["--save_dir", "full"])
+    # the "killed" run stops after 7 steps (checkpoint at step index 4 and the final one at 6)
+    out = _train(w, ["--save_dir", "part", "--max_steps", "7"])
+    assert "model saved" in out
+    _train(w, ["--save_dir", "resumed", "--init_from", "part", "--resume_exact"])
+    a, b = _final(os.path.join(w, "full")), _final(os.path.join(w, "resumed"))
+    assert int(a["global_step"]) == int(b["global_step"])
+    _assert_same(a, b)
+    # the carry matters: the same checkpoint without it resumes from a zero state and ends
+    # elsewhere
+    src = os.path.join(w, "part")
+    prefix = ckpt.latest_checkpoint(src)
+    sd = {k: v for k, v in ckpt.Saver.restore(prefix).items() if not k.startswith("dcr/state/")}
+    dst = os.path.join(w, "part_nostate")
+    os.makedirs(dst)
+    for f in ("config.pkl", "chars_vocab.pkl"):
+        shutil.copy(os.path.join(src, f), dst)
+    ckpt.Saver().save(dst, sd, int(prefix.rsplit("-", 1)[1]))
+    out = _train(w, ["--save_dir", "resumed2", "--init_from", "part_nostate", "--resume_exact"])
+    assert "zero state" in out
+    c = _final(os.path.join(w, "resumed2"))
+    assert not np.array_equal(a["embedding"], c["embedding"])
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _dp(dirs, extra):
+    port = _free_port()
+    workers = f"127.0.0.1:{port},127.0.0.1:{port + 1}"
+    procs = []
+    for i, d in enumerate(dirs):
+        cmd = ([sys.executable, os.path.join(ROOT, "train.py")] + COMMON + extra +
+               ["--distributed", "--worker_hosts", workers, "--job_name", "worker",
+                "--task_index", str(i), "--dist_timeout", "120"])
+        procs.append(subprocess.Popen(cmd, cwd=d, env=_env(), stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = [p.communicate(timeout=300)[0] for p in procs]
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o
+    return outs
+
+
+@pytest.mark.slow
+def test_dp_resume_with_checkpoint_on_rank0_only(tmp_path):
+    """Two gloo ranks in different working directories: only rank 0's save_dir exists."""
+    r0, r1 = tmp_path / "node0", tmp_path / "node1"
+    r0.mkdir()
+    r1.mkdir()
+    _dp([str(r0), str(r1)], ["--save_dir", "full"])
+    _dp([str(r0), str(r1)], ["--save_dir", "part", "--max_steps", "5"])
+    assert not (r1 / "part" / "checkpoint").exists()  # the non-chief never writes
+    outs = _dp([str(r0), str(r1)], ["--save_dir", "resumed", "--init_from", "part",
+                                     "--resume_exact"])
+    assert "restored" in outs[0]
+    _assert_same(_final(str(r0 / "full")), _final(str(r0 / "resumed")))
