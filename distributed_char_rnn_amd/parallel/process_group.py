@@ -104,22 +104,31 @@ class DistContext:
             os._exit(EXIT_PEER_LOST)
 
         def run():
-            failures = 0
+            # Each rank publishes a monotonically increasing beat counter; rank 0 notes, on its
+            # own monotonic clock, when each rank's counter last moved (no cross-host wall
+            # clocks: skew between hosts cannot declare a healthy rank dead)
+            failures, beat = 0, 0
+            last_seen = {}  # rank -> (counter, monotonic time it last changed)
             while not self._hb_stop.wait(period):
                 try:
-                    self.store.set(f"hb/{self.rank}", str(time.time()))
+                    beat += 1
+                    self.store.set(f"hb/{self.rank}", str(beat))
                     if self.store.check(["abort"]):
                         lost("abort: " + self.store.get("abort").decode())
                     if self.rank == 0:
-                        now = time.time()
+                        now = time.monotonic()
                         for r in range(self.world_size):
                             try:
-                                ts = float(self.store.get(f"hb/{r}").decode())
+                                c = int(self.store.get(f"hb/{r}").decode())
                             except Exception:
                                 continue
-                            if now - ts > 3 * period:
-                                self.store.set("abort", f"rank {r} silent for {now - ts:.1f}s")
-                                lost(f"rank {r} silent for {now - ts:.1f}s")
+                            prev = last_seen.get(r)
+                            if prev is None or prev[0] != c:
+                                last_seen[r] = (c, now)
+                            elif now - prev[1] > 3 * period:
+                                msg = f"rank {r} silent for {now - prev[1]:.1f}s"
+                                self.store.set("abort", msg)
+                                lost(msg)
                     failures = 0
                 except Exception:
                     if self._hb_stop.is_set():
@@ -128,7 +137,7 @@ class DistContext:
                     if failures >= 3:  # the store (rank 0 / ps) is gone
                         lost("rendezvous store unreachable")
 
-        self.store.set(f"hb/{self.rank}", str(time.time()))
+        self.store.set(f"hb/{self.rank}", "0")
         self._hb_thread = threading.Thread(target=run, daemon=True, name="dcr-heartbeat")
         self._hb_thread.start()
 
