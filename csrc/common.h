@@ -33,12 +33,16 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// Activations.  __expf lowers to v_exp_f32 (base-2) with one multiply; accuracy ~1 ulp-ish,
-// well inside bf16 operand noise.  tanh via 2*sigmoid(2x)-1 keeps one transcendental.
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// Activations.  __expf lowers to v_exp_f32 (base-2) with one multiply and the reciprocal to
+// v_rcp_f32 (1 ulp): two instructions.  A plain `1.0f / y` is an IEEE division, a ~10-
+// instruction v_div_scale / v_rcp / 4 x fma / v_div_fmas / v_div_fixup sequence: with 5
+// activations per cell unit it made the LSTM epilogue the longest phase of a persistent
+// kernel's tick (profiles/r2_pair_groups.md).  Both forms saturate cleanly: rcp(inf) = 0.
+__device__ __forceinline__ float rcpf_(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float sigmoidf_(float x) { return rcpf_(1.0f + __expf(-x)); }
 __device__ __forceinline__ float tanhf_(float x) {
   // tanh(x) = 1 - 2/(exp(2x)+1): saturates cleanly to +-1 for large |x|.
-  return 1.0f - 2.0f / (__expf(2.0f * x) + 1.0f);
+  return 1.0f - 2.0f * rcpf_(__expf(2.0f * x) + 1.0f);
 }
 __device__ __forceinline__ float reluf_(float x) { return x > 0.f ? x : 0.f; }
 

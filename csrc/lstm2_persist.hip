@@ -32,9 +32,10 @@
 
 namespace dcr {
 
-#define STAMP2(i)                                                                   \
+// s_memtime stamps of workgroup 0 (diagnostics, scripts/pair_bench.py --stamps): diag[tick][g][i]
+#define STAMPG(g, i)                                                                \
   if (a.diag && blockIdx.x == 0 && threadIdx.x == 0)                                \
-    a.diag[(size_t)tau * 8 + (i)] = __builtin_amdgcn_s_memtime();
+    a.diag[((size_t)tau * G + (g)) * 8 + (i)] = __builtin_amdgcn_s_memtime();
 
 constexpr int kPairMaxG = 4;
 
@@ -121,7 +122,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     // this role's slot t+1 is read by a later tick: layer l's up to slot T, layer l+1's up to
     // slot T-1 (by itself)
     const bool signal = act && (L == 0 || t + 1 < T);
-    STAMP2(0)
+    STAMPG(0, 0)
     // layer-l input projections of step tau (independent of the hand-off): group 0's rows are
     // loaded before the poll, group g+1's right behind group g's payload (a gathered row needs
     // its id first; loaded for all groups here, the wait overlaps the poll)
@@ -150,12 +151,13 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
                                               : cnt1 + (size_t)(tau - LAG) * 4,
                                           target, a.spin_limit, a.err, 9u);
     }
-    STAMP2(1)
+    STAMPG(0, 1)
     // (also orders this tick's first partial stores after the previous tick's epilogue reads)
     __syncthreads();
-    STAMP2(2)
+    STAMPG(0, 2)
 #pragma unroll
     for (int g = 0; g < G; ++g) {
+      STAMPG(g, 7)  // group phase start
       const int bg = col * G + g;
       const int b = bg * 32 + 16 * J + (lane & 15);
       const bool live = b < B;
@@ -245,9 +247,9 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
                 make_float4(acc[gt][0], acc[gt][1], acc[gt][2], acc[gt][3]);
         }
       }
-      STAMP2(3)
+      STAMPG(g, 3)
       __syncthreads();
-      STAMP2(4)
+      STAMPG(g, 4)
       // (G = 1) layer l+1's x-part of its step tau-1 (next tick) from slot tau of layer l
       auto do_stash = [&]() {
         if constexpr (G == 1) {
@@ -289,14 +291,14 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
           c[g][r] = gf[r] * c[g][r] + gi[r] * gj[r];
           h[r] = go[r] * tanhf_(c[g][r]);
         }
-        STAMP2(5)
+        STAMPG(g, 5)
         st4bf_sc1(ringL + (size_t)((t + 1) & 1) * ringsz + frag_index(b, u0, H), h[0], h[1], h[2],
                   h[3]);
         do_stash();  // MFMAs while the ring stores drain
         if (g == G - 1 && signal) {
           // one arrival per wave and tick, for all its groups' ring stores
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          STAMP2(6)
+          STAMPG(g, 6)
           if (lane == 0)
             __hip_atomic_fetch_add((L ? cnt1 : cnt0) + (size_t)(t + 1) * 4, 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -409,7 +411,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
       const int b = (col * G + g) * 32 + 16 * J + (lane & 15);
       const bool live = b < B;
       const size_t bh = (size_t)b * H + u0;
-      STAMP2(0)
+      STAMPG(g, 0)
       // recurrence-independent epilogue operands, issued before the wait (padded rows: zero)
       // (gates stay packed bf16 until the epilogue: registers are the limit here)
       bf16x4 g4[4];
@@ -464,7 +466,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
           dc[r] = dcv * gf[r];
         }
         *reinterpret_cast<float4*>(&dcs[g][w][lane][0]) = make_float4(dc[0], dc[1], dc[2], dc[3]);
-        STAMP2(5)
+        STAMPG(g, 5)
         // layer l+1's dZ_t feeds both layers at the next tick (t >= 0); layer l's only itself
         if (L || t >= 1) {
           bf16* const zr = zrL + (size_t)(t & 1) * slabn;
@@ -474,7 +476,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
           st4bf_sc1(zr + frag_index(b, 3 * H + u0, G4H), dO[0], dO[1], dO[2], dO[3]);
           if (g == G - 1) {  // one arrival per wave and tick, for all its groups' ring stores
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            STAMP2(6)
+            STAMPG(g, 6)
             if (lane == 0)
               __hip_atomic_fetch_add(cntL + (size_t)t * 4, 1u, __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
@@ -510,11 +512,11 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
                        : !poll_counter(ld1 ? cnt1 + (size_t)s1 * 4 : cnt0 + (size_t)s0 * 4,
                                        target, a.spin_limit, a.err, 10u);
           }
-          STAMP2(1)
+          STAMPG(g, 1)
         }
         // (for g > 0: the previous group's epilogue has read the partials)
         __syncthreads();
-        STAMP2(2)
+        STAMPG(g, 2)
         const size_t slab = sizeof(bf16) * slabn;
         const __amdgpu_buffer_rsrc_t r1 = make_rsrc(a.zring1 + (size_t)(s1 & 1) * slabn, slab);
         const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.zring0 + (size_t)(s0 & 1) * slabn, slab);
@@ -562,9 +564,9 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
                 make_float4(acc0[0], acc0[1], acc0[2], acc0[3]);
           }
         }
-        STAMP2(3)
+        STAMPG(g, 3)
         __syncthreads();
-        STAMP2(4)
+        STAMPG(g, 4)
         // layer l's dtop for its next tick, off the critical path (see xsl), issued right after
         // this wave's arrival: behind its row-major stores the compiler's conservative vmcnt waits
         // would make the MFMAs wait for their write-through
@@ -586,6 +588,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
       } else if (act) {
         epilogue([] {});
       }
+      STAMPG(g, 7)  // group phase end
     }
   }
   // bias-gradient partial of this role's 16-row tile column: reduce the 16 batch lanes

@@ -765,8 +765,8 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
   a.forget_bias = (float)forget_bias;
   a.spin_limit = (unsigned)spin_limit;
   if (has(diag)) {
-    TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)(T + 2) * 8,
-                "diag must hold [T+2, 8] int64 (ticks 0..T+1)");
+    TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)(T + 2) * G * 8,
+                "diag must hold [T+2, G, 8] int64 (ticks 0..T+1)");
     a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());
   }
   a.hring0 = ptr<bf16>(hring0);
@@ -831,8 +831,8 @@ void lstm2_persist_bwd(const at::Tensor& Wh0, const at::Tensor& Wh1, const at::T
   a.B = B; a.H = H; a.T = T; a.G = (int)G; a.nbg = nbg;
   a.spin_limit = (unsigned)spin_limit;
   if (has(diag)) {
-    TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)(T + 2) * 8,
-                "diag must hold [T+2, 8] int64 (ticks 0..T+1)");
+    TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)(T + 2) * G * 8,
+                "diag must hold [T+2, G, 8] int64 (ticks 0..T+1)");
     a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());
   }
   const int rc = dcr::launch_lstm2_bwd_persist(a, num_cus(), cur_stream());

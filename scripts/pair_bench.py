@@ -14,15 +14,40 @@ import torch
 
 from distributed_char_rnn_amd.ops import native
 
-NAMES = ["top->poll done", "poll->barrierA", "barrierA->mfma done", "mfma->barrierB",
-         "barrierB->epilogue math", "epi->drain done", "drain->next top"]
+FWD_TICK = ["tick: poll", "tick: barrier"]
+FWD_GROUP = [(7, 3, "start->MFMA done (payload + MFMA)"), (3, 4, "->barrier B"),
+             (4, 5, "->epilogue math"), (5, 6, "->drain done (last group)")]
+BWD_GROUP = [(0, 1, "start->poll done (group 0)"), (1, 2, "->barrier A"),
+             (2, 3, "->MFMA done (payload + MFMA)"), (3, 4, "->barrier B"),
+             (4, 5, "->epilogue math"), (5, 6, "->drain done (last group)"),
+             (6, 7, "->group end (stash, dz stores)")]
 
 
-def stamps(d, n_ticks):
-    d = d.cpu().numpy().astype("float64")
-    tot = (d[n_ticks - 2, 0] - d[2, 0]) / (n_ticks - 4)
-    dd = np.diff(np.concatenate([d[2:n_ticks - 2, :7], d[3:n_ticks - 1, [0]]], 1), axis=1)
-    return tot, dd.mean(0)
+def stamps(d, n_ticks, G, bwd):
+    """Mean per-tick phase durations (s_memtime ticks) of workgroup 0 over the steady ticks."""
+    d = d.cpu().numpy().astype("float64").reshape(-1, G, 8)[:n_ticks]
+    lo, hi = 3, n_ticks - 3
+    out = []
+    tick = (d[hi, 0, 0 if not bwd else 0] - d[lo, 0, 0]) / (hi - lo)
+    if not bwd:
+        out.append(("tick start->poll done", np.mean(d[lo:hi, 0, 1] - d[lo:hi, 0, 0])))
+        out.append(("poll->barrier A", np.mean(d[lo:hi, 0, 2] - d[lo:hi, 0, 1])))
+    for g in range(G):
+        rows = FWD_GROUP if not bwd else BWD_GROUP
+        for a, b, name in rows:
+            if (b == 6 or a == 6) and g != G - 1:
+                continue
+            if bwd and (a, b) in ((0, 1), (1, 2)) and g > 0:
+                if (a, b) == (0, 1):
+                    continue
+                a = 0
+            v = np.mean(d[lo:hi, g, b] - d[lo:hi, g, a])
+            out.append((f"g{g} {name}", v))
+        if not bwd:
+            nxt = d[lo:hi, g + 1, 7] if g + 1 < G else d[lo + 1:hi + 1, 0, 0]
+            last = 6 if g == G - 1 else 5
+            out.append((f"g{g} ->group end", np.mean(nxt - d[lo:hi, g, last])))
+    return tick, out
 
 
 def run(ops, H, T, B, G, want_stamps, reps=5):
@@ -43,7 +68,7 @@ def run(ops, H, T, B, G, want_stamps, reps=5):
     hr0, hr1 = (torch.empty(2 * Bp * H, dtype=torch.bfloat16, device=dev) for _ in range(2))
     cnt = torch.zeros(2, nbg * (T + 1) * 4, dtype=torch.int32, device=dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
-    dfw = torch.zeros(T + 2, 8, dtype=torch.int64, device=dev) if want_stamps else None
+    dfw = torch.zeros(T + 2, G, 8, dtype=torch.int64, device=dev) if want_stamps else None
 
     def fwd(diag=None):
         cnt.zero_()
@@ -55,7 +80,7 @@ def run(ops, H, T, B, G, want_stamps, reps=5):
     dz0, dz1 = (torch.empty(T, B, 4 * H, dtype=torch.bfloat16, device=dev) for _ in range(2))
     zr0, zr1 = (torch.empty(2 * Bp * 4 * H, dtype=torch.bfloat16, device=dev) for _ in range(2))
     db0, db1 = (torch.empty(2 * nbg // G, 4 * H, device=dev) for _ in range(2))
-    dbw = torch.zeros(T + 2, 8, dtype=torch.int64, device=dev) if want_stamps else None
+    dbw = torch.zeros(T + 2, G, 8, dtype=torch.int64, device=dev) if want_stamps else None
 
     def bwd(diag=None):
         cnt.zero_()
@@ -81,8 +106,8 @@ def run(ops, H, T, B, G, want_stamps, reps=5):
         fwd(dfw)
         bwd(dbw)
         torch.cuda.synchronize()
-        out["stamps_fwd"] = stamps(dfw, fticks)
-        out["stamps_bwd"] = stamps(dbw, T + 2)
+        out["stamps_fwd"] = stamps(dfw, fticks, G, False)
+        out["stamps_bwd"] = stamps(dbw, T + 2, G, True)
     return out
 
 
@@ -107,9 +132,9 @@ def main():
             for k in ("stamps_fwd", "stamps_bwd"):
                 if k in o:
                     tot, parts = o[k]
-                    print(f"   {k}: {tot:.0f} s_memtime ticks per tick (group 0 phase of WG 0)")
-                    for n, v in zip(NAMES, parts):
-                        print(f"     {n:<26}{v:8.0f}  {100 * v / tot:5.1f}%")
+                    print(f"   {k}: {tot:.0f} s_memtime ticks per tick (workgroup 0)")
+                    for n, v in parts:
+                        print(f"     {n:<40}{v:8.0f}  {100 * v / tot:5.1f}%")
 
 
 if __name__ == "__main__":
