@@ -43,6 +43,10 @@ def parse(argv=None):
     ap.add_argument("--allreduce_dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--clip_norm", default="tf", choices=["tf", "dense"],
                     help="embedding term of the clip norm (default: TF per-token semantics)")
+    ap.add_argument("--input_keep_prob", type=float, default=1.0,
+                    help="dropout (DropoutWrapper input keep prob; default off as in the reference)")
+    ap.add_argument("--output_keep_prob", type=float, default=1.0,
+                    help="dropout (DropoutWrapper output + embedding keep prob)")
     ap.add_argument("--profile", action="store_true", help="print a per-phase timing table")
     ap.add_argument("--dist_backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="auto = nccl (RCCL over xGMI) on GPUs; gloo = multi-rank rehearsal on "
@@ -79,7 +83,8 @@ def main(argv=None) -> int:
     rank, world = max(ctx.rank, 0), ctx.world_size
 
     cfg = ModelConfig(model=a.model, vocab_size=a.vocab, rnn_size=a.hidden, num_layers=a.layers,
-                      clip_norm=a.clip_norm)
+                      clip_norm=a.clip_norm, input_keep_prob=a.input_keep_prob,
+                      output_keep_prob=a.output_keep_prob)
     model = CharRNN(cfg, device=device, seed=1234)
     opt = TFAdam(model.store, clip=5.0, guard=model.error_word())
     sync = GradSync(model.store, world, a.bucket_mb, a.allreduce_dtype)
@@ -156,6 +161,7 @@ def main(argv=None) -> int:
             "vs_torch_nn_lstm_miopen": (cps / (MIOPEN_1GPU_CPS * world)
                                         if (a.model, a.hidden, a.layers, T, B) ==
                                         ("lstm", 512, 2, 128, 256) else None),
+            "keep_prob": [a.input_keep_prob, a.output_keep_prob],
             "final_loss": final_loss,
         }
         print(json.dumps(out), flush=True)

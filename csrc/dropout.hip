@@ -1,0 +1,109 @@
+// Dropout masks as bits (K3 of SURVEY.md §2.3) for the DropoutWrapper(input_keep_prob,
+// output_keep_prob) stack and the embedding dropout of the reference (model.py:31-34, 58-59).
+//
+// One mask per layer input (the embedding dropout x input dropout for layer 0, the output
+// dropout of layer l-1 x the input dropout of layer l for l > 0: a product of independent
+// Bernoulli draws is one Bernoulli draw of the product keep probability) plus one for the top
+// layer's output.  A mask is a [T, B, K/8] byte tensor (time-major rows r = t*B + b, bit i of
+// byte (r, j) = element (r, 8j + i)): 1/16 of a bf16 mask's bytes, regenerated per step from a
+// counter-based hash of (seed, stream, element) so the backward pass and the tests see exactly
+// the forward's draws.  Consumers: the persistent pair kernels (lstm2_persist.hip) read the
+// bits of their fragments in-kernel; everything else goes through the apply kernels below.
+#include "common.h"
+#include "kernels.h"
+
+namespace dcr {
+
+constexpr int kDropThreads = 256;
+
+// thread -> 32 consecutive elements (4 bytes, one dword store)
+__global__ void __launch_bounds__(kDropThreads) dropout_bits_kernel(
+    unsigned* __restrict__ bits, int64_t nwords, uint64_t seed, uint64_t stream, float keep) {
+  for (int64_t i = blockIdx.x * (int64_t)kDropThreads + threadIdx.x; i < nwords;
+       i += (int64_t)gridDim.x * kDropThreads) {
+    unsigned w = 0;
+#pragma unroll 8
+    for (int e = 0; e < 32; ++e)
+      w |= (uniform01(seed, stream, (uint64_t)i * 32 + e) < keep ? 1u : 0u) << e;
+    bits[i] = w;
+  }
+}
+
+// out[r, k] = in[r, k] * (bit ? scale : 0) for 8 consecutive k per thread (one mask byte).
+// In/out may alias (in place).  Row strides in elements.
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(kDropThreads) mask_apply_kernel(
+    const TI* __restrict__ in, int64_t ld_in, TO* __restrict__ out, int64_t ld_out,
+    const uint8_t* __restrict__ bits, int64_t rows, int K, float scale) {
+  const int kb = K / 8;
+  const int64_t n = rows * kb;
+  for (int64_t i = blockIdx.x * (int64_t)kDropThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kDropThreads) {
+    const int64_t r = i / kb;
+    const int j = (int)(i - r * kb);
+    const unsigned m = bits[i];
+    const TI* src = in + r * ld_in + 8 * j;
+    TO* dst = out + r * ld_out + 8 * j;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dst[e] = (TO)((m >> e & 1u) ? (float)src[e] * scale : 0.f);
+  }
+}
+
+// out[r, k] = E[ids[r], k] * (bit ? scale : 0): the masked layer-0 input rows
+__global__ void __launch_bounds__(kDropThreads) embed_dropout_kernel(
+    const int* __restrict__ ids, const float* __restrict__ E, const uint8_t* __restrict__ bits,
+    bf16* __restrict__ out, int64_t rows, int K, float scale) {
+  const int kb = K / 8;
+  const int64_t n = rows * kb;
+  for (int64_t i = blockIdx.x * (int64_t)kDropThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kDropThreads) {
+    const int64_t r = i / kb;
+    const int j = (int)(i - r * kb);
+    const unsigned m = bits ? bits[i] : 0xFFu;
+    const float4* src = reinterpret_cast<const float4*>(E + (int64_t)ids[r] * K + 8 * j);
+    const float4 a = src[0], b = src[1];
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf((m >> e & 1u) ? v[e] * scale : 0.f);
+    *reinterpret_cast<bf16x8*>(out + r * K + 8 * j) = o;
+  }
+}
+
+static int drop_grid(int64_t n) {
+  const int64_t b = (n + kDropThreads - 1) / kDropThreads;
+  return (int)(b < 4096 ? (b > 0 ? b : 1) : 4096);
+}
+
+void launch_dropout_bits(uint8_t* bits, int64_t nbytes, uint64_t seed, uint64_t stream,
+                         float keep, hipStream_t s) {
+  const int64_t nw = nbytes / 4;
+  dropout_bits_kernel<<<drop_grid(nw), kDropThreads, 0, s>>>(reinterpret_cast<unsigned*>(bits),
+                                                              nw, seed, stream, keep);
+}
+
+void launch_mask_apply(const void* in, bool in_bf16, int64_t ld_in, void* out, bool out_bf16,
+                       int64_t ld_out, const uint8_t* bits, int64_t rows, int K, float scale,
+                       hipStream_t s) {
+  const int g = drop_grid(rows * (K / 8));
+  if (in_bf16 && out_bf16)
+    mask_apply_kernel<bf16, bf16><<<g, kDropThreads, 0, s>>>(
+        (const bf16*)in, ld_in, (bf16*)out, ld_out, bits, rows, K, scale);
+  else if (in_bf16)
+    mask_apply_kernel<bf16, float><<<g, kDropThreads, 0, s>>>(
+        (const bf16*)in, ld_in, (float*)out, ld_out, bits, rows, K, scale);
+  else if (out_bf16)
+    mask_apply_kernel<float, bf16><<<g, kDropThreads, 0, s>>>(
+        (const float*)in, ld_in, (bf16*)out, ld_out, bits, rows, K, scale);
+  else
+    mask_apply_kernel<float, float><<<g, kDropThreads, 0, s>>>(
+        (const float*)in, ld_in, (float*)out, ld_out, bits, rows, K, scale);
+}
+
+void launch_embed_dropout(const int* ids, const float* E, const uint8_t* bits, bf16* out,
+                          int64_t rows, int K, float scale, hipStream_t s) {
+  embed_dropout_kernel<<<drop_grid(rows * (K / 8)), kDropThreads, 0, s>>>(ids, E, bits, out, rows,
+                                                                          K, scale);
+}
+
+}  // namespace dcr

@@ -112,6 +112,15 @@ int xent_num_partials(int N);
 void launch_xent(const float* logits, const int* targets, int N, int V, float grad_scale,
                  float* row_loss, bf16* dlogits, float* partial, float* loss_out, hipStream_t s);
 
+// ---- dropout.hip: bit masks ([rows, K/8] bytes) -----------------------------------------------
+void launch_dropout_bits(uint8_t* bits, int64_t nbytes, uint64_t seed, uint64_t stream,
+                         float keep, hipStream_t s);
+void launch_mask_apply(const void* in, bool in_bf16, int64_t ld_in, void* out, bool out_bf16,
+                       int64_t ld_out, const uint8_t* bits, int64_t rows, int K, float scale,
+                       hipStream_t s);
+void launch_embed_dropout(const int* ids, const float* E, const uint8_t* bits, bf16* out,
+                          int64_t rows, int K, float scale, hipStream_t s);
+
 // ---- embed.hip --------------------------------------------------------------------------
 int segsum_rows_per_chunk(int N);
 size_t segsum_workspace_floats(int N, int W, int V);
@@ -204,6 +213,8 @@ struct Lstm2Args {
   int G, nbg;           // batch groups per workgroup; 32-row batch groups (multiple of G)
   float forget_bias;
   unsigned spin_limit;
+  const uint8_t* xmask; // optional dropout bits of layer l+1's input [T, B, H/8] (dropout.hip)
+  float xscale;         //   and their 1/keep
 };
 // batch groups per workgroup for the two-layer kernels at (H, B) (force > 0: only that value),
 // 0 = unsupported
@@ -229,6 +240,10 @@ struct Lstm2BwdArgs {
   int B, H, T;
   int G, nbg;           // as Lstm2Args; zring0/1 hold [2, nbg*32, 4H]
   unsigned spin_limit;
+  const uint8_t* xmask; // optional dropout bits of layer l+1's input [T, B, H/8]: layer l's dtop
+  float xscale;
+  const uint8_t* omask; // optional dropout bits of layer l+1's output [T, B, H/8]: dtop1
+  float oscale;
 };
 int launch_lstm2_bwd_persist(const Lstm2BwdArgs& a, int cus, hipStream_t s);
 

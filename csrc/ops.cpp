@@ -705,6 +705,59 @@ void lstm_big_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::optiona
 // ------------------------------------------------------------------------------------------
 static int lstm2_nbg(int B, int G) { return ((B + 31) / 32 + G - 1) / G * G; }
 
+// dropout bit masks (dropout.hip): [T, B, H/8] uint8, time-major rows
+static const uint8_t* drop_bits(const c10::optional<at::Tensor>& m, int T, int B, int H,
+                                const char* name) {
+  if (!has(m)) return nullptr;
+  TORCH_CHECK(m->is_cuda() && m->is_contiguous() && m->scalar_type() == at::kByte, name,
+              " must be a contiguous uint8 GPU tensor");
+  TORCH_CHECK(m->numel() == (int64_t)T * B * (H / 8), name, " must be [T, B, H/8]");
+  return reinterpret_cast<const uint8_t*>(m->data_ptr());
+}
+
+void dropout_bits(at::Tensor& bits, int64_t seed, int64_t stream, double keep) {
+  TORCH_CHECK(bits.is_cuda() && bits.is_contiguous() && bits.scalar_type() == at::kByte,
+              "bits must be a contiguous uint8 GPU tensor");
+  TORCH_CHECK(bits.numel() % 4 == 0 && (reinterpret_cast<uintptr_t>(bits.data_ptr()) & 3) == 0,
+              "bits: a whole number of aligned 32-bit words");
+  dcr::launch_dropout_bits(reinterpret_cast<uint8_t*>(bits.data_ptr()), bits.numel(),
+                           (uint64_t)seed, (uint64_t)stream, (float)keep, cur_stream());
+}
+
+void mask_apply(const at::Tensor& in, const at::Tensor& bits, double scale, at::Tensor& out) {
+  TORCH_CHECK(in.is_cuda() && out.is_cuda() && in.dim() == 2 && out.dim() == 2 &&
+                  in.sizes() == out.sizes(), "mask_apply: 2-D GPU tensors of equal shape");
+  TORCH_CHECK(in.stride(1) == 1 && out.stride(1) == 1, "mask_apply: unit column stride");
+  const int64_t R = in.size(0);
+  const int K = (int)in.size(1);
+  TORCH_CHECK(K % 8 == 0, "mask_apply: K % 8 == 0");
+  for (const at::Tensor* t : {&in, (const at::Tensor*)&out})
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16 || t->scalar_type() == at::kFloat,
+                "mask_apply: bf16 or fp32");
+  TORCH_CHECK(bits.is_cuda() && bits.is_contiguous() && bits.scalar_type() == at::kByte &&
+                  bits.numel() == R * (K / 8), "mask_apply: bits must be [rows, K/8] uint8");
+  dcr::launch_mask_apply(in.data_ptr(), in.scalar_type() == at::kBFloat16, in.stride(0),
+                         out.data_ptr(), out.scalar_type() == at::kBFloat16, out.stride(0),
+                         reinterpret_cast<const uint8_t*>(bits.data_ptr()), R, K, (float)scale,
+                         cur_stream());
+}
+
+void embed_dropout(const at::Tensor& ids, const at::Tensor& E, const c10::optional<at::Tensor>& bits,
+                   double scale, at::Tensor& out) {
+  check_seq(ids, at::kInt, "ids");
+  check_seq(E, at::kFloat, "E");
+  check_seq(out, at::kBFloat16, "out");
+  const int64_t R = ids.numel();
+  const int K = (int)E.size(1);
+  TORCH_CHECK(K % 8 == 0 && out.numel() == R * K, "embed_dropout: out [rows, K], K % 8 == 0");
+  if (has(bits))
+    TORCH_CHECK(bits->is_cuda() && bits->is_contiguous() && bits->scalar_type() == at::kByte &&
+                    bits->numel() == R * (K / 8), "embed_dropout: bits [rows, K/8] uint8");
+  dcr::launch_embed_dropout(ptr<int>(ids), ptr<float>(E),
+                            has(bits) ? reinterpret_cast<const uint8_t*>(bits->data_ptr()) : nullptr,
+                            ptr<bf16>(out), R, K, (float)scale, cur_stream());
+}
+
 static void check_lstm2_counters(const at::Tensor& c, int nbg, int T) {
   TORCH_CHECK(c.is_cuda() && c.scalar_type() == at::kInt && c.is_contiguous() &&
                   c.numel() >= (int64_t)nbg * (T + 1) * 4, "counter buffer too small");
@@ -720,7 +773,8 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
                        int64_t spin_limit, at::Tensor& hring0, at::Tensor& hring1, int64_t G,
                        const c10::optional<at::Tensor>& clast0,
                        const c10::optional<at::Tensor>& clast1,
-                       const c10::optional<at::Tensor>& diag) {
+                       const c10::optional<at::Tensor>& diag,
+                       const c10::optional<at::Tensor>& xmask, double xscale) {
   for (auto* t : {&W0T, &W1T, &X1T}) check_seq(*t, at::kBFloat16, "W");
   check_seq(zx0, at::kFloat, "zx0");
   check_seq(bias1, at::kFloat, "bias1");
@@ -778,6 +832,8 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
     }
   a.clast0 = optr<float>(clast0);
   a.clast1 = optr<float>(clast1);
+  a.xmask = drop_bits(xmask, T, B, H, "xmask");
+  a.xscale = (float)xscale;
   const int rc = dcr::launch_lstm2_fwd_persist(a, num_cus(), cur_stream());
   TORCH_CHECK(rc == 0, "two-layer persistent LSTM forward not launched (", rc, ")");
 }
@@ -790,7 +846,9 @@ void lstm2_persist_bwd(const at::Tensor& Wh0, const at::Tensor& Wh1, const at::T
                        const c10::optional<at::Tensor>& db_part0,
                        const c10::optional<at::Tensor>& db_part1, at::Tensor& cnt0,
                        at::Tensor& cnt1, at::Tensor& err, int64_t spin_limit, int64_t G,
-                       const c10::optional<at::Tensor>& diag) {
+                       const c10::optional<at::Tensor>& diag,
+                       const c10::optional<at::Tensor>& xmask, double xscale,
+                       const c10::optional<at::Tensor>& omask, double oscale) {
   for (auto* t : {&Wh0, &Wh1, &Wx1}) check_seq(*t, at::kBFloat16, "W");
   check_seq(dtop1, at::kFloat, "dtop1");
   for (const at::Tensor* t : {&gates0, &gates1, (const at::Tensor*)&dz0, (const at::Tensor*)&dz1,
@@ -835,6 +893,10 @@ void lstm2_persist_bwd(const at::Tensor& Wh0, const at::Tensor& Wh1, const at::T
                 "diag must hold [T+2, G, 8] int64 (ticks 0..T+1)");
     a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());
   }
+  a.xmask = drop_bits(xmask, T, B, H, "xmask");
+  a.xscale = (float)xscale;
+  a.omask = drop_bits(omask, T, B, H, "omask");
+  a.oscale = (float)oscale;
   const int rc = dcr::launch_lstm2_bwd_persist(a, num_cus(), cur_stream());
   TORCH_CHECK(rc == 0, "two-layer persistent LSTM BPTT not launched (", rc, ")");
 }
@@ -1171,13 +1233,18 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor(e!) hbuf1, Tensor(f!) cbuf1, Tensor(g!)? gates1, Tensor(h!) hlast1, "
       "Tensor(i!) cnt0, Tensor(j!) cnt1, Tensor(k!) err, float forget_bias, int spin_limit, "
       "Tensor(l!) hring0, Tensor(m!) hring1, int G, Tensor(o!)? clast0=None, "
-      "Tensor(p!)? clast1=None, Tensor(q!)? diag=None) -> ()");
+      "Tensor(p!)? clast1=None, Tensor(q!)? diag=None, Tensor? xmask=None, "
+      "float xscale=1.0) -> ()");
   m.def(
       "lstm2_persist_bwd(Tensor Wh0, Tensor Wh1, Tensor Wx1, Tensor dtop1, Tensor gates0, "
       "Tensor cbuf0, Tensor gates1, Tensor cbuf1, Tensor(a!) dz0, Tensor(b!) dz1, "
       "Tensor(c!) zring0, Tensor(d!) zring1, Tensor(e!)? db_part0, Tensor(f!)? db_part1, "
       "Tensor(g!) cnt0, Tensor(h!) cnt1, Tensor(i!) err, int spin_limit, int G, "
-      "Tensor(j!)? diag=None) -> ()");
+      "Tensor(j!)? diag=None, Tensor? xmask=None, float xscale=1.0, Tensor? omask=None, "
+      "float oscale=1.0) -> ()");
+  m.def("dropout_bits(Tensor(a!) bits, int seed, int stream, float keep) -> ()");
+  m.def("mask_apply(Tensor input, Tensor bits, float scale, Tensor(a!) out) -> ()");
+  m.def("embed_dropout(Tensor ids, Tensor E, Tensor? bits, float scale, Tensor(a!) out) -> ()");
   m.def("sample_supported(int V, int H) -> int", [](int64_t V, int64_t H) -> int64_t {
     return dcr::sample_supported((int)V, (int)H);
   });
@@ -1232,6 +1299,9 @@ TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("gru_persist_fwd", &gru_persist_fwd);
   m.impl("lstm2_persist_fwd", &lstm2_persist_fwd);
   m.impl("lstm2_persist_bwd", &lstm2_persist_bwd);
+  m.impl("dropout_bits", &dropout_bits);
+  m.impl("mask_apply", &mask_apply);
+  m.impl("embed_dropout", &embed_dropout);
   m.impl("lstm_big_fwd", &lstm_big_fwd);
   m.impl("sample_step", &sample_step);
   m.impl("gru_persist_bwd", &gru_persist_bwd);

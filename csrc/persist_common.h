@@ -22,6 +22,15 @@ __device__ __forceinline__ bf16x8 ld8_sc1(__amdgpu_buffer_rsrc_t r, unsigned byt
   const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, kAuxSc1);
   return __builtin_bit_cast(bf16x8, v);
 }
+// The same with the address split into a per-lane VGPR part and a wave-uniform part passed as
+// the instruction's SGPR offset: a loop that loads many fragments then keeps ONE offset VGPR
+// instead of one per fragment (the KS = 16 BPTT had spilled its hoisted offsets to scratch,
+// each reload a serialising vmcnt(0) in the payload loop).
+__device__ __forceinline__ bf16x8 ld8_sc1(__amdgpu_buffer_rsrc_t r, unsigned lane_off,
+                                          unsigned uniform_off) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, lane_off, uniform_off, kAuxSc1);
+  return __builtin_bit_cast(bf16x8, v);
+}
 __device__ __forceinline__ void st4bf_sc1(bf16* p, float a, float b, float c, float d) {
   bf16x4 v;
   v[0] = f2bf(a); v[1] = f2bf(b); v[2] = f2bf(c); v[3] = f2bf(d);
@@ -134,6 +143,10 @@ __host__ __device__ __forceinline__ size_t frag_index(int b, int k, int K) {
 }
 __host__ __device__ __forceinline__ unsigned frag_load_off(int bg, int kstep, int K, int lane) {
   return (unsigned)((((size_t)bg * (K >> 5) + kstep) * 64 + lane) * 16);
+}
+// frag_load_off = lane * 16 + frag_tile_off (the wave-uniform part)
+__host__ __device__ __forceinline__ unsigned frag_tile_off(int bg, int kstep, int K) {
+  return (unsigned)(((size_t)bg * (K >> 5) + kstep) * 1024);
 }
 
 // Block -> (unit block, batch group).  Speed only: place the unit-block workgroups of one batch

@@ -23,7 +23,7 @@ optimizer step (W_hᵀ for the forward's A operand, W_h in TF layout for the bac
 from __future__ import annotations
 
 import os
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -134,7 +134,7 @@ class LayerBufs:
     dzx: Optional[torch.Tensor]
     x_in: Optional[torch.Tensor] = None      # bf16 [N, D] layer input (dense mode)
     clast32: Optional[torch.Tensor] = None   # fp32 [B, H] final c (persistent LSTM)
-    masks: Dict[str, torch.Tensor] = field(default_factory=dict)
+    x_drop: Optional[torch.Tensor] = None    # bf16 [N, D] masked layer input (dropout)
 
 
 class NativeBackend:
@@ -198,8 +198,10 @@ class NativeBackend:
         # (csrc/step_gemm.hip split-K; correct, but its fp32 split slabs cost more than they
         # save: LSTM-2048 108.5 vs 96.0 ms at B = 64, 216 vs 199 at B = 256)
         self.step_gemm_mode = os.environ.get("DCR_STEP_GEMM", "library")
-        self.gen = torch.Generator(device=self.dev)
-        self.gen.manual_seed(int(seed))
+        self._drop_seed = int(seed) * 0x9E3779B1 + 0x5EED
+        self._drop_step = 0
+        self._dm_bufs: Dict[Tuple[int, int], dict] = {}
+        self.last_dropout_masks: Optional[dict] = None
 
     # ------------------------------------------------------------------ weights
     def params_changed(self):
@@ -309,6 +311,8 @@ class NativeBackend:
                 dz=torch.empty(T, B, GW, dtype=bf16, device=dev) if training else None,
                 dzx=torch.empty(T, B, GW, dtype=bf16, device=dev) if (training and m == "nas") else None,
             )
+            if training and self._dropout(True):
+                lb.x_drop = torch.empty(N, H, dtype=bf16, device=dev)
             layers.append(lb)
         ws = max(self.ops.segsum_workspace(N, GW, self.V), self.ops.segsum_workspace(N, H, self.V),
                  self.ops.segsum_workspace(N, GW, 1), self.ops.segsum_workspace(N, self.V, 1), 1)
@@ -351,6 +355,8 @@ class NativeBackend:
                      torch.empty(2 * Bp * H, dtype=bf16, device=dev))
                     if (os.environ.get("DCR_FRAG", "1") != "0" or plan["pair"]) else None),
             # fragment-tiled dZ hand-off ring of the persistent BPTT (persist_common.h)
+            o_drop=(torch.empty(N, H, dtype=bf16, device=dev)
+                    if (training and self._dropout(True)) else None),
             zring=(torch.empty(2 * Bp * GW, dtype=bf16, device=dev)
                    if (training and (os.environ.get("DCR_FRAG", "1") != "0" or plan["pair_bwd"]))
                    else None),
@@ -437,7 +443,7 @@ class NativeBackend:
             return plan
         # two-layer wavefront kernels (lstm2_persist.hip) for layers (0,1), (2,3), ...: any
         # batch (padded to 32-row groups, G groups per workgroup), H in {128..512}
-        if self.L >= 2 and self.use_pair and not self._dropout(training):
+        if self.L >= 2 and self.use_pair:
             G = int(o.lstm2_plan(self.H, B, int(os.environ.get("DCR_PAIR_G", "0"))))
             if G:
                 plan.update(pair=True, pair_g=G, pair_nbg=int(o.lstm2_nbg(B, G)),
@@ -497,8 +503,47 @@ class NativeBackend:
         c = self.cfg
         return training and (c.input_keep_prob < 1.0 or c.output_keep_prob < 1.0)
 
-    def _mask(self, shape, keep: float) -> torch.Tensor:
-        return (torch.rand(shape, device=self.dev, generator=self.gen) < keep).to(bf16) * (1.0 / keep)
+    def _drop_masks(self, T: int, B: int) -> dict:
+        """This step's dropout masks as bits (csrc/dropout.hip), drawn once per training step.
+
+        DropoutWrapper(input_keep_prob, output_keep_prob) around every layer plus the
+        embedding dropout with output_keep_prob (model.py:31-34, 58-59; A-13) compose into ONE
+        mask per layer input -- layer 0: embedding x input dropout, layer l > 0: layer l-1's
+        output dropout x layer l's input dropout; independent Bernoulli draws multiply, so each
+        is one draw with keep = output_keep_prob * input_keep_prob -- and one on the top
+        layer's output (keep = output_keep_prob).  The persistent pair kernels read their
+        fragments' bits in-kernel; the other routes use ``ops.mask_apply``."""
+        c = self.cfg
+        p_in = float(c.output_keep_prob) * float(c.input_keep_prob)
+        p_out = float(c.output_keep_prob)
+        key = (T, B)
+        m = self._dm_bufs.get(key)
+        if m is None:
+            nb = lambda: torch.empty(T, B, self.H // 8, dtype=torch.uint8, device=self.dev)  # noqa: E731
+            m = self._dm_bufs[key] = dict(
+                inb=[nb() for _ in range(self.L)] if p_in < 1.0 else [None] * self.L,
+                out=nb() if p_out < 1.0 else None)
+        self._drop_step += 1
+        stream = self._drop_step << 8
+        for layer, bits in enumerate(m["inb"]):
+            if bits is not None:
+                self.ops.dropout_bits(bits, self._drop_seed, stream + layer, p_in)
+        if m["out"] is not None:
+            self.ops.dropout_bits(m["out"], self._drop_seed, stream + 255, p_out)
+        dm = dict(inb=m["inb"], out=m["out"], sin=1.0 / p_in, sout=1.0 / p_out)
+        self.last_dropout_masks = dm
+        return dm
+
+    def _masked(self, x: torch.Tensor, bits: Optional[torch.Tensor], scale: float,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """x ⊙ mask · scale over [N, K] rows (time-major, as the bits); ``out`` may be ``x``."""
+        if bits is None:
+            return x
+        N, K = bits.shape[0] * bits.shape[1], bits.shape[2] * 8
+        x2 = x.reshape(N, K)
+        o = torch.empty_like(x2) if out is None else out.view(N, K)
+        self.ops.mask_apply(x2, bits, scale, o)
+        return o
 
     # ------------------------------------------------------------------ forward
     def _forward(self, ids_tm: torch.Tensor, state, training: bool, want_logits: bool = True,
@@ -508,7 +553,7 @@ class NativeBackend:
         tasks = self._prep()
         bufs = self._buffers(B, T, training)
         drop = self._dropout(training)
-        c = self.cfg
+        dm = self._drop_masks(T, B) if drop else None
         # initial state into slot 0 of the sequence buffers, hand-off counters zeroed: all in
         # the same prep launch as the weight layouts
         for layer in range(self.L):
@@ -556,29 +601,34 @@ class NativeBackend:
                 zx = self._head["table"]
                 ids_arg = ids_tm
             else:
-                if layer == 0:
-                    X = self._head["E"][ids_tm.long()].to(bf16)  # [T, B, H]
-                    if training and c.output_keep_prob < 1.0:  # model.py:58-59 (A-13)
-                        lb.masks["emb"] = self._mask(X.shape, c.output_keep_prob)
-                        X = X * lb.masks["emb"]
+                inb = dm["inb"][layer] if dm else None
+                if layer == 0:  # the embedding rows (masked: embedding x input dropout)
+                    X = lb.x_drop if inb is not None else torch.empty(N, H, dtype=bf16,
+                                                                      device=self.dev)
+                    self.ops.embed_dropout(ids_tm.reshape(-1), self._head["E"], inb,
+                                           dm["sin"] if dm else 1.0, X)
                 else:
-                    X = x_prev
-                if drop and c.input_keep_prob < 1.0:
-                    lb.masks["in"] = self._mask(X.shape, c.input_keep_prob)
-                    X = X * lb.masks["in"]
-                lb.x_in = X.reshape(N, H).contiguous()
+                    X = x_prev.reshape(N, H)
+                    if inb is not None:
+                        X = self._masked(X, inb, dm["sin"], out=lb.x_drop)
+                lb.x_in = X if X.is_contiguous() else X.contiguous()
                 _mm_into(lb.x_in, lw.Wx, lb.zx.view(N, self.GW), bias=lw.bias)
                 zx = lb.zx
-            if bufs["pair"] and layer + 1 < self.L and not drop:
-                # layers (l, l+1) as one wavefront launch (lstm2_persist.hip): T+1 ticks
+            if bufs["pair"] and layer + 1 < self.L:
+                # layers (l, l+1) as one wavefront launch (lstm2_persist.hip): T+1 ticks; layer
+                # l+1's input dropout is applied to its fragments in-kernel
                 lw1, lb1 = self._w[layer + 1], bufs["layers"][layer + 1]
+                xm = dm["inb"][layer + 1] if dm else None
                 self.ops.lstm2_persist_fwd(lw.WhT, lw1.WhT, lw1.WxT, zx, ids_arg, lw1.bias,
                                            lb.hbuf, lb.cbuf, lb.gates, lb.hlast32,
                                            lb1.hbuf, lb1.cbuf, lb1.gates, lb1.hlast32,
                                            bufs["cnt"][layer], bufs["cnt"][layer + 1], self.err,
                                            FORGET_BIAS, self.spin_limit, *bufs["hrings"],
-                                           bufs["pair_g"], lb.clast32, lb1.clast32)
-                lb1.x_in = lb.hbuf[1:].reshape(N, H)
+                                           bufs["pair_g"], lb.clast32, lb1.clast32, None, xm,
+                                           dm["sin"] if dm else 1.0)
+                # layer l+1's (masked) input rows for its weight gradient
+                lb1.x_in = (self._masked(lb.hbuf[1:], xm, dm["sin"], out=lb1.x_drop)
+                            if xm is not None else lb.hbuf[1:].reshape(N, H))
                 x_prev = lb1.hbuf[1:]
                 paired = layer + 1
                 continue
@@ -607,12 +657,10 @@ class NativeBackend:
                 self.ops.rnn_fwd_seq(self.cell, lw.WhT, lw.WT2, zx, ids_arg, lb.hbuf, lb.h32,
                                      lb.cbuf, lb.gates, lb.pre, lb.aux, lb.rh, lb.hlast32,
                                      FORGET_BIAS)
-            out = lb.hbuf[1:]
-            if drop and c.output_keep_prob < 1.0:
-                lb.masks["out"] = self._mask(out.shape, c.output_keep_prob)
-                out = out * lb.masks["out"]
-            x_prev = out
+            x_prev = lb.hbuf[1:]
         O = x_prev.reshape(N, H)
+        if dm is not None and dm["out"] is not None:  # the top layer's output dropout
+            O = self._masked(O, dm["out"], dm["sout"], out=bufs["o_drop"])
         if not O.is_contiguous():
             O = O.contiguous()
         logits = bufs["logits"]
@@ -689,7 +737,7 @@ class NativeBackend:
             sb = s.by_name["rnnlm/softmax_b"]
             on_ready(sb.offset + sb.numel)
         drop = self._dropout(True)
-        c = self.cfg
+        dm = self.last_dropout_masks if drop else None
         deferred = []
         paired_done = -1  # lower layer whose BPTT already ran inside a two-layer wavefront
         # TF clip-norm term from dx_tok = dZ0·W_x0ᵀ: needed as an extra GEMM only on the layer-0
@@ -700,15 +748,17 @@ class NativeBackend:
         for layer in reversed(range(self.L)):
             lw, lb = self._w[layer], bufs["layers"][layer]
             names = [sp.name for sp in cell_specs(self.cfg, layer)]
+            pair_hi = bufs["pair_bwd"] and layer % 2 == 1 and dtop is not None
+            # the top layer's output dropout: in-kernel for the pair BPTT, else applied here
+            omask = dm["out"] if (dm is not None and layer == self.L - 1) else None
             if dtop is not None:
-                if "out" in lb.masks:
-                    dtop = dtop * lb.masks["out"]
                 dtop = dtop.contiguous()
+                if omask is not None and not pair_hi:
+                    dtop = self._masked(dtop, omask, dm["sout"], out=dtop).view(T, B, H)
             zx_nas = lb.zx if self.cfg.model == "nas" else None
             written = False  # this layer's kernel/bias gradients already in the flat buffer
             gather = (layer == 0 and not drop and self.cfg.model != "nas")
             fused_dew = bufs["persist"] and gather and V <= 128 and self.fused_dew
-            pair_hi = bufs["pair_bwd"] and layer % 2 == 1 and not drop and dtop is not None
             if pair_hi:
                 # layers (layer-1, layer) as one reverse wavefront (lstm2_persist.hip): T+1
                 # ticks, the lower layer's dtop = dZ·W_xᵀ of this layer computed in-kernel
@@ -720,7 +770,10 @@ class NativeBackend:
                                            bufs["zring2"], bufs["db_part"][lo][:nr],
                                            bufs["db_part"][layer][:nr], bufs["cnt"][self.L + lo],
                                            bufs["cnt"][self.L + layer], self.err,
-                                           self.spin_limit, bufs["pair_g"])
+                                           self.spin_limit, bufs["pair_g"], None,
+                                           dm["inb"][layer] if dm else None,
+                                           dm["sin"] if dm else 1.0, omask,
+                                           dm["sout"] if dm else 1.0)
                 paired_done = lo
                 if lo == 0 and user_ready is not None:
                     on_ready = _release()
@@ -732,7 +785,8 @@ class NativeBackend:
                     above = (self._w[layer + 1].Wx, bufs["layers"][layer + 1].dz)
                 self.ops.lstm_persist_bwd(lw.Wh, dtop if dtop is not None else bufs["dtop"],
                                           lb.dz, lb.gates, lb.cbuf, bufs["cnt"][self.L + layer],
-                                          self.err, self.spin_limit, bufs["db_part"][layer],
+                                          self.err, self.spin_limit,
+                                          bufs["db_part"][layer][: max(B // 16, 1)],
                                           ids_tm if fused_dew else None,
                                           bufs["dew_part"] if fused_dew else None, V, None,
                                           above[0] if above else None,
@@ -869,13 +923,11 @@ class NativeBackend:
                     dtop = None
                     continue
                 dX = _mm_into(dZx, lw.Wx.t(), bufs["dx"].view(N, H)).view(T, B, H)
-                if "in" in lb.masks:
-                    dX = dX * lb.masks["in"]
+                if dm is not None and dm["inb"][layer] is not None:  # this layer's input mask
+                    dX = self._masked(dX, dm["inb"][layer], dm["sin"], out=dX).view(T, B, H)
                 if layer > 0:
                     dtop = dX
                 else:
-                    if "emb" in lb.masks:
-                        dX = dX * lb.masks["emb"]
                     dXf = dX.reshape(N, H).float().contiguous()
                     self._embed_grad(dXf, ids_tm, bufs)
                     self._token_norm(dXf)

@@ -117,14 +117,20 @@ def _dropout(x, keep: float, gen: Optional[torch.Generator]):
 
 
 def forward(cfg: ModelConfig, params: dict, x: torch.Tensor, state: State, training: bool = True,
-            gen: Optional[torch.Generator] = None, taps: Optional[dict] = None):
+            gen: Optional[torch.Generator] = None, taps: Optional[dict] = None,
+            masks: Optional[dict] = None):
     """x: int [B, T].  Returns (logits [B*T, V] batch-major, final_state, outputs [B, T, H]).
     ``taps["emb"]`` receives the embedding_lookup output (the tensor whose gradient TF
-    represents as IndexedSlices)."""
+    represents as IndexedSlices).  ``masks`` (tests): explicit, already scaled dropout masks in
+    the native backend's composed form -- ``in[l]`` [B, T, H] on layer l's input (layer 0:
+    embedding x input dropout, l > 0: layer l-1's output x layer l's input dropout) and ``out``
+    on the top layer's output -- instead of drawing them here."""
     B, T = x.shape
     emb = params["embedding"][x.long()]  # [B, T, H]
     if taps is not None:
         taps["emb"] = emb
+    if masks is not None:
+        return _forward_masked(cfg, params, emb, state, masks)
     if training and cfg.output_keep_prob:
         emb = _dropout(emb, cfg.output_keep_prob, gen)
     wrap = training and (cfg.output_keep_prob < 1.0 or cfg.input_keep_prob < 1.0)
@@ -143,6 +149,27 @@ def forward(cfg: ModelConfig, params: dict, x: torch.Tensor, state: State, train
             inp = out
         outs.append(inp)
     out = torch.stack(outs, 1)  # [B, T, H]
+    logits = out.reshape(B * T, -1) @ params["rnnlm/softmax_w"] + params["rnnlm/softmax_b"]
+    return logits, state, out
+
+
+def _forward_masked(cfg, params, emb, state, masks):
+    B, T, _ = emb.shape
+    layer_w = [layer_weights(cfg, params, layer) for layer in range(cfg.num_layers)]
+    state = [tuple(s) for s in state]
+    outs = []
+    for t in range(T):
+        inp = emb[:, t]
+        for layer in range(cfg.num_layers):
+            if masks["in"][layer] is not None:
+                inp = inp * masks["in"][layer][:, t]
+            out, st = cell_step(cfg, inp, state[layer], layer_w[layer])
+            state[layer] = st
+            inp = out
+        if masks.get("out") is not None:
+            inp = inp * masks["out"][:, t]
+        outs.append(inp)
+    out = torch.stack(outs, 1)
     logits = out.reshape(B * T, -1) @ params["rnnlm/softmax_w"] + params["rnnlm/softmax_b"]
     return logits, state, out
 
@@ -175,12 +202,13 @@ class ReferenceBackend:
             out[n] = v.detach().requires_grad_(requires_grad) if requires_grad else v
         return out
 
-    def train_step(self, x, y, state: State, on_bucket_ready=None, want_extras: bool = False):
+    def train_step(self, x, y, state: State, on_bucket_ready=None, want_extras: bool = False,
+                   masks: Optional[dict] = None):
         params = self.params(True)
         gen = self.gen if self.store.device.type == "cpu" else None
         taps = {}
         logits, new_state, _ = forward(self.cfg, params, x, state, training=True, gen=gen,
-                                       taps=taps)
+                                       taps=taps, masks=masks)
         cost, per = loss_fn(logits, y)
         names = self.store.names()
         grads = torch.autograd.grad(cost, [params[n] for n in names] + [taps["emb"]],

@@ -1,0 +1,104 @@
+"""Dropout at speed (DropoutWrapper + embedding dropout, model.py:31-34, 58-59).
+
+The native backend draws one bit mask per layer input plus one on the top output per step
+(csrc/dropout.hip); the two-layer wavefront kernels apply theirs to MFMA fragments and to the
+stashed dtop in-kernel.  The oracle here is the fp32 autograd model run with *the kernel's own
+masks* (expanded from the bits), so forward, loss, final state and every gradient must agree to
+bf16 noise -- on the pair kernels, the single-layer / per-step kernels and the GRU route."""
+import pytest
+import torch
+
+from distributed_char_rnn_amd.models.char_rnn import CharRNN
+from distributed_char_rnn_amd.models.params import ModelConfig
+from distributed_char_rnn_amd.models.reference import ReferenceBackend
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+@pytest.fixture(autouse=True)
+def _env(monkeypatch):
+    monkeypatch.setenv("DCR_SPIN_LIMIT", str(1 << 20))
+    monkeypatch.setenv("DCR_PERSIST_MIN_T", "1")
+
+
+def expand(bits, scale):
+    """[T, B, H/8] uint8 -> [B, T, H] float mask (scaled), batch-major for the oracle."""
+    T, B, K8 = bits.shape
+    sh = torch.arange(8, device=bits.device, dtype=torch.uint8)
+    m = ((bits.unsqueeze(-1) >> sh) & 1).reshape(T, B, K8 * 8).float() * scale
+    return m.transpose(0, 1).contiguous()
+
+
+def _run(model, B, T, H, L, ikp, okp, env=None, monkeypatch=None, tol=6e-2):
+    for k, v in (env or {}).items():
+        monkeypatch.setenv(k, v)
+    cfg = ModelConfig(model=model, vocab_size=65, rnn_size=H, num_layers=L,
+                      input_keep_prob=ikp, output_keep_prob=okp)
+    nat = CharRNN(cfg, device="cuda", seed=3)
+    g = torch.Generator().manual_seed(B + T)
+    x = torch.randint(0, 65, (B, T), generator=g, dtype=torch.int32).cuda()
+    y = torch.randint(0, 65, (B, T), generator=g, dtype=torch.int32).cuda()
+    torch.manual_seed(1)
+    arity = 2 if model in ("lstm", "nas") else 1
+    st0 = [tuple(torch.randn(B, H, device="cuda") * 0.5 for _ in range(arity)) for _ in range(L)]
+    loss_n, st_n, _ = nat.backend.train_step(x, y, [tuple(s.clone() for s in t) for t in st0])
+    torch.cuda.synchronize()
+    nat.backend.check_errors()
+    g_nat = nat.store.grad.clone()
+    dm = nat.backend.last_dropout_masks
+    assert dm is not None
+    masks = {"in": [expand(b, dm["sin"]) if b is not None else None for b in dm["inb"]],
+             "out": expand(dm["out"], dm["sout"]) if dm["out"] is not None else None}
+    ref = ReferenceBackend(nat.store)
+    loss_r, st_r, _ = ref.train_step(x, y, [tuple(s.clone() for s in t) for t in st0],
+                                     masks=masks)
+    assert abs(loss_n.item() - loss_r.item()) < 2e-2 * max(1.0, abs(loss_r.item()))
+    for a_r, a_n in zip(st_r, st_n):
+        for s_r, s_n in zip(a_r, a_n):
+            assert rel(s_n, s_r) < 3e-2
+    for s in nat.store.specs:
+        e = rel(nat.store.view(s.name, g_nat), nat.store.gview(s.name))
+        assert e < tol, (s.name, e)
+    return nat, dm
+
+
+@pytest.mark.parametrize("B,T,H,L", [(64, 6, 128, 2), (256, 5, 512, 2), (50, 4, 256, 4),
+                                     (512, 3, 512, 2)])
+def test_dropout_on_pair_kernels_matches_oracle(B, T, H, L, monkeypatch):
+    nat, _ = _run("lstm", B, T, H, L, 0.8, 0.7)
+    assert nat.backend._persist_plan(B, True, T)["pair"]
+
+
+@pytest.mark.parametrize("ikp,okp", [(0.5, 1.0), (1.0, 0.6)])
+def test_dropout_single_keep_prob(ikp, okp):
+    _run("lstm", 64, 5, 256, 2, ikp, okp)
+
+
+def test_dropout_per_step_and_single_layer_kernels(monkeypatch):
+    _run("lstm", 48, 5, 128, 3, 0.8, 0.7)                                   # pair + single
+    _run("lstm", 32, 4, 128, 2, 0.8, 0.7, {"DCR_PERSIST": "0"}, monkeypatch)  # per-step
+
+
+def test_dropout_gru():
+    _run("gru", 64, 5, 128, 2, 0.8, 0.7)
+
+
+def test_dropout_masks_statistics_and_fresh_per_step():
+    cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=512, num_layers=2,
+                      input_keep_prob=0.8, output_keep_prob=0.5)
+    m = CharRNN(cfg, device="cuda", seed=5)
+    B, T = 256, 32
+    x = torch.randint(0, 65, (B, T), dtype=torch.int32, device="cuda")
+    m.backend.train_step(x, x, m.zero_state(B))
+    d1 = m.backend.last_dropout_masks
+    frac_in = expand(d1["inb"][1], 1.0).mean().item()
+    frac_out = expand(d1["out"], 1.0).mean().item()
+    assert abs(frac_in - 0.4) < 0.01 and abs(frac_out - 0.5) < 0.01
+    first = d1["inb"][0].clone()
+    m.backend.train_step(x, x, m.zero_state(B))
+    assert not torch.equal(first, m.backend.last_dropout_masks["inb"][0])
