@@ -16,25 +16,57 @@ namespace dcr {
 
 constexpr int kDropThreads = 256;
 
-// thread -> 32 consecutive elements (4 bytes, one dword store)
+// thread -> 32 consecutive elements (4 bytes, one dword store).  Each 64-bit hash yields four
+// 16-bit uniforms (keep resolution 2^-16): 8 hashes per 32 elements.
 __global__ void __launch_bounds__(kDropThreads) dropout_bits_kernel(
-    unsigned* __restrict__ bits, int64_t nwords, uint64_t seed, uint64_t stream, float keep) {
+    unsigned* __restrict__ bits, int64_t nwords, uint64_t seed, uint64_t stream, unsigned kt) {
+  const uint64_t key = seed ^ mix64(stream * 0x632BE59BD9B4E019ull);
   for (int64_t i = blockIdx.x * (int64_t)kDropThreads + threadIdx.x; i < nwords;
        i += (int64_t)gridDim.x * kDropThreads) {
     unsigned w = 0;
-#pragma unroll 8
-    for (int e = 0; e < 32; ++e)
-      w |= (uniform01(seed, stream, (uint64_t)i * 32 + e) < keep ? 1u : 0u) << e;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const uint64_t r = mix64(key + (uint64_t)i * 8 + q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        w |= ((unsigned)(r >> (16 * e)) & 0xFFFFu) < kt ? 1u << (4 * q + e) : 0u;
+    }
     bits[i] = w;
   }
 }
 
-// out[r, k] = in[r, k] * (bit ? scale : 0) for 8 consecutive k per thread (one mask byte).
-// In/out may alias (in place).  Row strides in elements.
+template <typename T> struct Vec8;
+template <> struct Vec8<bf16> {
+  static __device__ __forceinline__ void load(const bf16* p, float (&v)[8]) {
+    const bf16x8 x = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (float)x[e];
+  }
+  static __device__ __forceinline__ void store(bf16* p, const float (&v)[8]) {
+    bf16x8 x;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = f2bf(v[e]);
+    *reinterpret_cast<bf16x8*>(p) = x;
+  }
+};
+template <> struct Vec8<float> {
+  static __device__ __forceinline__ void load(const float* p, float (&v)[8]) {
+    const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  static __device__ __forceinline__ void store(float* p, const float (&v)[8]) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
+
+// out[r, k] = in[r, k] * (bit ? scale : 0), 8 consecutive k per thread (one mask byte, one
+// 16/32-B vector each way).  In/out may alias (in place).  Row strides in elements (multiples
+// of 8).
 template <typename TI, typename TO>
 __global__ void __launch_bounds__(kDropThreads) mask_apply_kernel(
-    const TI* __restrict__ in, int64_t ld_in, TO* __restrict__ out, int64_t ld_out,
-    const uint8_t* __restrict__ bits, int64_t rows, int K, float scale) {
+    const TI* in, int64_t ld_in, TO* out, int64_t ld_out, const uint8_t* __restrict__ bits,
+    int64_t rows, int K, float scale) {
   const int kb = K / 8;
   const int64_t n = rows * kb;
   for (int64_t i = blockIdx.x * (int64_t)kDropThreads + threadIdx.x; i < n;
@@ -42,10 +74,11 @@ __global__ void __launch_bounds__(kDropThreads) mask_apply_kernel(
     const int64_t r = i / kb;
     const int j = (int)(i - r * kb);
     const unsigned m = bits[i];
-    const TI* src = in + r * ld_in + 8 * j;
-    TO* dst = out + r * ld_out + 8 * j;
+    float v[8];
+    Vec8<TI>::load(in + r * ld_in + 8 * j, v);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) dst[e] = (TO)((m >> e & 1u) ? (float)src[e] * scale : 0.f);
+    for (int e = 0; e < 8; ++e) v[e] = (m >> e & 1u) ? v[e] * scale : 0.f;
+    Vec8<TO>::store(out + r * ld_out + 8 * j, v);
   }
 }
 
@@ -78,8 +111,10 @@ static int drop_grid(int64_t n) {
 void launch_dropout_bits(uint8_t* bits, int64_t nbytes, uint64_t seed, uint64_t stream,
                          float keep, hipStream_t s) {
   const int64_t nw = nbytes / 4;
-  dropout_bits_kernel<<<drop_grid(nw), kDropThreads, 0, s>>>(reinterpret_cast<unsigned*>(bits),
-                                                              nw, seed, stream, keep);
+  const double kt = (double)keep * 65536.0;
+  dropout_bits_kernel<<<drop_grid(nw), kDropThreads, 0, s>>>(
+      reinterpret_cast<unsigned*>(bits), nw, seed, stream,
+      kt >= 65536.0 ? 65536u : (kt <= 0.0 ? 0u : (unsigned)(kt + 0.5)));
 }
 
 void launch_mask_apply(const void* in, bool in_bf16, int64_t ld_in, void* out, bool out_bf16,

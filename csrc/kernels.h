@@ -241,9 +241,7 @@ struct Lstm2BwdArgs {
   int G, nbg;           // as Lstm2Args; zring0/1 hold [2, nbg*32, 4H]
   unsigned spin_limit;
   const uint8_t* xmask; // optional dropout bits of layer l+1's input [T, B, H/8]: layer l's dtop
-  float xscale;
-  const uint8_t* omask; // optional dropout bits of layer l+1's output [T, B, H/8]: dtop1
-  float oscale;
+  float xscale;         //   (dtop1 arrives with layer l+1's output dropout already applied)
 };
 int launch_lstm2_bwd_persist(const Lstm2BwdArgs& a, int cus, hipStream_t s);
 

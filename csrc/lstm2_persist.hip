@@ -78,10 +78,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
   const unsigned target = (unsigned)(H / 8);  // H/16 unit blocks x 2 epilogue waves per layer
   const size_t ringsz = (size_t)a.nbg * 32 * H;  // one ring slot (padded batch)
   bool dead = false;
-  // fragment loads: per-lane VGPR offset + wave-uniform SGPR offset (rings).  Slot 0 is read
-  // row-major with the whole offset in the VGPR: the buffer range check (which zero-fills the
-  // padded rows >= B) does not cover the SGPR offset
-  const unsigned lane16 = (unsigned)lane * 16;
+  // row-major slot-0 fragment offsets (rows >= B read as zero: buffer range check)
   const unsigned rm_lane = (unsigned)(((lane & 15) * H + kq) * sizeof(bf16));
   auto rm_off = [&](int bg, int j, int s) {
     return (unsigned)((((size_t)bg * 32 + 16 * j) * H + kbase + s * 32) * sizeof(bf16));
@@ -198,7 +195,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
           for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int s = 0; s < KS; ++s)
-              hf0[j][s] = ring0 ? ld8_sc1(r0, lane16, frag_tile_off(2 * bg + j, w * KS + s, H))
+              hf0[j][s] = ring0 ? ld8_sc1(r0, frag_load_off(2 * bg + j, w * KS + s, H, lane))
                                 : ld8_sc1(r0, rm_lane + rm_off(bg, j, s));
         }
         if (ld1) {
@@ -211,7 +208,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
           for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int s = 0; s < KS; ++s)
-              hf1[j][s] = ring1 ? ld8_sc1(r1, lane16, frag_tile_off(2 * bg + j, w * KS + s, H))
+              hf1[j][s] = ring1 ? ld8_sc1(r1, frag_load_off(2 * bg + j, w * KS + s, H, lane))
                                 : ld8_sc1(r1, rm_lane + rm_off(bg, j, s));
         }
       }
@@ -221,18 +218,15 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
       }
       // dropout of layer l+1's input (layer l's h of step tau-1): mask bytes of this lane's
       // x-part fragments (row b of tile j, k = kbase + 32 s + kq .. +7)
+      // (mask bytes are loaded at their use: no register is held for them across the
+      // payload phase, and only dropout pays their latency)
       const bool xdrop = a.xmask != nullptr && ld0 && tau >= 1;
-      unsigned mb[2] = {0u, 0u};  // byte s = the mask of fragment s (KS <= 4)
-      if (xdrop) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int bj = bg * 32 + 16 * j + (lane & 15);
-          const uint8_t* mrow = a.xmask + ((size_t)(tau - 1) * B + bj) * (H / 8);
-#pragma unroll
-          for (int s2 = 0; s2 < KS; ++s2)
-            if (bj < B) mb[j] |= (unsigned)mrow[(kbase + s2 * 32 + kq) >> 3] << (8 * s2);
-        }
-      }
+      auto mbyte = [&](int j, int s2) -> unsigned {
+        const int bj = bg * 32 + 16 * j + (lane & 15);
+        return bj < B ? (unsigned)a.xmask[((size_t)(tau - 1) * B + bj) * (H / 8) +
+                                          ((kbase + s2 * 32 + kq) >> 3)]
+                      : 0u;
+      };
       if (g > 0) __syncthreads();  // the previous group's epilogue has read the partials
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -265,7 +259,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
             if (xdrop) {  // masked input part, scaled by 1/keep, then the recurrent part
 #pragma unroll
               for (int s = 0; s < KS; ++s) {
-                const bf16x8 hm = mask_frag(hf0[j][s], mb[j] >> (8 * s));
+                const bf16x8 hm = mask_frag(hf0[j][s], mbyte(j, s));
 #pragma unroll
                 for (int gt = 0; gt < 4; ++gt) acc[gt] = mfma16(x1[gt][s], hm, acc[gt]);
               }
@@ -310,7 +304,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
               for (int gt = 0; gt < 4; ++gt) xs[0][j][gt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
               for (int s = 0; s < KS; ++s) {
-                const bf16x8 hm = xdrop ? mask_frag(hf0[j][s], mb[j] >> (8 * s)) : hf0[j][s];
+                const bf16x8 hm = xdrop ? mask_frag(hf0[j][s], mbyte(j, s)) : hf0[j][s];
 #pragma unroll
                 for (int gt = 0; gt < 4; ++gt) xs[0][j][gt] = mfma16(x1[gt][s], hm, xs[0][j][gt]);
               }
@@ -429,7 +423,6 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
 
   constexpr int KSG = KS / 4;  // k-steps per gate segment
   auto kcol = [&](int s) { return (s / KSG) * H + w * (H / 4) + (s % KSG) * 32; };
-  const unsigned lane16 = (unsigned)lane * 16;  // per-lane part of every fragment load
   bf16x8 wh0[KS], wh1[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
@@ -483,25 +476,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
         for (int gt = 0; gt < 4; ++gt) g4[gt] = *reinterpret_cast<const bf16x4*>(gp + gt * H);
         ld4f(cbL + (size_t)(t + 1) * B * H + bh, cc);
         ld4f(cbL + (size_t)t * B * H + bh, cp);
-        if (L) {
-          ld4f(a.dtop1 + (size_t)t * B * H + bh, dtop);
-          if (a.omask) {  // dropout of layer l+1's output (its forward mask, in-kernel)
-            const unsigned m = a.omask[((size_t)t * B + b) * (H / 8) + (u0 >> 3)] >> (u0 & 7);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) dtop[r] = (m >> r) & 1u ? dtop[r] * a.oscale : 0.f;
-          }
-        }
-      }
-      // dropout of layer l+1's input: mask of layer l's dtop (stashed partials, step T+1-tau)
-      unsigned xm = 0u;  // 4 bits per tile
-      if (a.xmask && on0) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int bj = (col * G + g) * 32 + 16 * j + (lane & 15);
-          if (bj < B)
-            xm |= ((unsigned)a.xmask[((size_t)(T + 1 - tau) * B + bj) * (H / 8) + (u0 >> 3)] >>
-                   (u0 & 7) & 0xFu) << (4 * j);
-        }
+        if (L) ld4f(a.dtop1 + (size_t)t * B * H + bh, dtop);
       }
       // after_arrive runs right after the wave's ring stores (and, for the last group, its
       // hand-off arrival), before its other stores
@@ -604,12 +579,12 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
           for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int s = 0; s < KS; ++s)
-              p1[j][s] = ld8_sc1(r1, lane16, frag_tile_off(tile0 + j, kcol(s) >> 5, G4H));
+              p1[j][s] = ld8_sc1(r1, frag_load_off(tile0 + j, kcol(s) >> 5, G4H, lane));
         }
         if (ld0) {
 #pragma unroll
           for (int s = 0; s < KS; ++s)
-            p0[s] = ld8_sc1(r0, lane16, frag_tile_off(tile0, kcol(s) >> 5, G4H));
+            p0[s] = ld8_sc1(r0, frag_load_off(tile0, kcol(s) >> 5, G4H, lane));
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -624,7 +599,13 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
           if (on0) {  // layer l: dtop (stashed last tick) + dZ_l[t+1] · W_h,lᵀ
             float4 x0 = *reinterpret_cast<const float4*>(&xsl[g][w][j][lane][0]);
             if (a.xmask) {
-              const unsigned m = xm >> (4 * j);
+              // dropout of layer l+1's input on layer l's dtop (step T+1-tau), loaded at its use:
+              // no register is held for it across the payload phase
+              const int bj = (col * G + g) * 32 + 16 * j + (lane & 15);
+              const unsigned m =
+                  bj < B ? (unsigned)a.xmask[((size_t)(T + 1 - tau) * B + bj) * (H / 8) +
+                                             (u0 >> 3)] >> (u0 & 7)
+                         : 0u;
               x0.x = m & 1u ? x0.x * a.xscale : 0.f;
               x0.y = m & 2u ? x0.y * a.xscale : 0.f;
               x0.z = m & 4u ? x0.z * a.xscale : 0.f;
@@ -638,7 +619,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int s = 0; s < KS; ++s)
-                  p0[s] = ld8_sc1(r0, lane16, frag_tile_off(tile0 + 1, kcol(s) >> 5, G4H));
+                  p0[s] = ld8_sc1(r0, frag_load_off(tile0 + 1, kcol(s) >> 5, G4H, lane));
               }
             }
             *reinterpret_cast<float4*>(&part[w][0][j][lane][0]) =

@@ -728,6 +728,10 @@ void mask_apply(const at::Tensor& in, const at::Tensor& bits, double scale, at::
   TORCH_CHECK(in.is_cuda() && out.is_cuda() && in.dim() == 2 && out.dim() == 2 &&
                   in.sizes() == out.sizes(), "mask_apply: 2-D GPU tensors of equal shape");
   TORCH_CHECK(in.stride(1) == 1 && out.stride(1) == 1, "mask_apply: unit column stride");
+  TORCH_CHECK(in.stride(0) % 8 == 0 && out.stride(0) % 8 == 0 &&
+                  (reinterpret_cast<uintptr_t>(in.data_ptr()) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(out.data_ptr()) & 15) == 0,
+              "mask_apply: 16-byte aligned rows (8-vector loads)");
   const int64_t R = in.size(0);
   const int K = (int)in.size(1);
   TORCH_CHECK(K % 8 == 0, "mask_apply: K % 8 == 0");
@@ -847,8 +851,7 @@ void lstm2_persist_bwd(const at::Tensor& Wh0, const at::Tensor& Wh1, const at::T
                        const c10::optional<at::Tensor>& db_part1, at::Tensor& cnt0,
                        at::Tensor& cnt1, at::Tensor& err, int64_t spin_limit, int64_t G,
                        const c10::optional<at::Tensor>& diag,
-                       const c10::optional<at::Tensor>& xmask, double xscale,
-                       const c10::optional<at::Tensor>& omask, double oscale) {
+                       const c10::optional<at::Tensor>& xmask, double xscale) {
   for (auto* t : {&Wh0, &Wh1, &Wx1}) check_seq(*t, at::kBFloat16, "W");
   check_seq(dtop1, at::kFloat, "dtop1");
   for (const at::Tensor* t : {&gates0, &gates1, (const at::Tensor*)&dz0, (const at::Tensor*)&dz1,
@@ -895,8 +898,6 @@ void lstm2_persist_bwd(const at::Tensor& Wh0, const at::Tensor& Wh1, const at::T
   }
   a.xmask = drop_bits(xmask, T, B, H, "xmask");
   a.xscale = (float)xscale;
-  a.omask = drop_bits(omask, T, B, H, "omask");
-  a.oscale = (float)oscale;
   const int rc = dcr::launch_lstm2_bwd_persist(a, num_cus(), cur_stream());
   TORCH_CHECK(rc == 0, "two-layer persistent LSTM BPTT not launched (", rc, ")");
 }
@@ -1240,8 +1241,7 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor cbuf0, Tensor gates1, Tensor cbuf1, Tensor(a!) dz0, Tensor(b!) dz1, "
       "Tensor(c!) zring0, Tensor(d!) zring1, Tensor(e!)? db_part0, Tensor(f!)? db_part1, "
       "Tensor(g!) cnt0, Tensor(h!) cnt1, Tensor(i!) err, int spin_limit, int G, "
-      "Tensor(j!)? diag=None, Tensor? xmask=None, float xscale=1.0, Tensor? omask=None, "
-      "float oscale=1.0) -> ()");
+      "Tensor(j!)? diag=None, Tensor? xmask=None, float xscale=1.0) -> ()");
   m.def("dropout_bits(Tensor(a!) bits, int seed, int stream, float keep) -> ()");
   m.def("mask_apply(Tensor input, Tensor bits, float scale, Tensor(a!) out) -> ()");
   m.def("embed_dropout(Tensor ids, Tensor E, Tensor? bits, float scale, Tensor(a!) out) -> ()");

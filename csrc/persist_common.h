@@ -144,6 +144,15 @@ __host__ __device__ __forceinline__ size_t frag_index(int b, int k, int K) {
 __host__ __device__ __forceinline__ unsigned frag_load_off(int bg, int kstep, int K, int lane) {
   return (unsigned)((((size_t)bg * (K >> 5) + kstep) * 64 + lane) * 16);
 }
+// A copy of `x` the compiler cannot see through: offsets built from it inside a loop stay in
+// the loop (base + constant, the constant folded into the load's immediate offset where it
+// fits) instead of being hoisted as one register per fragment.
+__device__ __forceinline__ unsigned opaque_vgpr(unsigned x) {
+  unsigned r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
 // frag_load_off = lane * 16 + frag_tile_off (the wave-uniform part)
 __host__ __device__ __forceinline__ unsigned frag_tile_off(int bg, int kstep, int K) {
   return (unsigned)(((size_t)bg * (K >> 5) + kstep) * 1024);

@@ -749,11 +749,11 @@ class NativeBackend:
             lw, lb = self._w[layer], bufs["layers"][layer]
             names = [sp.name for sp in cell_specs(self.cfg, layer)]
             pair_hi = bufs["pair_bwd"] and layer % 2 == 1 and dtop is not None
-            # the top layer's output dropout: in-kernel for the pair BPTT, else applied here
+            # the top layer's output dropout
             omask = dm["out"] if (dm is not None and layer == self.L - 1) else None
             if dtop is not None:
                 dtop = dtop.contiguous()
-                if omask is not None and not pair_hi:
+                if omask is not None:
                     dtop = self._masked(dtop, omask, dm["sout"], out=dtop).view(T, B, H)
             zx_nas = lb.zx if self.cfg.model == "nas" else None
             written = False  # this layer's kernel/bias gradients already in the flat buffer
@@ -772,8 +772,7 @@ class NativeBackend:
                                            bufs["cnt"][self.L + layer], self.err,
                                            self.spin_limit, bufs["pair_g"], None,
                                            dm["inb"][layer] if dm else None,
-                                           dm["sin"] if dm else 1.0, omask,
-                                           dm["sout"] if dm else 1.0)
+                                           dm["sin"] if dm else 1.0)
                 paired_done = lo
                 if lo == 0 and user_ready is not None:
                     on_ready = _release()
