@@ -67,6 +67,127 @@ __global__ void __launch_bounds__(kSegThreads) segsum_lds_kernel(
   }
 }
 
+// bf16 rows (16-byte aligned, ldx % 8 == 0) and V <= 128: the segment sum as a one-hot MFMA
+// product, out[v][w] = sum_n onehot(ids[n])[v] * X[n][w] -- no atomics.  (LDS fp32 atomics
+// measured ~190 G adds/s chip-wide on gfx950: 339 us for the [32768, 2048] dEW, 89 us for
+// the [32768, 512] dropout dE -- far below the HBM bound of the read.)
+//
+// mfma_f32_16x16x32_bf16 with A = onehotᵀ (rows v, k = tokens) built in registers from the
+// ids and B = the X tile (k = tokens, columns w).  B wants 8 consecutive TOKENS per lane, i.e.
+// a column of the row-major X tile: the tile is staged in LDS as it lies in memory and read
+// back with ds_read_b64_tr_b16 (gfx950's transposing LDS read: a 16-lane group reads a 4-row x
+// 16-column block and lane i receives column i).  Workgroup = 64 columns x one row chunk,
+// wave = one 16-column n-tile x all VT v-tiles; partials [chunk][V][W] are summed by
+// segsum_reduce_kernel in a fixed order (bitwise reproducible).
+constexpr int kOhCols = 64;               // columns per workgroup (4 waves x 16)
+constexpr int kOhRows = 128;              // rows staged per LDS fill (4 MFMA k-steps)
+constexpr int kOhLd = kOhCols + 8;        // LDS row stride (bf16): 144 B, fewer bank conflicts
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+template <int VT>
+__global__ void __launch_bounds__(kSegThreads) onehot_segsum_kernel(
+    const bf16* __restrict__ X, int ldx, const int* __restrict__ ids, int N, int W, int V,
+    int rows_per_chunk, float* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) bf16 tile[kOhRows][kOhLd];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane >> 4, m = lane & 15;
+  const int c0 = blockIdx.x * kOhCols, chunk = blockIdx.y;
+  const int r0 = chunk * rows_per_chunk, r1 = min(N, r0 + rows_per_chunk);
+  // rows >= r1 read as zero through the buffer range check (a NaN there would survive the
+  // one-hot zero; onehot_ok keeps the buffer below 2 GB)
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16*>(X), (short)0,
+      (unsigned)min((size_t)0xFFFFFFF0ull, sizeof(bf16) * (size_t)N * ldx), 0x00020000);
+  // staging: thread t -> rows (t >> 3) + 32 s, 8 columns at 8 (t & 7)
+  const int srow = threadIdx.x >> 3, scol = 8 * (threadIdx.x & 7);
+  f32x4 acc[VT];
+#pragma unroll
+  for (int vt = 0; vt < VT; ++vt) acc[vt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // transposing-read addresses: lane 4a + p of a 16-lane group names row a of its 4-row block,
+  // columns 4p .. 4p+3 of the wave's 16-column tile
+  const int ta = (lane & 15) >> 2, tp = lane & 3;
+  // software pipeline: the next fill's rows are loaded into registers while this one computes
+  auto fill = [&](int n0, bf16x8 (&st)[4]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      // a row outside [n0, r1) gets an offset past the buffer: the range check returns zero
+      // (a select on the loaded value would wait for the load right here)
+      const int row = n0 + srow + 32 * s;
+      const unsigned off = row < r1 ? (unsigned)(((size_t)row * ldx + c0 + scol) * sizeof(bf16))
+                                    : 0x80000000u;
+      st[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+    }
+  };
+  bf16x8 st[4];
+  fill(r0, st);
+  for (int n0 = r0; n0 < r1; n0 += kOhRows) {
+    __syncthreads();  // the previous fill has been read
+#pragma unroll
+    for (int s = 0; s < 4; ++s) *reinterpret_cast<bf16x8*>(&tile[srow + 32 * s][scol]) = st[s];
+    __syncthreads();
+    if (n0 + kOhRows < r1) fill(n0 + kOhRows, st);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      // the 8 tokens of this lane's k-slice: rows n0 + 32 s + 8 q + j
+      const int nb = n0 + 32 * s + 8 * q;
+      int id[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) id[j] = nb + j < r1 ? ids[nb + j] : -1;
+      const int rb = 32 * s + 8 * q + ta;
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s16x4*)&tile[rb][16 * wave + 4 * tp]);
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s16x4*)&tile[rb + 4][16 * wave + 4 * tp]);
+      u32x4 bu;
+      bu[0] = (unsigned)(unsigned short)lo[0] | ((unsigned)(unsigned short)lo[1] << 16);
+      bu[1] = (unsigned)(unsigned short)lo[2] | ((unsigned)(unsigned short)lo[3] << 16);
+      bu[2] = (unsigned)(unsigned short)hi[0] | ((unsigned)(unsigned short)hi[1] << 16);
+      bu[3] = (unsigned)(unsigned short)hi[2] | ((unsigned)(unsigned short)hi[3] << 16);
+      const bf16x8 b = __builtin_bit_cast(bf16x8, bu);
+#pragma unroll
+      for (int vt = 0; vt < VT; ++vt) {
+        const int v = 16 * vt + m;  // this lane's A row
+        u32x4 au;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          au[i] = (id[2 * i] == v ? 0x3F80u : 0u) | (id[2 * i + 1] == v ? 0x3F800000u : 0u);
+        acc[vt] = mfma16(__builtin_bit_cast(bf16x8, au), b, acc[vt]);
+      }
+    }
+  }
+  // D[v = 16 vt + 4 q + i][w = c0 + 16 wave + m]
+  const int w = c0 + 16 * wave + m;
+  if (w < W) {
+    float* out = partial + (size_t)chunk * V * W + w;
+#pragma unroll
+    for (int vt = 0; vt < VT; ++vt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int v = 16 * vt + 4 * q + i;
+        if (v < V) out[(size_t)v * W] = acc[vt][i];
+      }
+  }
+}
+
+static bool onehot_ok(const void* X, int ldx, const int* ids, int V) {
+  return ids != nullptr && V >= 1 && V <= 128 && ldx % 8 == 0 &&
+         (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+}
+static bool onehot_fits(int N, int ldx) {
+  return (size_t)N * ldx * sizeof(bf16) < 0x80000000ull;
+}
+
+// ~1024 workgroups (4 per CU) without making the partials larger than the data
+static int onehot_rows_per_chunk(int N, int W) {
+  const int strips = (W + kOhCols - 1) / kOhCols;
+  int chunks = (1024 + strips - 1) / strips;
+  chunks = chunks < 1 ? 1 : (chunks > 128 ? 128 : chunks);
+  int r = (N + chunks - 1) / chunks;
+  r = ((r + kOhRows - 1) / kOhRows) * kOhRows;
+  return r < kOhRows ? kOhRows : r;
+}
+
 template <typename T>
 __global__ void __launch_bounds__(kSegThreads) colsum_kernel(const T* __restrict__ X, int ldx, int N,
                                                             int W, int rows_per_chunk,
@@ -153,16 +274,39 @@ __global__ void __launch_bounds__(kSegThreads) colsum_vec_kernel(const bf16* __r
   }
 }
 
+// out = sum over chunks of partial[chunk][VW], in a fixed order (bitwise reproducible).  A
+// workgroup reduces 32 consecutive elements with 8 chunk lanes each (one thread per element
+// looped over all chunks serially: 31 us for 128 x [65 x 512]).
 __global__ void __launch_bounds__(kSegThreads) segsum_reduce_kernel(const float* __restrict__ partial,
                                                                    int nchunks, int64_t VW,
                                                                    float* __restrict__ out,
                                                                    int accumulate) {
-  for (int64_t i = blockIdx.x * (int64_t)kSegThreads + threadIdx.x; i < VW;
-       i += (int64_t)gridDim.x * kSegThreads) {
+  __shared__ float red[kSegThreads / 32][32];
+  const int e = threadIdx.x & 31, c = threadIdx.x >> 5;
+  for (int64_t base = (int64_t)blockIdx.x * 32; base < VW; base += (int64_t)gridDim.x * 32) {
+    const int64_t i = base + e;
     float s = 0.f;
-    for (int k = 0; k < nchunks; ++k) s += partial[(size_t)k * VW + i];
-    out[i] = accumulate ? out[i] + s : s;
+    if (i < VW) {
+#pragma unroll 4
+      for (int k = c; k < nchunks; k += kSegThreads / 32) s += partial[(size_t)k * VW + i];
+    }
+    red[c][e] = s;
+    __syncthreads();
+    if (c == 0 && i < VW) {
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < kSegThreads / 32; ++k) t += red[k][e];
+      out[i] = accumulate ? out[i] + t : t;
+    }
+    __syncthreads();
   }
+}
+
+static void launch_reduce(const float* partial, int nchunks, int64_t VW, float* out,
+                          int accumulate, hipStream_t s) {
+  const int64_t nb = (VW + 31) / 32;
+  segsum_reduce_kernel<<<(int)(nb < 8192 ? nb : 8192), kSegThreads, 0, s>>>(partial, nchunks, VW,
+                                                                            out, accumulate);
 }
 
 // Wide vocabularies: each workgroup owns kAtomicRows consecutive rows x one 256-column strip
@@ -213,9 +357,11 @@ int segsum_rows_per_chunk(int N) {
 
 size_t segsum_workspace_floats(int N, int W, int V) {
   if (V > kSegLdsMaxV) return 0;
-  const int rpc = segsum_rows_per_chunk(N);
-  const int nchunks = (N + rpc - 1) / rpc;
-  return (size_t)nchunks * V * W;
+  // the larger of the LDS route's and the one-hot route's partials (the caller does not know
+  // which one a launch takes)
+  const int rpc = segsum_rows_per_chunk(N), rpo = onehot_rows_per_chunk(N, W);
+  const size_t a = (size_t)((N + rpc - 1) / rpc), b = (size_t)((N + rpo - 1) / rpo);
+  return (a > b ? a : b) * V * W;
 }
 
 template <typename T>
@@ -225,6 +371,20 @@ static void launch_segsum_t(const T* X, int ldx, const int* ids, int N, int W, i
     if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float) * (size_t)V * W, s);
     dim3 grid((W + kSegThreads - 1) / kSegThreads, (N + kAtomicRows - 1) / kAtomicRows);
     segsum_atomic_kernel<T><<<grid, kSegThreads, 0, s>>>(X, ldx, ids, perm, N, W, out);
+    return;
+  }
+  if (sizeof(T) == 2 && onehot_ok(X, ldx, ids, V) && onehot_fits(N, ldx)) {
+    const int rpc = onehot_rows_per_chunk(N, W);
+    const int nchunks = (N + rpc - 1) / rpc;
+    dim3 grid((W + kOhCols - 1) / kOhCols, nchunks);
+    const bf16* Xb = reinterpret_cast<const bf16*>(X);
+    switch ((V + 15) / 16) {
+#define OH(VT) \
+  case VT: onehot_segsum_kernel<VT><<<grid, kSegThreads, 0, s>>>(Xb, ldx, ids, N, W, V, rpc, workspace); break;
+      OH(1) OH(2) OH(3) OH(4) OH(5) OH(6) OH(7) OH(8)
+#undef OH
+    }
+    launch_reduce(workspace, nchunks, (int64_t)V * W, out, accumulate, s);
     return;
   }
   const int rpc = segsum_rows_per_chunk(N);
@@ -241,10 +401,7 @@ static void launch_segsum_t(const T* X, int ldx, const int* ids, int N, int W, i
     const size_t lds = sizeof(float) * V * kSegCols;
     segsum_lds_kernel<T><<<grid, kSegThreads, lds, s>>>(X, ldx, ids, N, W, V, rpc, workspace);
   }
-  const int64_t VW = (int64_t)V * W;
-  int nb = (int)((VW + kSegThreads - 1) / kSegThreads);
-  if (nb > 2048) nb = 2048;
-  segsum_reduce_kernel<<<nb, kSegThreads, 0, s>>>(workspace, nchunks, VW, out, accumulate);
+  launch_reduce(workspace, nchunks, (int64_t)V * W, out, accumulate, s);
 }
 
 void launch_segsum_bf16(const bf16* X, int ldx, const int* ids, int N, int W, int V, float* out,

@@ -64,6 +64,10 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
   // reused by every group: a barrier separates one group's epilogue reads from the next
   // group's stores
   __shared__ __attribute__((aligned(16))) float part[4][2][2][4][64][4];
+  // dropout: the tick's input-mask bytes of the workgroup's rows, [row][H/8] (H <= 512),
+  // double-buffered by tick (the G = 1 stash reads them after the tick's last barrier)
+  constexpr int kMaskDw = 2 * G;  // DMA dwords per lane: 32 G rows x H/32 dwords / 256 lanes
+  __shared__ __attribute__((aligned(16))) unsigned mlds[2][G * 512];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
@@ -127,6 +131,20 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
 #pragma unroll
       for (int gt = 0; gt < 4; ++gt) xs[i][j][gt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  auto zx_row = [&](int tk, int g) -> const float* {
+    const int b = (col * G + g) * 32 + 16 * J + (lane & 15);
+    if (!(L == 0 && tk < T && b < B)) return nullptr;
+    return a.ids ? a.zx0 + (size_t)a.ids[(size_t)tk * B + b] * a.zx_ld
+                 : a.zx0 + ((size_t)tk * B + b) * a.zx_ld;
+  };
+  auto zx_load = [&](const float* zr, float (&dst)[4][4]) {
+    if (zr) {
+#pragma unroll
+      for (int gt = 0; gt < 4; ++gt) ld4f(zr + (size_t)gt * H + u0, dst[gt]);
+    }
+  };
+  float zxn[4][4] = {};
+
   for (int tau = 0; tau <= T + LAG - 1; ++tau) {
     const bool on0 = tau < T;                  // layer l   computes step tau
     const bool on1 = tau >= LAG;               // layer l+1 computes step tau-LAG
@@ -140,20 +158,30 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     STAMPG(0, 0)
     // layer-l input projections of step tau (independent of the hand-off): group 0's rows are
     // loaded before the poll, group g+1's right behind group g's payload (a gathered row needs
-    // its id first; loaded for all groups here, the wait overlaps the poll)
-    auto zx_row = [&](int g) -> const float* {
-      const int b = (col * G + g) * 32 + 16 * J + (lane & 15);
-      if (!(L == 0 && on0 && b < B)) return nullptr;
-      return a.ids ? a.zx0 + (size_t)a.ids[(size_t)tau * B + b] * a.zx_ld
-                   : a.zx0 + ((size_t)tau * B + b) * a.zx_ld;
-    };
+    // its id first; loaded for all groups here, the wait overlaps the poll).  (Loading group 0's
+    // rows at the end of the previous tick measured slower: 603 -> 691 us per launch.)
     const float* zrows[G];
 #pragma unroll
-    for (int g = 0; g < G; ++g) zrows[g] = zx_row(g);
-    float zxn[4][4] = {};
-    if (zrows[0]) {
+    for (int g = 0; g < G; ++g) zrows[g] = zx_row(tau, g);
+    zx_load(zrows[0], zxn);
+    // dropout of layer l+1's input (layer l's h of step tau-1): the mask bytes of the
+    // workgroup's 32G rows for this tick, DMA'd into LDS before the poll (no registers; the
+    // poll barrier waits for them).  A global byte load at each use had put its latency on the
+    // tick's critical path.
+    const bool xdrop = a.xmask != nullptr && ld0 && tau >= 1;
+    if (xdrop) {
+      const int r0 = col * G * 32;
+      const __amdgpu_buffer_rsrc_t rm =
+          make_rsrc(a.xmask + ((size_t)(tau - 1) * B + r0) * (H / 8),
+                    B > r0 ? (size_t)(B - r0) * (H / 8) : 0);  // rows >= B read as zero
 #pragma unroll
-      for (int gt = 0; gt < 4; ++gt) ld4f(zrows[0] + (size_t)gt * H + u0, zxn[gt]);
+      for (int k = 0; k < kMaskDw; ++k) {
+        const int i0 = 256 * k + 64 * w;  // this wave's 64 dwords (G H is a multiple of 64)
+        if (i0 < G * H)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rm, (__attribute__((address_space(3))) void*)&mlds[tau & 1][i0], 4,
+              4 * (i0 + lane), 0, 0, 0);
+      }
     }
     // hand-offs of the previous tick: layer l's slot tau, layer l+1's slot tau-LAG (slot 0 of
     // either is the prep-written initial state)
@@ -212,20 +240,13 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
                                 : ld8_sc1(r1, rm_lane + rm_off(bg, j, s));
         }
       }
-      if (g + 1 < G && zrows[g + 1]) {
-#pragma unroll
-        for (int gt = 0; gt < 4; ++gt) ld4f(zrows[g + 1] + (size_t)gt * H + u0, zxn[gt]);
-      }
-      // dropout of layer l+1's input (layer l's h of step tau-1): mask bytes of this lane's
-      // x-part fragments (row b of tile j, k = kbase + 32 s + kq .. +7)
-      // (mask bytes are loaded at their use: no register is held for them across the
-      // payload phase, and only dropout pays their latency)
-      const bool xdrop = a.xmask != nullptr && ld0 && tau >= 1;
+      if (g + 1 < G) zx_load(zrows[g + 1], zxn);
+      // mask byte of this lane's x-part fragment (row 16 j + lane%16 of the group, k = kbase +
+      // 32 s + kq .. +7), from the LDS stage (read at its use: no register is held for it
+      // across the payload phase)
       auto mbyte = [&](int j, int s2) -> unsigned {
-        const int bj = bg * 32 + 16 * j + (lane & 15);
-        return bj < B ? (unsigned)a.xmask[((size_t)(tau - 1) * B + bj) * (H / 8) +
-                                          ((kbase + s2 * 32 + kq) >> 3)]
-                      : 0u;
+        const uint8_t* m = reinterpret_cast<const uint8_t*>(mlds[tau & 1]);
+        return m[(g * 32 + 16 * j + (lane & 15)) * (H / 8) + ((kbase + s2 * 32 + kq) >> 3)];
       };
       if (g > 0) __syncthreads();  // the previous group's epilogue has read the partials
       __builtin_amdgcn_sched_barrier(0);
@@ -343,7 +364,9 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
         STAMPG(g, 5)
         st4bf_sc1(ringL + (size_t)((t + 1) & 1) * ringsz + frag_index(b, u0, H), h[0], h[1], h[2],
                   h[3]);
-        do_stash();  // MFMAs while the ring stores drain
+        // the stash MFMAs run while the ring stores drain; with dropout (LDS mask reads and
+        // fragment masking) the stash outlasts the drain, so it follows the arrival instead
+        if (!xdrop) do_stash();
         if (g == G - 1 && signal) {
           // one arrival per wave and tick, for all its groups' ring stores
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -352,6 +375,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
             __hip_atomic_fetch_add((L ? cnt1 : cnt0) + (size_t)(t + 1) * 4, 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
         }
+        if (xdrop) do_stash();
         if (live) {  // row-major copies for the GEMMs / head (not handed off)
           const size_t o = (size_t)(t + 1) * B * H + bh;
           st4bf(hbL + o, h[0], h[1], h[2], h[3]);
@@ -407,6 +431,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
   // product reads them, so they live in LDS and leave the registers to W_h,l / W_h,l+1 and the
   // payload
   __shared__ __attribute__((aligned(16))) bf16x8 wx1l[4][KS][64];
+  __shared__ unsigned short mb16[G * 32];  // dropout bits of the tick (see mdrop)
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
@@ -453,6 +478,17 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
     const bool ld0 = tau >= 3;                // dZ_l[T+2-tau]   (published at tick tau-1)
     const int t = L ? T - 1 - tau : T + 1 - tau;  // this role's step
     const bool act = L ? on1 : on0;
+    // dropout of layer l's dtop (layer l+1's input mask, step T+1-tau): the 16 units' bits of
+    // the workgroup's 32G rows, loaded here and staged in LDS after the poll (read in the MFMA
+    // phases, each followed by a barrier: one buffer)
+    const bool mdrop = a.xmask != nullptr && on0;
+    unsigned short mreg = 0;
+    if (mdrop && threadIdx.x < G * 32) {
+      const int r = col * G * 32 + threadIdx.x;
+      if (r < B)
+        mreg = *reinterpret_cast<const unsigned short*>(
+            a.xmask + ((size_t)(T + 1 - tau) * B + r) * (H / 8) + (ub0 >> 3));
+    }
     // (a rolled loop: unrolled, the scheduler hoists the next group's operand loads into this
     // group's MFMA phase and the KS = 16 kernel spills)
 #pragma unroll 1
@@ -561,6 +597,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
                        : !poll_counter(ld1 ? cnt1 + (size_t)s1 * 4 : cnt0 + (size_t)s0 * 4,
                                        target, a.spin_limit, a.err, 10u);
           }
+          if (mdrop && threadIdx.x < G * 32) mb16[threadIdx.x] = mreg;
           STAMPG(g, 1)
         }
         // (for g > 0: the previous group's epilogue has read the partials)
@@ -599,13 +636,9 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
           if (on0) {  // layer l: dtop (stashed last tick) + dZ_l[t+1] · W_h,lᵀ
             float4 x0 = *reinterpret_cast<const float4*>(&xsl[g][w][j][lane][0]);
             if (a.xmask) {
-              // dropout of layer l+1's input on layer l's dtop (step T+1-tau), loaded at its use:
-              // no register is held for it across the payload phase
-              const int bj = (col * G + g) * 32 + 16 * j + (lane & 15);
-              const unsigned m =
-                  bj < B ? (unsigned)a.xmask[((size_t)(T + 1 - tau) * B + bj) * (H / 8) +
-                                             (u0 >> 3)] >> (u0 & 7)
-                         : 0u;
+              // dropout of layer l+1's input on layer l's dtop (step T+1-tau): this lane's 4
+              // units' bits from the LDS stage
+              const unsigned m = (unsigned)mb16[g * 32 + 16 * j + (lane & 15)] >> (u0 - ub0);
               x0.x = m & 1u ? x0.x * a.xscale : 0.f;
               x0.y = m & 2u ? x0.y * a.xscale : 0.f;
               x0.z = m & 4u ? x0.z * a.xscale : 0.f;

@@ -8,7 +8,6 @@
 
 namespace dcr {
 
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kAuxSc1 = 16;  // buffer-op cache-policy bits: sc1 (bypass L1, write-through)
 #ifndef XCD_GROUPING
 #define XCD_GROUPING 1

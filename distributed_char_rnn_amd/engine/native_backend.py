@@ -336,6 +336,7 @@ class NativeBackend:
             **plan,
             dtop=torch.empty(T, B, H, dtype=f32, device=dev) if training else None,
             dx=torch.empty(T, B, H, dtype=f32, device=dev) if training else None,
+            dx_bf=torch.empty(N, H, dtype=bf16, device=dev) if training else None,
             db_part=(torch.empty(self.L, nrow, GW, dtype=f32, device=dev)
                      if training else None),
             dew_part=(torch.empty(max(B // 16, 1), self.V, GW, dtype=f32, device=dev)
@@ -921,15 +922,20 @@ class NativeBackend:
                         on_ready(s.layer_range(layer)[1])
                     dtop = None
                     continue
-                dX = _mm_into(dZx, lw.Wx.t(), bufs["dx"].view(N, H)).view(T, B, H)
+                if layer > 0:
+                    dX = _mm_into(dZx, lw.Wx.t(), bufs["dx"].view(N, H)).view(T, B, H)
+                else:  # only the embedding gradient reads it: bf16 rows for the segment sum
+                    dX = torch.mm(dZx, lw.Wx.t(), out=bufs["dx_bf"]).view(T, B, H)
                 if dm is not None and dm["inb"][layer] is not None:  # this layer's input mask
                     dX = self._masked(dX, dm["inb"][layer], dm["sin"], out=dX).view(T, B, H)
                 if layer > 0:
                     dtop = dX
                 else:
-                    dXf = dX.reshape(N, H).float().contiguous()
-                    self._embed_grad(dXf, ids_tm, bufs)
-                    self._token_norm(dXf)
+                    # (bf16 as the GEMM wrote it: the segment sum and the norm accumulate in
+                    # fp32 either way; an fp32 copy would only add a pass over [N, H])
+                    dXt = dX.reshape(N, H)
+                    self._embed_grad(dXt, ids_tm, bufs)
+                    self._token_norm(dXt)
             if not written:
                 self._write_input_grads(layer, names, dWx, dbias)
             if layer == 0:

@@ -93,10 +93,15 @@ def test_xent_kernel(dcr_ops):
     torch.testing.assert_close(dl.float(), lt.grad, rtol=1e-2, atol=1e-5)
 
 
-@pytest.mark.parametrize("V,W,N", [(65, 256, 5000), (1, 130, 777), (200, 64, 300),
-                                   (1, 3072, 5000), (1, 520, 777)])
-def test_segsum_kernel(dcr_ops, V, W, N):
-    X = torch.randn(N, W, device="cuda").to(torch.bfloat16)
+@pytest.mark.parametrize("V,W,N,ld,dt", [
+    (65, 256, 5000, 256, "bf16"), (1, 130, 777, 130, "bf16"), (200, 64, 300, 64, "bf16"),
+    (1, 3072, 5000, 3072, "bf16"), (1, 520, 777, 520, "bf16"),
+    # 16-byte-row route (segsum_vec_kernel): full strips, a ragged last strip, strided rows
+    (65, 512, 32768, 512, "bf16"), (96, 136, 1000, 136, "bf16"), (65, 2048, 4097, 2056, "bf16"),
+    (65, 256, 5000, 256, "fp32")])
+def test_segsum_kernel(dcr_ops, V, W, N, ld, dt):
+    X = torch.randn(N, ld, device="cuda")
+    X = (X.to(torch.bfloat16) if dt == "bf16" else X)[:, :W]
     ids = torch.randint(0, V, (N,), device="cuda", dtype=torch.int32) if V > 1 else None
     out = torch.empty(V, W, device="cuda")
     ws = torch.empty(max(1, dcr_ops.segsum_workspace(N, W, V)), device="cuda")
