@@ -50,7 +50,7 @@ def parse(argv=None):
     ap.add_argument("--profile", action="store_true", help="print a per-phase timing table")
     ap.add_argument("--dist_backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="auto = nccl (RCCL over xGMI) on GPUs; gloo = multi-rank rehearsal on "
-                         "one GPU (with DCR_PERSIST=0: persistent grids of two processes cannot "
+                         "one GPU (with DCR_RECURRENCE=step: persistent grids of two processes cannot "
                          "share the CUs)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu = plumbing check of the multi-rank contract (reference backend, gloo)")

@@ -20,6 +20,7 @@
 // Counters: two sets per launch (phase A and phase B), one per (batch group, step, K quarter).
 #include "common.h"
 #include "kernels.h"
+#include "debug_env.h"
 #include "persist_common.h"
 #include <stdlib.h>
 
@@ -417,8 +418,7 @@ static int gru_grid(int H, int B, int ub) { return (H / (16 * ub)) * (B / 16); }
 // co-resident with the GPU to themselves; 0 = not supported (per-step kernels instead).
 int gru_persist_ub(int H, int B, int cus) {
   if (H % 128 != 0 || H < 128 || H > 1024 || B % 16 != 0 || B < 16 || cus <= 0) return 0;
-  const char* e = getenv("DCR_GRU_UB");
-  const int first = (e && e[0] == '1') ? 1 : 2;
+  const int first = debug_int("gru_ub", 2) == 1 ? 1 : 2;  // DCR_DEBUG=gru_ub=1: 16-unit blocks
   for (int ub = first; ub >= 1; --ub) {
     bool ok = true;
     for (int bwd = 0; bwd < 2 && ok; ++bwd) {

@@ -14,10 +14,6 @@ void launch_global_norm(const float* g, int64_t n, float* partials, float* norm_
                         hipStream_t stream);
 void launch_sumsq(const void* x, bool is_bf16, int64_t n, float* partials, float* out,
                   hipStream_t stream);
-bool tok_norm_supported(int64_t N, int H, int K);
-int tok_norm_num_partials(int64_t N, int H);
-void launch_tok_norm(const bf16* dz, const bf16* w, int64_t N, int H, int K, float* partials,
-                     float* out, hipStream_t stream);
 void launch_adam_clip(float* p, const float* g, float* m, float* v, bf16* pbf, int64_t n,
                       float* partials, float* norm_out, float lr_t, float b1, float b2, float eps,
                       float clip, float gscale, int64_t n_norm, const float* extra_sq,
@@ -98,12 +94,6 @@ struct LstmEwArgs {
 };
 void launch_lstm_ew(bool bwd, const LstmEwArgs& a, hipStream_t s);
 
-// ---- step_gemm.hip ----------------------------------------------------------------------
-bool step_gemm_supported(int B, int N, int K);
-int step_gemm_splits(int B, int N, int K);
-void launch_step_gemm(const bf16* X, const bf16* W, int B, int N, int K, int splits, float* part,
-                      hipStream_t stream);
-
 void launch_fwd_step(int cell, const FwdStepArgs& a, hipStream_t s);
 void launch_bwd_step(int cell, const BwdStepArgs& a, hipStream_t s);
 
@@ -146,15 +136,11 @@ struct PersistArgs {
   const float* dtop;     // bwd: [T, B, H] fp32 gradient from above
   bf16* dz;              // bwd: [T, B, 4H] bf16 gate-pre-activation gradients
   float* db_part;        // bwd: [B/16, 4H] per-batch-group bias-gradient partials (or nullptr)
-  const int* bids;       // (unused)
   float* dew_part;       // bwd layer-0 gather mode: [B/16, V, 4H] dEW partials (or nullptr)
   int V;
-  const bf16* Wx;        // fwd: W_xᵀ [4H, H] fused input projection; bwd: W_x of the layer above
-                         //   [H, 4H] (TF layout) to fuse dtop = dZ_above · W_xᵀ (or nullptr)
-  const bf16* dzx;       // bwd fused dtop: dZ of the layer above [T, B, 4H] bf16
+  const bf16* Wx;        // fwd: W_xᵀ [4H, H] fused input projection (or nullptr)
   const bf16* xin;       // fwd fused input: [T, B, H] bf16 layer input
   const float* bias;     // fwd fused input: [4H] fp32
-  uint64_t* ring;        // fwd granule hand-off: [2, B, H/2] tagged granules (nullptr = counters)
   unsigned* cnt;         // [B/16, T+1] arrival counters (zeroed by the launcher)
   unsigned* err;         // timeout / error word (0 = ok)
   unsigned long long* diag;  // optional [T, 8] s_memtime stamps of workgroup 0 (diagnostics)
@@ -163,22 +149,18 @@ struct PersistArgs {
   unsigned spin_limit;
   int excl;              // bwd: all-loads-in-flight variant (one WG per CU: nothing may run beside it)
   int cnt_zeroed;        // counters already zeroed by the caller (batched prep launch)
-  bf16* hring;           // fwd: optional [2, B, H] fragment-tiled h hand-off ring
-  bf16* zring;           // bwd: optional [2, B, 4H] fragment-tiled dZ hand-off ring
+  bf16* hring;           // fwd: [2, B, H] fragment-tiled h hand-off ring
+  bf16* zring;           // bwd: [2, B, 4H] fragment-tiled dZ hand-off ring
                          //   (persist_common.h frag_index); dz stays row-major for the GEMMs
 };
 int lstm_persist_supported(int H, int B, int cus);
 int lstm_persist_grid(int H, int B, int cus);
 int lstm_persist_xfuse_supported(int H, int B, int cus);
 // max co-resident workgroups per CU of the instantiation a launch with these flags would use
-// (flags: 1 fused input/dtop, 2 diag stamps, 4 exclusive bwd, 8 granule fwd; V>0: fused dEW LDS)
+// (flags: 1 fused input projection (fwd), 2 diag stamps, 4 exclusive bwd; V>0: fused dEW LDS)
 int lstm_persist_occupancy(int bwd, int H, int B, int V, int flags, int cus);
 // return 0 on success, <0 if the grid cannot be co-resident or the shape is unsupported
 int launch_lstm_fwd_persist(const PersistArgs& a, int cus, hipStream_t s);
-// large-H (1024 < H <= 2048) persistent forward, 8-unit weight shards (lstm_big.hip); needs the
-// fragment-order ring a.hring
-int lstm_big_supported(int H, int B, int cus);
-int launch_lstm_big_fwd(const PersistArgs& a, int cus, hipStream_t s);
 int launch_lstm_bwd_persist(const PersistArgs& a, int cus, hipStream_t s);
 
 // wide-vocabulary softmax CE (xent.hip): bias added in-kernel, fused d softmax_b, V % 4 == 0,

@@ -58,7 +58,7 @@ __device__ __forceinline__ bf16x8 mask_frag(const bf16x8& v, unsigned m) {
 // product in the group's MFMA phase: the ticks are work-bound there (the G phases run back to
 // back, one drain per tick), and the stash would cost 32 registers per group.
 // ------------------------------------------------------------------------------------------
-template <int KS, int G>
+template <int KS, int G, bool DROP>
 __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) {
   // partials [wave][layer][tile][gate][lane][r] (16-B lane stride: conflict-free b128 access),
   // reused by every group: a barrier separates one group's epilogue reads from the next
@@ -67,7 +67,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
   // dropout: the tick's input-mask bytes of the workgroup's rows, [row][H/8] (H <= 512),
   // double-buffered by tick (the G = 1 stash reads them after the tick's last barrier)
   constexpr int kMaskDw = 2 * G;  // DMA dwords per lane: 32 G rows x H/32 dwords / 256 lanes
-  __shared__ __attribute__((aligned(16))) unsigned mlds[2][G * 512];
+  __shared__ __attribute__((aligned(16))) unsigned mlds[2][DROP ? G * 512 : 1];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
@@ -168,7 +168,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     // workgroup's 32G rows for this tick, DMA'd into LDS before the poll (no registers; the
     // poll barrier waits for them).  A global byte load at each use had put its latency on the
     // tick's critical path.
-    const bool xdrop = a.xmask != nullptr && ld0 && tau >= 1;
+    const bool xdrop = DROP && ld0 && tau >= 1;
     if (xdrop) {
       const int r0 = col * G * 32;
       const __amdgpu_buffer_rsrc_t rm =
@@ -413,7 +413,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
 // (w+1)*H/4) of every gate g and keeps the W_h,l / W_h,l+1 rows of its units for that K quarter
 // in registers (W_x,l+1 in LDS).  Wave w runs the cell-backward epilogue of layer w>>1 (0 = l,
 // 1 = l+1), batch tile w&1, of every group.
-template <int KS, int G>
+template <int KS, int G, bool DROP>
 __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs a) {
   // partials [wave][layer][tile][lane][unit r]: single-buffered -- every group phase that
   // writes them starts with a barrier, which each epilogue wave joins after its reads
@@ -431,7 +431,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
   // product reads them, so they live in LDS and leave the registers to W_h,l / W_h,l+1 and the
   // payload
   __shared__ __attribute__((aligned(16))) bf16x8 wx1l[4][KS][64];
-  __shared__ unsigned short mb16[G * 32];  // dropout bits of the tick (see mdrop)
+  __shared__ unsigned short mb16[DROP ? G * 32 : 1];  // dropout bits of the tick (see mdrop)
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
@@ -481,7 +481,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
     // dropout of layer l's dtop (layer l+1's input mask, step T+1-tau): the 16 units' bits of
     // the workgroup's 32G rows, loaded here and staged in LDS after the poll (read in the MFMA
     // phases, each followed by a barrier: one buffer)
-    const bool mdrop = a.xmask != nullptr && on0;
+    const bool mdrop = DROP && on0;
     unsigned short mreg = 0;
     if (mdrop && threadIdx.x < G * 32) {
       const int r = col * G * 32 + threadIdx.x;
@@ -635,7 +635,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
           }
           if (on0) {  // layer l: dtop (stashed last tick) + dZ_l[t+1] · W_h,lᵀ
             float4 x0 = *reinterpret_cast<const float4*>(&xsl[g][w][j][lane][0]);
-            if (a.xmask) {
+            if constexpr (DROP) {
               // dropout of layer l+1's input on layer l's dtop (step T+1-tau): this lane's 4
               // units' bits from the LDS stage
               const unsigned m = (unsigned)mb16[g * 32 + 16 * j + (lane & 15)] >> (u0 - ub0);
@@ -703,50 +703,62 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
   }
 }
 
-template <int KS>
+// DROP: the dropout instantiation (layer l+1's input masks in-kernel); without dropout that
+// code is compiled out (same-box A/B: the runtime-conditional form cost 2.5 % per step)
+template <int KS, bool DROP>
 static const void* lstm2_fwd_g(int G) {
   switch (G) {
-    case 1: return (const void*)lstm2_fwd_persist_kernel<KS, 1>;
-    case 2: return (const void*)lstm2_fwd_persist_kernel<KS, 2>;
-    case 3: return (const void*)lstm2_fwd_persist_kernel<KS, 3>;
-    case 4: return (const void*)lstm2_fwd_persist_kernel<KS, 4>;
+    case 1: return (const void*)lstm2_fwd_persist_kernel<KS, 1, DROP>;
+    case 2: return (const void*)lstm2_fwd_persist_kernel<KS, 2, DROP>;
+    case 3: return (const void*)lstm2_fwd_persist_kernel<KS, 3, DROP>;
+    case 4: return (const void*)lstm2_fwd_persist_kernel<KS, 4, DROP>;
   }
   return nullptr;
 }
 
-static const void* lstm2_pick(int H, int G) {
+template <bool DROP>
+static const void* lstm2_pick_t(int H, int G) {
   switch (H / 128) {
-    case 1: return lstm2_fwd_g<1>(G);
-    case 2: return lstm2_fwd_g<2>(G);
-    case 3: return lstm2_fwd_g<3>(G);
-    case 4: return lstm2_fwd_g<4>(G);
+    case 1: return lstm2_fwd_g<1, DROP>(G);
+    case 2: return lstm2_fwd_g<2, DROP>(G);
+    case 3: return lstm2_fwd_g<3, DROP>(G);
+    case 4: return lstm2_fwd_g<4, DROP>(G);
   }
   return nullptr;
 }
+static const void* lstm2_pick(int H, int G, bool drop) {
+  return drop ? lstm2_pick_t<true>(H, G) : lstm2_pick_t<false>(H, G);
+}
 
-template <int KS>
+template <int KS, bool DROP>
 static const void* lstm2_bwd_g(int G) {
   switch (G) {
-    case 1: return (const void*)lstm2_bwd_persist_kernel<KS, 1>;
-    case 2: return (const void*)lstm2_bwd_persist_kernel<KS, 2>;
-    case 3: return (const void*)lstm2_bwd_persist_kernel<KS, 3>;
-    case 4: return (const void*)lstm2_bwd_persist_kernel<KS, 4>;
+    case 1: return (const void*)lstm2_bwd_persist_kernel<KS, 1, DROP>;
+    case 2: return (const void*)lstm2_bwd_persist_kernel<KS, 2, DROP>;
+    case 3: return (const void*)lstm2_bwd_persist_kernel<KS, 3, DROP>;
+    case 4: return (const void*)lstm2_bwd_persist_kernel<KS, 4, DROP>;
   }
   return nullptr;
 }
 
-static const void* lstm2_bwd_pick(int H, int G) {
+template <bool DROP>
+static const void* lstm2_bwd_pick_t(int H, int G) {
   switch (H / 32) {  // KS = 4H / 4 waves / 32
-    case 4: return lstm2_bwd_g<4>(G);
-    case 8: return lstm2_bwd_g<8>(G);
-    case 12: return lstm2_bwd_g<12>(G);
-    case 16: return lstm2_bwd_g<16>(G);
+    case 4: return lstm2_bwd_g<4, DROP>(G);
+    case 8: return lstm2_bwd_g<8, DROP>(G);
+    case 12: return lstm2_bwd_g<12, DROP>(G);
+    case 16: return lstm2_bwd_g<16, DROP>(G);
   }
   return nullptr;
+}
+static const void* lstm2_bwd_pick(int H, int G, bool drop) {
+  return drop ? lstm2_bwd_pick_t<true>(H, G) : lstm2_bwd_pick_t<false>(H, G);
 }
 
 static bool lstm2_fits(int H, int G, int cols, int cus) {
-  const void* fns[2] = {lstm2_pick(H, G), lstm2_bwd_pick(H, G)};
+  // every instantiation a launch at (H, G) may use must be co-resident
+  const void* fns[4] = {lstm2_pick(H, G, false), lstm2_bwd_pick(H, G, false),
+                        lstm2_pick(H, G, true), lstm2_bwd_pick(H, G, true)};
   for (const void* fn : fns) {
     int o = 0;
     if (!fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, fn, 256, 0) != hipSuccess || o < 1)
@@ -778,14 +790,14 @@ static bool lstm2_args_ok(int H, int B, int nbg, int G, int cus) {
 int launch_lstm2_fwd_persist(const Lstm2Args& a, int cus, hipStream_t s) {
   if (!lstm2_args_ok(a.H, a.B, a.nbg, a.G, cus) || !a.hring0 || !a.hring1) return -2;
   void* args[] = {const_cast<Lstm2Args*>(&a)};
-  return hipLaunchKernel(lstm2_pick(a.H, a.G), dim3(lstm2_grid(a.H, a.nbg, a.G)), dim3(256), args,
+  return hipLaunchKernel(lstm2_pick(a.H, a.G, a.xmask != nullptr), dim3(lstm2_grid(a.H, a.nbg, a.G)), dim3(256), args,
                          0, s) == hipSuccess ? 0 : -3;
 }
 
 int launch_lstm2_bwd_persist(const Lstm2BwdArgs& a, int cus, hipStream_t s) {
   if (!lstm2_args_ok(a.H, a.B, a.nbg, a.G, cus)) return -2;
   void* args[] = {const_cast<Lstm2BwdArgs*>(&a)};
-  return hipLaunchKernel(lstm2_bwd_pick(a.H, a.G), dim3(lstm2_grid(a.H, a.nbg, a.G)), dim3(256),
+  return hipLaunchKernel(lstm2_bwd_pick(a.H, a.G, a.xmask != nullptr), dim3(lstm2_grid(a.H, a.nbg, a.G)), dim3(256),
                          args, 0, s) == hipSuccess ? 0 : -3;
 }
 

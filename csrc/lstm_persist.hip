@@ -28,7 +28,6 @@
 #include "common.h"
 #include "kernels.h"
 #include "persist_common.h"
-#include <stdlib.h>
 
 namespace dcr {
 
@@ -144,7 +143,7 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
     }
     STAMP(2)
     // h_{t-1} fragments (handed off by other workgroups: sc1 loads only)
-    const bool fring = a.hring && t > 0;  // slot 0 (initial state) is row-major
+    const bool fring = t > 0;  // slot 0 (initial state) is row-major
     const __amdgpu_buffer_rsrc_t hsrc =
         fring ? make_rsrc(a.hring + (size_t)(t & 1) * B * H, sizeof(bf16) * (size_t)B * H)
               : make_rsrc(a.hbuf + (size_t)t * B * H, sizeof(bf16) * (size_t)B * H);
@@ -193,11 +192,9 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
       }
       const size_t o = (size_t)(t + 1) * B * H + bh;
       STAMP(5)
-      if (a.hring)  // handed off in fragment order (write-through); row-major copy below
-        st4bf_sc1(a.hring + (size_t)((t + 1) & 1) * B * H + frag_index(b, u0, H), h[0], h[1],
-                  h[2], h[3]);
-      else
-        st4bf_sc1(a.hbuf + o, h[0], h[1], h[2], h[3]);  // handed off: write-through
+      // handed off in fragment order (write-through); row-major copy below
+      st4bf_sc1(a.hring + (size_t)((t + 1) & 1) * B * H + frag_index(b, u0, H), h[0], h[1], h[2],
+                h[3]);
       if (t + 1 < T) {
         // each epilogue wave publishes its own 16-unit slab: drain ONLY the hand-off store
         // (the activation-cache stores below are issued after the arrival, so the wait does
@@ -208,179 +205,6 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
           __hip_atomic_fetch_add(cnt + (size_t)(t + 1) * 4, 1u, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (a.hring) st4bf(a.hbuf + o, h[0], h[1], h[2], h[3]);
-      *reinterpret_cast<float4*>(a.cbuf + o) = make_float4(c[0], c[1], c[2], c[3]);
-      if (a.gates) {
-        bf16* gp = a.gates + ((size_t)t * B + b) * 4 * H + u0;
-        st4bf(gp, gi[0], gi[1], gi[2], gi[3]);
-        st4bf(gp + H, gj[0], gj[1], gj[2], gj[3]);
-        st4bf(gp + 2 * H, gf[0], gf[1], gf[2], gf[3]);
-        st4bf(gp + 3 * H, go[0], go[1], go[2], go[3]);
-      }
-      if (t == T - 1 && a.hlast32)
-        *reinterpret_cast<float4*>(a.hlast32 + bh) = make_float4(h[0], h[1], h[2], h[3]);
-      if (t == T - 1 && a.clast32)
-        *reinterpret_cast<float4*>(a.clast32 + bh) = make_float4(c[0], c[1], c[2], c[3]);
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// forward, data-tagged granule hand-off (Guideline 16 R2: "the data IS the flag")
-// ------------------------------------------------------------------------------------------
-// h_t travels through a 2-slot ring of 8-byte granules {lo: 2 x bf16, hi: tag = t+1} stored
-// `sc1` by ONE store each.  A consumer wave polls exactly the granules its MFMA fragments need
-// (two 16-B `sc1` loads per fragment) until every tag matches, then repacks the payload: no
-// drain-then-signal round trip, no counter, no workgroup barrier before the MFMAs.  Slot
-// (t+1)&1 is rewritten only at step t+2, which needs h_{t+1} from every consumer of slot (t+1)&1
-// -- so no live slot is ever overwritten.  The ring is zeroed before every launch.
-__device__ __forceinline__ uint64_t granule(float a, float b, unsigned tag) {
-  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-  bf16x2 v;
-  v[0] = f2bf(a);
-  v[1] = f2bf(b);
-  return ((uint64_t)tag << 32) | (uint64_t)__builtin_bit_cast(unsigned, v);
-}
-
-template <int KS, int UB>
-__global__ void __launch_bounds__(256, 1) lstm_fwd_granule_kernel(PersistArgs a) {
-  __shared__ __attribute__((aligned(16))) float part[2][4][UB][4][64][4];  // parity double buffer
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int H = a.H, B = a.B, T = a.T;
-  const int nwg_u = H / (16 * UB);
-  int ubk, bg;
-  map_block(blockIdx.x, nwg_u, B / 16, ubk, bg);
-  const int ub0 = ubk * 16 * UB, b0 = bg * 16;
-  const int kq = 8 * (lane >> 4);
-  const int kbase = w * (KS * 32);
-  const int HG = H / 2;  // granules per batch row
-
-  bf16x8 wf[UB][4][KS];
-#pragma unroll
-  for (int ui = 0; ui < UB; ++ui)
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-#pragma unroll
-      for (int s = 0; s < KS; ++s)
-        wf[ui][g][s] = ld8(a.W + (size_t)(g * H + ub0 + ui * 16 + (lane & 15)) * H + kbase +
-                           s * 32 + kq);
-
-  const int b = b0 + (lane & 15);
-  const bool epi = w < UB;
-  const int u0 = ub0 + (epi ? w : 0) * 16 + 4 * (lane >> 4);
-  const size_t bh = (size_t)b * H + u0;
-  float c[4] = {0.f, 0.f, 0.f, 0.f};
-  if (epi) ld4f(a.cbuf + bh, c);
-  bool dead = false;
-  // this lane's granule offset inside a ring slot (bytes): row b, granule (kbase + kq) / 2
-  const unsigned goff = (unsigned)(((size_t)b * HG + (kbase + kq) / 2) * sizeof(uint64_t));
-
-  for (int t = 0; t < T; ++t) {
-    float zx[4][4];
-    if (epi) {
-      const float* zrow = a.ids ? a.zx + (size_t)a.ids[(size_t)t * B + b] * a.zx_ld
-                                : a.zx + ((size_t)t * B + b) * a.zx_ld;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) ld4f(zrow + (size_t)g * H + u0, zx[g]);
-    }
-    bf16x8 hf[KS];
-    if (t == 0) {
-#pragma unroll
-      for (int s = 0; s < KS; ++s) hf[s] = ld8(a.hbuf + (size_t)b * H + kbase + s * 32 + kq);
-    } else {
-      const __amdgpu_buffer_rsrc_t rs =
-          make_rsrc(a.ring + (size_t)(t & 1) * B * HG, sizeof(uint64_t) * (size_t)B * HG);
-      const unsigned tag = (unsigned)t;
-      // probe: wave 0 watches ONE sentinel granule per producer slab (the last granule of batch
-      // row b0+15 of every 16-unit slab; lane l < H/16 watches slab l) so the payload is read
-      // ~once instead of being re-polled by every wave; stores are unordered, so the payload
-      // tags are still verified below (re-polled on the rare miss)
-      if (w == 0 && !dead) {
-        const int nslab = H / 16;
-        const unsigned soff = (unsigned)((((size_t)(b0 + 15) * HG) + (lane % nslab) * 8 + 7) *
-                                         sizeof(uint64_t));
-        unsigned sp = 0;
-        for (;;) {
-          typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-          const u32x2 gv = __builtin_amdgcn_raw_buffer_load_b64(rs, soff, 0, kAuxSc1);
-          if (__all(gv[1] == tag)) break;
-          if (++sp > a.spin_limit) {
-            __hip_atomic_store(a.err, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            dead = true;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-      __syncthreads();
-      unsigned spins = 0;
-      for (;;) {
-        bool ok = true;
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(rs, goff + s * 128, 0, kAuxSc1);
-          const u32x4 hi = __builtin_amdgcn_raw_buffer_load_b128(rs, goff + s * 128 + 16, 0, kAuxSc1);
-          ok &= (lo[1] == tag) & (lo[3] == tag) & (hi[1] == tag) & (hi[3] == tag);
-          u32x4 d;
-          d[0] = lo[0]; d[1] = lo[2]; d[2] = hi[0]; d[3] = hi[2];
-          hf[s] = __builtin_bit_cast(bf16x8, d);
-        }
-        if (__all(ok) || dead) break;
-        if (++spins > a.spin_limit) {
-          __hip_atomic_store(a.err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          dead = true;  // keep the barrier count consistent; results are garbage, err is set
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-#pragma unroll
-    for (int ui = 0; ui < UB; ++ui) {
-      f32x4 acc[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < KS; ++s)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) acc[g] = mfma16(wf[ui][g][s], hf[s], acc[g]);
-      float* dst = &part[t & 1][w][ui][0][lane][0];
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<float4*>(dst + g * 256) = make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
-    }
-    __syncthreads();
-    if (epi) {
-      float z[4][4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float4 s0 = *reinterpret_cast<const float4*>(&part[t & 1][0][w][g][lane][0]);
-        float4 s1 = *reinterpret_cast<const float4*>(&part[t & 1][1][w][g][lane][0]);
-        float4 s2 = *reinterpret_cast<const float4*>(&part[t & 1][2][w][g][lane][0]);
-        float4 s3 = *reinterpret_cast<const float4*>(&part[t & 1][3][w][g][lane][0]);
-        z[g][0] = s0.x + s1.x + s2.x + s3.x + zx[g][0];
-        z[g][1] = s0.y + s1.y + s2.y + s3.y + zx[g][1];
-        z[g][2] = s0.z + s1.z + s2.z + s3.z + zx[g][2];
-        z[g][3] = s0.w + s1.w + s2.w + s3.w + zx[g][3];
-      }
-      float gi[4], gj[4], gf[4], go[4], h[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        gi[r] = sigmoidf_(z[0][r]);
-        gj[r] = tanhf_(z[1][r]);
-        gf[r] = sigmoidf_(z[2][r] + a.forget_bias);
-        go[r] = sigmoidf_(z[3][r]);
-        c[r] = gf[r] * c[r] + gi[r] * gj[r];
-        h[r] = go[r] * tanhf_(c[r]);
-      }
-      if (t + 1 < T) {  // publish first: the hand-off is the critical path
-        uint64_t* gp = a.ring + (size_t)((t + 1) & 1) * B * HG + (size_t)b * HG + u0 / 2;
-        const unsigned tag = (unsigned)(t + 1);
-        __hip_atomic_store(gp, granule(h[0], h[1], tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(gp + 1, granule(h[2], h[3], tag), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      }
-      const size_t o = (size_t)(t + 1) * B * H + bh;
       st4bf(a.hbuf + o, h[0], h[1], h[2], h[3]);
       *reinterpret_cast<float4*>(a.cbuf + o) = make_float4(c[0], c[1], c[2], c[3]);
       if (a.gates) {
@@ -401,15 +225,11 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_granule_kernel(PersistArgs a)
 // ------------------------------------------------------------------------------------------
 // backward (BPTT)
 // ------------------------------------------------------------------------------------------
-// XB: the gradient arriving from the layer above, dtop_t = dZ^{l+1}_t · W_x^{l+1}ᵀ, is computed
-// in-kernel from register-resident W_x^{l+1} rows and the (already complete) dZ of the layer
-// above while the workgroup waits for the dZ_{t+1} hand-off -- no dX GEMM on the critical path.
-//
 // EXCL: all KS payload loads of a step are forced in flight together (sched_barrier); the extra
 // 4*KS live VGPRs push KS=16/UB=2 past 256 registers, i.e. one workgroup per CU, so this variant
 // is only launched when nothing can run beside it (see lstm_persist_occupancy and the backend's
 // exclusive mode).  Measured at H=512, B=256: 4.32 vs 5.0 us per BPTT step.
-template <int KS, int UB, bool DIAG = false, bool XB = false, bool EXCL = false>
+template <int KS, int UB, bool DIAG = false, bool EXCL = false>
 __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a) {
   __shared__ __attribute__((aligned(16))) float part[2][4][UB][64][4];  // parity double buffer
   // optional fused dEW accumulator (layer-0 gather mode): [V][UB*64] fp32, dynamic
@@ -436,17 +256,8 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
 #pragma unroll
     for (int s = 0; s < KS; ++s)
       wf[ui][s] = ld8(a.W + (size_t)(ub0 + ui * 16 + (lane & 15)) * G4H + kcol(s) + kq);
-  bf16x8 xw[XB ? UB : 1][XB ? KS : 1];
-  if constexpr (XB) {
-#pragma unroll
-    for (int ui = 0; ui < UB; ++ui)
-#pragma unroll
-      for (int s = 0; s < KS; ++s)
-        xw[ui][s] = ld8(a.Wx + (size_t)(ub0 + ui * 16 + (lane & 15)) * G4H + kcol(s) + kq);
-  }
 
   const int b = b0 + (lane & 15);
-  const unsigned doff = (unsigned)(((size_t)b * G4H + kq) * sizeof(bf16));
 
   const bool epi = w < UB;
   const int u0 = ub0 + (epi ? w : 0) * 16 + 4 * (lane >> 4);
@@ -479,47 +290,29 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
       ld4bf(gp, gi); ld4bf(gp + H, gj); ld4bf(gp + 2 * H, gf); ld4bf(gp + 3 * H, go);
       ld4f(a.cbuf + (size_t)(t + 1) * B * H + bh, cc);
       ld4f(a.cbuf + (size_t)t * B * H + bh, cp);
-      if constexpr (!XB) ld4f(a.dtop + (size_t)t * B * H + bh, dtop);
+      ld4f(a.dtop + (size_t)t * B * H + bh, dtop);
     }
-    // per-wave partial sums over this wave's K quarter: [x-part (XB)] + recurrent part
+    // per-wave partial sums of the recurrent product over this wave's K quarter
     f32x4 pacc[UB];
 #pragma unroll
     for (int ui = 0; ui < UB; ++ui) pacc[ui] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (XB) {
-      const bf16* zp = a.dzx + ((size_t)t * B + b) * G4H + kq;
-      bf16x8 zf[KS];
-#pragma unroll
-      for (int s = 0; s < KS; ++s) zf[s] = ld8(zp + kcol(s));
-#pragma unroll
-      for (int ui = 0; ui < UB; ++ui)
-#pragma unroll
-        for (int s = 0; s < KS; ++s) pacc[ui] = mfma16(xw[ui][s], zf[s], pacc[ui]);
-    }
-    if (t < T - 1 || XB) {
-     if (t < T - 1) {
+    if (t < T - 1) {
       if (threadIdx.x == kLstmPollerThread && !dead)
         dead = !poll_counter(cnt + (size_t)(t + 1) * 4, (unsigned)(H / 16), a.spin_limit, a.err, 2u);
       STAMP(1)
       __syncthreads();
       STAMP(2)
+      // fragment-tiled ring: one contiguous 1 KB load per k-step
       bf16x8 df[KS];
-      if (a.zring) {  // fragment-tiled ring: one contiguous 1 KB load per k-step
-        const __amdgpu_buffer_rsrc_t zsrc =
-            make_rsrc(a.zring + (size_t)((t + 1) & 1) * B * G4H, sizeof(bf16) * (size_t)B * G4H);
+      const __amdgpu_buffer_rsrc_t zsrc =
+          make_rsrc(a.zring + (size_t)((t + 1) & 1) * B * G4H, sizeof(bf16) * (size_t)B * G4H);
 #pragma unroll
-        for (int s = 0; s < KS; ++s) df[s] = ld8_sc1(zsrc, frag_load_off(bg, kcol(s) >> 5, G4H, lane));
-      } else {
-        const __amdgpu_buffer_rsrc_t dsrc =
-            make_rsrc(a.dz + (size_t)(t + 1) * B * G4H, sizeof(bf16) * (size_t)B * G4H);
-#pragma unroll
-        for (int s = 0; s < KS; ++s) df[s] = ld8_sc1(dsrc, doff + kcol(s) * 2);
-      }
+      for (int s = 0; s < KS; ++s) df[s] = ld8_sc1(zsrc, frag_load_off(bg, kcol(s) >> 5, G4H, lane));
       if constexpr (EXCL) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int ui = 0; ui < UB; ++ui)
 #pragma unroll
         for (int s = 0; s < KS; ++s) pacc[ui] = mfma16(wf[ui][s], df[s], pacc[ui]);
-     }
 #pragma unroll
       for (int ui = 0; ui < UB; ++ui)
         *reinterpret_cast<float4*>(&part[t & 1][w][ui][lane][0]) =
@@ -530,11 +323,7 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
     }
     if (epi) {
       float dh[4];
-      if constexpr (XB) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dtop[r] = 0.f;
-      }
-      if (t < T - 1 || XB) {
+      if (t < T - 1) {
         const float4 s0 = *reinterpret_cast<const float4*>(&part[t & 1][0][w][lane][0]);
         const float4 s1 = *reinterpret_cast<const float4*>(&part[t & 1][1][w][lane][0]);
         const float4 s2 = *reinterpret_cast<const float4*>(&part[t & 1][2][w][lane][0]);
@@ -559,18 +348,12 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
       }
       STAMP(5)
       bf16* dz = a.dz + ((size_t)t * B + b) * G4H + u0;
-      bf16* const zr = a.zring ? a.zring + (size_t)(t & 1) * B * G4H : nullptr;
-      if (zr) {  // handed-off copy in fragment order; row-major dz after the arrival
-        st4bf_sc1(zr + frag_index(b, u0, G4H), di[0], di[1], di[2], di[3]);
-        st4bf_sc1(zr + frag_index(b, H + u0, G4H), dj[0], dj[1], dj[2], dj[3]);
-        st4bf_sc1(zr + frag_index(b, 2 * H + u0, G4H), df_[0], df_[1], df_[2], df_[3]);
-        st4bf_sc1(zr + frag_index(b, 3 * H + u0, G4H), dO[0], dO[1], dO[2], dO[3]);
-      } else {
-        st4bf_sc1(dz, di[0], di[1], di[2], di[3]);
-        st4bf_sc1(dz + H, dj[0], dj[1], dj[2], dj[3]);
-        st4bf_sc1(dz + 2 * H, df_[0], df_[1], df_[2], df_[3]);
-        st4bf_sc1(dz + 3 * H, dO[0], dO[1], dO[2], dO[3]);
-      }
+      // handed-off copy in fragment order; row-major dz after the arrival
+      bf16* const zr = a.zring + (size_t)(t & 1) * B * G4H;
+      st4bf_sc1(zr + frag_index(b, u0, G4H), di[0], di[1], di[2], di[3]);
+      st4bf_sc1(zr + frag_index(b, H + u0, G4H), dj[0], dj[1], dj[2], dj[3]);
+      st4bf_sc1(zr + frag_index(b, 2 * H + u0, G4H), df_[0], df_[1], df_[2], df_[3]);
+      st4bf_sc1(zr + frag_index(b, 3 * H + u0, G4H), dO[0], dO[1], dO[2], dO[3]);
       if (t > 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         STAMP(6)
@@ -578,12 +361,10 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
           __hip_atomic_fetch_add(cnt + (size_t)t * 4, 1u, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (zr) {
-        st4bf(dz, di[0], di[1], di[2], di[3]);
-        st4bf(dz + H, dj[0], dj[1], dj[2], dj[3]);
-        st4bf(dz + 2 * H, df_[0], df_[1], df_[2], df_[3]);
-        st4bf(dz + 3 * H, dO[0], dO[1], dO[2], dO[3]);
-      }
+      st4bf(dz, di[0], di[1], di[2], di[3]);
+      st4bf(dz + H, dj[0], dj[1], dj[2], dj[3]);
+      st4bf(dz + 2 * H, df_[0], df_[1], df_[2], df_[3]);
+      st4bf(dz + 3 * H, dO[0], dO[1], dO[2], dO[3]);
       // off the critical path (after the arrival): accumulate the bf16-rounded dz exactly as
       // the dW GEMMs will see it
       float q[4][4];
@@ -642,36 +423,27 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
 // host side
 // ------------------------------------------------------------------------------------------
 // Kernel selection returns the exact instantiation so that launch and residency query agree.
-enum : int { PF_FUSED = 1, PF_DIAG = 2, PF_EXCL = 4, PF_GRANULE = 8 };
+enum : int { PF_FUSED = 1, PF_DIAG = 2, PF_EXCL = 4 };
 
 template <int KS, int UB>
 static const void* fwd_fn(int flags) {
-  if (flags & PF_GRANULE) return (const void*)lstm_fwd_granule_kernel<KS, UB>;
   if (flags & PF_FUSED) return (const void*)lstm_fwd_persist_kernel<KS, UB, false, true>;
   if (flags & PF_DIAG) return (const void*)lstm_fwd_persist_kernel<KS, UB, true, false>;
   return (const void*)lstm_fwd_persist_kernel<KS, UB, false, false>;
 }
 template <int KS, int UB>
 static const void* bwd_fn(int flags) {
-  if (flags & PF_FUSED) return (const void*)lstm_bwd_persist_kernel<KS, UB, false, true>;
   const bool d = flags & PF_DIAG, e = flags & PF_EXCL;
-  if (d && e) return (const void*)lstm_bwd_persist_kernel<KS, UB, true, false, true>;
-  if (d) return (const void*)lstm_bwd_persist_kernel<KS, UB, true, false, false>;
-  if (e) return (const void*)lstm_bwd_persist_kernel<KS, UB, false, false, true>;
-  return (const void*)lstm_bwd_persist_kernel<KS, UB, false, false, false>;
+  if (d && e) return (const void*)lstm_bwd_persist_kernel<KS, UB, true, true>;
+  if (d) return (const void*)lstm_bwd_persist_kernel<KS, UB, true, false>;
+  if (e) return (const void*)lstm_bwd_persist_kernel<KS, UB, false, true>;
+  return (const void*)lstm_bwd_persist_kernel<KS, UB, false, false>;
 }
 
 static int ub_for(int H, int B, int cus) {
-  // DCR_PERSIST_UB=1 forces 16-unit workgroups; default: 32-unit workgroups (measured 3.84 vs
-  // 4.02 ms/step at B=256, H=512: half the pollers, half the backward hand-off traffic);
-  // 16-unit ones only when H/16 is odd
+  // 32-unit workgroups (measured 3.84 vs 4.02 ms/step at B=256, H=512 against 16-unit ones:
+  // half the pollers, half the backward hand-off traffic); 16-unit ones only when H/16 is odd
   (void)B; (void)cus;
-  static int forced = -1;
-  if (forced < 0) {
-    const char* e = getenv("DCR_PERSIST_UB");
-    forced = (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
-  }
-  if (forced == 1) return 1;
   return ((H / 16) % 2 == 0) ? 2 : 1;
 }
 
@@ -741,18 +513,19 @@ static int launch_persist(int bwd, const PersistArgs& a, int flags, int cus, hip
     return -2;
   if (!a.cnt_zeroed)
     (void)hipMemsetAsync(a.cnt, 0, sizeof(unsigned) * (size_t)(a.B / 16) * (a.T + 1) * 4, s);
-  if (a.ring) (void)hipMemsetAsync(a.ring, 0, sizeof(uint64_t) * 2 * (size_t)a.B * (a.H / 2), s);
   void* args[] = {const_cast<PersistArgs*>(&a)};
   return hipLaunchKernel(fn, dim3(grid), dim3(256), args, lds, s) == hipSuccess ? 0 : -3;
 }
 
 int launch_lstm_fwd_persist(const PersistArgs& a, int cus, hipStream_t s) {
-  const int flags = (a.ring ? PF_GRANULE : 0) | (a.Wx ? PF_FUSED : 0) | (a.diag ? PF_DIAG : 0);
+  if (!a.hring) return -1;
+  const int flags = (a.Wx ? PF_FUSED : 0) | (a.diag ? PF_DIAG : 0);
   return launch_persist(0, a, flags, cus, s);
 }
 
 int launch_lstm_bwd_persist(const PersistArgs& a, int cus, hipStream_t s) {
-  const int flags = (a.Wx ? PF_FUSED : 0) | (a.diag ? PF_DIAG : 0) | (a.excl ? PF_EXCL : 0);
+  if (!a.zring) return -1;
+  const int flags = (a.diag ? PF_DIAG : 0) | (a.excl ? PF_EXCL : 0);
   return launch_persist(1, a, flags, cus, s);
 }
 

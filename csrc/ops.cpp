@@ -47,20 +47,6 @@ void sumsq(const at::Tensor& x, at::Tensor& partials, at::Tensor& out) {
                     ptr<float>(partials), ptr<float>(out), cur_stream());
 }
 
-// out[0] = sum over rows of ||dz[n, :] · wᵀ||^2  (dz [N, K] bf16, w [H, K] bf16), fused
-void tok_norm(const at::Tensor& dz, const at::Tensor& w, at::Tensor& partials, at::Tensor& out) {
-  CHECK_DEV(dz); CHECK_CONTIG(dz); CHECK_BF16(dz); CHECK_ALIGN16(dz);
-  CHECK_DEV(w); CHECK_CONTIG(w); CHECK_BF16(w); CHECK_ALIGN16(w);
-  CHECK_F32(partials); CHECK_F32(out);
-  TORCH_CHECK(dz.dim() == 2 && w.dim() == 2 && dz.size(1) == w.size(1), "tok_norm: shapes");
-  const int64_t N = dz.size(0);
-  const int H = (int)w.size(0), K = (int)w.size(1);
-  TORCH_CHECK(dcr::tok_norm_supported(N, H, K), "tok_norm: unsupported shape");
-  TORCH_CHECK(partials.numel() >= dcr::tok_norm_num_partials(N, H), "partials too small");
-  dcr::launch_tok_norm(ptr<bf16>(dz), ptr<bf16>(w), N, H, K, ptr<float>(partials),
-                       ptr<float>(out), cur_stream());
-}
-
 void adam_clip(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
                const c10::optional<at::Tensor>& pbf, at::Tensor& partials, at::Tensor& norm_out,
                double lr_t, double b1, double b2, double eps, double clip, double gscale,
@@ -262,20 +248,6 @@ void lstm_step_ew_bwd(const at::Tensor& dtop, const c10::optional<at::Tensor>& d
   a.dc = ptr<float>(dc);
   a.dz_out = ptr<bf16>(dz_out);
   dcr::launch_lstm_ew(true, a, cur_stream());
-}
-
-// partial[z] = X[:, z-th K slice] · W[:, same]ᵀ for z < S (step_gemm.hip); part [S, B, N] fp32
-void step_gemm(const at::Tensor& X, const at::Tensor& W, at::Tensor& part) {
-  check_seq(X, at::kBFloat16, "X");
-  check_seq(W, at::kBFloat16, "W");
-  check_seq(part, at::kFloat, "part");
-  TORCH_CHECK(X.dim() == 2 && W.dim() == 2 && X.size(1) == W.size(1), "step_gemm: shapes");
-  const int B = (int)X.size(0), K = (int)X.size(1), N = (int)W.size(0);
-  TORCH_CHECK(dcr::step_gemm_supported(B, N, K), "step_gemm: unsupported shape");
-  TORCH_CHECK(part.numel() % ((int64_t)B * N) == 0, "part must be [S, B, N]");
-  const int S = (int)(part.numel() / ((int64_t)B * N));
-  TORCH_CHECK(S >= 1 && K % (32 * S) == 0, "step_gemm: K must split into S 32-multiples");
-  dcr::launch_step_gemm(ptr<bf16>(X), ptr<bf16>(W), B, N, K, S, ptr<float>(part), cur_stream());
 }
 
 void rnn_bwd_seq(int64_t cell, const at::Tensor& W, const c10::optional<at::Tensor>& W2,
@@ -492,11 +464,10 @@ int64_t lstm_persist_supported(int64_t H, int64_t B) {
 void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::optional<at::Tensor>& ids,
                       at::Tensor& hbuf, at::Tensor& cbuf, const c10::optional<at::Tensor>& gates,
                       at::Tensor& hlast32, at::Tensor& cnt, at::Tensor& err, double forget_bias,
-                      int64_t spin_limit, const c10::optional<at::Tensor>& ring,
+                      int64_t spin_limit, at::Tensor& hring,
                       const c10::optional<at::Tensor>& diag, const c10::optional<at::Tensor>& WxT,
                       const c10::optional<at::Tensor>& xin, const c10::optional<at::Tensor>& bias,
-                      bool cnt_zeroed, const c10::optional<at::Tensor>& hring,
-                      const c10::optional<at::Tensor>& clast32) {
+                      bool cnt_zeroed, const c10::optional<at::Tensor>& clast32) {
   check_seq(WT, at::kBFloat16, "WT");
   check_seq(zx, at::kFloat, "zx");
   check_seq(hbuf, at::kBFloat16, "hbuf");
@@ -540,11 +511,6 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
   a.B = B; a.H = H; a.T = T;
   a.forget_bias = (float)forget_bias;
   a.spin_limit = (unsigned)spin_limit;
-  if (has(ring)) {
-    TORCH_CHECK(ring->is_cuda() && ring->element_size() == 8 && ring->is_contiguous(), "ring must be a contiguous 8-byte GPU tensor");
-    TORCH_CHECK(ring->numel() >= (int64_t)2 * B * (H / 2), "ring must hold [2, B, H/2] granules");
-    a.ring = reinterpret_cast<uint64_t*>(ring->data_ptr());
-  }
   if (xfuse) {
     a.Wx = optr<bf16>(WxT);
     a.xin = optr<bf16>(xin);
@@ -560,12 +526,9 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
     TORCH_CHECK(clast32->numel() == (int64_t)B * H, "clast32 must be [B, H]");
     a.clast32 = ptr<float>(*clast32);
   }
-  if (has(hring)) {
-    TORCH_CHECK(!has(ring), "the fragment ring and the granule hand-off are exclusive");
-    check_seq(*hring, at::kBFloat16, "hring");
-    TORCH_CHECK(hring->numel() >= (int64_t)2 * B * H, "hring must hold [2, B, H]");
-    a.hring = ptr<bf16>(*hring);
-  }
+  check_seq(hring, at::kBFloat16, "hring");
+  TORCH_CHECK(hring.numel() >= (int64_t)2 * B * H, "hring must hold [2, B, H]");
+  a.hring = ptr<bf16>(hring);
   const int rc = dcr::launch_lstm_fwd_persist(a, num_cus(), cur_stream());
   TORCH_CHECK(rc == 0, "persistent LSTM forward not launched (", rc,
               "): grid cannot be co-resident on this GPU for H=", H, " B=", B);
@@ -573,12 +536,10 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
 
 void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& dz,
                       const at::Tensor& gates, const at::Tensor& cbuf, at::Tensor& cnt,
-                      at::Tensor& err, int64_t spin_limit, const c10::optional<at::Tensor>& db_part,
-                      const c10::optional<at::Tensor>& ids,
+                      at::Tensor& err, int64_t spin_limit, at::Tensor& zring,
+                      const c10::optional<at::Tensor>& db_part, const c10::optional<at::Tensor>& ids,
                       const c10::optional<at::Tensor>& dew_part, int64_t V,
-                      const c10::optional<at::Tensor>& diag, const c10::optional<at::Tensor>& Wx_above,
-                      const c10::optional<at::Tensor>& dz_above, bool exclusive, bool cnt_zeroed,
-                      const c10::optional<at::Tensor>& zring) {
+                      const c10::optional<at::Tensor>& diag, bool exclusive, bool cnt_zeroed) {
   check_seq(W, at::kBFloat16, "W");
   check_seq(dtop, at::kFloat, "dtop");
   check_seq(dz, at::kBFloat16, "dz");
@@ -617,88 +578,14 @@ void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& d
     TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)T * 8, "diag must hold [T, 8] int64");
     a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());
   }
-  if (has(Wx_above)) {
-    check_seq(*Wx_above, at::kBFloat16, "Wx_above");
-    TORCH_CHECK(has(dz_above), "dz_above required with Wx_above");
-    check_seq(*dz_above, at::kBFloat16, "dz_above");
-    TORCH_CHECK(Wx_above->size(0) == H && Wx_above->size(1) == 4 * H, "Wx_above must be [H, 4H]");
-    TORCH_CHECK(dz_above->numel() == (int64_t)T * B * 4 * H, "dz_above must be [T, B, 4H]");
-    TORCH_CHECK(dcr::lstm_persist_xfuse_supported(H, B, num_cus()), "fused-dtop persistent BPTT unsupported");
-    a.Wx = optr<bf16>(Wx_above);
-    a.dzx = optr<bf16>(dz_above);
-  }
   a.excl = exclusive ? 1 : 0;
   a.cnt_zeroed = cnt_zeroed ? 1 : 0;
-  if (has(zring)) {
-    check_seq(*zring, at::kBFloat16, "zring");
-    TORCH_CHECK(zring->numel() >= (int64_t)2 * B * 4 * H, "zring must hold [2, B, 4H]");
-    a.zring = ptr<bf16>(*zring);
-  }
+  check_seq(zring, at::kBFloat16, "zring");
+  TORCH_CHECK(zring.numel() >= (int64_t)2 * B * 4 * H, "zring must hold [2, B, 4H]");
+  a.zring = ptr<bf16>(zring);
   const int rc = dcr::launch_lstm_bwd_persist(a, num_cus(), cur_stream());
   TORCH_CHECK(rc == 0, "persistent LSTM BPTT not launched (", rc,
               "): grid cannot be co-resident on this GPU for H=", H, " B=", B);
-}
-
-// ------------------------------------------------------------------------------------------
-// large-H persistent LSTM forward (lstm_big.hip)
-void lstm_big_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::optional<at::Tensor>& ids,
-                  at::Tensor& hbuf, at::Tensor& cbuf, const c10::optional<at::Tensor>& gates,
-                  at::Tensor& hlast32, at::Tensor& cnt, at::Tensor& err, double forget_bias,
-                  int64_t spin_limit, at::Tensor& hring, bool cnt_zeroed,
-                  const c10::optional<at::Tensor>& clast32,
-                  const c10::optional<at::Tensor>& diag) {
-  check_seq(WT, at::kBFloat16, "WT");
-  check_seq(zx, at::kFloat, "zx");
-  check_seq(hbuf, at::kBFloat16, "hbuf");
-  check_seq(cbuf, at::kFloat, "cbuf");
-  check_seq(hlast32, at::kFloat, "hlast32");
-  check_seq(hring, at::kBFloat16, "hring");
-  check_opt(gates, at::kBFloat16, "gates");
-  check_opt(ids, at::kInt, "ids");
-  TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == at::kInt && err.scalar_type() == at::kInt,
-              "cnt/err must be int32 GPU tensors");
-  const int T = (int)hbuf.size(0) - 1, B = (int)hbuf.size(1), H = (int)hbuf.size(2);
-  TORCH_CHECK(dcr::lstm_big_supported(H, B, num_cus()), "large-H persistent LSTM unsupported for H=",
-              H, " B=", B);
-  TORCH_CHECK(WT.size(0) == 4 * H && WT.size(1) == H, "WT must be [4H, H]");
-  TORCH_CHECK(zx.size(-1) == 4 * H, "zx rows must be 4H wide");
-  if (has(ids)) {
-    TORCH_CHECK(ids->numel() == (int64_t)T * B, "ids must be [T, B]");
-  } else {
-    TORCH_CHECK(zx.numel() == (int64_t)T * B * 4 * H, "zx must be [T, B, 4H]");
-  }
-  TORCH_CHECK(cbuf.numel() == (int64_t)(T + 1) * B * H, "cbuf must be [T+1, B, H]");
-  TORCH_CHECK(hlast32.numel() == (int64_t)B * H, "hlast32 must be [B, H]");
-  if (has(gates)) TORCH_CHECK(gates->numel() == (int64_t)T * B * 4 * H, "gates must be [T, B, 4H]");
-  TORCH_CHECK(hring.numel() >= (int64_t)2 * B * H, "hring must hold [2, B, H]");
-  TORCH_CHECK(cnt.numel() >= (int64_t)(B / 16) * (T + 1) * 4, "counter buffer too small");
-  dcr::PersistArgs a{};
-  a.W = ptr<bf16>(WT);
-  a.zx = ptr<float>(zx);
-  a.ids = optr<int>(ids);
-  a.zx_ld = 4 * H;
-  a.hbuf = ptr<bf16>(hbuf);
-  a.cbuf = ptr<float>(cbuf);
-  a.gates = optr<bf16>(gates);
-  a.hlast32 = ptr<float>(hlast32);
-  a.cnt = reinterpret_cast<unsigned*>(cnt.data_ptr());
-  a.err = reinterpret_cast<unsigned*>(err.data_ptr());
-  a.B = B; a.H = H; a.T = T;
-  a.forget_bias = (float)forget_bias;
-  a.spin_limit = (unsigned)spin_limit;
-  a.cnt_zeroed = cnt_zeroed ? 1 : 0;
-  a.hring = ptr<bf16>(hring);
-  if (has(clast32)) {
-    check_seq(*clast32, at::kFloat, "clast32");
-    TORCH_CHECK(clast32->numel() == (int64_t)B * H, "clast32 must be [B, H]");
-    a.clast32 = ptr<float>(*clast32);
-  }
-  if (has(diag)) {
-    TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)T * 8, "diag must hold [T, 8] int64");
-    a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());
-  }
-  const int rc = dcr::launch_lstm_big_fwd(a, num_cus(), cur_stream());
-  TORCH_CHECK(rc == 0, "large-H persistent LSTM forward not launched (", rc, ")");
 }
 
 // two-layer wavefront LSTM forward (lstm2_persist.hip)
@@ -1146,23 +1033,12 @@ TORCH_LIBRARY(dcr, m) {
       "float clip, float gscale=1.0, int n_norm=-1, Tensor? extra_sq=None, "
       "Tensor? skip_if=None) -> ()");
   m.def("sumsq(Tensor x, Tensor(a!) partials, Tensor(b!) out) -> ()");
-  m.def("step_gemm(Tensor X, Tensor W, Tensor(a!) part) -> ()");
-  m.def("step_gemm_splits(int B, int N, int K) -> int",
-        [](int64_t B, int64_t N, int64_t K) -> int64_t {
-          return dcr::step_gemm_supported((int)B, (int)N, (int)K)
-                     ? dcr::step_gemm_splits((int)B, (int)N, (int)K) : 0;
-        });
   m.def(
       "lstm_step_ew_fwd(Tensor zrec, Tensor zx, Tensor? ids, Tensor cprev, Tensor(a!) hout, "
       "Tensor(b!)? hout32, Tensor(c!) cout, Tensor(d!) gates, float forget_bias) -> ()");
   m.def(
       "lstm_step_ew_bwd(Tensor dtop, Tensor? dhrec, Tensor gates, Tensor c, Tensor cprev, "
       "Tensor(a!) dc, Tensor(b!) dz_out) -> ()");
-  m.def("tok_norm(Tensor dz, Tensor w, Tensor(a!) partials, Tensor(b!) out) -> ()");
-  m.def("tok_norm_supported(int N, int H, int K) -> bool",
-        [](int64_t N, int64_t H, int64_t K) -> bool {
-          return dcr::tok_norm_supported(N, (int)H, (int)K);
-        });
   m.def(
       "rnn_fwd_seq(int cell, Tensor WT, Tensor? WT2, Tensor zx, Tensor? ids, Tensor(a!) hbuf, "
       "Tensor(b!)? h32, Tensor(c!)? cbuf, Tensor(d!)? gates, Tensor(e!)? pre, Tensor(f!)? aux, "
@@ -1199,15 +1075,14 @@ TORCH_LIBRARY(dcr, m) {
   m.def(
       "lstm_persist_fwd(Tensor WT, Tensor zx, Tensor? ids, Tensor(a!) hbuf, Tensor(b!) cbuf, "
       "Tensor(c!)? gates, Tensor(d!) hlast32, Tensor(e!) cnt, Tensor(f!) err, float forget_bias, "
-      "int spin_limit, Tensor(g!)? ring, Tensor(h!)? diag=None, Tensor? WxT=None, Tensor? xin=None, "
-      "Tensor? bias=None, bool cnt_zeroed=False, Tensor(i!)? hring=None, "
-      "Tensor(j!)? clast32=None) -> ()");
+      "int spin_limit, Tensor(g!) hring, Tensor(h!)? diag=None, Tensor? WxT=None, "
+      "Tensor? xin=None, Tensor? bias=None, bool cnt_zeroed=False, "
+      "Tensor(i!)? clast32=None) -> ()");
   m.def(
       "lstm_persist_bwd(Tensor W, Tensor dtop, Tensor(a!) dz, Tensor gates, Tensor cbuf, "
-      "Tensor(b!) cnt, Tensor(c!) err, int spin_limit, Tensor(d!)? db_part, Tensor? ids, "
-      "Tensor(e!)? dew_part, int V, Tensor(f!)? diag=None, Tensor? Wx_above=None, "
-      "Tensor? dz_above=None, bool exclusive=False, bool cnt_zeroed=False, "
-      "Tensor(g!)? zring=None) -> ()");
+      "Tensor(b!) cnt, Tensor(c!) err, int spin_limit, Tensor(d!) zring, Tensor(e!)? db_part=None, "
+      "Tensor? ids=None, Tensor(f!)? dew_part=None, int V=0, Tensor(g!)? diag=None, "
+      "bool exclusive=False, bool cnt_zeroed=False) -> ()");
   m.def("head_supported(int V, int H) -> int", [](int64_t V, int64_t H) -> int64_t {
     return dcr::head_supported((int)V, (int)H);
   });
@@ -1252,14 +1127,6 @@ TORCH_LIBRARY(dcr, m) {
       "sample_step(Tensor O, Tensor WsT, Tensor bs, Tensor(a!) cur, Tensor(b!) out, "
       "Tensor(c!) pos, Tensor(d!) ctr, Tensor? u, Tensor(e!)? logits, int mode, int space_id, "
       "int seed) -> ()");
-  m.def("lstm_big_supported(int H, int B) -> int", [](int64_t H, int64_t B) -> int64_t {
-    return dcr::lstm_big_supported((int)H, (int)B, num_cus());
-  });
-  m.def(
-      "lstm_big_fwd(Tensor WT, Tensor zx, Tensor? ids, Tensor(a!) hbuf, Tensor(b!) cbuf, "
-      "Tensor(c!)? gates, Tensor(d!) hlast32, Tensor(e!) cnt, Tensor(f!) err, float forget_bias, "
-      "int spin_limit, Tensor(g!) hring, bool cnt_zeroed=False, Tensor(h!)? clast32=None, "
-      "Tensor(i!)? diag=None) -> ()");
   m.def("gru_persist_ub(int H, int B) -> int", [](int64_t H, int64_t B) -> int64_t {
     return dcr::gru_persist_ub((int)H, (int)B, num_cus());
   });
@@ -1282,10 +1149,8 @@ TORCH_LIBRARY(dcr, m) {
 TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("global_norm", &global_norm);
   m.impl("sumsq", &sumsq);
-  m.impl("step_gemm", &step_gemm);
   m.impl("lstm_step_ew_fwd", &lstm_step_ew_fwd);
   m.impl("lstm_step_ew_bwd", &lstm_step_ew_bwd);
-  m.impl("tok_norm", &tok_norm);
   m.impl("adam_clip", &adam_clip);
   m.impl("rnn_fwd_seq", &rnn_fwd_seq);
   m.impl("rnn_bwd_seq", &rnn_bwd_seq);
@@ -1302,7 +1167,6 @@ TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("dropout_bits", &dropout_bits);
   m.impl("mask_apply", &mask_apply);
   m.impl("embed_dropout", &embed_dropout);
-  m.impl("lstm_big_fwd", &lstm_big_fwd);
   m.impl("sample_step", &sample_step);
   m.impl("gru_persist_bwd", &gru_persist_bwd);
 }

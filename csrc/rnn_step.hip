@@ -24,6 +24,7 @@
 // LSTM kernels in lstm_persist.hip replace these for the flagship config.
 #include "common.h"
 #include "kernels.h"
+#include "debug_env.h"
 #include <stdlib.h>
 
 namespace dcr {
@@ -420,11 +421,11 @@ __global__ void __launch_bounds__(256) bwd_step_kernel(BwdStepArgs a) {
 // batch rows.  Larger NBT cuts weight traffic (which dominates at large H) but shrinks the grid.
 // Measured on 1x MI355X (4-layer LSTM-2048, T=512, B=64): NBT 1/2/4 -> 129/108/141 ms per
 // training step; the 3-layer GRU-1024 per-step path lost 20 % at NBT=4 (128 workgroups).  So
-// NBT=2 when that still leaves >= 256 workgroups (one per CU), else 1; DCR_STEP_NBT=1/2/4
+// NBT=2 when that still leaves >= 256 workgroups (one per CU), else 1; DCR_DEBUG=step_nbt=1/2/4
 // overrides.
 static int step_nbt(int G, int B, int H) {
-  const char* e = getenv("DCR_STEP_NBT");
-  const int forced = (e && (e[0] == '1' || e[0] == '2' || e[0] == '4')) ? e[0] - '0' : 0;
+  const int f = debug_int("step_nbt", 0);
+  const int forced = (f == 1 || f == 2 || f == 4) ? f : 0;
   const int nbt_tiles = (B + 15) / 16;
   for (int c : {4, 2}) {
     if (G * c > 16 || nbt_tiles < c) continue;

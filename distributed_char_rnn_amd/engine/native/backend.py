@@ -1,0 +1,96 @@
+"""``NativeBackend``: one stateful-TBPTT training step on the gfx950 kernels of csrc/.
+
+Replaces the reference's TF graph execution of one ``Session.run([summaries, cost,
+final_state, train_op])`` (train.py:199) -- T x L unrolled cell chains forward, tf.gradients
+backward -- with an explicit, hand-scheduled forward/backward:
+
+forward, per layer l (time-major rows n = t*B + b):
+  * layer 0 without dropout: Zx_0 = (E·W_x0 + b0)[ids] is gathered from a [V, G·H] table
+    inside the recurrent kernel (V = 65 rows instead of B·T rows); otherwise Zx = X_l·W_x + b
+    is one library GEMM over all T steps, or fused into the recurrent kernel;
+  * the recurrence: two-layer wavefront kernels (lstm2_persist.hip) for LSTM layer pairs,
+    weights-resident single-layer kernels (lstm_persist.hip, gru_persist.hip), or the fused
+    per-step kernels (rnn_step.hip) -- chosen per step shape by ``plan.make_plan``;
+head: fused logits + softmax-CE + dlogits + d softmax_b + dtop (head.hip);
+backward, top layer first: BPTT kernels (dZ per step, bias partials fused), weight gradients
+as split-K library GEMMs, gradient ranges reported ready for the bucketed all-reduce.
+
+All weights are refreshed from the fp32 master buffer into bf16 kernel layouts once per
+optimizer step (layouts.py).  Modules: plan (knobs, kernel choice), layouts, buffers, forward,
+backward, libstep (large-H library path), inference (logits, eval, sampling).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from ...models.params import ParamStore
+from ...ops import native
+from .backward import BackwardMixin
+from .buffers import BuffersMixin
+from .forward import ForwardMixin
+from .inference import InferenceMixin
+from .layouts import LayerWeights, LayoutsMixin
+from .libstep import LibStepMixin
+from .plan import Knobs
+
+CELL_ID = {"lstm": 0, "gru": 1, "rnn": 3, "nas": 4}
+
+
+class NativeBackend(LayoutsMixin, BuffersMixin, ForwardMixin, BackwardMixin, LibStepMixin,
+                    InferenceMixin):
+    def __init__(self, store: ParamStore, dtype: str = "auto", seed: int = 0,
+                 knobs: Optional[Knobs] = None):
+        if dtype not in ("auto", "bf16"):
+            raise ValueError("the native GPU path computes in bf16 (use --dtype bf16/auto)")
+        self.ops = native.ops()
+        self.store = store
+        self.cfg = store.cfg
+        self.dev = store.device
+        self.cell = CELL_ID[self.cfg.model]
+        self.H = self.cfg.rnn_size
+        self.V = self.cfg.vocab_size
+        self.L = self.cfg.num_layers
+        if self.H % 32 != 0:
+            raise ValueError("the GPU path needs rnn_size % 32 == 0")
+        self.GW = {"lstm": 4, "gru": 3, "rnn": 1, "nas": 8}[self.cfg.model] * self.H
+        self.knobs = knobs if knobs is not None else Knobs.from_env()
+        self.spin_limit = self.knobs.spin_limit
+        self.side_overlap = self.knobs.on("side")
+        self.dew_mode = self.knobs.dbg("dew", "gemm")
+        if self.dew_mode not in ("gemm", "segsum", "fused"):
+            raise ValueError(f"DCR_DEBUG dew={self.dew_mode!r}: gemm | segsum | fused")
+        # fused softmax head (csrc/head.hip): logits + CE + dlogits + d softmax_b + dtop
+        self.fused_head = self.knobs.on("fused_head") and bool(self.ops.head_supported(self.V,
+                                                                                          self.H))
+        # TF clip-norm semantics for the embedding gradient (models/params.py: clip_norm)
+        self.tf_norm = self.cfg.clip_norm == "tf"
+        self._wver = None
+        self._w: List[LayerWeights] = []
+        self._table_dirty = False
+        self._head = None
+        self._bufs: Dict[Tuple[int, int, bool], dict] = {}
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self._err_host: Optional[torch.Tensor] = None
+        self._side = None
+        self._side_used = False
+        self._steps = 0
+        self._npart: Optional[torch.Tensor] = None
+        self._drop_seed = int(seed) * 0x9E3779B1 + 0x5EED
+        self._drop_step = 0
+        self._dm_bufs: Dict[Tuple[int, int], dict] = {}
+        self.last_dropout_masks: Optional[dict] = None
+
+    def check_errors(self):
+        """Raise if a persistent kernel hit its spin timeout (forces a device sync).  The word
+        is cleared so the caller may recover (e.g. restore a checkpoint and continue)."""
+        v = int(self.err.item())
+        if v:
+            self.err.zero_()
+            if self._err_host is not None:
+                self._err_host.zero_()
+            raise RuntimeError(f"persistent recurrent kernel timed out (code {v}); the "
+                               "optimizer skipped the step's update.  Another process sharing "
+                               "this GPU can cause this (one rank per GPU); "
+                               "DCR_RECURRENCE=step selects the per-step kernels")

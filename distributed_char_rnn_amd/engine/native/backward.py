@@ -1,0 +1,316 @@
+"""Training step of the native backend: forward, fused softmax-CE, BPTT and the weight
+gradients (the reference's tf.gradients + clip_by_global_norm inputs, model.py:88-98), with
+gradient ranges reported ready (``on_ready``) for the bucketed all-reduce as they become final."""
+from __future__ import annotations
+
+import torch
+
+from ...models.params import cell_specs
+from .gemm import f32, mm_into, mm_tn, put
+from .layouts import SEG_LDS_MAX_V
+
+
+class BackwardMixin:
+    def train_step(self, x, y, state, on_ready=None, want_extras: bool = False):
+        ids_tm = x.t().contiguous()
+        tgt = y.t().contiguous().view(-1)
+        T, B = ids_tm.shape
+        H, V, N, GW = self.H, self.V, T * B, self.GW
+        wide = self._wide_xent(T * B)
+        bufs, O, logits, new_state = self._forward(ids_tm, state, True,
+                                                   want_logits=not self.fused_head,
+                                                   logits_bias=not wide)
+        P = bufs["plan"]
+        dlog = bufs["dlogits"]
+        s, hd = self.store, self._head
+        if self.fused_head:
+            # one launch: logits (only if asked for) -> CE -> bf16 dlogits, d softmax_b, dtop
+            self.ops.head(O, hd["WsT"], hd["Wsk"], hd["bs"], tgt, 1.0 / N,
+                          logits if want_extras else None, bufs["row_loss"], dlog,
+                          bufs["dtop"].view(N, H), s.gview("rnnlm/softmax_b"),
+                          bufs["head_part"], bufs["loss"])
+            mm_tn(O, dlog, s.gview("rnnlm/softmax_w"))
+            dtop = bufs["dtop"].view(T, B, H)
+        elif wide:
+            # wide vocabulary: one-read CE (bias added in-kernel), d softmax_b fused (xent_wide)
+            self.ops.xent_wide(logits, hd["bs"], tgt, 1.0 / N, bufs["row_loss"], dlog,
+                               bufs["colpart"], s.gview("rnnlm/softmax_b"), bufs["xpart"],
+                               bufs["loss"])
+            if want_extras:
+                logits += hd["bs"]
+            mm_tn(O, dlog, s.gview("rnnlm/softmax_w"))
+            dtop = mm_into(dlog, hd["Ws"].t(), bufs["dtop"].view(N, H)).view(T, B, H)
+        else:
+            self.ops.xent(logits, tgt, 1.0 / N, bufs["row_loss"], dlog, bufs["xpart"],
+                          bufs["loss"])
+            # ---- head gradients
+            mm_tn(O, dlog, s.gview("rnnlm/softmax_w"))
+            self.ops.segsum(dlog, None, 1, bufs["colsum"][:, :V], bufs["ws"], False)
+            s.gview("rnnlm/softmax_b").copy_(bufs["colsum"][0, :V])
+            dtop = mm_into(dlog, hd["Ws"].t(), bufs["dtop"].view(N, H)).view(T, B, H)
+        overlap = P.mode == "overlap" or not P.persistent
+        pending = []
+        user_ready = None
+        if on_ready is not None and not overlap:
+            # exclusive mode: nothing may run beside the persistent BPTT grids, so the gradient
+            # buckets are released (in the same order) only after the last BPTT launch; from
+            # then on readiness is forwarded directly (the remaining weight GEMMs overlap RCCL)
+            user_ready = on_ready
+            on_ready = pending.append
+
+        def _release():
+            for off in pending:
+                user_ready(off)
+            pending.clear()
+            return user_ready
+        if on_ready is not None:
+            sb = s.by_name["rnnlm/softmax_b"]
+            on_ready(sb.offset + sb.numel)
+        drop = self._dropout(True)
+        dm = self.last_dropout_masks if drop else None
+        paired_done = -1  # lower layer whose BPTT already ran inside a two-layer wavefront
+        # TF clip-norm term from dx_tok = dZ0·W_x0ᵀ: needed as an extra GEMM only on the layer-0
+        # gather route (every other route materialises dx_tok anyway)
+        gather0 = not drop and self.cfg.model != "nas"
+        fused_dew0 = P.persist and gather0 and V <= 128 and self.dew_mode == "fused"
+        tok_gemm = self.tf_norm and gather0 and not (V > SEG_LDS_MAX_V and not fused_dew0)
+        for layer in reversed(range(self.L)):
+            lw, lb = self._w[layer], bufs["layers"][layer]
+            names = [sp.name for sp in cell_specs(self.cfg, layer)]
+            pair_hi = P.pair_bwd and layer % 2 == 1 and dtop is not None
+            # the top layer's output dropout
+            omask = dm["out"] if (dm is not None and layer == self.L - 1) else None
+            if dtop is not None:
+                dtop = dtop.contiguous()
+                if omask is not None:
+                    dtop = self._masked(dtop, omask, dm["sout"], out=dtop).view(T, B, H)
+            zx_nas = lb.zx if self.cfg.model == "nas" else None
+            written = False  # this layer's kernel/bias gradients already in the flat buffer
+            gather = (layer == 0 and not drop and self.cfg.model != "nas")
+            fused_dew = P.persist and gather and V <= 128 and self.dew_mode == "fused"
+            if pair_hi:
+                # layers (layer-1, layer) as one reverse wavefront (lstm2_persist.hip): T+1
+                # ticks, the lower layer's dtop = dZ·W_xᵀ of this layer computed in-kernel
+                lo = layer - 1
+                lw0, lb0 = self._w[lo], bufs["layers"][lo]
+                nr = P.pair_rows
+                self.ops.lstm2_persist_bwd(lw0.Wh, lw.Wh, lw.Wx, dtop, lb0.gates, lb0.cbuf,
+                                           lb.gates, lb.cbuf, lb0.dz, lb.dz, bufs["zring"],
+                                           bufs["zring2"], bufs["db_part"][lo][:nr],
+                                           bufs["db_part"][layer][:nr], bufs["cnt"][self.L + lo],
+                                           bufs["cnt"][self.L + layer], self.err,
+                                           self.spin_limit, P.pair_g, None,
+                                           dm["inb"][layer] if dm else None,
+                                           dm["sin"] if dm else 1.0)
+                paired_done = lo
+                if lo == 0 and user_ready is not None:
+                    on_ready = _release()
+            elif layer == paired_done:
+                pass
+            elif P.persist:
+                self.ops.lstm_persist_bwd(lw.Wh, dtop, lb.dz, lb.gates, lb.cbuf,
+                                          bufs["cnt"][self.L + layer], self.err, self.spin_limit,
+                                          bufs["zring"], bufs["db_part"][layer][: max(B // 16, 1)],
+                                          ids_tm if fused_dew else None,
+                                          bufs["dew_part"] if fused_dew else None, V,
+                                          exclusive=P.bwd_excl, cnt_zeroed=True)
+                if layer == 0 and user_ready is not None:
+                    # the last persistent grid is queued: buckets may now run beside the
+                    # (non-persistent) layer-0 weight GEMMs
+                    on_ready = _release()
+            elif P.gru_persist:
+                gr = bufs["grings"]
+                self.ops.gru_persist_bwd(lw.W2, lw.Wh, dtop, lb.dz, lb.gates, lb.h32,
+                                         bufs["cnt"][self.L + layer], self.err, self.spin_limit,
+                                         cnt_zeroed=True, ring0=gr[0], ring1=gr[2])
+                if layer == 0 and user_ready is not None:
+                    on_ready = _release()
+            elif self._lib_step("bwd", B):
+                self._lstm_bwd_lib(lw, lb, dtop, bufs)
+            else:
+                self.ops.rnn_bwd_seq(self.cell, lw.Wh, lw.W2, dtop, lb.dz, lb.dzx, lb.gates,
+                                     lb.pre, lb.aux, zx_nas, lb.cbuf, lb.h32, lb.hbuf, bufs["dc"],
+                                     bufs["gpart"])
+            dZ = lb.dz.view(N, GW)
+            dZx = lb.dzx.view(N, GW) if lb.dzx is not None else dZ
+            Hprev = lb.hbuf[:T].reshape(N, H)
+            if (P.persist and layer > 0 and not drop and self.side_overlap and overlap
+                    and not pair_hi):
+                # Off the critical path: this layer's weight gradients (two [H x N]·[N x 4H]
+                # GEMMs) run on a side stream concurrently with the latency-bound BPTT of the
+                # layer below; the layer's all-reduce bucket is launched from that stream, so
+                # RCCL orders itself after the GEMMs.  Only dX stays on the critical path.
+                dbias = self._bias_sum(self._db_part(bufs, layer), names)
+                ev = torch.cuda.Event()
+                ev.record()
+                side = self._side_stream()
+                with torch.cuda.stream(side):
+                    side.wait_event(ev)
+                    mm_tn(Hprev, dZ, s.gview(names[0])[H:], split=False)
+                    mm_tn(lb.x_in, dZx, s.gview(names[0])[:H], split=False)
+                    s.gview(names[1]).copy_(dbias)
+                    dbias.record_stream(side)
+                    if on_ready is not None:
+                        on_ready(s.layer_range(layer)[1])
+                dtop = mm_into(dZx, lw.Wx.t(), bufs["dx"].view(N, H)).view(T, B, H)
+                self._side_used = True
+                continue
+            # recurrent-weight gradients
+            if self.cfg.model == "gru":
+                gk, gb, ck, cb = names
+                mm_tn(Hprev, dZ[:, : 2 * H], s.gview(gk)[H:])
+                mm_tn(lb.rh.view(N, H), dZ[:, 2 * H:], s.gview(ck)[H:])
+            elif self.cfg.model == "nas":
+                mm_tn(Hprev, dZ, s.gview(names[1]))
+            else:
+                mm_tn(Hprev, dZ, s.gview(names[0])[H:])
+            if gather and V > SEG_LDS_MAX_V and not fused_dew:
+                # wide vocabulary: the [V, GW] dEW segment sum would be an atomic scatter of
+                # N x GW values plus two fp32 [V, GW] GEMMs; the dense route scatters N x H
+                # instead: dW_x0 = E[ids]ᵀ·dZ0 (split-K), dE = segsum(dZ0·W_x0ᵀ)
+                Eb = hd.get("Ebf")                                  # refreshed with the table
+                X0 = (Eb[ids_tm.view(-1).long()] if Eb is not None
+                      else hd["E"][ids_tm.view(-1).long()].to(torch.bfloat16))    # [N, H]
+                dWx = mm_tn(X0, dZx)
+                if layer in bufs["pers_layers"]:
+                    dbias = self._bias_sum(self._db_part(bufs, layer), names)
+                else:
+                    self.ops.segsum(dZx, None, 1, bufs["colsum"][:, :GW], bufs["ws"], False)
+                    dbias = bufs["colsum"][0, :GW]
+                dXf = mm_into(dZx, lw.Wx.t(), bufs["dx"].view(N, H))
+                self._embed_grad(dXf, ids_tm, bufs)
+                self._token_norm(dXf)
+            elif gather:
+                dEW = self._dew(dZx, ids_tm, bufs, fused_dew)    # [V, GW] fp32
+                dWx = hd["E"].t() @ dEW                           # [H, GW] fp32
+                dbias = dEW.sum(0)
+                # layer 0's own gradients are final here: report them before the embedding
+                # gradient and the token-norm GEMM, so that under data parallelism the
+                # layer-0 bucket's all-reduce overlaps that work and the last bucket is only
+                # the embedding + norm slot
+                self._write_input_grads(layer, names, dWx, dbias)
+                written = True
+                if on_ready is not None:
+                    self._join_side()
+                    on_ready(s.layer_range(0)[1])
+                torch.mm(dEW, lw.Wx32.t(), out=s.gview("embedding"))
+                if tok_gemm:
+                    # sum_tok ||dZ0_tok·W_x0ᵀ||² into the norm slot: library GEMM to bf16 rows
+                    # + the sumsq kernel (66 us at the headline shape)
+                    self._token_norm(torch.mm(dZx, lw.Wx.t()))
+            else:
+                dWx = (mm_tn(lb.x_in, dZx, s.gview(names[0])[:H])
+                       if self.cfg.model in ("lstm", "rnn") else mm_tn(lb.x_in, dZx))
+                if layer in bufs["pers_layers"]:
+                    dbias = self._bias_sum(self._db_part(bufs, layer), names)  # fused in BPTT
+                else:
+                    self.ops.segsum(dZx, None, 1, bufs["colsum"][:, :GW], bufs["ws"], False)
+                    dbias = bufs["colsum"][0, :GW]
+                if pair_hi:  # the lower layer's dtop was fused into the wavefront BPTT
+                    self._write_input_grads(layer, names, dWx, dbias)
+                    if on_ready is not None:
+                        on_ready(s.layer_range(layer)[1])
+                    dtop = None
+                    continue
+                if layer > 0:
+                    dX = mm_into(dZx, lw.Wx.t(), bufs["dx"].view(N, H)).view(T, B, H)
+                else:  # only the embedding gradient reads it: bf16 rows for the segment sum
+                    dX = torch.mm(dZx, lw.Wx.t(), out=bufs["dx_bf"]).view(T, B, H)
+                if dm is not None and dm["inb"][layer] is not None:  # this layer's input mask
+                    dX = self._masked(dX, dm["inb"][layer], dm["sin"], out=dX).view(T, B, H)
+                if layer > 0:
+                    dtop = dX
+                else:
+                    # (bf16 as the GEMM wrote it: the segment sum and the norm accumulate in
+                    # fp32 either way)
+                    dXt = dX.reshape(N, H)
+                    self._embed_grad(dXt, ids_tm, bufs)
+                    self._token_norm(dXt)
+            if not written:
+                self._write_input_grads(layer, names, dWx, dbias)
+            if layer == 0:
+                # side-stream work (overlapped weight GEMMs of the layers above) may share the
+                # remaining buckets: join before reporting them ready
+                self._join_side()
+            if on_ready is not None:
+                on_ready(None if layer == 0 else s.layer_range(layer)[1])
+        self._join_side()
+        if pending:
+            _release()
+        extras = {"logits": logits, "loss": bufs["row_loss"]} if want_extras else None
+        self._steps += 1
+        if P.persistent:
+            self._poll_errors()
+        return bufs["loss"][0], new_state, extras
+
+    def _dew(self, dZ0: torch.Tensor, ids_tm: torch.Tensor, bufs, fused: bool) -> torch.Tensor:
+        """Layer-0 embedding-table gradient dEW = onehot(ids)ᵀ·dZ0 [V, GW] (gather route: the
+        forward read Zx0 = (E·W_x0 + b0)[ids]).  ``gemm`` (default): split-K MFMA library GEMM
+        against an exact 0/1 one-hot matrix -- the same fp32 sums of the bf16 dZ values as a
+        scatter; ``segsum``: the one-hot MFMA segment-sum kernel (csrc/embed.hip); ``fused``:
+        LDS partials accumulated inside the single-layer persistent BPTT."""
+        V = self.V
+        if fused:
+            return bufs["dew_part"].sum(0)
+        if self.dew_mode == "gemm" and bufs["onehot"] is not None:
+            oh = bufs["onehot"]
+            oh.zero_()
+            oh.scatter_(1, ids_tm.view(-1, 1).long(), 1.0)
+            return mm_tn(oh, dZ0)[:V]                 # rows >= V are zero padding
+        dEW = torch.empty(V, self.GW, dtype=f32, device=self.dev)
+        self.ops.segsum(dZ0, ids_tm.view(-1), V, dEW, bufs["ws"], False)
+        return dEW
+
+    def _poll_errors(self) -> None:
+        """Non-blocking check of the persistent kernels' error word: each step copies it into
+        pinned host memory behind its own work and reads the copy of an earlier step, so a
+        spin timeout raises within a step or two without a device sync.  (The optimizer skips
+        its update on device while the word is set: TFAdam(guard=err).)"""
+        if self._err_host is None:
+            self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        v = int(self._err_host[0])
+        if v:
+            self.check_errors()
+        self._err_host.copy_(self.err, non_blocking=True)
+
+    def _embed_grad(self, dX: torch.Tensor, ids_tm: torch.Tensor, bufs) -> None:
+        """dE = segsum(dX_tok, ids) into the gradient buffer.  Wide vocabularies take the
+        fp32-atomic route; there the ids are sorted first (a frequent id is then one register
+        run per 32-row chunk instead of one atomic per occurrence)."""
+        ids = ids_tm.view(-1)
+        out = self.store.gview("embedding")
+        if self.V > SEG_LDS_MAX_V and self.knobs.on("seg_sort"):
+            sid, perm = torch.sort(ids)
+            self.ops.segsum(dX, sid, self.V, out, bufs["ws"], False, perm.int())
+        else:
+            self.ops.segsum(dX, ids, self.V, out, bufs["ws"], False)
+
+    def _token_norm(self, dx_tok: torch.Tensor) -> None:
+        """TF clip-norm term of the embedding (ModelConfig.clip_norm == "tf"): the sum of
+        squares of the per-token input gradients (the IndexedSlices values), written into the
+        gradient buffer's norm slot (all-reduced with the last bucket, read by adam_clip)."""
+        if not self.tf_norm:
+            return
+        n = dx_tok.numel()
+        if self._npart is None or self._npart.numel() < self.ops.opt_num_partials(n):
+            self._npart = torch.empty(self.ops.opt_num_partials(n), dtype=f32, device=self.dev)
+        self.ops.sumsq(dx_tok.contiguous(), self._npart, self.store.norm_slot_view())
+
+    def _join_side(self) -> None:
+        if self._side_used:
+            torch.cuda.current_stream().wait_stream(self._side)
+            self._side_used = False
+
+    def _write_input_grads(self, layer: int, names, dWx: torch.Tensor, dbias: torch.Tensor):
+        s, H = self.store, self.H
+        if self.cfg.model == "gru":
+            gk, gb, ck, cb = names
+            s.gview(gk)[:H].copy_(dWx[:, : 2 * H])
+            s.gview(ck)[:H].copy_(dWx[:, 2 * H:])
+            s.gview(gb).copy_(dbias[: 2 * H])
+            s.gview(cb).copy_(dbias[2 * H:])
+        elif self.cfg.model == "nas":
+            s.gview(names[0]).copy_(dWx)
+        else:
+            put(s.gview(names[0])[:H], dWx)
+            put(s.gview(names[1]), dbias)

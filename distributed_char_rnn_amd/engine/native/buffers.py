@@ -1,0 +1,140 @@
+"""Per-(B, T, training) activation and workspace buffers of the native backend, allocated once
+per step shape (HBM is plentiful: 288 GB per MI355X) and reused every step."""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from .gemm import bf16, f32
+from .layouts import SEG_LDS_MAX_V
+from .plan import ExecutionPlan, make_plan
+
+
+@dataclass
+class LayerBufs:
+    hbuf: torch.Tensor
+    cbuf: Optional[torch.Tensor]
+    h32: Optional[torch.Tensor]
+    gates: Optional[torch.Tensor]
+    pre: Optional[torch.Tensor]
+    aux: Optional[torch.Tensor]
+    rh: Optional[torch.Tensor]
+    hlast32: torch.Tensor
+    zx: Optional[torch.Tensor]
+    dz: Optional[torch.Tensor]
+    dzx: Optional[torch.Tensor]
+    x_in: Optional[torch.Tensor] = None      # bf16 [N, D] layer input (dense mode)
+    clast32: Optional[torch.Tensor] = None   # fp32 [B, H] final c (persistent LSTM)
+    x_drop: Optional[torch.Tensor] = None    # bf16 [N, D] masked layer input (dropout)
+
+
+class BuffersMixin:
+    def _persist_plan(self, B: int, training: bool, T: int = 1 << 30) -> ExecutionPlan:
+        return make_plan(self.ops, self.cfg, self.knobs, B, training, T, self.side_overlap)
+
+    def _buffers(self, B: int, T: int, training: bool) -> dict:
+        key = (B, T, training)
+        if key in self._bufs:
+            return self._bufs[key]
+        H, GW, dev, m = self.H, self.GW, self.dev, self.cfg.model
+        N = B * T
+        plan = self._persist_plan(B, training, T)
+        Bp = max(B, 32 * plan.pair_nbg)  # hand-off rings of the pair kernels: padded batch
+        nrow = max(B // 16, plan.pair_rows, 1)
+        drop = self._dropout(training)
+        layers = []
+        for layer in range(self.L):
+            dense = layer > 0 or drop
+            lb = LayerBufs(
+                hbuf=torch.empty(T + 1, B, H, dtype=bf16, device=dev),
+                cbuf=torch.empty(T + 1, B, H, dtype=f32, device=dev) if m in ("lstm", "nas") else None,
+                h32=torch.empty(T + 1, B, H, dtype=f32, device=dev) if m == "gru" else None,
+                gates=(torch.empty(T, B, GW, dtype=bf16, device=dev)
+                       if m == "gru" or (m == "lstm" and training) else None),
+                pre=torch.empty(T, B, GW, dtype=f32, device=dev) if m == "nas" else None,
+                aux=torch.empty(T, B, H, dtype=f32, device=dev) if m == "nas" else None,
+                rh=torch.empty(T, B, H, dtype=bf16, device=dev) if m == "gru" else None,
+                hlast32=torch.empty(B, H, dtype=f32, device=dev),
+                zx=torch.empty(T, B, GW, dtype=f32, device=dev) if (dense or m == "nas") else None,
+                dz=torch.empty(T, B, GW, dtype=bf16, device=dev) if training else None,
+                dzx=torch.empty(T, B, GW, dtype=bf16, device=dev) if (training and m == "nas") else None,
+            )
+            if training and drop:
+                lb.x_drop = torch.empty(N, H, dtype=bf16, device=dev)
+            layers.append(lb)
+        ws = max(self.ops.segsum_workspace(N, GW, self.V), self.ops.segsum_workspace(N, H, self.V),
+                 self.ops.segsum_workspace(N, GW, 1), self.ops.segsum_workspace(N, self.V, 1), 1)
+        e = lambda *shape, dt=f32: torch.empty(*shape, dtype=dt, device=dev)  # noqa: E731
+        bufs = dict(
+            plan=plan,
+            layers=layers,
+            logits=e(N, self.V),
+            dlogits=e(N, self.V, dt=bf16) if training else None,
+            row_loss=e(N),
+            xpart=e(self.ops.xent_num_partials(N)),
+            loss=e(1),
+            dc=e(B, H),
+            gpart=e(B, H) if m == "gru" else None,
+            ws=e(ws),
+            colsum=e(1, max(GW, self.V)),
+            head_part=e(self.ops.head_workspace(N, self.V)) if self.fused_head else None,
+            onehot=(e(N, 8 * ((self.V + 7) // 8), dt=bf16)
+                    if (training and self.V <= SEG_LDS_MAX_V and self.dew_mode == "gemm")
+                    else None),
+            colpart=(e(self.ops.xent_wide_waves(N) * self.V)
+                     if (training and self._wide_xent(N)) else None),
+            dtop=e(T, B, H) if training else None,
+            dx=e(T, B, H) if training else None,
+            dx_bf=e(N, H, dt=bf16) if training else None,
+            db_part=e(self.L, nrow, GW) if training else None,
+            dew_part=(e(max(B // 16, 1), self.V, GW)
+                      if (training and self.V <= 128 and self.dew_mode == "fused") else None),
+            # one hand-off counter region per persistent launch (fwd layers, then bwd layers),
+            # zeroed together by the step's prep launch
+            cnt=torch.zeros(2 * self.L, max(2 * (B // 16 + 1), plan.pair_nbg) * (T + 1) * 4,
+                            dtype=torch.int32, device=dev),
+            # fragment-tiled hand-off rings of the persistent GRU: [h or dZc, r⊙h, dZg]
+            grings=((e(2 * B * H, dt=bf16), e(2 * B * H, dt=bf16), e(2 * B * 2 * H, dt=bf16))
+                    if m == "gru" else None),
+            # fragment-tiled h hand-off rings of the persistent forwards (persist_common.h)
+            hrings=(e(2 * Bp * H, dt=bf16), e(2 * Bp * H, dt=bf16)) if m == "lstm" else None,
+            # fragment-tiled dZ hand-off rings of the persistent BPTTs (one per layer of a pair)
+            zring=e(2 * Bp * GW, dt=bf16) if (training and m == "lstm") else None,
+            zring2=e(2 * Bp * GW, dt=bf16) if plan.pair_bwd else None,
+            o_drop=e(N, H, dt=bf16) if (training and drop) else None,
+        )
+        # layers run by the persistent LSTM kernels (their final state is written into fresh
+        # tensors, their bias gradients come from the kernels' db_part partials)
+        npair = 2 * (self.L // 2) if plan.pair else 0
+        bufs["pers_layers"] = set(range(npair)) | (set(range(npair, self.L)) if plan.persist
+                                                   else set())
+        self._bufs[key] = bufs
+        return bufs
+
+    def _wide_xent(self, N: int) -> bool:
+        """Library logits GEMM + one-read CE kernel (xent_wide) for vocabularies the fused head
+        does not cover (V > 256)."""
+        return (not self.fused_head and self.V >= 256 and self.knobs.on("wide_xent")
+                and bool(self.ops.xent_wide_supported(self.V)))
+
+    def _side_stream(self):
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.dev)
+        return self._side
+
+    @staticmethod
+    def _db_part(bufs, layer: int) -> torch.Tensor:
+        """The rows of the bias-gradient partials the layer's persistent BPTT kernel wrote."""
+        P = bufs["plan"]
+        if P.pair_bwd and layer < 2 * (len(bufs["layers"]) // 2):
+            return bufs["db_part"][layer][: P.pair_rows]
+        return bufs["db_part"][layer][: max(bufs["layers"][0].hbuf.shape[1] // 16, 1)]
+
+    def _bias_sum(self, part: torch.Tensor, names) -> torch.Tensor:
+        """Sum the per-batch-group bias partials; for cells with one [GW] bias the sum is
+        written straight into its gradient slice (the later copy_ is then a no-op)."""
+        if self.cfg.model in ("lstm", "rnn"):
+            return torch.sum(part, 0, out=self.store.gview(names[1]))
+        return part.sum(0)

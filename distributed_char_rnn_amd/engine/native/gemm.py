@@ -1,0 +1,76 @@
+"""Library GEMM helpers of the native backend (hipBLASLt through torch): bf16 MFMA operands,
+fp32 outputs written straight into gradient views, split-K for token reductions."""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+bf16 = torch.bfloat16
+f32 = torch.float32
+
+
+def mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """bf16 x bf16 -> fp32 GEMM on the MFMA library path."""
+    return torch.mm(a, b, out_dtype=f32)
+
+
+_OUT_OK = [None]
+
+
+def mm_into(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor,
+            bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """GEMM written straight into ``out`` (e.g. a gradient view of the flat buffer), avoiding
+    a temporary + copy; falls back to copy if this torch build lacks the out= overload."""
+    if _OUT_OK[0] is not False and out.is_contiguous():
+        try:
+            if bias is None:
+                torch.mm(a, b, out_dtype=f32, out=out)
+            else:
+                torch.addmm(bias, a, b, out_dtype=f32, out=out)
+            _OUT_OK[0] = True
+            return out
+        except (RuntimeError, TypeError):
+            _OUT_OK[0] = False
+    out.copy_(mm(a, b) if bias is None else torch.addmm(bias, a, b, out_dtype=f32))
+    return out
+
+
+def split_k(K: int, M: int, Nn: int) -> int:
+    """Split factor for a token-reduction GEMM with a small [M, Nn] output: the library tiles
+    such an output into a few dozen workgroups (the 512x2048, K=32768 weight gradient ran on 73
+    of 256 CUs at 335 TFLOP/s), so the reduction is split into S batched slices instead
+    (scripts/bench_gemms.py: 205 -> 97 us at S=8; the 512x65 head gradient 133 -> 27 us)."""
+    if K < 8192 or -(-M // 128) * -(-Nn // 256) >= 128:
+        return 1
+    S = 8 if M * Nn >= (1 << 18) else 16
+    while S > 1 and (K % S or K // S < 1024):
+        S //= 2
+    return S
+
+
+def mm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
+          split: bool = True) -> torch.Tensor:
+    """fp32 ``aᵀ·b`` for token-major bf16 operands ``a`` [K, M] and ``b`` [K, Nn] (weight
+    gradients: K = T·B tokens), split-K over batched MFMA GEMMs + one fp32 sum when the output
+    is too small to fill the chip.  ``split=False`` for GEMMs that run beside a persistent
+    kernel on a side stream: there a chip-filling grid only steals the recurrence's CUs
+    (measured: 256-workgroup split-K beside BPTT stretched both)."""
+    K, M = a.shape
+    Nn = b.shape[1]
+    S = split_k(K, M, Nn) if split else 1
+    if S == 1:
+        return mm(a.t(), b) if out is None else mm_into(a.t(), b, out)
+    part = torch.bmm(a.unflatten(0, (S, K // S)).transpose(1, 2), b.unflatten(0, (S, K // S)),
+                     out_dtype=f32)
+    if out is None:
+        return part.sum(0)
+    torch.sum(part, 0, out=out)
+    return out
+
+
+def put(dst: torch.Tensor, src: torch.Tensor):
+    """dst.copy_(src) unless src already is dst's memory (results written in place)."""
+    if not (src.data_ptr() == dst.data_ptr() and src.shape == dst.shape
+            and src.stride() == dst.stride()):
+        dst.copy_(src)

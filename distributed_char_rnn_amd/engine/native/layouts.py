@@ -1,0 +1,109 @@
+"""bf16 kernel layouts of the fp32 master weights, refreshed once per optimizer step by one
+batched prep launch (csrc/prep.hip): W_hᵀ for the forward's MFMA A operand, W_h in TF layout
+for the backward's, W_xᵀ for the fused input projections, the padded softmax head, and the
+layer-0 ``E·W_x0 + b0`` table that replaces the layer-0 input GEMM (model.py:55-58, 66-72)."""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from ...models.params import cell_specs
+from .gemm import bf16, f32
+
+SEG_LDS_MAX_V = 96  # csrc/embed.hip kSegLdsMaxV: larger vocabularies take the atomic scatter
+
+
+@dataclass
+class LayerWeights:
+    Wx: torch.Tensor            # [D, GW] bf16 input projection
+    Wx32: Optional[torch.Tensor]  # [D, GW] fp32 (layer-0 table / dE)
+    bias: torch.Tensor          # [GW] fp32 (zeros for NAS)
+    Wh: torch.Tensor            # [H, GWr] bf16 TF layout (backward A operand); GRU: Wc_h
+    WhT: torch.Tensor           # [GWr, H] bf16 (forward A operand); GRU: Wg_hᵀ
+    W2: Optional[torch.Tensor] = None   # GRU: Wg_h [H, 2H]
+    WxT: Optional[torch.Tensor] = None  # LSTM: W_xᵀ [4H, D] (fused-input persistent forward)
+    WT2: Optional[torch.Tensor] = None  # GRU: Wc_hᵀ [H, H]
+
+
+class LayoutsMixin:
+    def params_changed(self):
+        self._wver = None
+
+    def _alloc_weights(self):
+        """bf16 (and padded / concatenated fp32) layouts of the master weights, allocated once
+        and refreshed by ``_prep`` through the batched prep kernel."""
+        s, H, D, dev = self.store, self.H, self.H, self.dev
+        self._w, self._wtasks = [], []
+        T = self._wtasks
+        e = lambda *shape, dt=bf16: torch.empty(*shape, dtype=dt, device=dev)  # noqa: E731
+        for layer in range(self.L):
+            names = [sp.name for sp in cell_specs(self.cfg, layer)]
+            if self.cfg.model in ("lstm", "rnn"):
+                k, b = s.view(names[0]), s.view(names[1])
+                GW = k.shape[1]
+                lw = LayerWeights(Wx=e(D, GW), Wx32=k[:D], bias=b, Wh=e(H, GW), WhT=e(GW, H),
+                                  WxT=e(GW, D) if (layer > 0 and self.cfg.model == "lstm")
+                                  else None)
+                T += [(k[D:], lw.Wh, 0), (k[D:], lw.WhT, 1), (k[:D], lw.Wx, 0)]
+                if lw.WxT is not None:
+                    T.append((k[:D], lw.WxT, 1))
+            elif self.cfg.model == "gru":
+                gk, gb, ck, cb = (s.view(n) for n in names)
+                Wx32, bias = e(D, 3 * H, dt=f32), e(3 * H, dt=f32)
+                lw = LayerWeights(Wx=e(D, 3 * H), Wx32=Wx32, bias=bias, Wh=e(H, H),
+                                  WhT=e(2 * H, H), W2=e(H, 2 * H), WT2=e(H, H))
+                T += [(gk[:D], Wx32[:, : 2 * H], 0), (ck[:D], Wx32[:, 2 * H:], 0),
+                      (gk[:D], lw.Wx[:, : 2 * H], 0), (ck[:D], lw.Wx[:, 2 * H:], 0),
+                      (gk[D:], lw.W2, 0), (gk[D:], lw.WhT, 1), (ck[D:], lw.Wh, 0),
+                      (ck[D:], lw.WT2, 1), (gb.view(1, -1), bias[: 2 * H].view(1, -1), 0),
+                      (cb.view(1, -1), bias[2 * H:].view(1, -1), 0)]
+            else:  # nas
+                kx, km = s.view(names[0]), s.view(names[1])
+                lw = LayerWeights(Wx=e(D, 8 * H), Wx32=kx, bias=torch.zeros(8 * H, device=dev),
+                                  Wh=e(H, 8 * H), WhT=e(8 * H, H))
+                T += [(km, lw.Wh, 0), (km, lw.WhT, 1), (kx, lw.Wx, 0)]
+            self._w.append(lw)
+        Ws32 = s.view("rnnlm/softmax_w")
+        self._head = dict(E=s.view("embedding"), Ws=e(H, self.V), bs=s.view("rnnlm/softmax_b"))
+        T.append((Ws32, self._head["Ws"], 0))
+        if self.fused_head:
+            VP, VK = self.ops.head_pads(self.V)
+            self._head["WsT"] = torch.zeros(VP, H, dtype=bf16, device=dev)   # pads stay zero
+            self._head["Wsk"] = torch.zeros(H, VK, dtype=bf16, device=dev)
+            T += [(Ws32, self._head["WsT"][: self.V], 1),
+                  (Ws32, self._head["Wsk"][:, : self.V], 0)]
+
+    def _prep(self) -> list:
+        """Prep-kernel tasks that refresh the weight layouts after a parameter change (empty
+        when the weights are current); the layer-0 ``E·W_x + b`` table is recomputed after
+        they ran (``_run_prep``)."""
+        ver = getattr(self.store, "version", 0)
+        if not self._w:
+            self._alloc_weights()
+        elif self._wver == ver:
+            return []
+        self._wver = ver
+        self._table_dirty = True
+        return list(self._wtasks)
+
+    def _run_prep(self, tasks: list):
+        for i in range(0, len(tasks), 48):  # kPrepMaxTasks
+            chunk = tasks[i: i + 48]
+            self.ops.prep([t[0] for t in chunk], [t[1] for t in chunk], [t[2] for t in chunk])
+        if self._table_dirty:
+            w0 = self._w[0]
+            if self.V > SEG_LDS_MAX_V:
+                # wide vocabulary: the [V, H] x [H, GW] table product on bf16 MFMA operands
+                # (the fp32 GEMM took 139 us per step at V = 8192), i.e. the same operand
+                # precision as a bf16 layer-0 input projection; the bf16 E copy is also the
+                # row source of the dense backward route's X0 gather
+                Eb = self._head.get("Ebf")
+                if Eb is None or Eb.shape != self._head["E"].shape:
+                    Eb = self._head["Ebf"] = torch.empty_like(self._head["E"], dtype=bf16)
+                Eb.copy_(self._head["E"])
+                self._head["table"] = torch.addmm(w0.bias, Eb, w0.Wx, out_dtype=f32)
+            else:
+                self._head["table"] = torch.addmm(w0.bias, self._head["E"], w0.Wx32)  # [V, GW]
+            self._table_dirty = False

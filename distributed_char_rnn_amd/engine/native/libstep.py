@@ -1,0 +1,108 @@
+"""Large-H LSTM path: per-time-step recurrent GEMM on the library (hipBLASLt) + an
+epilogue-only cell kernel (csrc/lstm_ew.hip), each layer's T-step loop captured once as a
+hipGraph and replayed (the reference's per-step cuBLAS GEMM + pointwise kernels, model.py:72)."""
+from __future__ import annotations
+
+import torch
+
+from .forward import FORGET_BIAS
+from .gemm import f32
+
+
+class LibStepMixin:
+    def _lib_step(self, direction: str, B: int) -> bool:
+        """Per-time-step recurrent GEMM on the library path + epilogue-only cell kernel, for
+        LSTM with H > 1024 (no weights-resident kernel there).  The fused per-step kernels
+        re-read the whole step payload once per 16-unit block (128 x at H = 2048), so their
+        step time grows linearly with the batch; a library GEMM reads W_h once per step
+        (scripts/bench_step_gemms.py: 17-25 us for B = 64-256).  auto: BPTT always, forward
+        from B >= 128 (at B = 64 the fused forward step, 16.7 us, beats GEMM + epilogue).
+        DCR_RECURRENCE=library forces it, =step disables it."""
+        if self.cfg.model != "lstm" or self.knobs.recurrence == "step":
+            return False
+        if self.knobs.recurrence == "library":
+            return True
+        if self.H <= 1024:
+            return False
+        return direction == "bwd" or B >= 128
+
+    def _lstm_fwd_lib(self, lw, lb, zx, ids, bufs) -> None:
+        T, B = lb.gates.shape[0], lb.gates.shape[1]
+        zrec = bufs.get("zrec")
+        if zrec is None:
+            zrec = bufs["zrec"] = torch.empty(1, B, self.GW, dtype=f32, device=self.dev)
+
+        def body(zx, ids):
+            for t in range(T):
+                # B operand as W_hᵀ-transposed (NT form): 20.7 vs 25.6 us at B = 256
+                torch.mm(lb.hbuf[t], lw.WhT.t(), out_dtype=f32, out=zrec[0])
+                self.ops.lstm_step_ew_fwd(zrec, zx if ids is not None else zx[t],
+                                          ids[t] if ids is not None else None, lb.cbuf[t],
+                                          lb.hbuf[t + 1], lb.hlast32 if t == T - 1 else None,
+                                          lb.cbuf[t + 1], lb.gates[t], FORGET_BIAS)
+
+        self._run_lib_loop(bufs, ("fwd", id(lb)), body, zx, ids,
+                           a_static=lb.zx is not None and zx.data_ptr() == lb.zx.data_ptr())
+
+    def _lstm_bwd_lib(self, lw, lb, dtop, bufs) -> None:
+        T, B = dtop.shape[0], dtop.shape[1]
+        dh = bufs.get("dhrec")
+        if dh is None:
+            dh = bufs["dhrec"] = torch.empty(1, B, self.H, dtype=f32, device=self.dev)
+        dc = bufs["dc"]
+        WhT = lw.Wh.t()
+
+        def body(dtop, _unused):
+            dc.zero_()
+            for t in reversed(range(T)):
+                # dh = dtop_t + dZ_{t+1}·W_hᵀ: the GEMM writes the recurrent part, the cell
+                # kernel adds dtop_t (an addmm with a 2-D input costs a separate copy launch)
+                if t < T - 1:
+                    torch.mm(lb.dz[t + 1], WhT, out_dtype=f32, out=dh[0])
+                self.ops.lstm_step_ew_bwd(dtop[t], dh if t < T - 1 else None, lb.gates[t],
+                                          lb.cbuf[t + 1], lb.cbuf[t], dc, lb.dz[t])
+
+        static = any(buf is not None and dtop.data_ptr() == buf.data_ptr()
+                     for buf in (bufs["dtop"], bufs["dx"]))
+        self._run_lib_loop(bufs, ("bwd", id(lb)), body, dtop, None, a_static=static)
+
+    def _run_lib_loop(self, bufs, key, body, a, b, a_static: bool = False) -> None:
+        """Run a T-step library loop (2 launches per step) as a replayed hipGraph: eager,
+        the per-step host launch cost (~15 us) is as long as the GPU's step at B = 64.  The
+        graph is captured on the first call with static copies of the loop's varying inputs
+        (a: zx / table / dtop, b: ids) and replayed afterwards; everything else it touches
+        (h, c, gates, dZ buffers, the bf16 weights refreshed in place) is persistent.
+        ``a_static``: ``a`` is itself a persistent buffer (dense zx, the dtop / dx buffers),
+        captured directly instead of through a copy.  DCR_DEBUG=lib_graph=0 runs eagerly."""
+        if not self.knobs.on("lib_graph"):
+            body(a, b)
+            return
+        # the graphs live with the buffers they were captured on (and die with them)
+        graphs = bufs.setdefault("lib_graphs", {})
+        ent = graphs.get(key)
+        if ent is None or ent[1].shape != a.shape or (b is not None and ent[2].shape != b.shape):
+            sa = a if a_static else a.clone()
+            sb = b.clone() if b is not None else None
+            body(sa, sb)  # warm-up outside capture (library handles, workspaces)
+            g = torch.cuda.CUDAGraph()
+            try:
+                s = torch.cuda.Stream(device=self.dev)
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    with torch.cuda.graph(g, stream=s):
+                        body(sa, sb)
+                torch.cuda.current_stream().wait_stream(s)
+            except RuntimeError:
+                graphs[key] = ("eager", None, None)
+                body(a, b)
+                return
+            graphs[key] = ent = (g, sa, sb)
+        if ent[0] == "eager":
+            body(a, b)
+            return
+        g, sa, sb = ent
+        if sa.data_ptr() != a.data_ptr():
+            sa.copy_(a)
+        if sb is not None and sb.data_ptr() != b.data_ptr():
+            sb.copy_(b)
+        g.replay()

@@ -1,0 +1,196 @@
+"""Execution plan of the native backend: which kernels run a training / inference step at
+(B, T), and the environment knobs that may steer that choice.
+
+Public knobs (docs/DESIGN.md "Knobs"); everything else is chosen from measurements:
+
+=================  ==========================================================================
+DCR_RECURRENCE     ``auto`` (default): two-layer wavefront kernels for LSTM layer pairs, single-
+                   layer persistent kernels otherwise, per-step kernels where no persistent
+                   grid fits; ``single``: no layer-pair wavefronts; ``step``: the fused per-step
+                   kernels only (no persistent grids, e.g. several processes on one GPU);
+                   ``library``: library GEMM + epilogue kernel per step (large-H LSTM path)
+DCR_PAIR_G         batch groups per workgroup of the wavefront kernels (0 = smallest that fits)
+DCR_MODE           ``auto`` | ``exclusive`` | ``overlap``: whether anything (RCCL buckets,
+                   side-stream GEMMs) may run beside a persistent BPTT grid
+DCR_SPIN_LIMIT     bound of every hand-off spin (a timeout sets the error word instead of hanging)
+DCR_DEBUG          ``key=value,...`` diagnostic overrides for tests and same-box A/B runs
+                   (DEBUG_KEYS below; the C++ launchers read ``gru_ub`` and ``step_nbt``)
+=================  ==========================================================================
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+from typing import Dict, Mapping, Optional
+
+PERSIST_MIN_T = 8  # shortest sequence that takes the persistent (weights-resident) kernels
+# lstm_persist_occupancy flags (csrc/lstm_persist.hip PF_*)
+PF_FUSED, PF_DIAG, PF_EXCL = 1, 2, 4
+
+RECURRENCES = ("auto", "single", "step", "library")
+MODES = ("auto", "exclusive", "overlap")
+DEBUG_KEYS = {
+    "persist_min_t": "shortest T that takes the persistent kernels (default 8)",
+    "pair_bwd": "0: paired forward, single-layer BPTT",
+    "fused_head": "0: library logits GEMM + CE kernel instead of the fused head",
+    "dew": "layer-0 embedding-table gradient: gemm (one-hot MFMA GEMM, default) | segsum | fused",
+    "side": "0: no side-stream weight GEMMs in overlap mode",
+    "xfuse": "0: no fused input projection in the single-layer persistent forward",
+    "exclusive": "0: never pick the one-workgroup-per-CU single-layer BPTT variant",
+    "wide_xent": "0: no one-read CE kernel for wide vocabularies",
+    "seg_sort": "0: unsorted atomic embedding gradient for wide vocabularies",
+    "lib_graph": "0: eager library-step loops (no hipGraph replay)",
+    "sample_graph": "0: eager sampling loop (no hipGraph replay)",
+    "gru_ub": "1: 16-unit GRU workgroups (C++)",
+    "step_nbt": "1/2/4: batch tiles per per-step workgroup (C++)",
+}
+
+
+def _parse_debug(s: str) -> Dict[str, str]:
+    out = {}
+    for item in filter(None, (x.strip() for x in s.split(","))):
+        k, sep, v = item.partition("=")
+        if not sep:
+            raise ValueError(f"DCR_DEBUG entry {item!r} is not key=value")
+        if k not in DEBUG_KEYS:
+            raise ValueError(f"unknown DCR_DEBUG key {k!r} (known: {', '.join(DEBUG_KEYS)})")
+        out[k] = v
+    return out
+
+
+@dataclass(frozen=True)
+class Knobs:
+    recurrence: str = "auto"
+    pair_g: int = 0
+    mode: str = "auto"
+    spin_limit: int = 1 << 22
+    debug: Mapping[str, str] = field(default_factory=dict)
+
+    @classmethod
+    def from_env(cls, env: Optional[Mapping[str, str]] = None) -> "Knobs":
+        env = os.environ if env is None else env
+        rec = env.get("DCR_RECURRENCE", "auto")
+        mode = env.get("DCR_MODE", "auto")
+        if rec not in RECURRENCES:
+            raise ValueError(f"DCR_RECURRENCE={rec!r}: one of {RECURRENCES}")
+        if mode not in MODES:
+            raise ValueError(f"DCR_MODE={mode!r}: one of {MODES}")
+        return cls(recurrence=rec, pair_g=int(env.get("DCR_PAIR_G", "0")), mode=mode,
+                   spin_limit=int(env.get("DCR_SPIN_LIMIT", str(1 << 22))),
+                   debug=_parse_debug(env.get("DCR_DEBUG", "")))
+
+    def dbg(self, key: str, default: str) -> str:
+        return self.debug.get(key, default)
+
+    def on(self, key: str) -> bool:
+        """A debug switch that is on unless set to 0."""
+        return self.debug.get(key, "1") != "0"
+
+    @property
+    def persistent(self) -> bool:
+        return self.recurrence in ("auto", "single")
+
+
+@dataclass
+class ExecutionPlan:
+    """Kernel choice for one (B, T, training) step shape.
+
+    * ``pair`` / ``pair_bwd``: LSTM layers (0,1), (2,3), ... run as two-layer wavefronts
+      (csrc/lstm2_persist.hip) with ``pair_g`` 32-row batch groups per workgroup over
+      ``pair_nbg`` groups (the batch padded to 32-row groups);
+    * ``persist``: the remaining LSTM layers run the single-layer persistent kernels
+      (csrc/lstm_persist.hip), ``xfuse`` with the layer input projection fused in;
+    * ``gru_persist``: the persistent GRU kernels (csrc/gru_persist.hip);
+    * ``mode``: ``exclusive`` (nothing beside a persistent grid: weight GEMMs in stream order,
+      all-reduce buckets released after the last BPTT launch) or ``overlap``; ``bwd_excl``: the
+      one-workgroup-per-CU single-layer BPTT variant (all hand-off loads in flight).
+    """
+    persist: bool = False
+    xfuse: bool = False
+    mode: str = "exclusive"
+    bwd_excl: bool = False
+    gru_persist: bool = False
+    pair: bool = False
+    pair_bwd: bool = False
+    pair_g: int = 0
+    pair_nbg: int = 0
+
+    @property
+    def persistent(self) -> bool:
+        return self.persist or self.pair or self.gru_persist
+
+    @property
+    def pair_rows(self) -> int:
+        """Rows of the wavefront BPTT's bias-gradient partials (two per workgroup column)."""
+        return 2 * self.pair_nbg // max(self.pair_g, 1)
+
+
+def make_plan(ops, cfg, knobs: Knobs, B: int, training: bool, T: int,
+              side_overlap: bool) -> ExecutionPlan:
+    """Residency plan of the persistent kernels at batch ``B``.
+
+    Every workgroup of a persistent grid spins on its neighbours, so the whole grid must be
+    co-resident.  ``lstm_persist_occupancy`` reports how many workgroups of the exact
+    instantiation fit on one CU (registers + LDS).  The single-layer kernels run in one of two
+    modes:
+
+    * ``overlap``: RCCL buckets and the side-stream weight-gradient GEMMs run *beside* the BPTT
+      kernels, so every BPTT grid must leave a spare workgroup slot on each CU
+      (grid <= (occupancy - 1) * CUs);
+    * ``exclusive``: nothing runs beside the persistent kernels, which allows the faster
+      one-workgroup-per-CU BPTT variant.
+
+    Exclusive is preferred whenever its BPTT variant fits: with the weight GEMMs split-K in
+    stream order it measured 2.74-2.80 vs 3.03-3.06 ms/step for overlap (H=512, B=256, same
+    box) -- a chip-filling GEMM beside the latency-bound recurrence slows both.  The wavefront
+    kernels are one workgroup per CU and always exclusive.
+    """
+    plan = ExecutionPlan()
+    H, o = cfg.rnn_size, ops
+    if T < int(knobs.dbg("persist_min_t", str(PERSIST_MIN_T))) or not knobs.persistent:
+        # a persistent grid first loads every weight slice into registers (~6 MB for the
+        # 2-layer H=512 pair); for a handful of steps (sampling: T = 1) the per-step kernels,
+        # which stream W_h from L2, are faster (scripts/bench_sample.py)
+        return plan
+    if cfg.model == "gru":
+        # persistent GRU: the C++ side picks the unit block whose fwd and bwd grids are
+        # co-resident; always exclusive (nothing beside it)
+        plan.gru_persist = bool(o.gru_persist_ub(H, B))
+        return plan
+    if cfg.model != "lstm":
+        return plan
+    # two-layer wavefront kernels for layers (0,1), (2,3), ...: any batch (padded to 32-row
+    # groups, G groups per workgroup), H in {128..512}
+    if cfg.num_layers >= 2 and knobs.recurrence == "auto":
+        G = int(o.lstm2_plan(H, B, knobs.pair_g))
+        if G:
+            plan.pair, plan.pair_g, plan.pair_nbg = True, G, int(o.lstm2_nbg(B, G))
+            plan.pair_bwd = training and knobs.on("pair_bwd")
+    if not bool(o.lstm_persist_supported(H, B)):
+        return plan
+    cus, grid = int(o.num_cus()), int(o.lstm_persist_grid(H, B))
+    vdew = cfg.vocab_size if (training and cfg.vocab_size <= 128) else 0
+
+    def fits(bwd, flags, margin=0):
+        return all(grid <= (int(o.lstm_persist_occupancy(bwd, H, B, v, flags)) - margin) * cus
+                   for v in {0, vdew})
+
+    if not (fits(0, 0) and (not training or fits(1, 0))):
+        return plan
+    plan.persist = True
+    plan.xfuse = knobs.on("xfuse") and bool(o.lstm_persist_xfuse_supported(H, B))
+    if not training:
+        return plan
+    shared_ok = fits(1, 0, margin=1)
+    excl_ok = fits(1, PF_EXCL) and knobs.on("exclusive")
+    if knobs.mode == "overlap" and shared_ok:
+        mode = "overlap"
+    elif knobs.mode == "exclusive" or excl_ok:
+        mode = "exclusive"
+    else:
+        mode = "overlap" if (shared_ok and side_overlap) else "exclusive"
+    if plan.pair_bwd:
+        mode = "exclusive"  # one workgroup per CU (register-bound): nothing runs beside it
+    plan.mode = mode
+    plan.bwd_excl = mode == "exclusive" and excl_ok
+    return plan

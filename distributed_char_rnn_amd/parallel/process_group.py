@@ -166,10 +166,10 @@ def pick_device(topo: Topology, requested: str = "auto", log=print) -> torch.dev
             # more local ranks than GPUs: ranks share a device.  The persistent recurrent
             # kernels need every CU of the chip (one workgroup per CU, co-resident grids), so two
             # processes' grids on one GPU spin into the timeout: use the per-step kernels.
-            if os.environ.get("DCR_PERSIST", "1") != "0":
+            if os.environ.get("DCR_RECURRENCE", "auto") in ("auto", "single"):
                 log(f"[rank {topo.rank}] {local_world} local ranks share {n} GPU(s): persistent "
-                    "kernels disabled (DCR_PERSIST=0); run one rank per GPU for speed")
-                os.environ["DCR_PERSIST"] = "0"
+                    "kernels disabled (DCR_RECURRENCE=step); run one rank per GPU for speed")
+                os.environ["DCR_RECURRENCE"] = "step"
         dev = torch.device("cuda", topo.local_rank % max(n, 1))
         torch.cuda.set_device(dev)
         return dev

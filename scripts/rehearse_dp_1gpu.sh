@@ -1,11 +1,11 @@
 #!/bin/bash
 # Multi-rank data-parallel rehearsal on ONE GPU (the GPU box has one card): 2 ranks of bench.py
-# and train.py share cuda:0 over gloo with the per-step kernels (DCR_PERSIST=0: two processes'
+# and train.py share cuda:0 over gloo with the per-step kernels (DCR_RECURRENCE=step: two processes'
 # persistent grids cannot be co-resident).  Checks the GPU-side DP plumbing (bucketed all-reduce
 # of CUDA gradient buffers, barriers, max-over-ranks timing, rank-0 output); RCCL itself needs
 # the driver's 8-GPU node.
 set -o pipefail
-export PYTHONPATH=$PWD DCR_PERSIST=0
+export PYTHONPATH=$PWD DCR_RECURRENCE=step
 mkdir -p gpurun_out
 timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
   --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 4 --warmup 1 \

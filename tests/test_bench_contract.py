@@ -64,7 +64,7 @@ def test_bench_two_ranks_one_gpu():
     RCCL refuses them (duplicate GPU) and gloo carries the bucketed all-reduce; the per-step
     kernels run because two processes' persistent grids cannot both be co-resident on one chip
     (the spin timeout reports that instead of hanging, see native_backend.check_errors)."""
-    env = dict(os.environ, PYTHONPATH=ROOT, DCR_PERSIST="0")
+    env = dict(os.environ, PYTHONPATH=ROOT, DCR_RECURRENCE="step")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",

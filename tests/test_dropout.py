@@ -23,7 +23,7 @@ def rel(a, b):
 @pytest.fixture(autouse=True)
 def _env(monkeypatch):
     monkeypatch.setenv("DCR_SPIN_LIMIT", str(1 << 20))
-    monkeypatch.setenv("DCR_PERSIST_MIN_T", "1")
+    monkeypatch.setenv("DCR_DEBUG", "persist_min_t=1")
 
 
 def expand(bits, scale):
@@ -71,7 +71,7 @@ def _run(model, B, T, H, L, ikp, okp, env=None, monkeypatch=None, tol=6e-2):
                                      (512, 3, 512, 2)])
 def test_dropout_on_pair_kernels_matches_oracle(B, T, H, L, monkeypatch):
     nat, _ = _run("lstm", B, T, H, L, 0.8, 0.7)
-    assert nat.backend._persist_plan(B, True, T)["pair"]
+    assert nat.backend._persist_plan(B, True, T).pair
 
 
 @pytest.mark.parametrize("ikp,okp", [(0.5, 1.0), (1.0, 0.6)])
@@ -81,7 +81,7 @@ def test_dropout_single_keep_prob(ikp, okp):
 
 def test_dropout_per_step_and_single_layer_kernels(monkeypatch):
     _run("lstm", 48, 5, 128, 3, 0.8, 0.7)                                   # pair + single
-    _run("lstm", 32, 4, 128, 2, 0.8, 0.7, {"DCR_PERSIST": "0"}, monkeypatch)  # per-step
+    _run("lstm", 32, 4, 128, 2, 0.8, 0.7, {"DCR_RECURRENCE": "step"}, monkeypatch)  # per-step
 
 
 def test_dropout_gru():

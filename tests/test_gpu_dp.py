@@ -60,7 +60,7 @@ def test_rccl_one_rank_grad_sync_is_bitwise_identity(monkeypatch):
     try:
         b = CharRNN(ModelConfig(**CFG), device="cuda", seed=1)
         plan = b.backend._persist_plan(B, True, T)
-        assert plan["pair"] and plan["mode"] == "exclusive"
+        assert plan.pair and plan.mode == "exclusive"
         ob = TFAdam(b.store, clip=5.0, guard=b.error_word())
         sync = GradSync(b.store, 1, bucket_mb=1.0, enabled=True)  # several buckets
         assert len(sync.buckets) >= 3

@@ -18,7 +18,7 @@ def rel(a, b):
 @pytest.fixture(autouse=True)
 def _short_spins(monkeypatch):
     monkeypatch.setenv("DCR_SPIN_LIMIT", str(1 << 20))
-    monkeypatch.setenv("DCR_PERSIST_MIN_T", "1")  # short test sequences still take these kernels
+    monkeypatch.setenv("DCR_DEBUG", "persist_min_t=1")  # short test sequences still take these kernels
 
 
 def _model(B, H, L, seed=3, **kw):
@@ -31,7 +31,7 @@ def _model(B, H, L, seed=3, **kw):
                                      (128, 3, 1024, 2), (64, 7, 384, 3)])
 def test_gru_persist_matches_reference(B, T, H, L):
     cfg, nat = _model(B, H, L)
-    assert nat.backend._persist_plan(B, True)["gru_persist"], "expected the persistent path"
+    assert nat.backend._persist_plan(B, True).gru_persist, "expected the persistent path"
     ref = ReferenceBackend(nat.store)
     torch.manual_seed(1)
     x = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
@@ -55,10 +55,10 @@ def test_gru_persist_equals_per_step_kernels(monkeypatch):
     """Same bf16 math, different schedule: agreement to accumulation-order noise."""
     B, T, H = 64, 16, 256
     _, a = _model(B, H, 2, seed=5)
-    monkeypatch.setenv("DCR_PERSIST", "0")
+    monkeypatch.setenv("DCR_RECURRENCE", "step")
     _, b = _model(B, H, 2, seed=5)
-    assert a.backend._persist_plan(B, True)["gru_persist"]
-    assert not b.backend._persist_plan(B, True)["gru_persist"]
+    assert a.backend._persist_plan(B, True).gru_persist
+    assert not b.backend._persist_plan(B, True).gru_persist
     x = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
     la, sa, _ = a.backend.train_step(x, x, a.zero_state(B))
     lb, sb, _ = b.backend.train_step(x, x, b.zero_state(B))

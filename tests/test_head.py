@@ -82,7 +82,7 @@ def test_model_fused_head_equals_library_head(monkeypatch):
     B, T = 64, 16
     cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=256, num_layers=2)
     a = CharRNN(cfg, device="cuda", seed=11)
-    monkeypatch.setenv("DCR_FUSED_HEAD", "0")
+    monkeypatch.setenv("DCR_DEBUG", "fused_head=0")
     c = CharRNN(cfg, device="cuda", seed=11)
     assert a.backend.fused_head and not c.backend.fused_head
     x = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)

@@ -82,30 +82,6 @@ def test_sumsq_kernel(dcr_ops, dtype, n):
     assert out.item() == pytest.approx(float((x.double() ** 2).sum()), rel=1e-5)
 
 
-@pytest.mark.parametrize("N,H,K", [(128, 64, 256), (1024, 512, 2048), (384, 256, 768),
-                                   (256, 128, 128), (32768, 512, 2048), (256, 192, 768),
-                                   (256, 1024, 4096), (128, 2048, 2048)])
-def test_tok_norm_kernel(dcr_ops, N, H, K):
-    """Fused sum_n ||dz[n]·wᵀ||² (TF per-token embedding norm term) vs an fp64 reference of
-    the same bf16 operands."""
-    torch.manual_seed(4)
-    dz = (torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16)
-    w = (torch.randn(H, K, device="cuda") * 0.05).to(torch.bfloat16)
-    assert dcr_ops.tok_norm_supported(N, H, K)
-    parts = torch.empty((N // 128) * (H // 64), device="cuda")
-    out = torch.empty(1, device="cuda")
-    dcr_ops.tok_norm(dz, w, parts, out)
-    torch.cuda.synchronize()
-    want = float(((dz.double() @ w.double().t()) ** 2).sum())
-    assert out.item() == pytest.approx(want, rel=1e-4)
-
-
-def test_tok_norm_unsupported_shapes(dcr_ops):
-    assert not dcr_ops.tok_norm_supported(100, 512, 2048)   # N % 128
-    assert not dcr_ops.tok_norm_supported(128, 512, 96)     # K % 64
-    assert not dcr_ops.tok_norm_supported(128, 96, 384)     # H % 64
-
-
 @pytest.mark.parametrize("world", [2, 8])
 def test_adam_clip_folds_data_parallel_average(dcr_ops, world):
     """gscale = 1/world on the all-reduced SUM == the kernel on the averaged gradient."""
@@ -124,19 +100,3 @@ def test_adam_clip_folds_data_parallel_average(dcr_ops, world):
     torch.testing.assert_close(nb, na, rtol=1e-5, atol=0)
     torch.testing.assert_close(p, pa, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(m, ma, rtol=1e-5, atol=1e-7)
-
-
-@pytest.mark.parametrize("B,N,K", [(64, 8192, 2048), (64, 2048, 8192), (128, 512, 256),
-                                   (64, 64, 96)])
-def test_step_gemm_split_k(dcr_ops, B, N, K):
-    """Split-K step GEMM (csrc/step_gemm.hip): the S fp32 slabs sum to X·Wᵀ."""
-    torch.manual_seed(6)
-    X = (torch.randn(B, K, device="cuda") * 0.1).to(torch.bfloat16)
-    W = (torch.randn(N, K, device="cuda") * 0.05).to(torch.bfloat16)
-    S = dcr_ops.step_gemm_splits(B, N, K)
-    assert S >= 1
-    part = torch.full((S, B, N), float("nan"), device="cuda")
-    dcr_ops.step_gemm(X, W, part)
-    torch.cuda.synchronize()
-    want = X.double() @ W.double().t()
-    torch.testing.assert_close(part.sum(0).double(), want, rtol=1e-4, atol=1e-4)

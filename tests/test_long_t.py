@@ -52,7 +52,8 @@ def _window(ids, B, T, offset=0):
 def _compare(cfg, B, T, ids, state_scale=0.3, tol_state=3e-2, tol_grad=5e-2, plan_key=None):
     nat = CharRNN(cfg, device="cuda", seed=17)
     if plan_key is not None:
-        assert nat.backend._persist_plan(B, True, T)[plan_key], "not on the hand-written path"
+        plan = nat.backend._persist_plan(B, True, T)
+        assert getattr(plan, plan_key), ("not on the hand-written path", plan)
     ref = ReferenceBackend(nat.store)
     x, y = _window(ids, B, T)
     torch.manual_seed(2)

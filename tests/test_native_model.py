@@ -96,7 +96,7 @@ def test_xent_kernel(dcr_ops):
 @pytest.mark.parametrize("V,W,N,ld,dt", [
     (65, 256, 5000, 256, "bf16"), (1, 130, 777, 130, "bf16"), (200, 64, 300, 64, "bf16"),
     (1, 3072, 5000, 3072, "bf16"), (1, 520, 777, 520, "bf16"),
-    # 16-byte-row route (segsum_vec_kernel): full strips, a ragged last strip, strided rows
+    # one-hot MFMA route (onehot_segsum_kernel): full strips, a ragged strip, strided rows
     (65, 512, 32768, 512, "bf16"), (96, 136, 1000, 136, "bf16"), (65, 2048, 4097, 2056, "bf16"),
     (65, 256, 5000, 256, "fp32")])
 def test_segsum_kernel(dcr_ops, V, W, N, ld, dt):
@@ -134,13 +134,34 @@ def test_segsum_atomic_wide_vocab_runs(dcr_ops, N):
     torch.testing.assert_close(out2.double(), ref, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("dew,rec", [("segsum", "auto"), ("segsum", "single"),
+                                     ("fused", "single")])
+def test_embedding_table_gradient_routes_agree(dew, rec, monkeypatch):
+    """The layer-0 dEW = onehot(ids)ᵀ·dZ0 routes (library one-hot GEMM, one-hot MFMA segment
+    sum, LDS partials inside the single-layer BPTT) give the same gradients up to fp32
+    summation order."""
+    B, T, H = 64, 12, 128
+    torch.manual_seed(3)
+    x = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
+    y = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
+    monkeypatch.setenv("DCR_RECURRENCE", rec)
+    grads = []
+    for mode in ("gemm", dew):
+        monkeypatch.setenv("DCR_DEBUG", f"persist_min_t=1,dew={mode}")
+        cfg, nat, _ = _pair("lstm", B, T, H, 2, seed=4)
+        nat.backend.train_step(x, y, nat.zero_state(B))
+        torch.cuda.synchronize()
+        grads.append(nat.store.grad.clone())
+    assert rel(grads[1], grads[0]) < 1e-5
+
+
 @pytest.mark.parametrize("nbt", ["2", "4"])
 @pytest.mark.parametrize("model", ["lstm", "gru", "rnn", "nas"])
 def test_per_step_batch_tiles_match_reference(model, nbt, monkeypatch):
     """Per-step kernels with several batch tiles per workgroup (weight slice read once per
     NBT x 16 rows; ragged last group) against the fp32 oracle."""
-    monkeypatch.setenv("DCR_PERSIST", "0")
-    monkeypatch.setenv("DCR_STEP_NBT", nbt)
+    monkeypatch.setenv("DCR_RECURRENCE", "step")
+    monkeypatch.setenv("DCR_DEBUG", f"step_nbt={nbt}")
     B, T, H, L = 56, 5, 64, 2
     torch.manual_seed(2)
     cfg, nat, ref = _pair(model, B, T, H, L)
@@ -158,32 +179,11 @@ def test_per_step_batch_tiles_match_reference(model, nbt, monkeypatch):
         assert rel(nat.store.gview(s.name), nat.store.view(s.name, g_ref)) < 6e-2, s.name
 
 
-def test_tf_norm_slot_fused_kernel_matches_library_route(monkeypatch):
-    """DCR_TOK_NORM=fused (optim.hip tok_norm) and the default library GEMM + sumsq route
-    write the same per-token embedding norm term on the persistent headline path."""
-    torch.manual_seed(0)
-    B, T, H = 64, 16, 128
-    x = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
-    y = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
-    slots = []
-    for mode in ("library", "fused"):
-        monkeypatch.setenv("DCR_TOK_NORM", mode)
-        cfg, nat, _ = _pair("lstm", B, T, H, 2)
-        nat.backend.train_step(x, y, nat.zero_state(B))
-        torch.cuda.synchronize()
-        slots.append(nat.store.norm_slot_view().item())
-    assert slots[0] > 0
-    assert slots[1] == pytest.approx(slots[0], rel=2e-3)
-
-
-@pytest.mark.parametrize("gemm", ["library", "native"])
 @pytest.mark.parametrize("B,T,H,L", [(32, 5, 64, 2), (64, 4, 128, 1)])
-def test_library_step_lstm_path_matches_reference(B, T, H, L, gemm, monkeypatch):
-    """DCR_LIBSTEP=1: per-step library GEMM (h·W_h / dZ·W_hᵀ) + epilogue-only cell kernels
-    (the H > 1024 LSTM path) against the fp32 oracle, persistent kernels off."""
-    monkeypatch.setenv("DCR_PERSIST", "0")
-    monkeypatch.setenv("DCR_LIBSTEP", "1")
-    monkeypatch.setenv("DCR_STEP_GEMM", gemm)
+def test_library_step_lstm_path_matches_reference(B, T, H, L, monkeypatch):
+    """DCR_RECURRENCE=library: per-step library GEMM (h·W_h / dZ·W_hᵀ) + epilogue-only cell
+    kernels (the H > 1024 LSTM path) against the fp32 oracle, persistent kernels off."""
+    monkeypatch.setenv("DCR_RECURRENCE", "library")
     torch.manual_seed(5)
     cfg, nat, ref = _pair("lstm", B, T, H, L)
     assert nat.backend._lib_step("fwd", B) and nat.backend._lib_step("bwd", B)

@@ -21,7 +21,7 @@ def rel(a, b):
 @pytest.fixture(autouse=True)
 def _env(monkeypatch):
     monkeypatch.setenv("DCR_SPIN_LIMIT", str(1 << 20))
-    monkeypatch.setenv("DCR_PERSIST_MIN_T", "1")
+    monkeypatch.setenv("DCR_DEBUG", "persist_min_t=1")
 
 
 def _batch(B, T, V=65, seed=0):
@@ -39,8 +39,8 @@ def test_pair_matches_oracle(B, T, H, L, G, monkeypatch):
     cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=L)
     nat = CharRNN(cfg, device="cuda", seed=3)
     plan = nat.backend._persist_plan(B, True, T)
-    assert plan["pair"] and plan["pair_bwd"], plan
-    assert G == 0 or plan["pair_g"] == G
+    assert plan.pair and plan.pair_bwd, plan
+    assert G == 0 or plan.pair_g == G
     ref = ReferenceBackend(nat.store)
     x, y = _batch(B, T, seed=B)
     torch.manual_seed(1)
@@ -76,7 +76,7 @@ def test_pair_groups_agree(B, H, Gs, monkeypatch):
         monkeypatch.setenv("DCR_PAIR_G", str(G))
         m = CharRNN(cfg, device="cuda", seed=11)
         plan = m.backend._persist_plan(B, True, T)
-        if plan["pair_g"] != G:
+        if plan.pair_g != G:
             pytest.skip(f"G={G} not co-resident on this GPU")
         st = m.zero_state(B)
         for _ in range(2):  # carried state across steps
@@ -104,10 +104,10 @@ def test_pair_ragged_batch_equals_per_step_kernels(monkeypatch):
     B, T, H = 50, 12, 128
     cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=2)
     a = CharRNN(cfg, device="cuda", seed=5)
-    monkeypatch.setenv("DCR_PERSIST", "0")
+    monkeypatch.setenv("DCR_RECURRENCE", "step")
     b = CharRNN(cfg, device="cuda", seed=5)
-    assert a.backend._persist_plan(B, True, T)["pair"]
-    assert not b.backend._persist_plan(B, True, T)["pair"]
+    assert a.backend._persist_plan(B, True, T).pair
+    assert not b.backend._persist_plan(B, True, T).pair
     x, y = _batch(B, T, seed=3)
     sa, sb = a.zero_state(B), b.zero_state(B)
     for _ in range(3):

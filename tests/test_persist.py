@@ -15,15 +15,17 @@ def rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
 
 
-@pytest.fixture(autouse=True, params=["granule", "counter"])
+@pytest.fixture(autouse=True, params=["auto", "single"])
 def _short_spins(monkeypatch, request):
+    """auto: layer pairs on the wavefront kernels; single: every layer on the single-layer
+    kernels."""
     monkeypatch.setenv("DCR_SPIN_LIMIT", str(1 << 20))
-    monkeypatch.setenv("DCR_PERSIST_MIN_T", "1")  # short test sequences still take these kernels
-    monkeypatch.setenv("DCR_HANDOFF", request.param)
+    monkeypatch.setenv("DCR_DEBUG", "persist_min_t=1")  # short test sequences still qualify
+    monkeypatch.setenv("DCR_RECURRENCE", request.param)
 
 
 def _persist(backend, B):
-    return backend._persist_plan(B, True)["persist"]
+    return backend._persist_plan(B, True).persist
 
 
 @pytest.mark.parametrize("mode", ["exclusive", "overlap"])
@@ -60,9 +62,10 @@ def test_persist_equals_per_step_kernels(monkeypatch):
     B, T, H = 64, 16, 256
     cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=2)
     a = CharRNN(cfg, device="cuda", seed=5)
-    monkeypatch.setenv("DCR_PERSIST", "0")
+    monkeypatch.setenv("DCR_RECURRENCE", "step")
     b = CharRNN(cfg, device="cuda", seed=5)
-    assert _persist(a.backend, B) and not _persist(b.backend, B)
+    assert a.backend._persist_plan(B, True).persistent
+    assert not b.backend._persist_plan(B, True).persistent
     x = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
     la, sa, _ = a.backend.train_step(x, x, a.zero_state(B))
     lb, sb, _ = b.backend.train_step(x, x, b.zero_state(B))
@@ -120,7 +123,8 @@ def test_residency_plan_and_refusal(dcr_ops):
     cnt = torch.zeros((B // 16) * (T + 1) * 4, dtype=torch.int32, device=dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     with pytest.raises(RuntimeError, match="co-resident"):
-        dcr_ops.lstm_persist_fwd(WT, zx, None, hbuf, cbuf, None, h32, cnt, err, 1.0, 1 << 16, None)
+        ring = torch.zeros(2 * B * H, dtype=torch.bfloat16, device=dev)
+        dcr_ops.lstm_persist_fwd(WT, zx, None, hbuf, cbuf, None, h32, cnt, err, 1.0, 1 << 16, ring)
     # the model still trains through the per-step kernels
     x = torch.randint(0, 65, (B, T), device=dev, dtype=torch.int32)
     loss, _, _ = m.backend.train_step(x, x, m.zero_state(B))
@@ -132,11 +136,12 @@ def test_two_layer_wavefront_equals_single_layer_kernels(B, T, H, monkeypatch):
     """lstm2_persist.hip (layers 0 and 1 as one wavefront launch) vs two single-layer
     persistent launches: identical bf16 math, so agreement to accumulation-order noise."""
     cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=2)
+    monkeypatch.setenv("DCR_RECURRENCE", "auto")
     a = CharRNN(cfg, device="cuda", seed=9)
-    monkeypatch.setenv("DCR_PAIR", "0")
+    monkeypatch.setenv("DCR_RECURRENCE", "single")
     b = CharRNN(cfg, device="cuda", seed=9)
-    assert a.backend._persist_plan(B, True, T)["pair"]
-    assert not b.backend._persist_plan(B, True, T)["pair"]
+    assert a.backend._persist_plan(B, True, T).pair
+    assert not b.backend._persist_plan(B, True, T).pair
     x = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
     sa, sb = a.zero_state(B), b.zero_state(B)
     for _ in range(2):  # carried state across steps
@@ -160,11 +165,12 @@ def test_two_layer_wavefront_bptt_equals_single_layer_kernels(B, T, H, L, monkey
     """lstm2_bwd_persist_kernel (layers l and l+1 in one reverse wavefront, layer l's dtop
     fused in-kernel) vs single-layer persistent BPTT launches + the dX GEMM."""
     cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=L)
+    monkeypatch.setenv("DCR_RECURRENCE", "auto")
     a = CharRNN(cfg, device="cuda", seed=5)
-    monkeypatch.setenv("DCR_PAIR_BWD", "0")
+    monkeypatch.setenv("DCR_DEBUG", "persist_min_t=1,pair_bwd=0")
     b = CharRNN(cfg, device="cuda", seed=5)
-    assert a.backend._persist_plan(B, True, T)["pair_bwd"]
-    assert not b.backend._persist_plan(B, True, T)["pair_bwd"]
+    assert a.backend._persist_plan(B, True, T).pair_bwd
+    assert not b.backend._persist_plan(B, True, T).pair_bwd
     torch.manual_seed(2)
     x = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
     y = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
@@ -178,33 +184,3 @@ def test_two_layer_wavefront_bptt_equals_single_layer_kernels(B, T, H, L, monkey
     for s in a.store.specs:
         e = rel(a.store.gview(s.name), b.store.gview(s.name))
         assert e < 2e-3, (s.name, e)
-
-
-@pytest.mark.parametrize("B,T,H,L", [(64, 5, 2048, 2), (32, 4, 1152, 1), (32, 6, 1536, 2)])
-def test_large_h_forward_equals_per_step_kernels(B, T, H, L, monkeypatch):
-    """lstm_big.hip (weights-resident forward with 8-unit shards, 1024 < H <= 2048) vs the
-    per-step kernels: the same bf16 math, so agreement to accumulation-order noise."""
-    cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=L)
-    monkeypatch.setenv("DCR_BIG_FWD", "1")  # opt-in path
-    a = CharRNN(cfg, device="cuda", seed=4)
-    if not a.backend._persist_plan(B, True)["big_fwd"]:
-        pytest.skip("large-H persistent forward not co-resident for this shape")
-    monkeypatch.setenv("DCR_BIG_FWD", "0")
-    b = CharRNN(cfg, device="cuda", seed=4)
-    assert not b.backend._persist_plan(B, True)["big_fwd"]
-    torch.manual_seed(3)
-    x = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
-    y = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
-    st = [tuple(torch.randn(B, H, device="cuda") * 0.5 for _ in range(2)) for _ in range(L)]
-    la, sa, _ = a.backend.train_step(x, y, [tuple(s.clone() for s in t) for t in st])
-    lb, sb, _ = b.backend.train_step(x, y, [tuple(s.clone() for s in t) for t in st])
-    torch.cuda.synchronize()
-    a.backend.check_errors()
-    assert abs(la.item() - lb.item()) < 1e-3
-    for u, v in zip(sa, sb):
-        for p, q in zip(u, v):
-            assert rel(p, q) < 2e-3
-    assert rel(a.store.grad, b.store.grad) < 5e-3
-    ref = ReferenceBackend(a.store)
-    lr, _, _ = ref.train_step(x, y, [tuple(s.clone() for s in t) for t in st])
-    assert abs(la.item() - lr.item()) < 2e-2 * max(1.0, abs(lr.item()))
