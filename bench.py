@@ -48,6 +48,8 @@ def parse(argv=None):
     ap.add_argument("--output_keep_prob", type=float, default=1.0,
                     help="dropout (DropoutWrapper output + embedding keep prob)")
     ap.add_argument("--profile", action="store_true", help="print a per-phase timing table")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay each step from one captured HIP graph (one GPU, no dropout)")
     ap.add_argument("--dist_backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="auto = nccl (RCCL over xGMI) on GPUs; gloo = multi-rank rehearsal on "
                          "one GPU (with DCR_RECURRENCE=step: persistent grids of two processes cannot "
@@ -104,12 +106,24 @@ def main(argv=None) -> int:
 
         prof = PhaseProfiler(True, device)
 
+    graphed = None
+    if a.graph:
+        from distributed_char_rnn_amd.engine.graph_step import GraphedStep
+
+        ok, why = GraphedStep.supported(model, world)
+        if not ok:
+            print(f"--graph: {why}", file=sys.stderr)
+            return 2
+        graphed = GraphedStep(model, opt, log=lambda m: print(m, file=sys.stderr))
+
     def step(i, state):
         k = i % nbat
         x = xs[:, k * T:(k + 1) * T]
         y = ys[:, k * T:(k + 1) * T]
         if k == 0:
             state = model.zero_state(B)
+        if graphed is not None:
+            return graphed(x, y, state, 2e-3)
         sync.reset()
         if prof is None:
             loss, state, _ = model.train_step(x, y, state, sync)
@@ -162,6 +176,7 @@ def main(argv=None) -> int:
                                         if (a.model, a.hidden, a.layers, T, B) ==
                                         ("lstm", 512, 2, 128, 256) else None),
             "keep_prob": [a.input_keep_prob, a.output_keep_prob],
+            "graph": bool(a.graph),
             "final_loss": final_loss,
         }
         print(json.dumps(out), flush=True)

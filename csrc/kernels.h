@@ -17,7 +17,7 @@ void launch_sumsq(const void* x, bool is_bf16, int64_t n, float* partials, float
 void launch_adam_clip(float* p, const float* g, float* m, float* v, bf16* pbf, int64_t n,
                       float* partials, float* norm_out, float lr_t, float b1, float b2, float eps,
                       float clip, float gscale, int64_t n_norm, const float* extra_sq,
-                      const unsigned* skip_if, hipStream_t stream);
+                      const unsigned* skip_if, const float* lr_dev, hipStream_t stream);
 
 // ---- rnn_step.hip -----------------------------------------------------------------------
 enum CellKind { CELL_LSTM = 0, CELL_GRU_A = 1, CELL_GRU_B = 2, CELL_RNN = 3, CELL_NAS = 4 };

@@ -51,7 +51,8 @@ void adam_clip(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
                const c10::optional<at::Tensor>& pbf, at::Tensor& partials, at::Tensor& norm_out,
                double lr_t, double b1, double b2, double eps, double clip, double gscale,
                int64_t n_norm, const c10::optional<at::Tensor>& extra_sq,
-               const c10::optional<at::Tensor>& skip_if) {
+               const c10::optional<at::Tensor>& skip_if,
+               const c10::optional<at::Tensor>& lr_dev) {
   for (const at::Tensor* t : {(const at::Tensor*)&p, &g, (const at::Tensor*)&m, (const at::Tensor*)&v}) {
     CHECK_DEV(*t); CHECK_CONTIG(*t); CHECK_F32(*t); CHECK_ALIGN16(*t);
     TORCH_CHECK(t->numel() == p.numel(), "adam buffers must have equal numel");
@@ -75,12 +76,17 @@ void adam_clip(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
     CHECK_DEV(*skip_if);
     TORCH_CHECK(skip_if->element_size() == 4 && skip_if->numel() >= 1, "skip_if: one 32-bit word");
   }
+  if (lr_dev.has_value() && lr_dev->defined()) {
+    CHECK_DEV(*lr_dev); CHECK_F32(*lr_dev);
+    TORCH_CHECK(lr_dev->numel() >= 1, "lr_dev: one fp32 element");
+  }
   dcr::launch_adam_clip(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), pb,
                         p.numel(), ptr<float>(partials), ptr<float>(norm_out), (float)lr_t,
                         (float)b1, (float)b2, (float)eps, (float)clip, (float)gscale, n_norm, ex,
                         skip_if.has_value() && skip_if->defined()
                             ? reinterpret_cast<const unsigned*>(skip_if->data_ptr())
                             : nullptr,
+                        lr_dev.has_value() && lr_dev->defined() ? ptr<float>(*lr_dev) : nullptr,
                         cur_stream());
 }
 
@@ -1031,7 +1037,7 @@ TORCH_LIBRARY(dcr, m) {
       "adam_clip(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor(d!)? pbf, "
       "Tensor(e!) partials, Tensor(f!) norm_out, float lr_t, float b1, float b2, float eps, "
       "float clip, float gscale=1.0, int n_norm=-1, Tensor? extra_sq=None, "
-      "Tensor? skip_if=None) -> ()");
+      "Tensor? skip_if=None, Tensor? lr_dev=None) -> ()");
   m.def("sumsq(Tensor x, Tensor(a!) partials, Tensor(b!) out) -> ()");
   m.def(
       "lstm_step_ew_fwd(Tensor zrec, Tensor zx, Tensor? ids, Tensor cprev, Tensor(a!) hout, "

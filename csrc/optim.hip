@@ -73,13 +73,15 @@ __global__ void __launch_bounds__(kOptThreads) adam_apply_kernel(
     float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
     bf16* __restrict__ pbf, int64_t n, const float* __restrict__ partials, int nparts,
     float* __restrict__ norm_out, float lr_t, float b1, float b2, float eps, float clip,
-    float gscale, const unsigned* __restrict__ skip_if) {
+    float gscale, const unsigned* __restrict__ skip_if, const float* __restrict__ lr_dev) {
   __shared__ float red[kOptThreads / 64];
   // a persistent recurrent kernel that hit its spin timeout leaves garbage gradients and sets
   // its error word: the update is skipped on device (weights and slots stay unchanged) and the
   // host raises when it reads the word
   if (skip_if && __hip_atomic_load(skip_if, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
     return;
+  // a step replayed from a hipGraph reads its (per-step) lr_t from device memory
+  if (lr_dev) lr_t = *lr_dev;
   float acc = 0.f;
   for (int i = threadIdx.x; i < nparts; i += kOptThreads) acc += partials[i];
   const float sumsq = block_sum<kOptThreads>(acc, red);
@@ -162,11 +164,12 @@ void launch_sumsq(const void* x, bool is_bf16, int64_t n, float* partials, float
 void launch_adam_clip(float* p, const float* g, float* m, float* v, bf16* pbf, int64_t n,
                       float* partials, float* norm_out, float lr_t, float b1, float b2, float eps,
                       float clip, float gscale, int64_t n_norm, const float* extra_sq,
-                      const unsigned* skip_if, hipStream_t stream) {
+                      const unsigned* skip_if, const float* lr_dev, hipStream_t stream) {
   const int nb = opt_num_partials(n);
   sumsq_partials_kernel<float><<<nb, kOptThreads, 0, stream>>>(g, n_norm, partials, extra_sq);
   adam_apply_kernel<<<nb, kOptThreads, 0, stream>>>(p, g, m, v, pbf, n, partials, nb, norm_out,
-                                                    lr_t, b1, b2, eps, clip, gscale, skip_if);
+                                                    lr_t, b1, b2, eps, clip, gscale, skip_if,
+                                                    lr_dev);
 }
 
 }  // namespace dcr

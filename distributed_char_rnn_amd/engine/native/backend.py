@@ -76,6 +76,7 @@ class NativeBackend(LayoutsMixin, BuffersMixin, ForwardMixin, BackwardMixin, Lib
         self._side = None
         self._side_used = False
         self._steps = 0
+        self.capturing = False  # a hipGraph capture of train_step is in progress (graph_step.py)
         self._npart: Optional[torch.Tensor] = None
         self._drop_seed = int(seed) * 0x9E3779B1 + 0x5EED
         self._drop_step = 0

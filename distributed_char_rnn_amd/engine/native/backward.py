@@ -22,27 +22,30 @@ class BackwardMixin:
                                                    logits_bias=not wide)
         P = bufs["plan"]
         dlog = bufs["dlogits"]
+        # the returned loss is read by the caller after the NEXT step was enqueued (trainer
+        # logging): alternate two slots so that step does not overwrite it
+        li = self._steps & 1
+        loss_buf = bufs["loss"][li, :1]
         s, hd = self.store, self._head
         if self.fused_head:
             # one launch: logits (only if asked for) -> CE -> bf16 dlogits, d softmax_b, dtop
             self.ops.head(O, hd["WsT"], hd["Wsk"], hd["bs"], tgt, 1.0 / N,
                           logits if want_extras else None, bufs["row_loss"], dlog,
                           bufs["dtop"].view(N, H), s.gview("rnnlm/softmax_b"),
-                          bufs["head_part"], bufs["loss"])
+                          bufs["head_part"], loss_buf)
             mm_tn(O, dlog, s.gview("rnnlm/softmax_w"))
             dtop = bufs["dtop"].view(T, B, H)
         elif wide:
             # wide vocabulary: one-read CE (bias added in-kernel), d softmax_b fused (xent_wide)
             self.ops.xent_wide(logits, hd["bs"], tgt, 1.0 / N, bufs["row_loss"], dlog,
                                bufs["colpart"], s.gview("rnnlm/softmax_b"), bufs["xpart"],
-                               bufs["loss"])
+                               loss_buf)
             if want_extras:
                 logits += hd["bs"]
             mm_tn(O, dlog, s.gview("rnnlm/softmax_w"))
             dtop = mm_into(dlog, hd["Ws"].t(), bufs["dtop"].view(N, H)).view(T, B, H)
         else:
-            self.ops.xent(logits, tgt, 1.0 / N, bufs["row_loss"], dlog, bufs["xpart"],
-                          bufs["loss"])
+            self.ops.xent(logits, tgt, 1.0 / N, bufs["row_loss"], dlog, bufs["xpart"], loss_buf)
             # ---- head gradients
             mm_tn(O, dlog, s.gview("rnnlm/softmax_w"))
             self.ops.segsum(dlog, None, 1, bufs["colsum"][:, :V], bufs["ws"], False)
@@ -239,9 +242,9 @@ class BackwardMixin:
             _release()
         extras = {"logits": logits, "loss": bufs["row_loss"]} if want_extras else None
         self._steps += 1
-        if P.persistent:
+        if P.persistent and not self.capturing:
             self._poll_errors()
-        return bufs["loss"][0], new_state, extras
+        return loss_buf[0], new_state, extras
 
     def _dew(self, dZ0: torch.Tensor, ids_tm: torch.Tensor, bufs, fused: bool) -> torch.Tensor:
         """Layer-0 embedding-table gradient dEW = onehot(ids)ᵀ·dZ0 [V, GW] (gather route: the

@@ -74,7 +74,7 @@ class BuffersMixin:
             dlogits=e(N, self.V, dt=bf16) if training else None,
             row_loss=e(N),
             xpart=e(self.ops.xent_num_partials(N)),
-            loss=e(1),
+            loss=e(2, 4),  # two 16-B slots, ping-pong by step parity (see train_step)
             dc=e(B, H),
             gpart=e(B, H) if m == "gru" else None,
             ws=e(ws),

@@ -23,10 +23,10 @@ class InferenceMixin:
         if self.fused_head:
             hd = self._head
             self.ops.head(O, hd["WsT"], None, hd["bs"], tgt, 1.0, None, None, None, None, None,
-                          bufs["head_part"], bufs["loss"])
+                          bufs["head_part"], bufs["loss"][0, :1])
         else:
-            self.ops.xent(logits, tgt, 1.0, None, None, bufs["xpart"], bufs["loss"])
-        return bufs["loss"][0].clone(), new_state
+            self.ops.xent(logits, tgt, 1.0, None, None, bufs["xpart"], bufs["loss"][0, :1])
+        return bufs["loss"][0, 0].clone(), new_state
 
     @torch.no_grad()
     def sample_sequence(self, prime_ids, num: int, sampling_type: int, seed: int, num_samples: int,

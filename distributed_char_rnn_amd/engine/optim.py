@@ -59,11 +59,13 @@ class TFAdam:
         return lr * math.sqrt(1.0 - self.b2 ** t) / (1.0 - self.b1 ** t)
 
     @torch.no_grad()
-    def step(self, lr: float, grad_scale: float = 1.0) -> torch.Tensor:
+    def step(self, lr: float, grad_scale: float = 1.0,
+             lr_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Clip the flat gradient (times ``grad_scale``: 1/world when the data-parallel average
         is folded in here, see ``GradSync.finish(defer_scale=True)``) by global norm and apply
         one update.  Returns the pre-clip global norm as a 1-element device tensor (no host
-        sync)."""
+        sync).  ``lr_dev``: a device fp32 scalar the kernel reads lr_t from (a step captured in
+        a hipGraph; the caller writes ``lr_t(lr)`` into it before every replay)."""
         lr_t = self.lr_t(lr)
         st = self.store
         n = st.norm_slot  # every parameter; the norm slot and the padding after it are not
@@ -74,7 +76,7 @@ class TFAdam:
             mirror = self.mirror.narrow(0, 0, n) if self.mirror is not None else None
             self._ops.adam_clip(p, g, m, v, mirror, self._partials, self.last_norm, lr_t,
                                 self.b1, self.b2, self.eps, self.clip, float(grad_scale), n_norm,
-                                slot, self.guard)
+                                slot, self.guard, lr_dev)
         else:
             gn = g.narrow(0, 0, n_norm).double()
             sq = (gn * gn).sum() + (slot.double().sum() if slot is not None else 0.0)

@@ -34,6 +34,7 @@ from ..utils import checkpoint as ckpt
 from ..utils import data as data_mod
 from ..utils import safe_pickle
 from ..utils.metrics import MetricsLogger, PhaseProfiler, progress_line
+from .graph_step import GraphedStep
 from .optim import TFAdam, lr_for_epoch
 
 NEED_BE_SAME = ["model", "rnn_size", "num_layers", "seq_length"]
@@ -263,6 +264,15 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
                     "chars_per_sec": chars_per_step / max(dt, 1e-9), "rank_world": ctx.world_size})
         logger.scalar("train_loss", loss, gs)
 
+    # --graph: the whole step (fwd, head, BPTT, weight grads, clip + Adam) as one replayed
+    # hipGraph; summary steps that want the logits run eagerly
+    graphed = None
+    if getattr(args, "graph", "off") != "off":
+        ok, why = GraphedStep.supported(model, ctx.world_size)
+        if ok:
+            graphed = GraphedStep(model, opt, log=lambda m: _log(m, rank))
+        elif args.graph == "on":
+            _log(f"--graph on: not available ({why}); eager steps", rank)
     stop = False
     state = None
     for e in range(start_epoch, args.num_epochs):
@@ -278,12 +288,17 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
             t0 = time.time()
             x, y = loader.next_batch()
             want = chief and summary_every > 0 and (global_step % summary_every == 0)
-            with prof.phase("fwd_bwd"):
-                loss_t, state, extras = _step(model, x, y, state, sync, want)
-            with prof.phase("grad_sync"):
-                gs = sync.finish(defer_scale=True)
-            with prof.phase("optimizer"):
-                opt.step(lr, grad_scale=gs)
+            if graphed is not None and not want:
+                with prof.phase("graph_step"):
+                    loss_t, state = graphed(x, y, state, lr)
+                extras = None
+            else:
+                with prof.phase("fwd_bwd"):
+                    loss_t, state, extras = _step(model, x, y, state, sync, want)
+                with prof.phase("grad_sync"):
+                    gs = sync.finish(defer_scale=True)
+                with prof.phase("optimizer"):
+                    opt.step(lr, grad_scale=gs)
             global_step += 1
             steps_done += 1
             process_group.maybe_inject_fault(rank, global_step)

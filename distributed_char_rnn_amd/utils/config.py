@@ -88,7 +88,9 @@ def train_parser() -> argparse.ArgumentParser:
     g.add_argument("--heartbeat", type=float, default=0.0,
                    help="seconds between rank heartbeats in the rendezvous store (0 = off)")
     g.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
-                   help="capture the GPU training step in a HIP graph")
+                   help="replay the whole GPU training step (forward, BPTT, weight gradients, "
+                        "clip + Adam) as one captured HIP graph (engine/graph_step.py); auto = "
+                        "on wherever it applies (one rank, native backend, no dropout)")
     return p
 
 

@@ -1,0 +1,56 @@
+"""--graph: the whole training step replayed from one captured hipGraph
+(engine/graph_step.py) must follow the eager step exactly -- same kernels, same order."""
+import pytest
+import torch
+
+from distributed_char_rnn_amd.engine.graph_step import GraphedStep
+from distributed_char_rnn_amd.engine.optim import TFAdam
+from distributed_char_rnn_amd.models.char_rnn import CharRNN
+from distributed_char_rnn_amd.models.params import ModelConfig
+
+
+def test_graph_step_unsupported_cases_cpu():
+    cfg = ModelConfig(model="lstm", vocab_size=20, rnn_size=16, num_layers=2)
+    m = CharRNN(cfg, device="cpu", seed=0)
+    ok, why = GraphedStep.supported(m, 1)
+    assert not ok and "native" in why
+
+
+def _run(graph, cfg, B, T, steps, lr=2e-3):
+    m = CharRNN(cfg, device="cuda", seed=21)
+    opt = TFAdam(m.store, clip=5.0, guard=m.error_word())
+    gstep = GraphedStep(m, opt) if graph else None
+    g = torch.Generator().manual_seed(4)
+    data = [(torch.randint(0, cfg.vocab_size, (B, T), generator=g, dtype=torch.int32),
+             torch.randint(0, cfg.vocab_size, (B, T), generator=g, dtype=torch.int32))
+            for _ in range(steps)]
+    st = m.zero_state(B)
+    losses = []
+    for i, (x, y) in enumerate(data):
+        if i == 3:
+            st = m.zero_state(B)  # an epoch boundary: a foreign state is copied in
+        if gstep is not None:
+            loss, st = gstep(x.cuda(), y.cuda(), st, lr)
+        else:
+            loss, st, _ = m.train_step(x.cuda(), y.cuda(), st)
+            opt.step(lr)
+        losses.append(loss.clone())  # (eager losses are views of a ping-pong buffer)
+    torch.cuda.synchronize()
+    m.check_errors()
+    return [float(v) for v in losses], m.store.flat.clone(), opt, gstep, st
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,T,H,L", [(50, 50, 128, 2), (64, 16, 256, 3)])
+def test_graph_step_equals_eager(B, T, H, L):
+    cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=L)
+    le, pe, oe, _, se = _run(False, cfg, B, T, 7)
+    lg, pg, og, gs, sg = _run(True, cfg, B, T, 7)
+    assert gs.graph is not None and not gs.failed and gs.replays >= 4
+    assert og.t == oe.t == 7
+    assert lg == le
+    assert torch.equal(pg, pe)
+    assert torch.equal(og.m, oe.m) and torch.equal(og.v, oe.v)
+    for a, b in zip(sg, se):
+        for u, v in zip(a, b):
+            assert torch.equal(u, v)
