@@ -43,8 +43,10 @@ class GraphedStep:
 
     @staticmethod
     def supported(model, world: int) -> Tuple[bool, str]:
-        if model.device.type != "cuda" or model.backend_name != "native":
-            return False, "needs the native GPU backend"
+        from .native import NativeBackend
+
+        if model.device.type != "cuda" or not isinstance(model.backend, NativeBackend):
+            return False, "needs the native GPU backend (rnn_size a multiple of 32)"
         if world > 1:
             return False, "data parallel: the all-reduce buckets are released by host callbacks"
         c = model.cfg

@@ -39,17 +39,21 @@ class CharRNN:
         self.device = torch.device(device)
         self.store = ParamStore(cfg, self.device, seed)
         if backend == "auto":
-            # fp32 on the GPU runs the autograd oracle; the native kernels compute in bf16 and
-            # need rnn_size % 32 == 0 (MFMA tiles): other sizes run the autograd path on the GPU
-            backend = "native" if (self.device.type == "cuda" and dtype != "fp32"
-                                   and cfg.rnn_size % 32 == 0) else "reference"
-            if self.device.type == "cuda" and cfg.rnn_size % 32 != 0:
+            # fp32 on the GPU runs the autograd oracle; the native kernels compute in bf16
+            backend = "native" if (self.device.type == "cuda" and dtype != "fp32") else "reference"
+            if backend == "native" and cfg.rnn_size % 32 != 0 and cfg.model == "nas":
                 import warnings
 
-                warnings.warn(f"rnn_size={cfg.rnn_size} is not a multiple of 32: running the "
-                              "PyTorch autograd path on the GPU instead of the native kernels")
+                warnings.warn(f"NAS with rnn_size={cfg.rnn_size} (not a multiple of 32): "
+                              "running the PyTorch autograd path on the GPU")
+                backend = "reference"
         self.backend_name = backend
-        if backend == "native":
+        if backend == "native" and cfg.rnn_size % 32 != 0:
+            # the MFMA kernels tile H by 32 / 128: run a zero-padded model (engine/native/padded.py)
+            from ..engine.native.padded import PaddedNativeBackend
+
+            self.backend = PaddedNativeBackend(self.store, dtype=dtype, seed=seed or 0)
+        elif backend == "native":
             from ..engine.native_backend import NativeBackend
 
             self.backend = NativeBackend(self.store, dtype=dtype, seed=seed or 0)
