@@ -41,6 +41,8 @@ def parse(argv=None):
     ap.add_argument("--model", default="lstm")
     ap.add_argument("--bucket_mb", type=float, default=8.0)
     ap.add_argument("--allreduce_dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--dp_mode", default="replicated", choices=["replicated", "sharded"],
+                    help="sharded: reduce-scatter + Adam on a 1/world shard + all-gather")
     ap.add_argument("--clip_norm", default="tf", choices=["tf", "dense"],
                     help="embedding term of the clip norm (default: TF per-token semantics)")
     ap.add_argument("--input_keep_prob", type=float, default=1.0,
@@ -89,8 +91,16 @@ def main(argv=None) -> int:
                       output_keep_prob=a.output_keep_prob)
     model = CharRNN(cfg, device=device, seed=1234)
     opt = TFAdam(model.store, clip=5.0, guard=model.error_word())
-    sync = GradSync(model.store, world, a.bucket_mb, a.allreduce_dtype)
-    sync.broadcast_params(0)
+    sharded = a.dp_mode == "sharded" and world > 1
+    sync = GradSync(model.store, world, a.bucket_mb, a.allreduce_dtype,
+                    enabled=world > 1 and not sharded)
+    if world > 1:
+        dist.broadcast(model.store.flat, 0)
+    zstep = None
+    if sharded:
+        from distributed_char_rnn_amd.parallel.zero import ShardedStep
+
+        zstep = ShardedStep(model.store, opt, world, rank, wire=a.allreduce_dtype)
     model.params_changed()
 
     B, T = a.batch, a.seq
@@ -124,6 +134,10 @@ def main(argv=None) -> int:
             state = model.zero_state(B)
         if graphed is not None:
             return graphed(x, y, state, 2e-3)
+        if zstep is not None:
+            loss, state, _ = model.train_step(x, y, state)
+            zstep.step(2e-3)
+            return loss, state
         sync.reset()
         if prof is None:
             loss, state, _ = model.train_step(x, y, state, sync)
@@ -171,7 +185,7 @@ def main(argv=None) -> int:
             "data": "synthetic (Shakespeare-unigram token stream, random-init weights)",
             "config": {"model": f"{a.layers}-layer {a.model.upper()}-{a.hidden} (vocab {a.vocab})",
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": T,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}" + ("-zero1" if sharded else "")},
             "vs_torch_nn_lstm_miopen": (cps / (MIOPEN_1GPU_CPS * world)
                                         if (a.model, a.hidden, a.layers, T, B) ==
                                         ("lstm", 512, 2, 128, 256) else None),

@@ -93,6 +93,35 @@ class TFAdam:
         self.store.version += 1
         return self.last_norm
 
+    @torch.no_grad()
+    def step_range(self, lr: float, lo: int, hi: int, sumsq: torch.Tensor,
+                   grad_scale: float = 1.0) -> torch.Tensor:
+        """One update of the parameters [lo, hi) only, clipped by the GLOBAL norm
+        sqrt(``sumsq``) * grad_scale (a 1-element device tensor: the sum of squares of every
+        norm term, already reduced over ranks).  The sharded data-parallel step
+        (parallel/zero.py) calls this on each rank's shard."""
+        lr_t = self.lr_t(lr)
+        hi = min(hi, self.store.norm_slot)  # the norm slot and the tail padding are not params
+        if hi > lo:
+            p, g, m, v = (b[lo:hi] for b in (self.store.flat, self.store.grad, self.m, self.v))
+            if self.native:
+                self._ops.adam_clip(p, g, m, v, None, self._partials, self.last_norm, lr_t,
+                                    self.b1, self.b2, self.eps, self.clip, float(grad_scale), 0,
+                                    sumsq, self.guard)
+            else:
+                norm = torch.sqrt(sumsq.double().sum()).float() * grad_scale
+                s = self.clip / torch.clamp(norm, min=self.clip) if self.clip > 0 else torch.ones(())
+                gs = g * (s * grad_scale)
+                m.mul_(self.b1).add_(gs, alpha=1 - self.b1)
+                v.mul_(self.b2).addcmul_(gs, gs, value=1 - self.b2)
+                p.sub_(lr_t * m / (v.sqrt() + self.eps))
+                self.last_norm.copy_(norm.reshape(1))
+        else:  # a shard holding only the norm slot / tail padding: nothing to update
+            self.last_norm.copy_((torch.sqrt(sumsq.sum()) * grad_scale).reshape(1))
+        self.t += 1
+        self.store.version += 1
+        return self.last_norm
+
     # -- checkpoint support (TF slot names) ----------------------------------------------
     def slot_state(self):
         """TF-named Adam slots + beta powers for the checkpoint."""

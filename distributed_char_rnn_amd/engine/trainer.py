@@ -214,14 +214,17 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
             start_batch = int(sd.get("dcr/batch_pointer", -1)) + 1
         _log(f"restored {prefix} (global_step {global_step})", rank)
 
+    sharded = getattr(args, "dp_mode", "replicated") == "sharded" and ctx.world_size > 1
     sync = GradSync(model.store, ctx.world_size, getattr(args, "bucket_mb", 8.0),
-                    getattr(args, "allreduce_dtype", "fp32"))
+                    getattr(args, "allreduce_dtype", "fp32"),
+                    enabled=(ctx.world_size > 1 and not sharded))
+    zstep = None
     saved_state = None
     if ctx.world_size > 1:
         # rank 0's restore -> every rank: parameters, Adam slots, step counters (a rank that
         # kept opt.t = 0 would use a different lr_t and diverge; one that kept the batch
         # pointer 0 would run a different number of steps and hang the last all-reduce)
-        sync.broadcast_params(0)
+        ctx.broadcast_(model.store.flat)
         ctx.broadcast_(opt.m)
         ctx.broadcast_(opt.v)
         meta = torch.tensor([global_step, opt.t, start_epoch, start_batch], dtype=torch.int64,
@@ -264,6 +267,12 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
                     "chars_per_sec": chars_per_step / max(dt, 1e-9), "rank_world": ctx.world_size})
         logger.scalar("train_loss", loss, gs)
 
+    if sharded:
+        from ..parallel.zero import ShardedStep
+
+        zstep = ShardedStep(model.store, opt, ctx.world_size, rank,
+                            wire=getattr(args, "allreduce_dtype", "fp32"))
+        _log(f"sharded optimizer: shard {zstep.shard} of {model.store.numel} elements", rank)
     # --graph: the whole step (fwd, head, BPTT, weight grads, clip + Adam) as one replayed
     # hipGraph; summary steps that want the logits run eagerly
     graphed = None
@@ -288,7 +297,12 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
             t0 = time.time()
             x, y = loader.next_batch()
             want = chief and summary_every > 0 and (global_step % summary_every == 0)
-            if graphed is not None and not want:
+            if zstep is not None:  # sharded optimizer step (ZeRO-1)
+                with prof.phase("fwd_bwd"):
+                    loss_t, state, extras = _step(model, x, y, state, sync, want)
+                with prof.phase("sharded_step"):
+                    zstep.step(lr)
+            elif graphed is not None and not want:
                 with prof.phase("graph_step"):
                     loss_t, state = graphed(x, y, state, lr)
                 extras = None
@@ -320,6 +334,8 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
                     pending = None
                 model.check_errors()  # never checkpoint weights of a timed-out step
                 save_st = None
+                if zstep is not None:
+                    zstep.gather_slots()  # collective: the chief saves the full Adam slots
                 if getattr(args, "save_state", False):
                     save_st = gather_state(ctx, state)  # collective: every rank
                 if chief:

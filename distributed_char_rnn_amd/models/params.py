@@ -36,6 +36,7 @@ import torch
 
 CELL_SCOPES = {"lstm": "lstm_cell", "gru": "gru_cell", "rnn": "basic_rnn_cell", "nas": "nas_cell"}
 ALIGN = 64
+SHARD_ALIGN = 64 * 64  # world sizes dividing 64 get 64-element-aligned shards
 
 
 @dataclass(frozen=True)
@@ -136,7 +137,9 @@ class ParamStore:
         # buffer so data-parallel all-reduce sums it with everything else for free; the
         # optimizer never updates it.
         self.norm_slot = last.offset + (last.numel + ALIGN - 1) // ALIGN * ALIGN
-        self.numel = self.norm_slot + ALIGN
+        # total size a multiple of SHARD_ALIGN: the sharded data-parallel optimizer
+        # (parallel/zero.py) splits the flat buffers into world equal, 64-element-aligned shards
+        self.numel = -(-(self.norm_slot + ALIGN) // SHARD_ALIGN) * SHARD_ALIGN
         self.device = torch.device(device)
         self.flat = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
         self.grad = torch.zeros_like(self.flat)

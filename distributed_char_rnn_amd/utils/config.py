@@ -70,7 +70,12 @@ def train_parser() -> argparse.ArgumentParser:
     g.add_argument("--bucket_mb", type=float, default=8.0,
                    help="gradient all-reduce bucket size in MB (data parallel)")
     g.add_argument("--allreduce_dtype", default="fp32", choices=["fp32", "bf16"],
-                   help="wire dtype of the gradient all-reduce")
+                   help="wire dtype of the gradient exchange (bf16 with --dp_mode sharded: "
+                        "fp32 accumulation on the receiving rank)")
+    g.add_argument("--dp_mode", default="replicated", choices=["replicated", "sharded"],
+                   help="replicated: bucketed all-reduce + every rank updates every parameter; "
+                        "sharded: reduce-scatter + clip/Adam on this rank's 1/world shard + "
+                        "all-gather (ZeRO stage 1, parallel/zero.py)")
     g.add_argument("--dist_backend", default="auto", choices=["auto", "nccl", "gloo"],
                    help="torch.distributed backend (nccl = RCCL on ROCm)")
     g.add_argument("--dist_timeout", type=float, default=600.0,

@@ -101,3 +101,41 @@ def test_spin_timeout_leaves_weights_unchanged(monkeypatch):
     assert torch.equal(opt2.m, m0) and torch.equal(opt2.v, v0)
     with pytest.raises(RuntimeError, match="timed out"):
         m2.check_errors()
+
+
+def test_rccl_one_rank_sharded_step_matches_replicated(monkeypatch):
+    """parallel/zero.py over a real 1-rank RCCL communicator (reduce-scatter, scalar
+    all-reduce, all-gather on the persistent-kernel headline path): the shard is the whole
+    buffer, so the update equals the plain fused clip + Adam step up to the norm's summation
+    order."""
+    from distributed_char_rnn_amd.parallel.zero import ShardedStep
+
+    monkeypatch.setenv("DCR_SPIN_LIMIT", str(1 << 22))
+    B, T = 256, 32
+    g = torch.Generator().manual_seed(1)
+    x = torch.randint(0, 65, (B, T), generator=g, dtype=torch.int32).cuda()
+    y = torch.randint(0, 65, (B, T), generator=g, dtype=torch.int32).cuda()
+    a = CharRNN(ModelConfig(**CFG), device="cuda", seed=3)
+    oa = TFAdam(a.store, clip=0.01, guard=a.error_word())
+    la, na = _steps(a, oa, None, x, y, 3)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0,
+                            world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        b = CharRNN(ModelConfig(**CFG), device="cuda", seed=3)
+        ob = TFAdam(b.store, clip=0.01, guard=b.error_word())
+        zs = ShardedStep(b.store, ob, 1, 0)
+        st = b.zero_state(B)
+        nb = []
+        for _ in range(3):
+            lb, st, _ = b.train_step(x, y, st)
+            nb.append(float(zs.step(2e-3)))
+        zs.gather_slots()
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+    b.check_errors()
+    assert na[0] > 0.01  # clipping active
+    assert abs(lb.item() - la) < 1e-6 * max(1.0, abs(la))
+    for u, v in zip(nb, na):
+        assert abs(u - v) < 1e-4 * v
+    assert ((b.store.flat - a.store.flat).norm() / a.store.flat.norm()).item() < 1e-5
