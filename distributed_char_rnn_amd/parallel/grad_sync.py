@@ -17,6 +17,11 @@ Bucket sizing (``--bucket_mb``): xGMI is point-to-point, 7 links x ~153 GB/s per
 ring all-reduce of S bytes on N GPUs moves 2(N-1)/N·S per link, so an 8 MB bucket is ~90 us of
 wire time on 8 GPUs -- large enough to amortise RCCL's per-call latency (~10-30 us), small
 enough that the first bucket starts while BPTT of the lower layers still has >=1 ms to run.
+
+``wire_dtype="bf16"`` halves the bytes without summing in bf16: each bucket's world chunks
+travel once through an all_to_all, every rank sums its chunk in fp32, and the sums return
+through an all_gather (one rounding of the final sum instead of one per ring hop).  The sharded
+alternative (reduce-scatter + optimizer on a 1/world shard) is parallel/zero.py.
 """
 from __future__ import annotations
 
@@ -71,9 +76,17 @@ class GradSync:
             lo, hi = self.buckets[self._next]
             g = self.store.grad[lo:hi]
             if self.wire_bf16:
-                wire = g.to(torch.bfloat16)
-                w = dist.all_reduce(wire, group=self.group, async_op=True)
-                self._work.append((w, lo, hi, wire))
+                # bf16 on the wire, fp32 accumulation: the bucket's world chunks travel once
+                # through an all_to_all, each rank sums its chunk in fp32, the sums come back
+                # through an all_gather (finish).  A bf16 all-reduce would round after every
+                # ring hop: N-1 roundings of partial sums at N ranks.
+                n = hi - lo
+                c = -(-n // self.world)
+                send = torch.zeros(self.world * c, dtype=torch.bfloat16, device=g.device)
+                send[:n].copy_(g)
+                recv = torch.empty_like(send)
+                w = dist.all_to_all_single(recv, send, group=self.group, async_op=True)
+                self._work.append((w, lo, hi, recv))
             else:
                 w = dist.all_reduce(g, group=self.group, async_op=True)
                 self._work.append((w, lo, hi, None))
@@ -87,10 +100,17 @@ class GradSync:
         if not self.enabled:
             return 1.0
         self.ready(None)
-        for w, lo, hi, wire in self._work:
+        gathers = []
+        for w, lo, hi, recv in self._work:
             w.wait()
-            if wire is not None:
-                self.store.grad[lo:hi].copy_(wire)
+            if recv is not None:  # bf16 wire: fp32 sum of my chunk, then gather every chunk
+                mine = recv.view(self.world, -1).float().sum(0).to(torch.bfloat16)
+                full = torch.empty_like(recv)
+                gw = dist.all_gather_into_tensor(full, mine, group=self.group, async_op=True)
+                gathers.append((gw, lo, hi, full))
+        for gw, lo, hi, full in gathers:
+            gw.wait()
+            self.store.grad[lo:hi].copy_(full[: hi - lo])
         self._work.clear()
         self._next = 0
         if defer_scale:

@@ -103,6 +103,30 @@ def test_dp_two_ranks_equals_single_process_double_batch(bucket_mb, wire, defer)
     assert all(np.isfinite(losses))
 
 
+@pytest.mark.parametrize("bucket_mb", [8.0, 0.0005])
+def test_dp_bf16_wire_fp32_accumulation(bucket_mb):
+    """--allreduce_dtype bf16: bucket chunks travel as bf16 (all_to_all + all_gather) and are
+    summed in fp32 -- the result stays within bf16 rounding of the fp32 exchange."""
+    B, T, steps, world = 3, 5, 3, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_worker,
+                         args=(r, world, port, B, T, steps, q, bucket_mb, "bf16", True))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    flat, losses, norms = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref, ref_norms = _single(B * world, T, steps)
+    init = CharRNN(ModelConfig(**CFG), device="cpu", seed=123).store.flat.numpy()
+    np.testing.assert_allclose(norms, ref_norms, rtol=1e-2)
+    d, dr = flat - init, ref - init
+    assert np.linalg.norm(d - dr) / np.linalg.norm(dr) < 2e-2
+
+
 def test_grad_sync_buckets_are_contiguous_and_cover_buffer():
     st = ParamStore(ModelConfig(model="lstm", vocab_size=65, rnn_size=512, num_layers=2))
     gs = GradSync(st, world_size=2, bucket_mb=4.0, enabled=False)
