@@ -13,7 +13,7 @@ int opt_num_partials(int64_t n);
 void launch_global_norm(const float* g, int64_t n, float* partials, float* norm_out,
                         hipStream_t stream);
 void launch_sumsq(const void* x, bool is_bf16, int64_t n, float* partials, float* out,
-                  hipStream_t stream);
+                  unsigned* ticket, hipStream_t stream);
 void launch_adam_clip(float* p, const float* g, float* m, float* v, bf16* pbf, int64_t n,
                       float* partials, float* norm_out, float lr_t, float b1, float b2, float eps,
                       float clip, float gscale, int64_t n_norm, const float* extra_sq,
@@ -277,17 +277,28 @@ int head_num_partials(int N, int cus);
 int launch_head(const HeadArgs& a, int cus, float* db_out, float* loss_out, hipStream_t s);
 
 // batched per-step data movement (prep.hip)
-enum PrepMode : int { PREP_COPY = 0, PREP_TRANSPOSE = 1, PREP_ZERO = 2 };
+enum PrepMode : int {
+  PREP_COPY = 0, PREP_TRANSPOSE = 1, PREP_ZERO = 2, PREP_SUM = 3, PREP_COLSUM = 4,
+  PREP_ONEHOT = 5, PREP_TABLE = 6
+};
+enum PrepKind : int { PREP_F32 = 0, PREP_BF16 = 1, PREP_RAW32 = 2 };  // destination element
 struct PrepTask {
-  const float* src;     // fp32 row-strided source (unused for ZERO)
-  void* dst;            // bf16 or fp32 (ZERO: any 4-byte element type)
-  int rows, cols;       // source shape (ZERO: destination shape)
+  const void* src;      // fp32 row-strided source (RAW32: any 32-bit; ONEHOT: int32 [B, T] ids)
+  void* dst;            // bf16 / fp32 / raw 32-bit (ZERO: any 4-byte element type)
+  const float* src2;    // TABLE: W [kdim, cols]
+  const float* aux;     // TABLE: bias [cols] (optional)
+  int rows, cols;       // source shape (ZERO, ONEHOT, SUM, TABLE: destination shape)
   int src_ld, dst_ld;   // row strides in elements
+  int src2_ld;          // TABLE: row stride of W
+  int slab;             // SUM: elements between consecutive slabs
+  int nslab;            // SUM: number of slabs
+  int kdim;             // TABLE: reduction length; ONEHOT: batch B
   int mode;             // PrepMode
-  int dst_bf16;         // 1: bf16 destination
+  int kind;             // PrepKind
+  int vec4;             // SUM: float4 path (all strides and pointers 16-B aligned)
   int tile0;            // first tile (set by launch_prep)
 };
-constexpr int kPrepMaxTasks = 48;
+constexpr int kPrepMaxTasks = 40;  // keeps the by-value table (kernel arguments) near 3 KB
 struct PrepTable {
   PrepTask t[kPrepMaxTasks];
   int n;

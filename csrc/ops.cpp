@@ -37,14 +37,21 @@ void global_norm(const at::Tensor& g, at::Tensor& partials, at::Tensor& norm_out
 }
 
 // out[0] = sum(x^2) with fp32 accumulation; x fp32 or bf16
-void sumsq(const at::Tensor& x, at::Tensor& partials, at::Tensor& out) {
+void sumsq(const at::Tensor& x, at::Tensor& partials, at::Tensor& out,
+           const c10::optional<at::Tensor>& ticket) {
   CHECK_DEV(x); CHECK_CONTIG(x); CHECK_ALIGN16(x);
   TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16,
               "sumsq: fp32 or bf16");
   CHECK_F32(partials); CHECK_F32(out);
   TORCH_CHECK(partials.numel() >= dcr::opt_num_partials(x.numel()), "partials too small");
+  unsigned* tk = nullptr;  // one-launch form: a zeroed int32 ticket counter owned by the caller
+  if (ticket.has_value() && ticket->defined()) {
+    CHECK_DEV(*ticket); CHECK_I32(*ticket);
+    TORCH_CHECK(ticket->numel() >= 1, "sumsq: ticket needs one int32");
+    tk = reinterpret_cast<unsigned*>(ticket->data_ptr());
+  }
   dcr::launch_sumsq(x.data_ptr(), x.scalar_type() == at::kBFloat16, x.numel(),
-                    ptr<float>(partials), ptr<float>(out), cur_stream());
+                    ptr<float>(partials), ptr<float>(out), tk, cur_stream());
 }
 
 void adam_clip(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
@@ -986,37 +993,95 @@ void head(const at::Tensor& O, const at::Tensor& WsT, const c10::optional<at::Te
 // ------------------------------------------------------------------------------------------
 // batched per-step data movement (prep.hip)
 // ------------------------------------------------------------------------------------------
-void prep(at::TensorList src, at::TensorList dst, at::IntArrayRef mode) {
+void prep(at::TensorList src, at::TensorList dst, at::IntArrayRef mode, at::TensorList extra) {
   TORCH_CHECK(src.size() == dst.size() && dst.size() == mode.size(), "prep: list lengths differ");
   TORCH_CHECK((int)dst.size() <= dcr::kPrepMaxTasks, "prep: too many tasks");
   dcr::PrepTable tab{};
   tab.n = (int)dst.size();
+  size_t xi = 0;  // next unused tensor of `extra` (TABLE: W, bias)
   auto ld = [](const at::Tensor& t) -> int {
     TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1, "prep: views must be 2-D with unit column stride");
     return (int)t.stride(0);
   };
+  auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   for (int i = 0; i < tab.n; ++i) {
     const at::Tensor& d = dst[i];
+    const at::Tensor& s = src[i];
     TORCH_CHECK(d.is_cuda(), "prep: destinations must be GPU tensors");
     dcr::PrepTask& T = tab.t[i];
     T.mode = (int)mode[i];
     T.dst = d.data_ptr();
-    T.dst_ld = ld(d);
-    if (T.mode == dcr::PREP_ZERO) {
-      TORCH_CHECK(d.element_size() == 4, "prep: ZERO needs 4-byte elements");
-      T.rows = (int)d.size(0);
-      T.cols = (int)d.size(1);
+    if (T.mode == dcr::PREP_COLSUM) {
+      // bias partials [R, cols] -> [cols]
+      TORCH_CHECK(s.is_cuda() && s.scalar_type() == at::kFloat && d.scalar_type() == at::kFloat,
+                  "prep COLSUM: fp32");
+      TORCH_CHECK(d.is_contiguous() && d.numel() == s.size(-1), "prep COLSUM: dst must be [cols]");
+      T.src = s.data_ptr();
+      T.src_ld = ld(s);
+      T.rows = (int)s.size(0);
+      T.cols = (int)s.size(1);
+      T.dst_ld = T.cols;
       continue;
     }
-    const at::Tensor& s = src[i];
-    TORCH_CHECK(s.is_cuda() && s.scalar_type() == at::kFloat, "prep: sources must be fp32 GPU tensors");
-    TORCH_CHECK(d.scalar_type() == at::kBFloat16 || d.scalar_type() == at::kFloat,
-                "prep: destinations must be bf16 or fp32");
-    T.src = s.data_ptr<float>();
+    T.dst_ld = ld(d);
+    T.rows = (int)d.size(0);
+    T.cols = (int)d.size(1);
+    if (T.mode == dcr::PREP_ZERO) {
+      TORCH_CHECK(d.element_size() == 4, "prep: ZERO needs 4-byte elements");
+      continue;
+    }
+    TORCH_CHECK(s.is_cuda(), "prep: sources must be GPU tensors");
+    T.src = s.data_ptr();
+    if (T.mode == dcr::PREP_SUM) {
+      // split-K slabs [S, rows, cols] -> [rows, cols]
+      TORCH_CHECK(s.scalar_type() == at::kFloat && d.scalar_type() == at::kFloat, "prep SUM: fp32");
+      TORCH_CHECK(s.dim() == 3 && s.stride(2) == 1 && s.size(1) == d.size(0) && s.size(2) == d.size(1),
+                  "prep SUM: src must be [S, rows, cols] over dst [rows, cols]");
+      TORCH_CHECK(s.stride(0) < (int64_t)1 << 31, "prep SUM: slab too large");
+      T.src_ld = (int)s.stride(1);
+      T.slab = (int)s.stride(0);
+      T.nslab = (int)s.size(0);
+      T.vec4 = (T.cols % 4 == 0 && T.src_ld % 4 == 0 && T.dst_ld % 4 == 0 && T.slab % 4 == 0 &&
+                a16(T.src) && a16(T.dst)) ? 1 : 0;
+      continue;
+    }
+    if (T.mode == dcr::PREP_ONEHOT) {
+      // batch-major ids [B, T] -> time-major one-hot rows [T*B, VP] (bf16)
+      TORCH_CHECK(s.scalar_type() == at::kInt && d.scalar_type() == at::kBFloat16, "prep ONEHOT: int32 -> bf16");
+      T.src_ld = ld(s);
+      T.kdim = (int)s.size(0);
+      TORCH_CHECK(s.size(0) * s.size(1) == d.size(0), "prep ONEHOT: dst rows must be B*T");
+      continue;
+    }
+    if (T.mode == dcr::PREP_TABLE) {
+      // E [rows, K] · W [K, cols] + bias [cols], fp32
+      TORCH_CHECK(xi + 2 <= extra.size(), "prep TABLE: needs W and bias in `extra`");
+      const at::Tensor& W = extra[xi];
+      const at::Tensor& bias = extra[xi + 1];
+      xi += 2;
+      TORCH_CHECK(s.scalar_type() == at::kFloat && W.scalar_type() == at::kFloat &&
+                  d.scalar_type() == at::kFloat && bias.scalar_type() == at::kFloat, "prep TABLE: fp32");
+      TORCH_CHECK(s.size(0) == d.size(0) && W.size(0) == s.size(1) && W.size(1) == d.size(1) &&
+                  bias.is_contiguous() && bias.numel() == d.size(1), "prep TABLE: shape mismatch");
+      T.src_ld = ld(s);
+      T.src2 = W.data_ptr<float>();
+      T.src2_ld = ld(W);
+      T.aux = bias.data_ptr<float>();
+      T.kdim = (int)s.size(1);
+      continue;
+    }
     T.src_ld = ld(s);
     T.rows = (int)s.size(0);
     T.cols = (int)s.size(1);
-    T.dst_bf16 = d.scalar_type() == at::kBFloat16 ? 1 : 0;
+    if (s.scalar_type() == at::kInt) {
+      TORCH_CHECK(d.scalar_type() == at::kInt, "prep: int32 sources copy to int32");
+      T.kind = dcr::PREP_RAW32;
+    } else {
+      TORCH_CHECK(s.scalar_type() == at::kFloat, "prep: sources must be fp32 or int32");
+      TORCH_CHECK(d.scalar_type() == at::kBFloat16 || d.scalar_type() == at::kFloat,
+                  "prep: destinations must be bf16 or fp32");
+      T.kind = d.scalar_type() == at::kBFloat16 ? dcr::PREP_BF16 : dcr::PREP_F32;
+    }
     if (T.mode == dcr::PREP_COPY) {
       TORCH_CHECK(d.size(0) == s.size(0) && d.size(1) == s.size(1), "prep: copy shape mismatch");
     } else if (T.mode == dcr::PREP_TRANSPOSE) {
@@ -1038,7 +1103,7 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor(e!) partials, Tensor(f!) norm_out, float lr_t, float b1, float b2, float eps, "
       "float clip, float gscale=1.0, int n_norm=-1, Tensor? extra_sq=None, "
       "Tensor? skip_if=None, Tensor? lr_dev=None) -> ()");
-  m.def("sumsq(Tensor x, Tensor(a!) partials, Tensor(b!) out) -> ()");
+  m.def("sumsq(Tensor x, Tensor(a!) partials, Tensor(b!) out, Tensor(c!)? ticket=None) -> ()");
   m.def(
       "lstm_step_ew_fwd(Tensor zrec, Tensor zx, Tensor? ids, Tensor cprev, Tensor(a!) hout, "
       "Tensor(b!)? hout32, Tensor(c!) cout, Tensor(d!) gates, float forget_bias) -> ()");
@@ -1102,7 +1167,8 @@ TORCH_LIBRARY(dcr, m) {
       "head(Tensor O, Tensor WsT, Tensor? Wsk, Tensor bias, Tensor? targets, float grad_scale, "
       "Tensor(a!)? logits, Tensor(b!)? row_loss, Tensor(c!)? dlogits, Tensor(d!)? dtop, "
       "Tensor(e!)? db, Tensor(f!) part, Tensor(g!)? loss) -> ()");
-  m.def("prep(Tensor[] src, Tensor(a!)[] dst, int[] mode) -> ()");
+  m.def("prep(Tensor[] src, Tensor(a!)[] dst, int[] mode, Tensor[] extra) -> ()");
+  m.def("prep_max_tasks() -> int", []() -> int64_t { return dcr::kPrepMaxTasks; });
   m.def("lstm2_plan(int H, int B, int force=0) -> int",
         [](int64_t H, int64_t B, int64_t force) -> int64_t {
           return dcr::lstm2_plan_g((int)H, (int)B, num_cus(), (int)force);

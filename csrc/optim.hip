@@ -134,6 +134,56 @@ __global__ void __launch_bounds__(kOptThreads) norm_only_kernel(const float* __r
   if (threadIdx.x == 0) out[0] = take_sqrt ? sqrtf(t) : t;
 }
 
+// sumsq_partials + the final sum in ONE launch: each block stores its partial, then takes a
+// ticket; the block that draws the last ticket sums all partials in block order (the same
+// fixed order as norm_only_kernel: bitwise equal results) and resets the ticket counter for
+// the next launch (it must start zeroed: a torch.zeros buffer owned by the caller).  The
+// cross-block hand-off is the sc1 form of the in-launch split-K recipe of
+// cdna_hip_programming.md ("Projection GEMM at M = 256", item 2): write-through partial stores
+// drained (vmcnt(0)) before the agent-scope ticket add, sc1 loads of them in the last block.
+// 256 blocks (not 1024): the tickets are same-address atomics.
+template <typename T>
+__global__ void __launch_bounds__(kOptThreads) sumsq_final_kernel(
+    const T* __restrict__ g, int64_t n, float* __restrict__ partials, unsigned* __restrict__ ticket,
+    float* __restrict__ out) {
+  __shared__ float red[kOptThreads / 64];
+  __shared__ unsigned last;
+  constexpr int kVec = 16 / (int)sizeof(T);
+  float acc = 0.f;
+  const int64_t nv = n / kVec;
+  // 4 vectors in flight per trip (a 256-block grid streams 32 MB: one load per trip would be
+  // latency-bound)
+  const int64_t stride = (int64_t)gridDim.x * kOptThreads;
+  int64_t i = blockIdx.x * (int64_t)kOptThreads + threadIdx.x;
+  for (; i + 3 * stride < nv; i += 4 * stride) {
+    const float a0 = sqv(g, i), a1 = sqv(g, i + stride), a2 = sqv(g, i + 2 * stride),
+                a3 = sqv(g, i + 3 * stride);
+    acc += (a0 + a1) + (a2 + a3);
+  }
+  for (; i < nv; i += stride) acc += sqv(g, i);
+  if (blockIdx.x == 0)
+    for (int64_t j = nv * kVec + threadIdx.x; j < n; j += kOptThreads) acc += sq1(g, j);
+  const float t = block_sum<kOptThreads>(acc, red);
+  if (threadIdx.x == 0) {
+    // write-through (sc1) partial store drained before the ticket: no release fence (an
+    // agent-scope release writes back the L2 -- per block, that made this launch 32 us)
+    __hip_atomic_store(partials + blockIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned k = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = k == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += kOptThreads)
+    s += __hip_atomic_load(partials + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const float total = block_sum<kOptThreads>(s, red);
+  if (threadIdx.x == 0) {
+    out[0] = total;
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 int opt_num_partials(int64_t n) {
   // 4 blocks per CU-ish cap; enough to stream a few-MB buffer at HBM rate.
   int64_t blocks = (n / 4 + kOptThreads - 1) / kOptThreads;
@@ -150,8 +200,18 @@ void launch_global_norm(const float* g, int64_t n, float* partials, float* norm_
 }
 
 void launch_sumsq(const void* x, bool is_bf16, int64_t n, float* partials, float* out,
-                  hipStream_t stream) {
+                  unsigned* ticket, hipStream_t stream) {
   const int nb = opt_num_partials(n);
+  if (ticket) {
+    const int nb = opt_num_partials(n) < 256 ? opt_num_partials(n) : 256;
+    if (is_bf16)
+      sumsq_final_kernel<bf16><<<nb, kOptThreads, 0, stream>>>(static_cast<const bf16*>(x), n,
+                                                                partials, ticket, out);
+    else
+      sumsq_final_kernel<float><<<nb, kOptThreads, 0, stream>>>(static_cast<const float*>(x), n,
+                                                                 partials, ticket, out);
+    return;
+  }
   if (is_bf16)
     sumsq_partials_kernel<bf16><<<nb, kOptThreads, 0, stream>>>(
         static_cast<const bf16*>(x), n, partials, nullptr);

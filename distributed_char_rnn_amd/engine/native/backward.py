@@ -6,20 +6,31 @@ from __future__ import annotations
 import torch
 
 from ...models.params import cell_specs
-from .gemm import f32, mm_into, mm_tn, put
+from .gemm import SumQueue, f32, mm_into, mm_tn, put
 from .layouts import SEG_LDS_MAX_V
 
 
 class BackwardMixin:
     def train_step(self, x, y, state, on_ready=None, want_extras: bool = False):
-        ids_tm = x.t().contiguous()
-        tgt = y.t().contiguous().view(-1)
-        T, B = ids_tm.shape
+        B, T = x.shape
         H, V, N, GW = self.H, self.V, T * B, self.GW
         wide = self._wide_xent(T * B)
+        # the batch's time-major ids (and the one-hot rows of the embedding-table gradient) are
+        # produced by the step's prep launch, not by separate transpose / scatter kernels
+        bufs0 = self._buffers(B, T, True)
+        ids_tm, tgt = bufs0["ids_tm"], bufs0["tgt_tm"].view(-1)
+        id_tasks = self._id_tasks(x, y, bufs0)
         bufs, O, logits, new_state = self._forward(ids_tm, state, True,
                                                    want_logits=not self.fused_head,
-                                                   logits_bias=not wide)
+                                                   logits_bias=not wide, extra_tasks=id_tasks)
+        # deferred slab / bias sums of this step: one prep launch per flush (gemm.SumQueue)
+        q = SumQueue(self.ops)
+        if on_ready is not None:
+            cb_user = on_ready
+
+            def on_ready(off, _cb=cb_user):  # noqa: F811 - sums complete before a bucket leaves
+                q.flush()
+                _cb(off)
         P = bufs["plan"]
         dlog = bufs["dlogits"]
         # the returned loss is read by the caller after the NEXT step was enqueued (trainer
@@ -33,7 +44,7 @@ class BackwardMixin:
                           logits if want_extras else None, bufs["row_loss"], dlog,
                           bufs["dtop"].view(N, H), s.gview("rnnlm/softmax_b"),
                           bufs["head_part"], loss_buf)
-            mm_tn(O, dlog, s.gview("rnnlm/softmax_w"))
+            mm_tn(O, dlog, s.gview("rnnlm/softmax_w"), q=q)
             dtop = bufs["dtop"].view(T, B, H)
         elif wide:
             # wide vocabulary: one-read CE (bias added in-kernel), d softmax_b fused (xent_wide)
@@ -42,12 +53,12 @@ class BackwardMixin:
                                loss_buf)
             if want_extras:
                 logits += hd["bs"]
-            mm_tn(O, dlog, s.gview("rnnlm/softmax_w"))
+            mm_tn(O, dlog, s.gview("rnnlm/softmax_w"), q=q)
             dtop = mm_into(dlog, hd["Ws"].t(), bufs["dtop"].view(N, H)).view(T, B, H)
         else:
             self.ops.xent(logits, tgt, 1.0 / N, bufs["row_loss"], dlog, bufs["xpart"], loss_buf)
             # ---- head gradients
-            mm_tn(O, dlog, s.gview("rnnlm/softmax_w"))
+            mm_tn(O, dlog, s.gview("rnnlm/softmax_w"), q=q)
             self.ops.segsum(dlog, None, 1, bufs["colsum"][:, :V], bufs["ws"], False)
             s.gview("rnnlm/softmax_b").copy_(bufs["colsum"][0, :V])
             dtop = mm_into(dlog, hd["Ws"].t(), bufs["dtop"].view(N, H)).view(T, B, H)
@@ -161,12 +172,12 @@ class BackwardMixin:
             # recurrent-weight gradients
             if self.cfg.model == "gru":
                 gk, gb, ck, cb = names
-                mm_tn(Hprev, dZ[:, : 2 * H], s.gview(gk)[H:])
-                mm_tn(lb.rh.view(N, H), dZ[:, 2 * H:], s.gview(ck)[H:])
+                mm_tn(Hprev, dZ[:, : 2 * H], s.gview(gk)[H:], q=q)
+                mm_tn(lb.rh.view(N, H), dZ[:, 2 * H:], s.gview(ck)[H:], q=q)
             elif self.cfg.model == "nas":
-                mm_tn(Hprev, dZ, s.gview(names[1]))
+                mm_tn(Hprev, dZ, s.gview(names[1]), q=q)
             else:
-                mm_tn(Hprev, dZ, s.gview(names[0])[H:])
+                mm_tn(Hprev, dZ, s.gview(names[0])[H:], q=q)
             if gather and V > SEG_LDS_MAX_V and not fused_dew:
                 # wide vocabulary: the [V, GW] dEW segment sum would be an atomic scatter of
                 # N x GW values plus two fp32 [V, GW] GEMMs; the dense route scatters N x H
@@ -184,9 +195,16 @@ class BackwardMixin:
                 self._embed_grad(dXf, ids_tm, bufs)
                 self._token_norm(dXf)
             elif gather:
-                dEW = self._dew(dZx, ids_tm, bufs, fused_dew)    # [V, GW] fp32
-                dWx = hd["E"].t() @ dEW                           # [H, GW] fp32
-                dbias = dEW.sum(0)
+                # the bias gradient from the BPTT kernel's partials: summed in the same flush
+                # as dEW's slabs (rather than a column sum of dEW after it)
+                part_bias = layer in bufs["pers_layers"] and self.cfg.model in ("lstm", "rnn")
+                if part_bias:
+                    dbias = self._bias_sum(self._db_part(bufs, layer), names, q)
+                dEW = self._dew(dZx, ids_tm, bufs, fused_dew, q)  # [V, GW] fp32 (flushes q)
+                dWx = (torch.mm(hd["E"].t(), dEW, out=s.gview(names[0])[:H])
+                       if self.cfg.model in ("lstm", "rnn") else hd["E"].t() @ dEW)  # [H, GW]
+                if not part_bias:
+                    dbias = dEW.sum(0)
                 # layer 0's own gradients are final here: report them before the embedding
                 # gradient and the token-norm GEMM, so that under data parallelism the
                 # layer-0 bucket's all-reduce overlaps that work and the last bucket is only
@@ -202,10 +220,10 @@ class BackwardMixin:
                     # + the sumsq kernel (66 us at the headline shape)
                     self._token_norm(torch.mm(dZx, lw.Wx.t()))
             else:
-                dWx = (mm_tn(lb.x_in, dZx, s.gview(names[0])[:H])
+                dWx = (mm_tn(lb.x_in, dZx, s.gview(names[0])[:H], q=q)
                        if self.cfg.model in ("lstm", "rnn") else mm_tn(lb.x_in, dZx))
                 if layer in bufs["pers_layers"]:
-                    dbias = self._bias_sum(self._db_part(bufs, layer), names)  # fused in BPTT
+                    dbias = self._bias_sum(self._db_part(bufs, layer), names, q)  # fused in BPTT
                 else:
                     self.ops.segsum(dZx, None, 1, bufs["colsum"][:, :GW], bufs["ws"], False)
                     dbias = bufs["colsum"][0, :GW]
@@ -237,6 +255,7 @@ class BackwardMixin:
                 self._join_side()
             if on_ready is not None:
                 on_ready(None if layer == 0 else s.layer_range(layer)[1])
+        q.flush()
         self._join_side()
         if pending:
             _release()
@@ -246,7 +265,21 @@ class BackwardMixin:
             self._poll_errors()
         return loss_buf[0], new_state, extras
 
-    def _dew(self, dZ0: torch.Tensor, ids_tm: torch.Tensor, bufs, fused: bool) -> torch.Tensor:
+    def _id_tasks(self, x: torch.Tensor, y: torch.Tensor, bufs) -> list:
+        """Prep tasks (csrc/prep.hip) of the batch: x, y [B, T] int32 -> time-major [T, B]
+        copies, and on the layer-0 gather route the bf16 one-hot rows [T*B, VP] of dEW's GEMM."""
+        if x.dim() != 2 or x.stride(1) != 1:
+            x = x.contiguous()
+        if y.dim() != 2 or y.stride(1) != 1:
+            y = y.contiguous()
+        tasks = [(x, bufs["ids_tm"], 1), (y, bufs["tgt_tm"], 1)]
+        if (bufs["onehot"] is not None and not self._dropout(True)
+                and self.cfg.model != "nas"):
+            tasks.append((x, bufs["onehot"], 5))
+        return tasks
+
+    def _dew(self, dZ0: torch.Tensor, ids_tm: torch.Tensor, bufs, fused: bool,
+             q: SumQueue) -> torch.Tensor:
         """Layer-0 embedding-table gradient dEW = onehot(ids)ᵀ·dZ0 [V, GW] (gather route: the
         forward read Zx0 = (E·W_x0 + b0)[ids]).  ``gemm`` (default): split-K MFMA library GEMM
         against an exact 0/1 one-hot matrix -- the same fp32 sums of the bf16 dZ values as a
@@ -256,25 +289,29 @@ class BackwardMixin:
         if fused:
             return bufs["dew_part"].sum(0)
         if self.dew_mode == "gemm" and bufs["onehot"] is not None:
-            oh = bufs["onehot"]
-            oh.zero_()
-            oh.scatter_(1, ids_tm.view(-1, 1).long(), 1.0)
-            return mm_tn(oh, dZ0)[:V]                 # rows >= V are zero padding
+            # the one-hot rows were written by this step's prep launch (_id_tasks)
+            mm_tn(bufs["onehot"], dZ0, bufs["dew"], q=q)
+            q.flush()
+            return bufs["dew"][:V]                    # rows >= V are zero padding
         dEW = torch.empty(V, self.GW, dtype=f32, device=self.dev)
         self.ops.segsum(dZ0, ids_tm.view(-1), V, dEW, bufs["ws"], False)
         return dEW
 
+    ERR_POLL_EVERY = 4
+
     def _poll_errors(self) -> None:
-        """Non-blocking check of the persistent kernels' error word: each step copies it into
-        pinned host memory behind its own work and reads the copy of an earlier step, so a
-        spin timeout raises within a step or two without a device sync.  (The optimizer skips
-        its update on device while the word is set: TFAdam(guard=err).)"""
+        """Non-blocking check of the persistent kernels' error word: every ERR_POLL_EVERY-th
+        step copies it into pinned host memory behind its own work (a ~5 us blit launch, so
+        not every step) and every step reads the latest copy, so a spin timeout raises within
+        a few steps without a device sync.  (The optimizer skips its update on device while
+        the word is set -- TFAdam(guard=err) -- so no step in between corrupts the weights.)"""
         if self._err_host is None:
             self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         v = int(self._err_host[0])
         if v:
             self.check_errors()
-        self._err_host.copy_(self.err, non_blocking=True)
+        if self._steps % self.ERR_POLL_EVERY == 1:
+            self._err_host.copy_(self.err, non_blocking=True)
 
     def _embed_grad(self, dX: torch.Tensor, ids_tm: torch.Tensor, bufs) -> None:
         """dE = segsum(dX_tok, ids) into the gradient buffer.  Wide vocabularies take the
@@ -297,7 +334,10 @@ class BackwardMixin:
         n = dx_tok.numel()
         if self._npart is None or self._npart.numel() < self.ops.opt_num_partials(n):
             self._npart = torch.empty(self.ops.opt_num_partials(n), dtype=f32, device=self.dev)
-        self.ops.sumsq(dx_tok.contiguous(), self._npart, self.store.norm_slot_view())
+            # ticket of the one-launch form (zeroed once; the kernel's last block resets it)
+            self._ntick = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.ops.sumsq(dx_tok.contiguous(), self._npart, self.store.norm_slot_view(),
+                       self._ntick)
 
     def _join_side(self) -> None:
         if self._side_used:

@@ -83,6 +83,11 @@ class BuffersMixin:
             onehot=(e(N, 8 * ((self.V + 7) // 8), dt=bf16)
                     if (training and self.V <= SEG_LDS_MAX_V and self.dew_mode == "gemm")
                     else None),
+            dew=(e(8 * ((self.V + 7) // 8), GW)
+                 if (training and self.V <= SEG_LDS_MAX_V and self.dew_mode == "gemm") else None),
+            # time-major ids / targets of the batch, written by the step's prep launch
+            ids_tm=torch.empty(T, B, dtype=torch.int32, device=dev) if training else None,
+            tgt_tm=torch.empty(T, B, dtype=torch.int32, device=dev) if training else None,
             colpart=(e(self.ops.xent_wide_waves(N) * self.V)
                      if (training and self._wide_xent(N)) else None),
             dtop=e(T, B, H) if training else None,
@@ -132,9 +137,12 @@ class BuffersMixin:
             return bufs["db_part"][layer][: P.pair_rows]
         return bufs["db_part"][layer][: max(bufs["layers"][0].hbuf.shape[1] // 16, 1)]
 
-    def _bias_sum(self, part: torch.Tensor, names) -> torch.Tensor:
+    def _bias_sum(self, part: torch.Tensor, names, q=None) -> torch.Tensor:
         """Sum the per-batch-group bias partials; for cells with one [GW] bias the sum is
-        written straight into its gradient slice (the later copy_ is then a no-op)."""
+        written straight into its gradient slice (the later copy_ is then a no-op), deferred
+        to the queue's next flush when one is given (gemm.SumQueue)."""
         if self.cfg.model in ("lstm", "rnn"):
+            if q is not None:
+                return q.add_colsum(part, self.store.gview(names[1]))
             return torch.sum(part, 0, out=self.store.gview(names[1]))
         return part.sum(0)

@@ -61,10 +61,11 @@ class ForwardMixin:
 
     # ------------------------------------------------------------------ forward
     def _forward(self, ids_tm: torch.Tensor, state, training: bool, want_logits: bool = True,
-                 logits_bias: bool = True):
+                 logits_bias: bool = True, extra_tasks: Optional[list] = None):
+        """``extra_tasks``: more prep tasks for the step's one prep launch (the batch's ids)."""
         T, B = ids_tm.shape
         H, N = self.H, T * B
-        tasks = self._prep()
+        tasks = self._prep() + list(extra_tasks or [])
         bufs = self._buffers(B, T, training)
         P = bufs["plan"]
         drop = self._dropout(training)

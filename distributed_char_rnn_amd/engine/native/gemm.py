@@ -49,13 +49,46 @@ def split_k(K: int, M: int, Nn: int) -> int:
     return S
 
 
+class SumQueue:
+    """Deferred reductions of one training step, executed together as ONE prep launch
+    (csrc/prep.hip SUM / COLSUM tasks) instead of one torch reduce kernel each (~5-10 us per
+    launch on MI355X, seven of them per headline step).  Entries: split-K slabs of the weight
+    GEMMs (``mm_tn(..., q=queue)``) and the persistent kernels' bias partials.  A destination
+    is valid only after :meth:`flush`; the backend flushes before it reads one and before it
+    reports a gradient range ready for the all-reduce."""
+
+    SUM, COLSUM = 3, 4
+
+    def __init__(self, ops):
+        self.ops = ops
+        self.tasks = []
+
+    def add_sum(self, part: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        self.tasks.append((part, out, self.SUM))
+        return out
+
+    def add_colsum(self, part: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        self.tasks.append((part, out, self.COLSUM))
+        return out
+
+    def flush(self) -> None:
+        if not self.tasks:
+            return
+        cap = int(self.ops.prep_max_tasks())
+        for i in range(0, len(self.tasks), cap):
+            chunk = self.tasks[i: i + cap]
+            self.ops.prep([t[0] for t in chunk], [t[1] for t in chunk], [t[2] for t in chunk], [])
+        self.tasks.clear()
+
+
 def mm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
-          split: bool = True) -> torch.Tensor:
+          split: bool = True, q: Optional[SumQueue] = None) -> torch.Tensor:
     """fp32 ``aᵀ·b`` for token-major bf16 operands ``a`` [K, M] and ``b`` [K, Nn] (weight
     gradients: K = T·B tokens), split-K over batched MFMA GEMMs + one fp32 sum when the output
     is too small to fill the chip.  ``split=False`` for GEMMs that run beside a persistent
     kernel on a side stream: there a chip-filling grid only steals the recurrence's CUs
-    (measured: 256-workgroup split-K beside BPTT stretched both)."""
+    (measured: 256-workgroup split-K beside BPTT stretched both).  With a queue ``q`` (and an
+    ``out``) the slab sum is deferred to ``q.flush()``."""
     K, M = a.shape
     Nn = b.shape[1]
     S = split_k(K, M, Nn) if split else 1
@@ -65,6 +98,8 @@ def mm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
                      out_dtype=f32)
     if out is None:
         return part.sum(0)
+    if q is not None and out.dim() == 2 and out.stride(1) == 1:
+        return q.add_sum(part, out)
     torch.sum(part, 0, out=out)
     return out
 

@@ -77,21 +77,35 @@ class LayoutsMixin:
 
     def _prep(self) -> list:
         """Prep-kernel tasks that refresh the weight layouts after a parameter change (empty
-        when the weights are current); the layer-0 ``E·W_x + b`` table is recomputed after
-        they ran (``_run_prep``)."""
+        when the weights are current).  The layer-0 ``E·W_x + b`` table: for LSTM / RNN with a
+        narrow vocabulary a TABLE task of the same launch (it reads only fp32 master weights;
+        first in the list, so its FMA-heavy tiles start first), otherwise recomputed after the
+        launch (``_run_prep``)."""
         ver = getattr(self.store, "version", 0)
         if not self._w:
             self._alloc_weights()
         elif self._wver == ver:
             return []
         self._wver = ver
-        self._table_dirty = True
-        return list(self._wtasks)
+        tasks = list(self._wtasks)
+        w0 = self._w[0]
+        if self.V <= SEG_LDS_MAX_V and self.cfg.model in ("lstm", "rnn"):
+            tab = self._head.get("table")
+            if tab is None or tab.shape != (self.V, w0.Wx32.shape[1]):
+                tab = self._head["table"] = torch.empty(self.V, w0.Wx32.shape[1], dtype=f32,
+                                                        device=self.dev)
+            tasks.insert(0, (self._head["E"], tab, 6, [w0.Wx32, w0.bias]))
+        else:
+            self._table_dirty = True
+        return tasks
 
     def _run_prep(self, tasks: list):
-        for i in range(0, len(tasks), 48):  # kPrepMaxTasks
-            chunk = tasks[i: i + 48]
-            self.ops.prep([t[0] for t in chunk], [t[1] for t in chunk], [t[2] for t in chunk])
+        cap = int(self.ops.prep_max_tasks())
+        for i in range(0, len(tasks), cap):
+            chunk = tasks[i: i + cap]
+            extra = [x for t in chunk if len(t) > 3 for x in t[3]]
+            self.ops.prep([t[0] for t in chunk], [t[1] for t in chunk], [t[2] for t in chunk],
+                          extra)
         if self._table_dirty:
             w0 = self._w[0]
             if self.V > SEG_LDS_MAX_V:

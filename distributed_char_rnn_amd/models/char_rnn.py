@@ -70,7 +70,10 @@ class CharRNN:
         is called as gradient ranges become final.  Returns (cost tensor, final_state,
         extras)."""
         xi, yi = _as_ids(x, self.device), _as_ids(y, self.device)
-        cb = grad_sync.ready if grad_sync is not None else None
+        # a disabled sync (one rank) gets no callback: the backend then defers its gradient
+        # sums to one launch at the end of the step instead of flushing per bucket
+        cb = (grad_sync.ready if grad_sync is not None and getattr(grad_sync, "enabled", True)
+              else None)
         return self.backend.train_step(xi, yi, state, cb, want_extras=want_extras)
 
     def step_logits(self, x_t, state: State):

@@ -80,6 +80,18 @@ def test_sumsq_kernel(dcr_ops, dtype, n):
     dcr_ops.sumsq(x, parts, out)
     torch.cuda.synchronize()
     assert out.item() == pytest.approx(float((x.double() ** 2).sum()), rel=1e-5)
+    # one-launch form (last block sums the partials): same value, bitwise reproducible, ticket
+    # left at zero, reusable launch after launch
+    tick = torch.zeros(1, dtype=torch.int32, device="cuda")
+    first = None
+    for _ in range(3):
+        out1 = torch.empty(1, device="cuda")
+        dcr_ops.sumsq(x, parts, out1, tick)
+        torch.cuda.synchronize()
+        assert out1.item() == pytest.approx(float((x.double() ** 2).sum()), rel=1e-5)
+        first = out1 if first is None else first
+        assert torch.equal(out1, first)
+        assert int(tick.item()) == 0
 
 
 @pytest.mark.parametrize("world", [2, 8])

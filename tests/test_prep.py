@@ -18,7 +18,7 @@ def test_prep_copy_transpose_zero(dcr_ops):
     dst_t = torch.empty(2048, 300, dtype=torch.bfloat16, device="cuda")
     dcr_ops.prep([src_a, src_b, src_b, src_b, cnt, src_a],
                  [dst_a, dst_b[:65], dst_c, pad[:, :65], cnt, dst_t],
-                 [0, 1, 0, 0, 2, 1])
+                 [0, 1, 0, 0, 2, 1], [])
     torch.cuda.synchronize()
     assert torch.equal(dst_a, src_a.to(torch.bfloat16))
     assert torch.equal(dst_b[:65], src_b.t().to(torch.bfloat16))
@@ -33,4 +33,47 @@ def test_prep_copy_transpose_zero(dcr_ops):
 def test_prep_rejects_bad_shapes(dcr_ops):
     a = torch.randn(4, 8, device="cuda")
     with pytest.raises(RuntimeError):
-        dcr_ops.prep([a], [torch.empty(4, 8, dtype=torch.bfloat16, device="cuda")], [1])
+        dcr_ops.prep([a], [torch.empty(4, 8, dtype=torch.bfloat16, device="cuda")], [1], [])
+
+
+def test_prep_sum_colsum_onehot_table_raw(dcr_ops):
+    """The tail-collapse modes: split-K slab sums (vector and scalar paths), bias column sums,
+    time-major one-hot rows, the fp32 E·W + b table and raw int32 transposes -- one launch,
+    against fp32 PyTorch (sums in the kernel's fixed order are checked to fp32 rounding)."""
+    torch.manual_seed(1)
+    dev = "cuda"
+    part = torch.randn(8, 96, 2048, device=dev)               # float4 path
+    part_s = torch.randn(16, 70, 65, device=dev)              # scalar path (65 columns)
+    big = torch.zeros(2 * 96, 2048, device=dev)
+    out = big[96:]                                           # a row block of a larger buffer
+    out_s = torch.empty(70, 65, device=dev)
+    dbp = torch.randn(16, 2048, device=dev)
+    db = torch.empty(2048, device=dev)
+    B, T, VP = 48, 37, 72
+    idsrc = torch.randint(0, 65, (B, 3 * T), dtype=torch.int32, device=dev)
+    x = idsrc[:, T:2 * T]                                    # row-strided [B, T] view
+    oh = torch.full((T * B, VP), 5.0, dtype=torch.bfloat16, device=dev)
+    x_tm = torch.empty(T, B, dtype=torch.int32, device=dev)
+    E = torch.randn(65, 512, device=dev)
+    W = torch.randn(512, 2048, device=dev)
+    bias = torch.randn(2048, device=dev)
+    tab = torch.empty(65, 2048, device=dev)
+    dcr_ops.prep([E, part, part_s, dbp, x, x],
+                 [tab, out, out_s, db, oh, x_tm],
+                 [6, 3, 3, 4, 5, 1], [W, bias])
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out, part.sum(0), rtol=1e-6, atol=1e-5)
+    assert torch.count_nonzero(big[:96]) == 0
+    torch.testing.assert_close(out_s, part_s.sum(0), rtol=1e-6, atol=1e-5)
+    torch.testing.assert_close(db, dbp.sum(0), rtol=1e-6, atol=1e-5)
+    ref_oh = torch.nn.functional.one_hot(x.t().reshape(-1).long(), VP).to(torch.bfloat16)
+    assert torch.equal(oh, ref_oh)
+    assert torch.equal(x_tm, x.t())
+    ref_tab = (E.double() @ W.double() + bias.double()).float()
+    torch.testing.assert_close(tab, ref_tab, rtol=1e-5, atol=1e-3)
+    # bitwise reproducible: the same launch again gives the same bits
+    out2 = torch.empty_like(out)
+    tab2 = torch.empty_like(tab)
+    dcr_ops.prep([E, part], [tab2, out2], [6, 3], [W, bias])
+    torch.cuda.synchronize()
+    assert torch.equal(out2, out) and torch.equal(tab2, tab)
