@@ -46,10 +46,18 @@ class GradSync:
         self._work: List[Tuple[object, int, int, Optional[torch.Tensor]]] = []
 
     def _make_buckets(self, bucket_mb: float) -> List[Tuple[int, int]]:
-        """Cut the flat buffer at tensor boundaries into ~bucket_mb slices."""
+        """Cut the flat buffer at tensor boundaries into ~bucket_mb slices.  The last tensor
+        (the embedding, plus the clip-norm slot behind it) always forms its own final bucket:
+        it is the last gradient the backward finalises (after the layer-0 weight gradients, the
+        embedding GEMM and the token-norm GEMM), so only its few hundred KB -- not a whole
+        layer's ~8 MB -- are all-reduced after the backward with nothing left to overlap."""
         cap = max(1, int(bucket_mb * (1 << 20) / 4))
         cuts, lo, cur = [], 0, 0
-        for s in self.store.specs:
+        specs = self.store.specs
+        for i, s in enumerate(specs):
+            if i == len(specs) - 1 and len(specs) > 1 and cur > lo:
+                cuts.append((lo, cur))  # close the bucket before the final tensor
+                lo = cur
             end = s.offset + s.numel
             cur = end
             if cur - lo >= cap:
@@ -57,6 +65,15 @@ class GradSync:
                 lo = cur
         if cur > lo:
             cuts.append((lo, cur))
+        # a sliver left before the final bucket (a bias) joins its predecessor: one RCCL call
+        # fewer, and it is final no later than the predecessor's last tensor
+        merged = []
+        for i, (a, b) in enumerate(cuts):
+            if merged and i < len(cuts) - 1 and b - a < cap // 16:
+                merged[-1] = (merged[-1][0], b)
+            else:
+                merged.append((a, b))
+        cuts = merged
         # the flat buffer may have alignment padding at the end: cover it in the last bucket
         if cuts:
             cuts[-1] = (cuts[-1][0], self.store.numel)
