@@ -83,8 +83,8 @@ __global__ void __launch_bounds__(256) prep_kernel(PrepTable tab) {
         const float* p[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          // rows past the tile end re-read the tile's first row (never stored)
-          const int r = rr + 16 * i < r1 ? rr + 16 * i : rr;
+          // rows past the tile end re-read the tile's first row r0 (< r1; never stored)
+          const int r = rr + 16 * i < r1 ? rr + 16 * i : r0;
           p[i] = src + (size_t)r * T.src_ld + c;
           acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         }

@@ -3,7 +3,7 @@
 set -o pipefail
 run() {
   local name="$1"; shift
-  timeout -k 10 300 python bench.py "$@" 2>/dev/null | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$name', 'ms/step=%.3f' % d['ms_per_step'], 'chars/s=%.3fM' % (d['value']/1e6), 'loss=%.3f' % d['final_loss'])"
+  timeout -k 10 400 python bench.py "$@" 2>/dev/null | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$name', 'ms/step=%.3f' % d['ms_per_step'], 'chars/s=%.3fM' % (d['value']/1e6), 'loss=%.3f' % d['final_loss'])"
 }
 run "lstm512x2 seq128 B256 (headline)" --steps 40 --warmup 5 || exit 1
 run "lstm512x2 seq128 B256 (repeat)  " --steps 40 --warmup 5 || exit 1

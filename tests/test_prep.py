@@ -42,10 +42,10 @@ def test_prep_sum_colsum_onehot_table_raw(dcr_ops):
     against fp32 PyTorch (sums in the kernel's fixed order are checked to fp32 rounding)."""
     torch.manual_seed(1)
     dev = "cuda"
-    part = torch.randn(8, 96, 2048, device=dev)               # float4 path
+    part = torch.randn(8, 72, 2048, device=dev)               # float4 path (partial tile)
     part_s = torch.randn(16, 70, 65, device=dev)              # scalar path (65 columns)
-    big = torch.zeros(2 * 96, 2048, device=dev)
-    out = big[96:]                                           # a row block of a larger buffer
+    big = torch.zeros(2 * 72, 2048, device=dev)
+    out = big[72:]                                           # a row block of a larger buffer
     out_s = torch.empty(70, 65, device=dev)
     dbp = torch.randn(16, 2048, device=dev)
     db = torch.empty(2048, device=dev)
@@ -63,7 +63,7 @@ def test_prep_sum_colsum_onehot_table_raw(dcr_ops):
                  [6, 3, 3, 4, 5, 1], [W, bias])
     torch.cuda.synchronize()
     torch.testing.assert_close(out, part.sum(0), rtol=1e-6, atol=1e-5)
-    assert torch.count_nonzero(big[:96]) == 0
+    assert torch.count_nonzero(big[:72]) == 0
     torch.testing.assert_close(out_s, part_s.sum(0), rtol=1e-6, atol=1e-5)
     torch.testing.assert_close(db, dbp.sum(0), rtol=1e-6, atol=1e-5)
     ref_oh = torch.nn.functional.one_hot(x.t().reshape(-1).long(), VP).to(torch.bfloat16)
