@@ -16,7 +16,12 @@
 // owns UB*16 hidden units x 16 batch rows; its 4 waves split K in quarters and keep
 //   fwd: W_gᵀ rows (r and u gates of its units, K = H) and W_cᵀ rows (K = H)
 //   bwd: W_c rows (d(r⊙h) = dZc·W_cᵀ, K = H) and W_g rows (dh = dZg·W_gᵀ, K = 2H)
-// Wave w < UB runs the cell epilogue of unit block w with h_{t-1} / the dh carry in registers.
+// NT > 1 batch tiles per workgroup (batch group = NT*16 rows) reuse the resident weights for
+// NT x the MFMA work per hand-off: the recurrence is hand-off-latency bound (MFMA mostly idle),
+// so a larger batch runs at nearly the same tick time instead of falling off the persistent path
+// (B = 256 at H = 1024 needs NT = 2 to stay within one 256-workgroup co-resident grid).
+// Wave w < UB*NT runs the cell epilogue of unit block w % UB, batch tile w / UB, with h_{t-1} /
+// the dh carry in registers.
 // Counters: two sets per launch (phase A and phase B), one per (batch group, step, K quarter).
 #include "common.h"
 #include "kernels.h"
@@ -29,22 +34,22 @@ namespace dcr {
 // ------------------------------------------------------------------------------------------
 // forward
 // ------------------------------------------------------------------------------------------
-template <int KS, int UB>
+template <int KS, int UB, int NT>
 __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs a) {
   // single-buffered partials: every write of partA (partB) is separated from the previous
   // epilogue read by the phase-B (next phase-A) barrier, which the epilogue wave joins last
-  __shared__ __attribute__((aligned(16))) float partA[4][UB][64][8];
-  __shared__ __attribute__((aligned(16))) float partB[4][UB][64][4];
+  __shared__ __attribute__((aligned(16))) float partA[4][NT][UB][64][8];
+  __shared__ __attribute__((aligned(16))) float partB[4][NT][UB][64][4];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
   const int nwg_u = H / (16 * UB);
   int ubk, bg;
-  map_block(blockIdx.x, nwg_u, B / 16, ubk, bg);
-  const int ub0 = ubk * 16 * UB, b0 = bg * 16;
+  map_block(blockIdx.x, nwg_u, B / (16 * NT), ubk, bg);
+  const int ub0 = ubk * 16 * UB, b0 = bg * 16 * NT;
   const int kq = 8 * (lane >> 4);
   const int kbase = w * (KS * 32);
-  const size_t cset = (size_t)(B / 16) * (T + 1) * 4;
+  const size_t cset = (size_t)(B / (16 * NT)) * (T + 1) * 4;
   unsigned* cntH = a.cnt + (size_t)bg * (T + 1) * 4;         // slot t: h_t published
   unsigned* cntR = a.cnt + cset + (size_t)bg * (T + 1) * 4;  // slot t: r⊙h_{t-1} published
   const unsigned target = (unsigned)(H / (64 * UB));  // workgroups per K-quarter shard
@@ -65,10 +70,14 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
       wc[ui][s] = ld8(a.WcT + (size_t)row * H + kbase + s * 32 + kq);
     }
 
-  const int b = b0 + (lane & 15);
-  const unsigned hoff = (unsigned)(((size_t)b * H + kbase + kq) * sizeof(bf16));
-  const bool epi = w < UB;
-  const int u0 = ub0 + (epi ? w : 0) * 16 + 4 * (lane >> 4);
+  // MFMA operands: batch tile n's row-major offset (rows b0 + 16n + lane%16) / ring tile
+  const unsigned hoff = (unsigned)(((size_t)(b0 + (lane & 15)) * H + kbase + kq) * sizeof(bf16));
+  const unsigned tile_off = (unsigned)(16 * H * sizeof(bf16));  // + n * tile_off
+  // epilogue role: unit block w % UB of batch tile w / UB
+  const bool epi = w < UB * NT;
+  const int eu = epi ? w % UB : 0, en = epi ? w / UB : 0;
+  const int b = b0 + 16 * en + (lane & 15);
+  const int u0 = ub0 + eu * 16 + 4 * (lane >> 4);
   const size_t bh = (size_t)b * H + u0;
   const int G3 = 3 * H;
   float hp[4] = {0.f, 0.f, 0.f, 0.f};
@@ -93,22 +102,27 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
       const __amdgpu_buffer_rsrc_t src =
           fr ? make_rsrc(a.ring0 + (size_t)(t & 1) * B * H, sizeof(bf16) * (size_t)B * H)
              : make_rsrc(a.hbuf + (size_t)t * B * H, sizeof(bf16) * (size_t)B * H);
-      bf16x8 hf[KS];
+      bf16x8 hf[NT][KS];
 #pragma unroll
-      for (int s = 0; s < KS; ++s)
-        hf[s] = ld8_sc1(src, fr ? frag_load_off(bg, w * KS + s, H, lane) : hoff + s * 64);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int ui = 0; ui < UB; ++ui) {
-        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      for (int n = 0; n < NT; ++n)
 #pragma unroll
         for (int s = 0; s < KS; ++s)
+          hf[n][s] = ld8_sc1(src, fr ? frag_load_off(bg * NT + n, w * KS + s, H, lane)
+                                     : hoff + n * tile_off + s * 64);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int g = 0; g < 2; ++g) acc[g] = mfma16(wg[ui][g][s], hf[s], acc[g]);
-        float4* dst = reinterpret_cast<float4*>(&partA[w][ui][lane][0]);
-        dst[0] = make_float4(acc[0][0], acc[0][1], acc[0][2], acc[0][3]);
-        dst[1] = make_float4(acc[1][0], acc[1][1], acc[1][2], acc[1][3]);
-      }
+      for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int ui = 0; ui < UB; ++ui) {
+          f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+          for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int g = 0; g < 2; ++g) acc[g] = mfma16(wg[ui][g][s], hf[n][s], acc[g]);
+          float4* dst = reinterpret_cast<float4*>(&partA[w][n][ui][lane][0]);
+          dst[0] = make_float4(acc[0][0], acc[0][1], acc[0][2], acc[0][3]);
+          dst[1] = make_float4(acc[1][0], acc[1][1], acc[1][2], acc[1][3]);
+        }
     }
     __syncthreads();
     float uu[4];
@@ -116,10 +130,10 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
       float rr[4];
 #pragma unroll
       for (int g = 0; g < 2; ++g) {
-        const float4 s0 = reinterpret_cast<const float4*>(&partA[0][w][lane][0])[g];
-        const float4 s1 = reinterpret_cast<const float4*>(&partA[1][w][lane][0])[g];
-        const float4 s2 = reinterpret_cast<const float4*>(&partA[2][w][lane][0])[g];
-        const float4 s3 = reinterpret_cast<const float4*>(&partA[3][w][lane][0])[g];
+        const float4 s0 = reinterpret_cast<const float4*>(&partA[0][en][eu][lane][0])[g];
+        const float4 s1 = reinterpret_cast<const float4*>(&partA[1][en][eu][lane][0])[g];
+        const float4 s2 = reinterpret_cast<const float4*>(&partA[2][en][eu][lane][0])[g];
+        const float4 s3 = reinterpret_cast<const float4*>(&partA[3][en][eu][lane][0])[g];
         float* o = g == 0 ? rr : uu;
         o[0] = sigmoidf_(s0.x + s1.x + s2.x + s3.x + zx[g][0]);
         o[1] = sigmoidf_(s0.y + s1.y + s2.y + s3.y + zx[g][1]);
@@ -133,7 +147,7 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
         st4bf_sc1(a.rh + (size_t)t * B * H + bh, rh0, rh1, rh2, rh3);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0)
-        wg_arrive(&wg_cnt[0], UB, cntR + (size_t)t * 4 + (u0 / (H / 4)));
+        wg_arrive(&wg_cnt[0], UB * NT, cntR + (size_t)t * 4 + (u0 / (H / 4)));
       if (a.ring1) st4bf(a.rh + (size_t)t * B * H + bh, rh0, rh1, rh2, rh3);
       bf16* gp = a.gates + ((size_t)t * B + b) * G3 + u0;
       st4bf(gp, rr[0], rr[1], rr[2], rr[3]);
@@ -147,26 +161,31 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
       const __amdgpu_buffer_rsrc_t src =
           a.ring1 ? make_rsrc(a.ring1 + (size_t)(t & 1) * B * H, sizeof(bf16) * (size_t)B * H)
                   : make_rsrc(a.rh + (size_t)t * B * H, sizeof(bf16) * (size_t)B * H);
-      bf16x8 rf[KS];
+      bf16x8 rf[NT][KS];
 #pragma unroll
-      for (int s = 0; s < KS; ++s)
-        rf[s] = ld8_sc1(src, a.ring1 ? frag_load_off(bg, w * KS + s, H, lane) : hoff + s * 64);
+      for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+          rf[n][s] = ld8_sc1(src, a.ring1 ? frag_load_off(bg * NT + n, w * KS + s, H, lane)
+                                          : hoff + n * tile_off + s * 64);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int ui = 0; ui < UB; ++ui) {
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int n = 0; n < NT; ++n)
 #pragma unroll
-        for (int s = 0; s < KS; ++s) acc = mfma16(wc[ui][s], rf[s], acc);
-        *reinterpret_cast<float4*>(&partB[w][ui][lane][0]) =
-            make_float4(acc[0], acc[1], acc[2], acc[3]);
-      }
+        for (int ui = 0; ui < UB; ++ui) {
+          f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < KS; ++s) acc = mfma16(wc[ui][s], rf[n][s], acc);
+          *reinterpret_cast<float4*>(&partB[w][n][ui][lane][0]) =
+              make_float4(acc[0], acc[1], acc[2], acc[3]);
+        }
     }
     __syncthreads();
     if (epi) {
-      const float4 s0 = *reinterpret_cast<const float4*>(&partB[0][w][lane][0]);
-      const float4 s1 = *reinterpret_cast<const float4*>(&partB[1][w][lane][0]);
-      const float4 s2 = *reinterpret_cast<const float4*>(&partB[2][w][lane][0]);
-      const float4 s3 = *reinterpret_cast<const float4*>(&partB[3][w][lane][0]);
+      const float4 s0 = *reinterpret_cast<const float4*>(&partB[0][en][eu][lane][0]);
+      const float4 s1 = *reinterpret_cast<const float4*>(&partB[1][en][eu][lane][0]);
+      const float4 s2 = *reinterpret_cast<const float4*>(&partB[2][en][eu][lane][0]);
+      const float4 s3 = *reinterpret_cast<const float4*>(&partB[3][en][eu][lane][0]);
       float cc[4], h[4];
       cc[0] = tanhf_(s0.x + s1.x + s2.x + s3.x + zx[2][0]);
       cc[1] = tanhf_(s0.y + s1.y + s2.y + s3.y + zx[2][1]);
@@ -183,7 +202,7 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
       if (t + 1 < T) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0)
-          wg_arrive(&wg_cnt[1], UB, cntH + (size_t)(t + 1) * 4 + (u0 / (H / 4)));
+          wg_arrive(&wg_cnt[1], UB * NT, cntH + (size_t)(t + 1) * 4 + (u0 / (H / 4)));
       }
       if (a.ring0) st4bf(a.hbuf + o, h[0], h[1], h[2], h[3]);
       *reinterpret_cast<float4*>(a.h32 + o) = make_float4(h[0], h[1], h[2], h[3]);
@@ -202,21 +221,21 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
 //   phase B (t -> t-1): dh'_{t-1} = dtop_{t-1} + P + dZg_t · W_gᵀ;  dZc_{t-1}
 // dh' and P never leave the epilogue lane's registers.
 // ------------------------------------------------------------------------------------------
-template <int KA, int UB>
+template <int KA, int UB, int NT>
 __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs a) {
   constexpr int KB = 2 * KA;  // phase B reduces over K = 2H
-  __shared__ __attribute__((aligned(16))) float partA[4][UB][64][4];
-  __shared__ __attribute__((aligned(16))) float partB[4][UB][64][4];
+  __shared__ __attribute__((aligned(16))) float partA[4][NT][UB][64][4];
+  __shared__ __attribute__((aligned(16))) float partB[4][NT][UB][64][4];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
   const int nwg_u = H / (16 * UB);
   int ubk, bg;
-  map_block(blockIdx.x, nwg_u, B / 16, ubk, bg);
-  const int ub0 = ubk * 16 * UB, b0 = bg * 16;
+  map_block(blockIdx.x, nwg_u, B / (16 * NT), ubk, bg);
+  const int ub0 = ubk * 16 * UB, b0 = bg * 16 * NT;
   const int kq = 8 * (lane >> 4);
   const int kA = w * (KA * 32), kB = w * (KB * 32);
-  const size_t cset = (size_t)(B / 16) * (T + 1) * 4;
+  const size_t cset = (size_t)(B / (16 * NT)) * (T + 1) * 4;
   unsigned* cntC = a.cnt + (size_t)bg * (T + 1) * 4;         // slot t: dZc_t published
   unsigned* cntG = a.cnt + cset + (size_t)bg * (T + 1) * 4;  // slot t: dZg_t published
   const unsigned target = (unsigned)(H / (64 * UB));  // workgroups per K-quarter shard
@@ -236,12 +255,17 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
     for (int s = 0; s < KB; ++s) wg[ui][s] = ld8(a.Wg + (size_t)row * 2 * H + kB + s * 32 + kq);
   }
 
-  const int b = b0 + (lane & 15);
-  const bool epi = w < UB;
-  const int u0 = ub0 + (epi ? w : 0) * 16 + 4 * (lane >> 4);
+  // epilogue role: unit block w % UB of batch tile w / UB
+  const bool epi = w < UB * NT;
+  const int eu = epi ? w % UB : 0, en = epi ? w / UB : 0;
+  const int b = b0 + 16 * en + (lane & 15);
+  const int u0 = ub0 + eu * 16 + 4 * (lane >> 4);
   const size_t bh = (size_t)b * H + u0;
-  const unsigned offA = (unsigned)(((size_t)b * G3 + 2 * H + kA + kq) * sizeof(bf16));
-  const unsigned offB = (unsigned)(((size_t)b * G3 + kB + kq) * sizeof(bf16));
+  // MFMA operands (row-major dZ path): batch tile n at + n * tile_off
+  const int bm = b0 + (lane & 15);
+  const unsigned offA = (unsigned)(((size_t)bm * G3 + 2 * H + kA + kq) * sizeof(bf16));
+  const unsigned offB = (unsigned)(((size_t)bm * G3 + kB + kq) * sizeof(bf16));
+  const unsigned tile_off = (unsigned)(16 * G3 * sizeof(bf16));
   float dhp[4] = {0.f, 0.f, 0.f, 0.f};
 
   // dZc_{T-1} from the top gradient alone
@@ -261,7 +285,7 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
       st4bf_sc1(zrow, z0[0], z0[1], z0[2], z0[3]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0)
-      wg_arrive(&wg_cnt[1], UB, cntC + (size_t)(T - 1) * 4 + (u0 / (H / 4)));
+      wg_arrive(&wg_cnt[1], UB * NT, cntC + (size_t)(T - 1) * 4 + (u0 / (H / 4)));
     if (a.ring0) st4bf(zrow, z0[0], z0[1], z0[2], z0[3]);
   }
 
@@ -285,33 +309,40 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
       dead = !poll_shards4(cntC + (size_t)t * 4, target, a.spin_limit, a.err, 7u);
     __syncthreads();
     {
-      bf16x8 zf[KA];
+      bf16x8 zf[NT][KA];
       if (a.ring0) {
         const __amdgpu_buffer_rsrc_t rc =
             make_rsrc(a.ring0 + (size_t)(t & 1) * B * H, sizeof(bf16) * (size_t)B * H);
 #pragma unroll
-        for (int s = 0; s < KA; ++s) zf[s] = ld8_sc1(rc, frag_load_off(bg, w * KA + s, H, lane));
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+          for (int s = 0; s < KA; ++s)
+            zf[n][s] = ld8_sc1(rc, frag_load_off(bg * NT + n, w * KA + s, H, lane));
       } else {
 #pragma unroll
-        for (int s = 0; s < KA; ++s) zf[s] = ld8_sc1(zsrc, offA + s * 64);
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+          for (int s = 0; s < KA; ++s) zf[n][s] = ld8_sc1(zsrc, offA + n * tile_off + s * 64);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int ui = 0; ui < UB; ++ui) {
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int n = 0; n < NT; ++n)
 #pragma unroll
-        for (int s = 0; s < KA; ++s) acc = mfma16(wc[ui][s], zf[s], acc);
-        *reinterpret_cast<float4*>(&partA[w][ui][lane][0]) =
-            make_float4(acc[0], acc[1], acc[2], acc[3]);
-      }
+        for (int ui = 0; ui < UB; ++ui) {
+          f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < KA; ++s) acc = mfma16(wc[ui][s], zf[n][s], acc);
+          *reinterpret_cast<float4*>(&partA[w][n][ui][lane][0]) =
+              make_float4(acc[0], acc[1], acc[2], acc[3]);
+        }
     }
     __syncthreads();
     float P[4];
     if (epi) {
-      const float4 s0 = *reinterpret_cast<const float4*>(&partA[0][w][lane][0]);
-      const float4 s1 = *reinterpret_cast<const float4*>(&partA[1][w][lane][0]);
-      const float4 s2 = *reinterpret_cast<const float4*>(&partA[2][w][lane][0]);
-      const float4 s3 = *reinterpret_cast<const float4*>(&partA[3][w][lane][0]);
+      const float4 s0 = *reinterpret_cast<const float4*>(&partA[0][en][eu][lane][0]);
+      const float4 s1 = *reinterpret_cast<const float4*>(&partA[1][en][eu][lane][0]);
+      const float4 s2 = *reinterpret_cast<const float4*>(&partA[2][en][eu][lane][0]);
+      const float4 s3 = *reinterpret_cast<const float4*>(&partA[3][en][eu][lane][0]);
       const float drh[4] = {s0.x + s1.x + s2.x + s3.x, s0.y + s1.y + s2.y + s3.y,
                             s0.z + s1.z + s2.z + s3.z, s0.w + s1.w + s2.w + s3.w};
       float dzr[4], dzu[4];
@@ -334,7 +365,7 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
       if (t > 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0)
-          wg_arrive(&wg_cnt[0], UB, cntG + (size_t)t * 4 + (u0 / (H / 4)));
+          wg_arrive(&wg_cnt[0], UB * NT, cntG + (size_t)t * 4 + (u0 / (H / 4)));
       }
       if (a.ring1) {
         st4bf(dz, dzr[0], dzr[1], dzr[2], dzr[3]);
@@ -347,32 +378,34 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
       dead = !poll_shards4(cntG + (size_t)t * 4, target, a.spin_limit, a.err, 8u);
     __syncthreads();
     {
-      bf16x8 zf[KB];
-      if (a.ring1) {
-        const __amdgpu_buffer_rsrc_t rg =
-            make_rsrc(a.ring1 + (size_t)(t & 1) * B * 2 * H, sizeof(bf16) * (size_t)B * 2 * H);
+      // one batch tile at a time: KB = 2 KA payload fragments per tile is the register limit
+      const __amdgpu_buffer_rsrc_t rg =
+          a.ring1 ? make_rsrc(a.ring1 + (size_t)(t & 1) * B * 2 * H, sizeof(bf16) * (size_t)B * 2 * H)
+                  : zsrc;
 #pragma unroll
-        for (int s = 0; s < KB; ++s) zf[s] = ld8_sc1(rg, frag_load_off(bg, w * KB + s, 2 * H, lane));
-      } else {
+      for (int n = 0; n < NT; ++n) {
+        bf16x8 zf[KB];
 #pragma unroll
-        for (int s = 0; s < KB; ++s) zf[s] = ld8_sc1(zsrc, offB + s * 64);
-      }
-      __builtin_amdgcn_sched_barrier(0);
+        for (int s = 0; s < KB; ++s)
+          zf[s] = ld8_sc1(rg, a.ring1 ? frag_load_off(bg * NT + n, w * KB + s, 2 * H, lane)
+                                      : offB + n * tile_off + s * 64);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int ui = 0; ui < UB; ++ui) {
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int ui = 0; ui < UB; ++ui) {
+          f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < KB; ++s) acc = mfma16(wg[ui][s], zf[s], acc);
-        *reinterpret_cast<float4*>(&partB[w][ui][lane][0]) =
-            make_float4(acc[0], acc[1], acc[2], acc[3]);
+          for (int s = 0; s < KB; ++s) acc = mfma16(wg[ui][s], zf[s], acc);
+          *reinterpret_cast<float4*>(&partB[w][n][ui][lane][0]) =
+              make_float4(acc[0], acc[1], acc[2], acc[3]);
+        }
       }
     }
     __syncthreads();
     if (epi) {
-      const float4 s0 = *reinterpret_cast<const float4*>(&partB[0][w][lane][0]);
-      const float4 s1 = *reinterpret_cast<const float4*>(&partB[1][w][lane][0]);
-      const float4 s2 = *reinterpret_cast<const float4*>(&partB[2][w][lane][0]);
-      const float4 s3 = *reinterpret_cast<const float4*>(&partB[3][w][lane][0]);
+      const float4 s0 = *reinterpret_cast<const float4*>(&partB[0][en][eu][lane][0]);
+      const float4 s1 = *reinterpret_cast<const float4*>(&partB[1][en][eu][lane][0]);
+      const float4 s2 = *reinterpret_cast<const float4*>(&partB[2][en][eu][lane][0]);
+      const float4 s3 = *reinterpret_cast<const float4*>(&partB[3][en][eu][lane][0]);
       dhp[0] = dt[0] + P[0] + s0.x + s1.x + s2.x + s3.x;
       dhp[1] = dt[1] + P[1] + s0.y + s1.y + s2.y + s3.y;
       dhp[2] = dt[2] + P[2] + s0.z + s1.z + s2.z + s3.z;
@@ -388,7 +421,7 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
         st4bf_sc1(crow, dzc[0], dzc[1], dzc[2], dzc[3]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0)
-        wg_arrive(&wg_cnt[1], UB, cntC + (size_t)(t - 1) * 4 + (u0 / (H / 4)));
+        wg_arrive(&wg_cnt[1], UB * NT, cntC + (size_t)(t - 1) * 4 + (u0 / (H / 4)));
       if (a.ring0) st4bf(crow, dzc[0], dzc[1], dzc[2], dzc[3]);
     }
   }
@@ -397,50 +430,62 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
-template <int K, int U>
+template <int K, int U, int N>
 static const void* gru_fn(int bwd) {
-  return bwd ? (const void*)gru_bwd_persist_kernel<K, U> : (const void*)gru_fwd_persist_kernel<K, U>;
+  return bwd ? (const void*)gru_bwd_persist_kernel<K, U, N>
+             : (const void*)gru_fwd_persist_kernel<K, U, N>;
 }
 
-static const void* gru_pick(int bwd, int H, int ub) {
+static const void* gru_pick(int bwd, int H, int ub, int nt) {
   const int ks = H / 128;
-#define GP(K, U) \
-  if (ks == K && ub == U) return gru_fn<K, U>(bwd);
-  GP(1, 1) GP(2, 1) GP(3, 1) GP(4, 1) GP(6, 1) GP(8, 1)
-  GP(1, 2) GP(2, 2) GP(3, 2) GP(4, 2) GP(6, 2) GP(8, 2)
+#define GP(K, U, N) \
+  if (ks == K && ub == U && nt == N) return gru_fn<K, U, N>(bwd);
+  GP(1, 1, 1) GP(2, 1, 1) GP(3, 1, 1) GP(4, 1, 1) GP(6, 1, 1) GP(8, 1, 1)
+  GP(1, 2, 1) GP(2, 2, 1) GP(3, 2, 1) GP(4, 2, 1) GP(6, 2, 1) GP(8, 2, 1)
+  // NT > 1 (batch tiles sharing the resident weights): the power-of-two widths
+  GP(2, 2, 2) GP(4, 2, 2) GP(8, 2, 2)
+  GP(2, 1, 4) GP(4, 1, 4) GP(8, 1, 4)
 #undef GP
   return nullptr;
 }
 
-static int gru_grid(int H, int B, int ub) { return (H / (16 * ub)) * (B / 16); }
+static int gru_grid(int H, int B, int ub, int nt) { return (H / (16 * ub)) * (B / (16 * nt)); }
 
-// Largest unit block (32 then 16 units per workgroup) whose forward AND backward grids can be
-// co-resident with the GPU to themselves; 0 = not supported (per-step kernels instead).
+// Launch plan: the first (NT, UB) -- fewest batch tiles per workgroup, then the larger unit block
+// (32 before 16 units) -- whose forward AND backward grids are co-resident with the GPU to
+// themselves.  Returns UB | NT << 4; 0 = not supported (per-step kernels instead).
+// DCR_DEBUG=gru_ub=1 forces 16-unit blocks, gru_nt=N forces N batch tiles per workgroup.
 int gru_persist_ub(int H, int B, int cus) {
   if (H % 128 != 0 || H < 128 || H > 1024 || B % 16 != 0 || B < 16 || cus <= 0) return 0;
-  const int first = debug_int("gru_ub", 2) == 1 ? 1 : 2;  // DCR_DEBUG=gru_ub=1: 16-unit blocks
-  for (int ub = first; ub >= 1; --ub) {
-    bool ok = true;
-    for (int bwd = 0; bwd < 2 && ok; ++bwd) {
-      const void* fn = gru_pick(bwd, H, ub);
-      int occ = 0;
-      ok = fn && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 256, 0) == hipSuccess &&
-           gru_grid(H, B, ub) <= occ * cus;
+  const int first = debug_int("gru_ub", 2) == 1 ? 1 : 2;
+  const int force_nt = debug_int("gru_nt", 0);
+  for (int nt = 1; nt <= 4; nt *= 2) {
+    if ((force_nt > 0 && nt != force_nt) || B % (16 * nt) != 0) continue;
+    for (int ub = first; ub >= 1; --ub) {
+      if (ub * nt > 4) continue;  // one epilogue role per wave
+      bool ok = true;
+      for (int bwd = 0; bwd < 2 && ok; ++bwd) {
+        const void* fn = gru_pick(bwd, H, ub, nt);
+        int occ = 0;
+        ok = fn && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 256, 0) == hipSuccess &&
+             gru_grid(H, B, ub, nt) <= occ * cus;
+      }
+      if (ok) return ub | nt << 4;
     }
-    if (ok) return ub;
   }
   return 0;
 }
 
 int launch_gru_persist(int bwd, const GruPersistArgs& a, int cus, hipStream_t s) {
-  const int ub = gru_persist_ub(a.H, a.B, cus);
-  if (!ub) return -2;
-  const void* fn = gru_pick(bwd, a.H, ub);
+  const int plan = gru_persist_ub(a.H, a.B, cus);
+  if (!plan) return -2;
+  const int ub = plan & 15, nt = plan >> 4;
+  const void* fn = gru_pick(bwd, a.H, ub, nt);
   if (!fn) return -1;
   if (!a.cnt_zeroed)
     (void)hipMemsetAsync(a.cnt, 0, sizeof(unsigned) * 2 * (size_t)(a.B / 16) * (a.T + 1) * 4, s);
   void* args[] = {const_cast<GruPersistArgs*>(&a)};
-  return hipLaunchKernel(fn, dim3(gru_grid(a.H, a.B, ub)), dim3(256), args, 0, s) == hipSuccess
+  return hipLaunchKernel(fn, dim3(gru_grid(a.H, a.B, ub, nt)), dim3(256), args, 0, s) == hipSuccess
              ? 0 : -3;
 }
 

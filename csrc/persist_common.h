@@ -175,7 +175,7 @@ __host__ __device__ __forceinline__ void map_block(int bid, int nwg_u, int nbg, 
 }
 
 // Hand-off poller.  GRU kernels poll from lane 0 of wave 3, which never runs a cell epilogue
-// (UB <= 3), so polling overlaps the epilogue waves' drain and post-arrival work: 3-layer
+// (UB * NT <= 3), so polling overlaps the epilogue waves' drain and post-arrival work: 3-layer
 // GRU-1024 16.8 -> 15.3 ms/step.  The LSTM kernels keep the poller on wave 0 (an epilogue wave):
 // the same change measured 2.74 -> 3.18 ms/step there (forward 420 -> 508 us per layer).
 constexpr int kPollerThread = 192;

@@ -46,11 +46,17 @@ class LibStepMixin:
 
     def _lstm_bwd_lib(self, lw, lb, dtop, bufs) -> None:
         T, B = dtop.shape[0], dtop.shape[1]
+        # dZ·W_hᵀ as S split-K slabs over K = 4H (the cell kernel sums them): the unsplit
+        # [B, 8192] x [8192, 2048] product tiles a [B, 2048] output into too few workgroups
+        # (scripts/micro/step_gemm_large_b.py: B = 256 28.7 -> 19.3 us at S = 2, B = 512
+        # 34.7 -> 23.2 us and B = 1024 47.1 -> 36.7 us at S = 4)
+        S = 4 if B >= 512 else 2 if B >= 256 else 1
         dh = bufs.get("dhrec")
-        if dh is None:
-            dh = bufs["dhrec"] = torch.empty(1, B, self.H, dtype=f32, device=self.dev)
+        if dh is None or dh.shape[0] != S:
+            dh = bufs["dhrec"] = torch.empty(S, B, self.H, dtype=f32, device=self.dev)
         dc = bufs["dc"]
-        WhT = lw.Wh.t()
+        G4 = 4 * self.H
+        WhT = lw.Wh.t() if S == 1 else lw.Wh.view(self.H, S, G4 // S).permute(1, 2, 0)
 
         def body(dtop, _unused):
             dc.zero_()
@@ -58,7 +64,11 @@ class LibStepMixin:
                 # dh = dtop_t + dZ_{t+1}·W_hᵀ: the GEMM writes the recurrent part, the cell
                 # kernel adds dtop_t (an addmm with a 2-D input costs a separate copy launch)
                 if t < T - 1:
-                    torch.mm(lb.dz[t + 1], WhT, out_dtype=f32, out=dh[0])
+                    if S == 1:
+                        torch.mm(lb.dz[t + 1], WhT, out_dtype=f32, out=dh[0])
+                    else:
+                        torch.bmm(lb.dz[t + 1].view(B, S, G4 // S).transpose(0, 1), WhT,
+                                  out_dtype=f32, out=dh)
                 self.ops.lstm_step_ew_bwd(dtop[t], dh if t < T - 1 else None, lb.gates[t],
                                           lb.cbuf[t + 1], lb.cbuf[t], dc, lb.dz[t])
 

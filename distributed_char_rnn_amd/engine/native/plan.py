@@ -42,6 +42,7 @@ DEBUG_KEYS = {
     "lib_graph": "0: eager library-step loops (no hipGraph replay)",
     "sample_graph": "0: eager sampling loop (no hipGraph replay)",
     "gru_ub": "1: 16-unit GRU workgroups (C++)",
+    "gru_nt": "N: N batch tiles of 16 rows per GRU workgroup (C++)",
     "step_nbt": "1/2/4: batch tiles per per-step workgroup (C++)",
 }
 

@@ -83,3 +83,41 @@ def test_gru_persist_dropout_and_long_sequence():
     torch.cuda.synchronize()
     m.backend.check_errors()
     assert torch.isfinite(loss) and torch.isfinite(m.store.grad).all()
+
+
+@pytest.mark.parametrize("B,T,H,nt", [(64, 5, 256, 2), (64, 4, 512, 4), (96, 3, 1024, 2),
+                                      (256, 3, 1024, 0)])
+def test_gru_batch_tiles_per_workgroup(B, T, H, nt, monkeypatch):
+    """NT batch tiles per workgroup (gru_nt forced; nt = 0: the planner's own choice, NT = 2 at
+    B = 256, H = 1024) vs the fp32 oracle, and vs the NT = 1 schedule (same per-tile math)."""
+    dbg = "persist_min_t=1" + (f",gru_nt={nt}" if nt else "")
+    monkeypatch.setenv("DCR_DEBUG", dbg)
+    cfg, nat = _model(B, H, 2, seed=7)
+    plan = int(nat.backend.ops.gru_persist_ub(H, B))
+    assert plan >> 4 == (nt or 2), plan
+    ref = ReferenceBackend(nat.store)
+    torch.manual_seed(2)
+    x = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
+    y = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
+    st0 = [(torch.randn(B, H, device="cuda") * 0.5,) for _ in range(2)]
+    loss_r, st_r, _ = ref.train_step(x, y, [tuple(s.clone() for s in t) for t in st0])
+    g_ref = nat.store.grad.clone()
+    nat.store.grad.zero_()
+    loss_n, st_n, _ = nat.backend.train_step(x, y, [tuple(s.clone() for s in t) for t in st0])
+    torch.cuda.synchronize()
+    nat.backend.check_errors()
+    g_nt = nat.store.grad.clone()
+    assert abs(loss_n.item() - loss_r.item()) < 2e-2 * max(1.0, abs(loss_r.item()))
+    for a_r, a_n in zip(st_r, st_n):
+        assert rel(a_n[0], a_r[0]) < 3e-2
+    for s in nat.store.specs:
+        e = rel(nat.store.gview(s.name), nat.store.view(s.name, g_ref))
+        assert e < 6e-2, (s.name, e)
+    if nt and B < 256:  # NT = 1 fits these grids: same schedule per tile
+        monkeypatch.setenv("DCR_DEBUG", "persist_min_t=1,gru_nt=1")
+        _, one = _model(B, H, 2, seed=7)
+        assert int(one.backend.ops.gru_persist_ub(H, B)) >> 4 == 1
+        loss_1, st_1, _ = one.backend.train_step(x, y, [tuple(s.clone() for s in t) for t in st0])
+        torch.cuda.synchronize()
+        assert abs(loss_1.item() - loss_n.item()) < 1e-4
+        assert rel(g_nt, one.store.grad) < 1e-4

@@ -179,7 +179,8 @@ def test_per_step_batch_tiles_match_reference(model, nbt, monkeypatch):
         assert rel(nat.store.gview(s.name), nat.store.view(s.name, g_ref)) < 6e-2, s.name
 
 
-@pytest.mark.parametrize("B,T,H,L", [(32, 5, 64, 2), (64, 4, 128, 1)])
+# B = 512: the BPTT step product runs as split-K slabs summed by the cell kernel
+@pytest.mark.parametrize("B,T,H,L", [(32, 5, 64, 2), (64, 4, 128, 1), (512, 3, 64, 1)])
 def test_library_step_lstm_path_matches_reference(B, T, H, L, monkeypatch):
     """DCR_RECURRENCE=library: per-step library GEMM (h·W_h / dZ·W_hᵀ) + epilogue-only cell
     kernels (the H > 1024 LSTM path) against the fp32 oracle, persistent kernels off."""
