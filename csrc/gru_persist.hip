@@ -82,6 +82,13 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
   const int G3 = 3 * H;
   float hp[4] = {0.f, 0.f, 0.f, 0.f};
   if (epi) ld4f(a.h32 + bh, hp);  // h_0, fp32
+  // input bias added here when the dense zx was written without it (one [T·B, 3H] fp32 pass
+  // less behind the input GEMM)
+  float bx[3][4] = {};
+  if (epi && a.bias_x) {
+#pragma unroll
+    for (int g = 0; g < 3; ++g) ld4f(a.bias_x + (size_t)g * H + u0, bx[g]);
+  }
 
   for (int t = 0; t < T; ++t) {
     float zx[3][4];
@@ -135,10 +142,10 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
         const float4 s2 = reinterpret_cast<const float4*>(&partA[2][en][eu][lane][0])[g];
         const float4 s3 = reinterpret_cast<const float4*>(&partA[3][en][eu][lane][0])[g];
         float* o = g == 0 ? rr : uu;
-        o[0] = sigmoidf_(s0.x + s1.x + s2.x + s3.x + zx[g][0]);
-        o[1] = sigmoidf_(s0.y + s1.y + s2.y + s3.y + zx[g][1]);
-        o[2] = sigmoidf_(s0.z + s1.z + s2.z + s3.z + zx[g][2]);
-        o[3] = sigmoidf_(s0.w + s1.w + s2.w + s3.w + zx[g][3]);
+        o[0] = sigmoidf_(s0.x + s1.x + s2.x + s3.x + (zx[g][0] + bx[g][0]));
+        o[1] = sigmoidf_(s0.y + s1.y + s2.y + s3.y + (zx[g][1] + bx[g][1]));
+        o[2] = sigmoidf_(s0.z + s1.z + s2.z + s3.z + (zx[g][2] + bx[g][2]));
+        o[3] = sigmoidf_(s0.w + s1.w + s2.w + s3.w + (zx[g][3] + bx[g][3]));
       }
       const float rh0 = rr[0] * hp[0], rh1 = rr[1] * hp[1], rh2 = rr[2] * hp[2], rh3 = rr[3] * hp[3];
       if (a.ring1)
@@ -187,10 +194,10 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
       const float4 s2 = *reinterpret_cast<const float4*>(&partB[2][en][eu][lane][0]);
       const float4 s3 = *reinterpret_cast<const float4*>(&partB[3][en][eu][lane][0]);
       float cc[4], h[4];
-      cc[0] = tanhf_(s0.x + s1.x + s2.x + s3.x + zx[2][0]);
-      cc[1] = tanhf_(s0.y + s1.y + s2.y + s3.y + zx[2][1]);
-      cc[2] = tanhf_(s0.z + s1.z + s2.z + s3.z + zx[2][2]);
-      cc[3] = tanhf_(s0.w + s1.w + s2.w + s3.w + zx[2][3]);
+      cc[0] = tanhf_(s0.x + s1.x + s2.x + s3.x + (zx[2][0] + bx[2][0]));
+      cc[1] = tanhf_(s0.y + s1.y + s2.y + s3.y + (zx[2][1] + bx[2][1]));
+      cc[2] = tanhf_(s0.z + s1.z + s2.z + s3.z + (zx[2][2] + bx[2][2]));
+      cc[3] = tanhf_(s0.w + s1.w + s2.w + s3.w + (zx[2][3] + bx[2][3]));
 #pragma unroll
       for (int r = 0; r < 4; ++r) h[r] = uu[r] * hp[r] + (1.f - uu[r]) * cc[r];
       const size_t o = (size_t)(t + 1) * B * H + bh;

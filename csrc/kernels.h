@@ -181,6 +181,8 @@ struct Lstm2Args {
   const int* ids;       // gather mode: [T, B]
   int zx_ld;
   const float* bias1;   // layer l+1 bias [4H]
+  const float* bias0;   // optional layer l bias [4H], added in-kernel to a dense zx0 written
+                        // without it (null: zx0 / the gather table already holds it)
   bf16* hbuf0; float* cbuf0; bf16* gates0; float* hlast0;   // layer l   [T+1,B,H] ...
   bf16* hbuf1; float* cbuf1; bf16* gates1; float* hlast1;   // layer l+1
   unsigned* cnt0;       // [nbg, T+1, 4] arrivals of layer l   (zeroed by the caller)
@@ -232,6 +234,7 @@ struct GruPersistArgs {
   const bf16* WgT;      // fwd: W_g,hᵀ [2H, H] (r rows, then u rows)
   const bf16* WcT;      // fwd: W_c,hᵀ [H, H]
   const float* zx;      // fwd: [T, B, zx_ld] input projections (+bias) or [V, zx_ld] table
+  const float* bias_x;  // fwd: optional [3H] bias added in-kernel (zx written without it)
   const int* ids;       // fwd gather mode: [T, B]
   int zx_ld;            // 3H
   bf16* hbuf;           // [T+1, B, H] bf16 (slot 0 = h_0)

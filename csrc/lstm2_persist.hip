@@ -108,9 +108,14 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
   float* const hlL = L ? a.hlast1 : a.hlast0;
   float* const clL = L ? a.clast1 : a.clast0;
   bf16* const ringL = L ? a.hring1 : a.hring0;
-  float bias1[4][4];
+  // the role's bias: layer l+1's, or layer l's when its dense zx0 was written without it
+  // (saves a [T·B, 4H] fp32 pass over zx0 behind the input GEMM)
+  float biasL[4][4] = {};
+  const float* bsrc = L ? a.bias1 : a.bias0;
+  if (bsrc) {
 #pragma unroll
-  for (int gt = 0; gt < 4; ++gt) ld4f(a.bias1 + gt * H + u0, bias1[gt]);
+    for (int gt = 0; gt < 4; ++gt) ld4f(bsrc + gt * H + u0, biasL[gt]);
+  }
   constexpr int LAG = G == 1 ? 2 : 1;  // ticks layer l+1 runs behind layer l
   constexpr int NXS = 1;  // (unused for G > 1)
   float c[G][4];
@@ -345,7 +350,9 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
           const float4 s1 = *reinterpret_cast<const float4*>(&part[1][L][J][gt][lane][0]);
           const float4 s2 = *reinterpret_cast<const float4*>(&part[2][L][J][gt][lane][0]);
           const float4 s3 = *reinterpret_cast<const float4*>(&part[3][L][J][gt][lane][0]);
-          const float* add = L == 0 ? zx[gt] : bias1[gt];
+          float add[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) add[r] = L == 0 ? zx[gt][r] + biasL[gt][r] : biasL[gt][r];
           z[gt][0] = s0.x + s1.x + s2.x + s3.x + add[0];
           z[gt][1] = s0.y + s1.y + s2.y + s3.y + add[1];
           z[gt][2] = s0.z + s1.z + s2.z + s3.z + add[2];

@@ -678,7 +678,8 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
                        const c10::optional<at::Tensor>& clast0,
                        const c10::optional<at::Tensor>& clast1,
                        const c10::optional<at::Tensor>& diag,
-                       const c10::optional<at::Tensor>& xmask, double xscale) {
+                       const c10::optional<at::Tensor>& xmask, double xscale,
+                       const c10::optional<at::Tensor>& bias0) {
   for (auto* t : {&W0T, &W1T, &X1T}) check_seq(*t, at::kBFloat16, "W");
   check_seq(zx0, at::kFloat, "zx0");
   check_seq(bias1, at::kFloat, "bias1");
@@ -712,6 +713,11 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
   a.W0T = ptr<bf16>(W0T); a.W1T = ptr<bf16>(W1T); a.X1T = ptr<bf16>(X1T);
   a.zx0 = ptr<float>(zx0); a.ids = optr<int>(ids); a.zx_ld = 4 * H;
   a.bias1 = ptr<float>(bias1);
+  if (has(bias0)) {
+    check_seq(*bias0, at::kFloat, "bias0");
+    TORCH_CHECK(bias0->numel() == 4 * H && !has(ids), "bias0: [4H], dense zx0 only");
+  }
+  a.bias0 = optr<float>(bias0);
   a.hbuf0 = ptr<bf16>(hbuf0); a.cbuf0 = ptr<float>(cbuf0); a.gates0 = optr<bf16>(gates0);
   a.hlast0 = ptr<float>(hlast0);
   a.hbuf1 = ptr<bf16>(hbuf1); a.cbuf1 = ptr<float>(cbuf1); a.gates1 = optr<bf16>(gates1);
@@ -876,7 +882,8 @@ void gru_persist_fwd(const at::Tensor& WgT, const at::Tensor& WcT, const at::Ten
                      const c10::optional<at::Tensor>& ids, at::Tensor& hbuf, at::Tensor& h32,
                      at::Tensor& rh, at::Tensor& gates, const c10::optional<at::Tensor>& hlast32,
                      at::Tensor& cnt, at::Tensor& err, int64_t spin_limit, bool cnt_zeroed,
-                     const c10::optional<at::Tensor>& ring0, const c10::optional<at::Tensor>& ring1) {
+                     const c10::optional<at::Tensor>& ring0, const c10::optional<at::Tensor>& ring1,
+                     const c10::optional<at::Tensor>& bias_x) {
   check_seq(WgT, at::kBFloat16, "WgT");
   check_seq(WcT, at::kBFloat16, "WcT");
   check_seq(zx, at::kFloat, "zx");
@@ -902,6 +909,11 @@ void gru_persist_fwd(const at::Tensor& WgT, const at::Tensor& WcT, const at::Ten
   a.zx = ptr<float>(zx);
   a.ids = optr<int>(ids);
   a.zx_ld = 3 * H;
+  if (has(bias_x)) {
+    check_seq(*bias_x, at::kFloat, "bias_x");
+    TORCH_CHECK(bias_x->numel() == 3 * H && !has(ids), "bias_x: [3H], dense zx only");
+  }
+  a.bias_x = optr<float>(bias_x);
   a.hbuf = ptr<bf16>(hbuf);
   a.rh = ptr<bf16>(rh);
   a.hlast32 = optr<float>(hlast32);
@@ -1182,7 +1194,7 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor(i!) cnt0, Tensor(j!) cnt1, Tensor(k!) err, float forget_bias, int spin_limit, "
       "Tensor(l!) hring0, Tensor(m!) hring1, int G, Tensor(o!)? clast0=None, "
       "Tensor(p!)? clast1=None, Tensor(q!)? diag=None, Tensor? xmask=None, "
-      "float xscale=1.0) -> ()");
+      "float xscale=1.0, Tensor? bias0=None) -> ()");
   m.def(
       "lstm2_persist_bwd(Tensor Wh0, Tensor Wh1, Tensor Wx1, Tensor dtop1, Tensor gates0, "
       "Tensor cbuf0, Tensor gates1, Tensor cbuf1, Tensor(a!) dz0, Tensor(b!) dz1, "
@@ -1206,7 +1218,7 @@ TORCH_LIBRARY(dcr, m) {
       "gru_persist_fwd(Tensor WgT, Tensor WcT, Tensor zx, Tensor? ids, Tensor(a!) hbuf, "
       "Tensor(b!) h32, Tensor(c!) rh, Tensor(d!) gates, Tensor(e!)? hlast32, Tensor(f!) cnt, "
       "Tensor(g!) err, int spin_limit, bool cnt_zeroed=False, Tensor(h!)? ring0=None, "
-      "Tensor(i!)? ring1=None) -> ()");
+      "Tensor(i!)? ring1=None, Tensor? bias_x=None) -> ()");
   m.def(
       "gru_persist_bwd(Tensor Wg, Tensor Wc, Tensor dtop, Tensor(a!) dz, Tensor gates, "
       "Tensor h32, Tensor(b!) cnt, Tensor(c!) err, int spin_limit, bool cnt_zeroed=False, "

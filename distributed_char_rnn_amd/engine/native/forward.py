@@ -125,7 +125,12 @@ class ForwardMixin:
                     if inb is not None:
                         X = self._masked(X, inb, dm["sin"], out=lb.x_drop)
                 lb.x_in = X if X.is_contiguous() else X.contiguous()
-                mm_into(lb.x_in, lw.Wx, lb.zx.view(N, self.GW), bias=lw.bias)
+                # the two-layer LSTM and the GRU kernels add the input bias in their epilogue:
+                # the library GEMM with a bias ran as GEMM + a separate [N, GW] fp32 add pass
+                # (41 us / 114 us per layer in the dropout headline / GRU-1024 B = 256 profiles)
+                bias_in_kernel = ((P.pair and layer + 1 < self.L) or P.gru_persist)
+                mm_into(lb.x_in, lw.Wx, lb.zx.view(N, self.GW),
+                        bias=None if bias_in_kernel else lw.bias)
                 zx = lb.zx
             if P.pair and layer + 1 < self.L:
                 # layers (l, l+1) as one wavefront launch (lstm2_persist.hip): T+1 ticks; layer
@@ -138,7 +143,8 @@ class ForwardMixin:
                                            bufs["cnt"][layer], bufs["cnt"][layer + 1], self.err,
                                            FORGET_BIAS, self.spin_limit, *bufs["hrings"],
                                            P.pair_g, lb.clast32, lb1.clast32, None, xm,
-                                           dm["sin"] if dm else 1.0)
+                                           dm["sin"] if dm else 1.0,
+                                           lw.bias if ids_arg is None else None)
                 # layer l+1's (masked) input rows for its weight gradient
                 lb1.x_in = (self._masked(lb.hbuf[1:], xm, dm["sin"], out=lb1.x_drop)
                             if xm is not None else lb.hbuf[1:].reshape(N, H))
@@ -155,7 +161,7 @@ class ForwardMixin:
                 self.ops.gru_persist_fwd(lw.WhT, lw.WT2, zx, ids_arg, lb.hbuf, lb.h32, lb.rh,
                                          lb.gates, None, bufs["cnt"][layer], self.err,
                                          self.spin_limit, cnt_zeroed=True, ring0=gr[0],
-                                         ring1=gr[1])
+                                         ring1=gr[1], bias_x=lw.bias if ids_arg is None else None)
             elif self._lib_step("fwd", B):
                 self._lstm_fwd_lib(lw, lb, zx, ids_arg, bufs)
             else:
