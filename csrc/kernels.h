@@ -254,6 +254,22 @@ struct GruPersistArgs {
   unsigned spin_limit;
   int cnt_zeroed;
 };
+// token-reduction weight-gradient GEMM (wgrad.hip): C_s = A_chunkᵀ · B_chunk per split-K slab
+constexpr int kWgradMaxProblems = 4;
+constexpr int kWgradMaxSplit = 32;
+struct WgradProblem {
+  const bf16* A; long lda;   // [K, M] token-major rows (row stride lda elements)
+  const bf16* B; long ldb;   // [K, N]
+  float* C; long ldc;        // slab 0 of [S, M, N] fp32 partials (row stride ldc)
+  long slab;                 // elements between slabs
+};
+struct WgradArgs {
+  WgradProblem p[kWgradMaxProblems];
+  int np, S, M, N, K, tiles;  // tiles = (M / 256) * (N / 256) per (problem, slab)
+};
+bool wgrad_supported(int M, int N, int K);
+int wgrad_splits(int np, int M, int N, int K, int cus);
+void launch_wgrad(const WgradArgs& a, hipStream_t s);
 int gru_persist_ub(int H, int B, int cus);
 int launch_gru_persist(int bwd, const GruPersistArgs& a, int cus, hipStream_t s);
 

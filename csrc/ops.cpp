@@ -1005,6 +1005,42 @@ void head(const at::Tensor& O, const at::Tensor& WsT, const c10::optional<at::Te
 // ------------------------------------------------------------------------------------------
 // batched per-step data movement (prep.hip)
 // ------------------------------------------------------------------------------------------
+// ------------------------------------------------------------------------------------------
+// token-reduction weight-gradient GEMMs (wgrad.hip): part[p][s] = A_p[chunk s]ᵀ · B_p[chunk s]
+// ------------------------------------------------------------------------------------------
+void wgrad(at::TensorList A, at::TensorList B, at::Tensor& part) {
+  const int np = (int)A.size();
+  TORCH_CHECK(np >= 1 && np <= dcr::kWgradMaxProblems && (int)B.size() == np, "wgrad: 1..",
+              dcr::kWgradMaxProblems, " problems");
+  check_seq(part, at::kFloat, "part");
+  TORCH_CHECK(part.dim() == 4 && part.size(0) == np, "part must be [np, S, M, N]");
+  const int S = (int)part.size(1), M = (int)part.size(2), N = (int)part.size(3);
+  const int K = (int)A[0].size(0);
+  TORCH_CHECK(S >= 1 && S <= dcr::kWgradMaxSplit, "wgrad: 1..", dcr::kWgradMaxSplit, " slabs");
+  TORCH_CHECK(dcr::wgrad_supported(M, N, K), "wgrad: unsupported shape M=", M, " N=", N, " K=", K);
+  dcr::WgradArgs a{};
+  for (int i = 0; i < np; ++i) {
+    const at::Tensor& x = A[i];
+    const at::Tensor& y = B[i];
+    for (const at::Tensor* t : {&x, &y}) {
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->dim() == 2 &&
+                      t->stride(1) == 1 && t->stride(0) % 8 == 0 &&
+                      reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+                  "wgrad operands: bf16 [K, *] views with unit column stride, 16-B aligned rows");
+    }
+    TORCH_CHECK(x.size(0) == K && y.size(0) == K && x.size(1) == M && y.size(1) == N,
+                "wgrad: A_p must be [K, M], B_p [K, N]");
+    a.p[i].A = ptr<bf16>(x); a.p[i].lda = x.stride(0);
+    a.p[i].B = ptr<bf16>(y); a.p[i].ldb = y.stride(0);
+    a.p[i].C = part.data_ptr<float>() + (size_t)i * S * M * N;
+    a.p[i].ldc = N;
+    a.p[i].slab = (long)M * N;
+  }
+  a.np = np; a.S = S; a.M = M; a.N = N; a.K = K;
+  a.tiles = (M / 256) * (N / 256);
+  dcr::launch_wgrad(a, cur_stream());
+}
+
 void prep(at::TensorList src, at::TensorList dst, at::IntArrayRef mode, at::TensorList extra) {
   TORCH_CHECK(src.size() == dst.size() && dst.size() == mode.size(), "prep: list lengths differ");
   TORCH_CHECK((int)dst.size() <= dcr::kPrepMaxTasks, "prep: too many tasks");
@@ -1181,6 +1217,12 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor(e!)? db, Tensor(f!) part, Tensor(g!)? loss) -> ()");
   m.def("prep(Tensor[] src, Tensor(a!)[] dst, int[] mode, Tensor[] extra) -> ()");
   m.def("prep_max_tasks() -> int", []() -> int64_t { return dcr::kPrepMaxTasks; });
+  m.def("wgrad(Tensor[] A, Tensor[] B, Tensor(a!) part) -> ()");
+  m.def("wgrad_plan(int np, int M, int N, int K) -> int",
+        [](int64_t np, int64_t M, int64_t N, int64_t K) -> int64_t {
+          if (!dcr::wgrad_supported((int)M, (int)N, (int)K)) return 0;
+          return dcr::wgrad_splits((int)np, (int)M, (int)N, (int)K, num_cus());
+        });
   m.def("lstm2_plan(int H, int B, int force=0) -> int",
         [](int64_t H, int64_t B, int64_t force) -> int64_t {
           return dcr::lstm2_plan_g((int)H, (int)B, num_cus(), (int)force);
@@ -1245,6 +1287,7 @@ TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("lstm_persist_bwd", &lstm_persist_bwd);
   m.impl("head", &head);
   m.impl("prep", &prep);
+  m.impl("wgrad", &wgrad);
   m.impl("gru_persist_fwd", &gru_persist_fwd);
   m.impl("lstm2_persist_fwd", &lstm2_persist_fwd);
   m.impl("lstm2_persist_bwd", &lstm2_persist_bwd);

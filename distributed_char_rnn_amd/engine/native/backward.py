@@ -24,7 +24,7 @@ class BackwardMixin:
                                                    want_logits=not self.fused_head,
                                                    logits_bias=not wide, extra_tasks=id_tasks)
         # deferred slab / bias sums of this step: one prep launch per flush (gemm.SumQueue)
-        q = SumQueue(self.ops)
+        q = SumQueue(self.ops, wgrad=self.knobs.debug.get("wgrad") == "1")
         if on_ready is not None:
             cb_user = on_ready
 

@@ -59,9 +59,43 @@ class SumQueue:
 
     SUM, COLSUM = 3, 4
 
-    def __init__(self, ops):
+    def __init__(self, ops, wgrad: bool = False):
         self.ops = ops
         self.tasks = []
+        # token-reduction GEMMs deferred to the flush, run there as hand-written wgrad launches
+        # (csrc/wgrad.hip: 256 x 256 tiles, split-K slabs; one launch for every pending GEMM of
+        # one shape, so the headline's three weight gradients share one 240-workgroup grid)
+        self.wgrad = wgrad
+        self.gemms = []
+
+    def wgrad_ok(self, a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor]) -> bool:
+        if not self.wgrad or out is None or out.dim() != 2 or out.stride(1) != 1:
+            return False
+        for t in (a, b):
+            if (t.dtype != bf16 or not t.is_cuda or t.dim() != 2 or t.stride(1) != 1
+                    or t.stride(0) % 8 or t.data_ptr() % 16):
+                return False
+        K, M = a.shape
+        return (b.shape[0] == K and tuple(out.shape) == (M, b.shape[1])
+                and int(self.ops.wgrad_plan(1, M, b.shape[1], K)) > 0)
+
+    def add_gemm(self, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        self.gemms.append((a, b, out))
+        return out
+
+    def _run_gemms(self) -> None:
+        groups = {}
+        for a, b, out in self.gemms:
+            groups.setdefault((a.shape[1], b.shape[1], a.shape[0]), []).append((a, b, out))
+        self.gemms = []
+        for (M, Nn, K), items in groups.items():
+            for i in range(0, len(items), 4):  # csrc/kernels.h kWgradMaxProblems
+                chunk = items[i: i + 4]
+                S = int(self.ops.wgrad_plan(len(chunk), M, Nn, K))
+                part = torch.empty(len(chunk), S, M, Nn, dtype=f32, device=chunk[0][0].device)
+                self.ops.wgrad([c[0] for c in chunk], [c[1] for c in chunk], part)
+                for j, (_, _, out) in enumerate(chunk):
+                    self.add_sum(part[j], out)
 
     def add_sum(self, part: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         self.tasks.append((part, out, self.SUM))
@@ -72,6 +106,8 @@ class SumQueue:
         return out
 
     def flush(self) -> None:
+        if self.gemms:
+            self._run_gemms()
         if not self.tasks:
             return
         cap = int(self.ops.prep_max_tasks())
@@ -88,9 +124,12 @@ def mm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
     is too small to fill the chip.  ``split=False`` for GEMMs that run beside a persistent
     kernel on a side stream: there a chip-filling grid only steals the recurrence's CUs
     (measured: 256-workgroup split-K beside BPTT stretched both).  With a queue ``q`` (and an
-    ``out``) the slab sum is deferred to ``q.flush()``."""
+    ``out``) the slab sum is deferred to ``q.flush()``; shapes the hand-written wgrad kernel
+    covers (M, Nn multiples of 256, K of 32) are deferred whole and run there."""
     K, M = a.shape
     Nn = b.shape[1]
+    if q is not None and q.wgrad_ok(a, b, out):
+        return q.add_gemm(a, b, out)
     S = split_k(K, M, Nn) if split else 1
     if S == 1:
         return mm(a.t(), b) if out is None else mm_into(a.t(), b, out)

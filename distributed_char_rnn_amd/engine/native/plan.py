@@ -41,6 +41,7 @@ DEBUG_KEYS = {
     "seg_sort": "0: unsorted atomic embedding gradient for wide vocabularies",
     "lib_graph": "0: eager library-step loops (no hipGraph replay)",
     "sample_graph": "0: eager sampling loop (no hipGraph replay)",
+    "wgrad": "1: hand-written wgrad kernel for the weight gradients (default: library split-K)",
     "gru_ub": "1: 16-unit GRU workgroups (C++)",
     "gru_nt": "N: N batch tiles of 16 rows per GRU workgroup (C++)",
     "step_nbt": "1/2/4: batch tiles per per-step workgroup (C++)",
