@@ -199,11 +199,14 @@ struct Lstm2Args {
   unsigned spin_limit;
   const uint8_t* xmask; // optional dropout bits of layer l+1's input [T, B, H/8] (dropout.hip)
   float xscale;         //   and their 1/keep
+  const bf16* x0;       // optional (G = 1): layer l's bf16 input rows [T·B, H]; the input
+  const bf16* X0T;      //   projection x0·W_x,l (W_x,lᵀ [4H, H]) then runs in-kernel (zx0 unused)
 };
 // batch groups per workgroup for the two-layer kernels at (H, B) (force > 0: only that value),
 // 0 = unsupported
 int lstm2_plan_g(int H, int B, int cus, int force);
 int launch_lstm2_fwd_persist(const Lstm2Args& a, int cus, hipStream_t s);
+bool lstm2_xin_ok(int H, int cus);
 
 // two-layer wavefront LSTM BPTT (lstm2_persist.hip): layers l and l+1 in one launch, layer l
 // one step behind layer l+1; layer l's dtop = dZ_{l+1}·W_x,l+1ᵀ is computed in-kernel

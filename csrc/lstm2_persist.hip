@@ -58,8 +58,14 @@ __device__ __forceinline__ bf16x8 mask_frag(const bf16x8& v, unsigned m) {
 // product in the group's MFMA phase: the ticks are work-bound there (the G phases run back to
 // back, one drain per tick), and the stash would cost 32 registers per group.
 // ------------------------------------------------------------------------------------------
-template <int KS, int G, bool DROP>
+// XIN (G = 1): layer l's input projection x_t·W_x,l runs in-kernel from bf16 input rows a.x0
+// ([T·B, H], time-major; e.g. the dropout-masked embedding rows) instead of a library GEMM's
+// fp32 [T·B, 4H] zx0: W_x,lᵀ fragments sit in LDS, the rows' fragments are loaded and the
+// product accumulated BEFORE the tick's poll (it does not depend on the hand-off), and the
+// recurrent product is added on top after it.
+template <int KS, int G, bool DROP, bool XIN>
 __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) {
+  static_assert(!XIN || G == 1, "in-kernel input projection: one batch group per workgroup");
   // partials [wave][layer][tile][gate][lane][r] (16-B lane stride: conflict-free b128 access),
   // reused by every group: a barrier separates one group's epilogue reads from the next
   // group's stores
@@ -68,6 +74,9 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
   // double-buffered by tick (the G = 1 stash reads them after the tick's last barrier)
   constexpr int kMaskDw = 2 * G;  // DMA dwords per lane: 32 G rows x H/32 dwords / 256 lanes
   __shared__ __attribute__((aligned(16))) unsigned mlds[2][DROP ? G * 512 : 1];
+  // XIN: W_x,lᵀ fragments [wave][gate][k-step][lane] (64 KB at H = 512), read back only by the
+  // wave that wrote them
+  __shared__ __attribute__((aligned(16))) bf16x8 wx0l[XIN ? 4 : 1][4][XIN ? KS : 1][64];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
@@ -97,6 +106,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
       w0[gt][s] = ld8(a.W0T + row);
       w1[gt][s] = ld8(a.W1T + row);
       x1[gt][s] = ld8(a.X1T + row);
+      if constexpr (XIN) wx0l[w][gt][s][lane] = ld8(a.X0T + row);
     }
 
   // epilogue role: layer L, batch tile J of every group
@@ -138,7 +148,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
 
   auto zx_row = [&](int tk, int g) -> const float* {
     const int b = (col * G + g) * 32 + 16 * J + (lane & 15);
-    if (!(L == 0 && tk < T && b < B)) return nullptr;
+    if (XIN || !(L == 0 && tk < T && b < B)) return nullptr;
     return a.ids ? a.zx0 + (size_t)a.ids[(size_t)tk * B + b] * a.zx_ld
                  : a.zx0 + ((size_t)tk * B + b) * a.zx_ld;
   };
@@ -169,6 +179,32 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
 #pragma unroll
     for (int g = 0; g < G; ++g) zrows[g] = zx_row(tau, g);
     zx_load(zrows[0], zxn);
+    // XIN: layer l's input product of step tau (this wave's K quarter, both tiles, all gates),
+    // the recurrent product is accumulated on top after the poll
+    f32x4 xin[XIN ? 2 : 1][4];
+    if constexpr (XIN) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int gt = 0; gt < 4; ++gt) xin[j][gt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (tau < T) {
+        // rows >= B (padding) read as zero through the buffer range check
+        const __amdgpu_buffer_rsrc_t rx =
+            make_rsrc(a.x0 + (size_t)tau * B * H, sizeof(bf16) * (size_t)B * H);
+        bf16x8 xf[2][KS];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int s = 0; s < KS; ++s)
+            xf[j][s] = ld8_sc1(rx, rm_lane + rm_off(col, j, s));
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int gt = 0; gt < 4; ++gt) xin[j][gt] = mfma16(wx0l[w][gt][s][lane], xf[j][s], xin[j][gt]);
+      }
+    }
     // dropout of layer l+1's input (layer l's h of step tau-1): the mask bytes of the
     // workgroup's 32G rows for this tick, DMA'd into LDS before the poll (no registers; the
     // poll barrier waits for them).  A global byte load at each use had put its latency on the
@@ -260,7 +296,13 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
         if (on0) {
           f32x4 acc[4];
 #pragma unroll
-          for (int gt = 0; gt < 4; ++gt) acc[gt] = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int gt = 0; gt < 4; ++gt) {
+            if constexpr (XIN) {
+              acc[gt] = xin[j][gt];
+            } else {
+              acc[gt] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+          }
 #pragma unroll
           for (int s = 0; s < KS; ++s)
 #pragma unroll
@@ -713,28 +755,40 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
 // DROP: the dropout instantiation (layer l+1's input masks in-kernel); without dropout that
 // code is compiled out (same-box A/B: the runtime-conditional form cost 2.5 % per step)
 template <int KS, bool DROP>
-static const void* lstm2_fwd_g(int G) {
+static const void* lstm2_fwd_g(int G, bool xin) {
+  if (xin) return G == 1 ? (const void*)lstm2_fwd_persist_kernel<KS, 1, DROP, true> : nullptr;
   switch (G) {
-    case 1: return (const void*)lstm2_fwd_persist_kernel<KS, 1, DROP>;
-    case 2: return (const void*)lstm2_fwd_persist_kernel<KS, 2, DROP>;
-    case 3: return (const void*)lstm2_fwd_persist_kernel<KS, 3, DROP>;
-    case 4: return (const void*)lstm2_fwd_persist_kernel<KS, 4, DROP>;
+    case 1: return (const void*)lstm2_fwd_persist_kernel<KS, 1, DROP, false>;
+    case 2: return (const void*)lstm2_fwd_persist_kernel<KS, 2, DROP, false>;
+    case 3: return (const void*)lstm2_fwd_persist_kernel<KS, 3, DROP, false>;
+    case 4: return (const void*)lstm2_fwd_persist_kernel<KS, 4, DROP, false>;
   }
   return nullptr;
 }
 
 template <bool DROP>
-static const void* lstm2_pick_t(int H, int G) {
+static const void* lstm2_pick_t(int H, int G, bool xin) {
   switch (H / 128) {
-    case 1: return lstm2_fwd_g<1, DROP>(G);
-    case 2: return lstm2_fwd_g<2, DROP>(G);
-    case 3: return lstm2_fwd_g<3, DROP>(G);
-    case 4: return lstm2_fwd_g<4, DROP>(G);
+    case 1: return lstm2_fwd_g<1, DROP>(G, xin);
+    case 2: return lstm2_fwd_g<2, DROP>(G, xin);
+    case 3: return lstm2_fwd_g<3, DROP>(G, xin);
+    case 4: return lstm2_fwd_g<4, DROP>(G, xin);
   }
   return nullptr;
 }
-static const void* lstm2_pick(int H, int G, bool drop) {
-  return drop ? lstm2_pick_t<true>(H, G) : lstm2_pick_t<false>(H, G);
+static const void* lstm2_pick(int H, int G, bool drop, bool xin = false) {
+  return drop ? lstm2_pick_t<true>(H, G, xin) : lstm2_pick_t<false>(H, G, xin);
+}
+
+// the in-kernel input projection variant exists and is co-resident (G = 1 only)
+bool lstm2_xin_ok(int H, int cus) {
+  for (int drop = 0; drop < 2; ++drop) {
+    const void* fn = lstm2_pick(H, 1, drop, true);
+    int o = 0;
+    if (!fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, fn, 256, 0) != hipSuccess || o < 1)
+      return false;
+  }
+  return cus > 0;
 }
 
 template <int KS, bool DROP>
@@ -797,7 +851,9 @@ static bool lstm2_args_ok(int H, int B, int nbg, int G, int cus) {
 int launch_lstm2_fwd_persist(const Lstm2Args& a, int cus, hipStream_t s) {
   if (!lstm2_args_ok(a.H, a.B, a.nbg, a.G, cus) || !a.hring0 || !a.hring1) return -2;
   void* args[] = {const_cast<Lstm2Args*>(&a)};
-  return hipLaunchKernel(lstm2_pick(a.H, a.G, a.xmask != nullptr), dim3(lstm2_grid(a.H, a.nbg, a.G)), dim3(256), args,
+  if (a.x0 && (a.G != 1 || !lstm2_xin_ok(a.H, cus))) return -2;
+  return hipLaunchKernel(lstm2_pick(a.H, a.G, a.xmask != nullptr, a.x0 != nullptr),
+                         dim3(lstm2_grid(a.H, a.nbg, a.G)), dim3(256), args,
                          0, s) == hipSuccess ? 0 : -3;
 }
 

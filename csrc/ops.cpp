@@ -679,9 +679,13 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
                        const c10::optional<at::Tensor>& clast1,
                        const c10::optional<at::Tensor>& diag,
                        const c10::optional<at::Tensor>& xmask, double xscale,
-                       const c10::optional<at::Tensor>& bias0) {
+                       const c10::optional<at::Tensor>& bias0,
+                       const c10::optional<at::Tensor>& x0,
+                       const c10::optional<at::Tensor>& X0T) {
   for (auto* t : {&W0T, &W1T, &X1T}) check_seq(*t, at::kBFloat16, "W");
-  check_seq(zx0, at::kFloat, "zx0");
+  TORCH_CHECK(has(x0) == has(X0T), "pass x0 and X0T together");
+  const bool xin = has(x0);
+  if (!xin) check_seq(zx0, at::kFloat, "zx0");
   check_seq(bias1, at::kFloat, "bias1");
   for (auto* t : {&hbuf0, &hbuf1, &hring0, &hring1}) check_seq(*t, at::kBFloat16, "hbuf/hring");
   for (auto* t : {&cbuf0, &cbuf1, &hlast0, &hlast1}) check_seq(*t, at::kFloat, "state");
@@ -698,11 +702,20 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
   for (auto* t : {&W0T, &W1T, &X1T})
     TORCH_CHECK(t->size(0) == 4 * H && t->size(1) == H, "weights must be [4H, H]");
   TORCH_CHECK(bias1.numel() == 4 * H, "bias1 must be [4H]");
-  TORCH_CHECK(zx0.size(-1) == 4 * H, "zx0 rows must be 4H wide");
-  if (has(ids)) {
-    TORCH_CHECK(ids->numel() == (int64_t)T * B, "ids must be [T, B]");
+  if (xin) {
+    check_seq(*x0, at::kBFloat16, "x0");
+    check_seq(*X0T, at::kBFloat16, "X0T");
+    TORCH_CHECK(x0->numel() == (int64_t)T * B * H && X0T->size(0) == 4 * H && X0T->size(1) == H,
+                "x0 must be [T*B, H], X0T [4H, H]");
+    TORCH_CHECK(!has(ids) && G == 1 && dcr::lstm2_xin_ok(H, num_cus()),
+                "in-kernel input projection: dense rows, one batch group per workgroup");
   } else {
-    TORCH_CHECK(zx0.numel() == (int64_t)T * B * 4 * H, "zx0 must be [T, B, 4H]");
+    TORCH_CHECK(zx0.size(-1) == 4 * H, "zx0 rows must be 4H wide");
+    if (has(ids)) {
+      TORCH_CHECK(ids->numel() == (int64_t)T * B, "ids must be [T, B]");
+    } else {
+      TORCH_CHECK(zx0.numel() == (int64_t)T * B * 4 * H, "zx0 must be [T, B, 4H]");
+    }
   }
   for (auto* g : {&gates0, &gates1})
     if (has(*g)) TORCH_CHECK((*g)->numel() == (int64_t)T * B * 4 * H, "gates must be [T, B, 4H]");
@@ -711,7 +724,8 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
     TORCH_CHECK(r->numel() >= (int64_t)2 * nbg * 32 * H, "hring must hold [2, ", nbg * 32, ", H]");
   dcr::Lstm2Args a{};
   a.W0T = ptr<bf16>(W0T); a.W1T = ptr<bf16>(W1T); a.X1T = ptr<bf16>(X1T);
-  a.zx0 = ptr<float>(zx0); a.ids = optr<int>(ids); a.zx_ld = 4 * H;
+  a.zx0 = xin ? nullptr : ptr<float>(zx0); a.ids = optr<int>(ids); a.zx_ld = 4 * H;
+  a.x0 = optr<bf16>(x0); a.X0T = optr<bf16>(X0T);
   a.bias1 = ptr<float>(bias1);
   if (has(bias0)) {
     check_seq(*bias0, at::kFloat, "bias0");
@@ -1227,6 +1241,8 @@ TORCH_LIBRARY(dcr, m) {
         [](int64_t H, int64_t B, int64_t force) -> int64_t {
           return dcr::lstm2_plan_g((int)H, (int)B, num_cus(), (int)force);
         });
+  m.def("lstm2_xin_ok(int H) -> bool",
+        [](int64_t H) -> bool { return dcr::lstm2_xin_ok((int)H, num_cus()); });
   m.def("lstm2_nbg(int B, int G) -> int",
         [](int64_t B, int64_t G) -> int64_t { return lstm2_nbg((int)B, (int)G); });
   m.def(
@@ -1236,7 +1252,7 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor(i!) cnt0, Tensor(j!) cnt1, Tensor(k!) err, float forget_bias, int spin_limit, "
       "Tensor(l!) hring0, Tensor(m!) hring1, int G, Tensor(o!)? clast0=None, "
       "Tensor(p!)? clast1=None, Tensor(q!)? diag=None, Tensor? xmask=None, "
-      "float xscale=1.0, Tensor? bias0=None) -> ()");
+      "float xscale=1.0, Tensor? bias0=None, Tensor? x0=None, Tensor? X0T=None) -> ()");
   m.def(
       "lstm2_persist_bwd(Tensor Wh0, Tensor Wh1, Tensor Wx1, Tensor dtop1, Tensor gates0, "
       "Tensor cbuf0, Tensor gates1, Tensor cbuf1, Tensor(a!) dz0, Tensor(b!) dz1, "

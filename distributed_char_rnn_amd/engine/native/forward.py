@@ -59,6 +59,12 @@ class ForwardMixin:
         self.ops.mask_apply(x2, bits, scale, o)
         return o
 
+    def _xin_ok(self) -> bool:
+        v = getattr(self, "_xin_cache", None)
+        if v is None:
+            v = self._xin_cache = bool(self.ops.lstm2_xin_ok(self.H))
+        return v
+
     # ------------------------------------------------------------------ forward
     def _forward(self, ids_tm: torch.Tensor, state, training: bool, want_logits: bool = True,
                  logits_bias: bool = True, extra_tasks: Optional[list] = None):
@@ -110,6 +116,7 @@ class ForwardMixin:
                                           x_prev, lw.bias, cnt_zeroed=True, clast32=lb.clast32)
                 x_prev = lb.hbuf[1:]
                 continue
+            xin = False
             if gather:
                 zx = self._head["table"]
                 ids_arg = ids_tm
@@ -125,13 +132,21 @@ class ForwardMixin:
                     if inb is not None:
                         X = self._masked(X, inb, dm["sin"], out=lb.x_drop)
                 lb.x_in = X if X.is_contiguous() else X.contiguous()
-                # the two-layer LSTM and the GRU kernels add the input bias in their epilogue:
-                # the library GEMM with a bias ran as GEMM + a separate [N, GW] fp32 add pass
-                # (41 us / 114 us per layer in the dropout headline / GRU-1024 B = 256 profiles)
-                bias_in_kernel = ((P.pair and layer + 1 < self.L) or P.gru_persist)
-                mm_into(lb.x_in, lw.Wx, lb.zx.view(N, self.GW),
-                        bias=None if bias_in_kernel else lw.bias)
-                zx = lb.zx
+                # G = 1 two-layer forward: the input projection x·W_x runs in-kernel from these
+                # bf16 rows (no [N, 4H] fp32 zx round trip through HBM)
+                xin = (P.pair and layer + 1 < self.L and P.pair_g == 1 and lw.WxT is not None
+                       and self.knobs.on("xin") and self._xin_ok())
+                if xin:
+                    zx = lb.x_in
+                else:
+                    # the two-layer LSTM and the GRU kernels add the input bias in their
+                    # epilogue: the library GEMM with a bias ran as GEMM + a separate [N, GW]
+                    # fp32 add pass (41 us / 114 us per layer in the dropout headline / GRU-1024
+                    # B = 256 profiles)
+                    bias_in_kernel = ((P.pair and layer + 1 < self.L) or P.gru_persist)
+                    mm_into(lb.x_in, lw.Wx, lb.zx.view(N, self.GW),
+                            bias=None if bias_in_kernel else lw.bias)
+                    zx = lb.zx
             if P.pair and layer + 1 < self.L:
                 # layers (l, l+1) as one wavefront launch (lstm2_persist.hip): T+1 ticks; layer
                 # l+1's input dropout is applied to its fragments in-kernel
@@ -144,7 +159,8 @@ class ForwardMixin:
                                            FORGET_BIAS, self.spin_limit, *bufs["hrings"],
                                            P.pair_g, lb.clast32, lb1.clast32, None, xm,
                                            dm["sin"] if dm else 1.0,
-                                           lw.bias if ids_arg is None else None)
+                                           lw.bias if ids_arg is None else None,
+                                           lb.x_in if xin else None, lw.WxT if xin else None)
                 # layer l+1's (masked) input rows for its weight gradient
                 lb1.x_in = (self._masked(lb.hbuf[1:], xm, dm["sin"], out=lb1.x_drop)
                             if xm is not None else lb.hbuf[1:].reshape(N, H))

@@ -43,8 +43,12 @@ class LayoutsMixin:
             if self.cfg.model in ("lstm", "rnn"):
                 k, b = s.view(names[0]), s.view(names[1])
                 GW = k.shape[1]
+                # W_xᵀ: the fused input projections of layers above 0, and of layer 0 when
+                # dropout sends its masked embedding rows through the dense route (the two-layer
+                # forward then projects them in-kernel)
+                drop = self.cfg.input_keep_prob < 1.0 or self.cfg.output_keep_prob < 1.0
                 lw = LayerWeights(Wx=e(D, GW), Wx32=k[:D], bias=b, Wh=e(H, GW), WhT=e(GW, H),
-                                  WxT=e(GW, D) if (layer > 0 and self.cfg.model == "lstm")
+                                  WxT=e(GW, D) if (self.cfg.model == "lstm" and (layer > 0 or drop))
                                   else None)
                 T += [(k[D:], lw.Wh, 0), (k[D:], lw.WhT, 1), (k[:D], lw.Wx, 0)]
                 if lw.WxT is not None:
