@@ -41,8 +41,15 @@ def split_k(K: int, M: int, Nn: int) -> int:
     such an output into a few dozen workgroups (the 512x2048, K=32768 weight gradient ran on 73
     of 256 CUs at 335 TFLOP/s), so the reduction is split into S batched slices instead
     (scripts/bench_gemms.py: 205 -> 97 us at S=8; the 512x65 head gradient 133 -> 27 us)."""
-    if K < 8192 or -(-M // 128) * -(-Nn // 256) >= 128:
+    if K < 1024 or -(-M // 128) * -(-Nn // 256) >= 128:
         return 1
+    if K < 8192:
+        # short token reductions (the reference default, B = 50 x T = 50 = 2500 tokens): the
+        # [128, 512] weight gradients ran on 8 workgroups at ~30 us each; slices of >= 256 tokens
+        S = 8
+        while S > 1 and (K % S or K // S < 256):
+            S //= 2
+        return S
     S = 8 if M * Nn >= (1 << 18) else 16
     while S > 1 and (K % S or K // S < 1024):
         S //= 2

@@ -13,3 +13,5 @@ run "lstm2048x4 seq512 B64           " --hidden 2048 --layers 4 --seq 512 --batc
 run "lstm2048x4 seq512 B1024 (large)  " --hidden 2048 --layers 4 --seq 512 --batch 1024 --steps 2 --warmup 1 || exit 1
 run "lstm512x2 seq128 B256 vocab8192 " --vocab 8192 --steps 10 --warmup 3 || exit 1
 run "lstm128x1 seq32 B50 (tiny)      " --hidden 128 --layers 1 --seq 32 --batch 64 --steps 20 --warmup 5 || exit 1
+run "lstm128x2 seq50 B50 (ref default)" --hidden 128 --layers 2 --seq 50 --batch 50 --steps 30 --warmup 5 || exit 1
+run "lstm512x2 seq128 B256 dropout0.8 " --input_keep_prob 0.8 --output_keep_prob 0.8 --steps 30 --warmup 5 || exit 1
