@@ -239,6 +239,43 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     // (also orders this tick's first partial stores after the previous tick's epilogue reads)
     __syncthreads();
     STAMPG(0, 2)
+    // payload fragments of group g: slot 0 is row-major [B, H] (rows >= B read as zero: buffer
+    // bounds); later slots come from the fragment-tiled rings: one contiguous 1 KB load per
+    // (tile, k-step).  Double-buffered by group: group g+1's loads are issued before group g's
+    // MFMAs (the column's hand-off covers all its groups), so their latency overlaps group g's
+    // MFMA and epilogue phases instead of opening group g+1's.
+    // (only while the second buffer fits: at KS = 4, G >= 3 it spilled)
+    constexpr bool PREF = G > 1 && KS * G <= 8;
+    bf16x8 pf0[PREF ? 2 : 1][2][KS], pf1[PREF ? 2 : 1][2][KS];
+    auto load_group = [&](int g, bf16x8 (&hf0)[2][KS], bf16x8 (&hf1)[2][KS]) {
+      const int bg = col * G + g;
+      if (ld0) {
+        const bool ring0 = tau > 0;
+        const __amdgpu_buffer_rsrc_t r0 =
+            ring0 ? make_rsrc(a.hring0 + (size_t)(tau & 1) * ringsz, sizeof(bf16) * ringsz)
+                  : make_rsrc(a.hbuf0, sizeof(bf16) * (size_t)B * H);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int s = 0; s < KS; ++s)
+            hf0[j][s] = ring0 ? ld8_sc1(r0, frag_load_off(2 * bg + j, w * KS + s, H, lane))
+                              : ld8_sc1(r0, rm_lane + rm_off(bg, j, s));
+      }
+      if (ld1) {
+        const int s1 = tau - LAG;
+        const bool ring1 = s1 > 0;
+        const __amdgpu_buffer_rsrc_t r1 =
+            ring1 ? make_rsrc(a.hring1 + (size_t)(s1 & 1) * ringsz, sizeof(bf16) * ringsz)
+                  : make_rsrc(a.hbuf1, sizeof(bf16) * (size_t)B * H);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int s = 0; s < KS; ++s)
+            hf1[j][s] = ring1 ? ld8_sc1(r1, frag_load_off(2 * bg + j, w * KS + s, H, lane))
+                              : ld8_sc1(r1, rm_lane + rm_off(bg, j, s));
+      }
+    };
+    load_group(0, pf0[0], pf1[0]);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       STAMPG(g, 7)  // group phase start
@@ -251,35 +288,12 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
       for (int gt = 0; gt < 4; ++gt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) zx[gt][r] = zxn[gt][r];
-      bf16x8 hf0[2][KS], hf1[2][KS];
-      {
-        // slot 0 is row-major [B, H] (rows >= B read as zero: buffer bounds); later slots come
-        // from the fragment-tiled rings: one contiguous 1 KB load per (tile, k-step)
-        if (ld0) {
-          const bool ring0 = tau > 0;
-          const __amdgpu_buffer_rsrc_t r0 =
-              ring0 ? make_rsrc(a.hring0 + (size_t)(tau & 1) * ringsz, sizeof(bf16) * ringsz)
-                    : make_rsrc(a.hbuf0, sizeof(bf16) * (size_t)B * H);
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int s = 0; s < KS; ++s)
-              hf0[j][s] = ring0 ? ld8_sc1(r0, frag_load_off(2 * bg + j, w * KS + s, H, lane))
-                                : ld8_sc1(r0, rm_lane + rm_off(bg, j, s));
-        }
-        if (ld1) {
-          const int s1 = tau - LAG;
-          const bool ring1 = s1 > 0;
-          const __amdgpu_buffer_rsrc_t r1 =
-              ring1 ? make_rsrc(a.hring1 + (size_t)(s1 & 1) * ringsz, sizeof(bf16) * ringsz)
-                    : make_rsrc(a.hbuf1, sizeof(bf16) * (size_t)B * H);
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int s = 0; s < KS; ++s)
-              hf1[j][s] = ring1 ? ld8_sc1(r1, frag_load_off(2 * bg + j, w * KS + s, H, lane))
-                                : ld8_sc1(r1, rm_lane + rm_off(bg, j, s));
-        }
+      bf16x8 (&hf0)[2][KS] = pf0[PREF ? (g & 1) : 0];
+      bf16x8 (&hf1)[2][KS] = pf1[PREF ? (g & 1) : 0];
+      if constexpr (PREF) {
+        if (g + 1 < G) load_group(g + 1, pf0[(g + 1) & 1], pf1[(g + 1) & 1]);
+      } else {
+        if (g > 0) load_group(g, pf0[0], pf1[0]);
       }
       if (g + 1 < G) zx_load(zrows[g + 1], zxn);
       // mask byte of this lane's x-part fragment (row 16 j + lane%16 of the group, k = kbase +
