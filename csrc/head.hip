@@ -188,9 +188,16 @@ __global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs a) {
 #pragma unroll
         for (int tp = 0; tp < TPW; ++tp) {
           const int n = nb + tp * 16 + nl;
-          if (n < N)
-            *reinterpret_cast<float4*>(a.dtop + (size_t)n * H + (ht0 + j) * 16 + 4 * g) =
+          const int h0 = (ht0 + j) * 16 + 4 * g;
+          if (n < N) {
+            if (a.omask) {  // output dropout: this lane's 4 units' bits of token n
+              const unsigned m = (unsigned)a.omask[(size_t)n * (H / 8) + (h0 >> 3)] >> (h0 & 7);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) d[tp][r] = (m >> r) & 1u ? d[tp][r] * a.oscale : 0.f;
+            }
+            *reinterpret_cast<float4*>(a.dtop + (size_t)n * H + h0) =
                 make_float4(d[tp][0], d[tp][1], d[tp][2], d[tp][3]);
+          }
         }
       }
     }

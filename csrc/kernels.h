@@ -291,6 +291,8 @@ struct HeadArgs {
   bf16* dlogits;        // [N, V] bf16 or nullptr
   float* dtop;          // [N, H] fp32 or nullptr
   float* part;          // [grid, VP+1] partials workspace
+  const uint8_t* omask; // optional dropout bits of O ([N, H/8], dropout.hip): dtop is written
+  float oscale;         //   masked and scaled by 1/keep (the output dropout's backward)
 };
 int head_vpad(int V);
 int head_kpad(int V);

@@ -966,7 +966,8 @@ void head(const at::Tensor& O, const at::Tensor& WsT, const c10::optional<at::Te
           const c10::optional<at::Tensor>& logits, const c10::optional<at::Tensor>& row_loss,
           const c10::optional<at::Tensor>& dlogits, const c10::optional<at::Tensor>& dtop,
           const c10::optional<at::Tensor>& db, at::Tensor& part,
-          const c10::optional<at::Tensor>& loss) {
+          const c10::optional<at::Tensor>& loss, const c10::optional<at::Tensor>& omask,
+          double oscale) {
   TORCH_CHECK(O.is_cuda() && O.dim() == 2 && O.scalar_type() == at::kBFloat16 && O.stride(1) == 1,
               "O must be a row-major bf16 [N, H] GPU tensor");
   const int N = (int)O.size(0), H = (int)O.size(1), V = (int)bias.numel();
@@ -1012,6 +1013,13 @@ void head(const at::Tensor& O, const at::Tensor& WsT, const c10::optional<at::Te
   a.dlogits = optr<bf16>(dlogits);
   a.dtop = optr<float>(dtop);
   a.part = ptr<float>(part);
+  if (has(omask)) {
+    TORCH_CHECK(has(dtop) && omask->is_cuda() && omask->scalar_type() == at::kByte &&
+                    omask->is_contiguous() && omask->numel() == (int64_t)N * (H / 8) && H % 8 == 0,
+                "omask: uint8 [N, H/8] bits, with dtop");
+    a.omask = omask->data_ptr<uint8_t>();
+    a.oscale = (float)oscale;
+  }
   TORCH_CHECK(dcr::launch_head(a, num_cus(), optr<float>(db), optr<float>(loss), cur_stream()) == 0,
               "fused head launch failed");
 }
@@ -1228,7 +1236,8 @@ TORCH_LIBRARY(dcr, m) {
   m.def(
       "head(Tensor O, Tensor WsT, Tensor? Wsk, Tensor bias, Tensor? targets, float grad_scale, "
       "Tensor(a!)? logits, Tensor(b!)? row_loss, Tensor(c!)? dlogits, Tensor(d!)? dtop, "
-      "Tensor(e!)? db, Tensor(f!) part, Tensor(g!)? loss) -> ()");
+      "Tensor(e!)? db, Tensor(f!) part, Tensor(g!)? loss, Tensor? omask=None, "
+      "float oscale=1.0) -> ()");
   m.def("prep(Tensor[] src, Tensor(a!)[] dst, int[] mode, Tensor[] extra) -> ()");
   m.def("prep_max_tasks() -> int", []() -> int64_t { return dcr::kPrepMaxTasks; });
   m.def("wgrad(Tensor[] A, Tensor[] B, Tensor(a!) part) -> ()");

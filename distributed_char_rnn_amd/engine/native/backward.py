@@ -38,12 +38,18 @@ class BackwardMixin:
         li = self._steps & 1
         loss_buf = bufs["loss"][li, :1]
         s, hd = self.store, self._head
+        drop = self._dropout(True)
+        dm = self.last_dropout_masks if drop else None
+        head_omask = None  # the top output dropout applied by the head kernel to dtop
         if self.fused_head:
             # one launch: logits (only if asked for) -> CE -> bf16 dlogits, d softmax_b, dtop
+            # (masked by the top layer's output dropout in-kernel: no fp32 pass over dtop)
+            head_omask = dm["out"] if (dm is not None and self.knobs.on("head_omask")) else None
             self.ops.head(O, hd["WsT"], hd["Wsk"], hd["bs"], tgt, 1.0 / N,
                           logits if want_extras else None, bufs["row_loss"], dlog,
                           bufs["dtop"].view(N, H), s.gview("rnnlm/softmax_b"),
-                          bufs["head_part"], loss_buf)
+                          bufs["head_part"], loss_buf, head_omask,
+                          dm["sout"] if dm is not None else 1.0)
             mm_tn(O, dlog, s.gview("rnnlm/softmax_w"), q=q)
             dtop = bufs["dtop"].view(T, B, H)
         elif wide:
@@ -80,8 +86,6 @@ class BackwardMixin:
         if on_ready is not None:
             sb = s.by_name["rnnlm/softmax_b"]
             on_ready(sb.offset + sb.numel)
-        drop = self._dropout(True)
-        dm = self.last_dropout_masks if drop else None
         paired_done = -1  # lower layer whose BPTT already ran inside a two-layer wavefront
         # TF clip-norm term from dx_tok = dZ0·W_x0ᵀ: needed as an extra GEMM only on the layer-0
         # gather route (every other route materialises dx_tok anyway)
@@ -93,7 +97,8 @@ class BackwardMixin:
             names = [sp.name for sp in cell_specs(self.cfg, layer)]
             pair_hi = P.pair_bwd and layer % 2 == 1 and dtop is not None
             # the top layer's output dropout
-            omask = dm["out"] if (dm is not None and layer == self.L - 1) else None
+            omask = (dm["out"] if (dm is not None and layer == self.L - 1
+                                   and head_omask is None) else None)
             if dtop is not None:
                 dtop = dtop.contiguous()
                 if omask is not None:

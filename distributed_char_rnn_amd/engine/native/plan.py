@@ -41,6 +41,7 @@ DEBUG_KEYS = {
     "seg_sort": "0: unsorted atomic embedding gradient for wide vocabularies",
     "lib_graph": "0: eager library-step loops (no hipGraph replay)",
     "sample_graph": "0: eager sampling loop (no hipGraph replay)",
+    "head_omask": "0: top output dropout applied to dtop by a separate pass, not the head",
     "xin": "0: library GEMM for a dense layer-l input of the G = 1 two-layer forward",
     "wgrad": "1: hand-written wgrad kernel for the weight gradients (default: library split-K)",
     "gru_ub": "1: 16-unit GRU workgroups (C++)",
