@@ -17,16 +17,22 @@ namespace dcr {
 constexpr int kDropThreads = 256;
 
 // thread -> 32 consecutive elements (4 bytes, one dword store).  Each 64-bit hash yields four
-// 16-bit uniforms (keep resolution 2^-16): 8 hashes per 32 elements.
-__global__ void __launch_bounds__(kDropThreads) dropout_bits_kernel(
-    unsigned* __restrict__ bits, int64_t nwords, uint64_t seed, uint64_t stream, unsigned kt) {
-  const uint64_t key = seed ^ mix64(stream * 0x632BE59BD9B4E019ull);
-  for (int64_t i = blockIdx.x * (int64_t)kDropThreads + threadIdx.x; i < nwords;
+// 16-bit uniforms (keep resolution 2^-16): 8 hashes per 32 elements.  One launch fills all the
+// step's masks: segment m (nwords each, consecutive in memory) draws from its own stream with
+// its own keep threshold, element indices local to the segment (the bits equal a launch per mask).
+__global__ void __launch_bounds__(kDropThreads) dropout_bits_kernel(unsigned* __restrict__ bits,
+                                                                    DropSegs d, uint64_t seed) {
+  const int64_t total = d.nwords * d.n;
+  for (int64_t i = blockIdx.x * (int64_t)kDropThreads + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * kDropThreads) {
+    const int m = (int)(i / d.nwords);
+    const int64_t li = i - (int64_t)m * d.nwords;
+    const uint64_t key = seed ^ mix64(d.stream[m] * 0x632BE59BD9B4E019ull);
+    const unsigned kt = d.kt[m];
     unsigned w = 0;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      const uint64_t r = mix64(key + (uint64_t)i * 8 + q);
+      const uint64_t r = mix64(key + (uint64_t)li * 8 + q);
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         w |= ((unsigned)(r >> (16 * e)) & 0xFFFFu) < kt ? 1u << (4 * q + e) : 0u;
@@ -108,13 +114,14 @@ static int drop_grid(int64_t n) {
   return (int)(b < 4096 ? (b > 0 ? b : 1) : 4096);
 }
 
-void launch_dropout_bits(uint8_t* bits, int64_t nbytes, uint64_t seed, uint64_t stream,
-                         float keep, hipStream_t s) {
-  const int64_t nw = nbytes / 4;
+unsigned drop_threshold(float keep) {
   const double kt = (double)keep * 65536.0;
-  dropout_bits_kernel<<<drop_grid(nw), kDropThreads, 0, s>>>(
-      reinterpret_cast<unsigned*>(bits), nw, seed, stream,
-      kt >= 65536.0 ? 65536u : (kt <= 0.0 ? 0u : (unsigned)(kt + 0.5)));
+  return kt >= 65536.0 ? 65536u : (kt <= 0.0 ? 0u : (unsigned)(kt + 0.5));
+}
+
+void launch_dropout_bits(uint8_t* bits, const DropSegs& d, uint64_t seed, hipStream_t s) {
+  dropout_bits_kernel<<<drop_grid(d.nwords * d.n), kDropThreads, 0, s>>>(
+      reinterpret_cast<unsigned*>(bits), d, seed);
 }
 
 void launch_mask_apply(const void* in, bool in_bf16, int64_t ld_in, void* out, bool out_bf16,

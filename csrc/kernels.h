@@ -103,8 +103,15 @@ void launch_xent(const float* logits, const int* targets, int N, int V, float gr
                  float* row_loss, bf16* dlogits, float* partial, float* loss_out, hipStream_t s);
 
 // ---- dropout.hip: bit masks ([rows, K/8] bytes) -----------------------------------------------
-void launch_dropout_bits(uint8_t* bits, int64_t nbytes, uint64_t seed, uint64_t stream,
-                         float keep, hipStream_t s);
+constexpr int kDropMaxSegs = 16;
+struct DropSegs {             // n masks of nwords 32-bit words each, consecutive in memory
+  int n;
+  int64_t nwords;
+  uint64_t stream[kDropMaxSegs];
+  unsigned kt[kDropMaxSegs];  // keep threshold on a 16-bit uniform (drop_threshold)
+};
+unsigned drop_threshold(float keep);
+void launch_dropout_bits(uint8_t* bits, const DropSegs& d, uint64_t seed, hipStream_t s);
 void launch_mask_apply(const void* in, bool in_bf16, int64_t ld_in, void* out, bool out_bf16,
                        int64_t ld_out, const uint8_t* bits, int64_t rows, int K, float scale,
                        hipStream_t s);

@@ -620,8 +620,35 @@ void dropout_bits(at::Tensor& bits, int64_t seed, int64_t stream, double keep) {
               "bits must be a contiguous uint8 GPU tensor");
   TORCH_CHECK(bits.numel() % 4 == 0 && (reinterpret_cast<uintptr_t>(bits.data_ptr()) & 3) == 0,
               "bits: a whole number of aligned 32-bit words");
-  dcr::launch_dropout_bits(reinterpret_cast<uint8_t*>(bits.data_ptr()), bits.numel(),
-                           (uint64_t)seed, (uint64_t)stream, (float)keep, cur_stream());
+  dcr::DropSegs d{};
+  d.n = 1;
+  d.nwords = bits.numel() / 4;
+  d.stream[0] = (uint64_t)stream;
+  d.kt[0] = dcr::drop_threshold((float)keep);
+  dcr::launch_dropout_bits(reinterpret_cast<uint8_t*>(bits.data_ptr()), d, (uint64_t)seed,
+                           cur_stream());
+}
+
+// all masks of a step in one launch: bits [n, ...] (segment m = bits[m]), streams / keeps per m
+void dropout_bits_multi(at::Tensor& bits, int64_t seed, at::IntArrayRef streams,
+                        at::ArrayRef<double> keeps) {
+  TORCH_CHECK(bits.is_cuda() && bits.is_contiguous() && bits.scalar_type() == at::kByte &&
+                  bits.dim() >= 1, "bits must be a contiguous uint8 GPU tensor [n, ...]");
+  const int n = (int)bits.size(0);
+  TORCH_CHECK(n >= 1 && n <= dcr::kDropMaxSegs && (int)streams.size() == n &&
+                  (int)keeps.size() == n, "dropout_bits_multi: 1..", dcr::kDropMaxSegs, " masks");
+  const int64_t per = bits.numel() / n;
+  TORCH_CHECK(per % 4 == 0 && (reinterpret_cast<uintptr_t>(bits.data_ptr()) & 3) == 0,
+              "bits: a whole number of aligned 32-bit words per mask");
+  dcr::DropSegs d{};
+  d.n = n;
+  d.nwords = per / 4;
+  for (int i = 0; i < n; ++i) {
+    d.stream[i] = (uint64_t)streams[i];
+    d.kt[i] = dcr::drop_threshold((float)keeps[i]);
+  }
+  dcr::launch_dropout_bits(reinterpret_cast<uint8_t*>(bits.data_ptr()), d, (uint64_t)seed,
+                           cur_stream());
 }
 
 void mask_apply(const at::Tensor& in, const at::Tensor& bits, double scale, at::Tensor& out) {
@@ -1269,6 +1296,7 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor(g!) cnt0, Tensor(h!) cnt1, Tensor(i!) err, int spin_limit, int G, "
       "Tensor(j!)? diag=None, Tensor? xmask=None, float xscale=1.0) -> ()");
   m.def("dropout_bits(Tensor(a!) bits, int seed, int stream, float keep) -> ()");
+  m.def("dropout_bits_multi(Tensor(a!) bits, int seed, int[] streams, float[] keeps) -> ()");
   m.def("mask_apply(Tensor input, Tensor bits, float scale, Tensor(a!) out) -> ()");
   m.def("embed_dropout(Tensor ids, Tensor E, Tensor? bits, float scale, Tensor(a!) out) -> ()");
   m.def("sample_supported(int V, int H) -> int", [](int64_t V, int64_t H) -> int64_t {
@@ -1317,6 +1345,7 @@ TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("lstm2_persist_fwd", &lstm2_persist_fwd);
   m.impl("lstm2_persist_bwd", &lstm2_persist_bwd);
   m.impl("dropout_bits", &dropout_bits);
+  m.impl("dropout_bits_multi", &dropout_bits_multi);
   m.impl("mask_apply", &mask_apply);
   m.impl("embed_dropout", &embed_dropout);
   m.impl("sample_step", &sample_step);

@@ -33,17 +33,23 @@ class ForwardMixin:
         key = (T, B)
         m = self._dm_bufs.get(key)
         if m is None:
-            nb = lambda: torch.empty(T, B, self.H // 8, dtype=torch.uint8, device=self.dev)  # noqa: E731
+            # all masks of a step in one buffer, filled by one launch (segment per mask)
+            n_in = self.L if p_in < 1.0 else 0
+            n = n_in + (1 if p_out < 1.0 else 0)
+            allb = torch.empty(n, T, B, self.H // 8, dtype=torch.uint8, device=self.dev)
             m = self._dm_bufs[key] = dict(
-                inb=[nb() for _ in range(self.L)] if p_in < 1.0 else [None] * self.L,
-                out=nb() if p_out < 1.0 else None)
+                all=allb, n_in=n_in,
+                inb=[allb[i] for i in range(n_in)] if n_in else [None] * self.L,
+                out=allb[n_in] if p_out < 1.0 else None)
         self._drop_step += 1
         stream = self._drop_step << 8
-        for layer, bits in enumerate(m["inb"]):
-            if bits is not None:
-                self.ops.dropout_bits(bits, self._drop_seed, stream + layer, p_in)
+        streams = [stream + layer for layer in range(m["n_in"])]
+        keeps = [p_in] * m["n_in"]
         if m["out"] is not None:
-            self.ops.dropout_bits(m["out"], self._drop_seed, stream + 255, p_out)
+            streams.append(stream + 255)
+            keeps.append(p_out)
+        if streams:
+            self.ops.dropout_bits_multi(m["all"], self._drop_seed, streams, keeps)
         dm = dict(inb=m["inb"], out=m["out"], sin=1.0 / p_in, sout=1.0 / p_out)
         self.last_dropout_masks = dm
         return dm
