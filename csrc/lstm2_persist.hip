@@ -794,15 +794,22 @@ static const void* lstm2_pick(int H, int G, bool drop, bool xin = false) {
   return drop ? lstm2_pick_t<true>(H, G, xin) : lstm2_pick_t<false>(H, G, xin);
 }
 
-// the in-kernel input projection variant exists and is co-resident (G = 1 only)
+// the in-kernel input projection variant exists and is co-resident (G = 1 only); the answer
+// per (H, cus) is cached (the launcher asks on every step)
 bool lstm2_xin_ok(int H, int cus) {
+  static int cache_key = -1, cache_val = 0;
+  const int key = H * 4096 + cus;
+  if (key == cache_key) return cache_val != 0;
+  cache_key = key;
+  cache_val = 0;
   for (int drop = 0; drop < 2; ++drop) {
     const void* fn = lstm2_pick(H, 1, drop, true);
     int o = 0;
     if (!fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, fn, 256, 0) != hipSuccess || o < 1)
       return false;
   }
-  return cus > 0;
+  cache_val = cus > 0;
+  return cache_val != 0;
 }
 
 template <int KS, bool DROP>

@@ -138,10 +138,12 @@ class ForwardMixin:
                     if inb is not None:
                         X = self._masked(X, inb, dm["sin"], out=lb.x_drop)
                 lb.x_in = X if X.is_contiguous() else X.contiguous()
-                # G = 1 two-layer forward: the input projection x·W_x runs in-kernel from these
-                # bf16 rows (no [N, 4H] fp32 zx round trip through HBM)
+                # opt-in (DCR_DEBUG=xin=1): the G = 1 two-layer forward projects these bf16 rows
+                # in-kernel (no [N, 4H] fp32 zx round trip); measured slower than the library
+                # GEMM + zx once the forward's payload loads moved first (dropout headline 2.32
+                # vs 2.20 ms, same box)
                 xin = (P.pair and layer + 1 < self.L and P.pair_g == 1 and lw.WxT is not None
-                       and self.knobs.on("xin") and self._xin_ok())
+                       and self.knobs.debug.get("xin") == "1" and self._xin_ok())
                 if xin:
                     zx = lb.x_in
                 else:

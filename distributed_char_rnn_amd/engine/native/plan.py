@@ -42,7 +42,7 @@ DEBUG_KEYS = {
     "lib_graph": "0: eager library-step loops (no hipGraph replay)",
     "sample_graph": "0: eager sampling loop (no hipGraph replay)",
     "head_omask": "0: top output dropout applied to dtop by a separate pass, not the head",
-    "xin": "0: library GEMM for a dense layer-l input of the G = 1 two-layer forward",
+    "xin": "1: in-kernel input projection of a dense layer-l input (G = 1 two-layer forward)",
     "wgrad": "1: hand-written wgrad kernel for the weight gradients (default: library split-K)",
     "gru_ub": "1: 16-unit GRU workgroups (C++)",
     "gru_nt": "N: N batch tiles of 16 rows per GRU workgroup (C++)",
