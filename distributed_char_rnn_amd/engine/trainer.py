@@ -282,6 +282,7 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
             graphed = GraphedStep(model, opt, log=lambda m: _log(m, rank))
         elif args.graph == "on":
             _log(f"--graph on: not available ({why}); eager steps", rank)
+    dev_batches = _device_batches(loader, nb, device)
     stop = False
     state = None
     for e in range(start_epoch, args.num_epochs):
@@ -296,6 +297,8 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
         for b in range(b0, nb):
             t0 = time.time()
             x, y = loader.next_batch()
+            if dev_batches is not None:  # the same batch, already resident on the device
+                x, y = dev_batches[0][b], dev_batches[1][b]
             want = chief and summary_every > 0 and (global_step % summary_every == 0)
             if zstep is not None:  # sharded optimizer step (ZeRO-1)
                 with prof.phase("fwd_bwd"):
@@ -355,6 +358,24 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
         print(prof.table(), flush=True)
     logger.close()
     return 0
+
+
+DEVICE_BATCHES_MAX_BYTES = 4 << 30
+
+
+def _device_batches(loader, nb: int, device: torch.device):
+    """The epoch's x / y batches as two device-resident int32 [nb, B, T] tensors, uploaded
+    once (the reference's feed_dict copies every batch, train.py:203; here a step then needs no
+    pinning or host-to-device copy).  None on the CPU, or when the batches would take more than
+    DEVICE_BATCHES_MAX_BYTES of HBM (per-step copies then, models/char_rnn.py _as_ids)."""
+    if device.type != "cuda" or nb == 0:
+        return None
+    nbytes = 2 * 4 * nb * int(np.asarray(loader.x_batches[0]).size)
+    if nbytes > DEVICE_BATCHES_MAX_BYTES:
+        return None
+    up = lambda bs: torch.from_numpy(  # noqa: E731
+        np.ascontiguousarray(np.stack(bs[:nb]), dtype=np.int32)).to(device)
+    return up(loader.x_batches), up(loader.y_batches)
 
 
 def _broadcast_state(ctx, model: CharRNN, sd, batch: int, device):

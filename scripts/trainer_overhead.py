@@ -1,0 +1,34 @@
+"""Per-step wall time of the real training loop (engine/trainer.py) on the reference defaults
+(2-layer LSTM-128, B = 50, T = 50, tinyshakespeare), with and without the device-resident batch
+cache (trainer._device_batches), next to bench.py's time for the same step.  GPU box:
+    python scripts/trainer_overhead.py [eager|graph]"""
+import json
+import os
+import statistics
+import sys
+import tempfile
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_char_rnn_amd.engine import trainer  # noqa: E402
+
+graph = sys.argv[1] if len(sys.argv) > 1 else "off"
+
+
+def run(cache: bool) -> float:
+    orig = trainer._device_batches
+    if not cache:
+        trainer._device_batches = lambda *a: None
+    d = tempfile.mkdtemp()
+    mf = os.path.join(d, "m.jsonl")
+    try:
+        trainer.main(["--data_dir", "data/tinyshakespeare", "--save_dir", d + "/s", "--log_dir",
+                      d + "/l", "--max_steps", "400", "--save_every", "100000", "--log_every",
+                      "100000", "--metrics_file", mf, "--graph", graph])
+    finally:
+        trainer._device_batches = orig
+    rows = [r for r in map(json.loads, open(mf)) if "time_per_batch" in r]
+    return statistics.median(r["time_per_batch"] for r in rows[100:]) * 1e3
+
+
+for cache in (False, True, False, True):
+    print(f"graph={graph} device_batches={cache}: median {run(cache):.3f} ms/step", flush=True)
