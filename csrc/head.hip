@@ -77,21 +77,6 @@ __global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs a) {
       bf16x8 bo[TPW];
 #pragma unroll
       for (int tp = 0; tp < TPW; ++tp) bo[tp] = ld8(orow[tp] + k);
-      if (a.o_out) {
-        // the top layer's output dropout applied on load (bits of units k + 8g .. + 7 of
-        // token n: one byte), the masked row stored for the softmax_w gradient GEMM -- the
-        // same float(x) * scale -> bf16 rounding as mask_apply_kernel
-#pragma unroll
-        for (int tp = 0; tp < TPW; ++tp) {
-          const int n = nb + tp * 16 + nl;
-          const int nc = min(n, N - 1);
-          const unsigned m = a.omask[(size_t)nc * (H / 8) + (k >> 3) + g];
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            bo[tp][e] = f2bf((m >> e) & 1u ? (float)bo[tp][e] * a.oscale : 0.f);
-          if (n < N) *reinterpret_cast<bf16x8*>(a.o_out + (size_t)n * H + k + 8 * g) = bo[tp];
-        }
-      }
 #pragma unroll
       for (int vt = 0; vt < NVT; ++vt) {
         const bf16x8 af = ld8(wrow + (size_t)vt * 16 * H + k);

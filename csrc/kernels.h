@@ -300,8 +300,6 @@ struct HeadArgs {
   float* part;          // [grid, VP+1] partials workspace
   const uint8_t* omask; // optional dropout bits of O ([N, H/8], dropout.hip): dtop is written
   float oscale;         //   masked and scaled by 1/keep (the output dropout's backward)
-  bf16* o_out;          // optional [N, H] (with omask): O masked and scaled as it is loaded,
-                        //   stored here for the softmax_w gradient; the logits use it too
 };
 int head_vpad(int V);
 int head_kpad(int V);

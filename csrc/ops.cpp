@@ -994,7 +994,7 @@ void head(const at::Tensor& O, const at::Tensor& WsT, const c10::optional<at::Te
           const c10::optional<at::Tensor>& dlogits, const c10::optional<at::Tensor>& dtop,
           const c10::optional<at::Tensor>& db, at::Tensor& part,
           const c10::optional<at::Tensor>& loss, const c10::optional<at::Tensor>& omask,
-          double oscale, const c10::optional<at::Tensor>& o_out) {
+          double oscale) {
   TORCH_CHECK(O.is_cuda() && O.dim() == 2 && O.scalar_type() == at::kBFloat16 && O.stride(1) == 1,
               "O must be a row-major bf16 [N, H] GPU tensor");
   const int N = (int)O.size(0), H = (int)O.size(1), V = (int)bias.numel();
@@ -1046,13 +1046,6 @@ void head(const at::Tensor& O, const at::Tensor& WsT, const c10::optional<at::Te
                 "omask: uint8 [N, H/8] bits, with dtop");
     a.omask = omask->data_ptr<uint8_t>();
     a.oscale = (float)oscale;
-  }
-  if (has(o_out)) {
-    TORCH_CHECK(has(omask), "o_out needs omask");
-    check_seq(*o_out, at::kBFloat16, "o_out");
-    TORCH_CHECK(o_out->numel() == (int64_t)N * H, "o_out must be [N, H]");
-    TORCH_CHECK(o_out->data_ptr() != O.data_ptr(), "o_out must not alias O");
-    a.o_out = ptr<bf16>(*o_out);
   }
   TORCH_CHECK(dcr::launch_head(a, num_cus(), optr<float>(db), optr<float>(loss), cur_stream()) == 0,
               "fused head launch failed");
@@ -1271,7 +1264,7 @@ TORCH_LIBRARY(dcr, m) {
       "head(Tensor O, Tensor WsT, Tensor? Wsk, Tensor bias, Tensor? targets, float grad_scale, "
       "Tensor(a!)? logits, Tensor(b!)? row_loss, Tensor(c!)? dlogits, Tensor(d!)? dtop, "
       "Tensor(e!)? db, Tensor(f!) part, Tensor(g!)? loss, Tensor? omask=None, "
-      "float oscale=1.0, Tensor(h!)? o_out=None) -> ()");
+      "float oscale=1.0) -> ()");
   m.def("prep(Tensor[] src, Tensor(a!)[] dst, int[] mode, Tensor[] extra) -> ()");
   m.def("prep_max_tasks() -> int", []() -> int64_t { return dcr::kPrepMaxTasks; });
   m.def("wgrad(Tensor[] A, Tensor[] B, Tensor(a!) part) -> ()");

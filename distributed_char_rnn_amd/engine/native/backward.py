@@ -49,10 +49,7 @@ class BackwardMixin:
                           logits if want_extras else None, bufs["row_loss"], dlog,
                           bufs["dtop"].view(N, H), s.gview("rnnlm/softmax_b"),
                           bufs["head_part"], loss_buf, head_omask,
-                          dm["sout"] if dm is not None else 1.0,
-                          bufs["o_drop"] if head_omask is not None else None)
-            if head_omask is not None:
-                O = bufs["o_drop"]  # the masked top outputs, stored by the head kernel
+                          dm["sout"] if dm is not None else 1.0)
             mm_tn(O, dlog, s.gview("rnnlm/softmax_w"), q=q)
             dtop = bufs["dtop"].view(T, B, H)
         elif wide:

@@ -194,10 +194,7 @@ class ForwardMixin:
                                      FORGET_BIAS)
             x_prev = lb.hbuf[1:]
         O = x_prev.reshape(N, H)
-        if (dm is not None and dm["out"] is not None
-                and not (self.fused_head and self.knobs.on("head_omask"))):
-            # the top layer's output dropout (with the fused head the head kernel masks O as it
-            # loads it and stores the masked rows itself)
+        if dm is not None and dm["out"] is not None:  # the top layer's output dropout
             O = self._masked(O, dm["out"], dm["sout"], out=bufs["o_drop"])
         if not O.is_contiguous():
             O = O.contiguous()
