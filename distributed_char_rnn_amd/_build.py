@@ -4,7 +4,10 @@
 
 No hipify, no JIT cache, no CUDA path: the library is built for ``--offload-arch=gfx950`` and
 loaded with ``torch.ops.load_library`` (see ``ops/native.py``).  Objects are cached under
-``build/`` and rebuilt when the source or any ``csrc/*.h`` header is newer.
+``build/`` and rebuilt when the source or any ``csrc/*.h`` header is newer.  The library's
+sidecar ``_C.so.srchash`` records the sha256 of every ``csrc/`` file plus the compile flags it
+was built from; the loader compares it with the sources it finds next to it and rebuilds (or,
+with ``DCR_AUTOBUILD=0``, refuses to load) a library that does not match them.
 
 Usage: ``python -m distributed_char_rnn_amd._build [--force] [-j N]``
 """
@@ -67,6 +70,28 @@ COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-r
           "-ffp-contract=fast"]
 
 
+def source_hash() -> str:
+    """sha256 over every csrc/ file (name + bytes), the compile flags and the target arch."""
+    import hashlib
+
+    h = hashlib.sha256()
+    h.update(" ".join(COMMON).encode())
+    for f in sorted(glob.glob(os.path.join(CSRC, "*"))):
+        if os.path.isfile(f):
+            h.update(os.path.basename(f).encode() + b"\0")
+            with open(f, "rb") as fh:
+                h.update(fh.read())
+    return h.hexdigest()
+
+
+def recorded_hash(lib: str = OUT) -> str | None:
+    try:
+        with open(lib + ".srchash") as fh:
+            return fh.read().strip() or None
+    except OSError:
+        return None
+
+
 def _stale(obj: str, src: str, headers) -> bool:
     if not os.path.exists(obj):
         return True
@@ -78,6 +103,9 @@ def _stale(obj: str, src: str, headers) -> bool:
 
 def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> str:
     os.makedirs(BUILD, exist_ok=True)
+    want = source_hash()
+    if recorded_hash() != want and os.path.exists(OUT):
+        force = True  # the library was built from other sources (mtimes can lie after a copy)
     hipcc = _hipcc()
     cflags, ldflags, _ = _torch_flags()
     headers = glob.glob(os.path.join(CSRC, "*.h"))
@@ -117,6 +145,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         os.replace(tmp, OUT)
+    with open(OUT + ".srchash", "w") as fh:
+        fh.write(want + "\n")
     return OUT
 
 

@@ -19,7 +19,8 @@ What changes from step to step is kept in device memory the graph reads:
 Not captured (``GraphedStep.supported`` says why): data parallelism (the all-reduce buckets are
 released by host callbacks), dropout (its mask seeds are per-step host values) and summary steps
 that want the logits (run eagerly).  The persistent kernels' error word is polled outside the
-graph, one step behind, as in eager mode.
+graph (a non-blocking copy every ERR_POLL_EVERY-th replay, read one replay later), as in eager
+mode.
 """
 from __future__ import annotations
 
@@ -63,6 +64,11 @@ class GraphedStep:
         torch.cuda.synchronize()
         be._wver = None  # the captured prep launch must refresh the weight layouts every replay
         g = torch.cuda.CUDAGraph()
+        # the capture records one optimizer step without running it: its host counters (Adam's
+        # t, the parameter version, the backend's step count) are restored whether or not the
+        # capture succeeds -- an eager fallback after a failed capture would otherwise apply
+        # Adam's bias correction one step off for the rest of the run
+        t0, v0, s0 = self.opt.t, self.model.store.version, be._steps
         be.capturing = True
         try:
             with torch.cuda.graph(g):
@@ -73,8 +79,8 @@ class GraphedStep:
                         d.copy_(s)
         finally:
             be.capturing = False
-        # the capture recorded one optimizer step without running it: undo its host counters
-        self.opt.t -= 1
+            self.opt.t, self.model.store.version, be._steps = t0, v0, s0
+            be._wver = None  # the captured layout refresh has not run: an eager step redoes it
         self.loss = loss
         self.graph = g
 
@@ -108,7 +114,11 @@ class GraphedStep:
         self.opt.t += 1
         self.model.store.version += 1
         self.replays += 1
-        self.model.backend._poll_errors()
+        # the replay ran a training step: count it, so _poll_errors' every-k-th non-blocking
+        # copy of the error word happens during replays as in eager mode
+        be = self.model.backend
+        be._steps += 1
+        be._poll_errors()
         return self.loss.clone(), self.state_in
 
     def _eager(self, x, y, state, lr):

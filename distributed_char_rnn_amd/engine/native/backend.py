@@ -41,7 +41,7 @@ CELL_ID = {"lstm": 0, "gru": 1, "rnn": 3, "nas": 4}
 class NativeBackend(LayoutsMixin, BuffersMixin, ForwardMixin, BackwardMixin, LibStepMixin,
                     InferenceMixin):
     def __init__(self, store: ParamStore, dtype: str = "auto", seed: int = 0,
-                 knobs: Optional[Knobs] = None):
+                 knobs: Optional[Knobs] = None, rank: int = 0):
         if dtype not in ("auto", "bf16"):
             raise ValueError("the native GPU path computes in bf16 (use --dtype bf16/auto)")
         self.ops = native.ops()
@@ -78,7 +78,10 @@ class NativeBackend(LayoutsMixin, BuffersMixin, ForwardMixin, BackwardMixin, Lib
         self._steps = 0
         self.capturing = False  # a hipGraph capture of train_step is in progress (graph_step.py)
         self._npart: Optional[torch.Tensor] = None
-        self._drop_seed = int(seed) * 0x9E3779B1 + 0x5EED
+        # dropout masks: every data-parallel rank draws its own (the reference's workers each
+        # had their own TF RNG), from the shared seed mixed with the rank; the step counter is
+        # checkpointed (``drop_step``) so --resume_exact continues the mask sequence
+        self._drop_seed = (int(seed) * 0x9E3779B1 + 0x5EED + int(rank) * 0x632BE5AB) & ((1 << 62) - 1)
         self._drop_step = 0
         self._dm_bufs: Dict[Tuple[int, int], dict] = {}
         self.last_dropout_masks: Optional[dict] = None

@@ -65,7 +65,7 @@ def _real_offsets(store: ParamStore) -> torch.Tensor:
 class PaddedNativeBackend:
     """Drop-in for :class:`NativeBackend` (same methods) over a zero-padded private model."""
 
-    def __init__(self, store: ParamStore, dtype: str = "auto", seed: int = 0):
+    def __init__(self, store: ParamStore, dtype: str = "auto", seed: int = 0, rank: int = 0):
         if store.cfg.model == "nas":
             raise ValueError("NAS cells need rnn_size % 32 == 0 on the GPU path")
         self.store = store
@@ -75,7 +75,7 @@ class PaddedNativeBackend:
         pcfg = replace(store.cfg, rnn_size=self.Hp)
         self.pstore = ParamStore(pcfg, store.device, seed=None)
         self.pstore.flat.zero_()
-        self.inner = NativeBackend(self.pstore, dtype=dtype, seed=seed)
+        self.inner = NativeBackend(self.pstore, dtype=dtype, seed=seed, rank=rank)
         dev = store.device
         self._dst = _index_map(store, self.pstore).to(dev)   # padded offsets
         self._src = _real_offsets(store).to(dev)             # real offsets

@@ -82,11 +82,12 @@ class TFAdam:
             sq = (gn * gn).sum() + (slot.double().sum() if slot is not None else 0.0)
             norm = torch.sqrt(sq).float() * grad_scale
             s = self.clip / torch.clamp(norm, min=self.clip) if self.clip > 0 else torch.ones(())
-            gs = g * (s * grad_scale)
-            m.mul_(self.b1).add_(gs, alpha=1 - self.b1)
-            v.mul_(self.b2).addcmul_(gs, gs, value=1 - self.b2)
-            p.sub_(lr_t * m / (v.sqrt() + self.eps))
             self.last_norm.copy_(norm.reshape(1))
+            if not self._guard_set():
+                gs = g * (s * grad_scale)
+                m.mul_(self.b1).add_(gs, alpha=1 - self.b1)
+                v.mul_(self.b2).addcmul_(gs, gs, value=1 - self.b2)
+                p.sub_(lr_t * m / (v.sqrt() + self.eps))
             if self.mirror is not None:
                 self.mirror.copy_(st.flat)
         self.t += 1
@@ -98,11 +99,22 @@ class TFAdam:
                    grad_scale: float = 1.0) -> torch.Tensor:
         """One update of the parameters [lo, hi) only, clipped by the GLOBAL norm
         sqrt(``sumsq``) * grad_scale (a 1-element device tensor: the sum of squares of every
-        norm term, already reduced over ranks).  The sharded data-parallel step
-        (parallel/zero.py) calls this on each rank's shard."""
+        norm term, already reduced over ranks)."""
+        return self.step_ranges(lr, [(lo, hi)], sumsq, grad_scale)
+
+    @torch.no_grad()
+    def step_ranges(self, lr: float, ranges, sumsq: torch.Tensor,
+                    grad_scale: float = 1.0) -> torch.Tensor:
+        """One update (one Adam step t -> t+1) of the parameters in each [lo, hi) of
+        ``ranges``, clipped by the GLOBAL norm sqrt(``sumsq``) * grad_scale.  The sharded
+        data-parallel step (parallel/zero.py) calls this with the chunks a rank owns."""
         lr_t = self.lr_t(lr)
-        hi = min(hi, self.store.norm_slot)  # the norm slot and the tail padding are not params
-        if hi > lo:
+        applied = False
+        for lo, hi in ranges:
+            hi = min(hi, self.store.norm_slot)  # the norm slot and the tail padding: not params
+            if hi <= lo:
+                continue
+            applied = True
             p, g, m, v = (b[lo:hi] for b in (self.store.flat, self.store.grad, self.m, self.v))
             if self.native:
                 self._ops.adam_clip(p, g, m, v, None, self._partials, self.last_norm, lr_t,
@@ -110,17 +122,23 @@ class TFAdam:
                                     sumsq, self.guard)
             else:
                 norm = torch.sqrt(sumsq.double().sum()).float() * grad_scale
+                self.last_norm.copy_(norm.reshape(1))
+                if self._guard_set():
+                    continue
                 s = self.clip / torch.clamp(norm, min=self.clip) if self.clip > 0 else torch.ones(())
                 gs = g * (s * grad_scale)
                 m.mul_(self.b1).add_(gs, alpha=1 - self.b1)
                 v.mul_(self.b2).addcmul_(gs, gs, value=1 - self.b2)
                 p.sub_(lr_t * m / (v.sqrt() + self.eps))
-                self.last_norm.copy_(norm.reshape(1))
-        else:  # a shard holding only the norm slot / tail padding: nothing to update
+        if not applied:  # a rank owning only the norm slot / tail padding: nothing to update
             self.last_norm.copy_((torch.sqrt(sumsq.sum()) * grad_scale).reshape(1))
         self.t += 1
         self.store.version += 1
         return self.last_norm
+
+    def _guard_set(self) -> bool:
+        """CPU path: the error word is set (the GPU kernel reads it on device instead)."""
+        return self.guard is not None and bool(int(self.guard.reshape(-1)[0]))
 
     # -- checkpoint support (TF slot names) ----------------------------------------------
     def slot_state(self):

@@ -100,6 +100,8 @@ def checkpoint_tensors(model: CharRNN, opt: TFAdam, global_step: int, lr: float,
     t["Variable"] = np.array(lr, dtype=np.float32)
     t["dcr/epoch"] = np.array(epoch, dtype=np.int64)
     t["dcr/batch_pointer"] = np.array(batch, dtype=np.int64)
+    # the dropout mask counter: --resume_exact continues the mask sequence (same on every rank)
+    t["dcr/drop_step"] = np.array(model.drop_step, dtype=np.int64)
     if state is not None:
         for li, st in enumerate(state):
             for si, s in enumerate(st):
@@ -157,12 +159,13 @@ def restore(model: CharRNN, opt: TFAdam, prefix: str):
     return sd
 
 
-def build_model(args, vocab_size: int, device) -> CharRNN:
+def build_model(args, vocab_size: int, device, rank: int = 0) -> CharRNN:
     cfg = ModelConfig(model=args.model, vocab_size=vocab_size, rnn_size=args.rnn_size,
                       num_layers=args.num_layers, input_keep_prob=args.input_keep_prob,
                       output_keep_prob=args.output_keep_prob,
                       clip_norm=getattr(args, "clip_norm", "tf"))
-    return CharRNN(cfg, device=device, seed=args.seed, dtype=getattr(args, "dtype", "auto"))
+    return CharRNN(cfg, device=device, seed=args.seed, dtype=getattr(args, "dtype", "auto"),
+                   rank=rank)
 
 
 def train(args: argparse.Namespace) -> int:
@@ -200,7 +203,7 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
         safe_pickle.dump((tuple(loader.chars), dict(loader.vocab)),
                          os.path.join(args.save_dir, "chars_vocab.pkl"))
 
-    model = build_model(args, loader.vocab_size, device)
+    model = build_model(args, loader.vocab_size, device, rank)
     # a persistent-kernel timeout makes the optimizer skip its update on device
     opt = TFAdam(model.store, clip=args.grad_clip, guard=model.error_word())
     global_step = 0
@@ -212,12 +215,15 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
         if getattr(args, "resume_exact", False):
             start_epoch = int(sd.get("dcr/epoch", 0))
             start_batch = int(sd.get("dcr/batch_pointer", -1)) + 1
+            model.drop_step = int(sd.get("dcr/drop_step", 0))
         _log(f"restored {prefix} (global_step {global_step})", rank)
 
     sharded = getattr(args, "dp_mode", "replicated") == "sharded" and ctx.world_size > 1
+    # every rank's error word is MAX-reduced before the optimizer reads it (GradSync.finish /
+    # ShardedStep.step): one rank's timed-out recurrence makes every rank skip the update
     sync = GradSync(model.store, ctx.world_size, getattr(args, "bucket_mb", 8.0),
                     getattr(args, "allreduce_dtype", "fp32"),
-                    enabled=(ctx.world_size > 1 and not sharded))
+                    enabled=(ctx.world_size > 1 and not sharded), guard=model.error_word())
     zstep = None
     saved_state = None
     if ctx.world_size > 1:
@@ -227,10 +233,11 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
         ctx.broadcast_(model.store.flat)
         ctx.broadcast_(opt.m)
         ctx.broadcast_(opt.v)
-        meta = torch.tensor([global_step, opt.t, start_epoch, start_batch], dtype=torch.int64,
-                            device=device if ctx.backend == "nccl" else "cpu")
+        meta = torch.tensor([global_step, opt.t, start_epoch, start_batch, model.drop_step],
+                            dtype=torch.int64, device=device if ctx.backend == "nccl" else "cpu")
         ctx.broadcast_(meta)
-        global_step, opt.t, start_epoch, start_batch = (int(v) for v in meta.tolist())
+        global_step, opt.t, start_epoch, start_batch, model.drop_step = (int(v) for v in
+                                                                         meta.tolist())
         model.params_changed()
         if start_batch > 0:
             saved_state = _broadcast_state(ctx, model, sd, args.batch_size, device)
@@ -271,8 +278,10 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
         from ..parallel.zero import ShardedStep
 
         zstep = ShardedStep(model.store, opt, ctx.world_size, rank,
-                            wire=getattr(args, "allreduce_dtype", "fp32"))
-        _log(f"sharded optimizer: shard {zstep.shard} of {model.store.numel} elements", rank)
+                            wire=getattr(args, "allreduce_dtype", "fp32"),
+                            bucket_mb=getattr(args, "bucket_mb", 8.0), guard=model.error_word())
+        _log(f"sharded optimizer: shard {zstep.shard} of {model.store.numel} elements in "
+             f"{len(zstep.buckets)} buckets", rank)
     # --graph: the whole step (fwd, head, BPTT, weight grads, clip + Adam) as one replayed
     # hipGraph; summary steps that want the logits run eagerly
     graphed = None
@@ -300,9 +309,10 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
             if dev_batches is not None:  # the same batch, already resident on the device
                 x, y = dev_batches[0][b], dev_batches[1][b]
             want = chief and summary_every > 0 and (global_step % summary_every == 0)
-            if zstep is not None:  # sharded optimizer step (ZeRO-1)
+            if zstep is not None:  # sharded optimizer step (ZeRO-1): the backward launches
+                # each bucket's reduce-scatter as soon as its gradients are final
                 with prof.phase("fwd_bwd"):
-                    loss_t, state, extras = _step(model, x, y, state, sync, want)
+                    loss_t, state, extras = _step(model, x, y, state, zstep, want)
                 with prof.phase("sharded_step"):
                     zstep.step(lr)
             elif graphed is not None and not want:
@@ -407,7 +417,9 @@ def _broadcast_state(ctx, model: CharRNN, sd, batch: int, device):
     return out
 
 
-def _step(model: CharRNN, x, y, state, sync: GradSync, want_extras: bool):
+def _step(model: CharRNN, x, y, state, sync, want_extras: bool):
+    """``sync``: a GradSync (replicated) or ShardedStep (sharded): both are reset here and
+    driven by the backward's readiness callbacks."""
     sync.reset()
     loss, new_state, extras = model.train_step(x, y, state, sync, want_extras=want_extras)
     return loss, new_state, (extras if want_extras else None)

@@ -3,7 +3,7 @@
 Equivalent of the reference ``Model`` (model.py:8-140) minus the TF graph: parameters live in a
 :class:`ParamStore` (flat fp32 buffers, TF names) and execution is delegated to a backend:
 
-* ``native``    -- gfx950 HIP kernels (engine/native_backend.py): fused recurrent cell
+* ``native``    -- gfx950 HIP kernels (engine/native/): fused recurrent cell
                    kernels, fused softmax-CE, embedding-projection gather/segment-sum, etc.
                    Mandatory on GPU; raises if the native library is missing.
 * ``reference`` -- pure PyTorch autograd with TF cell semantics (models/reference.py); the
@@ -34,7 +34,9 @@ def _as_ids(x, device: torch.device) -> torch.Tensor:
 
 class CharRNN:
     def __init__(self, cfg: ModelConfig, device="cpu", seed: Optional[int] = 0,
-                 backend: str = "auto", dtype: str = "auto"):
+                 backend: str = "auto", dtype: str = "auto", rank: int = 0):
+        """``seed`` initialises the parameters (identical on every data-parallel rank);
+        ``rank`` only decorrelates the ranks' dropout masks."""
         self.cfg = cfg
         self.device = torch.device(device)
         self.store = ParamStore(cfg, self.device, seed)
@@ -52,13 +54,13 @@ class CharRNN:
             # the MFMA kernels tile H by 32 / 128: run a zero-padded model (engine/native/padded.py)
             from ..engine.native.padded import PaddedNativeBackend
 
-            self.backend = PaddedNativeBackend(self.store, dtype=dtype, seed=seed or 0)
+            self.backend = PaddedNativeBackend(self.store, dtype=dtype, seed=seed or 0, rank=rank)
         elif backend == "native":
-            from ..engine.native_backend import NativeBackend
+            from ..engine.native import NativeBackend
 
-            self.backend = NativeBackend(self.store, dtype=dtype, seed=seed or 0)
+            self.backend = NativeBackend(self.store, dtype=dtype, seed=seed or 0, rank=rank)
         elif backend == "reference":
-            self.backend = ReferenceBackend(self.store, seed=seed or 0)
+            self.backend = ReferenceBackend(self.store, seed=(seed or 0) + 7919 * rank)
         else:
             raise ValueError(f"unknown backend {backend}")
 
@@ -92,6 +94,18 @@ class CharRNN:
         check = getattr(self.backend, "check_errors", None)
         if check is not None:
             check()
+
+    @property
+    def drop_step(self) -> int:
+        """Dropout mask counter of the native backend (checkpointed for --resume_exact)."""
+        be = getattr(self.backend, "inner", self.backend)
+        return int(getattr(be, "_drop_step", 0))
+
+    @drop_step.setter
+    def drop_step(self, v: int) -> None:
+        be = getattr(self.backend, "inner", self.backend)
+        if hasattr(be, "_drop_step"):
+            be._drop_step = int(v)
 
     def params_changed(self):
         """Call after parameters were modified outside the optimizer (restore/broadcast)."""

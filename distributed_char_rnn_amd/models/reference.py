@@ -213,12 +213,6 @@ class ReferenceBackend:
         names = self.store.names()
         grads = torch.autograd.grad(cost, [params[n] for n in names] + [taps["emb"]],
                                     allow_unused=True)
-        for n, g in zip(names, grads):
-            gv = self.store.gview(n)
-            if g is None:
-                gv.zero_()
-            else:
-                gv.copy_(g)
         # TF's clip norm term for the embedding: the per-token IndexedSlices values
         g_tok = grads[-1]
         slot = self.store.norm_slot_view()
@@ -226,8 +220,20 @@ class ReferenceBackend:
             slot.copy_((g_tok.double() ** 2).sum().reshape(1))
         else:
             slot.zero_()
+        # readiness reported tensor by tensor in the flat buffer's order (head, top layer, ...,
+        # embedding), as the native backward does, so the data-parallel buckets launch one by
+        # one on this path too
+        for n, g in zip(names, grads):
+            gv = self.store.gview(n)
+            if g is None:
+                gv.zero_()
+            else:
+                gv.copy_(g)
+            if on_bucket_ready is not None and n != names[-1]:
+                sp = self.store.by_name[n]
+                on_bucket_ready(sp.offset + sp.numel)
         if on_bucket_ready is not None:
-            on_bucket_ready(None)  # everything is ready at once on this path
+            on_bucket_ready(None)
         detached = [tuple(s.detach() for s in st) for st in new_state]
         return cost.detach(), detached, {"logits": logits.detach(), "loss": per.detach()}
 

@@ -24,16 +24,38 @@ def library_path() -> str:
     return _LIB
 
 
+BUILD_INFO: dict = {}
+
+
+def _in_tree() -> bool:
+    return not os.environ.get("DCR_NATIVE_LIB")
+
+
 def try_load(build_if_missing: bool = False) -> bool:
-    """Load the library once; returns True on success."""
+    """Load the library once; returns True on success.  The in-tree library must match the
+    sources next to it (``_build.source_hash`` vs its ``.srchash`` sidecar): a stale one is
+    rebuilt first when building is allowed, and refused otherwise."""
     global _loaded, _err
     with _lock:
         if _loaded:
             return True
-        if not os.path.exists(_LIB) and build_if_missing:
-            from .. import _build
+        from .. import _build
 
+        if _in_tree() and os.path.isdir(_build.CSRC):
+            want, have = _build.source_hash(), _build.recorded_hash(_LIB)
+            BUILD_INFO.update(source_hash=want, library_hash=have)
+            if os.path.exists(_LIB) and have != want:
+                if not build_if_missing:
+                    _err = (f"{_LIB} was built from other sources (hash {have} != {want}); "
+                            "rebuild with python -m distributed_char_rnn_amd._build")
+                    return False
+                print(f"[dcr] native library stale (built from {have}, sources {want}): "
+                      "rebuilding", flush=True)
+                _build.build()
+                BUILD_INFO.update(library_hash=_build.recorded_hash(_LIB), rebuilt=True)
+        if not os.path.exists(_LIB) and build_if_missing:
             _build.build()
+            BUILD_INFO.update(library_hash=_build.recorded_hash(_LIB), rebuilt=True)
         if not os.path.exists(_LIB):
             _err = f"native library not built: {_LIB} (run python -m distributed_char_rnn_amd._build)"
             return False

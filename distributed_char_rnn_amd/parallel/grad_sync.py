@@ -35,15 +35,24 @@ from ..models.params import ParamStore
 
 class GradSync:
     def __init__(self, store: ParamStore, world_size: int, bucket_mb: float = 8.0,
-                 wire_dtype: str = "fp32", group=None, enabled: Optional[bool] = None):
+                 wire_dtype: str = "fp32", group=None, enabled: Optional[bool] = None,
+                 guard: Optional[torch.Tensor] = None):
+        """``guard``: the rank's persistent-kernel error word (``TFAdam(guard=...)``).  It is
+        MAX-reduced over ranks in :meth:`finish`, on the stream, before the optimizer reads it:
+        a rank whose recurrence timed out contributed garbage gradients to the sum, so EVERY
+        rank must skip that update (a local guard alone would let the healthy ranks apply it
+        while the faulty one skips, and the replicas would diverge)."""
         self.store = store
         self.world = world_size
         self.group = group
         self.enabled = (world_size > 1) if enabled is None else enabled
         self.wire_bf16 = wire_dtype == "bf16"
+        self.guard = guard
         self.buckets = self._make_buckets(bucket_mb)
         self._next = 0
         self._work: List[Tuple[object, int, int, Optional[torch.Tensor]]] = []
+        # bf16 wire: per-bucket send / receive / gather buffers, allocated once
+        self._wire_bufs: dict = {}
 
     def _make_buckets(self, bucket_mb: float) -> List[Tuple[int, int]]:
         """Cut the flat buffer at tensor boundaries into ~bucket_mb slices.  The last tensor
@@ -97,11 +106,8 @@ class GradSync:
                 # through an all_to_all, each rank sums its chunk in fp32, the sums come back
                 # through an all_gather (finish).  A bf16 all-reduce would round after every
                 # ring hop: N-1 roundings of partial sums at N ranks.
-                n = hi - lo
-                c = -(-n // self.world)
-                send = torch.zeros(self.world * c, dtype=torch.bfloat16, device=g.device)
-                send[:n].copy_(g)
-                recv = torch.empty_like(send)
+                send, recv = self._bufs_for(lo, hi, g.device)[:2]
+                send[: hi - lo].copy_(g)  # the tail padding stays zero (allocated zeroed)
                 w = dist.all_to_all_single(recv, send, group=self.group, async_op=True)
                 self._work.append((w, lo, hi, recv))
             else:
@@ -121,10 +127,14 @@ class GradSync:
         for w, lo, hi, recv in self._work:
             w.wait()
             if recv is not None:  # bf16 wire: fp32 sum of my chunk, then gather every chunk
-                mine = recv.view(self.world, -1).float().sum(0).to(torch.bfloat16)
-                full = torch.empty_like(recv)
-                gw = dist.all_gather_into_tensor(full, mine, group=self.group, async_op=True)
+                _, _, mine, mine16, full = self._bufs_for(lo, hi, recv.device)
+                torch.sum(recv.view(self.world, -1), 0, dtype=torch.float32, out=mine)
+                mine16.copy_(mine)
+                gw = dist.all_gather_into_tensor(full, mine16, group=self.group, async_op=True)
                 gathers.append((gw, lo, hi, full))
+        if self.guard is not None:
+            # one rank's timed-out recurrence poisons the summed gradient: every rank skips
+            dist.all_reduce(self.guard, op=dist.ReduceOp.MAX, group=self.group)
         for gw, lo, hi, full in gathers:
             gw.wait()
             self.store.grad[lo:hi].copy_(full[: hi - lo])
@@ -137,6 +147,22 @@ class GradSync:
         # ranks): averaging the gradients scales it by 1/world^2, not 1/world
         self.store.norm_slot_view().mul_(1.0 / self.world)
         return 1.0
+
+    def _bufs_for(self, lo: int, hi: int, device) -> tuple:
+        """bf16-wire buffers of bucket [lo, hi): (send, recv) of world·c bf16 elements, the
+        chunk sum [c] in fp32 and bf16, and the gathered bf16 [world·c]; allocated on first use
+        and reused every step (no allocator traffic on the step's critical path)."""
+        key = (lo, hi)
+        b = self._wire_bufs.get(key)
+        if b is None:
+            c = -(-(hi - lo) // self.world)
+            b = (torch.zeros(self.world * c, dtype=torch.bfloat16, device=device),
+                 torch.empty(self.world * c, dtype=torch.bfloat16, device=device),
+                 torch.empty(c, dtype=torch.float32, device=device),
+                 torch.empty(c, dtype=torch.bfloat16, device=device),
+                 torch.empty(self.world * c, dtype=torch.bfloat16, device=device))
+            self._wire_bufs[key] = b
+        return b
 
     def broadcast_params(self, src: int = 0):
         if self.enabled:

@@ -3,7 +3,9 @@
 # its own time limit; the slot limits of MI355X_MICROARCH.md "rocprofv3 PMC slots").
 set -o pipefail
 export TMPDIR=/tmp PYTHONPATH=$PWD
-mkdir -p gpurun_out/pmc
+D=${1:-gpurun_out/pmc}; shift
+BA=${*:---steps 5 --warmup 2}
+mkdir -p $D
 i=0
 for pass in \
   "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES" \
@@ -13,7 +15,7 @@ for pass in \
   "WRITE_SIZE"; do
   i=$((i+1))
   echo "== pass $i: $pass"
-  timeout -s KILL 90 rocprofv3 --pmc $pass -d gpurun_out/pmc/p$i -o run --output-format csv -- \
-    python3 bench.py --steps 5 --warmup 2 > gpurun_out/pmc/p$i.log 2>&1 || { tail -5 gpurun_out/pmc/p$i.log; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc $pass -d $D/p$i -o run --output-format csv -- \
+    python3 bench.py $BA > $D/p$i.log 2>&1 || { tail -5 $D/p$i.log; exit 1; }
 done
 echo done

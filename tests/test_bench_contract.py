@@ -63,7 +63,7 @@ def test_bench_two_ranks_one_gpu():
     """The DP path on real GPU tensors: two ranks share cuda:0 (the GPU box has one card), so
     RCCL refuses them (duplicate GPU) and gloo carries the bucketed all-reduce; the per-step
     kernels run because two processes' persistent grids cannot both be co-resident on one chip
-    (the spin timeout reports that instead of hanging, see native_backend.check_errors)."""
+    (the spin timeout reports that instead of hanging, see engine/native/backend.py check_errors)."""
     env = dict(os.environ, PYTHONPATH=ROOT, DCR_RECURRENCE="step")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)

@@ -1,0 +1,185 @@
+"""Data parallelism at world 4 on gloo (CPU), both DP modes, and the cross-rank error-word guard.
+
+* replicated (bucketed all-reduce) and sharded (bucketed reduce-scatter + owned-chunk Adam +
+  all-gather, parallel/zero.py) steps at world 4 equal one process on the 4x batch, with
+  clipping active and many small buckets, and the sharded buckets are launched from the
+  backward's readiness callbacks (before ``step``), not after it;
+* a persistent-kernel timeout on ONE rank (its error word set) makes EVERY rank skip the update
+  in both modes, so the replicas never diverge (the guard used to be rank-local);
+* ``train.py`` with 4 gloo ranks on a corpus that splits into unequal shards runs the same number
+  of steps per epoch on every rank in both modes and ends with the same checkpoint.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from distributed_char_rnn_amd.engine.optim import TFAdam
+from distributed_char_rnn_amd.models.char_rnn import CharRNN
+from distributed_char_rnn_amd.models.params import ModelConfig
+from distributed_char_rnn_amd.parallel.grad_sync import GradSync
+from distributed_char_rnn_amd.parallel.zero import ShardedStep, shard_buckets
+
+CFG = dict(model="lstm", vocab_size=11, rnn_size=8, num_layers=2)
+CLIP = 0.05
+B, T = 2, 6
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _data(rows, steps):
+    rng = np.random.default_rng(1)
+    return rng.integers(0, 11, size=(steps, rows, T + 1)).astype(np.int32)
+
+
+def _worker(rank, world, port, mode, steps, fault_rank, fault_step, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = CharRNN(ModelConfig(**CFG), device="cpu", seed=9)
+        guard = torch.zeros(1, dtype=torch.int32)
+        opt = TFAdam(m.store, clip=CLIP, guard=guard)
+        dist.broadcast(m.store.flat, 0)
+        if mode == "replicated":
+            sync = GradSync(m.store, world, 0.0005, "fp32", guard=guard)
+        else:
+            sync = ShardedStep(m.store, opt, world, rank, wire="fp32", bucket_mb=0.0005,
+                               guard=guard)
+        data = _data(B * world, steps)
+        st = m.zero_state(B)
+        norms, snaps, early = [], [], []
+        for s in range(steps):
+            blk = data[s, rank * B:(rank + 1) * B]
+            sync.reset()
+            guard.zero_()
+            _, st, _ = m.train_step(blk[:, :-1], blk[:, 1:], st, sync)
+            if s == fault_step and rank == fault_rank:
+                guard.fill_(10)  # this rank's recurrence "timed out" during the step
+            if mode == "replicated":
+                gs = sync.finish(defer_scale=True)
+                norms.append(float(opt.step(0.01, grad_scale=gs)))
+            else:
+                early.append(len(sync.launched))  # buckets launched during the backward
+                norms.append(float(sync.step(0.01)))
+            snaps.append(m.store.flat.numpy().copy())
+        if mode != "replicated":
+            sync.gather_slots()
+        q.put((rank, snaps, opt.m.numpy().copy(), norms, early, int(guard.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(mode, world=4, steps=3, fault_rank=-1, fault_step=-1):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, mode, steps, fault_rank, fault_step, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    out = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    return sorted(out, key=lambda o: o[0])
+
+
+def _single(world, steps=3):
+    m = CharRNN(ModelConfig(**CFG), device="cpu", seed=9)
+    opt = TFAdam(m.store, clip=CLIP)
+    data = _data(B * world, steps)
+    st = m.zero_state(B * world)
+    norms, snaps = [], []
+    for s in range(steps):
+        _, st, _ = m.train_step(data[s, :, :-1], data[s, :, 1:], st)
+        norms.append(float(opt.step(0.01)))
+        snaps.append(m.store.flat.numpy().copy())
+    return snaps, norms
+
+
+@pytest.mark.parametrize("mode", ["replicated", "sharded"])
+def test_world4_equals_single_process(mode):
+    ref, ref_norms = _single(4)
+    out = _run(mode)
+    assert all(n > CLIP for n in ref_norms), "clipping must be active"
+    for rank, snaps, _, norms, early, _ in out:
+        np.testing.assert_allclose(norms, ref_norms, rtol=1e-4)
+        np.testing.assert_allclose(snaps[-1], ref[-1], rtol=2e-4, atol=2e-6)
+        np.testing.assert_array_equal(snaps[-1], out[0][1][-1])  # replicas identical
+        if mode == "sharded":
+            # every bucket but the last (embedding + norm slot) left during the backward
+            assert all(e >= 2 for e in early), early
+
+
+def test_sharded_buckets_cover_buffer_and_align():
+    from distributed_char_rnn_amd.models.params import ParamStore
+
+    st = ParamStore(ModelConfig(model="lstm", vocab_size=65, rnn_size=512, num_layers=2))
+    for world in (2, 4, 8):
+        b = shard_buckets(st, world, 4.0)
+        assert b[0][0] == 0 and b[-1][1] == st.numel and len(b) >= 3
+        for (lo, hi), (lo2, _) in zip(b, b[1:]):
+            assert hi == lo2 and hi > lo
+        assert all((hi - lo) % (world * 64) == 0 for lo, hi in b)
+
+
+@pytest.mark.parametrize("mode", ["replicated", "sharded"])
+def test_error_word_on_one_rank_skips_update_everywhere(mode):
+    out = _run(mode, world=2, steps=3, fault_rank=1, fault_step=1)
+    for rank, snaps, _, _, _, guard in out:
+        # step 1's update was skipped on EVERY rank (the guard was MAX-reduced)
+        np.testing.assert_array_equal(snaps[1], snaps[0])
+        assert not np.array_equal(snaps[2], snaps[1])  # step 2 (guard cleared) updated
+        np.testing.assert_array_equal(snaps[-1], out[0][1][-1])
+        assert guard == 0
+
+
+def test_train_py_world4_unequal_shards_both_modes(tmp_path):
+    """4 gloo ranks of train.py: 3999 synthetic chars split 1000/1000/1000/999, i.e. 10, 10, 10
+    and 9 batches of 4 x 25: the trainer equalises every rank to the minimum (9 steps), and the
+    replicated and sharded runs end with the same checkpoint."""
+    from distributed_char_rnn_amd.utils import checkpoint as ckpt
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    common = ["--synthetic_text", "3999", "--num_epochs", "1", "--batch_size", "4",
+              "--seq_length", "25", "--rnn_size", "16", "--num_layers", "2", "--device", "cpu",
+              "--log_dir", "logs", "--save_every", "1000", "--seed", "3", "--grad_clip", "0.05",
+              "--bucket_mb", "0.001"]
+    env = dict(os.environ, PYTHONPATH=root, OMP_NUM_THREADS="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    finals = {}
+    for mode in ("replicated", "sharded"):
+        port = free_port()
+        workers = ",".join(f"127.0.0.1:{port + i}" for i in range(4))
+        procs = [subprocess.Popen([sys.executable, os.path.join(root, "train.py")] + common +
+                                  ["--save_dir", mode, "--dp_mode", mode, "--distributed",
+                                   "--worker_hosts", workers, "--job_name", "worker",
+                                   "--task_index", str(i), "--dist_timeout", "120"],
+                                  cwd=str(tmp_path), env=env, stdout=subprocess.PIPE,
+                                  stderr=subprocess.STDOUT, text=True) for i in range(4)]
+        outs = [p.communicate(timeout=400)[0] for p in procs]
+        for p, o in zip(procs, outs):
+            assert p.returncode == 0, o
+        assert "9/9 (epoch 0)" in outs[0], outs[0][-2000:]  # min over ranks: 999 // 100
+        sd = ckpt.Saver.restore(ckpt.latest_checkpoint(str(tmp_path / mode)))
+        finals[mode] = {k: np.asarray(v) for k, v in sd.items()}
+    a, b = finals["replicated"], finals["sharded"]
+    for k in a:
+        if k.startswith("dcr/") or np.asarray(a[k]).dtype.kind not in "fc":
+            continue
+        np.testing.assert_allclose(b[k], a[k], rtol=1e-4, atol=1e-6, err_msg=k)

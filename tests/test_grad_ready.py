@@ -1,4 +1,4 @@
-"""The gradient-readiness contract of the native backward (engine/native_backend.py).
+"""The gradient-readiness contract of the native backward (engine/native/backward.py).
 
 Data parallelism (parallel/grad_sync.py) launches an RCCL all-reduce of flat-buffer slice
 [0, upto) as soon as the backend reports ``ready(upto)``; the collective is ordered after the

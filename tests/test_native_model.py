@@ -127,7 +127,7 @@ def test_segsum_atomic_wide_vocab_runs(dcr_ops, N):
     ref = torch.zeros(V, W, device="cuda", dtype=torch.float64)
     ref.index_add_(0, ids.long(), X.double())
     torch.testing.assert_close(out.double(), ref, rtol=1e-4, atol=1e-4)
-    # sorted route: ids sorted + source-row permutation (native_backend._embed_grad)
+    # sorted route: ids sorted + source-row permutation (engine/native/backward.py _embed_grad)
     sid, perm = torch.sort(ids)
     out2 = torch.empty(V, W, device="cuda")
     dcr_ops.segsum(X, sid, V, out2, ws, False, perm.int())
