@@ -208,6 +208,8 @@ struct Lstm2Args {
   float xscale;         //   and their 1/keep
   const bf16* x0;       // optional (G = 1): layer l's bf16 input rows [T·B, H]; the input
   const bf16* X0T;      //   projection x0·W_x,l (W_x,lᵀ [4H, H]) then runs in-kernel (zx0 unused)
+  int wgarr;            // 1: one counter add per workgroup and layer (the layer's last epilogue
+                        //   wave signals for both, persist_common.h wg_arrive); 0: one per wave
 };
 // batch groups per workgroup for the two-layer kernels at (H, B) (force > 0: only that value),
 // 0 = unsupported
@@ -236,8 +238,15 @@ struct Lstm2BwdArgs {
   unsigned spin_limit;
   const uint8_t* xmask; // optional dropout bits of layer l+1's input [T, B, H/8]: layer l's dtop
   float xscale;         //   (dtop1 arrives with layer l+1's output dropout already applied)
+  int db_rows;          // rows of db_part0/1 (the wide kernel zeroes the ones past its columns)
+  int wgarr;            // as Lstm2Args::wgarr
+  int diag_all;         // diag holds [grid, T+2, 8] s_memrealtime stamps of every workgroup
 };
 int launch_lstm2_bwd_persist(const Lstm2BwdArgs& a, int cus, hipStream_t s);
+// the 32-unit x 16-row form of the same BPTT (lstm2_bwd_wide.hip): nbg = ceil(B / 16) 16-row
+// columns, G = 1
+bool lstm2_bwd_wide_ok(int H, int B, int cus);
+int launch_lstm2_bwd_wide(const Lstm2BwdArgs& a, int cus, hipStream_t s);
 
 // persistent GRU recurrence (gru_persist.hip)
 struct GruPersistArgs {

@@ -1,0 +1,408 @@
+// Two-layer wavefront LSTM BPTT with 32-unit x 16-row workgroup tiles (gfx950).
+//
+// Reference: tf.gradients through the unrolled two-layer stack (model.py:72, 91); the schedule
+// is lstm2_persist.hip's reverse wavefront (layer l+1 at step T-1-tau, layer l two ticks
+// behind, layer l's dtop = dZ_{l+1}·W_x,l+1ᵀ computed in-kernel).  What changes is the tile.
+//
+// Why.  Every BPTT tick a workgroup must read the whole 4H-wide dZ rows of its batch rows for
+// both layers (dh = dZ·W_hᵀ reduces over all 4H gate columns).  With 16 units x 32 rows per
+// workgroup (lstm2_persist.hip) that is 256 KB per workgroup and tick -- 8 MB per XCD per tick
+// out of a 4 MB L2 at ~4.3 TB/s: the payload phase was L2-bandwidth bound (42 % of a 5.7 us
+// tick, profiles/r2_pair_groups_stamps.txt).  Here a workgroup owns 32 units x 16 rows: the
+// same MFMA work per workgroup and tick, HALF the payload bytes (128 KB), half the producer
+// arrivals per hand-off counter, and twice the resident weights -- W_h,l and W_h,l+1 for 32
+// units (256 VGPRs per lane) in registers, W_x,l+1 for 32 units (128 KB) in LDS.
+//
+// Geometry.  Workgroup (ubk, col): hidden units [32 ubk, 32 ubk + 32) of both layers, batch
+// rows [16 col, 16 col + 16) (rows >= B are padding: zero inputs, zero gradients, written only
+// to the hand-off ring).  Grid (H/32) x ceil(B/16), one workgroup per CU.  Wave w reduces over
+// the K quarter {g·H + [w·H/4, (w+1)·H/4)} of every gate g (KS = H/32 k-steps of 32) and runs
+// the cell-backward epilogue of layer w>>1, unit half w&1 (units 32 ubk + 16 (w&1) + [0, 16)).
+//
+// Hand-off protocol: persist_common.h / lstm2_persist.hip (sc1 fragment-order ring stores,
+// vmcnt(0), one agent-scope counter add per storing wave per (column, slot); one poller per
+// workgroup; every load of handed-off bytes is a buffer_load sc1).  Ring rows are 16-row MFMA
+// tiles, so the ring layout is the one lstm2_persist.hip uses.
+//
+// Bias gradients: each epilogue lane's 16 dZ values (4 gates x 4 units) are reduced over the
+// 16 rows of its DPP row by a 4-stage butterfly reduce-scatter (row_mirror, row_half_mirror,
+// quad_perm xor 2, xor 1) after the hand-off arrival: lane r of a row ends with the row sum of
+// value r, accumulated in ONE register over the launch (LDS holds only W_x and the partials).
+#include "common.h"
+#include "kernels.h"
+#include "persist_common.h"
+#include "debug_env.h"
+
+namespace dcr {
+
+// Diagnostics.  a.diag [T+2, 8]: s_memtime phase stamps of workgroup 0.  With a.diag_all the
+// buffer is [grid, T+2, 8] and every workgroup records s_memrealtime (100 MHz, one clock for the
+// whole chip) at the same points, except that slot 5 is layer l+1's hand-off arrival (wave 2)
+// and slot 6 layer l's (wave 0): the cross-workgroup skew of every tick (scripts/pair_bench.py
+// --skew).
+#define STAMPW(i)                                                                    \
+  if (a.diag && threadIdx.x == 0 && (i) != 5 && (i) != 6) {                          \
+    if (a.diag_all)                                                                  \
+      a.diag[((size_t)blockIdx.x * (T + 2) + tau) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    else if (blockIdx.x == 0)                                                        \
+      a.diag[(size_t)tau * 8 + (i)] = __builtin_amdgcn_s_memtime();                  \
+  }
+#define STAMP_ARRIVE()                                                               \
+  if (a.diag && lane == 0 && (w == 0 || w == 2)) {                                   \
+    if (a.diag_all)                                                                  \
+      a.diag[((size_t)blockIdx.x * (T + 2) + tau) * 8 + (w ? 5 : 6)] =               \
+          __builtin_amdgcn_s_memrealtime();                                          \
+    else if (blockIdx.x == 0 && w == 0)                                              \
+      a.diag[(size_t)tau * 8 + 6] = __builtin_amdgcn_s_memtime();                    \
+  }
+
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL,
+                                                               0xF, 0xF, true));
+}
+
+// One butterfly stage over N values: lanes paired by the DPP involution CTRL exchange the half
+// they do not keep (`hi`: keep the upper half) and add; returns N/2 values.
+template <int CTRL, int N>
+__device__ __forceinline__ void bfly(float (&v)[16], bool hi) {
+#pragma unroll
+  for (int k = 0; k < N / 2; ++k) {
+    const float send = hi ? v[k] : v[k + N / 2];
+    const float keep = hi ? v[k + N / 2] : v[k];
+    v[k] = keep + dppf<CTRL>(send);
+  }
+}
+
+// Row-sum reduce-scatter of 16 values over the 16 lanes of a DPP row: returns, in lane r of the
+// row, the sum over the row's lanes of v[r].
+__device__ __forceinline__ float row_reduce_scatter16(float (&v)[16], int lane) {
+  const int r = lane & 15;
+  bfly<0x140, 16>(v, (r & 8) != 0);  // row_mirror: r <-> 15 - r
+  bfly<0x141, 8>(v, (r & 4) != 0);   // row_half_mirror: r <-> r ^ 7 (within 8)
+  bfly<0x4E, 4>(v, (r & 2) != 0);    // quad_perm [2,3,0,1]: r <-> r ^ 2
+  bfly<0xB1, 2>(v, (r & 1) != 0);    // quad_perm [1,0,3,2]: r <-> r ^ 1
+  return v[0];
+}
+
+// PF: where the epilogue operands (gates, c, dtop, dropout bits; HBM reads, ~1.3 us under
+// load) are loaded.  vmcnt retires in issue order, so whatever is loaded before the hand-off
+// poll delays the poller's first counter check by its latency.
+//   0: at the tick start, before the poll (the poll then waits for them: +1.35 us hand-off)
+//   1: right behind the tick's payload loads (the MFMA / epilogue phase waits for them instead)
+//   2: one tick ahead, right after the previous tick's hand-off arrival: their latency runs
+//      concurrently with the hand-off's own (~1.7 us from arrival to the consumers' poll)
+template <int KS, bool DROP, int PF>
+__global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) {
+  static_assert(KS % 4 == 0, "K quarter = whole 32-wide k-steps per gate");
+  // partials [wave][layer][unit half][lane][4]
+  __shared__ __attribute__((aligned(16))) float part[4][2][2][64][4];
+  // W_x,l+1 fragments [wave][unit half][k-step][lane] (128 KB at H = 512), read back only by
+  // the wave that wrote them (the off-critical-path dtop stash)
+  __shared__ __attribute__((aligned(16))) bf16x8 wx1l[4][2][KS][64];
+  __shared__ unsigned arrl[2];              // per-layer arrivals of the tick (wgarr)
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int H = a.H, B = a.B, T = a.T;
+  const int G4H = 4 * H;
+  const int ncol = a.nbg;  // 16-row columns (the host passes ceil(B / 16))
+  int ubk, col;
+  map_block(blockIdx.x, H / 32, ncol, ubk, col);
+  const int ub0 = ubk * 32;
+  const int kq = 8 * (lane >> 4);
+  unsigned* cnt0 = a.cnt0 + (size_t)col * (T + 1) * 4;
+  unsigned* cnt1 = a.cnt1 + (size_t)col * (T + 1) * 4;
+  // arrivals per (column, slot) and layer: H/32 unit blocks x (one per workgroup | 2 waves)
+  const unsigned target = (unsigned)(a.wgarr ? H / 32 : H / 16);
+  if (threadIdx.x < 2) arrl[threadIdx.x] = 0u;  // (ordered before any add by tick 0's barrier)
+  const size_t slabn = (size_t)ncol * 16 * G4H;  // one ring slot, elements
+  bool dead = false;
+
+  constexpr int KSG = KS / 4;  // k-steps per gate segment
+  auto kcol = [&](int s) { return (s / KSG) * H + w * (H / 4) + (s % KSG) * 32; };
+  bf16x8 wh0[2][KS], wh1[2][KS];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const size_t row = (size_t)(ub0 + 16 * u + (lane & 15)) * G4H + kcol(s) + kq;
+      wh0[u][s] = ld8(a.Wh0 + row);
+      wh1[u][s] = ld8(a.Wh1 + row);
+      wx1l[w][u][s][lane] = ld8(a.Wx1 + row);
+    }
+
+  // epilogue role: layer L, unit half U
+  const int L = w >> 1, U = w & 1;
+  const int u0 = ub0 + 16 * U + 4 * (lane >> 4);
+  const int b = col * 16 + (lane & 15);
+  const bool live = b < B;
+  const bf16* const gtL = L ? a.gates1 : a.gates0;
+  const float* const cbL = L ? a.cbuf1 : a.cbuf0;
+  bf16* const dzL = L ? a.dz1 : a.dz0;
+  bf16* const zrL = L ? a.zring1 : a.zring0;
+  unsigned* const cntL = L ? cnt1 : cnt0;
+  const size_t bh = (size_t)b * H + u0;
+  float dc[4] = {0.f, 0.f, 0.f, 0.f};
+  float dbacc = 0.f;  // this lane's bias-gradient sum (value lane & 15 of its row, see header)
+  // layer l's dtop partial of its NEXT tick (this wave's K quarter, both unit halves), computed
+  // off the critical path from the tick's dZ_{l+1} fragments
+  f32x4 xs[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  const __amdgpu_buffer_rsrc_t rz1 = make_rsrc(a.zring1, sizeof(bf16) * 2 * slabn);
+  const __amdgpu_buffer_rsrc_t rz0 = make_rsrc(a.zring0, sizeof(bf16) * 2 * slabn);
+
+  // recurrence-independent epilogue operands of a tick (padded rows: zero) and the dropout
+  // bits of layer l's dtop (layer l+1's input mask at step T+1-tau: this row's 32 units)
+  bf16x4 g4[4];
+  float cc[4], cp[4], dtop[4];
+  unsigned mrow = 0;
+  auto prefetch = [&](int tk) {
+    const int tt = L ? T - 1 - tk : T + 1 - tk;
+    const bool ac = L ? tk < T : tk >= 2;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int gt = 0; gt < 4; ++gt) g4[gt][r] = (bf16)0.f;
+      cc[r] = cp[r] = dtop[r] = 0.f;
+    }
+    if (ac && live) {
+      const bf16* gp = gtL + ((size_t)tt * B + b) * G4H + u0;
+#pragma unroll
+      for (int gt = 0; gt < 4; ++gt) g4[gt] = *reinterpret_cast<const bf16x4*>(gp + gt * H);
+      ld4f(cbL + (size_t)(tt + 1) * B * H + bh, cc);
+      ld4f(cbL + (size_t)tt * B * H + bh, cp);
+      if (L) ld4f(a.dtop1 + (size_t)tt * B * H + bh, dtop);
+    }
+    if (DROP && tk >= 2 && tk <= T + 1 && live)
+      mrow = *reinterpret_cast<const unsigned*>(a.xmask + ((size_t)(T + 1 - tk) * B + b) * (H / 8) +
+                                                (ub0 >> 3));
+  };
+
+  for (int tau = 0; tau <= T + 1; ++tau) {
+    const bool on1 = tau < T;                 // layer l+1 computes step T-1-tau
+    const bool on0 = tau >= 2;                // layer l computes step T+1-tau (two ticks behind)
+    const bool ld1 = tau >= 1 && tau <= T;    // dZ_{l+1}[T-tau] (published at tick tau-1)
+    const bool ld0 = tau >= 3;                // dZ_l[T+2-tau]   (published at tick tau-1)
+    const int t = L ? T - 1 - tau : T + 1 - tau;  // this role's step
+    const bool act = L ? on1 : on0;
+    STAMPW(0)
+    if (PF != 2 || tau == 0) prefetch(tau);
+    const int s1 = T - tau, s0 = T + 2 - tau;  // ring slots of dZ_{l+1} and dZ_l
+    if (tau >= 1) {
+      if (threadIdx.x == kLstmPollerThread && !dead && (ld1 || ld0)) {
+        dead = (ld1 && ld0)
+                   ? !poll_counter2(cnt1 + (size_t)s1 * 4, target, cnt0 + (size_t)s0 * 4, target,
+                                    a.spin_limit, a.err, 10u)
+                   : !poll_counter(ld1 ? cnt1 + (size_t)s1 * 4 : cnt0 + (size_t)s0 * 4, target,
+                                   a.spin_limit, a.err, 10u);
+      }
+    }
+    STAMPW(1)
+    // (also: every wave's previous-tick epilogue has read the partials)
+    __syncthreads();
+    STAMPW(2)
+    bf16x8 p1[KS], p0[KS];
+    if (tau >= 1) {
+      const unsigned o1 = (unsigned)((s1 & 1) * slabn * sizeof(bf16));
+      const unsigned o0 = (unsigned)((s0 & 1) * slabn * sizeof(bf16));
+      if (ld1) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+          p1[s] = ld8_sc1(rz1, frag_load_off(col, kcol(s) >> 5, G4H, lane) + o1);
+      }
+      if (ld0) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+          p0[s] = ld8_sc1(rz0, frag_load_off(col, kcol(s) >> 5, G4H, lane) + o0);
+      }
+      if (PF == 1) prefetch(tau);
+      __builtin_amdgcn_sched_barrier(0);
+      if (on1) {  // layer l+1: dh partial = dZ_{l+1}[t+1] · W_h,l+1ᵀ, both unit halves
+        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          acc[0] = mfma16(wh1[0][s], p1[s], acc[0]);
+          acc[1] = mfma16(wh1[1][s], p1[s], acc[1]);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          *reinterpret_cast<float4*>(&part[w][1][u][lane][0]) =
+              make_float4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
+      }
+      if (on0) {  // layer l: dtop (stashed last tick) + dZ_l[t+1] · W_h,lᵀ
+        f32x4 acc[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          float4 x0 = make_float4(xs[u][0], xs[u][1], xs[u][2], xs[u][3]);
+          if constexpr (DROP) {
+            // layer l+1's input dropout on layer l's dtop: this lane's 4 units' bits
+            const unsigned m = mrow >> (16 * u + 4 * (lane >> 4));
+            x0.x = m & 1u ? x0.x * a.xscale : 0.f;
+            x0.y = m & 2u ? x0.y * a.xscale : 0.f;
+            x0.z = m & 4u ? x0.z * a.xscale : 0.f;
+            x0.w = m & 8u ? x0.w * a.xscale : 0.f;
+          }
+          acc[u] = f32x4{x0.x, x0.y, x0.z, x0.w};
+        }
+        if (ld0) {
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {
+            acc[0] = mfma16(wh0[0][s], p0[s], acc[0]);
+            acc[1] = mfma16(wh0[1][s], p0[s], acc[1]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          *reinterpret_cast<float4*>(&part[w][0][u][lane][0]) =
+              make_float4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
+      }
+    } else {
+      // tick 0: layer l+1's first step has no recurrent input
+      *reinterpret_cast<float4*>(&part[w][1][0][lane][0]) = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(&part[w][1][1][lane][0]) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    STAMPW(3)
+    __syncthreads();
+    STAMPW(4)
+    if (act) {
+      float dh[4];
+      {
+        const float4 q0 = *reinterpret_cast<const float4*>(&part[0][L][U][lane][0]);
+        const float4 q1 = *reinterpret_cast<const float4*>(&part[1][L][U][lane][0]);
+        const float4 q2 = *reinterpret_cast<const float4*>(&part[2][L][U][lane][0]);
+        const float4 q3 = *reinterpret_cast<const float4*>(&part[3][L][U][lane][0]);
+        dh[0] = q0.x + q1.x + q2.x + q3.x + dtop[0];
+        dh[1] = q0.y + q1.y + q2.y + q3.y + dtop[1];
+        dh[2] = q0.z + q1.z + q2.z + q3.z + dtop[2];
+        dh[3] = q0.w + q1.w + q2.w + q3.w + dtop[3];
+      }
+      float di[4], dj[4], df_[4], dO[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float gi = (float)g4[0][r], gj = (float)g4[1][r];
+        const float gf = (float)g4[2][r], go = (float)g4[3][r];
+        const float th = tanhf_(cc[r]);
+        const float dcv = dc[r] + dh[r] * go * (1.f - th * th);
+        dO[r] = dh[r] * th * go * (1.f - go);
+        di[r] = dcv * gj * gi * (1.f - gi);
+        dj[r] = dcv * gi * (1.f - gj * gj);
+        df_[r] = dcv * cp[r] * gf * (1.f - gf);
+        dc[r] = dcv * gf;
+      }
+      if (a.diag && !a.diag_all && blockIdx.x == 0 && threadIdx.x == 0)
+        a.diag[(size_t)tau * 8 + 5] = __builtin_amdgcn_s_memtime();
+      // layer l+1's dZ_t feeds both layers at the next tick (t >= 0); layer l's only itself
+      if (L || t >= 1) {
+        bf16* const zr = zrL + (size_t)(t & 1) * slabn;
+        st4bf_sc1(zr + frag_index(b, u0, G4H), di[0], di[1], di[2], di[3]);
+        st4bf_sc1(zr + frag_index(b, H + u0, G4H), dj[0], dj[1], dj[2], dj[3]);
+        st4bf_sc1(zr + frag_index(b, 2 * H + u0, G4H), df_[0], df_[1], df_[2], df_[3]);
+        st4bf_sc1(zr + frag_index(b, 3 * H + u0, G4H), dO[0], dO[1], dO[2], dO[3]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        STAMP_ARRIVE()
+        if (lane == 0) {
+          if (a.wgarr)
+            wg_arrive(&arrl[L], 2u, cntL + (size_t)t * 4);
+          else
+            __hip_atomic_fetch_add(cntL + (size_t)t * 4, 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      // off the critical path from here: the next tick's epilogue operands, layer l's next
+      // dtop, the row-major dZ copy for the weight GEMMs, the bias gradient
+      float dcur[16];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        dcur[r] = di[r]; dcur[4 + r] = dj[r]; dcur[8 + r] = df_[r]; dcur[12 + r] = dO[r];
+      }
+      if (live) {
+        bf16* dz = dzL + ((size_t)t * B + b) * G4H + u0;
+        st4bf(dz, dcur[0], dcur[1], dcur[2], dcur[3]);
+        st4bf(dz + H, dcur[4], dcur[5], dcur[6], dcur[7]);
+        st4bf(dz + 2 * H, dcur[8], dcur[9], dcur[10], dcur[11]);
+        st4bf(dz + 3 * H, dcur[12], dcur[13], dcur[14], dcur[15]);
+      }
+      // bias gradient of the bf16-rounded dz, exactly as the weight GEMMs see it (padded rows
+      // add zero)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dcur[i] = (float)f2bf(dcur[i]);
+      dbacc += row_reduce_scatter16(dcur, lane);
+      if (PF == 2 && tau < T + 1) prefetch(tau + 1);
+      if (ld1) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < KS; ++s) x = mfma16(wx1l[w][u][s][lane], p1[s], x);
+          xs[u] = x;
+        }
+      }
+    } else {
+      if (PF == 2 && tau < T + 1) prefetch(tau + 1);
+      if (ld1) {
+        // a wave without an epilogue this tick still stashes layer l's next dtop
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < KS; ++s) x = mfma16(wx1l[w][u][s][lane], p1[s], x);
+          xs[u] = x;
+        }
+      }
+    }
+    STAMPW(7)
+  }
+  // bias-gradient partial of this role's 16-row column: lane r of row q holds value r
+  float* const dbp = L ? a.db_part1 : a.db_part0;
+  if (dbp) {
+    const int r = lane & 15;
+    dbp[(size_t)col * G4H + (r >> 2) * H + u0 + (r & 3)] = dbacc;
+    // rows of the partial buffer past the last column (the host sizes it for 32-row groups)
+    if (col == ncol - 1)
+      for (int c2 = ncol; c2 < a.db_rows; ++c2) dbp[(size_t)c2 * G4H + (r >> 2) * H + u0 + (r & 3)] = 0.f;
+  }
+}
+
+template <bool DROP, int PF>
+static const void* lstm2_bwd_wide_pick_t(int H) {
+  switch (H / 32) {  // KS = 4H / 4 waves / 32
+    case 4: return (const void*)lstm2_bwd_wide_kernel<4, DROP, PF>;
+    case 8: return (const void*)lstm2_bwd_wide_kernel<8, DROP, PF>;
+    case 12: return (const void*)lstm2_bwd_wide_kernel<12, DROP, PF>;
+    case 16: return (const void*)lstm2_bwd_wide_kernel<16, DROP, PF>;
+  }
+  return nullptr;
+}
+template <bool DROP>
+static const void* lstm2_bwd_wide_pick(int H) {
+  switch (debug_int("wide_pf", 0)) {
+    case 1: return lstm2_bwd_wide_pick_t<DROP, 1>(H);
+    case 2: return lstm2_bwd_wide_pick_t<DROP, 2>(H);
+  }
+  return lstm2_bwd_wide_pick_t<DROP, 0>(H);
+}
+
+// The 32-unit x 16-row BPTT applies at (H, B): H a multiple of 128 up to 512, and the grid of
+// (H/32) x ceil(B/16) workgroups co-resident (one per CU).  DCR_DEBUG=wide=0 disables it.
+bool lstm2_bwd_wide_ok(int H, int B, int cus) {
+  if (debug_int("wide", 1) == 0) return false;
+  if (H % 128 != 0 || H < 128 || H > 512 || B < 1 || cus <= 0) return false;
+  const int grid = (H / 32) * ((B + 15) / 16);
+  for (int drop = 0; drop < 2; ++drop) {
+    const void* fn = drop ? lstm2_bwd_wide_pick<true>(H) : lstm2_bwd_wide_pick<false>(H);
+    int o = 0;
+    if (!fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, fn, 256, 0) != hipSuccess || o < 1)
+      return false;
+    if (grid > o * cus) return false;
+  }
+  return true;
+}
+
+int launch_lstm2_bwd_wide(const Lstm2BwdArgs& a, int cus, hipStream_t s) {
+  if (!lstm2_bwd_wide_ok(a.H, a.B, cus) || a.nbg != (a.B + 15) / 16) return -2;
+  void* args[] = {const_cast<Lstm2BwdArgs*>(&a)};
+  const void* fn = a.xmask ? lstm2_bwd_wide_pick<true>(a.H) : lstm2_bwd_wide_pick<false>(a.H);
+  return hipLaunchKernel(fn, dim3((a.H / 32) * a.nbg), dim3(256), args, 0, s) == hipSuccess ? 0
+                                                                                             : -3;
+}
+
+}  // namespace dcr

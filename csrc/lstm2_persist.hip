@@ -88,7 +88,10 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
   const int kbase = w * (KS * 32);
   unsigned* const cnt0 = a.cnt0 + (size_t)col * (T + 1) * 4;
   unsigned* const cnt1 = a.cnt1 + (size_t)col * (T + 1) * 4;
-  const unsigned target = (unsigned)(H / 8);  // H/16 unit blocks x 2 epilogue waves per layer
+  // arrivals per (column, slot) and layer: H/16 unit blocks x (one per workgroup | 2 waves)
+  const unsigned target = (unsigned)(a.wgarr ? H / 16 : H / 8);
+  __shared__ unsigned arrl[2];  // per-layer arrivals of the tick (wgarr)
+  if (threadIdx.x < 2) arrl[threadIdx.x] = 0u;  // (ordered before any add by tick 0's barrier)
   const size_t ringsz = (size_t)a.nbg * 32 * H;  // one ring slot (padded batch)
   bool dead = false;
   // row-major slot-0 fragment offsets (rows >= B read as zero: buffer range check)
@@ -434,9 +437,13 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
           // one arrival per wave and tick, for all its groups' ring stores
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           STAMPG(g, 6)
-          if (lane == 0)
-            __hip_atomic_fetch_add((L ? cnt1 : cnt0) + (size_t)(t + 1) * 4, 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0) {
+            unsigned* const c = (L ? cnt1 : cnt0) + (size_t)(t + 1) * 4;
+            if (a.wgarr)
+              wg_arrive(&arrl[L], 2u, c);
+            else
+              __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
         }
         if (xdrop) do_stash();
         if (live) {  // row-major copies for the GEMMs / head (not handed off)
@@ -505,7 +512,10 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
   const int kq = 8 * (lane >> 4);
   unsigned* cnt0 = a.cnt0 + (size_t)col * (T + 1) * 4;
   unsigned* cnt1 = a.cnt1 + (size_t)col * (T + 1) * 4;
-  const unsigned target = (unsigned)(H / 8);  // H/16 unit blocks x 2 epilogue waves per layer
+  // arrivals per (column, slot) and layer: H/16 unit blocks x (one per workgroup | 2 waves)
+  const unsigned target = (unsigned)(a.wgarr ? H / 16 : H / 8);
+  __shared__ unsigned arrl[2];  // per-layer arrivals of the tick (wgarr)
+  if (threadIdx.x < 2) arrl[threadIdx.x] = 0u;  // (ordered before any add by tick 0's barrier)
   const size_t slabn = (size_t)a.nbg * 32 * G4H;  // one ring slot (padded batch), elements
   bool dead = false;
 
@@ -625,9 +635,13 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
           if (g == G - 1) {  // one arrival per wave and tick, for all its groups' ring stores
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             STAMPG(g, 6)
-            if (lane == 0)
-              __hip_atomic_fetch_add(cntL + (size_t)t * 4, 1u, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) {
+              if (a.wgarr)
+                wg_arrive(&arrl[L], 2u, cntL + (size_t)t * 4);
+              else
+                __hip_atomic_fetch_add(cntL + (size_t)t * 4, 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
           }
         }
         after_arrive();

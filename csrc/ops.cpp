@@ -6,6 +6,7 @@
 #include <torch/library.h>
 
 #include "kernels.h"
+#include "debug_env.h"
 
 namespace {
 
@@ -769,6 +770,7 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
   a.B = B; a.H = H; a.T = T; a.G = (int)G; a.nbg = nbg;
   a.forget_bias = (float)forget_bias;
   a.spin_limit = (unsigned)spin_limit;
+  a.wgarr = dcr::debug_int("wgarr", 1);  // one hand-off add per workgroup and layer
   if (has(diag)) {
     TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)(T + 2) * G * 8,
                 "diag must hold [T+2, G, 8] int64 (ticks 0..T+1)");
@@ -838,14 +840,27 @@ void lstm2_persist_bwd(const at::Tensor& Wh0, const at::Tensor& Wh1, const at::T
   a.err = reinterpret_cast<unsigned*>(err.data_ptr());
   a.B = B; a.H = H; a.T = T; a.G = (int)G; a.nbg = nbg;
   a.spin_limit = (unsigned)spin_limit;
+  a.wgarr = dcr::debug_int("wgarr", 1);  // one hand-off add per workgroup and layer
   if (has(diag)) {
     TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)(T + 2) * G * 8,
                 "diag must hold [T+2, G, 8] int64 (ticks 0..T+1)");
     a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());
+    // [grid, T+2, 8]: every workgroup stamps (the wide kernel's skew diagnostics)
+    a.diag_all = diag->numel() >= (int64_t)(H / 32) * ((B + 15) / 16) * (T + 2) * 8 &&
+                 diag->numel() > (int64_t)(T + 2) * G * 8;
   }
   a.xmask = drop_bits(xmask, T, B, H, "xmask");
   a.xscale = (float)xscale;
-  const int rc = dcr::launch_lstm2_bwd_persist(a, num_cus(), cur_stream());
+  a.db_rows = 2 * nbg / (int)G;
+  int rc;
+  if (G == 1 && dcr::lstm2_bwd_wide_ok(H, B, num_cus())) {
+    // 32-unit x 16-row workgroups: half the dZ payload per workgroup and tick
+    a.nbg = (B + 15) / 16;
+    for (auto* c : {&cnt0, &cnt1}) check_lstm2_counters(*c, a.nbg, T);
+    rc = dcr::launch_lstm2_bwd_wide(a, num_cus(), cur_stream());
+  } else {
+    rc = dcr::launch_lstm2_bwd_persist(a, num_cus(), cur_stream());
+  }
   TORCH_CHECK(rc == 0, "two-layer persistent LSTM BPTT not launched (", rc, ")");
 }
 
@@ -1279,6 +1294,9 @@ TORCH_LIBRARY(dcr, m) {
         });
   m.def("lstm2_xin_ok(int H) -> bool",
         [](int64_t H) -> bool { return dcr::lstm2_xin_ok((int)H, num_cus()); });
+  m.def("lstm2_bwd_wide_ok(int H, int B) -> bool", [](int64_t H, int64_t B) -> bool {
+    return dcr::lstm2_bwd_wide_ok((int)H, (int)B, num_cus());
+  });
   m.def("lstm2_nbg(int B, int G) -> int",
         [](int64_t B, int64_t G) -> int64_t { return lstm2_nbg((int)B, (int)G); });
   m.def(

@@ -14,6 +14,8 @@
 #   pmc[=<bench.py args>]      the PMC counter passes (scripts/pmc_passes.sh)
 #   py=<script,args>           any python script of the repo (e.g. py=scripts/pair_bench.py,--stamps)
 #   ab=<A.so>,<B.so>[,rounds,<bench args>]  same-box A/B of two builds (scripts/ab_bench.sh)
+#   abenv=<VAR=value>[;<bench args>]  same-box A/B of bench.py without / with an environment
+#                              setting (e.g. abenv=DCR_DEBUG=wide=0), 3 alternating rounds
 #
 # Example: gpurun --timeout 900 -- bash scripts/gpu.sh r3_base tests bench trace
 set -o pipefail
@@ -61,6 +63,18 @@ for step in "$@"; do
     ab)
       bash scripts/ab_bench.sh $(sp "$arg") > "$O/ab.log" 2>&1 || { tail -20 "$O/ab.log"; exit 1; }
       cat "$O/ab.log" ;;
+    abenv)
+      EV=${arg%%;*}; BA="--steps,40,--warmup,5"; [[ "$arg" == *";"* ]] && BA=${arg#*;}
+      for i in 1 2 3; do
+        for v in base env; do
+          if [ $v = base ]; then
+            ms=$(timeout -k 10 120 python bench.py $(sp "$BA") | python -c "import json,sys; print('%.4f' % json.loads(sys.stdin.read())['ms_per_step'])") || exit 1
+          else
+            ms=$(env "$EV" timeout -k 10 120 python bench.py $(sp "$BA") | python -c "import json,sys; print('%.4f' % json.loads(sys.stdin.read())['ms_per_step'])") || exit 1
+          fi
+          echo "$v $ms" | tee -a "$O/abenv.log"
+        done
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

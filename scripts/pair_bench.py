@@ -50,7 +50,46 @@ def stamps(d, n_ticks, G, bwd):
     return tick, out
 
 
-def run(ops, H, T, B, G, want_stamps, reps=5):
+def map_block(bid, nwg_u, ncol):
+    """persist_common.h map_block: block -> (unit block, column)."""
+    if ncol % 8 == 0:
+        xcd, j = bid % 8, bid // 8
+        return j % nwg_u, xcd + 8 * (j // nwg_u)
+    return bid % nwg_u, bid // nwg_u
+
+
+def skew(d, H, B, T):
+    """Cross-workgroup timing of the wide BPTT from [grid, T+2, 8] s_memrealtime stamps (10 ns):
+    slot 1 poll done, 3 payload + MFMA done, 5 / 6 layer l+1 / l hand-off arrival."""
+    d = d.cpu().numpy().astype("float64") * 0.01  # us
+    grid, ncol, nwg_u = d.shape[0], (B + 15) // 16, H // 32
+    cols = np.array([map_block(b, nwg_u, ncol)[1] for b in range(grid)])
+    lo, hi = 4, T - 4
+    rows = []
+    for tau in range(lo, hi):
+        for c in range(ncol):
+            m = cols == c
+            a1, a0 = d[m, tau, 5], d[m, tau, 6]
+            last = max(a1.max(), a0.max())
+            p_next = d[m, tau + 1, 1]
+            p_now = d[m, tau, 1]
+            rows.append((a1.max() - a1.min(), a0.max() - a0.min(), np.median(p_next - last),
+                         (p_next - last).min(), p_now.max() - p_now.min(),
+                         np.median(a1 - p_now), (a1 - p_now).max(), np.median(d[m, tau, 3] - p_now),
+                         (d[m, tau, 3] - p_now).max(), np.median(d[m, tau + 1, 0] - d[m, tau, 0])))
+    r = np.array(rows).mean(0)
+    names = ["arrival skew in a column, layer l+1", "arrival skew in a column, layer l",
+             "last arrival -> poll done (median consumer)", "last arrival -> poll done (first)",
+             "poll-done skew in a column", "poll done -> own arrival (median)",
+             "poll done -> own arrival (slowest)", "poll done -> payload+MFMA done (median)",
+             "poll done -> payload+MFMA done (slowest)", "tick period"]
+    per_wg = np.mean(d[:, lo:hi, 5] - d[:, lo:hi, 1], axis=1)
+    xcd = np.arange(grid) % 8
+    by_xcd = [per_wg[xcd == x].mean() for x in range(8)]
+    return list(zip(names, r)), by_xcd
+
+
+def run(ops, H, T, B, G, want_stamps, reps=5, want_skew=False):
     dev = "cuda"
     G = int(ops.lstm2_plan(H, B, G))
     if not G:
@@ -66,7 +105,7 @@ def run(ops, H, T, B, G, want_stamps, reps=5):
     g0, g1 = (torch.empty(T, B, 4 * H, dtype=torch.bfloat16, device=dev) for _ in range(2))
     hl0, hl1 = (torch.empty(B, H, device=dev) for _ in range(2))
     hr0, hr1 = (torch.empty(2 * Bp * H, dtype=torch.bfloat16, device=dev) for _ in range(2))
-    cnt = torch.zeros(2, nbg * (T + 1) * 4, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(2, 2 * nbg * (T + 1) * 4, dtype=torch.int32, device=dev)  # 16-row columns
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     dfw = torch.zeros(T + 2, G, 8, dtype=torch.int64, device=dev) if want_stamps else None
 
@@ -108,6 +147,12 @@ def run(ops, H, T, B, G, want_stamps, reps=5):
         torch.cuda.synchronize()
         out["stamps_fwd"] = stamps(dfw, fticks, G, False)
         out["stamps_bwd"] = stamps(dbw, T + 2, G, True)
+    if want_skew and G == 1 and ops.lstm2_bwd_wide_ok(H, B):
+        grid = (H // 32) * ((B + 15) // 16)
+        dall = torch.zeros(grid, T + 2, 8, dtype=torch.int64, device=dev)
+        bwd(dall)
+        torch.cuda.synchronize()
+        out["skew_bwd"] = skew(dall, H, B, T)
     return out
 
 
@@ -118,11 +163,12 @@ def main():
     ap.add_argument("--B", type=int, nargs="+", default=[256, 512, 1024])
     ap.add_argument("--G", type=int, nargs="+", default=[0])
     ap.add_argument("--stamps", action="store_true")
+    ap.add_argument("--skew", action="store_true", help="every workgroup's hand-off timing (wide BPTT)")
     a = ap.parse_args()
     ops = native.ops()
     for B in a.B:
         for G in a.G:
-            o = run(ops, a.H, a.T, B, G, a.stamps)
+            o = run(ops, a.H, a.T, B, G, a.stamps, want_skew=a.skew)
             if o is None:
                 print(f"H={a.H} B={B} G={G}: no co-resident grid", flush=True)
                 continue
@@ -135,6 +181,13 @@ def main():
                     print(f"   {k}: {tot:.0f} s_memtime ticks per tick (workgroup 0)")
                     for n, v in parts:
                         print(f"     {n:<40}{v:8.0f}  {100 * v / tot:5.1f}%")
+            if "skew_bwd" in o:
+                rows, by_xcd = o["skew_bwd"]
+                print("   skew_bwd (every workgroup, s_memrealtime, us, mean over steady ticks):")
+                for n, v in rows:
+                    print(f"     {n:<46}{v:7.2f}")
+                print("     poll done -> layer l+1 arrival by XCD (b % 8): " +
+                      " ".join(f"{v:.2f}" for v in by_xcd))
 
 
 if __name__ == "__main__":
