@@ -162,6 +162,22 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     }
   };
   float zxn[4][4] = {};
+  // G = 1: the layer-l input projection rows are loaded one tick ahead (at the previous tick's
+  // group start, behind its payload loads) and the gather ids two ticks ahead.  vmcnt retires in
+  // issue order, so rows loaded at the tick start (an id load, then the dependent table row: two
+  // round trips) had made the poller's first counter check wait for them every tick.
+  constexpr bool ZXA = G == 1 && !XIN;
+  const int bz = col * G * 32 + 16 * J + (lane & 15);  // (G = 1) this lane's row
+  const bool zl = ZXA && L == 0 && bz < B;
+  int idn = 0;  // gather id of the next tick's row
+  auto zx_row1 = [&](int tk, int id) -> const float* {
+    return a.ids ? a.zx0 + (size_t)id * a.zx_ld : a.zx0 + ((size_t)tk * B + bz) * a.zx_ld;
+  };
+  if (zl) {
+    const int id0 = a.ids ? a.ids[bz] : 0;
+    zx_load(zx_row1(0, id0), zxn);
+    if (a.ids && T > 1) idn = a.ids[(size_t)B + bz];
+  }
 
   for (int tau = 0; tau <= T + LAG - 1; ++tau) {
     const bool on0 = tau < T;                  // layer l   computes step tau
@@ -179,9 +195,11 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     // its id first; loaded for all groups here, the wait overlaps the poll).  (Loading group 0's
     // rows at the end of the previous tick measured slower: 603 -> 691 us per launch.)
     const float* zrows[G];
+    if constexpr (!ZXA) {
 #pragma unroll
-    for (int g = 0; g < G; ++g) zrows[g] = zx_row(tau, g);
-    zx_load(zrows[0], zxn);
+      for (int g = 0; g < G; ++g) zrows[g] = zx_row(tau, g);
+      zx_load(zrows[0], zxn);
+    }
     // XIN: layer l's input product of step tau (this wave's K quarter, both tiles, all gates),
     // the recurrent product is accumulated on top after the poll
     f32x4 xin[XIN ? 2 : 1][4];
@@ -298,7 +316,15 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
       } else {
         if (g > 0) load_group(g, pf0[0], pf1[0]);
       }
-      if (g + 1 < G) zx_load(zrows[g + 1], zxn);
+      if constexpr (ZXA) {
+        // the next tick's row (and the id of the one after), behind this tick's payload loads
+        if (zl && tau + 1 < T) {
+          zx_load(zx_row1(tau + 1, idn), zxn);
+          if (a.ids && tau + 2 < T) idn = a.ids[(size_t)(tau + 2) * B + bz];
+        }
+      } else {
+        if (g + 1 < G) zx_load(zrows[g + 1], zxn);
+      }
       // mask byte of this lane's x-part fragment (row 16 j + lane%16 of the group, k = kbase +
       // 32 s + kq .. +7), from the LDS stage (read at its use: no register is held for it
       // across the payload phase)
