@@ -91,7 +91,8 @@ __device__ __forceinline__ float row_reduce_scatter16(float (&v)[16], int lane) 
 //   0: at the tick start, before the poll (the poll then waits for them: +1.35 us hand-off)
 //   1: right behind the tick's payload loads (the MFMA / epilogue phase waits for them instead)
 //   2: one tick ahead, right after the previous tick's hand-off arrival: their latency runs
-//      concurrently with the hand-off's own (~1.7 us from arrival to the consumers' poll)
+//      concurrently with the hand-off's own (~1.7 us from arrival to the consumers' poll);
+//      the default (same-box A/B: 1.711 vs 1.726 ms/step for 0; 1 was slower than 0)
 template <int KS, bool DROP, int PF>
 __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) {
   static_assert(KS % 4 == 0, "K quarter = whole 32-wide k-steps per gate");
@@ -155,6 +156,15 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
   bf16x4 g4[4];
   float cc[4], cp[4], dtop[4];
   unsigned mrow = 0;
+  // buffer loads: a 32-bit per-lane offset fixed for the launch plus a wave-uniform per-tick
+  // offset in an SGPR (64-bit per-lane addresses had spilled, the reload a vmcnt(0) drain)
+  const __amdgpu_buffer_rsrc_t rg = make_rsrc(gtL, sizeof(bf16) * (size_t)T * B * G4H);
+  const __amdgpu_buffer_rsrc_t rc = make_rsrc(cbL, sizeof(float) * (size_t)(T + 1) * B * H);
+  const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.dtop1, sizeof(float) * (size_t)T * B * H);
+  const __amdgpu_buffer_rsrc_t rm = make_rsrc(a.xmask, DROP ? (size_t)T * B * (H / 8) : 0);
+  const unsigned vg = opaque_vgpr((unsigned)(((size_t)b * G4H + u0) * sizeof(bf16)));
+  const unsigned vc = opaque_vgpr((unsigned)(bh * sizeof(float)));
+  const unsigned vm = (unsigned)(b * (H / 8) + (ub0 >> 3));
   auto prefetch = [&](int tk) {
     const int tt = L ? T - 1 - tk : T + 1 - tk;
     const bool ac = L ? tk < T : tk >= 2;
@@ -165,16 +175,30 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
       cc[r] = cp[r] = dtop[r] = 0.f;
     }
     if (ac && live) {
-      const bf16* gp = gtL + ((size_t)tt * B + b) * G4H + u0;
+      const unsigned sg = (unsigned)((size_t)tt * B * G4H * sizeof(bf16));
 #pragma unroll
-      for (int gt = 0; gt < 4; ++gt) g4[gt] = *reinterpret_cast<const bf16x4*>(gp + gt * H);
-      ld4f(cbL + (size_t)(tt + 1) * B * H + bh, cc);
-      ld4f(cbL + (size_t)tt * B * H + bh, cp);
-      if (L) ld4f(a.dtop1 + (size_t)tt * B * H + bh, dtop);
+      for (int gt = 0; gt < 4; ++gt)
+        g4[gt] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(
+                                                rg, vg, sg + gt * H * (unsigned)sizeof(bf16), 0));
+      const unsigned sc = (unsigned)((size_t)tt * B * H * sizeof(float));
+      // (whole-vector bit casts: clang's __builtin_bit_cast of an ext-vector ELEMENT reads
+      // element 0 whatever the index, and the load is narrowed to one dword)
+      const f32x4 c1 = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, vc, sc + B * H * (unsigned)sizeof(float), 0));
+      const f32x4 c0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, vc, sc, 0));
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        cc[r] = c1[r];
+        cp[r] = c0[r];
+      }
+      if (L) {
+        const f32x4 d = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rd, vc, sc, 0));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dtop[r] = d[r];
+      }
     }
     if (DROP && tk >= 2 && tk <= T + 1 && live)
-      mrow = *reinterpret_cast<const unsigned*>(a.xmask + ((size_t)(T + 1 - tk) * B + b) * (H / 8) +
-                                                (ub0 >> 3));
+      mrow = __builtin_amdgcn_raw_buffer_load_b32(rm, vm, (unsigned)((size_t)(T + 1 - tk) * B * (H / 8)), 0);
   };
 
   for (int tau = 0; tau <= T + 1; ++tau) {
@@ -326,27 +350,20 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
 #pragma unroll
       for (int i = 0; i < 16; ++i) dcur[i] = (float)f2bf(dcur[i]);
       dbacc += row_reduce_scatter16(dcur, lane);
-      if (PF == 2 && tau < T + 1) prefetch(tau + 1);
-      if (ld1) {
+    }
+    if (PF == 2 && tau < T + 1) prefetch(tau + 1);
+    if (ld1) {  // every wave (with an epilogue this tick or not) stashes layer l's next dtop
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int u = 0; u < 2; ++u) {
+        f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int s = 0; s < KS; ++s) x = mfma16(wx1l[w][u][s][lane], p1[s], x);
-          xs[u] = x;
+        for (int s = 0; s < KS; ++s) {
+          x = mfma16(wx1l[w][u][s][lane], p1[s], x);
+          // (PF = 2: bound the LDS fragments the scheduler hoists ahead of the MFMAs; the
+          // prefetched operands are live here too)
+          if (PF == 2 && (s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
-      }
-    } else {
-      if (PF == 2 && tau < T + 1) prefetch(tau + 1);
-      if (ld1) {
-        // a wave without an epilogue this tick still stashes layer l's next dtop
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int s = 0; s < KS; ++s) x = mfma16(wx1l[w][u][s][lane], p1[s], x);
-          xs[u] = x;
-        }
+        xs[u] = x;
       }
     }
     STAMPW(7)
@@ -374,11 +391,11 @@ static const void* lstm2_bwd_wide_pick_t(int H) {
 }
 template <bool DROP>
 static const void* lstm2_bwd_wide_pick(int H) {
-  switch (debug_int("wide_pf", 0)) {
+  switch (debug_int("wide_pf", 2)) {
+    case 0: return lstm2_bwd_wide_pick_t<DROP, 0>(H);
     case 1: return lstm2_bwd_wide_pick_t<DROP, 1>(H);
-    case 2: return lstm2_bwd_wide_pick_t<DROP, 2>(H);
   }
-  return lstm2_bwd_wide_pick_t<DROP, 0>(H);
+  return lstm2_bwd_wide_pick_t<DROP, 2>(H);
 }
 
 // The 32-unit x 16-row BPTT applies at (H, B): H a multiple of 128 up to 512, and the grid of

@@ -853,7 +853,8 @@ void lstm2_persist_bwd(const at::Tensor& Wh0, const at::Tensor& Wh1, const at::T
   a.xscale = (float)xscale;
   a.db_rows = 2 * nbg / (int)G;
   int rc;
-  if (G == 1 && dcr::lstm2_bwd_wide_ok(H, B, num_cus())) {
+  // (the wide kernel addresses its activation operands with 32-bit buffer offsets)
+  if (G == 1 && dcr::lstm2_bwd_wide_ok(H, B, num_cus()) && n4 * 2 < ((int64_t)1 << 32)) {
     // 32-unit x 16-row workgroups: half the dZ payload per workgroup and tick
     a.nbg = (B + 15) / 16;
     for (auto* c : {&cnt0, &cnt1}) check_lstm2_counters(*c, a.nbg, T);

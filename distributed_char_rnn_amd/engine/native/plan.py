@@ -34,7 +34,7 @@ DEBUG_KEYS = {
     "pair_bwd": "0: paired forward, single-layer BPTT",
     "wide": "0: the 16-unit x 32-row pair BPTT instead of the 32 x 16 one (C++ launcher)",
     "wgarr": "0: one hand-off counter add per epilogue wave in the pair kernels (C++ launcher)",
-    "wide_pf": "wide BPTT epilogue-operand loads: 0 (default) before the poll, 1 after the payload, 2 one tick ahead (C++ launcher)",
+    "wide_pf": "wide BPTT epilogue-operand loads: 0 before the poll, 1 after the payload, 2 (default) one tick ahead (C++ launcher)",
     "fused_head": "0: library logits GEMM + CE kernel instead of the fused head",
     "dew": "layer-0 embedding-table gradient: gemm (one-hot MFMA GEMM, default) | segsum | fused",
     "side": "0: no side-stream weight GEMMs in overlap mode",
