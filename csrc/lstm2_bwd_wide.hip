@@ -93,6 +93,11 @@ __device__ __forceinline__ float row_reduce_scatter16(float (&v)[16], int lane) 
 //   2: one tick ahead, right after the previous tick's hand-off arrival: their latency runs
 //      concurrently with the hand-off's own (~1.7 us from arrival to the consumers' poll);
 //      the default (same-box A/B: 1.711 vs 1.726 ms/step for 0; 1 was slower than 0)
+//   3: 2 for waves 1-3, 1 for wave 0, whose lane 0 polls: the poll then waits for no HBM load
+//   4: 2 for waves 1-3; wave 0 (the poller) issues no HBM load at all: wave 1 DMAs wave 0's
+//      operands (buffer_load ... lds, 16 dwords per lane) into a per-parity LDS buffer one tick
+//      ahead, and wave 0 reads them after the tick's second barrier (wave 1's waits on its own
+//      younger payload loads have covered the DMA by then).  No dropout variant.
 template <int KS, bool DROP, int PF>
 __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) {
   static_assert(KS % 4 == 0, "K quarter = whole 32-wide k-steps per gate");
@@ -102,6 +107,8 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
   // the wave that wrote them (the off-critical-path dtop stash)
   __shared__ __attribute__((aligned(16))) bf16x8 wx1l[4][2][KS][64];
   __shared__ unsigned arrl[2];              // per-layer arrivals of the tick (wgarr)
+  // PF = 4: wave 0's epilogue operands by tick parity: g4 (8 dwords), c_{t+1} (4), c_t (4)
+  __shared__ __attribute__((aligned(16))) unsigned opb[PF == 4 ? 2 : 1][PF == 4 ? 16 : 1][64];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
@@ -209,7 +216,8 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
     const int t = L ? T - 1 - tau : T + 1 - tau;  // this role's step
     const bool act = L ? on1 : on0;
     STAMPW(0)
-    if (PF != 2 || tau == 0) prefetch(tau);
+    if (PF == 0 || (PF == 1 && tau == 0) || (PF >= 2 && tau == 0 && !(PF == 4 && w == 0)))
+      prefetch(tau);
     const int s1 = T - tau, s0 = T + 2 - tau;  // ring slots of dZ_{l+1} and dZ_l
     if (tau >= 1) {
       if (threadIdx.x == kLstmPollerThread && !dead && (ld1 || ld0)) {
@@ -238,7 +246,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
         for (int s = 0; s < KS; ++s)
           p0[s] = ld8_sc1(rz0, frag_load_off(col, kcol(s) >> 5, G4H, lane) + o0);
       }
-      if (PF == 1) prefetch(tau);
+      if (PF == 1 || (PF == 3 && w == 0)) prefetch(tau);
       __builtin_amdgcn_sched_barrier(0);
       if (on1) {  // layer l+1: dh partial = dZ_{l+1}[t+1] · W_h,l+1ᵀ, both unit halves
         f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
@@ -287,6 +295,24 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
     STAMPW(3)
     __syncthreads();
     STAMPW(4)
+    if constexpr (PF == 4) if (w == 0 && act) {  // this wave's operands, DMA'd by wave 1
+      const unsigned(&ob)[16][64] = opb[tau & 1];
+#pragma unroll
+      for (int gt = 0; gt < 4; ++gt)
+        g4[gt] = __builtin_bit_cast(bf16x4, u32x2{ob[2 * gt][lane], ob[2 * gt + 1][lane]});
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        cc[r] = live ? __builtin_bit_cast(float, ob[8 + r][lane]) : 0.f;
+        cp[r] = live ? __builtin_bit_cast(float, ob[12 + r][lane]) : 0.f;
+        dtop[r] = 0.f;  // (layer l: its dtop is inside the partials; prefetch() never ran here)
+      }
+      if (!live) {
+#pragma unroll
+        for (int gt = 0; gt < 4; ++gt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) g4[gt][r] = (bf16)0.f;
+      }
+    }
     if (act) {
       float dh[4];
       {
@@ -351,7 +377,32 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
       for (int i = 0; i < 16; ++i) dcur[i] = (float)f2bf(dcur[i]);
       dbacc += row_reduce_scatter16(dcur, lane);
     }
-    if (PF == 2 && tau < T + 1) prefetch(tau + 1);
+    if ((PF == 2 || ((PF == 3 || PF == 4) && w != 0)) && tau < T + 1) prefetch(tau + 1);
+    if constexpr (PF == 4) if (w == 1 && tau + 1 >= 2 && tau + 1 <= T + 1) {
+      // wave 0's (layer l, unit half 0) operands of the next tick into opb[(tau + 1) & 1]
+      const int tt = T - tau;  // = T + 1 - (tau + 1)
+      const unsigned q = 4 * (lane >> 4);
+      const unsigned og = (unsigned)(((size_t)b * G4H + ub0 + q) * sizeof(bf16));
+      const unsigned oc = (unsigned)(((size_t)b * H + ub0 + q) * sizeof(float));
+      const unsigned sg = (unsigned)((size_t)tt * B * G4H * sizeof(bf16));
+      const unsigned sc = (unsigned)((size_t)tt * B * H * sizeof(float));
+      unsigned(&ob)[16][64] = opb[(tau + 1) & 1];
+#pragma unroll
+      for (int gt = 0; gt < 4; ++gt)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rg, (__attribute__((address_space(3))) void*)&ob[2 * gt + h][0], 4, og + 4 * h,
+              sg + gt * H * (unsigned)sizeof(bf16), 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rc, (__attribute__((address_space(3))) void*)&ob[8 + r][0], 4, oc + 4 * r,
+            sc + B * H * (unsigned)sizeof(float), 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rc, (__attribute__((address_space(3))) void*)&ob[12 + r][0], 4, oc + 4 * r, sc, 0, 0);
+      }
+    }
     if (ld1) {  // every wave (with an epilogue this tick or not) stashes layer l's next dtop
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -361,7 +412,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
           x = mfma16(wx1l[w][u][s][lane], p1[s], x);
           // (PF = 2: bound the LDS fragments the scheduler hoists ahead of the MFMAs; the
           // prefetched operands are live here too)
-          if (PF == 2 && (s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+          if (PF >= 2 && (s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
         xs[u] = x;
       }
@@ -394,6 +445,8 @@ static const void* lstm2_bwd_wide_pick(int H) {
   switch (debug_int("wide_pf", 2)) {
     case 0: return lstm2_bwd_wide_pick_t<DROP, 0>(H);
     case 1: return lstm2_bwd_wide_pick_t<DROP, 1>(H);
+    case 3: return lstm2_bwd_wide_pick_t<DROP, 3>(H);
+    case 4: return DROP ? lstm2_bwd_wide_pick_t<DROP, 2>(H) : lstm2_bwd_wide_pick_t<DROP, 4>(H);
   }
   return lstm2_bwd_wide_pick_t<DROP, 2>(H);
 }

@@ -20,9 +20,10 @@ def rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
 
 
-def _run(cfg, B, T, wide, monkeypatch, steps=2):
+def _run(cfg, B, T, wide, monkeypatch, steps=2, pf=None):
     monkeypatch.setenv("DCR_SPIN_LIMIT", str(1 << 20))
-    monkeypatch.setenv("DCR_DEBUG", "persist_min_t=1" + ("" if wide else ",wide=0"))
+    monkeypatch.setenv("DCR_DEBUG", "persist_min_t=1" + ("" if wide else ",wide=0") +
+                       (f",wide_pf={pf}" if pf is not None else ""))
     m = CharRNN(cfg, device="cuda", seed=21)
     plan = m.backend._persist_plan(B, True, T)
     assert plan.pair_bwd and plan.pair_g == 1, plan
@@ -37,15 +38,17 @@ def _run(cfg, B, T, wide, monkeypatch, steps=2):
     return m, loss.item(), [s.clone() for t in st for s in t]
 
 
+@pytest.mark.parametrize("pf", [None, 0, 1, 3, 4])
 @pytest.mark.parametrize("B,T,H,drop", [(256, 8, 512, False), (50, 7, 128, False),
                                         (37, 6, 512, False), (100, 5, 256, True),
                                         (256, 6, 512, True)])
-def test_wide_bptt_equals_narrow(B, T, H, drop, monkeypatch, dcr_ops):
+def test_wide_bptt_equals_narrow(B, T, H, drop, pf, monkeypatch, dcr_ops):
+    """Every operand-prefetch mode of the wide kernel (``wide_pf``, None = the default)."""
     assert dcr_ops.lstm2_bwd_wide_ok(H, B)
     kp = 0.8 if drop else 1.0
     cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=2,
                       input_keep_prob=kp, output_keep_prob=kp)
-    a, la, sa = _run(cfg, B, T, True, monkeypatch)
+    a, la, sa = _run(cfg, B, T, True, monkeypatch, pf=pf)
     b, lb, sb = _run(cfg, B, T, False, monkeypatch)
     assert la == lb
     for u, v in zip(sa, sb):
