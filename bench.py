@@ -49,7 +49,11 @@ def parse(argv=None):
                     help="dropout (DropoutWrapper input keep prob; default off as in the reference)")
     ap.add_argument("--output_keep_prob", type=float, default=1.0,
                     help="dropout (DropoutWrapper output + embedding keep prob)")
-    ap.add_argument("--profile", action="store_true", help="print a per-phase timing table")
+    ap.add_argument("--profile", action="store_true",
+                    help="print a per-phase timing table and the gradient buckets' overlap windows")
+    ap.add_argument("--force_sync", action="store_true",
+                    help="run the bucketed RCCL gradient exchange even on one rank (measures its "
+                         "cost and release schedule on a one-GPU box)")
     ap.add_argument("--graph", action="store_true",
                     help="replay each step from one captured HIP graph (one GPU, no dropout)")
     ap.add_argument("--dist_backend", default="auto", choices=["auto", "nccl", "gloo"],
@@ -93,14 +97,24 @@ def main(argv=None) -> int:
     opt = TFAdam(model.store, clip=5.0, guard=model.error_word())
     sharded = a.dp_mode == "sharded" and world > 1
     sync = GradSync(model.store, world, a.bucket_mb, a.allreduce_dtype,
-                    enabled=world > 1 and not sharded)
+                    enabled=(world > 1 or a.force_sync) and not sharded,
+                    guard=model.error_word(), timing=a.profile)
+    if sync.enabled and sync.guard_view is not None:
+        opt.guard = sync.guard_view  # every rank's error word, summed with the last bucket
+    if a.force_sync and world == 1 and not dist.is_initialized():
+        import os
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        dist.init_process_group(backend, rank=0, world_size=1)
     if world > 1:
         dist.broadcast(model.store.flat, 0)
     zstep = None
     if sharded:
         from distributed_char_rnn_amd.parallel.zero import ShardedStep
 
-        zstep = ShardedStep(model.store, opt, world, rank, wire=a.allreduce_dtype)
+        zstep = ShardedStep(model.store, opt, world, rank, wire=a.allreduce_dtype,
+                            bucket_mb=a.bucket_mb, guard=model.error_word())
     model.params_changed()
 
     B, T = a.batch, a.seq
@@ -134,8 +148,9 @@ def main(argv=None) -> int:
             state = model.zero_state(B)
         if graphed is not None:
             return graphed(x, y, state, 2e-3)
-        if zstep is not None:
-            loss, state, _ = model.train_step(x, y, state)
+        if zstep is not None:  # each bucket's reduce-scatter leaves during the backward
+            zstep.reset()
+            loss, state, _ = model.train_step(x, y, state, zstep)
             zstep.step(2e-3)
             return loss, state
         sync.reset()
@@ -177,6 +192,18 @@ def main(argv=None) -> int:
     if rank == 0:
         if prof is not None:
             print(prof.table(), file=sys.stderr)
+            win = sync.windows()
+            if win:
+                print("gradient buckets (last step): release after step start / overlap window "
+                      "until the backward ends", file=sys.stderr)
+                for i, nb, t, w in win:
+                    print(f"  bucket {i}: {nb / 2**20:7.2f} MB  released {t:8.3f} ms  window "
+                          f"{w:7.3f} ms", file=sys.stderr)
+                for n in (2, 4, 8):
+                    ex = " ".join(f"{bw} GB/s: {GradSync.exposed_ms(win, n, bw):.3f} ms"
+                                  for bw in (100, 300))
+                    print(f"  modelled exposed all-reduce time at N={n} (bus bandwidth) {ex}",
+                          file=sys.stderr)
         out = {
             "metric": METRIC, "value": cps, "unit": "chars/sec", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms,
@@ -195,6 +222,8 @@ def main(argv=None) -> int:
         }
         print(json.dumps(out), flush=True)
     ctx.shutdown()
+    if a.force_sync and world == 1 and dist.is_initialized():
+        dist.destroy_process_group()
     return 0
 
 

@@ -224,6 +224,8 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
     sync = GradSync(model.store, ctx.world_size, getattr(args, "bucket_mb", 8.0),
                     getattr(args, "allreduce_dtype", "fp32"),
                     enabled=(ctx.world_size > 1 and not sharded), guard=model.error_word())
+    if sync.enabled and sync.guard_view is not None:
+        opt.guard = sync.guard_view  # the error words of every rank, summed with the last bucket
     zstep = None
     saved_state = None
     if ctx.world_size > 1:

@@ -36,23 +36,37 @@ from ..models.params import ParamStore
 class GradSync:
     def __init__(self, store: ParamStore, world_size: int, bucket_mb: float = 8.0,
                  wire_dtype: str = "fp32", group=None, enabled: Optional[bool] = None,
-                 guard: Optional[torch.Tensor] = None):
-        """``guard``: the rank's persistent-kernel error word (``TFAdam(guard=...)``).  It is
-        MAX-reduced over ranks in :meth:`finish`, on the stream, before the optimizer reads it:
-        a rank whose recurrence timed out contributed garbage gradients to the sum, so EVERY
-        rank must skip that update (a local guard alone would let the healthy ranks apply it
-        while the faulty one skips, and the replicas would diverge)."""
+                 guard: Optional[torch.Tensor] = None, timing: bool = False):
+        """``guard``: the rank's persistent-kernel error word.  A rank whose recurrence timed out
+        contributed garbage gradients to the sum, so EVERY rank must skip that update (a local
+        guard alone would let the healthy ranks apply it while the faulty one skips, and the
+        replicas would diverge).  The word rides along with the last bucket: it is copied (as
+        a float) into a padding slot of the gradient buffer behind the clip-norm slot, summed
+        with everything else, and ``guard_view`` -- that slot's bits as int32, non-zero iff any
+        rank's word was -- is what the optimizer must use as its guard (``TFAdam.guard``).  No
+        extra collective per step."""
         self.store = store
         self.world = world_size
         self.group = group
         self.enabled = (world_size > 1) if enabled is None else enabled
         self.wire_bf16 = wire_dtype == "bf16"
         self.guard = guard
+        self.guard_slot = store.norm_slot + 1
+        if self.guard_slot >= store.numel:
+            raise ValueError("no padding slot for the error word behind the clip-norm slot")
+        self.guard_view = (store.grad[self.guard_slot:self.guard_slot + 1].view(torch.int32)
+                           if guard is not None else None)
         self.buckets = self._make_buckets(bucket_mb)
         self._next = 0
         self._work: List[Tuple[object, int, int, Optional[torch.Tensor]]] = []
         # bf16 wire: per-bucket send / receive / gather buffers, allocated once
         self._wire_bufs: dict = {}
+        # --profile: CUDA events at the step start, at each bucket's release (its gradients are
+        # final on the compute stream) and at the end of the backward (finish), see windows()
+        self.timing = timing and store.flat.device.type == "cuda"
+        self._ev_start = None
+        self._ev_ready: List[Tuple[int, object]] = []
+        self._ev_end = None
 
     def _make_buckets(self, bucket_mb: float) -> List[Tuple[int, int]]:
         """Cut the flat buffer at tensor boundaries into ~bucket_mb slices.  The last tensor
@@ -91,6 +105,11 @@ class GradSync:
     def reset(self):
         self._next = 0
         self._work.clear()
+        if self.timing:
+            self._ev_start = torch.cuda.Event(enable_timing=True)
+            self._ev_start.record()
+            self._ev_ready = []
+            self._ev_end = None
 
     def ready(self, upto: Optional[int] = None):
         """Launch every not-yet-launched bucket that ends at or below flat offset ``upto``
@@ -101,6 +120,12 @@ class GradSync:
         while self._next < len(self.buckets) and self.buckets[self._next][1] <= lim:
             lo, hi = self.buckets[self._next]
             g = self.store.grad[lo:hi]
+            if self.guard is not None and lo <= self.guard_slot < hi:
+                self.store.grad[self.guard_slot:self.guard_slot + 1].copy_(self.guard)
+            if self.timing:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                self._ev_ready.append((self._next, ev))
             if self.wire_bf16:
                 # bf16 on the wire, fp32 accumulation: the bucket's world chunks travel once
                 # through an all_to_all, each rank sums its chunk in fp32, the sums come back
@@ -122,6 +147,9 @@ class GradSync:
         pass over the gradient buffer)."""
         if not self.enabled:
             return 1.0
+        if self.timing:
+            self._ev_end = torch.cuda.Event(enable_timing=True)
+            self._ev_end.record()
         self.ready(None)
         gathers = []
         for w, lo, hi, recv in self._work:
@@ -132,9 +160,6 @@ class GradSync:
                 mine16.copy_(mine)
                 gw = dist.all_gather_into_tensor(full, mine16, group=self.group, async_op=True)
                 gathers.append((gw, lo, hi, full))
-        if self.guard is not None:
-            # one rank's timed-out recurrence poisons the summed gradient: every rank skips
-            dist.all_reduce(self.guard, op=dist.ReduceOp.MAX, group=self.group)
         for gw, lo, hi, full in gathers:
             gw.wait()
             self.store.grad[lo:hi].copy_(full[: hi - lo])
@@ -142,11 +167,40 @@ class GradSync:
         self._next = 0
         if defer_scale:
             return 1.0 / self.world
-        self.store.grad.mul_(1.0 / self.world)
+        self.store.grad.mul_(1.0 / self.world)  # (the guard slot stays non-zero iff it was)
         # the clip-norm slot holds a SUM OF SQUARES (TF's per-token embedding term, summed over
         # ranks): averaging the gradients scales it by 1/world^2, not 1/world
         self.store.norm_slot_view().mul_(1.0 / self.world)
         return 1.0
+
+    def windows(self) -> List[Tuple[int, int, float, float]]:
+        """(bucket, bytes on the wire, release time from the step start [ms], overlap window =
+        end of the backward - release [ms]) of the last step; synchronises.  Buckets released
+        by ``finish`` itself have a zero window."""
+        if not (self.timing and self._ev_start is not None and self._ev_end is not None):
+            return []
+        torch.cuda.synchronize()
+        out = []
+        esz = 2 if self.wire_bf16 else 4
+        for i, ev in self._ev_ready:
+            lo, hi = self.buckets[i]
+            t = self._ev_start.elapsed_time(ev)
+            out.append((i, (hi - lo) * esz, t, max(0.0, self._ev_start.elapsed_time(self._ev_end) - t)))
+        return out
+
+    @staticmethod
+    def exposed_ms(windows, world: int, busbw_gbps: float, latency_us: float = 25.0) -> float:
+        """Communication time left after the backward ends, for a ring all-reduce of each bucket
+        at ``busbw_gbps`` bus bandwidth (2(N-1)/N·S / busbw + latency per call), buckets issued in
+        order on one stream, each no earlier than its release."""
+        if world <= 1 or not windows:
+            return 0.0
+        end_bwd = max(t + w for _, _, t, w in windows)
+        tnow = 0.0
+        for _, nbytes, t, _ in windows:
+            cost = 2.0 * (world - 1) / world * nbytes / (busbw_gbps * 1e9) * 1e3 + latency_us * 1e-3
+            tnow = max(tnow, t) + cost
+        return max(0.0, tnow - end_bwd)
 
     def _bufs_for(self, lo: int, hi: int, device) -> tuple:
         """bf16-wire buffers of bucket [lo, hi): (send, recv) of world·c bf16 elements, the

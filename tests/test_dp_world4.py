@@ -56,6 +56,7 @@ def _worker(rank, world, port, mode, steps, fault_rank, fault_step, q):
         dist.broadcast(m.store.flat, 0)
         if mode == "replicated":
             sync = GradSync(m.store, world, 0.0005, "fp32", guard=guard)
+            opt.guard = sync.guard_view  # the error words summed with the last bucket
         else:
             sync = ShardedStep(m.store, opt, world, rank, wire="fp32", bucket_mb=0.0005,
                                guard=guard)
@@ -66,9 +67,9 @@ def _worker(rank, world, port, mode, steps, fault_rank, fault_step, q):
             blk = data[s, rank * B:(rank + 1) * B]
             sync.reset()
             guard.zero_()
-            _, st, _ = m.train_step(blk[:, :-1], blk[:, 1:], st, sync)
             if s == fault_step and rank == fault_rank:
-                guard.fill_(10)  # this rank's recurrence "timed out" during the step
+                guard.fill_(10)  # this rank's recurrence "times out" during the step's backward
+            _, st, _ = m.train_step(blk[:, :-1], blk[:, 1:], st, sync)
             if mode == "replicated":
                 gs = sync.finish(defer_scale=True)
                 norms.append(float(opt.step(0.01, grad_scale=gs)))
@@ -78,6 +79,7 @@ def _worker(rank, world, port, mode, steps, fault_rank, fault_step, q):
             snaps.append(m.store.flat.numpy().copy())
         if mode != "replicated":
             sync.gather_slots()
+        guard.zero_()
         q.put((rank, snaps, opt.m.numpy().copy(), norms, early, int(guard.item())))
     finally:
         dist.destroy_process_group()
