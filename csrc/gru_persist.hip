@@ -23,6 +23,10 @@
 // Wave w < UB*NT runs the cell epilogue of unit block w % UB, batch tile w / UB, with h_{t-1} /
 // the dh carry in registers.
 // Counters: two sets per launch (phase A and phase B), one per (batch group, step, K quarter).
+// Any batch: a ragged batch is padded to whole 16·NT-row groups (rows >= B read zero through the
+// buffer range checks, write only the fragment-tiled hand-off rings -- sized for the padded
+// batch -- and never the row-major buffers), so the reference default B = 50 (train.py:46)
+// stays on the persistent kernels.
 #include "common.h"
 #include "kernels.h"
 #include "debug_env.h"
@@ -30,6 +34,11 @@
 #include <stdlib.h>
 
 namespace dcr {
+
+// rows of the padded batch: whole groups of NT 16-row tiles
+__host__ __device__ __forceinline__ int gru_rows(int B, int nt) {
+  return (B + 16 * nt - 1) / (16 * nt) * (16 * nt);
+}
 
 // ------------------------------------------------------------------------------------------
 // forward
@@ -43,13 +52,14 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
+  const int Bp = gru_rows(B, NT);  // ring rows (padded batch)
   const int nwg_u = H / (16 * UB);
   int ubk, bg;
-  map_block(blockIdx.x, nwg_u, B / (16 * NT), ubk, bg);
+  map_block(blockIdx.x, nwg_u, Bp / (16 * NT), ubk, bg);
   const int ub0 = ubk * 16 * UB, b0 = bg * 16 * NT;
   const int kq = 8 * (lane >> 4);
   const int kbase = w * (KS * 32);
-  const size_t cset = (size_t)(B / (16 * NT)) * (T + 1) * 4;
+  const size_t cset = (size_t)(Bp / (16 * NT)) * (T + 1) * 4;
   unsigned* cntH = a.cnt + (size_t)bg * (T + 1) * 4;         // slot t: h_t published
   unsigned* cntR = a.cnt + cset + (size_t)bg * (T + 1) * 4;  // slot t: r⊙h_{t-1} published
   const unsigned target = (unsigned)(H / (64 * UB));  // workgroups per K-quarter shard
@@ -77,11 +87,12 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
   const bool epi = w < UB * NT;
   const int eu = epi ? w % UB : 0, en = epi ? w / UB : 0;
   const int b = b0 + 16 * en + (lane & 15);
+  const bool live = b < B;  // padded rows: zero inputs, ring stores only
   const int u0 = ub0 + eu * 16 + 4 * (lane >> 4);
   const size_t bh = (size_t)b * H + u0;
   const int G3 = 3 * H;
   float hp[4] = {0.f, 0.f, 0.f, 0.f};
-  if (epi) ld4f(a.h32 + bh, hp);  // h_0, fp32
+  if (epi && live) ld4f(a.h32 + bh, hp);  // h_0, fp32
   // input bias added here when the dense zx was written without it (one [T·B, 3H] fp32 pass
   // less behind the input GEMM)
   float bx[3][4] = {};
@@ -91,8 +102,8 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
   }
 
   for (int t = 0; t < T; ++t) {
-    float zx[3][4];
-    if (epi) {
+    float zx[3][4] = {};
+    if (epi && live) {
       const float* zrow = a.ids ? a.zx + (size_t)a.ids[(size_t)t * B + b] * a.zx_ld
                                 : a.zx + ((size_t)t * B + b) * a.zx_ld;
 #pragma unroll
@@ -107,7 +118,7 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
     {
       const bool fr = a.ring0 && t > 0;  // slot 0 (initial state) is row-major
       const __amdgpu_buffer_rsrc_t src =
-          fr ? make_rsrc(a.ring0 + (size_t)(t & 1) * B * H, sizeof(bf16) * (size_t)B * H)
+          fr ? make_rsrc(a.ring0 + (size_t)(t & 1) * Bp * H, sizeof(bf16) * (size_t)Bp * H)
              : make_rsrc(a.hbuf + (size_t)t * B * H, sizeof(bf16) * (size_t)B * H);
       bf16x8 hf[NT][KS];
 #pragma unroll
@@ -149,16 +160,18 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
       }
       const float rh0 = rr[0] * hp[0], rh1 = rr[1] * hp[1], rh2 = rr[2] * hp[2], rh3 = rr[3] * hp[3];
       if (a.ring1)
-        st4bf_sc1(a.ring1 + (size_t)(t & 1) * B * H + frag_index(b, u0, H), rh0, rh1, rh2, rh3);
+        st4bf_sc1(a.ring1 + (size_t)(t & 1) * Bp * H + frag_index(b, u0, H), rh0, rh1, rh2, rh3);
       else
         st4bf_sc1(a.rh + (size_t)t * B * H + bh, rh0, rh1, rh2, rh3);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0)
         wg_arrive(&wg_cnt[0], UB * NT, cntR + (size_t)t * 4 + (u0 / (H / 4)));
-      if (a.ring1) st4bf(a.rh + (size_t)t * B * H + bh, rh0, rh1, rh2, rh3);
-      bf16* gp = a.gates + ((size_t)t * B + b) * G3 + u0;
-      st4bf(gp, rr[0], rr[1], rr[2], rr[3]);
-      st4bf(gp + H, uu[0], uu[1], uu[2], uu[3]);
+      if (live) {
+        if (a.ring1) st4bf(a.rh + (size_t)t * B * H + bh, rh0, rh1, rh2, rh3);
+        bf16* gp = a.gates + ((size_t)t * B + b) * G3 + u0;
+        st4bf(gp, rr[0], rr[1], rr[2], rr[3]);
+        st4bf(gp + H, uu[0], uu[1], uu[2], uu[3]);
+      }
     }
     // ---- phase B: c~ from r⊙h_{t-1}
     if (threadIdx.x == kPollerThread && !dead)
@@ -166,7 +179,7 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
     __syncthreads();
     {
       const __amdgpu_buffer_rsrc_t src =
-          a.ring1 ? make_rsrc(a.ring1 + (size_t)(t & 1) * B * H, sizeof(bf16) * (size_t)B * H)
+          a.ring1 ? make_rsrc(a.ring1 + (size_t)(t & 1) * Bp * H, sizeof(bf16) * (size_t)Bp * H)
                   : make_rsrc(a.rh + (size_t)t * B * H, sizeof(bf16) * (size_t)B * H);
       bf16x8 rf[NT][KS];
 #pragma unroll
@@ -202,7 +215,7 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
       for (int r = 0; r < 4; ++r) h[r] = uu[r] * hp[r] + (1.f - uu[r]) * cc[r];
       const size_t o = (size_t)(t + 1) * B * H + bh;
       if (a.ring0)
-        st4bf_sc1(a.ring0 + (size_t)((t + 1) & 1) * B * H + frag_index(b, u0, H), h[0], h[1],
+        st4bf_sc1(a.ring0 + (size_t)((t + 1) & 1) * Bp * H + frag_index(b, u0, H), h[0], h[1],
                   h[2], h[3]);
       else
         st4bf_sc1(a.hbuf + o, h[0], h[1], h[2], h[3]);
@@ -211,11 +224,13 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
         if (lane == 0)
           wg_arrive(&wg_cnt[1], UB * NT, cntH + (size_t)(t + 1) * 4 + (u0 / (H / 4)));
       }
-      if (a.ring0) st4bf(a.hbuf + o, h[0], h[1], h[2], h[3]);
-      *reinterpret_cast<float4*>(a.h32 + o) = make_float4(h[0], h[1], h[2], h[3]);
-      st4bf(a.gates + ((size_t)t * B + b) * G3 + 2 * H + u0, cc[0], cc[1], cc[2], cc[3]);
-      if (t == T - 1 && a.hlast32)
-        *reinterpret_cast<float4*>(a.hlast32 + bh) = make_float4(h[0], h[1], h[2], h[3]);
+      if (live) {
+        if (a.ring0) st4bf(a.hbuf + o, h[0], h[1], h[2], h[3]);
+        *reinterpret_cast<float4*>(a.h32 + o) = make_float4(h[0], h[1], h[2], h[3]);
+        st4bf(a.gates + ((size_t)t * B + b) * G3 + 2 * H + u0, cc[0], cc[1], cc[2], cc[3]);
+        if (t == T - 1 && a.hlast32)
+          *reinterpret_cast<float4*>(a.hlast32 + bh) = make_float4(h[0], h[1], h[2], h[3]);
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) hp[r] = h[r];
     }
@@ -236,13 +251,14 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
+  const int Bp = gru_rows(B, NT);  // ring rows (padded batch)
   const int nwg_u = H / (16 * UB);
   int ubk, bg;
-  map_block(blockIdx.x, nwg_u, B / (16 * NT), ubk, bg);
+  map_block(blockIdx.x, nwg_u, Bp / (16 * NT), ubk, bg);
   const int ub0 = ubk * 16 * UB, b0 = bg * 16 * NT;
   const int kq = 8 * (lane >> 4);
   const int kA = w * (KA * 32), kB = w * (KB * 32);
-  const size_t cset = (size_t)(B / (16 * NT)) * (T + 1) * 4;
+  const size_t cset = (size_t)(Bp / (16 * NT)) * (T + 1) * 4;
   unsigned* cntC = a.cnt + (size_t)bg * (T + 1) * 4;         // slot t: dZc_t published
   unsigned* cntG = a.cnt + cset + (size_t)bg * (T + 1) * 4;  // slot t: dZg_t published
   const unsigned target = (unsigned)(H / (64 * UB));  // workgroups per K-quarter shard
@@ -266,6 +282,7 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
   const bool epi = w < UB * NT;
   const int eu = epi ? w % UB : 0, en = epi ? w / UB : 0;
   const int b = b0 + 16 * en + (lane & 15);
+  const bool live = b < B;  // padded rows: zero inputs, ring stores only
   const int u0 = ub0 + eu * 16 + 4 * (lane >> 4);
   const size_t bh = (size_t)b * H + u0;
   // MFMA operands (row-major dZ path): batch tile n at + n * tile_off
@@ -277,29 +294,31 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
 
   // dZc_{T-1} from the top gradient alone
   if (epi) {
-    float uu[4], cc[4];
-    ld4f(a.dtop + (size_t)(T - 1) * B * H + bh, dhp);
-    const bf16* gp = a.gates + ((size_t)(T - 1) * B + b) * G3 + u0;
-    ld4bf(gp + H, uu);
-    ld4bf(gp + 2 * H, cc);
+    float uu[4] = {0.f, 0.f, 0.f, 0.f}, cc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (live) {
+      ld4f(a.dtop + (size_t)(T - 1) * B * H + bh, dhp);
+      const bf16* gp = a.gates + ((size_t)(T - 1) * B + b) * G3 + u0;
+      ld4bf(gp + H, uu);
+      ld4bf(gp + 2 * H, cc);
+    }
     float z0[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) z0[r] = dhp[r] * (1.f - uu[r]) * (1.f - cc[r] * cc[r]);
     bf16* const zrow = a.dz + ((size_t)(T - 1) * B + b) * G3 + 2 * H + u0;
     if (a.ring0)
-      st4bf_sc1(a.ring0 + (size_t)((T - 1) & 1) * B * H + frag_index(b, u0, H), z0[0], z0[1], z0[2], z0[3]);
+      st4bf_sc1(a.ring0 + (size_t)((T - 1) & 1) * Bp * H + frag_index(b, u0, H), z0[0], z0[1], z0[2], z0[3]);
     else
       st4bf_sc1(zrow, z0[0], z0[1], z0[2], z0[3]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0)
       wg_arrive(&wg_cnt[1], UB * NT, cntC + (size_t)(T - 1) * 4 + (u0 / (H / 4)));
-    if (a.ring0) st4bf(zrow, z0[0], z0[1], z0[2], z0[3]);
+    if (a.ring0 && live) st4bf(zrow, z0[0], z0[1], z0[2], z0[3]);
   }
 
   for (int t = T - 1; t >= 0; --t) {
     // recurrence-independent epilogue operands, issued before the waits
-    float rr[4], uu[4], cc[4], hp[4], dt[4], up[4], cp[4];
-    if (epi) {
+    float rr[4] = {}, uu[4] = {}, cc[4] = {}, hp[4] = {}, dt[4] = {}, up[4] = {}, cp[4] = {};
+    if (epi && live) {
       const bf16* gp = a.gates + ((size_t)t * B + b) * G3 + u0;
       ld4bf(gp, rr); ld4bf(gp + H, uu); ld4bf(gp + 2 * H, cc);
       ld4f(a.h32 + (size_t)t * B * H + bh, hp);
@@ -319,7 +338,7 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
       bf16x8 zf[NT][KA];
       if (a.ring0) {
         const __amdgpu_buffer_rsrc_t rc =
-            make_rsrc(a.ring0 + (size_t)(t & 1) * B * H, sizeof(bf16) * (size_t)B * H);
+            make_rsrc(a.ring0 + (size_t)(t & 1) * Bp * H, sizeof(bf16) * (size_t)Bp * H);
 #pragma unroll
         for (int n = 0; n < NT; ++n)
 #pragma unroll
@@ -362,7 +381,7 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
       }
       bf16* dz = a.dz + ((size_t)t * B + b) * G3 + u0;
       if (a.ring1) {
-        bf16* gr = a.ring1 + (size_t)(t & 1) * B * 2 * H;
+        bf16* gr = a.ring1 + (size_t)(t & 1) * Bp * 2 * H;
         st4bf_sc1(gr + frag_index(b, u0, 2 * H), dzr[0], dzr[1], dzr[2], dzr[3]);
         st4bf_sc1(gr + frag_index(b, H + u0, 2 * H), dzu[0], dzu[1], dzu[2], dzu[3]);
       } else {
@@ -374,7 +393,7 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
         if (lane == 0)
           wg_arrive(&wg_cnt[0], UB * NT, cntG + (size_t)t * 4 + (u0 / (H / 4)));
       }
-      if (a.ring1) {
+      if (a.ring1 && live) {
         st4bf(dz, dzr[0], dzr[1], dzr[2], dzr[3]);
         st4bf(dz + H, dzu[0], dzu[1], dzu[2], dzu[3]);
       }
@@ -387,7 +406,7 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
     {
       // one batch tile at a time: KB = 2 KA payload fragments per tile is the register limit
       const __amdgpu_buffer_rsrc_t rg =
-          a.ring1 ? make_rsrc(a.ring1 + (size_t)(t & 1) * B * 2 * H, sizeof(bf16) * (size_t)B * 2 * H)
+          a.ring1 ? make_rsrc(a.ring1 + (size_t)(t & 1) * Bp * 2 * H, sizeof(bf16) * (size_t)Bp * 2 * H)
                   : zsrc;
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
@@ -422,14 +441,14 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
       for (int r = 0; r < 4; ++r) dzc[r] = dhp[r] * (1.f - up[r]) * (1.f - cp[r] * cp[r]);
       bf16* const crow = a.dz + ((size_t)(t - 1) * B + b) * G3 + 2 * H + u0;
       if (a.ring0)
-        st4bf_sc1(a.ring0 + (size_t)((t - 1) & 1) * B * H + frag_index(b, u0, H), dzc[0], dzc[1],
+        st4bf_sc1(a.ring0 + (size_t)((t - 1) & 1) * Bp * H + frag_index(b, u0, H), dzc[0], dzc[1],
                   dzc[2], dzc[3]);
       else
         st4bf_sc1(crow, dzc[0], dzc[1], dzc[2], dzc[3]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0)
         wg_arrive(&wg_cnt[1], UB * NT, cntC + (size_t)(t - 1) * 4 + (u0 / (H / 4)));
-      if (a.ring0) st4bf(crow, dzc[0], dzc[1], dzc[2], dzc[3]);
+      if (a.ring0 && live) st4bf(crow, dzc[0], dzc[1], dzc[2], dzc[3]);
     }
   }
 }
@@ -456,18 +475,21 @@ static const void* gru_pick(int bwd, int H, int ub, int nt) {
   return nullptr;
 }
 
-static int gru_grid(int H, int B, int ub, int nt) { return (H / (16 * ub)) * (B / (16 * nt)); }
+static int gru_grid(int H, int B, int ub, int nt) {
+  return (H / (16 * ub)) * (gru_rows(B, nt) / (16 * nt));
+}
 
 // Launch plan: the first (NT, UB) -- fewest batch tiles per workgroup, then the larger unit block
 // (32 before 16 units) -- whose forward AND backward grids are co-resident with the GPU to
 // themselves.  Returns UB | NT << 4; 0 = not supported (per-step kernels instead).
 // DCR_DEBUG=gru_ub=1 forces 16-unit blocks, gru_nt=N forces N batch tiles per workgroup.
 int gru_persist_ub(int H, int B, int cus) {
-  if (H % 128 != 0 || H < 128 || H > 1024 || B % 16 != 0 || B < 16 || cus <= 0) return 0;
+  if (H % 128 != 0 || H < 128 || H > 1024 || B < 1 || cus <= 0) return 0;
   const int first = debug_int("gru_ub", 2) == 1 ? 1 : 2;
   const int force_nt = debug_int("gru_nt", 0);
   for (int nt = 1; nt <= 4; nt *= 2) {
-    if ((force_nt > 0 && nt != force_nt) || B % (16 * nt) != 0) continue;
+    // (a ragged batch pads to whole groups of nt tiles: prefer the smallest nt that fits)
+    if (force_nt > 0 && nt != force_nt) continue;
     for (int ub = first; ub >= 1; --ub) {
       if (ub * nt > 4) continue;  // one epilogue role per wave
       bool ok = true;
@@ -483,14 +505,27 @@ int gru_persist_ub(int H, int B, int cus) {
   return 0;
 }
 
+// a ragged batch's padded rows exist only in the fragment-tiled rings: the row-major hand-off
+// path (no rings) needs whole 16-row tiles
+static bool B_ragged_needs_rings(const GruPersistArgs& a) {
+  return a.B % 16 != 0 && (!a.ring0 || !a.ring1);
+}
+// padded rows of the batch under the launch plan (ring sizing)
+int gru_persist_rows(int H, int B, int cus) {
+  const int plan = gru_persist_ub(H, B, cus);
+  return plan ? gru_rows(B, plan >> 4) : 0;
+}
+
 int launch_gru_persist(int bwd, const GruPersistArgs& a, int cus, hipStream_t s) {
   const int plan = gru_persist_ub(a.H, a.B, cus);
   if (!plan) return -2;
   const int ub = plan & 15, nt = plan >> 4;
   const void* fn = gru_pick(bwd, a.H, ub, nt);
   if (!fn) return -1;
+  if (B_ragged_needs_rings(a)) return -2;
   if (!a.cnt_zeroed)
-    (void)hipMemsetAsync(a.cnt, 0, sizeof(unsigned) * 2 * (size_t)(a.B / 16) * (a.T + 1) * 4, s);
+    (void)hipMemsetAsync(a.cnt, 0,
+                         sizeof(unsigned) * 2 * (size_t)(gru_rows(a.B, nt) / (16 * nt)) * (a.T + 1) * 4, s);
   void* args[] = {const_cast<GruPersistArgs*>(&a)};
   return hipLaunchKernel(fn, dim3(gru_grid(a.H, a.B, ub, nt)), dim3(256), args, 0, s) == hipSuccess
              ? 0 : -3;

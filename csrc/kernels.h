@@ -290,6 +290,7 @@ bool wgrad_supported(int M, int N, int K);
 int wgrad_splits(int np, int M, int N, int K, int cus);
 void launch_wgrad(const WgradArgs& a, hipStream_t s);
 int gru_persist_ub(int H, int B, int cus);
+int gru_persist_rows(int H, int B, int cus);  // padded batch rows of the launch plan (rings)
 int launch_gru_persist(int bwd, const GruPersistArgs& a, int cus, hipStream_t s);
 
 // fused softmax head (head.hip)

@@ -52,9 +52,10 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
+  const int Bp = (B + 15) / 16 * 16;  // ring rows: a ragged batch pads to whole 16-row tiles
   const int nwg_u = H / (16 * UB);
   int ubk, bg;
-  map_block(blockIdx.x, nwg_u, B / 16, ubk, bg);
+  map_block(blockIdx.x, nwg_u, Bp / 16, ubk, bg);
   const int ub0 = ubk * 16 * UB, b0 = bg * 16;
   const int kq = 8 * (lane >> 4);
   const int kbase = w * (KS * 32);
@@ -85,6 +86,7 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
   }
 
   const int b = b0 + (lane & 15);
+  const bool live = b < B;  // padded rows: zero inputs, ring stores only
   const unsigned hoff = (unsigned)(((size_t)b * H + kbase + kq) * sizeof(bf16));
 
   // epilogue ownership: wave ui (< UB) owns unit block ui; lane: batch b, units u0..u0+3
@@ -92,7 +94,7 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
   const int u0 = ub0 + (epi ? w : 0) * 16 + 4 * (lane >> 4);
   const size_t bh = (size_t)b * H + u0;
   float c[4] = {0.f, 0.f, 0.f, 0.f};
-  if (epi) ld4f(a.cbuf + bh, c);
+  if (epi && live) ld4f(a.cbuf + bh, c);
   float bias[4][4];
   if constexpr (XF) {
     if (epi) {
@@ -104,7 +106,7 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
   for (int t = 0; t < T; ++t) {
     STAMP(0)
     // x-projection pre-activations of step t (independent of the recurrence: issue early)
-    float zx[4][4];
+    float zx[4][4] = {};
     f32x4 acc[UB][4];
 #pragma unroll
     for (int ui = 0; ui < UB; ++ui)
@@ -112,10 +114,10 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
       for (int g = 0; g < 4; ++g) acc[ui][g] = f32x4{0.f, 0.f, 0.f, 0.f};
     if constexpr (XF) {
       // input projection of step t: independent of the recurrence, runs before the wait
-      const bf16* xp = a.xin + ((size_t)t * B + b) * H + kbase + kq;
+      const bf16* xp = a.xin + ((size_t)t * B + (live ? b : 0)) * H + kbase + kq;
       bf16x8 xf[KS];
 #pragma unroll
-      for (int s = 0; s < KS; ++s) xf[s] = ld8(xp + s * 32);
+      for (int s = 0; s < KS; ++s) xf[s] = live ? ld8(xp + s * 32) : zero8();
 #pragma unroll
       for (int ui = 0; ui < UB; ++ui)
 #pragma unroll
@@ -128,7 +130,7 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
 #pragma unroll
           for (int r = 0; r < 4; ++r) zx[g][r] = bias[g][r];
       }
-    } else if (epi) {
+    } else if (epi && live) {
       const float* zrow = a.ids ? a.zx + (size_t)a.ids[(size_t)t * B + b] * a.zx_ld
                                 : a.zx + ((size_t)t * B + b) * a.zx_ld;
 #pragma unroll
@@ -145,7 +147,7 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
     // h_{t-1} fragments (handed off by other workgroups: sc1 loads only)
     const bool fring = t > 0;  // slot 0 (initial state) is row-major
     const __amdgpu_buffer_rsrc_t hsrc =
-        fring ? make_rsrc(a.hring + (size_t)(t & 1) * B * H, sizeof(bf16) * (size_t)B * H)
+        fring ? make_rsrc(a.hring + (size_t)(t & 1) * Bp * H, sizeof(bf16) * (size_t)Bp * H)
               : make_rsrc(a.hbuf + (size_t)t * B * H, sizeof(bf16) * (size_t)B * H);
     bf16x8 hf[KS];
 #pragma unroll
@@ -193,7 +195,7 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
       const size_t o = (size_t)(t + 1) * B * H + bh;
       STAMP(5)
       // handed off in fragment order (write-through); row-major copy below
-      st4bf_sc1(a.hring + (size_t)((t + 1) & 1) * B * H + frag_index(b, u0, H), h[0], h[1], h[2],
+      st4bf_sc1(a.hring + (size_t)((t + 1) & 1) * Bp * H + frag_index(b, u0, H), h[0], h[1], h[2],
                 h[3]);
       if (t + 1 < T) {
         // each epilogue wave publishes its own 16-unit slab: drain ONLY the hand-off store
@@ -205,6 +207,7 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_kernel(PersistArgs a)
           __hip_atomic_fetch_add(cnt + (size_t)(t + 1) * 4, 1u, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
       }
+      if (!live) continue;  // (after the hand-off: padded rows exist only in the ring)
       st4bf(a.hbuf + o, h[0], h[1], h[2], h[3]);
       *reinterpret_cast<float4*>(a.cbuf + o) = make_float4(c[0], c[1], c[2], c[3]);
       if (a.gates) {
@@ -237,9 +240,10 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
+  const int Bp = (B + 15) / 16 * 16;  // ring rows (padded batch)
   const int nwg_u = H / (16 * UB);
   int ubk, bg;
-  map_block(blockIdx.x, nwg_u, B / 16, ubk, bg);
+  map_block(blockIdx.x, nwg_u, Bp / 16, ubk, bg);
   const int ub0 = ubk * 16 * UB, b0 = bg * 16;
   const int kq = 8 * (lane >> 4);
   unsigned* cnt = a.cnt + (size_t)bg * (T + 1) * 4;
@@ -258,6 +262,7 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
       wf[ui][s] = ld8(a.W + (size_t)(ub0 + ui * 16 + (lane & 15)) * G4H + kcol(s) + kq);
 
   const int b = b0 + (lane & 15);
+  const bool live = b < B;  // padded rows: zero operands and gradients, ring stores only
 
   const bool epi = w < UB;
   const int u0 = ub0 + (epi ? w : 0) * 16 + 4 * (lane >> 4);
@@ -282,9 +287,9 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
   for (int t = T - 1; t >= 0; --t) {
     STAMP(0)
     // recurrence-independent epilogue operands, issued before the wait
-    float gi[4], gj[4], gf[4], go[4], cc[4], cp[4], dtop[4];
+    float gi[4] = {}, gj[4] = {}, gf[4] = {}, go[4] = {}, cc[4] = {}, cp[4] = {}, dtop[4] = {};
     int tok = 0;  // fused dEW row (issued with the other recurrence-independent operands)
-    if (epi) {
+    if (epi && live) {
       if (fuse_dew) tok = a.ids[(size_t)t * B + b];
       const bf16* gp = a.gates + ((size_t)t * B + b) * G4H + u0;
       ld4bf(gp, gi); ld4bf(gp + H, gj); ld4bf(gp + 2 * H, gf); ld4bf(gp + 3 * H, go);
@@ -305,7 +310,7 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
       // fragment-tiled ring: one contiguous 1 KB load per k-step
       bf16x8 df[KS];
       const __amdgpu_buffer_rsrc_t zsrc =
-          make_rsrc(a.zring + (size_t)((t + 1) & 1) * B * G4H, sizeof(bf16) * (size_t)B * G4H);
+          make_rsrc(a.zring + (size_t)((t + 1) & 1) * Bp * G4H, sizeof(bf16) * (size_t)Bp * G4H);
 #pragma unroll
       for (int s = 0; s < KS; ++s) df[s] = ld8_sc1(zsrc, frag_load_off(bg, kcol(s) >> 5, G4H, lane));
       if constexpr (EXCL) __builtin_amdgcn_sched_barrier(0);
@@ -349,7 +354,7 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
       STAMP(5)
       bf16* dz = a.dz + ((size_t)t * B + b) * G4H + u0;
       // handed-off copy in fragment order; row-major dz after the arrival
-      bf16* const zr = a.zring + (size_t)(t & 1) * B * G4H;
+      bf16* const zr = a.zring + (size_t)(t & 1) * Bp * G4H;
       st4bf_sc1(zr + frag_index(b, u0, G4H), di[0], di[1], di[2], di[3]);
       st4bf_sc1(zr + frag_index(b, H + u0, G4H), dj[0], dj[1], dj[2], dj[3]);
       st4bf_sc1(zr + frag_index(b, 2 * H + u0, G4H), df_[0], df_[1], df_[2], df_[3]);
@@ -361,6 +366,7 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_kernel(PersistArgs a)
           __hip_atomic_fetch_add(cnt + (size_t)t * 4, 1u, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
       }
+      if (!live) continue;  // (padded rows: zero gradients, nothing row-major)
       st4bf(dz, di[0], di[1], di[2], di[3]);
       st4bf(dz + H, dj[0], dj[1], dj[2], dj[3]);
       st4bf(dz + 2 * H, df_[0], df_[1], df_[2], df_[3]);
@@ -474,12 +480,12 @@ static size_t dyn_lds(int bwd, int H, int B, int V, int cus) {
 int lstm_persist_supported(int H, int B, int cus) {
   // shape support only; whether a grid can be co-resident is lstm_persist_occupancy's job
   (void)cus;
-  if (H % 128 != 0 || B % 16 != 0 || H > 1024 || H < 128) return 0;
+  if (H % 128 != 0 || B < 1 || H > 1024 || H < 128) return 0;
   return (H / 16) % ub_for(H, B, cus) == 0 ? 1 : 0;
 }
 
 int lstm_persist_grid(int H, int B, int cus) {
-  return (H / (16 * ub_for(H, B, cus))) * (B / 16);
+  return (H / (16 * ub_for(H, B, cus))) * ((B + 15) / 16);
 }
 
 int lstm_persist_occupancy(int bwd, int H, int B, int V, int flags, int cus) {
@@ -512,7 +518,7 @@ static int launch_persist(int bwd, const PersistArgs& a, int flags, int cus, hip
       grid > occ * cus)
     return -2;
   if (!a.cnt_zeroed)
-    (void)hipMemsetAsync(a.cnt, 0, sizeof(unsigned) * (size_t)(a.B / 16) * (a.T + 1) * 4, s);
+    (void)hipMemsetAsync(a.cnt, 0, sizeof(unsigned) * (size_t)((a.B + 15) / 16) * (a.T + 1) * 4, s);
   void* args[] = {const_cast<PersistArgs*>(&a)};
   return hipLaunchKernel(fn, dim3(grid), dim3(256), args, lds, s) == hipSuccess ? 0 : -3;
 }

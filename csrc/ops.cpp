@@ -510,7 +510,7 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
     TORCH_CHECK(zx.numel() == (int64_t)T * B * 4 * H, "zx must be [T, B, 4H]");
   }
   if (has(gates)) TORCH_CHECK(gates->numel() == (int64_t)T * B * 4 * H, "gates must be [T, B, 4H]");
-  TORCH_CHECK(cnt.numel() >= (int64_t)(B / 16) * (T + 1) * 4, "counter buffer too small");
+  TORCH_CHECK(cnt.numel() >= (int64_t)((B + 15) / 16) * (T + 1) * 4, "counter buffer too small");
   dcr::PersistArgs a{};
   a.W = ptr<bf16>(WT);
   a.zx = ptr<float>(zx);
@@ -541,7 +541,7 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
     a.clast32 = ptr<float>(*clast32);
   }
   check_seq(hring, at::kBFloat16, "hring");
-  TORCH_CHECK(hring.numel() >= (int64_t)2 * B * H, "hring must hold [2, B, H]");
+  TORCH_CHECK(hring.numel() >= (int64_t)2 * ((B + 15) / 16 * 16) * H, "hring must hold [2, ceil16(B), H]");
   a.hring = ptr<bf16>(hring);
   const int rc = dcr::launch_lstm_fwd_persist(a, num_cus(), cur_stream());
   TORCH_CHECK(rc == 0, "persistent LSTM forward not launched (", rc,
@@ -564,7 +564,7 @@ void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& d
   TORCH_CHECK(W.size(0) == H && W.size(1) == 4 * H, "W must be [H, 4H]");
   TORCH_CHECK(dz.numel() == (int64_t)T * B * 4 * H && gates.numel() == (int64_t)T * B * 4 * H, "dz/gates shape");
   TORCH_CHECK(cbuf.numel() == (int64_t)(T + 1) * B * H, "cbuf shape");
-  TORCH_CHECK(cnt.numel() >= (int64_t)(B / 16) * (T + 1) * 4, "counter buffer too small");
+  TORCH_CHECK(cnt.numel() >= (int64_t)((B + 15) / 16) * (T + 1) * 4, "counter buffer too small");
   dcr::PersistArgs a{};
   a.W = ptr<bf16>(W);
   a.dtop = ptr<float>(dtop);
@@ -578,12 +578,14 @@ void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& d
   check_opt(db_part, at::kFloat, "db_part");
   check_opt(dew_part, at::kFloat, "dew_part");
   check_opt(ids, at::kInt, "ids");
-  if (has(db_part)) TORCH_CHECK(db_part->numel() == (int64_t)(B / 16) * 4 * H, "db_part must be [B/16, 4H]");
+  if (has(db_part))
+    TORCH_CHECK(db_part->numel() == (int64_t)((B + 15) / 16) * 4 * H, "db_part must be [ceil(B/16), 4H]");
   a.db_part = optr<float>(db_part);
   if (has(dew_part)) {
     TORCH_CHECK(has(ids) && ids->numel() == (int64_t)T * B, "dew_part needs ids [T, B]");
     TORCH_CHECK(V >= 1 && V <= 128, "fused dEW supports V <= 128");
-    TORCH_CHECK(dew_part->numel() == (int64_t)(B / 16) * V * 4 * H, "dew_part must be [B/16, V, 4H]");
+    TORCH_CHECK(dew_part->numel() == (int64_t)((B + 15) / 16) * V * 4 * H,
+                "dew_part must be [ceil(B/16), V, 4H]");
     a.dew_part = optr<float>(dew_part);
     a.ids = optr<int>(ids);
     a.V = (int)V;
@@ -595,7 +597,8 @@ void lstm_persist_bwd(const at::Tensor& W, const at::Tensor& dtop, at::Tensor& d
   a.excl = exclusive ? 1 : 0;
   a.cnt_zeroed = cnt_zeroed ? 1 : 0;
   check_seq(zring, at::kBFloat16, "zring");
-  TORCH_CHECK(zring.numel() >= (int64_t)2 * B * 4 * H, "zring must hold [2, B, 4H]");
+  TORCH_CHECK(zring.numel() >= (int64_t)2 * ((B + 15) / 16 * 16) * 4 * H,
+              "zring must hold [2, ceil16(B), 4H]");
   a.zring = ptr<bf16>(zring);
   const int rc = dcr::launch_lstm_bwd_persist(a, num_cus(), cur_stream());
   TORCH_CHECK(rc == 0, "persistent LSTM BPTT not launched (", rc,
@@ -912,8 +915,9 @@ static void gru_common(dcr::GruPersistArgs& a, const at::Tensor& gates, const at
   if (has(ring0)) {
     check_seq(*ring0, at::kBFloat16, "ring0");
     check_seq(*ring1, at::kBFloat16, "ring1");
-    TORCH_CHECK(ring0->numel() >= (int64_t)2 * B * H && ring1->numel() >= 2 * B * w1,
-                "hand-off rings too small");
+    const int64_t Bp = dcr::gru_persist_rows(H, B, num_cus());  // padded batch rows
+    TORCH_CHECK(ring0->numel() >= (int64_t)2 * Bp * H && ring1->numel() >= 2 * Bp * w1,
+                "hand-off rings too small (", 2 * Bp, " padded rows)");
     a.ring0 = ptr<bf16>(*ring0);
     a.ring1 = ptr<bf16>(*ring1);
   }
@@ -923,7 +927,8 @@ static void gru_common(dcr::GruPersistArgs& a, const at::Tensor& gates, const at
   TORCH_CHECK(h32.numel() == (int64_t)(T + 1) * B * H, "h32 must be [T+1, B, H]");
   TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == at::kInt && err.scalar_type() == at::kInt,
               "cnt/err must be int32 GPU tensors");
-  TORCH_CHECK(cnt.numel() >= (int64_t)2 * (B / 16) * (T + 1) * 4, "counter buffer too small");
+  TORCH_CHECK(cnt.numel() >= (int64_t)2 * ((B + 15) / 16) * (T + 1) * 4, "counter buffer too small");
+  TORCH_CHECK(B % 16 == 0 || has(ring0), "a ragged batch (B % 16 != 0) needs the hand-off rings");
   TORCH_CHECK(dcr::gru_persist_ub(H, B, num_cus()) > 0, "persistent GRU unsupported for H=", H,
               " B=", B, " (grid cannot be co-resident)");
   a.gates = ptr<bf16>(gates);

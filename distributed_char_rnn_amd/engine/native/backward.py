@@ -129,7 +129,7 @@ class BackwardMixin:
             elif P.persist:
                 self.ops.lstm_persist_bwd(lw.Wh, dtop, lb.dz, lb.gates, lb.cbuf,
                                           bufs["cnt"][self.L + layer], self.err, self.spin_limit,
-                                          bufs["zring"], bufs["db_part"][layer][: max(B // 16, 1)],
+                                          bufs["zring"], bufs["db_part"][layer][: -(-B // 16)],
                                           ids_tm if fused_dew else None,
                                           bufs["dew_part"] if fused_dew else None, V,
                                           exclusive=P.bwd_excl, cnt_zeroed=True)

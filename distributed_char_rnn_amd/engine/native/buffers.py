@@ -41,8 +41,10 @@ class BuffersMixin:
         H, GW, dev, m = self.H, self.GW, self.dev, self.cfg.model
         N = B * T
         plan = self._persist_plan(B, training, T)
-        Bp = max(B, 32 * plan.pair_nbg)  # hand-off rings of the pair kernels: padded batch
-        nrow = max(B // 16, plan.pair_rows, 1)
+        # hand-off rings: the batch padded to whole 32-row groups (pair kernels) / 16-row tiles
+        Bp = max(-(-B // 32) * 32, 32 * plan.pair_nbg)
+        Bg = -(-B // 64) * 64  # GRU rings: whole groups of up to 4 16-row tiles
+        nrow = max(-(-B // 16), plan.pair_rows, 1)
         drop = self._dropout(training)
         layers = []
         for layer in range(self.L):
@@ -94,14 +96,16 @@ class BuffersMixin:
             dx=e(T, B, H) if training else None,
             dx_bf=e(N, H, dt=bf16) if training else None,
             db_part=e(self.L, nrow, GW) if training else None,
-            dew_part=(e(max(B // 16, 1), self.V, GW)
+            dew_part=(e(-(-B // 16), self.V, GW)
                       if (training and self.V <= 128 and self.dew_mode == "fused") else None),
             # one hand-off counter region per persistent launch (fwd layers, then bwd layers),
             # zeroed together by the step's prep launch
             cnt=torch.zeros(2 * self.L, max(2 * (B // 16 + 1), plan.pair_nbg) * (T + 1) * 4,
                             dtype=torch.int32, device=dev),
-            # fragment-tiled hand-off rings of the persistent GRU: [h or dZc, r⊙h, dZg]
-            grings=((e(2 * B * H, dt=bf16), e(2 * B * H, dt=bf16), e(2 * B * 2 * H, dt=bf16))
+            # fragment-tiled hand-off rings of the persistent GRU: [h or dZc, r⊙h, dZg], sized
+            # for the batch padded to whole 64-row groups (a ragged batch's padded rows live
+            # only in the rings)
+            grings=((e(2 * Bg * H, dt=bf16), e(2 * Bg * H, dt=bf16), e(2 * Bg * 2 * H, dt=bf16))
                     if m == "gru" else None),
             # fragment-tiled h hand-off rings of the persistent forwards (persist_common.h)
             hrings=(e(2 * Bp * H, dt=bf16), e(2 * Bp * H, dt=bf16)) if m == "lstm" else None,
@@ -135,7 +139,7 @@ class BuffersMixin:
         P = bufs["plan"]
         if P.pair_bwd and layer < 2 * (len(bufs["layers"]) // 2):
             return bufs["db_part"][layer][: P.pair_rows]
-        return bufs["db_part"][layer][: max(bufs["layers"][0].hbuf.shape[1] // 16, 1)]
+        return bufs["db_part"][layer][: -(-bufs["layers"][0].hbuf.shape[1] // 16)]
 
     def _bias_sum(self, part: torch.Tensor, names, q=None) -> torch.Tensor:
         """Sum the per-batch-group bias partials; for cells with one [GW] bias the sum is
