@@ -173,6 +173,31 @@ int launch_lstm_bwd_persist(const PersistArgs& a, int cus, hipStream_t s);
 // wide-vocabulary softmax CE (xent.hip): bias added in-kernel, fused d softmax_b, V % 4 == 0,
 // V <= 8192
 int xent_wide_waves(int N);
+// loss = sum(partial[0:nb]) / N; db = column sums of colpart [ncp, V] (when both given)
+void launch_xent_finalize(const float* partial, int nb, int N, float* loss_out,
+                          const float* colpart, int ncp, int V, float* db, hipStream_t s);
+
+// fused wide-vocabulary head (head_wide.hip): logits -> lse -> loss, bf16 dlogits, d softmax_b
+// partials, without writing fp32 logits
+struct HeadWideArgs {
+  const bf16* O; int ldo;      // [N, H] top-layer outputs (bf16, row stride ldo)
+  const bf16* WsT;             // [V, H] softmax_wᵀ (bf16)
+  const float* bias;           // [V] softmax_b (or nullptr)
+  const int* targets;          // [N] (or nullptr: no loss)
+  int N, V, H;
+  float grad_scale;            // 1 / N
+  float* row_loss;             // [N] (optional)
+  bf16* dlogits;               // [N, V] (optional: training)
+  float* logits;               // [N, V] fp32 (optional: summaries / eval)
+  float* colpart;              // [head_wide_colpart_rows(N), V] d softmax_b partials (optional)
+  float* partial;              // [head_wide_blocks(N)] loss partials
+  float* stats;                // [head_wide_stats_floats(N)] per-half softmax stats (8-B aligned)
+};
+int head_wide_blocks(int N);
+int head_wide_colpart_rows(int N);
+size_t head_wide_stats_floats(int N);
+int head_wide_supported(int V, int H);
+int launch_head_wide(const HeadWideArgs& a, float* db, float* loss_out, hipStream_t s);
 int xent_wide_blocks(int N);
 int xent_wide_supported(int V);
 void launch_xent_wide(const float* logits, const float* bias, const int* targets, int N, int V,

@@ -429,6 +429,50 @@ void xent_wide(const at::Tensor& logits, const c10::optional<at::Tensor>& bias,
                         optr<float>(db), ptr<float>(partial), ptr<float>(loss_out), cur_stream());
 }
 
+// fused wide-vocabulary head (head_wide.hip); colpart [head_wide_colpart_rows(N), V]; workspace ws
+// [head_wide_workspace(N)] = loss partials + the two passes' softmax stats
+void head_wide(const at::Tensor& O, const at::Tensor& WsT, const c10::optional<at::Tensor>& bias,
+               const c10::optional<at::Tensor>& targets, double grad_scale,
+               const c10::optional<at::Tensor>& row_loss, const c10::optional<at::Tensor>& dlogits,
+               const c10::optional<at::Tensor>& logits, const c10::optional<at::Tensor>& colpart,
+               const c10::optional<at::Tensor>& db, at::Tensor& ws, at::Tensor& loss_out) {
+  TORCH_CHECK(O.is_cuda() && O.dim() == 2 && O.scalar_type() == at::kBFloat16 && O.stride(1) == 1,
+              "O must be a row-major bf16 [N, H] GPU tensor");
+  check_seq(WsT, at::kBFloat16, "WsT");
+  const int N = (int)O.size(0), H = (int)O.size(1), V = (int)WsT.size(0);
+  TORCH_CHECK(WsT.dim() == 2 && WsT.size(1) == H, "WsT must be [V, H]");
+  TORCH_CHECK(dcr::head_wide_supported(V, H), "fused wide head: H = 512, V % 64 == 0");
+  check_opt(bias, at::kFloat, "bias");
+  check_opt(targets, at::kInt, "targets");
+  check_opt(row_loss, at::kFloat, "row_loss");
+  check_opt(dlogits, at::kBFloat16, "dlogits");
+  check_opt(logits, at::kFloat, "logits");
+  check_opt(colpart, at::kFloat, "colpart");
+  check_opt(db, at::kFloat, "db");
+  check_seq(ws, at::kFloat, "ws");
+  if (has(bias)) TORCH_CHECK(bias->numel() == V, "bias must be [V]");
+  if (has(targets)) TORCH_CHECK(targets->numel() == N, "targets must be [N]");
+  if (has(row_loss)) TORCH_CHECK(row_loss->numel() == N, "row_loss must be [N]");
+  if (has(dlogits)) TORCH_CHECK(dlogits->numel() == (int64_t)N * V, "dlogits must be [N, V]");
+  if (has(logits)) TORCH_CHECK(logits->numel() == (int64_t)N * V, "logits must be [N, V]");
+  const int nb = dcr::head_wide_blocks(N);
+  if (has(colpart))
+    TORCH_CHECK(colpart->numel() >= (int64_t)dcr::head_wide_colpart_rows(N) * V, "colpart too small");
+  if (has(db)) TORCH_CHECK(has(colpart) && has(dlogits) && db->numel() == V, "db needs colpart, dlogits, [V]");
+  const int64_t soff = (nb + 3) / 4 * 4;  // stats 16-B aligned behind the partials
+  TORCH_CHECK(ws.numel() >= soff + (int64_t)dcr::head_wide_stats_floats(N), "ws too small");
+  dcr::HeadWideArgs a{};
+  a.O = ptr<bf16>(O); a.ldo = (int)O.stride(0);
+  a.WsT = ptr<bf16>(WsT); a.bias = optr<float>(bias); a.targets = optr<int>(targets);
+  a.N = N; a.V = V; a.H = H; a.grad_scale = (float)grad_scale;
+  a.row_loss = optr<float>(row_loss); a.dlogits = optr<bf16>(dlogits);
+  a.logits = optr<float>(logits); a.colpart = optr<float>(colpart);
+  a.partial = ptr<float>(ws);
+  a.stats = ptr<float>(ws) + soff;
+  TORCH_CHECK(dcr::launch_head_wide(a, optr<float>(db), ptr<float>(loss_out), cur_stream()) == 0,
+              "fused wide head not launched");
+}
+
 void segsum(const at::Tensor& X, const c10::optional<at::Tensor>& ids, int64_t V, at::Tensor& out,
             at::Tensor& workspace, bool accumulate, const c10::optional<at::Tensor>& perm) {
   TORCH_CHECK(X.is_cuda() && X.dim() == 2 && X.stride(1) == 1, "X must be a row-major 2-D GPU tensor");
@@ -1243,6 +1287,20 @@ TORCH_LIBRARY(dcr, m) {
       "xent_wide(Tensor logits, Tensor? bias, Tensor targets, float grad_scale, Tensor(a!)? row_loss, "
       "Tensor(b!)? dlogits, Tensor(c!)? colpart, Tensor(d!)? db, Tensor(e!) partial, "
       "Tensor(f!) loss_out) -> ()");
+  m.def(
+      "head_wide(Tensor O, Tensor WsT, Tensor? bias, Tensor? targets, float grad_scale, "
+      "Tensor(a!)? row_loss, Tensor(b!)? dlogits, Tensor(c!)? logits, Tensor(d!)? colpart, "
+      "Tensor(e!)? db, Tensor(f!) ws, Tensor(g!) loss_out) -> ()");
+  m.def("head_wide_supported(int V, int H) -> int", [](int64_t V, int64_t H) -> int64_t {
+    return dcr::head_wide_supported((int)V, (int)H);
+  });
+  m.def("head_wide_blocks(int N) -> int",
+        [](int64_t N) -> int64_t { return dcr::head_wide_blocks((int)N); });
+  m.def("head_wide_colpart_rows(int N) -> int",
+        [](int64_t N) -> int64_t { return dcr::head_wide_colpart_rows((int)N); });
+  m.def("head_wide_workspace(int N) -> int", [](int64_t N) -> int64_t {
+    return (dcr::head_wide_blocks((int)N) + 3) / 4 * 4 + (int64_t)dcr::head_wide_stats_floats((int)N);
+  });
   m.def("xent_wide_supported(int V) -> int",
         [](int64_t V) -> int64_t { return dcr::xent_wide_supported((int)V); });
   m.def("xent_wide_waves(int n) -> int",
@@ -1354,6 +1412,7 @@ TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("sumsq", &sumsq);
   m.impl("lstm_step_ew_fwd", &lstm_step_ew_fwd);
   m.impl("lstm_step_ew_bwd", &lstm_step_ew_bwd);
+  m.impl("head_wide", &head_wide);
   m.impl("adam_clip", &adam_clip);
   m.impl("rnn_fwd_seq", &rnn_fwd_seq);
   m.impl("rnn_bwd_seq", &rnn_bwd_seq);

@@ -231,6 +231,12 @@ __global__ void __launch_bounds__(256) xent_colsum_kernel(const float* __restric
   }
 }
 
+void launch_xent_finalize(const float* partial, int nb, int N, float* loss_out,
+                          const float* colpart, int ncp, int V, float* db, hipStream_t s) {
+  sum_partials_kernel<<<1, kXentThreads, 0, s>>>(partial, nb, 1.0f / (float)N, loss_out);
+  if (colpart && db) xent_colsum_kernel<<<(V / 4 + 3) / 4, 256, 0, s>>>(colpart, ncp, V, db);
+}
+
 int xent_wide_blocks(int N) { return (N + kWideRPB - 1) / kWideRPB; }
 int xent_wide_waves(int N) { return xent_wide_blocks(N); }  // partial rows: one per block
 int xent_wide_supported(int V) { return V % 4 == 0 && V <= 256 * 4 * 16 ? 1 : 0; }

@@ -64,6 +64,10 @@ class NativeBackend(LayoutsMixin, BuffersMixin, ForwardMixin, BackwardMixin, Lib
         # fused softmax head (csrc/head.hip): logits + CE + dlogits + d softmax_b + dtop
         self.fused_head = self.knobs.on("fused_head") and bool(self.ops.head_supported(self.V,
                                                                                           self.H))
+        # fused wide-vocabulary head (csrc/head_wide.hip): logits + CE + bf16 dlogits + d softmax_b
+        # without the fp32 logits round trip, for the vocabularies the narrow head does not cover
+        self.wide_head = (not self.fused_head and self.knobs.on("wide_head")
+                          and bool(self.ops.head_wide_supported(self.V, self.H)))
         # TF clip-norm semantics for the embedding gradient (models/params.py: clip_norm)
         self.tf_norm = self.cfg.clip_norm == "tf"
         self._wver = None

@@ -21,7 +21,8 @@ class BackwardMixin:
         ids_tm, tgt = bufs0["ids_tm"], bufs0["tgt_tm"].view(-1)
         id_tasks = self._id_tasks(x, y, bufs0)
         bufs, O, logits, new_state = self._forward(ids_tm, state, True,
-                                                   want_logits=not self.fused_head,
+                                                   want_logits=not (self.fused_head
+                                                                    or self.wide_head),
                                                    logits_bias=not wide, extra_tasks=id_tasks)
         # deferred slab / bias sums of this step: one prep launch per flush (gemm.SumQueue)
         q = SumQueue(self.ops, wgrad=self.knobs.debug.get("wgrad") == "1")
@@ -52,6 +53,14 @@ class BackwardMixin:
                           dm["sout"] if dm is not None else 1.0)
             mm_tn(O, dlog, s.gview("rnnlm/softmax_w"), q=q)
             dtop = bufs["dtop"].view(T, B, H)
+        elif self.wide_head:
+            # wide vocabulary, one launch: logits (recomputed, never written unless asked for)
+            # -> CE -> bf16 dlogits + d softmax_b partials (csrc/head_wide.hip)
+            self.ops.head_wide(O, hd["WsTw"], hd["bs"], tgt, 1.0 / N, bufs["row_loss"], dlog,
+                               logits if want_extras else None, bufs["hw_colpart"],
+                               s.gview("rnnlm/softmax_b"), bufs["hw_part"], loss_buf)
+            mm_tn(O, dlog, s.gview("rnnlm/softmax_w"), q=q)
+            dtop = mm_into(dlog, hd["Ws"].t(), bufs["dtop"].view(N, H)).view(T, B, H)
         elif wide:
             # wide vocabulary: one-read CE (bias added in-kernel), d softmax_b fused (xent_wide)
             self.ops.xent_wide(logits, hd["bs"], tgt, 1.0 / N, bufs["row_loss"], dlog,

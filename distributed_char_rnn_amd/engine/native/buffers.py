@@ -82,6 +82,10 @@ class BuffersMixin:
             ws=e(ws),
             colsum=e(1, max(GW, self.V)),
             head_part=e(self.ops.head_workspace(N, self.V)) if self.fused_head else None,
+            # fused wide head: per-workgroup loss partials and d softmax_b column partials
+            hw_part=e(self.ops.head_wide_workspace(N)) if self.wide_head else None,
+            hw_colpart=(e(self.ops.head_wide_colpart_rows(N) * self.V)
+                        if (training and self.wide_head) else None),
             onehot=(e(N, 8 * ((self.V + 7) // 8), dt=bf16)
                     if (training and self.V <= SEG_LDS_MAX_V and self.dew_mode == "gemm")
                     else None),
@@ -124,8 +128,8 @@ class BuffersMixin:
 
     def _wide_xent(self, N: int) -> bool:
         """Library logits GEMM + one-read CE kernel (xent_wide) for vocabularies the fused head
-        does not cover (V > 256)."""
-        return (not self.fused_head and self.V >= 256 and self.knobs.on("wide_xent")
+        does not cover (V > 256) when the fused wide head does not either."""
+        return (not self.fused_head and not self.wide_head and self.V >= 256 and self.knobs.on("wide_xent")
                 and bool(self.ops.xent_wide_supported(self.V)))
 
     def _side_stream(self):

@@ -19,8 +19,12 @@ class InferenceMixin:
         ids_tm = x.t().contiguous()
         tgt = y.t().contiguous().view(-1)
         bufs, O, logits, new_state = self._forward(ids_tm, state, False,
-                                                   want_logits=not self.fused_head)
-        if self.fused_head:
+                                                   want_logits=not (self.fused_head
+                                                                    or self.wide_head))
+        if self.wide_head:
+            self.ops.head_wide(O, self._head["WsTw"], self._head["bs"], tgt, 1.0, None, None,
+                               None, None, None, bufs["hw_part"], bufs["loss"][0, :1])
+        elif self.fused_head:
             hd = self._head
             self.ops.head(O, hd["WsT"], None, hd["bs"], tgt, 1.0, None, None, None, None, None,
                           bufs["head_part"], bufs["loss"][0, :1])

@@ -79,6 +79,10 @@ class LayoutsMixin:
             T += [(Ws32, self._head["WsT"][: self.V], 1),
                   (Ws32, self._head["Wsk"][:, : self.V], 0)]
 
+        if self.wide_head:
+            self._head["WsTw"] = e(self.V, H)   # softmax_wᵀ [V, H] (head_wide.hip)
+            T.append((Ws32, self._head["WsTw"], 1))
+
     def _prep(self) -> list:
         """Prep-kernel tasks that refresh the weight layouts after a parameter change (empty
         when the weights are current).  The layer-0 ``E·W_x + b`` table: for LSTM / RNN with a

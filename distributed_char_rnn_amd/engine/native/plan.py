@@ -43,6 +43,7 @@ DEBUG_KEYS = {
     "xfuse": "0: no fused input projection in the single-layer persistent forward",
     "exclusive": "0: never pick the one-workgroup-per-CU single-layer BPTT variant",
     "wide_xent": "0: no one-read CE kernel for wide vocabularies",
+    "wide_head": "0: library logits GEMM + one-read CE instead of the fused wide-vocabulary head",
     "seg_sort": "0: unsorted atomic embedding gradient for wide vocabularies",
     "lib_graph": "0: eager library-step loops (no hipGraph replay)",
     "sample_graph": "0: eager sampling loop (no hipGraph replay)",

@@ -1,0 +1,89 @@
+"""Fused wide-vocabulary head (csrc/head_wide.hip) against the fp32 PyTorch oracle: logits ->
+sequence loss (model.py:76-85) -> bf16 dlogits and d softmax_b in one launch, and the training
+step that uses it at the 8k-token config's vocabulary (V = 8192) against the reference backend."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+@pytest.mark.parametrize("N,V", [(1000, 8192), (129, 256), (4100, 1024), (64, 64)])
+def test_head_wide_matches_torch(N, V, dcr_ops):
+    H = 512
+    assert dcr_ops.head_wide_supported(V, H)
+    g = torch.Generator(device="cuda").manual_seed(N + V)
+    O = (torch.randn(N, H, device="cuda", generator=g) * 0.5).bfloat16()
+    Ws = (torch.randn(H, V, device="cuda", generator=g) * 0.1)
+    WsT = Ws.t().contiguous().bfloat16()
+    bias = torch.randn(V, device="cuda", generator=g)
+    y = torch.randint(0, V, (N,), device="cuda", dtype=torch.int32, generator=g)
+    nb = dcr_ops.head_wide_blocks(N)
+    rl = torch.empty(N, device="cuda")
+    dl = torch.empty(N, V, dtype=torch.bfloat16, device="cuda")
+    lg = torch.empty(N, V, device="cuda")
+    colpart = torch.empty(dcr_ops.head_wide_colpart_rows(N) * V, device="cuda")
+    db = torch.empty(V, device="cuda")
+    part = torch.empty(dcr_ops.head_wide_workspace(N), device="cuda")
+    loss = torch.empty(1, device="cuda")
+    dcr_ops.head_wide(O, WsT, bias, y, 1.0 / N, rl, dl, lg, colpart, db, part, loss)
+    torch.cuda.synchronize()
+    lt = (O.float() @ WsT.float().t() + bias).requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(lt, y.long(), reduction="none")
+    ref.mean().backward()
+    assert rel(lg, lt.detach()) < 1e-5
+    torch.testing.assert_close(rl, ref.detach(), rtol=1e-4, atol=1e-3)
+    assert abs(loss.item() - ref.mean().item()) < 1e-4 * max(1.0, ref.mean().item())
+    assert rel(dl.float(), lt.grad) < 1e-2
+    assert rel(db, dl.float().sum(0)) < 1e-5   # exactly the bf16 dlogits the GEMMs see
+    # eval form: loss only, nothing else written
+    loss2 = torch.empty(1, device="cuda")
+    dcr_ops.head_wide(O, WsT, bias, y, 1.0, None, None, None, None, None, part, loss2)
+    assert abs(loss2.item() - loss.item()) < 1e-5 * max(1.0, loss.item())
+
+
+def test_model_wide_head_matches_reference_v8192():
+    """The 8k-token config's head shape (V = 8192, H = 512) through the training step: loss and
+    every gradient against the fp32 autograd oracle, and against the library-logits route."""
+    import os
+
+    from distributed_char_rnn_amd.models.char_rnn import CharRNN
+    from distributed_char_rnn_amd.models.params import ModelConfig
+    from distributed_char_rnn_amd.models.reference import ReferenceBackend
+
+    B, T, H, V = 32, 10, 512, 8192
+    cfg = ModelConfig(model="lstm", vocab_size=V, rnn_size=H, num_layers=2)
+    nat = CharRNN(cfg, device="cuda", seed=4)
+    assert nat.backend.wide_head and not nat.backend.fused_head
+    ref = ReferenceBackend(nat.store)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.randint(0, V, (B, T), device="cuda", dtype=torch.int32, generator=g)
+    y = torch.randint(0, V, (B, T), device="cuda", dtype=torch.int32, generator=g)
+    loss_r, _, _ = ref.train_step(x, y, nat.zero_state(B))
+    g_ref = nat.store.grad.clone()
+    nat.store.grad.zero_()
+    loss_n, _, ex = nat.backend.train_step(x, y, nat.zero_state(B), want_extras=True)
+    torch.cuda.synchronize()
+    assert abs(loss_n.item() - loss_r.item()) < 1e-2 * max(1.0, abs(loss_r.item()))
+    for sp in nat.store.specs:
+        e = rel(nat.store.gview(sp.name), nat.store.view(sp.name, g_ref))
+        assert e < 6e-2, (sp.name, e)
+    g_wide = nat.store.grad.clone()
+    ev = nat.backend.eval_loss(x, y, nat.zero_state(B))[0]
+    assert abs(ev.item() - loss_n.item()) < 1e-3
+    # the library-logits route (DCR_DEBUG wide_head=0): same loss, same gradients
+    os.environ["DCR_DEBUG"] = "wide_head=0"
+    try:
+        lib = CharRNN(cfg, device="cuda", seed=4)
+    finally:
+        del os.environ["DCR_DEBUG"]
+    assert not lib.backend.wide_head
+    loss_l, _, ex_l = lib.backend.train_step(x, y, lib.zero_state(B), want_extras=True)
+    torch.cuda.synchronize()
+    assert abs(loss_l.item() - loss_n.item()) < 2e-3
+    assert rel(ex["logits"], ex_l["logits"]) < 1e-3
+    assert rel(g_wide, lib.store.grad) < 2e-2
