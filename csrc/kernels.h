@@ -94,6 +94,20 @@ struct LstmEwArgs {
 };
 void launch_lstm_ew(bool bwd, const LstmEwArgs& a, hipStream_t s);
 
+// ---- lstm_gemm_step.hip: fused large-H LSTM step (MFMA GEMM + cell epilogue) -------------
+struct BigStepArgs {
+  int B, H, S;             // S: split-K slices (set by the launcher)
+  const bf16* A;           // forward: W_hᵀ [4H, H]; backward: W_h [H, 4H]
+  const bf16* X;           // forward: h_{t-1} [B, H]; backward: dZ_{t+1} [B, 4H]
+  float* ws;               // split-K slabs (big_step_workspace floats)
+  unsigned* cnt;           // [tiles] arrival tickets, zero between launches
+  LstmEwArgs ew;           // epilogue operands (forward / backward fields as in lstm_ew.hip)
+};
+bool big_step_supported(int B, int H);
+void big_step_workspace(bool bwd, int B, int H, int cus, int force_S, int64_t* ws_floats,
+                        int64_t* tickets);
+int launch_big_step(bool bwd, const BigStepArgs& a, int cus, int force_S, hipStream_t s);
+
 void launch_fwd_step(int cell, const FwdStepArgs& a, hipStream_t s);
 void launch_bwd_step(int cell, const BwdStepArgs& a, hipStream_t s);
 

@@ -264,6 +264,107 @@ void lstm_step_ew_bwd(const at::Tensor& dtop, const c10::optional<at::Tensor>& d
   dcr::launch_lstm_ew(true, a, cur_stream());
 }
 
+int num_cus();
+
+// Fused large-H LSTM steps (lstm_gemm_step.hip): the recurrent MFMA GEMM of one time step with
+// the cell (or cell-backward) epilogue in the same launch.  ws / cnt: split-K slabs and arrival
+// tickets (big_step_workspace; cnt zero-initialised once, the kernels leave it zero).
+void check_big_ws(bool bwd, int B, int H, int64_t force_S, const at::Tensor& ws,
+                  const at::Tensor& cnt) {
+  TORCH_CHECK(dcr::big_step_supported(B, H), "big step: H must be a multiple of 128");
+  int64_t wf = 0, nt = 0;
+  dcr::big_step_workspace(bwd, B, H, num_cus(), (int)force_S, &wf, &nt);
+  check_seq(ws, at::kFloat, "ws");
+  TORCH_CHECK(ws.numel() >= wf, "big step: workspace too small (", ws.numel(), " < ", wf, ")");
+  TORCH_CHECK(cnt.is_cuda() && cnt.element_size() == 4 && cnt.numel() >= nt,
+              "big step: ticket buffer too small");
+}
+
+int64_t lstm_big_step_fwd(const at::Tensor& WhT, const at::Tensor& hprev, const at::Tensor& zx,
+                          const c10::optional<at::Tensor>& ids, const at::Tensor& cprev,
+                          at::Tensor& hout, const c10::optional<at::Tensor>& hout32,
+                          at::Tensor& cout, at::Tensor& gates, at::Tensor& ws, at::Tensor& cnt,
+                          double forget_bias, int64_t force_S) {
+  check_seq(WhT, at::kBFloat16, "WhT");
+  check_seq(hprev, at::kBFloat16, "hprev");
+  check_seq(zx, at::kFloat, "zx");
+  check_seq(cprev, at::kFloat, "cprev");
+  check_seq(hout, at::kBFloat16, "hout");
+  check_seq(cout, at::kFloat, "cout");
+  check_seq(gates, at::kBFloat16, "gates");
+  check_opt(ids, at::kInt, "ids");
+  check_opt(hout32, at::kFloat, "hout32");
+  const int B = (int)hout.size(0), H = (int)hout.size(1);
+  TORCH_CHECK(WhT.size(0) == 4 * H && WhT.size(1) == H, "WhT must be [4H, H]");
+  TORCH_CHECK(hprev.numel() == (int64_t)B * H && cprev.numel() == hprev.numel() &&
+                  cout.numel() == hprev.numel() && gates.numel() == (int64_t)B * 4 * H,
+              "lstm_big_step_fwd: shapes");
+  TORCH_CHECK(zx.size(-1) == 4 * H, "zx row must be 4H");
+  if (has(ids)) {
+    TORCH_CHECK(ids->numel() == B, "ids must be [B]");
+  } else {
+    TORCH_CHECK(zx.numel() == (int64_t)B * 4 * H, "zx must be [B, 4H]");
+  }
+  if (has(hout32)) TORCH_CHECK(hout32->numel() == (int64_t)B * H, "hout32 shape");
+  check_big_ws(false, B, H, force_S, ws, cnt);
+  dcr::BigStepArgs a{};
+  a.B = B;
+  a.H = H;
+  a.A = ptr<bf16>(WhT);
+  a.X = ptr<bf16>(hprev);
+  a.ws = ptr<float>(ws);
+  a.cnt = reinterpret_cast<unsigned*>(cnt.data_ptr());
+  a.ew.B = B;
+  a.ew.H = H;
+  a.ew.forget_bias = (float)forget_bias;
+  a.ew.zx = ptr<float>(zx);
+  a.ew.ids = has(ids) ? ptr<int>(*ids) : nullptr;
+  a.ew.cprev = ptr<float>(cprev);
+  a.ew.hout = ptr<bf16>(hout);
+  a.ew.hout32 = optr<float>(hout32);
+  a.ew.cout = ptr<float>(cout);
+  a.ew.gates = ptr<bf16>(gates);
+  return dcr::launch_big_step(false, a, num_cus(), (int)force_S, cur_stream());
+}
+
+int64_t lstm_big_step_bwd(const at::Tensor& Wh, const at::Tensor& dznext, const at::Tensor& dtop,
+                          const at::Tensor& gates, const at::Tensor& c, const at::Tensor& cprev,
+                          at::Tensor& dc, at::Tensor& dz_out, at::Tensor& ws, at::Tensor& cnt,
+                          int64_t force_S) {
+  check_seq(Wh, at::kBFloat16, "Wh");
+  check_seq(dznext, at::kBFloat16, "dznext");
+  check_seq(dtop, at::kFloat, "dtop");
+  check_seq(gates, at::kBFloat16, "gates");
+  check_seq(c, at::kFloat, "c");
+  check_seq(cprev, at::kFloat, "cprev");
+  check_seq(dc, at::kFloat, "dc");
+  check_seq(dz_out, at::kBFloat16, "dz_out");
+  const int B = (int)dtop.size(0), H = (int)dtop.size(1);
+  TORCH_CHECK(Wh.size(0) == H && Wh.size(1) == 4 * H, "Wh must be [H, 4H]");
+  TORCH_CHECK(dznext.numel() == (int64_t)B * 4 * H && gates.numel() == dznext.numel() &&
+                  dz_out.numel() == dznext.numel(), "lstm_big_step_bwd: shapes");
+  TORCH_CHECK(c.numel() == (int64_t)B * H && cprev.numel() == c.numel() && dc.numel() == c.numel(),
+              "lstm_big_step_bwd: state shapes");
+  TORCH_CHECK(dznext.data_ptr() != dz_out.data_ptr(), "dznext and dz_out must differ");
+  check_big_ws(true, B, H, force_S, ws, cnt);
+  dcr::BigStepArgs a{};
+  a.B = B;
+  a.H = H;
+  a.A = ptr<bf16>(Wh);
+  a.X = ptr<bf16>(dznext);
+  a.ws = ptr<float>(ws);
+  a.cnt = reinterpret_cast<unsigned*>(cnt.data_ptr());
+  a.ew.B = B;
+  a.ew.H = H;
+  a.ew.dtop = ptr<float>(dtop);
+  a.ew.gates_in = ptr<bf16>(gates);
+  a.ew.c = ptr<float>(c);
+  a.ew.cprev = ptr<float>(cprev);
+  a.ew.dc = ptr<float>(dc);
+  a.ew.dz_out = ptr<bf16>(dz_out);
+  return dcr::launch_big_step(true, a, num_cus(), (int)force_S, cur_stream());
+}
+
 void rnn_bwd_seq(int64_t cell, const at::Tensor& W, const c10::optional<at::Tensor>& W2,
                  const at::Tensor& dtop, at::Tensor& dz, const c10::optional<at::Tensor>& dzx,
                  const c10::optional<at::Tensor>& gates, const c10::optional<at::Tensor>& pre,
@@ -1273,6 +1374,23 @@ TORCH_LIBRARY(dcr, m) {
       "lstm_step_ew_bwd(Tensor dtop, Tensor? dhrec, Tensor gates, Tensor c, Tensor cprev, "
       "Tensor(a!) dc, Tensor(b!) dz_out) -> ()");
   m.def(
+      "lstm_big_step_fwd(Tensor WhT, Tensor hprev, Tensor zx, Tensor? ids, Tensor cprev, "
+      "Tensor(a!) hout, Tensor(b!)? hout32, Tensor(c!) cout, Tensor(d!) gates, Tensor(e!) ws, "
+      "Tensor(f!) cnt, float forget_bias, int force_S=0) -> int");
+  m.def(
+      "lstm_big_step_bwd(Tensor Wh, Tensor dznext, Tensor dtop, Tensor gates, Tensor c, "
+      "Tensor cprev, Tensor(a!) dc, Tensor(b!) dz_out, Tensor(c!) ws, Tensor(d!) cnt, "
+      "int force_S=0) -> int");
+  m.def("big_step_workspace(bool bwd, int B, int H, int force_S=0) -> int[]",
+        [](bool bwd, int64_t B, int64_t H, int64_t force_S) -> std::vector<int64_t> {
+          int64_t wf = 0, nt = 0;
+          dcr::big_step_workspace(bwd, (int)B, (int)H, num_cus(), (int)force_S, &wf, &nt);
+          return {wf, nt};
+        });
+  m.def("big_step_supported(int B, int H) -> bool", [](int64_t B, int64_t H) -> bool {
+    return dcr::big_step_supported((int)B, (int)H);
+  });
+  m.def(
       "rnn_fwd_seq(int cell, Tensor WT, Tensor? WT2, Tensor zx, Tensor? ids, Tensor(a!) hbuf, "
       "Tensor(b!)? h32, Tensor(c!)? cbuf, Tensor(d!)? gates, Tensor(e!)? pre, Tensor(f!)? aux, "
       "Tensor(g!)? rh, Tensor(h!)? hlast32, float forget_bias) -> ()");
@@ -1412,6 +1530,8 @@ TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("sumsq", &sumsq);
   m.impl("lstm_step_ew_fwd", &lstm_step_ew_fwd);
   m.impl("lstm_step_ew_bwd", &lstm_step_ew_bwd);
+  m.impl("lstm_big_step_fwd", &lstm_big_step_fwd);
+  m.impl("lstm_big_step_bwd", &lstm_big_step_bwd);
   m.impl("head_wide", &head_wide);
   m.impl("adam_clip", &adam_clip);
   m.impl("rnn_fwd_seq", &rnn_fwd_seq);

@@ -101,9 +101,36 @@ def _stale(obj: str, src: str, headers) -> bool:
     return any(os.path.getmtime(h) > t for h in headers)
 
 
+class _BuildLock:
+    """Inter-process lock around a build: the ranks of a multi-process run that all find a
+    stale library would otherwise compile into the same object files and link into the same
+    temporary library at once (one rank then loads a half-written _C.so)."""
+
+    def __enter__(self):
+        import fcntl
+
+        os.makedirs(os.path.dirname(OUT), exist_ok=True)
+        self.fh = open(OUT + ".lock", "w")
+        fcntl.flock(self.fh, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *exc):
+        import fcntl
+
+        fcntl.flock(self.fh, fcntl.LOCK_UN)
+        self.fh.close()
+
+
 def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> str:
+    with _BuildLock():
+        return _build_locked(force, jobs, verbose)
+
+
+def _build_locked(force: bool, jobs: int | None, verbose: bool) -> str:
     os.makedirs(BUILD, exist_ok=True)
     want = source_hash()
+    if not force and recorded_hash() == want and os.path.exists(OUT):
+        return OUT  # another process built it while this one waited for the lock
     if recorded_hash() != want and os.path.exists(OUT):
         force = True  # the library was built from other sources (mtimes can lie after a copy)
     hipcc = _hipcc()
@@ -137,7 +164,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     objs = [o for o, _ in results]
     if force or not os.path.exists(OUT) or any(os.path.getmtime(o) > os.path.getmtime(OUT)
                                                for o in objs):
-        tmp = OUT + ".tmp"
+        tmp = f"{OUT}.tmp{os.getpid()}"
         cmd = [hipcc, *COMMON, "-shared", "-o", tmp, *objs, *ldflags]
         if verbose:
             print(" ".join(cmd), flush=True)
@@ -145,8 +172,10 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         os.replace(tmp, OUT)
-    with open(OUT + ".srchash", "w") as fh:
+    tmp_hash = f"{OUT}.srchash.tmp{os.getpid()}"
+    with open(tmp_hash, "w") as fh:
         fh.write(want + "\n")
+    os.replace(tmp_hash, OUT + ".srchash")
     return OUT
 
 

@@ -1,6 +1,12 @@
-"""Large-H LSTM path: per-time-step recurrent GEMM on the library (hipBLASLt) + an
-epilogue-only cell kernel (csrc/lstm_ew.hip), each layer's T-step loop captured once as a
-hipGraph and replayed (the reference's per-step cuBLAS GEMM + pointwise kernels, model.py:72)."""
+"""Large-H LSTM path (rnn_size > 1024, BASELINE config 4): one launch per time step, each
+layer's T-step loop captured once as a hipGraph and replayed (the reference runs the same
+per-step MatMul + pointwise cell inside its static unroll, model.py:72).
+
+Default: the fused MFMA step kernels of csrc/lstm_gemm_step.hip -- the recurrent GEMM of the
+step with the LSTM cell (forward) or cell-backward (BPTT) epilogue in registers, no fp32
+[B, 4H] pre-activation round trip.  ``DCR_DEBUG=bigstep=0`` restores the previous form: a
+library (hipBLASLt) GEMM per step followed by an epilogue-only cell kernel (csrc/lstm_ew.hip).
+"""
 from __future__ import annotations
 
 import torch
@@ -11,73 +17,113 @@ from .gemm import f32
 
 class LibStepMixin:
     def _lib_step(self, direction: str, B: int) -> bool:
-        """Per-time-step recurrent GEMM on the library path + epilogue-only cell kernel, for
-        LSTM with H > 1024 (no weights-resident kernel there).  The fused per-step kernels
-        re-read the whole step payload once per 16-unit block (128 x at H = 2048), so their
-        step time grows linearly with the batch; a library GEMM reads W_h once per step
-        (scripts/bench_step_gemms.py: 17-25 us for B = 64-256).  auto: BPTT always, forward
-        from B >= 128 (at B = 64 the fused forward step, 16.7 us, beats GEMM + epilogue).
-        DCR_RECURRENCE=library forces it, =step disables it."""
+        """One launch per time step for LSTM with H > 1024 (no weights-resident kernel fits
+        there).  With the fused step kernels both directions always take this path; on the
+        library form (bigstep=0) the forward at B < 128 keeps the fused per-step kernels of
+        rnn_step.hip (16.7 us at B = 64 beat GEMM + epilogue).  DCR_RECURRENCE=library forces
+        it, =step disables it."""
         if self.cfg.model != "lstm" or self.knobs.recurrence == "step":
             return False
         if self.knobs.recurrence == "library":
             return True
         if self.H <= 1024:
             return False
+        if self._big_step_ok(B):
+            return True
         return direction == "bwd" or B >= 128
+
+    def _big_step_ok(self, B: int) -> bool:
+        return self.knobs.on("bigstep") and bool(self.ops.big_step_supported(B, self.H))
+
+    def _big_ws(self, bufs, bwd: bool, B: int):
+        """Split-K slabs + arrival tickets of the fused step kernels (the tickets start at zero
+        and every launch leaves them at zero)."""
+        key = "big_ws_bwd" if bwd else "big_ws_fwd"
+        S = int(self.knobs.dbg("bigstep_s", "0"))
+        ent = bufs.get(key)
+        if ent is None or ent[2] != (B, S):
+            wf, nt = self.ops.big_step_workspace(bwd, B, self.H, S)
+            ent = bufs[key] = (torch.empty(max(int(wf), 4), dtype=f32, device=self.dev),
+                               torch.zeros(max(int(nt), 1), dtype=torch.int32, device=self.dev),
+                               (B, S))
+        return ent[0], ent[1], S
 
     def _lstm_fwd_lib(self, lw, lb, zx, ids, bufs) -> None:
         T, B = lb.gates.shape[0], lb.gates.shape[1]
-        zrec = bufs.get("zrec")
-        if zrec is None:
-            zrec = bufs["zrec"] = torch.empty(1, B, self.GW, dtype=f32, device=self.dev)
+        if self._big_step_ok(B):
+            ws, cnt, S = self._big_ws(bufs, False, B)
 
-        def body(zx, ids):
-            for t in range(T):
-                # B operand as W_hᵀ-transposed (NT form): 20.7 vs 25.6 us at B = 256
-                torch.mm(lb.hbuf[t], lw.WhT.t(), out_dtype=f32, out=zrec[0])
-                self.ops.lstm_step_ew_fwd(zrec, zx if ids is not None else zx[t],
-                                          ids[t] if ids is not None else None, lb.cbuf[t],
-                                          lb.hbuf[t + 1], lb.hlast32 if t == T - 1 else None,
-                                          lb.cbuf[t + 1], lb.gates[t], FORGET_BIAS)
+            def body(zx, ids):
+                for t in range(T):
+                    self.ops.lstm_big_step_fwd(
+                        lw.WhT, lb.hbuf[t], zx if ids is not None else zx[t],
+                        ids[t] if ids is not None else None, lb.cbuf[t], lb.hbuf[t + 1],
+                        lb.hlast32 if t == T - 1 else None, lb.cbuf[t + 1], lb.gates[t], ws, cnt,
+                        FORGET_BIAS, S)
+        else:
+            zrec = bufs.get("zrec")
+            if zrec is None:
+                zrec = bufs["zrec"] = torch.empty(1, B, self.GW, dtype=f32, device=self.dev)
+
+            def body(zx, ids):
+                for t in range(T):
+                    # B operand as W_hᵀ-transposed (NT form): 20.7 vs 25.6 us at B = 256
+                    torch.mm(lb.hbuf[t], lw.WhT.t(), out_dtype=f32, out=zrec[0])
+                    self.ops.lstm_step_ew_fwd(zrec, zx if ids is not None else zx[t],
+                                              ids[t] if ids is not None else None, lb.cbuf[t],
+                                              lb.hbuf[t + 1], lb.hlast32 if t == T - 1 else None,
+                                              lb.cbuf[t + 1], lb.gates[t], FORGET_BIAS)
 
         self._run_lib_loop(bufs, ("fwd", id(lb)), body, zx, ids,
                            a_static=lb.zx is not None and zx.data_ptr() == lb.zx.data_ptr())
 
     def _lstm_bwd_lib(self, lw, lb, dtop, bufs) -> None:
         T, B = dtop.shape[0], dtop.shape[1]
-        # dZ·W_hᵀ as S split-K slabs over K = 4H (the cell kernel sums them): the unsplit
-        # [B, 8192] x [8192, 2048] product tiles a [B, 2048] output into too few workgroups
-        # (scripts/micro/step_gemm_large_b.py: B = 256 28.7 -> 19.3 us at S = 2, B = 512
-        # 34.7 -> 23.2 us and B = 1024 47.1 -> 36.7 us at S = 4)
-        S = 4 if B >= 512 else 2 if B >= 256 else 1
-        dh = bufs.get("dhrec")
-        if dh is None or dh.shape[0] != S:
-            dh = bufs["dhrec"] = torch.empty(S, B, self.H, dtype=f32, device=self.dev)
         dc = bufs["dc"]
-        G4 = 4 * self.H
-        WhT = lw.Wh.t() if S == 1 else lw.Wh.view(self.H, S, G4 // S).permute(1, 2, 0)
+        if self._big_step_ok(B):
+            ws, cnt, S = self._big_ws(bufs, True, B)
 
-        def body(dtop, _unused):
-            dc.zero_()
-            for t in reversed(range(T)):
-                # dh = dtop_t + dZ_{t+1}·W_hᵀ: the GEMM writes the recurrent part, the cell
-                # kernel adds dtop_t (an addmm with a 2-D input costs a separate copy launch)
-                if t < T - 1:
-                    if S == 1:
-                        torch.mm(lb.dz[t + 1], WhT, out_dtype=f32, out=dh[0])
-                    else:
-                        torch.bmm(lb.dz[t + 1].view(B, S, G4 // S).transpose(0, 1), WhT,
-                                  out_dtype=f32, out=dh)
-                self.ops.lstm_step_ew_bwd(dtop[t], dh if t < T - 1 else None, lb.gates[t],
-                                          lb.cbuf[t + 1], lb.cbuf[t], dc, lb.dz[t])
+            def body(dtop, _unused):
+                dc.zero_()
+                # the last step has no recurrent term: the epilogue-only cell kernel
+                self.ops.lstm_step_ew_bwd(dtop[T - 1], None, lb.gates[T - 1], lb.cbuf[T],
+                                          lb.cbuf[T - 1], dc, lb.dz[T - 1])
+                for t in reversed(range(T - 1)):
+                    self.ops.lstm_big_step_bwd(lw.Wh, lb.dz[t + 1], dtop[t], lb.gates[t],
+                                               lb.cbuf[t + 1], lb.cbuf[t], dc, lb.dz[t], ws, cnt,
+                                               S)
+        else:
+            # dZ·W_hᵀ as S split-K slabs over K = 4H (the cell kernel sums them): the unsplit
+            # [B, 8192] x [8192, 2048] product tiles a [B, 2048] output into too few workgroups
+            # (scripts/micro/step_gemm_large_b.py: B = 256 28.7 -> 19.3 us at S = 2, B = 512
+            # 34.7 -> 23.2 us and B = 1024 47.1 -> 36.7 us at S = 4)
+            S = 4 if B >= 512 else 2 if B >= 256 else 1
+            dh = bufs.get("dhrec")
+            if dh is None or dh.shape[0] != S:
+                dh = bufs["dhrec"] = torch.empty(S, B, self.H, dtype=f32, device=self.dev)
+            G4 = 4 * self.H
+            WhT = lw.Wh.t() if S == 1 else lw.Wh.view(self.H, S, G4 // S).permute(1, 2, 0)
+
+            def body(dtop, _unused):
+                dc.zero_()
+                for t in reversed(range(T)):
+                    # dh = dtop_t + dZ_{t+1}·W_hᵀ: the GEMM writes the recurrent part, the cell
+                    # kernel adds dtop_t (an addmm with a 2-D input costs a separate copy launch)
+                    if t < T - 1:
+                        if S == 1:
+                            torch.mm(lb.dz[t + 1], WhT, out_dtype=f32, out=dh[0])
+                        else:
+                            torch.bmm(lb.dz[t + 1].view(B, S, G4 // S).transpose(0, 1), WhT,
+                                      out_dtype=f32, out=dh)
+                    self.ops.lstm_step_ew_bwd(dtop[t], dh if t < T - 1 else None, lb.gates[t],
+                                              lb.cbuf[t + 1], lb.cbuf[t], dc, lb.dz[t])
 
         static = any(buf is not None and dtop.data_ptr() == buf.data_ptr()
                      for buf in (bufs["dtop"], bufs["dx"]))
         self._run_lib_loop(bufs, ("bwd", id(lb)), body, dtop, None, a_static=static)
 
     def _run_lib_loop(self, bufs, key, body, a, b, a_static: bool = False) -> None:
-        """Run a T-step library loop (2 launches per step) as a replayed hipGraph: eager,
+        """Run a T-step loop (one or two launches per step) as a replayed hipGraph: eager,
         the per-step host launch cost (~15 us) is as long as the GPU's step at B = 64.  The
         graph is captured on the first call with static copies of the loop's varying inputs
         (a: zx / table / dtop, b: ids) and replayed afterwards; everything else it touches
