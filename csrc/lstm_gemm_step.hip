@@ -433,6 +433,7 @@ using Cfg3 = BsCfg<64, 64, 1, 1, 4, true>;     // BwdS : 64 x 64, BK = 128
 using Cfg4 = BsCfg<64, 128, 4, 2, 1, false>;   // FwdL8: 256 x 128, 8 waves of 64 x 64
 using Cfg5 = BsCfg<128, 128, 2, 4, 1, true>;   // BwdL8: 128 x 128, 8 waves of 64 x 32
 using Cfg6 = BsCfg<32, 128, 2, 4, 1, false>;   // FwdM8: 128 x 128, 8 waves of 64 x 32
+using Cfg7 = BsCfg<32, 256, 2, 4, 1, false>;   // FwdW8: 128 x 256, 8 waves of 64 x 64
 
 namespace {
 struct BsPlan {
@@ -458,16 +459,19 @@ BsPlan bs_cfg(int id) {
     case 3: return bs_fill<Cfg3>(3);
     case 4: return bs_fill<Cfg4>(4);
     case 5: return bs_fill<Cfg5>(5);
-    default: return bs_fill<Cfg6>(6);
+    case 6: return bs_fill<Cfg6>(6);
+    default: return bs_fill<Cfg7>(7);
   }
 }
 bool bs_cfg_bwd(int id) { return id == 2 || id == 3 || id == 5; }
 
 BsPlan bs_plan(bool bwd, int B, int H, int cus, int force_S) {
-  const bool large = B >= 256;
-  int id = bwd ? (large ? 2 : 3) : (large ? 0 : 1);
+  // forward: the configuration whose grid is closest to one workgroup per CU without a K split
+  // (scripts/micro/big_step_bench.py at H = 2048: B = 128 cfg 1 13.7 us, B = 512 cfg 6 26.9 us,
+  // B = 1024 cfg 4 45.7 us; split-K slices of large tiles lose to the serial slab reduction)
+  int id = bwd ? (B >= 256 ? 2 : 3) : (B <= 160 ? 1 : B <= 640 ? 6 : 7);
   const int forced = debug_int("bigstep_cfg", -1);
-  if (forced >= 0 && forced <= 6 && bs_cfg_bwd(forced) == bwd && H % bs_cfg(forced).BU == 0)
+  if (forced >= 0 && forced <= 7 && bs_cfg_bwd(forced) == bwd && H % bs_cfg(forced).BU == 0)
     id = forced;
   BsPlan p = bs_cfg(id);
   p.tiles = (H / p.BU) * ((B + p.BN - 1) / p.BN);
@@ -511,7 +515,8 @@ int launch_big_step(bool bwd, const BigStepArgs& a0, int cus, int force_S, hipSt
     case 3: bs_launch<Cfg3>(grid, a, s); break;
     case 4: bs_launch<Cfg4>(grid, a, s); break;
     case 5: bs_launch<Cfg5>(grid, a, s); break;
-    default: bs_launch<Cfg6>(grid, a, s); break;
+    case 6: bs_launch<Cfg6>(grid, a, s); break;
+    default: bs_launch<Cfg7>(grid, a, s); break;
   }
   return p.S;
 }

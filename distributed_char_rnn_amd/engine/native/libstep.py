@@ -2,10 +2,11 @@
 layer's T-step loop captured once as a hipGraph and replayed (the reference runs the same
 per-step MatMul + pointwise cell inside its static unroll, model.py:72).
 
-Default: the fused MFMA step kernels of csrc/lstm_gemm_step.hip -- the recurrent GEMM of the
-step with the LSTM cell (forward) or cell-backward (BPTT) epilogue in registers, no fp32
-[B, 4H] pre-activation round trip.  ``DCR_DEBUG=bigstep=0`` restores the previous form: a
-library (hipBLASLt) GEMM per step followed by an epilogue-only cell kernel (csrc/lstm_ew.hip).
+Two forms of a step: the fused MFMA step kernels of csrc/lstm_gemm_step.hip -- the recurrent
+GEMM of the step with the LSTM cell (forward) or cell-backward (BPTT) epilogue in registers, no
+fp32 [B, 4H] pre-activation round trip -- and the library form, a hipBLASLt GEMM per step
+followed by an epilogue-only cell kernel (csrc/lstm_ew.hip).  Each direction and batch takes the
+one measured faster (``_big_step_ok``); ``DCR_DEBUG=bigstep=0|2`` forces library | fused.
 """
 from __future__ import annotations
 
@@ -18,22 +19,31 @@ from .gemm import f32
 class LibStepMixin:
     def _lib_step(self, direction: str, B: int) -> bool:
         """One launch per time step for LSTM with H > 1024 (no weights-resident kernel fits
-        there).  With the fused step kernels both directions always take this path; on the
-        library form (bigstep=0) the forward at B < 128 keeps the fused per-step kernels of
-        rnn_step.hip (16.7 us at B = 64 beat GEMM + epilogue).  DCR_RECURRENCE=library forces
-        it, =step disables it."""
+        there), both directions at every batch: at B = 64 the library-form forward also beats
+        the fused per-step kernels of rnn_step.hip (4-layer LSTM-2048, T = 512: 87.7 vs 92.4 ms
+        per training step, same box).  DCR_RECURRENCE=library forces this path for any H,
+        =step disables it."""
         if self.cfg.model != "lstm" or self.knobs.recurrence == "step":
             return False
         if self.knobs.recurrence == "library":
             return True
         if self.H <= 1024:
             return False
-        if self._big_step_ok(B):
-            return True
-        return direction == "bwd" or B >= 128
+        return True
 
-    def _big_step_ok(self, B: int) -> bool:
-        return self.knobs.on("bigstep") and bool(self.ops.big_step_supported(B, self.H))
+    # forward steps at B >= 96 beat the library form (scripts/micro/big_step_bench.py, H = 2048:
+    # B = 128 13.7 vs 17.3 us, B = 512 26.9 vs 32.2, B = 1024 45.7 vs 49.9); at B = 64 the
+    # library form is faster (13.7 vs 15.5) and so is the BPTT step at every batch (split-K
+    # slabs of K = 4H: 22.6 vs 20.6 us at B = 64, 82 vs 56 at B = 1024)
+    BIG_FWD_MIN_B = 96
+
+    def _big_step_ok(self, direction: str, B: int) -> bool:
+        """Fused MFMA step kernels (csrc/lstm_gemm_step.hip) for this direction and batch.
+        DCR_DEBUG=bigstep=0: never, =1 (default): where measured faster, =2: always."""
+        mode = self.knobs.dbg("bigstep", "1")
+        if mode == "0" or not bool(self.ops.big_step_supported(B, self.H)):
+            return False
+        return mode == "2" or (direction == "fwd" and B >= self.BIG_FWD_MIN_B)
 
     def _big_ws(self, bufs, bwd: bool, B: int):
         """Split-K slabs + arrival tickets of the fused step kernels (the tickets start at zero
@@ -50,7 +60,7 @@ class LibStepMixin:
 
     def _lstm_fwd_lib(self, lw, lb, zx, ids, bufs) -> None:
         T, B = lb.gates.shape[0], lb.gates.shape[1]
-        if self._big_step_ok(B):
+        if self._big_step_ok("fwd", B):
             ws, cnt, S = self._big_ws(bufs, False, B)
 
             def body(zx, ids):
@@ -80,7 +90,7 @@ class LibStepMixin:
     def _lstm_bwd_lib(self, lw, lb, dtop, bufs) -> None:
         T, B = dtop.shape[0], dtop.shape[1]
         dc = bufs["dc"]
-        if self._big_step_ok(B):
+        if self._big_step_ok("bwd", B):
             ws, cnt, S = self._big_ws(bufs, True, B)
 
             def body(dtop, _unused):

@@ -46,8 +46,8 @@ DEBUG_KEYS = {
     "wide_head": "0: library logits GEMM + one-read CE instead of the fused wide-vocabulary head",
     "seg_sort": "0: unsorted atomic embedding gradient for wide vocabularies",
     "lib_graph": "0: eager library-step loops (no hipGraph replay)",
-    "bigstep": "0: large-H LSTM steps as library GEMM + epilogue kernel instead of the fused "
-               "MFMA step kernels (csrc/lstm_gemm_step.hip)",
+    "bigstep": "large-H LSTM steps: 0 library GEMM + epilogue kernel, 1 (default) the fused MFMA "
+               "step kernels (csrc/lstm_gemm_step.hip) where measured faster, 2 fused always",
     "bigstep_s": "n: force n split-K slices in the fused large-H step kernels",
     "bigstep_cfg": "id: force tile configuration id of the fused large-H step kernels (C++)",
     "sample_graph": "0: eager sampling loop (no hipGraph replay)",

@@ -51,7 +51,7 @@ def main():
     dev = "cuda"
     WhT = (torch.randn(4 * H, H, device=dev) / H ** 0.5).to(torch.bfloat16)
     Wh = WhT.t().contiguous()
-    for B in (int(x) for x in a.B.split(",")):
+    for B in (int(x) for x in a.B.replace(":", ",").split(",")):
         h = torch.randn(NSTEP + 1, B, H, device=dev).to(torch.bfloat16)
         c = torch.randn(NSTEP + 1, B, H, device=dev)
         zx = torch.randn(B, 4 * H, device=dev)
@@ -96,7 +96,7 @@ def main():
 
         fl = 2.0 * B * 4 * H * H
         if a.cfgs:
-            for cid in (int(x) for x in a.cfgs.split(",")):
+            for cid in (int(x) for x in a.cfgs.replace(":", ",").split(",")):
                 os.environ["DCR_DEBUG"] = f"bigstep_cfg={cid}"
                 bwd = cid in (2, 3, 5)
                 # the workspace depends on the configuration's tile count

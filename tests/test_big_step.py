@@ -115,7 +115,7 @@ def test_big_step_matches_library_path_in_training(ops):
     res = []
     old = os.environ.get("DCR_DEBUG")
     try:
-        for dbg in ("bigstep=1", "bigstep=0"):
+        for dbg in ("bigstep=2", "bigstep=0"):
             os.environ["DCR_DEBUG"] = dbg
             m = CharRNN(cfg, device="cuda:0", seed=0)
             loss, _, _ = m.train_step(x, y, m.zero_state(B))
@@ -132,7 +132,8 @@ def test_big_step_matches_library_path_in_training(ops):
 
 
 @pytest.mark.parametrize("cfg,B,H", [(4, 256, 2048), (4, 300, 1024), (6, 1024, 2048),
-                                     (6, 100, 512), (5, 512, 2048), (5, 37, 256)])
+                                     (6, 100, 512), (5, 512, 2048), (5, 37, 256),
+                                     (7, 1024, 2048), (7, 200, 1024)])
 def test_big_step_tile_configs(ops, monkeypatch, cfg, B, H):
     """Every forced tile configuration (DCR_DEBUG=bigstep_cfg) against the fp32 reference."""
     monkeypatch.setenv("DCR_DEBUG", f"bigstep_cfg={cfg}")
