@@ -1345,10 +1345,17 @@ void prep(at::TensorList src, at::TensorList dst, at::IntArrayRef mode, at::Tens
                   "prep: destinations must be bf16 or fp32");
       T.kind = d.scalar_type() == at::kBFloat16 ? dcr::PREP_BF16 : dcr::PREP_F32;
     }
+    // float4 reads / 4-element writes (the weight-layout refresh of every step: 27 us in scalar
+    // form at the headline shape, profiles/r2_s5_prep_split.txt)
+    const bool al = T.src_ld % 4 == 0 && T.dst_ld % 4 == 0 && a16(T.src) &&
+                    (reinterpret_cast<uintptr_t>(T.dst) & 7) == 0 && T.kind != dcr::PREP_RAW32 &&
+                    (T.kind == dcr::PREP_BF16 || a16(T.dst));
     if (T.mode == dcr::PREP_COPY) {
       TORCH_CHECK(d.size(0) == s.size(0) && d.size(1) == s.size(1), "prep: copy shape mismatch");
+      T.vec4 = (al && T.cols % 4 == 0) ? 1 : 0;
     } else if (T.mode == dcr::PREP_TRANSPOSE) {
       TORCH_CHECK(d.size(0) == s.size(1) && d.size(1) == s.size(0), "prep: transpose shape mismatch");
+      T.vec4 = (al && T.cols % 4 == 0 && T.rows % 4 == 0) ? 1 : 0;
     } else {
       TORCH_CHECK(false, "prep: unknown mode");
     }

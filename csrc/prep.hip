@@ -41,6 +41,17 @@ __device__ __forceinline__ void prep_put(const PrepTask& T, size_t idx, float v)
   else reinterpret_cast<float*>(T.dst)[idx] = v;
 }
 
+// 4 consecutive destination elements (16-B aligned fp32 / 8-B aligned bf16: vec4 tasks)
+__device__ __forceinline__ void prep_put4(const PrepTask& T, size_t idx, float4 v) {
+  if (T.kind == PREP_BF16) {
+    bf16x4 b;
+    b[0] = f2bf(v.x); b[1] = f2bf(v.y); b[2] = f2bf(v.z); b[3] = f2bf(v.w);
+    *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(T.dst) + idx) = b;
+  } else {
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(T.dst) + idx) = v;
+  }
+}
+
 __global__ void __launch_bounds__(256) prep_kernel(PrepTable tab) {
   __shared__ float tile[kPrepTile][kPrepTile + 1];
   int bid = blockIdx.x, k = 0;
@@ -66,6 +77,14 @@ __global__ void __launch_bounds__(256) prep_kernel(PrepTable tab) {
           if (c0 + tx < T.cols)
             reinterpret_cast<unsigned*>(T.dst)[(size_t)r * T.dst_ld + c0 + tx] =
                 s[(size_t)r * T.src_ld + c0 + tx];
+        return;
+      }
+      if (T.vec4) {  // 16 lanes x float4 per 64-column row, 16 rows per pass
+        const int c = c0 + 4 * (threadIdx.x & 15);
+        if (c >= T.cols) return;
+        for (int r = r0 + (threadIdx.x >> 4); r < r1; r += 16)
+          prep_put4(T, (size_t)r * T.dst_ld + c,
+                    *reinterpret_cast<const float4*>(src + (size_t)r * T.src_ld + c));
         return;
       }
       for (int r = r0 + ty; r < r1; r += 4)
@@ -237,6 +256,23 @@ __global__ void __launch_bounds__(256) prep_kernel(PrepTable tab) {
       if (c0 + c < T.cols && r0 + tx < T.rows)
         reinterpret_cast<unsigned*>(T.dst)[(size_t)(c0 + c) * T.dst_ld + r0 + tx] =
             __builtin_bit_cast(unsigned, tile[tx][c]);
+    return;
+  }
+  if (T.vec4) {
+    // float4 row reads into the tile; each thread then writes 4 consecutive destination
+    // elements (source rows r..r+3 of one column) as one 8-B (bf16) / 16-B (fp32) store
+    const int cq = 4 * (threadIdx.x & 15);
+    for (int r = threadIdx.x >> 4; r < kPrepTile; r += 16)
+      if (r0 + r < T.rows && c0 + cq < T.cols) {
+        const float4 v = *reinterpret_cast<const float4*>(src + (size_t)(r0 + r) * T.src_ld + c0 + cq);
+        tile[r][cq] = v.x; tile[r][cq + 1] = v.y; tile[r][cq + 2] = v.z; tile[r][cq + 3] = v.w;
+      }
+    __syncthreads();
+    const int rq = 4 * (threadIdx.x & 15);
+    for (int c = threadIdx.x >> 4; c < kPrepTile; c += 16)
+      if (c0 + c < T.cols && r0 + rq < T.rows)
+        prep_put4(T, (size_t)(c0 + c) * T.dst_ld + r0 + rq,
+                  make_float4(tile[rq][c], tile[rq + 1][c], tile[rq + 2][c], tile[rq + 3][c]));
     return;
   }
   for (int r = ty; r < kPrepTile; r += 4)

@@ -77,3 +77,21 @@ def test_prep_sum_colsum_onehot_table_raw(dcr_ops):
     dcr_ops.prep([E, part], [tab2, out2], [6, 3], [W, bias])
     torch.cuda.synchronize()
     assert torch.equal(out2, out) and torch.equal(tab2, tab)
+
+
+def test_prep_copy_transpose_vec4(dcr_ops):
+    """Aligned tasks take the float4 paths (16-B reads, 4-element writes); partial tiles at the
+    right / bottom edges, bf16 and fp32 destinations."""
+    torch.manual_seed(1)
+    src = torch.randn(300, 2052, device="cuda")          # 300 rows (partial 64-row tile)
+    sub = src[:, 4:4 + 1000]                             # 16-B aligned view, 1000 cols
+    d_copy = torch.empty(300, 1000, dtype=torch.bfloat16, device="cuda")
+    d_copy32 = torch.empty(300, 1000, device="cuda")
+    d_t = torch.empty(1000, 300, dtype=torch.bfloat16, device="cuda")
+    d_t32 = torch.empty(1000, 300, device="cuda")
+    dcr_ops.prep([sub, sub, sub, sub], [d_copy, d_copy32, d_t, d_t32], [0, 0, 1, 1], [])
+    torch.cuda.synchronize()
+    assert torch.equal(d_copy, sub.to(torch.bfloat16))
+    assert torch.equal(d_copy32, sub)
+    assert torch.equal(d_t, sub.t().to(torch.bfloat16))
+    assert torch.equal(d_t32, sub.t().contiguous())
