@@ -19,6 +19,7 @@
 // d softmax_w = Oᵀ·dlog stays a split-K library GEMM (token reduction, engine/native_backend.py).
 #include "common.h"
 #include "kernels.h"
+#include "debug_env.h"
 
 namespace dcr {
 
@@ -33,6 +34,9 @@ __global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs a) {
   constexpr int TPW = kHeadTPW;
   __shared__ __attribute__((aligned(16))) bf16 sdl[4][TPW * 16][SLD];
   __shared__ float red[4][VP + 1];
+  // softmax_wᵀ [VP, H] staged once per workgroup (shared by its 4 waves), 16-B chunk c of row r
+  // at chunk c ^ (r & 15): the 16 rows of a fragment read hit 16 distinct bank groups
+  extern __shared__ __attribute__((aligned(16))) bf16 swt[];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nl = lane & 15, g = lane >> 4;
@@ -59,6 +63,25 @@ __global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs a) {
   float lacc = 0.f;
 
   const int nchunks = (N + TPW * 16 - 1) / (TPW * 16);
+  const int hc = H / 8;  // 16-B chunks per softmax_wᵀ row
+  if (a.lds_wst) {
+    // every thread's loads issued together (8 per batch), then the swizzled LDS stores
+    for (int i0 = threadIdx.x; i0 < VP * hc; i0 += 8 * kHeadThreads) {
+      bf16x8 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = i0 + j * kHeadThreads;
+        v[j] = i < VP * hc ? ld8(a.WsT + (size_t)(i / hc) * H + 8 * (i % hc)) : zero8();
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = i0 + j * kHeadThreads;
+        const int r = i / hc, c = i % hc;
+        if (i < VP * hc) *reinterpret_cast<bf16x8*>(&swt[(size_t)r * H + 8 * (c ^ (r & 15))]) = v[j];
+      }
+    }
+    __syncthreads();
+  }
   for (int chunk = blockIdx.x * 4 + w; chunk < nchunks; chunk += gridDim.x * 4) {
     const int nb = chunk * TPW * 16;
     // ---- logits
@@ -71,17 +94,42 @@ __global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs a) {
 #pragma unroll
     for (int tp = 0; tp < TPW; ++tp)
       orow[tp] = a.O + (size_t)min(nb + tp * 16 + nl, N - 1) * a.ldo + 8 * g;
-    const bf16* wrow = a.WsT + (size_t)nl * H + 8 * g;
+    if (a.lds_wst) {
+      // A fragments from the LDS image; the chunk's O fragments in groups of 8 k-steps, each
+      // group's 16 loads issued together (one L2 round trip per group instead of per k-step)
+      for (int k0 = 0; k0 < H; k0 += 256) {
+        bf16x8 bo[8][TPW];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int tp = 0; tp < TPW; ++tp)
+            bo[j][tp] = k0 + 32 * j < H ? ld8(orow[tp] + k0 + 32 * j) : zero8();
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (k0 + 32 * j >= H) break;
+          const int c = (k0 + 32 * j) / 8 + g;  // logical chunk of this lane's 8 k
+#pragma unroll
+          for (int vt = 0; vt < NVT; ++vt) {
+            const bf16x8 af =
+                *reinterpret_cast<const bf16x8*>(&swt[(size_t)(16 * vt + nl) * H + 8 * (c ^ nl)]);
+#pragma unroll
+            for (int tp = 0; tp < TPW; ++tp) acc[tp][vt] = mfma16(af, bo[j][tp], acc[tp][vt]);
+          }
+        }
+      }
+    } else {
+      const bf16* wrow = a.WsT + (size_t)nl * H + 8 * g;
 #pragma unroll 2
-    for (int k = 0; k < H; k += 32) {
-      bf16x8 bo[TPW];
+      for (int k = 0; k < H; k += 32) {
+        bf16x8 bo[TPW];
 #pragma unroll
-      for (int tp = 0; tp < TPW; ++tp) bo[tp] = ld8(orow[tp] + k);
+        for (int tp = 0; tp < TPW; ++tp) bo[tp] = ld8(orow[tp] + k);
 #pragma unroll
-      for (int vt = 0; vt < NVT; ++vt) {
-        const bf16x8 af = ld8(wrow + (size_t)vt * 16 * H + k);
+        for (int vt = 0; vt < NVT; ++vt) {
+          const bf16x8 af = ld8(wrow + (size_t)vt * 16 * H + k);
 #pragma unroll
-        for (int tp = 0; tp < TPW; ++tp) acc[tp][vt] = mfma16(af, bo[tp], acc[tp][vt]);
+          for (int tp = 0; tp < TPW; ++tp) acc[tp][vt] = mfma16(af, bo[tp], acc[tp][vt]);
+        }
       }
     }
     // ---- softmax cross-entropy per token
@@ -261,9 +309,25 @@ int head_num_partials(int N, int cus) {
   return g < cap ? (g > 0 ? g : 1) : cap;
 }
 
+// dynamic LDS of the staged softmax_wᵀ image: VP x H bf16 while it fits beside the static
+// arrays (V <= 80 at H = 512: 80 KB); larger heads stream it from L2 (lds_wst = 0)
+constexpr size_t kHeadLdsWst = 96 * 1024;
+
 template <int NVT>
-static void head_inst(const HeadArgs& a, int grid, hipStream_t s) {
-  head_kernel<NVT><<<grid, kHeadThreads, 0, s>>>(a);
+static void head_inst(const HeadArgs& a0, int grid, hipStream_t s) {
+  HeadArgs a = a0;
+  const size_t bytes = (size_t)16 * NVT * a.H * sizeof(bf16);
+  // (the chunk swizzle c ^ (r & 15) needs whole groups of 16 chunks per row: H % 128 == 0)
+  a.lds_wst = bytes <= kHeadLdsWst && a.H % 128 == 0 && debug_int("head_lds", 1) != 0 ? 1 : 0;
+  if (a.lds_wst) {
+    static bool attr_set = false;  // opt in to > 64 KB of dynamic LDS once per instantiation
+    if (!attr_set) {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&head_kernel<NVT>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHeadLdsWst);
+      attr_set = true;
+    }
+  }
+  head_kernel<NVT><<<grid, kHeadThreads, a.lds_wst ? bytes : 0, s>>>(a);
 }
 
 int launch_head(const HeadArgs& a, int cus, float* db_out, float* loss_out, hipStream_t s) {

@@ -349,6 +349,7 @@ struct HeadArgs {
   float* part;          // [grid, VP+1] partials workspace
   const uint8_t* omask; // optional dropout bits of O ([N, H/8], dropout.hip): dtop is written
   float oscale;         //   masked and scaled by 1/keep (the output dropout's backward)
+  int lds_wst;          // set by the launcher: softmax_wᵀ staged in (dynamic) LDS
 };
 int head_vpad(int V);
 int head_kpad(int V);
