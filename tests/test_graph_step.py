@@ -54,3 +54,33 @@ def test_graph_step_equals_eager(B, T, H, L):
     for a, b in zip(sg, se):
         for u, v in zip(a, b):
             assert torch.equal(u, v)
+
+
+@pytest.mark.gpu
+def test_graph_replays_poll_the_error_word():
+    """A persistent-kernel error raised while the step is graph-replayed is reported within a
+    few replays (the replays count as steps for the every-k-th non-blocking error-word copy),
+    not silently skipped until the next checkpoint."""
+    cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=128, num_layers=2)
+    B, T = 32, 16
+    m = CharRNN(cfg, device="cuda", seed=5)
+    opt = TFAdam(m.store, clip=5.0, guard=m.error_word())
+    gstep = GraphedStep(m, opt)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randint(0, 65, (B, T), generator=g, dtype=torch.int32).cuda()
+    y = torch.randint(0, 65, (B, T), generator=g, dtype=torch.int32).cuda()
+    st = m.zero_state(B)
+    for _ in range(4):
+        _, st = gstep(x, y, st, 2e-3)
+    torch.cuda.synchronize()
+    assert gstep.graph is not None and gstep.replays >= 2
+    m.error_word().fill_(7)  # as a spin timeout inside a replay would
+    raised = False
+    for _ in range(2 * m.backend.ERR_POLL_EVERY + 2):
+        try:
+            _, st = gstep(x, y, st, 2e-3)
+        except RuntimeError as e:
+            assert "code 7" in str(e)
+            raised = True
+            break
+    assert raised

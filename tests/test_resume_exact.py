@@ -112,3 +112,23 @@ def test_dp_resume_with_checkpoint_on_rank0_only(tmp_path):
                                      "--resume_exact"])
     assert "restored" in outs[0]
     _assert_same(_final(str(r0 / "full")), _final(str(r0 / "resumed")))
+
+
+@pytest.mark.gpu
+def test_resume_exact_with_dropout_continues_the_mask_sequence(tmp_path):
+    """On the native GPU path the dropout masks come from a per-step counter: --resume_exact
+    restores it (``dcr/drop_step``), so a killed + resumed dropout run ends where the
+    uninterrupted one does; without the counter it would replay the masks of step 1."""
+    w = str(tmp_path)
+    gpu = ["--device", "cuda", "--input_keep_prob", "0.8", "--output_keep_prob", "0.9",
+           "--rnn_size", "128", "--graph", "off"]
+    _train(w, ["--save_dir", "full"] + gpu)
+    _train(w, ["--save_dir", "part", "--max_steps", "7"] + gpu)
+    part = _final(os.path.join(w, "part"))
+    assert int(part["dcr/drop_step"]) == 7
+    _train(w, ["--save_dir", "resumed", "--init_from", "part", "--resume_exact"] + gpu)
+    a, b = _final(os.path.join(w, "full")), _final(os.path.join(w, "resumed"))
+    assert int(a["global_step"]) == int(b["global_step"])
+    assert int(a["dcr/drop_step"]) == int(b["dcr/drop_step"])
+    for k in (k for k in a if not k.startswith("dcr/")):
+        np.testing.assert_allclose(a[k], b[k], rtol=1e-5, atol=1e-6, err_msg=k)
