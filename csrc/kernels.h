@@ -249,6 +249,9 @@ struct Lstm2Args {
   const bf16* X0T;      //   projection x0·W_x,l (W_x,lᵀ [4H, H]) then runs in-kernel (zx0 unused)
   int wgarr;            // 1: one counter add per workgroup and layer (the layer's last epilogue
                         //   wave signals for both, persist_common.h wg_arrive); 0: one per wave
+  int hld;              // row stride (elements) of hbuf0 / hbuf1: H, or 2H when both layers' h
+                        //   live interleaved in one [T+2, B, 2H] buffer (row t+1 = [h_l(t),
+                        //   h_l+1(t-1)]: the operand of layer l+1's merged weight gradient)
 };
 // batch groups per workgroup for the two-layer kernels at (H, B) (force > 0: only that value),
 // 0 = unsupported

@@ -99,6 +99,12 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
   auto rm_off = [&](int bg, int j, int s) {
     return (unsigned)((((size_t)bg * 32 + 16 * j) * H + kbase + s * 32) * sizeof(bf16));
   };
+  // the same for the h buffers (row stride hld: H, or 2H in the pair-interleaved layout)
+  const int hld = a.hld;
+  const unsigned rmh_lane = (unsigned)(((lane & 15) * hld + kq) * sizeof(bf16));
+  auto rmh_off = [&](int bg, int j, int s) {
+    return (unsigned)((((size_t)bg * 32 + 16 * j) * hld + kbase + s * 32) * sizeof(bf16));
+  };
 
   bf16x8 w0[4][KS], w1[4][KS], x1[4][KS];
 #pragma unroll
@@ -274,26 +280,26 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
         const bool ring0 = tau > 0;
         const __amdgpu_buffer_rsrc_t r0 =
             ring0 ? make_rsrc(a.hring0 + (size_t)(tau & 1) * ringsz, sizeof(bf16) * ringsz)
-                  : make_rsrc(a.hbuf0, sizeof(bf16) * (size_t)B * H);
+                  : make_rsrc(a.hbuf0, sizeof(bf16) * (size_t)B * hld);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int s = 0; s < KS; ++s)
             hf0[j][s] = ring0 ? ld8_sc1(r0, frag_load_off(2 * bg + j, w * KS + s, H, lane))
-                              : ld8_sc1(r0, rm_lane + rm_off(bg, j, s));
+                              : ld8_sc1(r0, rmh_lane + rmh_off(bg, j, s));
       }
       if (ld1) {
         const int s1 = tau - LAG;
         const bool ring1 = s1 > 0;
         const __amdgpu_buffer_rsrc_t r1 =
             ring1 ? make_rsrc(a.hring1 + (size_t)(s1 & 1) * ringsz, sizeof(bf16) * ringsz)
-                  : make_rsrc(a.hbuf1, sizeof(bf16) * (size_t)B * H);
+                  : make_rsrc(a.hbuf1, sizeof(bf16) * (size_t)B * hld);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int s = 0; s < KS; ++s)
             hf1[j][s] = ring1 ? ld8_sc1(r1, frag_load_off(2 * bg + j, w * KS + s, H, lane))
-                              : ld8_sc1(r1, rm_lane + rm_off(bg, j, s));
+                              : ld8_sc1(r1, rmh_lane + rmh_off(bg, j, s));
       }
     };
     load_group(0, pf0[0], pf1[0]);
@@ -474,7 +480,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
         if (xdrop) do_stash();
         if (live) {  // row-major copies for the GEMMs / head (not handed off)
           const size_t o = (size_t)(t + 1) * B * H + bh;
-          st4bf(hbL + o, h[0], h[1], h[2], h[3]);
+          st4bf(hbL + ((size_t)(t + 1) * B + b) * hld + u0, h[0], h[1], h[2], h[3]);
           *reinterpret_cast<float4*>(cbL + o) = make_float4(c[g][0], c[g][1], c[g][2], c[g][3]);
           if (gtL) {
             bf16* gp = gtL + ((size_t)t * B + b) * 4 * H + u0;

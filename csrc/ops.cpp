@@ -863,7 +863,18 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
   const bool xin = has(x0);
   if (!xin) check_seq(zx0, at::kFloat, "zx0");
   check_seq(bias1, at::kFloat, "bias1");
-  for (auto* t : {&hbuf0, &hbuf1, &hring0, &hring1}) check_seq(*t, at::kBFloat16, "hbuf/hring");
+  for (auto* t : {&hring0, &hring1}) check_seq(*t, at::kBFloat16, "hring");
+  // hbuf0 / hbuf1: [T+1, B, H] with rows of stride hld >= H (the pair-interleaved layout of
+  // engine/native/buffers.py puts both layers in one [T+2, B, 2H] buffer: hld = 2H)
+  for (auto* t : {&hbuf0, &hbuf1}) {
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->dim() == 3,
+                "hbuf must be a bf16 GPU tensor [T+1, B, H]");
+    TORCH_CHECK(t->stride(2) == 1 && t->stride(1) >= t->size(2) && t->stride(1) % 8 == 0 &&
+                    t->stride(0) == t->size(1) * t->stride(1) &&
+                    (reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0,
+                "hbuf rows must be unit-stride, 16-B aligned, stride a multiple of 8, slot-dense");
+  }
+  TORCH_CHECK(hbuf1.stride(1) == hbuf0.stride(1), "hbuf0 and hbuf1 must share the row stride");
   for (auto* t : {&cbuf0, &cbuf1, &hlast0, &hlast1}) check_seq(*t, at::kFloat, "state");
   check_opt(gates0, at::kBFloat16, "gates0");
   check_opt(gates1, at::kBFloat16, "gates1");
@@ -873,7 +884,8 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
               "two-layer persistent LSTM: no co-resident grid for H=", H, " B=", B, " G=", G);
   const int nbg = lstm2_nbg(B, (int)G);
   TORCH_CHECK(hbuf1.sizes() == hbuf0.sizes(), "hbuf1 must match hbuf0");
-  TORCH_CHECK(cbuf0.numel() == hbuf0.numel() && cbuf1.numel() == hbuf0.numel(), "cbuf shape");
+  TORCH_CHECK(cbuf0.numel() == (int64_t)(T + 1) * B * H && cbuf1.numel() == cbuf0.numel(),
+              "cbuf shape");
   TORCH_CHECK(hlast0.numel() == (int64_t)B * H && hlast1.numel() == (int64_t)B * H, "hlast shape");
   for (auto* t : {&W0T, &W1T, &X1T})
     TORCH_CHECK(t->size(0) == 4 * H && t->size(1) == H, "weights must be [4H, H]");
@@ -902,6 +914,7 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
   a.W0T = ptr<bf16>(W0T); a.W1T = ptr<bf16>(W1T); a.X1T = ptr<bf16>(X1T);
   a.zx0 = xin ? nullptr : ptr<float>(zx0); a.ids = optr<int>(ids); a.zx_ld = 4 * H;
   a.x0 = optr<bf16>(x0); a.X0T = optr<bf16>(X0T);
+  a.hld = (int)hbuf0.stride(1);
   a.bias1 = ptr<float>(bias1);
   if (has(bias0)) {
     check_seq(*bias0, at::kFloat, "bias0");

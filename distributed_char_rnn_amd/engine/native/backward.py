@@ -190,6 +190,11 @@ class BackwardMixin:
                 mm_tn(lb.rh.view(N, H), dZ[:, 2 * H:], s.gview(ck)[H:], q=q)
             elif self.cfg.model == "nas":
                 mm_tn(Hprev, dZ, s.gview(names[1]), q=q)
+            elif lb.x_merged:
+                # pair-interleaved h (buffers.py): rows [x_t, h_{t-1}] of this layer's kernel
+                # lie side by side, so its W_x and W_h gradients are ONE [2H x 4H] GEMM
+                C = bufs["pair_h"][layer]
+                mm_tn(C[1:T + 1].reshape(N, 2 * H), dZ, s.gview(names[0]), q=q)
             else:
                 mm_tn(Hprev, dZ, s.gview(names[0])[H:], q=q)
             if gather and V > SEG_LDS_MAX_V and not fused_dew:
@@ -234,8 +239,11 @@ class BackwardMixin:
                     # + the sumsq kernel (66 us at the headline shape)
                     self._token_norm(torch.mm(dZx, lw.Wx.t()))
             else:
-                dWx = (mm_tn(lb.x_in, dZx, s.gview(names[0])[:H], q=q)
-                       if self.cfg.model in ("lstm", "rnn") else mm_tn(lb.x_in, dZx))
+                if lb.x_merged:  # written by the merged GEMM above
+                    dWx = s.gview(names[0])[:H]
+                else:
+                    dWx = (mm_tn(lb.x_in, dZx, s.gview(names[0])[:H], q=q)
+                           if self.cfg.model in ("lstm", "rnn") else mm_tn(lb.x_in, dZx))
                 if layer in bufs["pers_layers"]:
                     dbias = self._bias_sum(self._db_part(bufs, layer), names, q)  # fused in BPTT
                 else:

@@ -28,6 +28,7 @@ class LayerBufs:
     x_in: Optional[torch.Tensor] = None      # bf16 [N, D] layer input (dense mode)
     clast32: Optional[torch.Tensor] = None   # fp32 [B, H] final c (persistent LSTM)
     x_drop: Optional[torch.Tensor] = None    # bf16 [N, D] masked layer input (dropout)
+    x_merged: bool = False                   # x_in and h_{t-1} interleaved: one dW GEMM
 
 
 class BuffersMixin:
@@ -66,12 +67,28 @@ class BuffersMixin:
             if training and drop:
                 lb.x_drop = torch.empty(N, H, dtype=bf16, device=dev)
             layers.append(lb)
+        # pair-interleaved h (training, two-layer wavefront forwards): layers (l, l+1) write
+        # their h rows into one [T+2, B, 2H] buffer C with row t+1 = [h_l(t), h_l+1(t-1)], i.e.
+        # exactly the rows [x_t, h_{t-1}] of layer l+1's kernel [2H, 4H]: its two weight
+        # gradients become ONE [2H x 4H] token-reduction GEMM over C (backward.py)
+        # (scripts/micro/dw_gemm_forms.py: 3 GEMMs + slab sums 273 us -> 233 us).
+        # hbuf_l = C[0:T+1, :, :H], hbuf_l+1 = C[1:T+2, :, H:] (row stride 2H).
+        pair_h = {}
+        if training and plan.pair and m == "lstm" and self.knobs.on("pair_dw"):
+            for lo in range(0, 2 * (self.L // 2), 2):
+                if lo > 0 and plan.persist and plan.xfuse and not drop:
+                    continue  # forward.py runs these layers on the fused single-layer kernels
+                C = torch.empty(T + 2, B, 2 * H, dtype=bf16, device=dev)
+                layers[lo].hbuf = C[0:T + 1, :, :H]
+                layers[lo + 1].hbuf = C[1:T + 2, :, H:]
+                pair_h[lo + 1] = C
         ws = max(self.ops.segsum_workspace(N, GW, self.V), self.ops.segsum_workspace(N, H, self.V),
                  self.ops.segsum_workspace(N, GW, 1), self.ops.segsum_workspace(N, self.V, 1), 1)
         e = lambda *shape, dt=f32: torch.empty(*shape, dtype=dt, device=dev)  # noqa: E731
         bufs = dict(
             plan=plan,
             layers=layers,
+            pair_h=pair_h,
             logits=e(N, self.V),
             dlogits=e(N, self.V, dt=bf16) if training else None,
             row_loss=e(N),

@@ -115,6 +115,8 @@ class ForwardMixin:
             # before the optimizer), so the one-workgroup-per-CU fused variant is safe here
             xfuse = P.persist and P.xfuse and layer > 0 and not drop and lw.WxT is not None
             if xfuse:
+                if not x_prev.is_contiguous():  # h of a pair-interleaved layer (row stride 2H)
+                    x_prev = x_prev.contiguous()
                 lb.x_in = x_prev.reshape(N, H)
                 self.ops.lstm_persist_fwd(lw.WhT, lw.bias, None, lb.hbuf, lb.cbuf, lb.gates,
                                           lb.hlast32, bufs["cnt"][layer], self.err, FORGET_BIAS,
@@ -137,13 +139,15 @@ class ForwardMixin:
                     X = x_prev.reshape(N, H)
                     if inb is not None:
                         X = self._masked(X, inb, dm["sin"], out=lb.x_drop)
-                lb.x_in = X if X.is_contiguous() else X.contiguous()
                 # opt-in (DCR_DEBUG=xin=1): the G = 1 two-layer forward projects these bf16 rows
                 # in-kernel (no [N, 4H] fp32 zx round trip); measured slower than the library
                 # GEMM + zx once the forward's payload loads moved first (dropout headline 2.32
                 # vs 2.20 ms, same box)
                 xin = (P.pair and layer + 1 < self.L and P.pair_g == 1 and lw.WxT is not None
                        and self.knobs.debug.get("xin") == "1" and self._xin_ok())
+                # (row-strided rows -- the h of a pair-interleaved layer -- feed the library
+                # GEMMs as they are; the in-kernel projection wants dense rows)
+                lb.x_in = X.contiguous() if (xin or X.stride(-1) != 1) else X
                 if xin:
                     zx = lb.x_in
                 else:
@@ -169,9 +173,11 @@ class ForwardMixin:
                                            dm["sin"] if dm else 1.0,
                                            lw.bias if ids_arg is None else None,
                                            lb.x_in if xin else None, lw.WxT if xin else None)
-                # layer l+1's (masked) input rows for its weight gradient
+                # layer l+1's (masked) input rows for its weight gradient; unmasked rows of a
+                # pair-interleaved buffer feed ONE GEMM for both of its weight gradients
                 lb1.x_in = (self._masked(lb.hbuf[1:], xm, dm["sin"], out=lb1.x_drop)
                             if xm is not None else lb.hbuf[1:].reshape(N, H))
+                lb1.x_merged = xm is None and (layer + 1) in bufs.get("pair_h", {})
                 x_prev = lb1.hbuf[1:]
                 paired = layer + 1
                 continue
@@ -196,7 +202,7 @@ class ForwardMixin:
         O = x_prev.reshape(N, H)
         if dm is not None and dm["out"] is not None:  # the top layer's output dropout
             O = self._masked(O, dm["out"], dm["sout"], out=bufs["o_drop"])
-        if not O.is_contiguous():
+        if O.stride(-1) != 1 or O.stride(0) % 8:  # the heads take row-strided O (ldo)
             O = O.contiguous()
         logits = bufs["logits"]
         if want_logits:

@@ -53,6 +53,8 @@ DEBUG_KEYS = {
     "sample_graph": "0: eager sampling loop (no hipGraph replay)",
     "head_omask": "0: top output dropout applied to dtop by a separate pass, not the head",
     "xin": "1: in-kernel input projection of a dense layer-l input (G = 1 two-layer forward)",
+    "pair_dw": "0: separate h buffers per layer of a wavefront pair (two weight GEMMs for the "
+               "upper layer instead of one over the pair-interleaved h)",
     "head_lds": "0: fused head streams softmax_wᵀ from L2 instead of staging it in LDS (C++)",
     "wgrad": "1: hand-written wgrad kernel for the weight gradients (default: library split-K)",
     "gru_ub": "1: 16-unit GRU workgroups (C++)",
