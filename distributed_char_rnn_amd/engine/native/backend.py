@@ -87,6 +87,7 @@ class NativeBackend(LayoutsMixin, BuffersMixin, ForwardMixin, BackwardMixin, Lib
         # checkpointed (``drop_step``) so --resume_exact continues the mask sequence
         self._drop_seed = (int(seed) * 0x9E3779B1 + 0x5EED + int(rank) * 0x632BE5AB) & ((1 << 62) - 1)
         self._drop_step = 0
+        self._sorted_ids = None  # wide vocabulary: (sorted ids, permutation) of this step
         self._dm_bufs: Dict[Tuple[int, int], dict] = {}
         self.last_dropout_masks: Optional[dict] = None
 

@@ -24,6 +24,22 @@ class BackwardMixin:
                                                    want_logits=not (self.fused_head
                                                                     or self.wide_head),
                                                    logits_bias=not wide, extra_tasks=id_tasks)
+        # wide vocabulary: the embedding gradient's id sort (~10 small rocPRIM launches, ~50 us)
+        # runs on the side stream beside the (non-persistent) wide head instead of at the end
+        # of the backward; the main stream joins it before the persistent BPTT launches
+        self._sorted_ids = None
+        sort_ev = None
+        if (self.V > SEG_LDS_MAX_V and self.knobs.on("seg_sort") and not self._dropout(True)
+                and self.cfg.model != "nas" and not self.capturing):
+            side = self._side_stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                sid, perm = torch.sort(ids_tm.view(-1))
+                self._sorted_ids = (sid, perm.int())
+                sort_ev = torch.cuda.Event()
+                sort_ev.record(side)
+            for t_ in self._sorted_ids:
+                t_.record_stream(torch.cuda.current_stream())
         # deferred slab / bias sums of this step: one prep launch per flush (gemm.SumQueue)
         q = SumQueue(self.ops, wgrad=self.knobs.debug.get("wgrad") == "1")
         if on_ready is not None:
@@ -77,6 +93,8 @@ class BackwardMixin:
             self.ops.segsum(dlog, None, 1, bufs["colsum"][:, :V], bufs["ws"], False)
             s.gview("rnnlm/softmax_b").copy_(bufs["colsum"][0, :V])
             dtop = mm_into(dlog, hd["Ws"].t(), bufs["dtop"].view(N, H)).view(T, B, H)
+        if sort_ev is not None:  # nothing may share CUs with the persistent BPTT grid
+            torch.cuda.current_stream().wait_event(sort_ev)
         overlap = P.mode == "overlap" or not P.persistent
         pending = []
         user_ready = None
@@ -204,9 +222,14 @@ class BackwardMixin:
                 Eb = hd.get("Ebf")                                  # refreshed with the table
                 X0 = (Eb[ids_tm.view(-1).long()] if Eb is not None
                       else hd["E"][ids_tm.view(-1).long()].to(torch.bfloat16))    # [N, H]
-                dWx = mm_tn(X0, dZx)
+                # (written into the gradient buffer; the slab and bias-partial sums go to the
+                # step's deferred flush instead of separate reduce launches)
+                lstm_like = self.cfg.model in ("lstm", "rnn")
+                dWx = (mm_tn(X0, dZx, s.gview(names[0])[:H], q=q) if lstm_like
+                       else mm_tn(X0, dZx))
                 if layer in bufs["pers_layers"]:
-                    dbias = self._bias_sum(self._db_part(bufs, layer), names)
+                    dbias = self._bias_sum(self._db_part(bufs, layer), names,
+                                           q if lstm_like else None)
                 else:
                     self.ops.segsum(dZx, None, 1, bufs["colsum"][:, :GW], bufs["ws"], False)
                     dbias = bufs["colsum"][0, :GW]
@@ -342,8 +365,12 @@ class BackwardMixin:
         ids = ids_tm.view(-1)
         out = self.store.gview("embedding")
         if self.V > SEG_LDS_MAX_V and self.knobs.on("seg_sort"):
-            sid, perm = torch.sort(ids)
-            self.ops.segsum(dX, sid, self.V, out, bufs["ws"], False, perm.int())
+            if self._sorted_ids is not None:  # sorted beside the head (train_step)
+                sid, perm = self._sorted_ids
+            else:
+                sid, perm = torch.sort(ids)
+                perm = perm.int()
+            self.ops.segsum(dX, sid, self.V, out, bufs["ws"], False, perm)
         else:
             self.ops.segsum(dX, ids, self.V, out, bufs["ws"], False)
 
