@@ -219,9 +219,9 @@ class BackwardMixin:
                 # wide vocabulary: the [V, GW] dEW segment sum would be an atomic scatter of
                 # N x GW values plus two fp32 [V, GW] GEMMs; the dense route scatters N x H
                 # instead: dW_x0 = E[ids]ᵀ·dZ0 (split-K), dE = segsum(dZ0·W_x0ᵀ)
-                Eb = hd.get("Ebf")                                  # refreshed with the table
-                X0 = (Eb[ids_tm.view(-1).long()] if Eb is not None
-                      else hd["E"][ids_tm.view(-1).long()].to(torch.bfloat16))    # [N, H]
+                # X0 = E[ids] as bf16 rows: one gather kernel (embed_dropout without a mask)
+                X0 = bufs["dx_bf"]
+                self.ops.embed_dropout(ids_tm.reshape(-1), hd["E"], None, 1.0, X0)
                 # (written into the gradient buffer; the slab and bias-partial sums go to the
                 # step's deferred flush instead of separate reduce launches)
                 lstm_like = self.cfg.model in ("lstm", "rnn")

@@ -105,6 +105,20 @@ class LayoutsMixin:
             tasks.insert(0, (self._head["E"], tab, 6, [w0.Wx32, w0.bias]))
         else:
             self._table_dirty = True
+            if self.V > SEG_LDS_MAX_V and self.cfg.model in ("lstm", "rnn"):
+                # wide vocabulary: the table's bias rows (a stride-0 broadcast COPY) and the
+                # bf16 copy of E ride in this launch; _run_prep adds E·W_x0 on top (one GEMM with
+                # beta = 1 instead of addmm's separate bias-broadcast pass + a copy launch)
+                tab = self._head.get("table")
+                if tab is None or tab.shape != (self.V, w0.Wx32.shape[1]):
+                    tab = self._head["table"] = torch.empty(self.V, w0.Wx32.shape[1], dtype=f32,
+                                                            device=self.dev)
+                Eb = self._head.get("Ebf")
+                if Eb is None or Eb.shape != self._head["E"].shape:
+                    Eb = self._head["Ebf"] = torch.empty_like(self._head["E"], dtype=bf16)
+                tasks += [(w0.bias.view(1, -1).expand(self.V, -1), tab, 0),
+                          (self._head["E"], Eb, 0)]
+                self._table_bias_in = True
         return tasks
 
     def _run_prep(self, tasks: list):
@@ -122,10 +136,18 @@ class LayoutsMixin:
                 # precision as a bf16 layer-0 input projection; the bf16 E copy is also the
                 # row source of the dense backward route's X0 gather
                 Eb = self._head.get("Ebf")
-                if Eb is None or Eb.shape != self._head["E"].shape:
-                    Eb = self._head["Ebf"] = torch.empty_like(self._head["E"], dtype=bf16)
-                Eb.copy_(self._head["E"])
-                self._head["table"] = torch.addmm(w0.bias, Eb, w0.Wx, out_dtype=f32)
+                if getattr(self, "_table_bias_in", False):  # bias rows + Eb written by prep
+                    self._table_bias_in = False
+                    tab = self._head["table"]
+                    try:
+                        torch.addmm(tab, Eb, w0.Wx, out_dtype=f32, out=tab)
+                    except RuntimeError:  # a torch build without the in-place mixed-dtype form
+                        self._head["table"] = torch.addmm(w0.bias, Eb, w0.Wx, out_dtype=f32)
+                else:
+                    if Eb is None or Eb.shape != self._head["E"].shape:
+                        Eb = self._head["Ebf"] = torch.empty_like(self._head["E"], dtype=bf16)
+                    Eb.copy_(self._head["E"])
+                    self._head["table"] = torch.addmm(w0.bias, Eb, w0.Wx, out_dtype=f32)
             else:
                 self._head["table"] = torch.addmm(w0.bias, self._head["E"], w0.Wx32)  # [V, GW]
             self._table_dirty = False
