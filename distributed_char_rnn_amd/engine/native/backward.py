@@ -211,7 +211,7 @@ class BackwardMixin:
             elif lb.x_merged:
                 # pair-interleaved h (buffers.py): rows [x_t, h_{t-1}] of this layer's kernel
                 # lie side by side, so its W_x and W_h gradients are ONE [2H x 4H] GEMM
-                C = bufs["pair_h"][layer]
+                C = bufs["pair_h"][layer][0]
                 mm_tn(C[1:T + 1].reshape(N, 2 * H), dZ, s.gview(names[0]), q=q)
             else:
                 mm_tn(Hprev, dZ, s.gview(names[0])[H:], q=q)

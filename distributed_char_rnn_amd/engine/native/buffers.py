@@ -73,15 +73,25 @@ class BuffersMixin:
         # gradients become ONE [2H x 4H] token-reduction GEMM over C (backward.py)
         # (scripts/micro/dw_gemm_forms.py: 3 GEMMs + slab sums 273 us -> 233 us).
         # hbuf_l = C[0:T+1, :, :H], hbuf_l+1 = C[1:T+2, :, H:] (row stride 2H).
+        # With dropout, layer l+1's input is the MASKED h_l: the pair forward's mask pass then
+        # writes those rows into C's x half instead (mode "x"), layer l+1's h stays in the h
+        # half, and layer l's h lives in the x half of a second buffer (the pair kernel wants one
+        # row stride for both layers' h).
         pair_h = {}
         if training and plan.pair and m == "lstm" and self.knobs.on("pair_dw"):
             for lo in range(0, 2 * (self.L // 2), 2):
                 if lo > 0 and plan.persist and plan.xfuse and not drop:
                     continue  # forward.py runs these layers on the fused single-layer kernels
                 C = torch.empty(T + 2, B, 2 * H, dtype=bf16, device=dev)
-                layers[lo].hbuf = C[0:T + 1, :, :H]
                 layers[lo + 1].hbuf = C[1:T + 2, :, H:]
-                pair_h[lo + 1] = C
+                if drop:
+                    C0 = torch.empty(T + 1, B, 2 * H, dtype=bf16, device=dev)
+                    layers[lo].hbuf = C0[:, :, :H]
+                    layers[lo + 1].x_drop = C[1:T + 1, :, :H].reshape(N, H)
+                    pair_h[lo + 1] = (C, "x")
+                else:
+                    layers[lo].hbuf = C[0:T + 1, :, :H]
+                    pair_h[lo + 1] = (C, "h")
         ws = max(self.ops.segsum_workspace(N, GW, self.V), self.ops.segsum_workspace(N, H, self.V),
                  self.ops.segsum_workspace(N, GW, 1), self.ops.segsum_workspace(N, self.V, 1), 1)
         e = lambda *shape, dt=f32: torch.empty(*shape, dtype=dt, device=dev)  # noqa: E731

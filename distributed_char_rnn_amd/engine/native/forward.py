@@ -177,7 +177,8 @@ class ForwardMixin:
                 # pair-interleaved buffer feed ONE GEMM for both of its weight gradients
                 lb1.x_in = (self._masked(lb.hbuf[1:], xm, dm["sin"], out=lb1.x_drop)
                             if xm is not None else lb.hbuf[1:].reshape(N, H))
-                lb1.x_merged = xm is None and (layer + 1) in bufs.get("pair_h", {})
+                ph = bufs.get("pair_h", {}).get(layer + 1)
+                lb1.x_merged = ph is not None and (xm is None) == (ph[1] == "h")
                 x_prev = lb1.hbuf[1:]
                 paired = layer + 1
                 continue
