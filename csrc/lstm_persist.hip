@@ -454,6 +454,9 @@ static int ub_for(int H, int B, int cus) {
 }
 
 static const void* pick(int bwd, int H, int B, int flags, int cus) {
+  // H > 1024: 16-unit x NT-tile workgroups (lstm_persist_nt.hip; no fused input, no fused
+  // dEW, no diag stamps: the plain instantiation for every flag)
+  if (H > 1024) return (flags & PF_FUSED) ? nullptr : lstm_persist_nt_fn(bwd, H, B, cus);
   const int ub = ub_for(H, B, cus);
   if (!bwd) {
     const int ks = H / 128;
@@ -474,17 +477,18 @@ static const void* pick(int bwd, int H, int B, int flags, int cus) {
 }
 
 static size_t dyn_lds(int bwd, int H, int B, int V, int cus) {
-  return (bwd && V > 0) ? sizeof(float) * (size_t)V * (ub_for(H, B, cus) * 64 + 1) : 0;
+  return (bwd && V > 0 && H <= 1024) ? sizeof(float) * (size_t)V * (ub_for(H, B, cus) * 64 + 1) : 0;
 }
 
 int lstm_persist_supported(int H, int B, int cus) {
   // shape support only; whether a grid can be co-resident is lstm_persist_occupancy's job
-  (void)cus;
-  if (H % 128 != 0 || B < 1 || H > 1024 || H < 128) return 0;
+  if (H > 1024) return lstm_persist_nt_tiles(H, B, cus) > 0 ? 1 : 0;
+  if (H % 128 != 0 || B < 1 || H < 128) return 0;
   return (H / 16) % ub_for(H, B, cus) == 0 ? 1 : 0;
 }
 
 int lstm_persist_grid(int H, int B, int cus) {
+  if (H > 1024) return lstm_persist_nt_grid(H, B, cus);
   return (H / (16 * ub_for(H, B, cus))) * ((B + 15) / 16);
 }
 
@@ -511,7 +515,7 @@ int lstm_persist_xfuse_supported(int H, int B, int cus) {
 static int launch_persist(int bwd, const PersistArgs& a, int flags, int cus, hipStream_t s) {
   const int grid = lstm_persist_grid(a.H, a.B, cus);
   const void* fn = pick(bwd, a.H, a.B, flags, cus);
-  if (!fn) return -1;
+  if (!fn || (a.H > 1024 && a.dew_part)) return -1;
   const size_t lds = dyn_lds(bwd, a.H, a.B, a.dew_part ? a.V : 0, cus);
   int occ = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 256, lds) != hipSuccess ||

@@ -1,0 +1,364 @@
+// Persistent weights-resident LSTM recurrence for LARGE hidden sizes (H = 2048) at small batch
+// (gfx950).  BASELINE config 4 (4-layer LSTM-2048, seq 512) at B = 64.
+//
+// Reference: TF's statically unrolled LSTMCell chain (model.py:61-73) and its tf.gradients
+// backward (model.py:91) -- the same recurrence as lstm_persist.hip, which covers H <= 1024.
+//
+// Why a separate kernel.  At H = 2048 one 16-unit block of W_h is 4 gates x 16 units x 2048 K
+// (fwd) / 16 units x 8192 K (bwd) = 256 KB of bf16: split over the 4 waves' K quarters that is
+// 256 VGPRs per lane, the whole arch-VGPR file, so a workgroup is alone on its CU and the
+// (H/16) x (B/16) grid of lstm_persist.hip (512 workgroups at B = 64) cannot be co-resident.
+// Here a workgroup owns 16 units x NT 16-row batch tiles: the resident weight slice is reused
+// for NT tiles per step, and the grid is (H/16) x ceil(B / 16NT) = 256 workgroups at B = 64
+// (NT = 2).  The per-step library path it replaces re-streams all 32 MB of W_h from the MALL
+// every step (13.7 us fwd / 20.6 us bwd at B = 64, profiles/r3_big_step.md); here a step moves
+// only the handed-off activations (h: 256 KB, dZ: 1 MB per step, L2-resident).
+//
+// Per step (fwd): wave w loads the fragment-tiled h_{t-1} k-steps of its K quarter for every
+// tile (ONE contiguous 1 KB sc1 load per k-step), multiplies them against its resident W_hᵀ
+// fragments (mfma_f32_16x16x32_bf16, swapped operands: A = weight rows, B = batch rows), the
+// four K partials meet in LDS, and wave n < NT runs the cell epilogue of tile n (c in registers
+// across all T steps).  BPTT: K = 4H, wave w reduces over the gate columns g*H + [w H/4,
+// (w+1) H/4) of every gate (its loads are streamed in 16-k-step chunks to bound registers).
+//
+// Hand-off (persist_common.h "Valid forms" first row): each epilogue wave stores its tile sc1
+// in fragment order, drains (vmcnt(0)) and adds to an LDS counter; the workgroup's last such
+// wave does ONE agent-scope add on shard (unit block & 3) of the (batch group, step) counter;
+// ONE poller lane per workgroup polls the four shards with one 16-B sc1 load (+ s_sleep); a
+// workgroup barrier releases the waves; every load of handed-off bytes is buffer_load sc1.
+// 128 unit blocks per batch group would otherwise be 128 atomics on one address per step.
+// Every spin is bounded; a timeout sets the error word and the grid still drains.
+#include "common.h"
+#include "kernels.h"
+#include "persist_common.h"
+
+namespace dcr {
+
+template <int KS, int NT>
+__global__ void __launch_bounds__(256, 1) lstm_fwd_persist_nt_kernel(PersistArgs a) {
+  // single-buffered partials: every step starts with a workgroup barrier that the epilogue
+  // waves reach only after reading the previous step's partials
+  __shared__ __attribute__((aligned(16))) float part[4][NT][4][64][4];
+  __shared__ unsigned arr;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int H = a.H, B = a.B, T = a.T;
+  const int Bp = (B + 15) / 16 * 16;
+  const int ntile = Bp / 16, nbg = (ntile + NT - 1) / NT;
+  const int nwg_u = H / 16;
+  int ubk, bg;
+  map_block(blockIdx.x, nwg_u, nbg, ubk, bg);
+  const int ub0 = ubk * 16, tile0 = bg * NT;
+  const int ntl = ntile - tile0 < NT ? ntile - tile0 : NT;  // tiles of this batch group
+  const int kq = 8 * (lane >> 4);
+  const int kbase = w * (KS * 32);
+  unsigned* cnt = a.cnt + (size_t)bg * (T + 1) * 4;
+  const unsigned target = (unsigned)(nwg_u / 4);
+  bool dead = false;
+  if (threadIdx.x == 0) arr = 0u;
+
+  // resident A fragments: rows g*H + ub0 + (lane&15) of W_hᵀ, this wave's K quarter
+  bf16x8 wf[4][KS];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      wf[g][s] = ld8(a.W + (size_t)(g * H + ub0 + (lane & 15)) * H + kbase + s * 32 + kq);
+
+  // epilogue: wave w < ntl owns tile tile0 + w (lane: batch row b, units u0..u0+3)
+  const bool epi = w < ntl;
+  const int b = (tile0 + (epi ? w : 0)) * 16 + (lane & 15);
+  const bool live = epi && b < B;
+  const int u0 = ub0 + 4 * (lane >> 4);
+  const size_t bh = (size_t)b * H + u0;
+  float c[4] = {0.f, 0.f, 0.f, 0.f};
+  if (live) ld4f(a.cbuf + bh, c);
+  __syncthreads();  // arr
+
+  for (int t = 0; t < T; ++t) {
+    float zx[4][4] = {};
+    if (live) {
+      const float* zrow = a.ids ? a.zx + (size_t)a.ids[(size_t)t * B + b] * a.zx_ld
+                                : a.zx + ((size_t)t * B + b) * a.zx_ld;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) ld4f(zrow + (size_t)g * H + u0, zx[g]);
+    }
+    if (t > 0) {
+      if (threadIdx.x == kLstmPollerThread && !dead)
+        dead = !poll_shards4(cnt + (size_t)t * 4, target, a.spin_limit, a.err, 1u);
+    }
+    __syncthreads();
+    const bool fring = t > 0;  // slot 0 (initial state) is row-major
+    const __amdgpu_buffer_rsrc_t hsrc =
+        fring ? make_rsrc(a.hring + (size_t)(t & 1) * Bp * H, sizeof(bf16) * (size_t)Bp * H)
+              : make_rsrc(a.hbuf, sizeof(bf16) * (size_t)B * H);
+    // every tile's h fragments are issued before the first MFMA (NT x KS loads in flight)
+    bf16x8 hfs[NT][KS];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      if (n >= ntl) break;  // wave-uniform
+      const int tile = tile0 + n;
+      const unsigned roff =
+          (unsigned)(((size_t)(tile * 16 + (lane & 15)) * H + kbase + kq) * sizeof(bf16));
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        hfs[n][s] = fring ? ld8_sc1(hsrc, (unsigned)lane * 16u, frag_tile_off(tile, w * KS + s, H))
+                          : ld8_sc1(hsrc, roff + s * 64);
+    }
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      if (n >= ntl) break;  // wave-uniform
+      const bf16x8 (&hf)[KS] = hfs[n];
+      f32x4 acc[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g] = mfma16(wf[g][s], hf[s], acc[g]);
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(&part[w][n][g][lane][0]) =
+            make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
+    }
+    __syncthreads();
+    if (epi) {
+      float z[4][4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 s0 = *reinterpret_cast<const float4*>(&part[0][w][g][lane][0]);
+        const float4 s1 = *reinterpret_cast<const float4*>(&part[1][w][g][lane][0]);
+        const float4 s2 = *reinterpret_cast<const float4*>(&part[2][w][g][lane][0]);
+        const float4 s3 = *reinterpret_cast<const float4*>(&part[3][w][g][lane][0]);
+        z[g][0] = s0.x + s1.x + s2.x + s3.x + zx[g][0];
+        z[g][1] = s0.y + s1.y + s2.y + s3.y + zx[g][1];
+        z[g][2] = s0.z + s1.z + s2.z + s3.z + zx[g][2];
+        z[g][3] = s0.w + s1.w + s2.w + s3.w + zx[g][3];
+      }
+      float gi[4], gj[4], gf[4], go[4], h[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        gi[r] = sigmoidf_(z[0][r]);
+        gj[r] = tanhf_(z[1][r]);
+        gf[r] = sigmoidf_(z[2][r] + a.forget_bias);
+        go[r] = sigmoidf_(z[3][r]);
+        c[r] = gf[r] * c[r] + gi[r] * gj[r];
+        h[r] = go[r] * tanhf_(c[r]);
+      }
+      // (padded rows are handed off too: zero inputs, finite values, never read back)
+      st4bf_sc1(a.hring + (size_t)((t + 1) & 1) * Bp * H + frag_index(b, u0, H), h[0], h[1], h[2],
+                h[3]);
+      if (t + 1 < T) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) wg_arrive(&arr, (unsigned)ntl, cnt + (size_t)(t + 1) * 4 + (ubk & 3));
+      }
+      if (live) {
+        const size_t o = (size_t)(t + 1) * B * H + bh;
+        st4bf(a.hbuf + o, h[0], h[1], h[2], h[3]);
+        *reinterpret_cast<float4*>(a.cbuf + o) = make_float4(c[0], c[1], c[2], c[3]);
+        if (a.gates) {
+          bf16* gp = a.gates + ((size_t)t * B + b) * 4 * H + u0;
+          st4bf(gp, gi[0], gi[1], gi[2], gi[3]);
+          st4bf(gp + H, gj[0], gj[1], gj[2], gj[3]);
+          st4bf(gp + 2 * H, gf[0], gf[1], gf[2], gf[3]);
+          st4bf(gp + 3 * H, go[0], go[1], go[2], go[3]);
+        }
+        if (t == T - 1 && a.hlast32)
+          *reinterpret_cast<float4*>(a.hlast32 + bh) = make_float4(h[0], h[1], h[2], h[3]);
+        if (t == T - 1 && a.clast32)
+          *reinterpret_cast<float4*>(a.clast32 + bh) = make_float4(c[0], c[1], c[2], c[3]);
+      }
+    }
+  }
+}
+
+// KS = 4H / 128 k-steps per wave (K = 4H split by unit quarter inside every gate, as in
+// lstm_persist.hip); the payload of one tile is streamed in chunks of KSG = KS / 4 k-steps (one
+// gate segment), two chunks in flight next to the 256 weight VGPRs.
+template <int KS, int NT>
+__global__ void __launch_bounds__(256, 1) lstm_bwd_persist_nt_kernel(PersistArgs a) {
+  __shared__ __attribute__((aligned(16))) float part[4][NT][64][4];
+  __shared__ unsigned arr;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int H = a.H, B = a.B, T = a.T;
+  const int Bp = (B + 15) / 16 * 16;
+  const int ntile = Bp / 16, nbg = (ntile + NT - 1) / NT;
+  const int nwg_u = H / 16;
+  int ubk, bg;
+  map_block(blockIdx.x, nwg_u, nbg, ubk, bg);
+  const int ub0 = ubk * 16, tile0 = bg * NT;
+  const int ntl = ntile - tile0 < NT ? ntile - tile0 : NT;
+  const int kq = 8 * (lane >> 4);
+  const int G4H = 4 * H;
+  unsigned* cnt = a.cnt + (size_t)bg * (T + 1) * 4;
+  const unsigned target = (unsigned)(nwg_u / 4);
+  bool dead = false;
+  if (threadIdx.x == 0) arr = 0u;
+
+  constexpr int KSG = KS / 4;  // k-steps per gate segment
+  bf16x8 wf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+    wf[s] = ld8(a.W + (size_t)(ub0 + (lane & 15)) * G4H + (s / KSG) * H + w * (H / 4) +
+                (s % KSG) * 32 + kq);
+
+  const bool epi = w < ntl;
+  const int b = (tile0 + (epi ? w : 0)) * 16 + (lane & 15);
+  const bool live = epi && b < B;
+  const int u0 = ub0 + 4 * (lane >> 4);
+  const size_t bh = (size_t)b * H + u0;
+  float dc[4] = {0.f, 0.f, 0.f, 0.f};
+  float dbacc[4][4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dbacc[g][r] = 0.f;
+  __syncthreads();  // arr
+
+  for (int t = T - 1; t >= 0; --t) {
+    float gi[4] = {}, gj[4] = {}, gf[4] = {}, go[4] = {}, cc[4] = {}, cp[4] = {}, dtop[4] = {};
+    if (live) {
+      const bf16* gp = a.gates + ((size_t)t * B + b) * G4H + u0;
+      ld4bf(gp, gi); ld4bf(gp + H, gj); ld4bf(gp + 2 * H, gf); ld4bf(gp + 3 * H, go);
+      ld4f(a.cbuf + (size_t)(t + 1) * B * H + bh, cc);
+      ld4f(a.cbuf + (size_t)t * B * H + bh, cp);
+      ld4f(a.dtop + (size_t)t * B * H + bh, dtop);
+    }
+    if (t < T - 1) {
+      if (threadIdx.x == kLstmPollerThread && !dead)
+        dead = !poll_shards4(cnt + (size_t)(t + 1) * 4, target, a.spin_limit, a.err, 2u);
+      __syncthreads();
+      const __amdgpu_buffer_rsrc_t zsrc =
+          make_rsrc(a.zring + (size_t)((t + 1) & 1) * Bp * G4H, sizeof(bf16) * (size_t)Bp * G4H);
+      // chunk c = (tile n = c / 4, gate g = c % 4); two chunk buffers: the loads of chunk c+1
+      // are issued before the MFMAs of chunk c (two chunks = 128 VGPRs in flight)
+      const int nch = 4 * ntl;
+      bf16x8 db[2][KSG];
+      auto load_chunk = [&](int c, bf16x8 (&d)[KSG]) {
+        const int tile = tile0 + c / 4, g = c % 4;
+#pragma unroll
+        for (int s = 0; s < KSG; ++s)
+          d[s] = ld8_sc1(zsrc, (unsigned)lane * 16u,
+                         frag_tile_off(tile, (g * H + w * (H / 4)) / 32 + s, G4H));
+      };
+      load_chunk(0, db[0]);
+      f32x4 pacc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 4 * NT; ++c) {
+        if (c >= nch) break;  // wave-uniform
+        if (c + 1 < nch) load_chunk(c + 1, db[(c + 1) & 1]);
+#pragma unroll
+        for (int s = 0; s < KSG; ++s) pacc = mfma16(wf[(c % 4) * KSG + s], db[c & 1][s], pacc);
+        if (c % 4 == 3) {
+          *reinterpret_cast<float4*>(&part[w][c / 4][lane][0]) =
+              make_float4(pacc[0], pacc[1], pacc[2], pacc[3]);
+          pacc = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      __syncthreads();
+    }
+    if (epi) {
+      float dh[4];
+      if (t < T - 1) {
+        const float4 s0 = *reinterpret_cast<const float4*>(&part[0][w][lane][0]);
+        const float4 s1 = *reinterpret_cast<const float4*>(&part[1][w][lane][0]);
+        const float4 s2 = *reinterpret_cast<const float4*>(&part[2][w][lane][0]);
+        const float4 s3 = *reinterpret_cast<const float4*>(&part[3][w][lane][0]);
+        dh[0] = s0.x + s1.x + s2.x + s3.x + dtop[0];
+        dh[1] = s0.y + s1.y + s2.y + s3.y + dtop[1];
+        dh[2] = s0.z + s1.z + s2.z + s3.z + dtop[2];
+        dh[3] = s0.w + s1.w + s2.w + s3.w + dtop[3];
+      } else {
+        dh[0] = dtop[0]; dh[1] = dtop[1]; dh[2] = dtop[2]; dh[3] = dtop[3];
+      }
+      float di[4], dj[4], df_[4], dO[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float th = tanhf_(cc[r]);
+        const float dcv = dc[r] + dh[r] * go[r] * (1.f - th * th);
+        dO[r] = dh[r] * th * go[r] * (1.f - go[r]);
+        di[r] = dcv * gj[r] * gi[r] * (1.f - gi[r]);
+        dj[r] = dcv * gi[r] * (1.f - gj[r] * gj[r]);
+        df_[r] = dcv * cp[r] * gf[r] * (1.f - gf[r]);
+        dc[r] = dcv * gf[r];
+      }
+      bf16* const zr = a.zring + (size_t)(t & 1) * Bp * G4H;
+      st4bf_sc1(zr + frag_index(b, u0, G4H), di[0], di[1], di[2], di[3]);
+      st4bf_sc1(zr + frag_index(b, H + u0, G4H), dj[0], dj[1], dj[2], dj[3]);
+      st4bf_sc1(zr + frag_index(b, 2 * H + u0, G4H), df_[0], df_[1], df_[2], df_[3]);
+      st4bf_sc1(zr + frag_index(b, 3 * H + u0, G4H), dO[0], dO[1], dO[2], dO[3]);
+      if (t > 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) wg_arrive(&arr, (unsigned)ntl, cnt + (size_t)t * 4 + (ubk & 3));
+      }
+      if (live) {
+        bf16* dz = a.dz + ((size_t)t * B + b) * G4H + u0;
+        st4bf(dz, di[0], di[1], di[2], di[3]);
+        st4bf(dz + H, dj[0], dj[1], dj[2], dj[3]);
+        st4bf(dz + 2 * H, df_[0], df_[1], df_[2], df_[3]);
+        st4bf(dz + 3 * H, dO[0], dO[1], dO[2], dO[3]);
+        // the bias gradient sums the bf16-rounded dz exactly as the dW GEMMs see it
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          dbacc[0][r] += (float)f2bf(di[r]);
+          dbacc[1][r] += (float)f2bf(dj[r]);
+          dbacc[2][r] += (float)f2bf(df_[r]);
+          dbacc[3][r] += (float)f2bf(dO[r]);
+        }
+      }
+    }
+  }
+  // bias-gradient partial of each 16-row tile: reduce its 16 batch lanes (lane bits 0..3)
+  if (epi && a.db_part) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = dbacc[g][r];
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        v += __shfl_xor(v, 4, 64);
+        v += __shfl_xor(v, 8, 64);
+        dbacc[g][r] = v;
+      }
+    if ((lane & 15) == 0) {
+      float* dst = a.db_part + (size_t)(tile0 + w) * G4H + u0;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(dst + g * H) =
+            make_float4(dbacc[g][0], dbacc[g][1], dbacc[g][2], dbacc[g][3]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host side (called from lstm_persist.hip's selection for H > 1024)
+// ------------------------------------------------------------------------------------------
+// Batch tiles per workgroup: the smallest NT in {1, 2} whose (H/16) x ceil(B/16NT) grid fits
+// one workgroup per CU; 0 if none does (the large-batch steps stay on the library form, where
+// the per-step GEMMs are efficient) or the shape has no instantiation.
+int lstm_persist_nt_tiles(int H, int B, int cus) {
+  if (H != 2048 || B < 1 || cus <= 0) return 0;
+  const int ntile = (B + 15) / 16;
+  for (int nt = 1; nt <= 2; nt *= 2)
+    if ((H / 16) * ((ntile + nt - 1) / nt) <= cus) return nt;
+  return 0;
+}
+
+int lstm_persist_nt_grid(int H, int B, int cus) {
+  const int nt = lstm_persist_nt_tiles(H, B, cus);
+  return nt ? (H / 16) * (((B + 15) / 16 + nt - 1) / nt) : 0;
+}
+
+const void* lstm_persist_nt_fn(int bwd, int H, int B, int cus) {
+  switch (lstm_persist_nt_tiles(H, B, cus)) {
+    case 1: return bwd ? (const void*)lstm_bwd_persist_nt_kernel<64, 1>
+                       : (const void*)lstm_fwd_persist_nt_kernel<16, 1>;
+    case 2: return bwd ? (const void*)lstm_bwd_persist_nt_kernel<64, 2>
+                       : (const void*)lstm_fwd_persist_nt_kernel<16, 2>;
+  }
+  return nullptr;
+}
+
+}  // namespace dcr

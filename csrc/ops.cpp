@@ -616,6 +616,10 @@ int num_cus() {
   return cus;
 }
 
+int64_t lstm_persist_nt_tiles(int64_t H, int64_t B) {
+  return dcr::lstm_persist_nt_tiles((int)H, (int)B, num_cus());
+}
+
 int64_t lstm_persist_supported(int64_t H, int64_t B) {
   return dcr::lstm_persist_supported((int)H, (int)B, num_cus());
 }
@@ -1446,6 +1450,7 @@ TORCH_LIBRARY(dcr, m) {
   m.def("xent_num_partials(int n) -> int",
         [](int64_t n) -> int64_t { return dcr::xent_num_partials((int)n); });
   m.def("lstm_persist_supported(int H, int B) -> int", &lstm_persist_supported);
+  m.def("lstm_persist_nt_tiles(int H, int B) -> int", &lstm_persist_nt_tiles);
   m.def("num_cus() -> int", []() -> int64_t { return num_cus(); });
   m.def("lstm_persist_grid(int H, int B) -> int", [](int64_t H, int64_t B) -> int64_t {
     return dcr::lstm_persist_grid((int)H, (int)B, num_cus());

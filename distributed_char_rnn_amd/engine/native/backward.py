@@ -117,7 +117,7 @@ class BackwardMixin:
         # TF clip-norm term from dx_tok = dZ0·W_x0ᵀ: needed as an extra GEMM only on the layer-0
         # gather route (every other route materialises dx_tok anyway)
         gather0 = not drop and self.cfg.model != "nas"
-        fused_dew0 = P.persist and gather0 and V <= 128 and self.dew_mode == "fused"
+        fused_dew0 = P.persist and P.persist_bwd and gather0 and V <= 128 and self.dew_mode == "fused"
         tok_gemm = self.tf_norm and gather0 and not (V > SEG_LDS_MAX_V and not fused_dew0)
         for layer in reversed(range(self.L)):
             lw, lb = self._w[layer], bufs["layers"][layer]
@@ -133,7 +133,7 @@ class BackwardMixin:
             zx_nas = lb.zx if self.cfg.model == "nas" else None
             written = False  # this layer's kernel/bias gradients already in the flat buffer
             gather = (layer == 0 and not drop and self.cfg.model != "nas")
-            fused_dew = P.persist and gather and V <= 128 and self.dew_mode == "fused"
+            fused_dew = P.persist and P.persist_bwd and gather and V <= 128 and self.dew_mode == "fused"
             if pair_hi:
                 # layers (layer-1, layer) as one reverse wavefront (lstm2_persist.hip): T+1
                 # ticks, the lower layer's dtop = dZ·W_xᵀ of this layer computed in-kernel
@@ -153,7 +153,7 @@ class BackwardMixin:
                     on_ready = _release()
             elif layer == paired_done:
                 pass
-            elif P.persist:
+            elif P.persist and P.persist_bwd:
                 self.ops.lstm_persist_bwd(lw.Wh, dtop, lb.dz, lb.gates, lb.cbuf,
                                           bufs["cnt"][self.L + layer], self.err, self.spin_limit,
                                           bufs["zring"], bufs["db_part"][layer][: -(-B // 16)],
@@ -227,7 +227,7 @@ class BackwardMixin:
                 lstm_like = self.cfg.model in ("lstm", "rnn")
                 dWx = (mm_tn(X0, dZx, s.gview(names[0])[:H], q=q) if lstm_like
                        else mm_tn(X0, dZx))
-                if layer in bufs["pers_layers"]:
+                if layer in bufs["bpart_layers"]:
                     dbias = self._bias_sum(self._db_part(bufs, layer), names,
                                            q if lstm_like else None)
                 else:
@@ -239,7 +239,7 @@ class BackwardMixin:
             elif gather:
                 # the bias gradient from the BPTT kernel's partials: summed in the same flush
                 # as dEW's slabs (rather than a column sum of dEW after it)
-                part_bias = layer in bufs["pers_layers"] and self.cfg.model in ("lstm", "rnn")
+                part_bias = layer in bufs["bpart_layers"] and self.cfg.model in ("lstm", "rnn")
                 if part_bias:
                     dbias = self._bias_sum(self._db_part(bufs, layer), names, q)
                 dEW = self._dew(dZx, ids_tm, bufs, fused_dew, q)  # [V, GW] fp32 (flushes q)
@@ -267,7 +267,7 @@ class BackwardMixin:
                 else:
                     dWx = (mm_tn(lb.x_in, dZx, s.gview(names[0])[:H], q=q)
                            if self.cfg.model in ("lstm", "rnn") else mm_tn(lb.x_in, dZx))
-                if layer in bufs["pers_layers"]:
+                if layer in bufs["bpart_layers"]:
                     dbias = self._bias_sum(self._db_part(bufs, layer), names, q)  # fused in BPTT
                 else:
                     self.ops.segsum(dZx, None, 1, bufs["colsum"][:, :GW], bufs["ws"], False)

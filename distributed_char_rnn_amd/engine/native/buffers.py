@@ -150,6 +150,9 @@ class BuffersMixin:
         npair = 2 * (self.L // 2) if plan.pair else 0
         bufs["pers_layers"] = set(range(npair)) | (set(range(npair, self.L)) if plan.persist
                                                    else set())
+        # layers whose BPTT kernel writes bias-gradient partials (db_part)
+        bufs["bpart_layers"] = (bufs["pers_layers"] if plan.persist_bwd
+                                else set(range(npair)))
         self._bufs[key] = bufs
         return bufs
 

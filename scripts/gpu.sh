@@ -47,7 +47,7 @@ for step in "$@"; do
       tag=$(echo "$A" | tr -c 'a-zA-Z0-9' '_' | cut -c1-40)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$tag" -o run -- \
         python3 bench.py $(sp "$A") > "$O/prof_$tag.log" 2>&1 || { tail -20 "$O/prof_$tag.log"; exit 1; }
-      python scripts/step_trace.py "$O/prof_$tag/run_results.db" > "$O/step_trace_$tag.txt" || exit 1
+      python scripts/step_trace.py "$O/prof_$tag/run_results.db" ${TRACE_MARKER:-lstm2_fwd} > "$O/step_trace_$tag.txt" || exit 1
       tail -1 "$O/step_trace_$tag.txt"; tail -1 "$O/prof_$tag.log" ;;
     configs)
       bash scripts/bench_all_configs.sh 2>&1 | tee "$O/all_configs.txt" || exit 1 ;;

@@ -115,8 +115,10 @@ def test_big_step_matches_library_path_in_training(ops):
     res = []
     old = os.environ.get("DCR_DEBUG")
     try:
+        # (persist_min_t: keep the step off the persistent H = 2048 kernels, which T = 8
+        # would otherwise take -- tests/test_persist_nt.py covers those)
         for dbg in ("bigstep=2", "bigstep=0"):
-            os.environ["DCR_DEBUG"] = dbg
+            os.environ["DCR_DEBUG"] = dbg + ",persist_min_t=100000"
             m = CharRNN(cfg, device="cuda:0", seed=0)
             loss, _, _ = m.train_step(x, y, m.zero_state(B))
             torch.cuda.synchronize()
