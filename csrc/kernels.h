@@ -170,6 +170,7 @@ struct PersistArgs {
   unsigned spin_limit;
   int excl;              // bwd: all-loads-in-flight variant (one WG per CU: nothing may run beside it)
   int cnt_zeroed;        // counters already zeroed by the caller (batched prep launch)
+  int poller;            // H > 1024 kernels: thread that polls the hand-off counters (launcher)
   bf16* hring;           // fwd: [2, B, H] fragment-tiled h hand-off ring
   bf16* zring;           // bwd: [2, B, 4H] fragment-tiled dZ hand-off ring
                          //   (persist_common.h frag_index); dz stays row-major for the GEMMs

@@ -28,6 +28,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "persist_common.h"
+#include "debug_env.h"
 
 namespace dcr {
 
@@ -523,7 +524,10 @@ static int launch_persist(int bwd, const PersistArgs& a, int flags, int cus, hip
     return -2;
   if (!a.cnt_zeroed)
     (void)hipMemsetAsync(a.cnt, 0, sizeof(unsigned) * (size_t)((a.B + 15) / 16) * (a.T + 1) * 4, s);
-  void* args[] = {const_cast<PersistArgs*>(&a)};
+  PersistArgs b = a;
+  // H > 1024: the poller lane's wave (DCR_DEBUG=nt_poll=w; default wave 0, an epilogue wave)
+  b.poller = a.H > 1024 ? 64 * (debug_int("nt_poll", 0) & 3) : 0;
+  void* args[] = {&b};
   return hipLaunchKernel(fn, dim3(grid), dim3(256), args, lds, s) == hipSuccess ? 0 : -3;
 }
 

@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_nt_kernel(PersistArgs
       for (int g = 0; g < 4; ++g) ld4f(zrow + (size_t)g * H + u0, zx[g]);
     }
     if (t > 0) {
-      if (threadIdx.x == kLstmPollerThread && !dead)
+      if ((int)threadIdx.x == a.poller && !dead)
         dead = !poll_shards4(cnt + (size_t)t * 4, target, a.spin_limit, a.err, 1u);
     }
     __syncthreads();
@@ -226,7 +226,7 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_nt_kernel(PersistArgs
       ld4f(a.dtop + (size_t)t * B * H + bh, dtop);
     }
     if (t < T - 1) {
-      if (threadIdx.x == kLstmPollerThread && !dead)
+      if ((int)threadIdx.x == a.poller && !dead)
         dead = !poll_shards4(cnt + (size_t)(t + 1) * 4, target, a.spin_limit, a.err, 2u);
       __syncthreads();
       const __amdgpu_buffer_rsrc_t zsrc =
