@@ -73,6 +73,13 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_nt_kernel(PersistArgs
   const size_t bh = (size_t)b * H + u0;
   float c[4] = {0.f, 0.f, 0.f, 0.f};
   if (live) ld4f(a.cbuf + bh, c);
+  // input bias added here when the dense zx was written without it (the library GEMM with a
+  // bias ran as a separate 1 GB fp32 broadcast pass, 155 us per layer at B = 64)
+  float bx[4][4] = {};
+  if (epi && a.bias) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) ld4f(a.bias + (size_t)g * H + u0, bx[g]);
+  }
   __syncthreads();  // arr
 
   for (int t = 0; t < T; ++t) {
@@ -130,10 +137,10 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_nt_kernel(PersistArgs
         const float4 s1 = *reinterpret_cast<const float4*>(&part[1][w][g][lane][0]);
         const float4 s2 = *reinterpret_cast<const float4*>(&part[2][w][g][lane][0]);
         const float4 s3 = *reinterpret_cast<const float4*>(&part[3][w][g][lane][0]);
-        z[g][0] = s0.x + s1.x + s2.x + s3.x + zx[g][0];
-        z[g][1] = s0.y + s1.y + s2.y + s3.y + zx[g][1];
-        z[g][2] = s0.z + s1.z + s2.z + s3.z + zx[g][2];
-        z[g][3] = s0.w + s1.w + s2.w + s3.w + zx[g][3];
+        z[g][0] = s0.x + s1.x + s2.x + s3.x + (zx[g][0] + bx[g][0]);
+        z[g][1] = s0.y + s1.y + s2.y + s3.y + (zx[g][1] + bx[g][1]);
+        z[g][2] = s0.z + s1.z + s2.z + s3.z + (zx[g][2] + bx[g][2]);
+        z[g][3] = s0.w + s1.w + s2.w + s3.w + (zx[g][3] + bx[g][3]);
       }
       float gi[4], gj[4], gf[4], go[4], h[4];
 #pragma unroll

@@ -658,6 +658,11 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
   } else {
     TORCH_CHECK(zx.numel() == (int64_t)T * B * 4 * H, "zx must be [T, B, 4H]");
   }
+  if (!xfuse && has(bias)) {  // input bias added in the cell epilogue (H > 1024 kernels)
+    TORCH_CHECK(H > 1024, "an in-kernel input bias without the fused projection needs H > 1024");
+    check_seq(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() == 4 * H, "bias must be [4H]");
+  }
   if (has(gates)) TORCH_CHECK(gates->numel() == (int64_t)T * B * 4 * H, "gates must be [T, B, 4H]");
   TORCH_CHECK(cnt.numel() >= (int64_t)((B + 15) / 16) * (T + 1) * 4, "counter buffer too small");
   dcr::PersistArgs a{};
@@ -677,8 +682,8 @@ void lstm_persist_fwd(const at::Tensor& WT, const at::Tensor& zx, const c10::opt
   if (xfuse) {
     a.Wx = optr<bf16>(WxT);
     a.xin = optr<bf16>(xin);
-    a.bias = optr<float>(bias);
   }
+  a.bias = optr<float>(bias);
   if (has(diag)) {
     TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)T * 8, "diag must hold [T, 8] int64");
     a.diag = reinterpret_cast<unsigned long long*>(diag->data_ptr());

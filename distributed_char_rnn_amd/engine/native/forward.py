@@ -155,7 +155,8 @@ class ForwardMixin:
                     # epilogue: the library GEMM with a bias ran as GEMM + a separate [N, GW]
                     # fp32 add pass (41 us / 114 us per layer in the dropout headline / GRU-1024
                     # B = 256 profiles)
-                    bias_in_kernel = ((P.pair and layer + 1 < self.L) or P.gru_persist)
+                    bias_in_kernel = ((P.pair and layer + 1 < self.L) or P.gru_persist
+                                      or (P.persist and H > 1024))
                     mm_into(lb.x_in, lw.Wx, lb.zx.view(N, self.GW),
                             bias=None if bias_in_kernel else lw.bias)
                     zx = lb.zx
@@ -186,7 +187,8 @@ class ForwardMixin:
                 self.ops.lstm_persist_fwd(lw.WhT, zx, ids_arg, lb.hbuf, lb.cbuf, lb.gates,
                                           lb.hlast32, bufs["cnt"][layer], self.err, FORGET_BIAS,
                                           self.spin_limit, bufs["hrings"][0], cnt_zeroed=True,
-                                          clast32=lb.clast32)
+                                          clast32=lb.clast32,
+                                          bias=lw.bias if (ids_arg is None and H > 1024) else None)
             elif P.gru_persist:
                 gr = bufs["grings"]
                 self.ops.gru_persist_fwd(lw.WhT, lw.WT2, zx, ids_arg, lb.hbuf, lb.h32, lb.rh,

@@ -42,6 +42,13 @@ def test_nt_kernels_match_oracle(B, T, L, nt_bwd, dcr_ops, monkeypatch):
     assert nt in (1, 2)
     cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=L)
     nat = CharRNN(cfg, device="cuda", seed=5)
+    # non-zero biases (TF initialises them to zero): the upper layers' input bias is added in
+    # the persistent forward's epilogue, not by the input GEMM
+    gb = torch.Generator().manual_seed(7)
+    for sp in nat.store.specs:
+        if sp.name.endswith("bias"):
+            nat.store.view(sp.name).copy_(torch.randn(sp.shape, generator=gb) * 0.3)
+    nat.params_changed()
     P = nat.backend._persist_plan(B, True, T)
     assert P.persist and not P.pair and P.persist_bwd == bool(nt_bwd)
     x, y, st0 = _batch(B, T, H, L, B)
