@@ -79,6 +79,7 @@ struct LstmEwArgs {
   const float* zrec;       // recurrent pre-activation slabs
   const float* zx;         // [B, 4H] input projection + bias, or the [V, 4H] table with ids
   const int* ids;          // [B] or nullptr
+  const float* bias;       // optional [4H]: input bias not folded into a dense zx
   const float* cprev;      // [B, H]
   bf16* hout;              // [B, H]
   float* hout32;           // optional [B, H]

@@ -41,6 +41,13 @@ __global__ void __launch_bounds__(kEwThreads) lstm_ew_fwd_kernel(LstmEwArgs a) {
     const float4 v = ew_ld4(zx + (size_t)g * H + u);
     z[g][0] = v.x; z[g][1] = v.y; z[g][2] = v.z; z[g][3] = v.w;
   }
+  if (a.bias) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 v = ew_ld4(a.bias + (size_t)g * H + u);
+      z[g][0] += v.x; z[g][1] += v.y; z[g][2] += v.z; z[g][3] += v.w;
+    }
+  }
   for (int s = 0; s < a.nsplit; ++s) {
     const float* zr = a.zrec + ((size_t)s * a.B + b) * G + u;
 #pragma unroll

@@ -365,6 +365,10 @@ __global__ void __launch_bounds__(C::NW * 64, 1) lstm_gemm_step_kernel(BigStepAr
           const float4 v = bs_ld4f(zrow + (size_t)g * H + u);
           const f32x4 c4 = red[g * C::UFW + uf][r];
           z[g][0] = c4[0] + v.x; z[g][1] = c4[1] + v.y; z[g][2] = c4[2] + v.z; z[g][3] = c4[3] + v.w;
+          if (e.bias) {
+            const float4 bv = bs_ld4f(e.bias + (size_t)g * H + u);
+            z[g][0] += bv.x; z[g][1] += bv.y; z[g][2] += bv.z; z[g][3] += bv.w;
+          }
         }
         const float4 cpv = bs_ld4f(e.cprev + bh);
         const float cp[4] = {cpv.x, cpv.y, cpv.z, cpv.w};

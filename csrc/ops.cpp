@@ -195,7 +195,8 @@ void rnn_fwd_seq(int64_t cell, const at::Tensor& WT, const c10::optional<at::Ten
 void lstm_step_ew_fwd(const at::Tensor& zrec, const at::Tensor& zx,
                       const c10::optional<at::Tensor>& ids, const at::Tensor& cprev,
                       at::Tensor& hout, const c10::optional<at::Tensor>& hout32, at::Tensor& cout,
-                      at::Tensor& gates, double forget_bias) {
+                      at::Tensor& gates, double forget_bias,
+                      const c10::optional<at::Tensor>& bias) {
   check_seq(zrec, at::kFloat, "zrec");
   check_seq(zx, at::kFloat, "zx");
   check_seq(cprev, at::kFloat, "cprev");
@@ -222,6 +223,11 @@ void lstm_step_ew_fwd(const at::Tensor& zrec, const at::Tensor& zx,
   a.zrec = ptr<float>(zrec);
   a.zx = ptr<float>(zx);
   a.ids = has(ids) ? ptr<int>(*ids) : nullptr;
+  if (has(bias)) {
+    check_seq(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() == 4 * H, "bias must be [4H]");
+    a.bias = ptr<float>(*bias);
+  }
   a.cprev = ptr<float>(cprev);
   a.hout = ptr<bf16>(hout);
   a.hout32 = optr<float>(hout32);
@@ -284,7 +290,8 @@ int64_t lstm_big_step_fwd(const at::Tensor& WhT, const at::Tensor& hprev, const 
                           const c10::optional<at::Tensor>& ids, const at::Tensor& cprev,
                           at::Tensor& hout, const c10::optional<at::Tensor>& hout32,
                           at::Tensor& cout, at::Tensor& gates, at::Tensor& ws, at::Tensor& cnt,
-                          double forget_bias, int64_t force_S) {
+                          double forget_bias, int64_t force_S,
+                          const c10::optional<at::Tensor>& bias) {
   check_seq(WhT, at::kBFloat16, "WhT");
   check_seq(hprev, at::kBFloat16, "hprev");
   check_seq(zx, at::kFloat, "zx");
@@ -318,6 +325,11 @@ int64_t lstm_big_step_fwd(const at::Tensor& WhT, const at::Tensor& hprev, const 
   a.ew.H = H;
   a.ew.forget_bias = (float)forget_bias;
   a.ew.zx = ptr<float>(zx);
+  if (has(bias)) {
+    check_seq(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() == 4 * H, "bias must be [4H]");
+    a.ew.bias = ptr<float>(*bias);
+  }
   a.ew.ids = has(ids) ? ptr<int>(*ids) : nullptr;
   a.ew.cprev = ptr<float>(cprev);
   a.ew.hout = ptr<bf16>(hout);
@@ -1398,14 +1410,15 @@ TORCH_LIBRARY(dcr, m) {
   m.def("sumsq(Tensor x, Tensor(a!) partials, Tensor(b!) out, Tensor(c!)? ticket=None) -> ()");
   m.def(
       "lstm_step_ew_fwd(Tensor zrec, Tensor zx, Tensor? ids, Tensor cprev, Tensor(a!) hout, "
-      "Tensor(b!)? hout32, Tensor(c!) cout, Tensor(d!) gates, float forget_bias) -> ()");
+      "Tensor(b!)? hout32, Tensor(c!) cout, Tensor(d!) gates, float forget_bias, "
+      "Tensor? bias=None) -> ()");
   m.def(
       "lstm_step_ew_bwd(Tensor dtop, Tensor? dhrec, Tensor gates, Tensor c, Tensor cprev, "
       "Tensor(a!) dc, Tensor(b!) dz_out) -> ()");
   m.def(
       "lstm_big_step_fwd(Tensor WhT, Tensor hprev, Tensor zx, Tensor? ids, Tensor cprev, "
       "Tensor(a!) hout, Tensor(b!)? hout32, Tensor(c!) cout, Tensor(d!) gates, Tensor(e!) ws, "
-      "Tensor(f!) cnt, float forget_bias, int force_S=0) -> int");
+      "Tensor(f!) cnt, float forget_bias, int force_S=0, Tensor? bias=None) -> int");
   m.def(
       "lstm_big_step_bwd(Tensor Wh, Tensor dznext, Tensor dtop, Tensor gates, Tensor c, "
       "Tensor cprev, Tensor(a!) dc, Tensor(b!) dz_out, Tensor(c!) ws, Tensor(d!) cnt, "

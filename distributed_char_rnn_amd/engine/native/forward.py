@@ -156,7 +156,8 @@ class ForwardMixin:
                     # fp32 add pass (41 us / 114 us per layer in the dropout headline / GRU-1024
                     # B = 256 profiles)
                     bias_in_kernel = ((P.pair and layer + 1 < self.L) or P.gru_persist
-                                      or (P.persist and H > 1024))
+                                      or (P.persist and H > 1024)
+                                      or (not P.persist and self._lib_step("fwd", B)))
                     mm_into(lb.x_in, lw.Wx, lb.zx.view(N, self.GW),
                             bias=None if bias_in_kernel else lw.bias)
                     zx = lb.zx
@@ -196,7 +197,8 @@ class ForwardMixin:
                                          self.spin_limit, cnt_zeroed=True, ring0=gr[0],
                                          ring1=gr[1], bias_x=lw.bias if ids_arg is None else None)
             elif self._lib_step("fwd", B):
-                self._lstm_fwd_lib(lw, lb, zx, ids_arg, bufs)
+                self._lstm_fwd_lib(lw, lb, zx, ids_arg, bufs,
+                                   bias=lw.bias if ids_arg is None else None)
             else:
                 self.ops.rnn_fwd_seq(self.cell, lw.WhT, lw.WT2, zx, ids_arg, lb.hbuf, lb.h32,
                                      lb.cbuf, lb.gates, lb.pre, lb.aux, lb.rh, lb.hlast32,

@@ -18,10 +18,11 @@ from .gemm import f32
 
 class LibStepMixin:
     def _lib_step(self, direction: str, B: int) -> bool:
-        """One launch per time step for LSTM with H > 1024 (no weights-resident kernel fits
-        there), both directions at every batch: at B = 64 the library-form forward also beats
-        the fused per-step kernels of rnn_step.hip (4-layer LSTM-2048, T = 512: 87.7 vs 92.4 ms
-        per training step, same box).  DCR_RECURRENCE=library forces this path for any H,
+        """One launch per time step for LSTM with H > 1024 where the persistent kernels of
+        lstm_persist_nt.hip do not apply (B > 64 at H = 2048, or T below the persistent
+        minimum), both directions: the library-form forward also beats the fused per-step
+        kernels of rnn_step.hip (4-layer LSTM-2048, T = 512, B = 64: 87.7 vs 92.4 ms per
+        training step, same box).  DCR_RECURRENCE=library forces this path for any H,
         =step disables it."""
         if self.cfg.model != "lstm" or self.knobs.recurrence == "step":
             return False
@@ -58,7 +59,10 @@ class LibStepMixin:
                                (B, S))
         return ent[0], ent[1], S
 
-    def _lstm_fwd_lib(self, lw, lb, zx, ids, bufs) -> None:
+    def _lstm_fwd_lib(self, lw, lb, zx, ids, bufs, bias=None) -> None:
+        """``bias``: the input bias, added by the cell epilogue when the dense ``zx`` was
+        written without it (a bias-initialised library GEMM output is a separate [T·B, 4H]
+        fp32 broadcast pass: 16 GB per layer for config 4 at B = 1024)."""
         T, B = lb.gates.shape[0], lb.gates.shape[1]
         if self._big_step_ok("fwd", B):
             ws, cnt, S = self._big_ws(bufs, False, B)
@@ -69,7 +73,7 @@ class LibStepMixin:
                         lw.WhT, lb.hbuf[t], zx if ids is not None else zx[t],
                         ids[t] if ids is not None else None, lb.cbuf[t], lb.hbuf[t + 1],
                         lb.hlast32 if t == T - 1 else None, lb.cbuf[t + 1], lb.gates[t], ws, cnt,
-                        FORGET_BIAS, S)
+                        FORGET_BIAS, S, bias)
         else:
             zrec = bufs.get("zrec")
             if zrec is None:
@@ -82,7 +86,7 @@ class LibStepMixin:
                     self.ops.lstm_step_ew_fwd(zrec, zx if ids is not None else zx[t],
                                               ids[t] if ids is not None else None, lb.cbuf[t],
                                               lb.hbuf[t + 1], lb.hlast32 if t == T - 1 else None,
-                                              lb.cbuf[t + 1], lb.gates[t], FORGET_BIAS)
+                                              lb.cbuf[t + 1], lb.gates[t], FORGET_BIAS, bias)
 
         self._run_lib_loop(bufs, ("fwd", id(lb)), body, zx, ids,
                            a_static=lb.zx is not None and zx.data_ptr() == lb.zx.data_ptr())

@@ -32,14 +32,20 @@ def _batch(B, T, H, L, seed):
     return x, y, st0
 
 
-@pytest.mark.parametrize("B,T,L,nt_bwd", [(64, 6, 2, 0), (20, 5, 1, 0), (64, 6, 2, 1),
-                                          (20, 5, 1, 1), (7, 4, 1, 1)])
-def test_nt_kernels_match_oracle(B, T, L, nt_bwd, dcr_ops, monkeypatch):
-    """Default: both directions persistent; nt_bwd=0: persistent forward, library BPTT steps."""
-    monkeypatch.setenv("DCR_DEBUG", f"persist_min_t=1,nt_bwd={nt_bwd}")
+@pytest.mark.parametrize("B,T,L,dbg", [(64, 6, 2, "nt_bwd=0"), (20, 5, 1, "nt_bwd=0"),
+                                       (64, 6, 2, "nt_bwd=1"), (20, 5, 1, "nt_bwd=1"),
+                                       (7, 4, 1, "nt_bwd=1"), (64, 6, 2, "lib"),
+                                       (96, 4, 2, "lib,bigstep=2")])
+def test_nt_kernels_match_oracle(B, T, L, dbg, dcr_ops, monkeypatch):
+    """Default: both directions persistent; nt_bwd=0: persistent forward, library BPTT steps;
+    lib: the per-step library / fused step kernels (the upper layer's input bias added by
+    their cell epilogues)."""
+    lib = dbg.startswith("lib")
+    monkeypatch.setenv("DCR_DEBUG", "persist_min_t=100000" + dbg[3:] if lib
+                       else f"persist_min_t=1,{dbg}")
     H = 2048
-    nt = int(dcr_ops.lstm_persist_nt_tiles(H, B))
-    assert nt in (1, 2)
+    if not lib:
+        assert int(dcr_ops.lstm_persist_nt_tiles(H, B)) in (1, 2)
     cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=L)
     nat = CharRNN(cfg, device="cuda", seed=5)
     # non-zero biases (TF initialises them to zero): the upper layers' input bias is added in
@@ -50,7 +56,8 @@ def test_nt_kernels_match_oracle(B, T, L, nt_bwd, dcr_ops, monkeypatch):
             nat.store.view(sp.name).copy_(torch.randn(sp.shape, generator=gb) * 0.3)
     nat.params_changed()
     P = nat.backend._persist_plan(B, True, T)
-    assert P.persist and not P.pair and P.persist_bwd == bool(nt_bwd)
+    assert not P.pair
+    assert P.persist == (not lib) and (lib or P.persist_bwd == (dbg == "nt_bwd=1"))
     x, y, st0 = _batch(B, T, H, L, B)
     ref = ReferenceBackend(nat.store)
     loss_r, st_r, _ = ref.train_step(x, y, [tuple(s.clone() for s in t) for t in st0])
