@@ -97,3 +97,26 @@ def test_nt_kernels_match_library_path(monkeypatch):
     for a1, a0 in zip(s1, s0):
         for t1, t0 in zip(a1, a0):
             assert rel(t1, t0) < 1e-2
+
+
+def test_nt_spin_timeout_drains_and_guards(monkeypatch):
+    """A forced hand-off timeout (DCR_SPIN_LIMIT=1) in the H = 2048 persistent kernels: every
+    workgroup still finishes (bounded polls, the grid drains), the error word is set, the
+    guarded optimizer leaves the weights unchanged and check_errors raises."""
+    from distributed_char_rnn_amd.engine.optim import TFAdam
+
+    monkeypatch.setenv("DCR_SPIN_LIMIT", "1")
+    B, T, H = 64, 32, 2048
+    cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=1)
+    m = CharRNN(cfg, device="cuda", seed=2)
+    assert m.backend._persist_plan(B, True, T).persist
+    opt = TFAdam(m.store, clip=5.0, guard=m.error_word())
+    x, y, _ = _batch(B, T, H, 1, 3)
+    p0 = m.store.flat.clone()
+    m.train_step(x, y, m.zero_state(B))
+    opt.step(2e-3)
+    torch.cuda.synchronize()
+    assert int(m.backend.err.item()) != 0, "the forced timeout did not trigger"
+    assert torch.equal(m.store.flat, p0)
+    with pytest.raises(RuntimeError, match="timed out"):
+        m.check_errors()
