@@ -6,7 +6,7 @@ from __future__ import annotations
 import torch
 
 from ...models.params import cell_specs
-from .gemm import SumQueue, f32, mm_into, mm_tn, put
+from .gemm import SumQueue, f32, mm_into, mm_tn, mm_tn_cols, put
 from .layouts import SEG_LDS_MAX_V
 
 
@@ -264,6 +264,12 @@ class BackwardMixin:
             else:
                 if lb.x_merged:  # written by the merged GEMM above
                     dWx = s.gview(names[0])[:H]
+                elif self.cfg.model == "gru" and self.knobs.on("gru_dwx"):
+                    # [H, 3H] split over the gates / candidate kernels by the flush's slab sums
+                    gk, _, ck, _ = names
+                    mm_tn_cols(lb.x_in, dZx, [(0, 2 * H, s.gview(gk)[:H]),
+                                              (2 * H, 3 * H, s.gview(ck)[:H])], q)
+                    dWx = None
                 else:
                     dWx = (mm_tn(lb.x_in, dZx, s.gview(names[0])[:H], q=q)
                            if self.cfg.model in ("lstm", "rnn") else mm_tn(lb.x_in, dZx))
@@ -397,8 +403,9 @@ class BackwardMixin:
         s, H = self.store, self.H
         if self.cfg.model == "gru":
             gk, gb, ck, cb = names
-            s.gview(gk)[:H].copy_(dWx[:, : 2 * H])
-            s.gview(ck)[:H].copy_(dWx[:, 2 * H:])
+            if dWx is not None:  # (None: written by mm_tn_cols's deferred slab sums)
+                s.gview(gk)[:H].copy_(dWx[:, : 2 * H])
+                s.gview(ck)[:H].copy_(dWx[:, 2 * H:])
             s.gview(gb).copy_(dbias[: 2 * H])
             s.gview(cb).copy_(dbias[2 * H:])
         elif self.cfg.model == "nas":

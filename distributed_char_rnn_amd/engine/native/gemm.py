@@ -150,6 +150,25 @@ def mm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
     return out
 
 
+def mm_tn_cols(a: torch.Tensor, b: torch.Tensor, outs, q: SumQueue) -> None:
+    """``aᵀ·b`` whose output columns go to several destinations: ``outs`` = [(c0, c1, out),
+    ...] takes columns [c0, c1) into ``out`` (the GRU's input-weight gradient [H, 3H] belongs
+    to two kernels: gates [:, :2H] and candidate [:, 2H:]).  One split-K GEMM; each
+    destination's slab sum is a task of the queue's flush -- no full-width temporary, sum and
+    copies."""
+    K, M = a.shape
+    S = split_k(K, M, b.shape[1])
+    if S == 1:
+        full = mm(a.t(), b)
+        for c0, c1, out in outs:
+            out.copy_(full[:, c0:c1])
+        return
+    part = torch.bmm(a.unflatten(0, (S, K // S)).transpose(1, 2), b.unflatten(0, (S, K // S)),
+                     out_dtype=f32)
+    for c0, c1, out in outs:
+        q.add_sum(part[:, :, c0:c1], out)
+
+
 def put(dst: torch.Tensor, src: torch.Tensor):
     """dst.copy_(src) unless src already is dst's memory (results written in place)."""
     if not (src.data_ptr() == dst.data_ptr() and src.shape == dst.shape

@@ -55,6 +55,7 @@ DEBUG_KEYS = {
     "xin": "1: in-kernel input projection of a dense layer-l input (G = 1 two-layer forward)",
     "pair_dw": "0: separate h buffers per layer of a wavefront pair (two weight GEMMs for the "
                "upper layer instead of one over the pair-interleaved h)",
+    "gru_dwx": "0: GRU input-weight gradient as one [H, 3H] temporary + sum + two copies",
     "head_lds": "0: fused head streams softmax_wᵀ from L2 instead of staging it in LDS (C++)",
     "nt_bwd": "0: H > 1024: persistent forward (csrc/lstm_persist_nt.hip) but library-GEMM "
               "BPTT steps",
