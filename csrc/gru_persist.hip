@@ -64,8 +64,15 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
   unsigned* cntR = a.cnt + cset + (size_t)bg * (T + 1) * 4;  // slot t: r⊙h_{t-1} published
   const unsigned target = (unsigned)(H / (64 * UB));  // workgroups per K-quarter shard
   __shared__ unsigned wg_cnt[2];  // LDS last-arriver counters (phase A / phase B)
+  __shared__ int loc_s;
   if (threadIdx.x < 2) wg_cnt[threadIdx.x] = 0;
-  __syncthreads();
+  // XCD-resident hand-offs (persist_common.h): exchange word in slot 0 of the h set (no counter
+  // there); local flags (value = published slot + 1 for r⊙h, slot for h) from dword 4 of each set
+  unsigned long long* const xw = reinterpret_cast<unsigned long long*>(cntH + 2);
+  const bool tryloc = a.xcdloc && T >= 16 && nwg_u <= 64;
+  if (tryloc && threadIdx.x == 0) xcd_publish(xw);
+  unsigned* const flH = cntH + 4;
+  unsigned* const flR = cntR + 4;
   bool dead = false;
 
   bf16x8 wg[UB][2][KS], wc[UB][KS];
@@ -79,6 +86,12 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
         wg[ui][g][s] = ld8(a.WgT + (size_t)(g * H + row) * H + kbase + s * 32 + kq);
       wc[ui][s] = ld8(a.WcT + (size_t)row * H + kbase + s * 32 + kq);
     }
+  if (threadIdx.x == 0) {
+    loc_s = tryloc ? xcd_decide(xw, (unsigned)nwg_u, a.spin_limit, a.err, 14u) : 0;
+    if (loc_s && ubk == 0) cntH[1] = 1u;  // (diagnostics: the column ran XCD-local)
+  }
+  __syncthreads();
+  const bool loc = __builtin_amdgcn_readfirstlane(loc_s) != 0;
 
   // MFMA operands: batch tile n's row-major offset (rows b0 + 16n + lane%16) / ring tile
   const unsigned hoff = (unsigned)(((size_t)(b0 + (lane & 15)) * H + kbase + kq) * sizeof(bf16));
@@ -111,8 +124,12 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
     }
     // ---- phase A: [r, u] from h_{t-1}
     if (t > 0) {
-      if (threadIdx.x == kPollerThread && !dead)
+      if (loc) {
+        if (w == kPollerThread / 64 && !dead)
+          dead = !poll_flags1(flH, nwg_u, (unsigned)t, a.spin_limit, a.err, 5u);
+      } else if (threadIdx.x == kPollerThread && !dead) {
         dead = !poll_shards4(cntH + (size_t)t * 4, target, a.spin_limit, a.err, 5u);
+      }
       __syncthreads();
     }
     {
@@ -160,12 +177,16 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
       }
       const float rh0 = rr[0] * hp[0], rh1 = rr[1] * hp[1], rh2 = rr[2] * hp[2], rh3 = rr[3] * hp[3];
       if (a.ring1)
-        st4bf_sc1(a.ring1 + (size_t)(t & 1) * Bp * H + frag_index(b, u0, H), rh0, rh1, rh2, rh3);
+        st4bf_ho(loc, a.ring1 + (size_t)(t & 1) * Bp * H + frag_index(b, u0, H), rh0, rh1, rh2, rh3);
       else
-        st4bf_sc1(a.rh + (size_t)t * B * H + bh, rh0, rh1, rh2, rh3);
+        st4bf_ho(loc, a.rh + (size_t)t * B * H + bh, rh0, rh1, rh2, rh3);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0)
-        wg_arrive(&wg_cnt[0], UB * NT, cntR + (size_t)t * 4 + (u0 / (H / 4)));
+      if (lane == 0) {
+        if (loc)
+          wg_arrive_flag(&wg_cnt[0], UB * NT, flR + ubk, (unsigned)t + 1u);
+        else
+          wg_arrive(&wg_cnt[0], UB * NT, cntR + (size_t)t * 4 + (u0 / (H / 4)));
+      }
       if (live) {
         if (a.ring1) st4bf(a.rh + (size_t)t * B * H + bh, rh0, rh1, rh2, rh3);
         bf16* gp = a.gates + ((size_t)t * B + b) * G3 + u0;
@@ -174,8 +195,12 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
       }
     }
     // ---- phase B: c~ from r⊙h_{t-1}
-    if (threadIdx.x == kPollerThread && !dead)
+    if (loc) {
+      if (w == kPollerThread / 64 && !dead)
+        dead = !poll_flags1(flR, nwg_u, (unsigned)t + 1u, a.spin_limit, a.err, 6u);
+    } else if (threadIdx.x == kPollerThread && !dead) {
       dead = !poll_shards4(cntR + (size_t)t * 4, target, a.spin_limit, a.err, 6u);
+    }
     __syncthreads();
     {
       const __amdgpu_buffer_rsrc_t src =
@@ -215,14 +240,18 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
       for (int r = 0; r < 4; ++r) h[r] = uu[r] * hp[r] + (1.f - uu[r]) * cc[r];
       const size_t o = (size_t)(t + 1) * B * H + bh;
       if (a.ring0)
-        st4bf_sc1(a.ring0 + (size_t)((t + 1) & 1) * Bp * H + frag_index(b, u0, H), h[0], h[1],
-                  h[2], h[3]);
+        st4bf_ho(loc, a.ring0 + (size_t)((t + 1) & 1) * Bp * H + frag_index(b, u0, H), h[0], h[1],
+                 h[2], h[3]);
       else
-        st4bf_sc1(a.hbuf + o, h[0], h[1], h[2], h[3]);
+        st4bf_ho(loc, a.hbuf + o, h[0], h[1], h[2], h[3]);
       if (t + 1 < T) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-          wg_arrive(&wg_cnt[1], UB * NT, cntH + (size_t)(t + 1) * 4 + (u0 / (H / 4)));
+        if (lane == 0) {
+          if (loc)
+            wg_arrive_flag(&wg_cnt[1], UB * NT, flH + ubk, (unsigned)t + 1u);
+          else
+            wg_arrive(&wg_cnt[1], UB * NT, cntH + (size_t)(t + 1) * 4 + (u0 / (H / 4)));
+        }
       }
       if (live) {
         if (a.ring0) st4bf(a.hbuf + o, h[0], h[1], h[2], h[3]);
@@ -263,8 +292,15 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
   unsigned* cntG = a.cnt + cset + (size_t)bg * (T + 1) * 4;  // slot t: dZg_t published
   const unsigned target = (unsigned)(H / (64 * UB));  // workgroups per K-quarter shard
   __shared__ unsigned wg_cnt[2];  // LDS last-arriver counters (phase A / phase B)
+  __shared__ int loc_s;
   if (threadIdx.x < 2) wg_cnt[threadIdx.x] = 0;
-  __syncthreads();
+  // XCD-resident hand-offs: exchange word in slot 0 of the dZg set (no counter there); local flag
+  // value = T - (published slot), monotonic over the reverse sweep
+  unsigned long long* const xw = reinterpret_cast<unsigned long long*>(cntG + 2);
+  const bool tryloc = a.xcdloc && T >= 16 && nwg_u <= 64;
+  if (tryloc && threadIdx.x == 0) xcd_publish(xw);
+  unsigned* const flC = cntC + 4;
+  unsigned* const flG = cntG + 4;
   const int G3 = 3 * H;
   bool dead = false;
 
@@ -277,6 +313,12 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
 #pragma unroll
     for (int s = 0; s < KB; ++s) wg[ui][s] = ld8(a.Wg + (size_t)row * 2 * H + kB + s * 32 + kq);
   }
+  if (threadIdx.x == 0) {
+    loc_s = tryloc ? xcd_decide(xw, (unsigned)nwg_u, a.spin_limit, a.err, 15u) : 0;
+    if (loc_s && ubk == 0) cntG[1] = 1u;  // (diagnostics: the column ran XCD-local)
+  }
+  __syncthreads();
+  const bool loc = __builtin_amdgcn_readfirstlane(loc_s) != 0;
 
   // epilogue role: unit block w % UB of batch tile w / UB
   const bool epi = w < UB * NT;
@@ -306,12 +348,17 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
     for (int r = 0; r < 4; ++r) z0[r] = dhp[r] * (1.f - uu[r]) * (1.f - cc[r] * cc[r]);
     bf16* const zrow = a.dz + ((size_t)(T - 1) * B + b) * G3 + 2 * H + u0;
     if (a.ring0)
-      st4bf_sc1(a.ring0 + (size_t)((T - 1) & 1) * Bp * H + frag_index(b, u0, H), z0[0], z0[1], z0[2], z0[3]);
+      st4bf_ho(loc, a.ring0 + (size_t)((T - 1) & 1) * Bp * H + frag_index(b, u0, H), z0[0], z0[1],
+               z0[2], z0[3]);
     else
-      st4bf_sc1(zrow, z0[0], z0[1], z0[2], z0[3]);
+      st4bf_ho(loc, zrow, z0[0], z0[1], z0[2], z0[3]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0)
-      wg_arrive(&wg_cnt[1], UB * NT, cntC + (size_t)(T - 1) * 4 + (u0 / (H / 4)));
+    if (lane == 0) {
+      if (loc)
+        wg_arrive_flag(&wg_cnt[1], UB * NT, flC + ubk, 1u);  // slot T-1
+      else
+        wg_arrive(&wg_cnt[1], UB * NT, cntC + (size_t)(T - 1) * 4 + (u0 / (H / 4)));
+    }
     if (a.ring0 && live) st4bf(zrow, z0[0], z0[1], z0[2], z0[3]);
   }
 
@@ -331,8 +378,12 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
     const __amdgpu_buffer_rsrc_t zsrc =
         make_rsrc(a.dz + (size_t)t * B * G3, sizeof(bf16) * (size_t)B * G3);
     // ---- phase A: d(r⊙h_{t-1}) = dZc_t · W_cᵀ
-    if (threadIdx.x == kPollerThread && !dead)
+    if (loc) {
+      if (w == kPollerThread / 64 && !dead)
+        dead = !poll_flags1(flC, nwg_u, (unsigned)(T - t), a.spin_limit, a.err, 7u);
+    } else if (threadIdx.x == kPollerThread && !dead) {
       dead = !poll_shards4(cntC + (size_t)t * 4, target, a.spin_limit, a.err, 7u);
+    }
     __syncthreads();
     {
       bf16x8 zf[NT][KA];
@@ -382,16 +433,20 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
       bf16* dz = a.dz + ((size_t)t * B + b) * G3 + u0;
       if (a.ring1) {
         bf16* gr = a.ring1 + (size_t)(t & 1) * Bp * 2 * H;
-        st4bf_sc1(gr + frag_index(b, u0, 2 * H), dzr[0], dzr[1], dzr[2], dzr[3]);
-        st4bf_sc1(gr + frag_index(b, H + u0, 2 * H), dzu[0], dzu[1], dzu[2], dzu[3]);
+        st4bf_ho(loc, gr + frag_index(b, u0, 2 * H), dzr[0], dzr[1], dzr[2], dzr[3]);
+        st4bf_ho(loc, gr + frag_index(b, H + u0, 2 * H), dzu[0], dzu[1], dzu[2], dzu[3]);
       } else {
-        st4bf_sc1(dz, dzr[0], dzr[1], dzr[2], dzr[3]);
-        st4bf_sc1(dz + H, dzu[0], dzu[1], dzu[2], dzu[3]);
+        st4bf_ho(loc, dz, dzr[0], dzr[1], dzr[2], dzr[3]);
+        st4bf_ho(loc, dz + H, dzu[0], dzu[1], dzu[2], dzu[3]);
       }
       if (t > 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-          wg_arrive(&wg_cnt[0], UB * NT, cntG + (size_t)t * 4 + (u0 / (H / 4)));
+        if (lane == 0) {
+          if (loc)
+            wg_arrive_flag(&wg_cnt[0], UB * NT, flG + ubk, (unsigned)(T - t));
+          else
+            wg_arrive(&wg_cnt[0], UB * NT, cntG + (size_t)t * 4 + (u0 / (H / 4)));
+        }
       }
       if (a.ring1 && live) {
         st4bf(dz, dzr[0], dzr[1], dzr[2], dzr[3]);
@@ -400,8 +455,12 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
     }
     if (t == 0) break;  // dh'_{-1} (the initial state's gradient) is not needed
     // ---- phase B: dh'_{t-1} = dtop_{t-1} + P + dZg_t · W_gᵀ
-    if (threadIdx.x == kPollerThread && !dead)
+    if (loc) {
+      if (w == kPollerThread / 64 && !dead)
+        dead = !poll_flags1(flG, nwg_u, (unsigned)(T - t), a.spin_limit, a.err, 8u);
+    } else if (threadIdx.x == kPollerThread && !dead) {
       dead = !poll_shards4(cntG + (size_t)t * 4, target, a.spin_limit, a.err, 8u);
+    }
     __syncthreads();
     {
       // one batch tile at a time: KB = 2 KA payload fragments per tile is the register limit
@@ -441,13 +500,17 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
       for (int r = 0; r < 4; ++r) dzc[r] = dhp[r] * (1.f - up[r]) * (1.f - cp[r] * cp[r]);
       bf16* const crow = a.dz + ((size_t)(t - 1) * B + b) * G3 + 2 * H + u0;
       if (a.ring0)
-        st4bf_sc1(a.ring0 + (size_t)((t - 1) & 1) * Bp * H + frag_index(b, u0, H), dzc[0], dzc[1],
-                  dzc[2], dzc[3]);
+        st4bf_ho(loc, a.ring0 + (size_t)((t - 1) & 1) * Bp * H + frag_index(b, u0, H), dzc[0],
+                 dzc[1], dzc[2], dzc[3]);
       else
-        st4bf_sc1(crow, dzc[0], dzc[1], dzc[2], dzc[3]);
+        st4bf_ho(loc, crow, dzc[0], dzc[1], dzc[2], dzc[3]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0)
-        wg_arrive(&wg_cnt[1], UB * NT, cntC + (size_t)(t - 1) * 4 + (u0 / (H / 4)));
+      if (lane == 0) {
+        if (loc)
+          wg_arrive_flag(&wg_cnt[1], UB * NT, flC + ubk, (unsigned)(T - t + 1));  // slot t-1
+        else
+          wg_arrive(&wg_cnt[1], UB * NT, cntC + (size_t)(t - 1) * 4 + (u0 / (H / 4)));
+      }
       if (a.ring0 && live) st4bf(crow, dzc[0], dzc[1], dzc[2], dzc[3]);
     }
   }

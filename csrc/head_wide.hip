@@ -30,6 +30,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "persist_common.h"
+#include "debug_env.h"
 
 namespace dcr {
 
@@ -409,13 +410,37 @@ int head_wide_supported(int V, int H) { return H == 512 && V >= 64 && V % 64 == 
 int launch_head_wide(const HeadWideArgs& a, float* db, float* loss_out, hipStream_t s) {
   if (!head_wide_supported(a.V, a.H) || a.N <= 0 || !a.stats) return -1;
   // 32-bit buffer offsets of the outputs, up to the last block's padded rows (which the range
-  // check drops)
+  // check drops).  Larger token counts run as chunks of whole 256-token blocks that each fit:
+  // every per-token / per-block output is offset to the chunk, each chunk keeps its own stats
+  // region ((2 kHwSplit + 1) floats per token, so the chunks tile head_wide_stats_floats(N)),
+  // and one finalize sums all blocks' partials.
   const int nb = head_wide_blocks(a.N);
-  const size_t rows = (size_t)nb * kHwTok;
-  if ((a.logits && rows * a.V * 4 >= (1ull << 32)) || (a.dlogits && rows * a.V * 2 >= (1ull << 32)))
-    return -2;
-  if (a.targets || a.dlogits) hipLaunchKernelGGL((head_wide_kernel<16, 1>), dim3(nb * kHwSplit), dim3(512), 0, s, a);
-  hipLaunchKernelGGL((head_wide_kernel<16, 2>), dim3(nb * kHwSplit), dim3(512), 0, s, a);
+  const size_t bpr = a.logits ? 4 * (size_t)a.V : a.dlogits ? 2 * (size_t)a.V : 0;  // bytes / row
+  int chunk_blocks = nb;
+  if (bpr) {
+    const size_t max_rows = ((1ull << 32) - 1) / bpr;
+    chunk_blocks = (int)(max_rows / kHwTok);
+    if (chunk_blocks < 1) return -2;
+  }
+  const int force = debug_int("hw_chunk", 0);  // (tests: chunking at small N)
+  if (force > 0 && force < chunk_blocks) chunk_blocks = force;
+  for (int b0 = 0; b0 < nb; b0 += chunk_blocks) {
+    const int cb = nb - b0 < chunk_blocks ? nb - b0 : chunk_blocks;
+    const size_t n0 = (size_t)b0 * kHwTok;
+    HeadWideArgs c = a;
+    c.N = (int)((size_t)a.N - n0 < (size_t)cb * kHwTok ? (size_t)a.N - n0 : (size_t)cb * kHwTok);
+    c.O = a.O + n0 * a.ldo;
+    if (a.targets) c.targets = a.targets + n0;
+    if (a.row_loss) c.row_loss = a.row_loss + n0;
+    if (a.dlogits) c.dlogits = a.dlogits + n0 * a.V;
+    if (a.logits) c.logits = a.logits + n0 * a.V;
+    if (a.colpart) c.colpart = a.colpart + (size_t)b0 * 8 * a.V;
+    if (a.partial) c.partial = a.partial + b0;
+    c.stats = a.stats + (size_t)(2 * kHwSplit + 1) * n0;
+    if (c.targets || c.dlogits)
+      hipLaunchKernelGGL((head_wide_kernel<16, 1>), dim3(cb * kHwSplit), dim3(512), 0, s, c);
+    hipLaunchKernelGGL((head_wide_kernel<16, 2>), dim3(cb * kHwSplit), dim3(512), 0, s, c);
+  }
   launch_xent_finalize(a.partial, nb, a.N, loss_out, a.dlogits ? a.colpart : nullptr, 8 * nb, a.V,
                        db, s);
   return 0;

@@ -258,6 +258,8 @@ struct Lstm2Args {
   int hld;              // row stride (elements) of hbuf0 / hbuf1: H, or 2H when both layers' h
                         //   live interleaved in one [T+2, B, 2H] buffer (row t+1 = [h_l(t),
                         //   h_l+1(t-1)]: the operand of layer l+1's merged weight gradient)
+  int xcdloc;           // 1: XCD-resident hand-offs for columns found on one XCD (persist_common.h;
+                        //   exchange word: dwords 2-3 of cnt0's slot 0 per column); 0: write-through
 };
 // batch groups per workgroup for the two-layer kernels at (H, B) (force > 0: only that value),
 // 0 = unsupported
@@ -289,6 +291,7 @@ struct Lstm2BwdArgs {
   int db_rows;          // rows of db_part0/1 (the wide kernel zeroes the ones past its columns)
   int wgarr;            // as Lstm2Args::wgarr
   int diag_all;         // diag holds [grid, T+2, 8] s_memrealtime stamps of every workgroup
+  int xcdloc;           // as Lstm2Args::xcdloc (exchange word: dwords 2-3 of cnt0's slot 0)
 };
 int launch_lstm2_bwd_persist(const Lstm2BwdArgs& a, int cus, hipStream_t s);
 // the 32-unit x 16-row form of the same BPTT (lstm2_bwd_wide.hip): nbg = ceil(B / 16) 16-row
@@ -320,6 +323,8 @@ struct GruPersistArgs {
   int B, H, T;
   unsigned spin_limit;
   int cnt_zeroed;
+  int xcdloc;           // as Lstm2Args::xcdloc (exchange word: dwords 2-3 of slot 0 of the fwd's
+                        //   h set / the bwd's dZg set, which no counter uses)
 };
 // token-reduction weight-gradient GEMM (wgrad.hip): C_s = A_chunkᵀ · B_chunk per split-K slab
 constexpr int kWgradMaxProblems = 4;

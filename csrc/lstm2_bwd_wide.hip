@@ -120,6 +120,12 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
   const int kq = 8 * (lane >> 4);
   unsigned* cnt0 = a.cnt0 + (size_t)col * (T + 1) * 4;
   unsigned* cnt1 = a.cnt1 + (size_t)col * (T + 1) * 4;
+  // XCD-resident hand-offs (persist_common.h): publish now, decide after the weight loads
+  unsigned long long* const xw = reinterpret_cast<unsigned long long*>(cnt0 + 2);
+  const bool tryloc = a.xcdloc && a.wgarr && T >= 8 && H / 32 <= 32;
+  if (tryloc && threadIdx.x == 0) xcd_publish(xw);
+  unsigned* const fl0 = cnt0 + 4;  // (local form) per-workgroup flags of layer l / l+1
+  unsigned* const fl1 = cnt1 + 4;
   // arrivals per (column, slot) and layer: H/32 unit blocks x (one per workgroup | 2 waves)
   const unsigned target = (unsigned)(a.wgarr ? H / 32 : H / 16);
   if (threadIdx.x < 2) arrl[threadIdx.x] = 0u;  // (ordered before any add by tick 0's barrier)
@@ -138,6 +144,13 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
       wh1[u][s] = ld8(a.Wh1 + row);
       wx1l[w][u][s][lane] = ld8(a.Wx1 + row);
     }
+  __shared__ int loc_s;
+  if (threadIdx.x == 0) {
+    loc_s = tryloc ? xcd_decide(xw, (unsigned)(H / 32), a.spin_limit, a.err, 13u) : 0;
+    if (loc_s && ubk == 0) cnt0[1] = 1u;  // (diagnostics: the column ran XCD-local)
+  }
+  __syncthreads();
+  const bool loc = __builtin_amdgcn_readfirstlane(loc_s) != 0;
 
   // epilogue role: layer L, unit half U
   const int L = w >> 1, U = w & 1;
@@ -219,7 +232,10 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
     if (PF == 0 || (PF == 1 && tau == 0) || (PF >= 2 && tau == 0 && !(PF == 4 && w == 0)))
       prefetch(tau);
     const int s1 = T - tau, s0 = T + 2 - tau;  // ring slots of dZ_{l+1} and dZ_l
-    if (tau >= 1) {
+    if (tau >= 1 && loc) {  // flags of both layers' producing tick (tau - 1) + 1
+      if (w == 0 && !dead && (ld1 || ld0))
+        dead = !poll_flags2(fl0, ld0, fl1, ld1, H / 32, (unsigned)tau, a.spin_limit, a.err, 10u);
+    } else if (tau >= 1) {
       if (threadIdx.x == kLstmPollerThread && !dead && (ld1 || ld0)) {
         dead = (ld1 && ld0)
                    ? !poll_counter2(cnt1 + (size_t)s1 * 4, target, cnt0 + (size_t)s0 * 4, target,
@@ -343,14 +359,16 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
       // layer l+1's dZ_t feeds both layers at the next tick (t >= 0); layer l's only itself
       if (L || t >= 1) {
         bf16* const zr = zrL + (size_t)(t & 1) * slabn;
-        st4bf_sc1(zr + frag_index(b, u0, G4H), di[0], di[1], di[2], di[3]);
-        st4bf_sc1(zr + frag_index(b, H + u0, G4H), dj[0], dj[1], dj[2], dj[3]);
-        st4bf_sc1(zr + frag_index(b, 2 * H + u0, G4H), df_[0], df_[1], df_[2], df_[3]);
-        st4bf_sc1(zr + frag_index(b, 3 * H + u0, G4H), dO[0], dO[1], dO[2], dO[3]);
+        st4bf_ho(loc, zr + frag_index(b, u0, G4H), di[0], di[1], di[2], di[3]);
+        st4bf_ho(loc, zr + frag_index(b, H + u0, G4H), dj[0], dj[1], dj[2], dj[3]);
+        st4bf_ho(loc, zr + frag_index(b, 2 * H + u0, G4H), df_[0], df_[1], df_[2], df_[3]);
+        st4bf_ho(loc, zr + frag_index(b, 3 * H + u0, G4H), dO[0], dO[1], dO[2], dO[3]);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         STAMP_ARRIVE()
         if (lane == 0) {
-          if (a.wgarr)
+          if (loc)
+            wg_arrive_flag(&arrl[L], 2u, (L ? fl1 : fl0) + ubk, (unsigned)tau + 1u);
+          else if (a.wgarr)
             wg_arrive(&arrl[L], 2u, cntL + (size_t)t * 4);
           else
             __hip_atomic_fetch_add(cntL + (size_t)t * 4, 1u, __ATOMIC_RELAXED,

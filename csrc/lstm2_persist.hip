@@ -88,9 +88,17 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
   const int kbase = w * (KS * 32);
   unsigned* const cnt0 = a.cnt0 + (size_t)col * (T + 1) * 4;
   unsigned* const cnt1 = a.cnt1 + (size_t)col * (T + 1) * 4;
+  // XCD-resident hand-offs (persist_common.h): publish this workgroup's XCD now, decide after
+  // the weight loads (the exchange's round trip overlaps them)
+  unsigned long long* const xw = reinterpret_cast<unsigned long long*>(cnt0 + 2);
+  const bool tryloc = a.xcdloc && a.wgarr && T >= 8 && nwg_u <= 32;
+  if (tryloc && threadIdx.x == 0) xcd_publish(xw);
+  unsigned* const fl0 = cnt0 + 4;  // (local form) per-workgroup flags of layer l / l+1
+  unsigned* const fl1 = cnt1 + 4;
   // arrivals per (column, slot) and layer: H/16 unit blocks x (one per workgroup | 2 waves)
   const unsigned target = (unsigned)(a.wgarr ? H / 16 : H / 8);
   __shared__ unsigned arrl[2];  // per-layer arrivals of the tick (wgarr)
+  __shared__ int loc_s;
   if (threadIdx.x < 2) arrl[threadIdx.x] = 0u;  // (ordered before any add by tick 0's barrier)
   const size_t ringsz = (size_t)a.nbg * 32 * H;  // one ring slot (padded batch)
   bool dead = false;
@@ -117,6 +125,12 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
       x1[gt][s] = ld8(a.X1T + row);
       if constexpr (XIN) wx0l[w][gt][s][lane] = ld8(a.X0T + row);
     }
+  if (threadIdx.x == 0) {
+    loc_s = tryloc ? xcd_decide(xw, (unsigned)nwg_u, a.spin_limit, a.err, 11u) : 0;
+    if (loc_s && ubk == 0) cnt0[1] = 1u;  // (diagnostics: the column ran XCD-local)
+  }
+  __syncthreads();
+  const bool loc = __builtin_amdgcn_readfirstlane(loc_s) != 0;
 
   // epilogue role: layer L, batch tile J of every group
   const int L = w >> 1, J = w & 1;
@@ -254,7 +268,10 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     // hand-offs of the previous tick: layer l's slot tau, layer l+1's slot tau-LAG (slot 0 of
     // either is the prep-written initial state)
     const bool pw0 = ld0 && tau >= 1, pw1 = ld1 && tau >= LAG + 1;
-    if ((pw0 || pw1) && threadIdx.x == kLstmPollerThread && !dead) {
+    if (loc) {  // flags of both layers' producing ticks (tau - 1) + 1
+      if ((pw0 || pw1) && w == 0 && !dead)
+        dead = !poll_flags2(fl0, pw0, fl1, pw1, nwg_u, (unsigned)tau, a.spin_limit, a.err, 9u);
+    } else if ((pw0 || pw1) && threadIdx.x == kLstmPollerThread && !dead) {
       dead = (pw0 && pw1) ? !poll_counter2(cnt0 + (size_t)tau * 4, target,
                                            cnt1 + (size_t)(tau - LAG) * 4, target, a.spin_limit,
                                            a.err, 9u)
@@ -460,8 +477,8 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
           h[r] = go[r] * tanhf_(c[g][r]);
         }
         STAMPG(g, 5)
-        st4bf_sc1(ringL + (size_t)((t + 1) & 1) * ringsz + frag_index(b, u0, H), h[0], h[1], h[2],
-                  h[3]);
+        st4bf_ho(loc, ringL + (size_t)((t + 1) & 1) * ringsz + frag_index(b, u0, H), h[0], h[1],
+                 h[2], h[3]);
         // the stash MFMAs run while the ring stores drain; with dropout (LDS mask reads and
         // fragment masking) the stash outlasts the drain, so it follows the arrival instead
         if (!xdrop) do_stash();
@@ -471,7 +488,9 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
           STAMPG(g, 6)
           if (lane == 0) {
             unsigned* const c = (L ? cnt1 : cnt0) + (size_t)(t + 1) * 4;
-            if (a.wgarr)
+            if (loc)
+              wg_arrive_flag(&arrl[L], 2u, (L ? fl1 : fl0) + ubk, (unsigned)tau + 1u);
+            else if (a.wgarr)
               wg_arrive(&arrl[L], 2u, c);
             else
               __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -544,9 +563,15 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
   const int kq = 8 * (lane >> 4);
   unsigned* cnt0 = a.cnt0 + (size_t)col * (T + 1) * 4;
   unsigned* cnt1 = a.cnt1 + (size_t)col * (T + 1) * 4;
+  unsigned long long* const xw = reinterpret_cast<unsigned long long*>(cnt0 + 2);
+  const bool tryloc = a.xcdloc && a.wgarr && T >= 8 && H / 16 <= 32;
+  if (tryloc && threadIdx.x == 0) xcd_publish(xw);
+  unsigned* const fl0 = cnt0 + 4;  // (local form) per-workgroup flags of layer l / l+1
+  unsigned* const fl1 = cnt1 + 4;
   // arrivals per (column, slot) and layer: H/16 unit blocks x (one per workgroup | 2 waves)
   const unsigned target = (unsigned)(a.wgarr ? H / 16 : H / 8);
   __shared__ unsigned arrl[2];  // per-layer arrivals of the tick (wgarr)
+  __shared__ int loc_s;
   if (threadIdx.x < 2) arrl[threadIdx.x] = 0u;  // (ordered before any add by tick 0's barrier)
   const size_t slabn = (size_t)a.nbg * 32 * G4H;  // one ring slot (padded batch), elements
   bool dead = false;
@@ -561,6 +586,12 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
     wh1[s] = ld8(a.Wh1 + row);
     wx1l[w][s][lane] = ld8(a.Wx1 + row);  // read back only by this wave
   }
+  if (threadIdx.x == 0) {
+    loc_s = tryloc ? xcd_decide(xw, (unsigned)(H / 16), a.spin_limit, a.err, 12u) : 0;
+    if (loc_s && ubk == 0) cnt0[1] = 1u;  // (diagnostics: the column ran XCD-local)
+  }
+  __syncthreads();
+  const bool loc = __builtin_amdgcn_readfirstlane(loc_s) != 0;
 
   // epilogue role: layer L, batch tile J of every group
   const int L = w >> 1, J = w & 1;
@@ -660,15 +691,17 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
         // layer l+1's dZ_t feeds both layers at the next tick (t >= 0); layer l's only itself
         if (L || t >= 1) {
           bf16* const zr = zrL + (size_t)(t & 1) * slabn;
-          st4bf_sc1(zr + frag_index(b, u0, G4H), di[0], di[1], di[2], di[3]);
-          st4bf_sc1(zr + frag_index(b, H + u0, G4H), dj[0], dj[1], dj[2], dj[3]);
-          st4bf_sc1(zr + frag_index(b, 2 * H + u0, G4H), df_[0], df_[1], df_[2], df_[3]);
-          st4bf_sc1(zr + frag_index(b, 3 * H + u0, G4H), dO[0], dO[1], dO[2], dO[3]);
+          st4bf_ho(loc, zr + frag_index(b, u0, G4H), di[0], di[1], di[2], di[3]);
+          st4bf_ho(loc, zr + frag_index(b, H + u0, G4H), dj[0], dj[1], dj[2], dj[3]);
+          st4bf_ho(loc, zr + frag_index(b, 2 * H + u0, G4H), df_[0], df_[1], df_[2], df_[3]);
+          st4bf_ho(loc, zr + frag_index(b, 3 * H + u0, G4H), dO[0], dO[1], dO[2], dO[3]);
           if (g == G - 1) {  // one arrival per wave and tick, for all its groups' ring stores
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             STAMPG(g, 6)
             if (lane == 0) {
-              if (a.wgarr)
+              if (loc)
+                wg_arrive_flag(&arrl[L], 2u, (L ? fl1 : fl0) + ubk, (unsigned)tau + 1u);
+              else if (a.wgarr)
                 wg_arrive(&arrl[L], 2u, cntL + (size_t)t * 4);
               else
                 __hip_atomic_fetch_add(cntL + (size_t)t * 4, 1u, __ATOMIC_RELAXED,
@@ -699,7 +732,11 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
         bf16x8 p1[2][KS];
         const int s1 = T - tau, s0 = T + 2 - tau;  // ring slots of dZ_{l+1} and dZ_l
         if (g == 0) {  // the column's hand-off of the previous tick, for all groups
-          if (threadIdx.x == kLstmPollerThread && !dead && (ld1 || ld0)) {
+          if (loc) {  // flags of both layers' producing tick (tau - 1) + 1
+            if (w == 0 && !dead && (ld1 || ld0))
+              dead = !poll_flags2(fl0, ld0, fl1, ld1, H / 16, (unsigned)tau, a.spin_limit, a.err,
+                                  10u);
+          } else if (threadIdx.x == kLstmPollerThread && !dead && (ld1 || ld0)) {
             dead = (ld1 && ld0)
                        ? !poll_counter2(cnt1 + (size_t)s1 * 4, target, cnt0 + (size_t)s0 * 4,
                                         target, a.spin_limit, a.err, 10u)

@@ -953,6 +953,7 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
   a.forget_bias = (float)forget_bias;
   a.spin_limit = (unsigned)spin_limit;
   a.wgarr = dcr::debug_int("wgarr", 1);  // one hand-off add per workgroup and layer
+  a.xcdloc = dcr::debug_int("xcdloc", 1);  // XCD-resident hand-offs where placement allows
   if (has(diag)) {
     TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)(T + 2) * G * 8,
                 "diag must hold [T+2, G, 8] int64 (ticks 0..T+1)");
@@ -1023,6 +1024,7 @@ void lstm2_persist_bwd(const at::Tensor& Wh0, const at::Tensor& Wh1, const at::T
   a.B = B; a.H = H; a.T = T; a.G = (int)G; a.nbg = nbg;
   a.spin_limit = (unsigned)spin_limit;
   a.wgarr = dcr::debug_int("wgarr", 1);  // one hand-off add per workgroup and layer
+  a.xcdloc = dcr::debug_int("xcdloc", 1);  // XCD-resident hand-offs where placement allows
   if (has(diag)) {
     TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)(T + 2) * G * 8,
                 "diag must hold [T+2, G, 8] int64 (ticks 0..T+1)");
@@ -1117,6 +1119,7 @@ static void gru_common(dcr::GruPersistArgs& a, const at::Tensor& gates, const at
   a.B = B; a.H = H; a.T = T;
   a.spin_limit = (unsigned)spin_limit;
   a.cnt_zeroed = cnt_zeroed ? 1 : 0;
+  a.xcdloc = dcr::debug_int("xcdloc", 1);  // XCD-resident hand-offs where placement allows
 }
 
 void gru_persist_fwd(const at::Tensor& WgT, const at::Tensor& WcT, const at::Tensor& zx,

@@ -41,6 +41,112 @@ __device__ __forceinline__ void st4bf(bf16* p, float a, float b, float c, float 
   v[0] = f2bf(a); v[1] = f2bf(b); v[2] = f2bf(c); v[3] = f2bf(d);
   *reinterpret_cast<bf16x4*>(p) = v;
 }
+
+// ---- XCD-resident hand-offs ------------------------------------------------------------------
+// A batch column's hand-off (its producers and consumers are the same workgroup set) can keep its
+// lines in ONE XCD's L2 when every workgroup of the column runs on that XCD: the payload is then
+// stored PLAIN (the line stays in the producer XCD's L2; an sc1 store writes through and DROPS
+// it, so a same-XCD reader pays the fabric round trip: MI355X_MICROARCH.md, "stores of each
+// flavour"), still drained with vmcnt(0) before the counter add; consumers keep sc1 loads (L1
+// bypass, L2-served) after the poll.  HIP promises no placement, so it is checked in-kernel: each
+// workgroup adds 1 << (8 XCC_ID) to its column's 8-B exchange word (zeroed with the counters)
+// and waits until all nwg (<= 255) have; the column runs local only if one byte holds them all,
+// otherwise it keeps the write-through protocol above.  Every workgroup of a column reads the
+// same final word, so producers and consumers agree.  Validated by scripts/micro/handoff_xcd.hip
+// (tagged lines, uneven load) and bitwise against the write-through protocol
+// (tests/test_handoff_local.py).
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & 7u;
+}
+__device__ __forceinline__ void xcd_publish(unsigned long long* word) {
+  __hip_atomic_fetch_add(word, 1ull << (8 * xcc_id()), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// (one lane) 1: all nwg workgroups of the column share one XCD; 0: not, or timed out (error
+// word set, the caller keeps going so the grid drains)
+__device__ __forceinline__ int xcd_decide(unsigned long long* word, unsigned nwg, unsigned limit,
+                                          unsigned* err, unsigned code) {
+  unsigned spins = 0;
+  for (;;) {
+    const unsigned long long m = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned tot = 0;
+    int one = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const unsigned c = (unsigned)(m >> (8 * i)) & 0xFFu;
+      tot += c;
+      one |= c == nwg;
+    }
+    if (tot >= nwg) return one;
+    if (++spins > limit) {
+      __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return 0;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+// The local form's signal is not an atomic counter (agent-scope atomics are performed at the
+// memory side and drop the line: ~1.5 us of a 3.1 us tick in scripts/micro/handoff_xcd.hip) but
+// one flag dword per producing workgroup and layer, stored plain (L2-resident) by the LAST of the
+// workgroup's storing waves (LDS counter, every storing wave drained first): value = producing
+// tick + 1, monotonic.  One consumer wave polls all flags of both layers with ONE sc1 dword
+// load per lane (lanes [0, n): layer l, [32, 32 + n): layer l+1) and a wave vote: 1.35 vs 3.11 us
+// per tick in the micro-benchmark, no stale tag over 48k checked column-ticks.  The flags live
+// in the (then unused) counter slots 1-8 of each layer's column region (needs T >= 8, n <= 32).
+__device__ __forceinline__ void wg_arrive_flag(unsigned* lds_cnt, unsigned nwaves, unsigned* flag,
+                                               unsigned value) {
+  const unsigned old = __hip_atomic_fetch_add(lds_cnt, 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (old == nwaves - 1) {
+    __hip_atomic_store(lds_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // plain
+  }
+}
+// (a whole wave) wait until the n flags of each needed layer are >= target; false on timeout
+// (error word set)
+__device__ __forceinline__ bool poll_flags2(const unsigned* f0, bool need0, const unsigned* f1,
+                                            bool need1, int n, unsigned target, unsigned limit,
+                                            unsigned* err, unsigned code) {
+  const int lane = threadIdx.x & 63, i = lane & 31;
+  const bool hi = lane >= 32;
+  const bool watch = i < n && (hi ? need1 : need0);
+  const unsigned* p = (hi ? f1 : f0) + (i < n ? i : 0);
+  unsigned spins = 0;
+  for (;;) {
+    const unsigned v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__all(!watch || v >= target)) return true;
+    if (++spins > limit) {
+      if (lane == 0) __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+// (a whole wave) the same for one set of n <= 64 flags (lane i watches flag i)
+__device__ __forceinline__ bool poll_flags1(const unsigned* f, int n, unsigned target,
+                                            unsigned limit, unsigned* err, unsigned code) {
+  const int lane = threadIdx.x & 63;
+  const bool watch = lane < n;
+  const unsigned* p = f + (watch ? lane : 0);
+  unsigned spins = 0;
+  for (;;) {
+    const unsigned v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__all(!watch || v >= target)) return true;
+    if (++spins > limit) {
+      if (lane == 0) __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+// a hand-off payload store: plain when the column is XCD-local, write-through (sc1) otherwise
+__device__ __forceinline__ void st4bf_ho(bool local, bf16* p, float a, float b, float c, float d) {
+  if (local)
+    st4bf(p, a, b, c, d);
+  else
+    st4bf_sc1(p, a, b, c, d);
+}
 __device__ __forceinline__ void ld4bf(const bf16* p, float (&o)[4]) {
   const bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
   o[0] = (float)v[0]; o[1] = (float)v[1]; o[2] = (float)v[2]; o[3] = (float)v[3];

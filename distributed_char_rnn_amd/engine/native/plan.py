@@ -15,7 +15,7 @@ DCR_MODE           ``auto`` | ``exclusive`` | ``overlap``: whether anything (RCC
 DCR_SPIN_LIMIT     bound of every hand-off spin (a timeout sets the error word instead of hanging)
 DCR_DEBUG          ``key=value,...`` diagnostic overrides for tests and same-box A/B runs
                    (DEBUG_KEYS below; the C++ launchers read ``gru_ub``, ``step_nbt``,
-                   ``wide``, ``wgarr``, ``wide_pf``)
+                   ``wide``, ``wgarr``, ``xcdloc``, ``wide_pf``)
 =================  ==========================================================================
 """
 from __future__ import annotations
@@ -35,6 +35,8 @@ DEBUG_KEYS = {
     "pair_bwd": "0: paired forward, single-layer BPTT",
     "wide": "0: the 16-unit x 32-row pair BPTT instead of the 32 x 16 one (C++ launcher)",
     "wgarr": "0: one hand-off counter add per epilogue wave in the pair kernels (C++ launcher)",
+    "xcdloc": "0: write-through (sc1) hand-offs + atomic counters everywhere, never the "
+              "XCD-resident form (plain payload, L2 flags) on single-XCD columns (C++ launcher)",
     "wide_pf": "wide BPTT epilogue-operand loads: 0 before the poll, 1 after the payload, "
                "2 (default) one tick ahead, 3 / 4 poller-wave variants (C++ launcher)",
     "fused_head": "0: library logits GEMM + CE kernel instead of the fused head",

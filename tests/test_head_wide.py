@@ -46,6 +46,37 @@ def test_head_wide_matches_torch(N, V, dcr_ops):
     assert abs(loss2.item() - loss.item()) < 1e-5 * max(1.0, loss.item())
 
 
+@pytest.mark.parametrize("chunk", [1, 3])
+def test_head_wide_chunked_identical(chunk, dcr_ops, monkeypatch):
+    """Token counts whose [N, V] outputs pass the kernel's 32-bit buffer offsets run as chunks
+    of whole 256-token blocks (launch_head_wide).  Forced small chunks (DCR_DEBUG hw_chunk)
+    must give bitwise the same loss, row losses, dlogits, logits and d softmax_b as one launch."""
+    H, V, N = 512, 1024, 256 * 7 + 77
+    g = torch.Generator(device="cuda").manual_seed(7)
+    O = (torch.randn(N, H, device="cuda", generator=g) * 0.5).bfloat16()
+    WsT = (torch.randn(V, H, device="cuda", generator=g) * 0.1).bfloat16()
+    bias = torch.randn(V, device="cuda", generator=g)
+    y = torch.randint(0, V, (N,), device="cuda", dtype=torch.int32, generator=g)
+
+    def run():
+        rl = torch.empty(N, device="cuda")
+        dl = torch.empty(N, V, dtype=torch.bfloat16, device="cuda")
+        lg = torch.empty(N, V, device="cuda")
+        colpart = torch.empty(dcr_ops.head_wide_colpart_rows(N) * V, device="cuda")
+        db = torch.empty(V, device="cuda")
+        part = torch.empty(dcr_ops.head_wide_workspace(N), device="cuda")
+        loss = torch.empty(1, device="cuda")
+        dcr_ops.head_wide(O, WsT, bias, y, 1.0 / N, rl, dl, lg, colpart, db, part, loss)
+        torch.cuda.synchronize()
+        return rl, dl, lg, db, loss
+
+    one = run()
+    monkeypatch.setenv("DCR_DEBUG", f"hw_chunk={chunk}")
+    chunked = run()
+    for a, b in zip(one, chunked):
+        assert torch.equal(a, b)
+
+
 def test_model_wide_head_matches_reference_v8192():
     """The 8k-token config's head shape (V = 8192, H = 512) through the training step: loss and
     every gradient against the fp32 autograd oracle, and against the library-logits route."""
