@@ -99,6 +99,11 @@ def main(argv=None) -> int:
     sync = GradSync(model.store, world, a.bucket_mb, a.allreduce_dtype,
                     enabled=(world > 1 or a.force_sync) and not sharded,
                     guard=model.error_word(), timing=a.profile)
+    if a.force_sync and a.graph:
+        # the captured step never calls sync.ready, so nothing would write the guard slot and
+        # the exchange would not be measured at all
+        raise SystemExit("bench.py: --force_sync measures the eager bucketed exchange; "
+                         "drop --graph")
     if sync.enabled and sync.guard_view is not None:
         opt.guard = sync.guard_view  # every rank's error word, summed with the last bucket
     if a.force_sync and world == 1 and not dist.is_initialized():

@@ -77,6 +77,10 @@ class NativeBackend(LayoutsMixin, BuffersMixin, ForwardMixin, BackwardMixin, Lib
         self._bufs: Dict[Tuple[int, int, bool], dict] = {}
         self.err = torch.zeros(1, dtype=torch.int32, device=self.dev)
         self._err_host: Optional[torch.Tensor] = None
+        # data parallelism: the trainer polls the error word itself after the gradient exchange
+        # has folded every rank's word into each rank's own (GradSync.finish / ShardedStep), so
+        # all ranks see a timeout -- and raise -- on the same step
+        self.defer_err_poll = False
         self._side = None
         self._side_used = False
         self._steps = 0

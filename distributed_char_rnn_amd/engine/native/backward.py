@@ -281,6 +281,9 @@ class BackwardMixin:
                 if pair_hi:  # the lower layer's dtop was fused into the wavefront BPTT
                     self._write_input_grads(layer, names, dWx, dbias)
                     if on_ready is not None:
+                        # a bucket cut (zero.shard_buckets rounds cuts down) may end inside a
+                        # layer above whose gradients a side stream wrote: join it first
+                        self._join_side()
                         on_ready(s.layer_range(layer)[1])
                     dtop = None
                     continue
@@ -312,7 +315,7 @@ class BackwardMixin:
             _release()
         extras = {"logits": logits, "loss": bufs["row_loss"]} if want_extras else None
         self._steps += 1
-        if P.persistent and not self.capturing:
+        if P.persistent and not self.capturing and not self.defer_err_poll:
             self._poll_errors()
         return loss_buf[0], new_state, extras
 

@@ -41,7 +41,13 @@ class TFAdam:
         self.b1, self.b2, self.eps, self.clip = beta1, beta2, eps, clip
         self.m = torch.zeros_like(store.flat)
         self.v = torch.zeros_like(store.flat)
-        self.t = 0  # number of applied updates (TF beta{1,2}_power = b^t after t updates)
+        # number of update STEPS taken (TF beta{1,2}_power = b^t after t steps).  A step whose
+        # update the guard skipped (a persistent-kernel timeout) still counts: the skip is
+        # decided on the device and the host cannot know it without a sync, so t -- and with it
+        # Adam's bias correction -- then runs one step ahead of the updates actually applied
+        # (the CPU path counts the same way, so both paths agree).  A timed-out step raises at
+        # the next error poll anyway; resuming from the last checkpoint restores t exactly.
+        self.t = 0
         self.native = store.device.type == "cuda"
         self.last_norm = torch.zeros(1, device=store.device)
         self.mirror: Optional[torch.Tensor] = None

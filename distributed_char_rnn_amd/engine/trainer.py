@@ -284,6 +284,11 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
                             bucket_mb=getattr(args, "bucket_mb", 8.0), guard=model.error_word())
         _log(f"sharded optimizer: shard {zstep.shard} of {model.store.numel} elements in "
              f"{len(zstep.buckets)} buckets", rank)
+    # data parallelism: poll the persistent kernels' error word after the exchange has folded
+    # every rank's word into each rank's own, so all ranks raise on the same step
+    defer_poll = ctx.world_size > 1 and hasattr(model.backend, "defer_err_poll")
+    if defer_poll:
+        model.backend.defer_err_poll = True
     # --graph: the whole step (fwd, head, BPTT, weight grads, clip + Adam) as one replayed
     # hipGraph; summary steps that want the logits run eagerly
     graphed = None
@@ -328,6 +333,8 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
                     gs = sync.finish(defer_scale=True)
                 with prof.phase("optimizer"):
                     opt.step(lr, grad_scale=gs)
+            if defer_poll:
+                model.poll_errors()
             global_step += 1
             steps_done += 1
             process_group.maybe_inject_fault(rank, global_step)

@@ -89,6 +89,14 @@ class CharRNN:
         ``TFAdam(guard=...)``; None on the reference backend."""
         return getattr(self.backend, "err", None)
 
+    def poll_errors(self) -> None:
+        """Non-blocking error-word poll (raises a few steps after a persistent-kernel timeout
+        without a device sync); the backend's own poll runs inside train_step unless
+        ``defer_err_poll`` is set (data parallelism: the trainer calls this after the exchange)."""
+        poll = getattr(self.backend, "_poll_errors", None)
+        if poll is not None:
+            poll()
+
     def check_errors(self) -> None:
         """Raise if a persistent kernel timed out (synchronises the device)."""
         check = getattr(self.backend, "check_errors", None)

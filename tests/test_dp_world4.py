@@ -62,7 +62,7 @@ def _worker(rank, world, port, mode, steps, fault_rank, fault_step, q):
                                guard=guard)
         data = _data(B * world, steps)
         st = m.zero_state(B)
-        norms, snaps, early = [], [], []
+        norms, snaps, early, seen = [], [], [], []
         for s in range(steps):
             blk = data[s, rank * B:(rank + 1) * B]
             sync.reset()
@@ -77,10 +77,11 @@ def _worker(rank, world, port, mode, steps, fault_rank, fault_step, q):
                 early.append(len(sync.launched))  # buckets launched during the backward
                 norms.append(float(sync.step(0.01)))
             snaps.append(m.store.flat.numpy().copy())
+            seen.append(int(guard.item()))  # this rank's own word after the exchange
         if mode != "replicated":
             sync.gather_slots()
         guard.zero_()
-        q.put((rank, snaps, opt.m.numpy().copy(), norms, early, int(guard.item())))
+        q.put((rank, snaps, opt.m.numpy().copy(), norms, early, int(guard.item()), seen))
     finally:
         dist.destroy_process_group()
 
@@ -118,7 +119,7 @@ def test_world4_equals_single_process(mode):
     ref, ref_norms = _single(4)
     out = _run(mode)
     assert all(n > CLIP for n in ref_norms), "clipping must be active"
-    for rank, snaps, _, norms, early, _ in out:
+    for rank, snaps, _, norms, early, _, _ in out:
         np.testing.assert_allclose(norms, ref_norms, rtol=1e-4)
         np.testing.assert_allclose(snaps[-1], ref[-1], rtol=2e-4, atol=2e-6)
         np.testing.assert_array_equal(snaps[-1], out[0][1][-1])  # replicas identical
@@ -142,9 +143,11 @@ def test_sharded_buckets_cover_buffer_and_align():
 @pytest.mark.parametrize("mode", ["replicated", "sharded"])
 def test_error_word_on_one_rank_skips_update_everywhere(mode):
     out = _run(mode, world=2, steps=3, fault_rank=1, fault_step=1)
-    for rank, snaps, _, _, _, guard in out:
+    for rank, snaps, _, _, _, guard, seen in out:
         # step 1's update was skipped on EVERY rank (the guard was MAX-reduced)
         np.testing.assert_array_equal(snaps[1], snaps[0])
+        # ... and folded back into every rank's own word, so all ranks raise on that step
+        assert seen[0] == 0 and seen[1] != 0 and seen[2] == 0, (rank, seen)
         assert not np.array_equal(snaps[2], snaps[1])  # step 2 (guard cleared) updated
         np.testing.assert_array_equal(snaps[-1], out[0][1][-1])
         assert guard == 0
