@@ -55,7 +55,7 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_persist_kernel(GruPersistArgs 
   const int Bp = gru_rows(B, NT);  // ring rows (padded batch)
   const int nwg_u = H / (16 * UB);
   int ubk, bg;
-  map_block(blockIdx.x, nwg_u, Bp / (16 * NT), ubk, bg);
+  if (!map_block_grid(blockIdx.x, gridDim.x, nwg_u, Bp / (16 * NT), ubk, bg)) return;  // padding
   const int ub0 = ubk * 16 * UB, b0 = bg * 16 * NT;
   const int kq = 8 * (lane >> 4);
   const int kbase = w * (KS * 32);
@@ -283,7 +283,7 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
   const int Bp = gru_rows(B, NT);  // ring rows (padded batch)
   const int nwg_u = H / (16 * UB);
   int ubk, bg;
-  map_block(blockIdx.x, nwg_u, Bp / (16 * NT), ubk, bg);
+  if (!map_block_grid(blockIdx.x, gridDim.x, nwg_u, Bp / (16 * NT), ubk, bg)) return;  // padding
   const int ub0 = ubk * 16 * UB, b0 = bg * 16 * NT;
   const int kq = 8 * (lane >> 4);
   const int kA = w * (KA * 32), kB = w * (KB * 32);
@@ -590,8 +590,13 @@ int launch_gru_persist(int bwd, const GruPersistArgs& a, int cus, hipStream_t s)
     (void)hipMemsetAsync(a.cnt, 0,
                          sizeof(unsigned) * 2 * (size_t)(gru_rows(a.B, nt) / (16 * nt)) * (a.T + 1) * 4, s);
   void* args[] = {const_cast<GruPersistArgs*>(&a)};
-  return hipLaunchKernel(fn, dim3(gru_grid(a.H, a.B, ub, nt)), dim3(256), args, 0, s) == hipSuccess
-             ? 0 : -3;
+  // the XCD-padded grid (persist_common.h xcd_grid) when it is co-resident
+  int grid = gru_grid(a.H, a.B, ub, nt), o = 0;
+  const int padded = xcd_grid(a.H / (16 * ub), gru_rows(a.B, nt) / (16 * nt));
+  if (padded != grid && hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, fn, 256, 0) == hipSuccess &&
+      padded <= o * cus)
+    grid = padded;
+  return hipLaunchKernel(fn, dim3(grid), dim3(256), args, 0, s) == hipSuccess ? 0 : -3;
 }
 
 }  // namespace dcr

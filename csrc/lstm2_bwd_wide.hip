@@ -115,7 +115,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
   const int G4H = 4 * H;
   const int ncol = a.nbg;  // 16-row columns (the host passes ceil(B / 16))
   int ubk, col;
-  map_block(blockIdx.x, H / 32, ncol, ubk, col);
+  if (!map_block_grid(blockIdx.x, gridDim.x, H / 32, ncol, ubk, col)) return;  // padding
   const int ub0 = ubk * 32;
   const int kq = 8 * (lane >> 4);
   unsigned* cnt0 = a.cnt0 + (size_t)col * (T + 1) * 4;
@@ -489,8 +489,13 @@ int launch_lstm2_bwd_wide(const Lstm2BwdArgs& a, int cus, hipStream_t s) {
   if (!lstm2_bwd_wide_ok(a.H, a.B, cus) || a.nbg != (a.B + 15) / 16) return -2;
   void* args[] = {const_cast<Lstm2BwdArgs*>(&a)};
   const void* fn = a.xmask ? lstm2_bwd_wide_pick<true>(a.H) : lstm2_bwd_wide_pick<false>(a.H);
-  return hipLaunchKernel(fn, dim3((a.H / 32) * a.nbg), dim3(256), args, 0, s) == hipSuccess ? 0
-                                                                                             : -3;
+  // the XCD-padded grid (persist_common.h xcd_grid) when it is co-resident
+  int grid = (a.H / 32) * a.nbg, o = 0;
+  const int padded = xcd_grid(a.H / 32, a.nbg);
+  if (padded != grid && hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, fn, 256, 0) == hipSuccess &&
+      padded <= o * cus)
+    grid = padded;
+  return hipLaunchKernel(fn, dim3(grid), dim3(256), args, 0, s) == hipSuccess ? 0 : -3;
 }
 
 }  // namespace dcr

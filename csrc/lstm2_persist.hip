@@ -82,7 +82,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
   const int H = a.H, B = a.B, T = a.T;
   const int nwg_u = H / 16;
   int ubk, col;
-  map_block(blockIdx.x, nwg_u, a.nbg / G, ubk, col);
+  if (!map_block_grid(blockIdx.x, gridDim.x, nwg_u, a.nbg / G, ubk, col)) return;  // padding
   const int ub0 = ubk * 16;
   const int kq = 8 * (lane >> 4);
   const int kbase = w * (KS * 32);
@@ -558,7 +558,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
   const int H = a.H, B = a.B, T = a.T;
   const int G4H = 4 * H;
   int ubk, col;
-  map_block(blockIdx.x, H / 16, a.nbg / G, ubk, col);
+  if (!map_block_grid(blockIdx.x, gridDim.x, H / 16, a.nbg / G, ubk, col)) return;  // padding
   const int ub0 = ubk * 16;
   const int kq = 8 * (lane >> 4);
   unsigned* cnt0 = a.cnt0 + (size_t)col * (T + 1) * 4;
@@ -945,7 +945,15 @@ int lstm2_plan_g(int H, int B, int cus, int force) {
   return 0;
 }
 
-static int lstm2_grid(const int H, const int nbg, const int G) { return (H / 16) * (nbg / G); }
+// the XCD-padded grid (persist_common.h xcd_grid) when it is co-resident, else the plain one
+static int lstm2_grid(const void* fn, const int H, const int nbg, const int G, const int cus) {
+  const int plain = (H / 16) * (nbg / G), padded = xcd_grid(H / 16, nbg / G);
+  int o = 0;
+  if (padded != plain && hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, fn, 256, 0) == hipSuccess &&
+      padded <= o * cus)
+    return padded;
+  return plain;
+}
 
 static bool lstm2_args_ok(int H, int B, int nbg, int G, int cus) {
   if (G < 1 || G > kPairMaxG || nbg % G != 0 || nbg * 32 < B) return false;
@@ -956,16 +964,17 @@ int launch_lstm2_fwd_persist(const Lstm2Args& a, int cus, hipStream_t s) {
   if (!lstm2_args_ok(a.H, a.B, a.nbg, a.G, cus) || !a.hring0 || !a.hring1) return -2;
   void* args[] = {const_cast<Lstm2Args*>(&a)};
   if (a.x0 && (a.G != 1 || !lstm2_xin_ok(a.H, cus))) return -2;
-  return hipLaunchKernel(lstm2_pick(a.H, a.G, a.xmask != nullptr, a.x0 != nullptr),
-                         dim3(lstm2_grid(a.H, a.nbg, a.G)), dim3(256), args,
-                         0, s) == hipSuccess ? 0 : -3;
+  const void* fn = lstm2_pick(a.H, a.G, a.xmask != nullptr, a.x0 != nullptr);
+  return hipLaunchKernel(fn, dim3(lstm2_grid(fn, a.H, a.nbg, a.G, cus)), dim3(256), args, 0, s) ==
+                 hipSuccess ? 0 : -3;
 }
 
 int launch_lstm2_bwd_persist(const Lstm2BwdArgs& a, int cus, hipStream_t s) {
   if (!lstm2_args_ok(a.H, a.B, a.nbg, a.G, cus)) return -2;
   void* args[] = {const_cast<Lstm2BwdArgs*>(&a)};
-  return hipLaunchKernel(lstm2_bwd_pick(a.H, a.G, a.xmask != nullptr), dim3(lstm2_grid(a.H, a.nbg, a.G)), dim3(256),
-                         args, 0, s) == hipSuccess ? 0 : -3;
+  const void* fn = lstm2_bwd_pick(a.H, a.G, a.xmask != nullptr);
+  return hipLaunchKernel(fn, dim3(lstm2_grid(fn, a.H, a.nbg, a.G, cus)), dim3(256), args, 0, s) ==
+                 hipSuccess ? 0 : -3;
 }
 
 }  // namespace dcr

@@ -280,6 +280,31 @@ __host__ __device__ __forceinline__ void map_block(int bid, int nwg_u, int nbg, 
   }
 }
 
+// Grid of a column-mapped persistent launch padded to whole XCD groups: 8 x nwg_u workgroups per
+// 8 columns.  Under round-robin dispatch blocks b, b + 8, ... share an XCD, so with this grid
+// every column's nwg_u workgroups can sit on ONE XCD even when there are fewer than 8
+// (or not a multiple of 8) columns -- the XCD-resident hand-off form then applies to the small
+// shapes too (the reference default B = 50 has 2 forward columns).  Blocks of the padding
+// columns exit at once.  The launcher uses it only when the padded grid is still co-resident;
+// with a multiple of 8 columns it equals the plain grid.
+__host__ __device__ __forceinline__ int xcd_grid(int nwg_u, int ncol) {
+  return 8 * nwg_u * ((ncol + 7) / 8);
+}
+// map_block for a launch of `grid` workgroups: the XCD-grouped map when grid == xcd_grid (false
+// for a padding block, which must exit), otherwise the plain column-major map
+__host__ __device__ __forceinline__ bool map_block_grid(int bid, int grid, int nwg_u, int ncol,
+                                                        int& ubk, int& col) {
+  if (XCD_GROUPING && grid == xcd_grid(nwg_u, ncol)) {
+    const int x = bid % 8, j = bid / 8;
+    col = x + 8 * (j / nwg_u);
+    ubk = j % nwg_u;
+    return col < ncol;
+  }
+  ubk = bid % nwg_u;
+  col = bid / nwg_u;
+  return true;
+}
+
 // Hand-off poller.  GRU kernels poll from lane 0 of wave 3, which never runs a cell epilogue
 // (UB * NT <= 3), so polling overlaps the epilogue waves' drain and post-arrival work: 3-layer
 // GRU-1024 16.8 -> 15.3 ms/step.  The LSTM kernels keep the poller on wave 0 (an epilogue wave):

@@ -64,6 +64,34 @@ static void check_map(int nwg_u, int nbg) {
   }
 }
 
+// map_block_grid: with the XCD-padded grid every real (unit block, column) pair is hit exactly
+// once, padding blocks report false, and each column's blocks share bid % 8 (one XCD under
+// round-robin dispatch); with the plain grid it is the plain column-major bijection
+static void check_map_grid(int nwg_u, int ncol) {
+  for (int padded = 0; padded < 2; ++padded) {
+    const int grid = padded ? dcr::xcd_grid(nwg_u, ncol) : nwg_u * ncol;
+    std::vector<unsigned char> seen((size_t)nwg_u * ncol, 0);
+    std::vector<int> xcd(ncol, -1);
+    int real = 0;
+    for (int bid = 0; bid < grid; ++bid) {
+      int ubk = -1, col = -1;
+      if (!dcr::map_block_grid(bid, grid, nwg_u, ncol, ubk, col)) continue;
+      ++real;
+      CHECK(ubk >= 0 && ubk < nwg_u && col >= 0 && col < ncol, "map_block_grid(%d,%d,%d,%d)",
+            bid, grid, nwg_u, ncol);
+      if (ubk < 0 || ubk >= nwg_u || col < 0 || col >= ncol) continue;
+      const size_t i = (size_t)col * nwg_u + ubk;
+      CHECK(!seen[i], "map_block_grid collision (%d,%d) from bid %d", ubk, col, bid);
+      seen[i] = 1;
+      if (grid == dcr::xcd_grid(nwg_u, ncol)) {
+        CHECK(xcd[col] < 0 || xcd[col] == bid % 8, "column %d spans XCD groups", col);
+        xcd[col] = bid % 8;
+      }
+    }
+    CHECK(real == nwg_u * ncol, "map_block_grid: %d real blocks, want %d", real, nwg_u * ncol);
+  }
+}
+
 int main() {
   const int Bs[] = {16, 32, 48, 256};
   const int Ks[] = {32, 128, 512, 2048, 3 * 1024};
@@ -72,7 +100,10 @@ int main() {
   const int us[] = {1, 4, 8, 32, 64, 128};
   const int gs[] = {1, 2, 3, 8, 16, 24};
   for (int u : us)
-    for (int g : gs) check_map(u, g);
+    for (int g : gs) {
+      check_map(u, g);
+      check_map_grid(u, g);
+    }
   if (failures) {
     std::fprintf(stderr, "%d layout check(s) failed\n", failures);
     return 1;

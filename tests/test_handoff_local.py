@@ -50,21 +50,23 @@ def _run(cfg, B, T, loc, monkeypatch, steps):
     return m, losses, [s.clone() for t in st for s in t], marks
 
 
-@pytest.mark.parametrize("model,B,T,H,drop,steps", [
-    ("lstm", 256, 1024, 512, False, 4),  # headline shape: fwd G = 1 + wide BPTT, 4 x 1026 ticks
-    ("lstm", 512, 64, 512, False, 2),    # forward G = 2 + the 16 x 32 BPTT at G = 2
-    ("lstm", 50, 40, 128, False, 2),     # ragged batch, H = 128
-    ("lstm", 256, 64, 512, True, 2),     # dropout instantiations
-    ("gru", 128, 512, 1024, False, 3),   # config 3's GRU-1024 shape: 2 hand-offs per step
-    ("gru", 50, 40, 256, False, 2),      # ragged GRU batch
+# `local`: whether every column's workgroups sit on one XCD (the XCD-padded grid,
+# persist_common.h xcd_grid, also covers fewer than 8 columns)
+@pytest.mark.parametrize("model,B,T,H,drop,steps,local", [
+    ("lstm", 256, 1024, 512, False, 4, 1),  # headline shape: fwd G = 1 + wide BPTT, 4 x 1026 ticks
+    ("lstm", 512, 64, 512, False, 2, 1),    # forward G = 2 + the 16 x 32 BPTT at G = 2
+    ("lstm", 50, 40, 128, False, 2, 1),     # ragged batch, H = 128: 2 columns (padded grid)
+    ("lstm", 256, 64, 512, True, 2, 1),     # dropout instantiations
+    ("gru", 128, 512, 1024, False, 3, 1),   # config 3's GRU-1024 shape: 2 hand-offs per step
+    ("gru", 50, 40, 256, False, 2, 1),      # ragged GRU batch: 4 columns (padded grid)
 ])
-def test_local_handoff_bitwise(model, B, T, H, drop, steps, monkeypatch):
+def test_local_handoff_bitwise(model, B, T, H, drop, steps, local, monkeypatch):
     kp = 0.8 if drop else 1.0
     cfg = ModelConfig(model=model, vocab_size=65, rnn_size=H, num_layers=2,
                       input_keep_prob=kp, output_keep_prob=kp)
     a, la, sa, ma = _run(cfg, B, T, True, monkeypatch, steps)
     b, lb, sb, mb = _run(cfg, B, T, False, monkeypatch, steps)
-    assert ma == (1, 1), ma  # the local form ran (round-robin placement: one XCD per column)
+    assert ma == (local, local), ma  # the local form ran where it can (one XCD per column)
     assert mb == (0, 0), mb
     assert la == lb
     for u, v in zip(sa, sb):
