@@ -89,15 +89,23 @@ __device__ __forceinline__ float row_reduce_scatter16(float (&v)[16], int lane) 
 // load) are loaded.  vmcnt retires in issue order, so whatever is loaded before the hand-off
 // poll delays the poller's first counter check by its latency.
 //   0: at the tick start, before the poll (the poll then waits for them: +1.35 us hand-off)
-//   1: right behind the tick's payload loads (the MFMA / epilogue phase waits for them instead)
+//   1: right behind the tick's payload loads (the MFMA / epilogue phase waits for them instead);
+//      the default with the XCD-resident hand-off, whose poll returns ~0.8 us after the last
+//      arrival (BPTT 4.80 vs 5.23 us per tick for 2, scripts/pair_bench.py, same box)
 //   2: one tick ahead, right after the previous tick's hand-off arrival: their latency runs
-//      concurrently with the hand-off's own (~1.7 us from arrival to the consumers' poll);
-//      the default (same-box A/B: 1.711 vs 1.726 ms/step for 0; 1 was slower than 0)
+//      concurrently with the hand-off's own (~1.7 us from arrival to the consumers' poll with
+//      the write-through hand-off: there it was the best, 1.711 vs 1.726 ms/step for 0)
 //   3: 2 for waves 1-3, 1 for wave 0, whose lane 0 polls: the poll then waits for no HBM load
 //   4: 2 for waves 1-3; wave 0 (the poller) issues no HBM load at all: wave 1 DMAs wave 0's
 //      operands (buffer_load ... lds, 16 dwords per lane) into a per-parity LDS buffer one tick
 //      ahead, and wave 0 reads them after the tick's second barrier (wave 1's waits on its own
 //      younger payload loads have covered the DMA by then).  No dropout variant.
+//   5: 1's operand loads, plus the row-major dZ copy of the PREVIOUS tick stored behind the
+//      payload loads (kept packed in registers across the tick boundary) and layer l's dtop
+//      stash in front of the arrival (its MFMAs overlapping the ring stores' drain), so that no
+//      store sits in front of the next poll.  Measured slower (1.630 vs 1.619 ms/step against
+//      2): the compiler's waitcnt analysis cannot count the conditional stores, so the MFMA
+//      phase's wait became vmcnt(0) and covered them, and the drain waited for the HBM loads.
 template <int KS, bool DROP, int PF>
 __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) {
   static_assert(KS % 4 == 0, "K quarter = whole 32-wide k-steps per gate");
@@ -109,6 +117,11 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
   __shared__ unsigned arrl[2];              // per-layer arrivals of the tick (wgarr)
   // PF = 4: wave 0's epilogue operands by tick parity: g4 (8 dwords), c_{t+1} (4), c_t (4)
   __shared__ __attribute__((aligned(16))) unsigned opb[PF == 4 ? 2 : 1][PF == 4 ? 16 : 1][64];
+  // wave 0 (the hand-off poller) hands its row-major dZ copy to wave 2 (same rows and units,
+  // layer l+1), which stores it one tick later: vmcnt retires in issue order, so the poller's
+  // own stores made its flag loads wait for their acknowledgement; by tick parity, [gate][lane]
+  constexpr bool OFFL = PF == 1 || PF == 2;
+  __shared__ __attribute__((aligned(16))) u32x2 offl[OFFL ? 2 : 1][4][64];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
@@ -165,6 +178,17 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
   const size_t bh = (size_t)b * H + u0;
   float dc[4] = {0.f, 0.f, 0.f, 0.f};
   float dbacc = 0.f;  // this lane's bias-gradient sum (value lane & 15 of its row, see header)
+  // PF = 5: the previous tick's row-major dZ values (bf16, as st4bf rounds them) and their step
+  bf16x4 dzp[4];
+  int tpend = -1;
+  auto flush_dz = [&]() {
+    if (tpend >= 0 && live) {
+      bf16* dz = dzL + ((size_t)tpend * B + b) * G4H + u0;
+#pragma unroll
+      for (int gt = 0; gt < 4; ++gt) *reinterpret_cast<bf16x4*>(dz + gt * H) = dzp[gt];
+    }
+    tpend = -1;
+  };
   // layer l's dtop partial of its NEXT tick (this wave's K quarter, both unit halves), computed
   // off the critical path from the tick's dZ_{l+1} fragments
   f32x4 xs[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
@@ -229,7 +253,8 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
     const int t = L ? T - 1 - tau : T + 1 - tau;  // this role's step
     const bool act = L ? on1 : on0;
     STAMPW(0)
-    if (PF == 0 || (PF == 1 && tau == 0) || (PF >= 2 && tau == 0 && !(PF == 4 && w == 0)))
+    if (PF == 0 || ((PF == 1 || PF == 5) && tau == 0) ||
+        ((PF >= 2 && PF <= 4) && tau == 0 && !(PF == 4 && w == 0)))
       prefetch(tau);
     const int s1 = T - tau, s0 = T + 2 - tau;  // ring slots of dZ_{l+1} and dZ_l
     if (tau >= 1 && loc) {  // flags of both layers' producing tick (tau - 1) + 1
@@ -262,7 +287,8 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
         for (int s = 0; s < KS; ++s)
           p0[s] = ld8_sc1(rz0, frag_load_off(col, kcol(s) >> 5, G4H, lane) + o0);
       }
-      if (PF == 1 || (PF == 3 && w == 0)) prefetch(tau);
+      if (PF == 1 || PF == 5 || (PF == 3 && w == 0)) prefetch(tau);
+      if constexpr (PF == 5) flush_dz();  // last tick's dZ rows, behind this tick's loads
       __builtin_amdgcn_sched_barrier(0);
       if (on1) {  // layer l+1: dh partial = dZ_{l+1}[t+1] · W_h,l+1ᵀ, both unit halves
         f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
@@ -311,6 +337,25 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
     STAMPW(3)
     __syncthreads();
     STAMPW(4)
+    // layer l's dtop partial for its next tick from this tick's dZ_{l+1} fragments
+    bool stashed = false;
+    auto do_stash = [&]() {
+      if (ld1) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {
+            x = mfma16(wx1l[w][u][s][lane], p1[s], x);
+            // (PF = 2: bound the LDS fragments the scheduler hoists ahead of the MFMAs; the
+            // prefetched operands are live here too)
+            if (PF >= 2 && (s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+          }
+          xs[u] = x;
+        }
+      }
+      stashed = true;
+    };
     if constexpr (PF == 4) if (w == 0 && act) {  // this wave's operands, DMA'd by wave 1
       const unsigned(&ob)[16][64] = opb[tau & 1];
 #pragma unroll
@@ -363,6 +408,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
         st4bf_ho(loc, zr + frag_index(b, H + u0, G4H), dj[0], dj[1], dj[2], dj[3]);
         st4bf_ho(loc, zr + frag_index(b, 2 * H + u0, G4H), df_[0], df_[1], df_[2], df_[3]);
         st4bf_ho(loc, zr + frag_index(b, 3 * H + u0, G4H), dO[0], dO[1], dO[2], dO[3]);
+        if constexpr (PF == 5) do_stash();  // its MFMAs overlap the ring stores' drain
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         STAMP_ARRIVE()
         if (lane == 0) {
@@ -382,7 +428,21 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
       for (int r = 0; r < 4; ++r) {
         dcur[r] = di[r]; dcur[4 + r] = dj[r]; dcur[8 + r] = df_[r]; dcur[12 + r] = dO[r];
       }
-      if (live) {
+      if constexpr (PF == 5) {  // stored behind the next tick's payload loads (flush_dz)
+#pragma unroll
+        for (int gt = 0; gt < 4; ++gt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dzp[gt][r] = f2bf(dcur[4 * gt + r]);
+        tpend = t;
+      } else if (OFFL && w == 0) {  // stored by wave 2 one tick later
+#pragma unroll
+        for (int gt = 0; gt < 4; ++gt) {
+          bf16x4 v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = f2bf(dcur[4 * gt + r]);
+          offl[tau & 1][gt][lane] = __builtin_bit_cast(u32x2, v);
+        }
+      } else if (live) {
         bf16* dz = dzL + ((size_t)t * B + b) * G4H + u0;
         st4bf(dz, dcur[0], dcur[1], dcur[2], dcur[3]);
         st4bf(dz + H, dcur[4], dcur[5], dcur[6], dcur[7]);
@@ -421,21 +481,27 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
             rc, (__attribute__((address_space(3))) void*)&ob[12 + r][0], 4, oc + 4 * r, sc, 0, 0);
       }
     }
-    if (ld1) {  // every wave (with an epilogue this tick or not) stashes layer l's next dtop
+    if (!stashed) do_stash();  // every wave (with an epilogue this tick or not)
+    // wave 0's dZ copy of tick tau-1 (layer l, step T+2-tau), written before this tick's first
+    // barrier (wave 0 is active from tick 2)
+    auto store_offl = [&](int tk) {
+      const int t0 = T + 1 - tk;
+      bf16* dz = a.dz0 + ((size_t)t0 * B + b) * G4H + u0;
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          x = mfma16(wx1l[w][u][s][lane], p1[s], x);
-          // (PF = 2: bound the LDS fragments the scheduler hoists ahead of the MFMAs; the
-          // prefetched operands are live here too)
-          if (PF >= 2 && (s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-        }
-        xs[u] = x;
-      }
-    }
+      for (int gt = 0; gt < 4; ++gt) *reinterpret_cast<u32x2*>(dz + gt * H) = offl[tk & 1][gt][lane];
+    };
+    if (OFFL && w == 2 && tau >= 3 && live) store_offl(tau - 1);
     STAMPW(7)
+  }
+  if constexpr (PF == 5) flush_dz();
+  if constexpr (OFFL) {  // wave 0's last copy (tick T + 1, step 0)
+    __syncthreads();
+    if (w == 2 && live) {
+      bf16* dz = a.dz0 + (size_t)b * G4H + u0;
+#pragma unroll
+      for (int gt = 0; gt < 4; ++gt)
+        *reinterpret_cast<u32x2*>(dz + gt * H) = offl[(T + 1) & 1][gt][lane];
+    }
   }
   // bias-gradient partial of this role's 16-row column: lane r of row q holds value r
   float* const dbp = L ? a.db_part1 : a.db_part0;
@@ -460,13 +526,14 @@ static const void* lstm2_bwd_wide_pick_t(int H) {
 }
 template <bool DROP>
 static const void* lstm2_bwd_wide_pick(int H) {
-  switch (debug_int("wide_pf", 2)) {
+  switch (debug_int("wide_pf", 1)) {
     case 0: return lstm2_bwd_wide_pick_t<DROP, 0>(H);
-    case 1: return lstm2_bwd_wide_pick_t<DROP, 1>(H);
+    case 2: return lstm2_bwd_wide_pick_t<DROP, 2>(H);
     case 3: return lstm2_bwd_wide_pick_t<DROP, 3>(H);
     case 4: return DROP ? lstm2_bwd_wide_pick_t<DROP, 2>(H) : lstm2_bwd_wide_pick_t<DROP, 4>(H);
+    case 5: return lstm2_bwd_wide_pick_t<DROP, 5>(H);
   }
-  return lstm2_bwd_wide_pick_t<DROP, 2>(H);
+  return lstm2_bwd_wide_pick_t<DROP, 1>(H);
 }
 
 // The 32-unit x 16-row BPTT applies at (H, B): H a multiple of 128 up to 512, and the grid of

@@ -36,6 +36,11 @@ namespace dcr {
 #define STAMPG(g, i)                                                                \
   if (a.diag && blockIdx.x == 0 && threadIdx.x == 0)                                \
     a.diag[((size_t)tau * G + (g)) * 8 + (i)] = __builtin_amdgcn_s_memtime();
+// The forward's stamps exist only in its DIAG instantiation: a conditional store between the
+// payload loads and the MFMAs makes the compiler's waitcnt analysis assume the path without it,
+// so every later wait degrades to vmcnt(0) (see the G = 1 notes in the kernel)
+#define STAMPF(g, i) \
+  if constexpr (DIAG) { STAMPG(g, i) }
 
 constexpr int kPairMaxG = 4;
 
@@ -63,7 +68,7 @@ __device__ __forceinline__ bf16x8 mask_frag(const bf16x8& v, unsigned m) {
 // fp32 [T·B, 4H] zx0: W_x,lᵀ fragments sit in LDS, the rows' fragments are loaded and the
 // product accumulated BEFORE the tick's poll (it does not depend on the hand-off), and the
 // recurrent product is added on top after it.
-template <int KS, int G, bool DROP, bool XIN>
+template <int KS, int G, bool DROP, bool XIN, bool DIAG>
 __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) {
   static_assert(!XIN || G == 1, "in-kernel input projection: one batch group per workgroup");
   // partials [wave][layer][tile][gate][lane][r] (16-B lane stride: conflict-free b128 access),
@@ -77,6 +82,15 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
   // XIN: W_x,lᵀ fragments [wave][gate][k-step][lane] (64 KB at H = 512), read back only by the
   // wave that wrote them
   __shared__ __attribute__((aligned(16))) bf16x8 wx0l[XIN ? 4 : 1][4][XIN ? KS : 1][64];
+  // G = 1 gather mode (the headline): the workgroup's slice of the zx0 table -- 16 units x 4
+  // gates of every vocabulary row, rows padded to 68 floats so 16 lanes reading 16 different
+  // rows hit distinct banks -- and the gather ids of its 32 rows for every tick live in LDS, so
+  // a tick issues no per-row loads (vmcnt retires in order: the one-tick-ahead row loads had
+  // made every later wait of the tick cover them; 4.10 -> 3.72 us per tick without them)
+  constexpr bool ZTAB = G == 1 && !XIN;
+  constexpr int kTabMaxV = 128, kTabLd = 68, kTabMaxT = 256;
+  __shared__ __attribute__((aligned(16))) float ztab[ZTAB ? kTabMaxV * kTabLd : 4];
+  __shared__ int idsl[ZTAB ? kTabMaxT * 32 : 1];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
@@ -125,6 +139,18 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
       x1[gt][s] = ld8(a.X1T + row);
       if constexpr (XIN) wx0l[w][gt][s][lane] = ld8(a.X0T + row);
     }
+  // the gather table slice and ids (ZTAB; read after the barrier below)
+  const bool ztl = ZTAB && a.ids && a.zx_rows > 0 && a.zx_rows <= kTabMaxV && T <= kTabMaxT;
+  if (ztl) {
+    for (int i = threadIdx.x; i < a.zx_rows * 64; i += 256) {
+      const int v = i >> 6, cc = i & 63;  // column cc = gate (cc >> 4), unit ub0 + (cc & 15)
+      ztab[v * kTabLd + cc] = a.zx0[(size_t)v * a.zx_ld + (cc >> 4) * H + ub0 + (cc & 15)];
+    }
+    for (int i = threadIdx.x; i < T * 32; i += 256) {
+      const int tk = i >> 5, r = col * 32 + (i & 31);
+      idsl[i] = r < B ? a.ids[(size_t)tk * B + r] : 0;
+    }
+  }
   if (threadIdx.x == 0) {
     loc_s = tryloc ? xcd_decide(xw, (unsigned)nwg_u, a.spin_limit, a.err, 11u) : 0;
     if (loc_s && ubk == 0) cnt0[1] = 1u;  // (diagnostics: the column ran XCD-local)
@@ -188,7 +214,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
   // round trips) had made the poller's first counter check wait for them every tick.
   constexpr bool ZXA = G == 1 && !XIN;
   const int bz = col * G * 32 + 16 * J + (lane & 15);  // (G = 1) this lane's row
-  const bool zl = ZXA && L == 0 && bz < B;
+  const bool zl = ZXA && L == 0 && bz < B && !ztl;
   int idn = 0;  // gather id of the next tick's row
   auto zx_row1 = [&](int tk, int id) -> const float* {
     return a.ids ? a.zx0 + (size_t)id * a.zx_ld : a.zx0 + ((size_t)tk * B + bz) * a.zx_ld;
@@ -198,6 +224,37 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     zx_load(zx_row1(0, id0), zxn);
     if (a.ids && T > 1) idn = a.ids[(size_t)B + bz];
   }
+  // G = 1: the tick keeps the compiler's waitcnt analysis exact between its payload loads and
+  // its MFMAs -- straight-line, unconditional vector-memory operations only (out-of-range
+  // buffer offsets / empty buffer descriptors instead of branches) -- so that the MFMA phase
+  // waits for the payload alone.  That makes it free to store the previous tick's row-major
+  // h / c / gates copies right behind the payload loads (their acknowledgement then overlaps
+  // the MFMA and epilogue phases), instead of after the arrival, where vmcnt's in-order
+  // retirement had made the poller's flag loads wait for them (4.10 -> 3.33 us per tick
+  // without any row-major store, scripts/pair_bench.py).
+  constexpr bool DEFER = G == 1;
+  bf16x4 rm_h = {}, rm_g[4] = {};
+  float rm_c[4] = {};
+  int rm_t = -1;
+  const __amdgpu_buffer_rsrc_t r_h = make_rsrc(hbL, sizeof(bf16) * (size_t)(T + 1) * B * hld);
+  const __amdgpu_buffer_rsrc_t r_c = make_rsrc(cbL, sizeof(float) * (size_t)(T + 1) * B * H);
+  const __amdgpu_buffer_rsrc_t r_g = make_rsrc(gtL, gtL ? sizeof(bf16) * (size_t)T * B * 4 * H : 0);
+  const int brow = col * G * 32 + 16 * J + (lane & 15);  // (G = 1) this lane's row
+  auto flush_rm = [&]() {
+    constexpr unsigned kOut = 0x7FFFFFF0u;  // out of range: dropped
+    const bool ok = rm_t >= 0 && brow < B;
+    const unsigned oh = ok ? (unsigned)((((size_t)(rm_t + 1) * B + brow) * hld + u0) * sizeof(bf16)) : kOut;
+    const unsigned oc = ok ? (unsigned)(((size_t)(rm_t + 1) * B * H + (size_t)brow * H + u0) * sizeof(float)) : kOut;
+    const unsigned og = ok ? (unsigned)((((size_t)rm_t * B + brow) * 4 * H + u0) * sizeof(bf16)) : kOut;
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, rm_h), r_h, oh, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(
+        __builtin_bit_cast(u32x4, f32x4{rm_c[0], rm_c[1], rm_c[2], rm_c[3]}), r_c, oc, 0, 0);
+#pragma unroll
+    for (int gt = 0; gt < 4; ++gt)
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, rm_g[gt]), r_g,
+                                            og + gt * H * (unsigned)sizeof(bf16), 0, 0);
+    rm_t = -1;
+  };
 
   for (int tau = 0; tau <= T + LAG - 1; ++tau) {
     const bool on0 = tau < T;                  // layer l   computes step tau
@@ -209,7 +266,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     // this role's slot t+1 is read by a later tick: layer l's up to slot T, layer l+1's up to
     // slot T-1 (by itself)
     const bool signal = act && (L == 0 || t + 1 < T);
-    STAMPG(0, 0)
+    STAMPF(0, 0)
     // layer-l input projections of step tau (independent of the hand-off): group 0's rows are
     // loaded before the poll, group g+1's right behind group g's payload (a gathered row needs
     // its id first; loaded for all groups here, the wait overlaps the poll).  (Loading group 0's
@@ -279,10 +336,10 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
                                               : cnt1 + (size_t)(tau - LAG) * 4,
                                           target, a.spin_limit, a.err, 9u);
     }
-    STAMPG(0, 1)
+    STAMPF(0, 1)
     // (also orders this tick's first partial stores after the previous tick's epilogue reads)
     __syncthreads();
-    STAMPG(0, 2)
+    STAMPF(0, 2)
     // payload fragments of group g: slot 0 is row-major [B, H] (rows >= B read as zero: buffer
     // bounds); later slots come from the fragment-tiled rings: one contiguous 1 KB load per
     // (tile, k-step).  Double-buffered by group: group g+1's loads are issued before group g's
@@ -293,6 +350,29 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     bf16x8 pf0[PREF ? 2 : 1][2][KS], pf1[PREF ? 2 : 1][2][KS];
     auto load_group = [&](int g, bf16x8 (&hf0)[2][KS], bf16x8 (&hf1)[2][KS]) {
       const int bg = col * G + g;
+      if constexpr (G == 1) {  // unconditional: a skipped layer reads an empty descriptor
+        const bool ring0 = tau > 0;
+        const __amdgpu_buffer_rsrc_t r0 =
+            !ld0 ? make_rsrc(a.hring0, 0)
+                 : ring0 ? make_rsrc(a.hring0 + (size_t)(tau & 1) * ringsz, sizeof(bf16) * ringsz)
+                         : make_rsrc(a.hbuf0, sizeof(bf16) * (size_t)B * hld);
+        const int s1 = tau - LAG;
+        const bool ring1 = s1 > 0;
+        const __amdgpu_buffer_rsrc_t r1 =
+            !ld1 ? make_rsrc(a.hring1, 0)
+                 : ring1 ? make_rsrc(a.hring1 + (size_t)(s1 & 1) * ringsz, sizeof(bf16) * ringsz)
+                         : make_rsrc(a.hbuf1, sizeof(bf16) * (size_t)B * hld);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {
+            const unsigned of = frag_load_off(2 * bg + j, w * KS + s, H, lane);
+            const unsigned orow = rmh_lane + rmh_off(bg, j, s);
+            hf0[j][s] = ld8_sc1(r0, ring0 ? of : orow);
+            hf1[j][s] = ld8_sc1(r1, ring1 ? of : orow);
+          }
+        return;
+      }
       if (ld0) {
         const bool ring0 = tau > 0;
         const __amdgpu_buffer_rsrc_t r0 =
@@ -320,9 +400,10 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
       }
     };
     load_group(0, pf0[0], pf1[0]);
+    if constexpr (DEFER) flush_rm();  // the previous tick's row-major copies
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      STAMPG(g, 7)  // group phase start
+      STAMPF(g, 7)  // group phase start
       const int bg = col * G + g;
       const int b = bg * 32 + 16 * J + (lane & 15);
       const bool live = b < B;
@@ -332,6 +413,14 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
       for (int gt = 0; gt < 4; ++gt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) zx[gt][r] = zxn[gt][r];
+      if (ZTAB && ztl && L == 0 && on0) {  // this row's table entry (padded rows: id 0, unused)
+        const float* zt = &ztab[idsl[tau * 32 + 16 * J + (lane & 15)] * kTabLd + 4 * (lane >> 4)];
+#pragma unroll
+        for (int gt = 0; gt < 4; ++gt) {
+          const float4 v = *reinterpret_cast<const float4*>(zt + 16 * gt);
+          zx[gt][0] = v.x; zx[gt][1] = v.y; zx[gt][2] = v.z; zx[gt][3] = v.w;
+        }
+      }
       bf16x8 (&hf0)[2][KS] = pf0[PREF ? (g & 1) : 0];
       bf16x8 (&hf1)[2][KS] = pf1[PREF ? (g & 1) : 0];
       if constexpr (PREF) {
@@ -425,9 +514,9 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
                 make_float4(acc[gt][0], acc[gt][1], acc[gt][2], acc[gt][3]);
         }
       }
-      STAMPG(g, 3)
+      STAMPF(g, 3)
       __syncthreads();
-      STAMPG(g, 4)
+      STAMPF(g, 4)
       // (G = 1) layer l+1's x-part of its step tau-1 (next tick) from slot tau of layer l
       auto do_stash = [&]() {
         if constexpr (G == 1) {
@@ -476,7 +565,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
           c[g][r] = gf[r] * c[g][r] + gi[r] * gj[r];
           h[r] = go[r] * tanhf_(c[g][r]);
         }
-        STAMPG(g, 5)
+        STAMPF(g, 5)
         st4bf_ho(loc, ringL + (size_t)((t + 1) & 1) * ringsz + frag_index(b, u0, H), h[0], h[1],
                  h[2], h[3]);
         // the stash MFMAs run while the ring stores drain; with dropout (LDS mask reads and
@@ -485,7 +574,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
         if (g == G - 1 && signal) {
           // one arrival per wave and tick, for all its groups' ring stores
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          STAMPG(g, 6)
+          STAMPF(g, 6)
           if (lane == 0) {
             unsigned* const c = (L ? cnt1 : cnt0) + (size_t)(t + 1) * 4;
             if (loc)
@@ -497,7 +586,20 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
           }
         }
         if (xdrop) do_stash();
-        if (live) {  // row-major copies for the GEMMs / head (not handed off)
+        if (DEFER) {  // row-major copies: stored behind the next tick's payload loads
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            rm_h[r] = f2bf(h[r]);
+            rm_c[r] = c[g][r];
+            rm_g[0][r] = f2bf(gi[r]); rm_g[1][r] = f2bf(gj[r]);
+            rm_g[2][r] = f2bf(gf[r]); rm_g[3][r] = f2bf(go[r]);
+          }
+          rm_t = t;
+          if (live && t == T - 1 && hlL)
+            *reinterpret_cast<float4*>(hlL + bh) = make_float4(h[0], h[1], h[2], h[3]);
+          if (live && t == T - 1 && clL)
+            *reinterpret_cast<float4*>(clL + bh) = make_float4(c[g][0], c[g][1], c[g][2], c[g][3]);
+        } else if (live) {  // row-major copies for the GEMMs / head (not handed off)
           const size_t o = (size_t)(t + 1) * B * H + bh;
           st4bf(hbL + ((size_t)(t + 1) * B + b) * hld + u0, h[0], h[1], h[2], h[3]);
           *reinterpret_cast<float4*>(cbL + o) = make_float4(c[g][0], c[g][1], c[g][2], c[g][3]);
@@ -518,6 +620,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
       }
     }
   }
+  if constexpr (DEFER) flush_rm();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -852,29 +955,32 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
 // DROP: the dropout instantiation (layer l+1's input masks in-kernel); without dropout that
 // code is compiled out (same-box A/B: the runtime-conditional form cost 2.5 % per step)
 template <int KS, bool DROP>
-static const void* lstm2_fwd_g(int G, bool xin) {
-  if (xin) return G == 1 ? (const void*)lstm2_fwd_persist_kernel<KS, 1, DROP, true> : nullptr;
+static const void* lstm2_fwd_g(int G, bool xin, bool diag) {
+  if (xin) return G == 1 ? (const void*)lstm2_fwd_persist_kernel<KS, 1, DROP, true, false> : nullptr;
   switch (G) {
-    case 1: return (const void*)lstm2_fwd_persist_kernel<KS, 1, DROP, false>;
-    case 2: return (const void*)lstm2_fwd_persist_kernel<KS, 2, DROP, false>;
-    case 3: return (const void*)lstm2_fwd_persist_kernel<KS, 3, DROP, false>;
-    case 4: return (const void*)lstm2_fwd_persist_kernel<KS, 4, DROP, false>;
+    case 1:
+      // (the stamped instantiation exists for the stamp-diagnosed shape only)
+      if (diag && !DROP) return (const void*)lstm2_fwd_persist_kernel<KS, 1, DROP, false, true>;
+      return (const void*)lstm2_fwd_persist_kernel<KS, 1, DROP, false, false>;
+    case 2: return (const void*)lstm2_fwd_persist_kernel<KS, 2, DROP, false, false>;
+    case 3: return (const void*)lstm2_fwd_persist_kernel<KS, 3, DROP, false, false>;
+    case 4: return (const void*)lstm2_fwd_persist_kernel<KS, 4, DROP, false, false>;
   }
   return nullptr;
 }
 
 template <bool DROP>
-static const void* lstm2_pick_t(int H, int G, bool xin) {
+static const void* lstm2_pick_t(int H, int G, bool xin, bool diag) {
   switch (H / 128) {
-    case 1: return lstm2_fwd_g<1, DROP>(G, xin);
-    case 2: return lstm2_fwd_g<2, DROP>(G, xin);
-    case 3: return lstm2_fwd_g<3, DROP>(G, xin);
-    case 4: return lstm2_fwd_g<4, DROP>(G, xin);
+    case 1: return lstm2_fwd_g<1, DROP>(G, xin, diag);
+    case 2: return lstm2_fwd_g<2, DROP>(G, xin, diag);
+    case 3: return lstm2_fwd_g<3, DROP>(G, xin, diag);
+    case 4: return lstm2_fwd_g<4, DROP>(G, xin, diag);
   }
   return nullptr;
 }
-static const void* lstm2_pick(int H, int G, bool drop, bool xin = false) {
-  return drop ? lstm2_pick_t<true>(H, G, xin) : lstm2_pick_t<false>(H, G, xin);
+static const void* lstm2_pick(int H, int G, bool drop, bool xin = false, bool diag = false) {
+  return drop ? lstm2_pick_t<true>(H, G, xin, diag) : lstm2_pick_t<false>(H, G, xin, diag);
 }
 
 // the in-kernel input projection variant exists and is co-resident (G = 1 only); the answer
@@ -964,7 +1070,7 @@ int launch_lstm2_fwd_persist(const Lstm2Args& a, int cus, hipStream_t s) {
   if (!lstm2_args_ok(a.H, a.B, a.nbg, a.G, cus) || !a.hring0 || !a.hring1) return -2;
   void* args[] = {const_cast<Lstm2Args*>(&a)};
   if (a.x0 && (a.G != 1 || !lstm2_xin_ok(a.H, cus))) return -2;
-  const void* fn = lstm2_pick(a.H, a.G, a.xmask != nullptr, a.x0 != nullptr);
+  const void* fn = lstm2_pick(a.H, a.G, a.xmask != nullptr, a.x0 != nullptr, a.diag != nullptr);
   return hipLaunchKernel(fn, dim3(lstm2_grid(fn, a.H, a.nbg, a.G, cus)), dim3(256), args, 0, s) ==
                  hipSuccess ? 0 : -3;
 }

@@ -934,6 +934,7 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
   dcr::Lstm2Args a{};
   a.W0T = ptr<bf16>(W0T); a.W1T = ptr<bf16>(W1T); a.X1T = ptr<bf16>(X1T);
   a.zx0 = xin ? nullptr : ptr<float>(zx0); a.ids = optr<int>(ids); a.zx_ld = 4 * H;
+  a.zx_rows = (!xin && has(ids)) ? (int)(zx0.numel() / (4 * H)) : 0;
   a.x0 = optr<bf16>(x0); a.X0T = optr<bf16>(X0T);
   a.hld = (int)hbuf0.stride(1);
   a.bias1 = ptr<float>(bias1);
