@@ -40,15 +40,17 @@ namespace dcr {
 // whole chip) at the same points, except that slot 5 is layer l+1's hand-off arrival (wave 2)
 // and slot 6 layer l's (wave 0): the cross-workgroup skew of every tick (scripts/pair_bench.py
 // --skew).
+// (only in the DIAG instantiations: a conditional store between the payload loads and the MFMAs
+// degrades the compiler's waitcnt counts to vmcnt(0), see PF = 5)
 #define STAMPW(i)                                                                    \
-  if (a.diag && threadIdx.x == 0 && (i) != 5 && (i) != 6) {                          \
+  if (DIAG && a.diag && threadIdx.x == 0 && (i) != 5 && (i) != 6) {                  \
     if (a.diag_all)                                                                  \
       a.diag[((size_t)blockIdx.x * (T + 2) + tau) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
     else if (blockIdx.x == 0)                                                        \
       a.diag[(size_t)tau * 8 + (i)] = __builtin_amdgcn_s_memtime();                  \
   }
 #define STAMP_ARRIVE()                                                               \
-  if (a.diag && lane == 0 && (w == 0 || w == 2)) {                                   \
+  if (DIAG && a.diag && lane == 0 && (w == 0 || w == 2)) {                           \
     if (a.diag_all)                                                                  \
       a.diag[((size_t)blockIdx.x * (T + 2) + tau) * 8 + (w ? 5 : 6)] =               \
           __builtin_amdgcn_s_memrealtime();                                          \
@@ -103,10 +105,14 @@ __device__ __forceinline__ float row_reduce_scatter16(float (&v)[16], int lane) 
 //   5: 1's operand loads, plus the row-major dZ copy of the PREVIOUS tick stored behind the
 //      payload loads (kept packed in registers across the tick boundary) and layer l's dtop
 //      stash in front of the arrival (its MFMAs overlapping the ring stores' drain), so that no
-//      store sits in front of the next poll.  Measured slower (1.630 vs 1.619 ms/step against
-//      2): the compiler's waitcnt analysis cannot count the conditional stores, so the MFMA
-//      phase's wait became vmcnt(0) and covered them, and the drain waited for the HBM loads.
-template <int KS, bool DROP, int PF>
+//      store sits in front of the next poll.  Every vector-memory operation from the payload
+//      loads to the MFMAs is unconditional (empty descriptors / out-of-range offsets instead of
+//      branches): with conditional ones the compiler's waitcnt analysis assumes the path
+//      without them and the MFMA phase's waits degrade to vmcnt(0), covering the stores (the
+//      first form of this order measured 1.630 vs 1.619 ms/step against 2 for that reason).
+//      Still slower than 1 (1.55 vs 1.52 ms/step, same box): the drain before the arrival now
+//      waits for the HBM operand loads and the deferred stores (3.4 k cycles incl. the stash).
+template <int KS, bool DROP, int PF, bool DIAG>
 __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) {
   static_assert(KS % 4 == 0, "K quarter = whole 32-wide k-steps per gate");
   // partials [wave][layer][unit half][lane][4]
@@ -181,12 +187,15 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
   // PF = 5: the previous tick's row-major dZ values (bf16, as st4bf rounds them) and their step
   bf16x4 dzp[4];
   int tpend = -1;
-  auto flush_dz = [&]() {
-    if (tpend >= 0 && live) {
-      bf16* dz = dzL + ((size_t)tpend * B + b) * G4H + u0;
+  constexpr unsigned kOut = 0x7FFFFFF0u;  // an out-of-range buffer offset: dropped / reads 0
+  const __amdgpu_buffer_rsrc_t rdz = make_rsrc(dzL, sizeof(bf16) * (size_t)T * B * G4H);
+  auto flush_dz = [&]() {  // (unconditional: see PF = 5)
+    const unsigned o = (tpend >= 0 && live)
+                           ? (unsigned)((((size_t)tpend * B + b) * G4H + u0) * sizeof(bf16)) : kOut;
 #pragma unroll
-      for (int gt = 0; gt < 4; ++gt) *reinterpret_cast<bf16x4*>(dz + gt * H) = dzp[gt];
-    }
+    for (int gt = 0; gt < 4; ++gt)
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, dzp[gt]), rdz,
+                                            o + gt * H * (unsigned)sizeof(bf16), 0, 0);
     tpend = -1;
   };
   // layer l's dtop partial of its NEXT tick (this wave's K quarter, both unit halves), computed
@@ -209,7 +218,38 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
   const unsigned vg = opaque_vgpr((unsigned)(((size_t)b * G4H + u0) * sizeof(bf16)));
   const unsigned vc = opaque_vgpr((unsigned)(bh * sizeof(float)));
   const unsigned vm = (unsigned)(b * (H / 8) + (ub0 >> 3));
+  const __amdgpu_buffer_rsrc_t rdL = make_rsrc(a.dtop1, L ? sizeof(float) * (size_t)T * B * H : 0);
+  auto prefetch_u = [&](int tk) {  // PF = 5: unconditional, out-of-range lanes read zero
+    const int tt = L ? T - 1 - tk : T + 1 - tk;
+    const bool ac = L ? tk < T : tk >= 2;
+    const unsigned vgo = (ac && live) ? vg : kOut, vco = (ac && live) ? vc : kOut;
+    const unsigned sg = ac ? (unsigned)((size_t)tt * B * G4H * sizeof(bf16)) : 0u;
+    const unsigned sc = ac ? (unsigned)((size_t)tt * B * H * sizeof(float)) : 0u;
+#pragma unroll
+    for (int gt = 0; gt < 4; ++gt)
+      g4[gt] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(
+                                              rg, vgo, sg + gt * H * (unsigned)sizeof(bf16), 0));
+    const f32x4 c1 = __builtin_bit_cast(
+        f32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, vco, sc + B * H * (unsigned)sizeof(float), 0));
+    const f32x4 c0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, vco, sc, 0));
+    const f32x4 d = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rdL, vco, sc, 0));
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      cc[r] = c1[r];
+      cp[r] = c0[r];
+      dtop[r] = d[r];
+    }
+    if (DROP) {
+      const bool md = tk >= 2 && tk <= T + 1 && live;
+      mrow = __builtin_amdgcn_raw_buffer_load_b32(
+          rm, md ? vm : kOut, md ? (unsigned)((size_t)(T + 1 - tk) * B * (H / 8)) : 0u, 0);
+    }
+  };
   auto prefetch = [&](int tk) {
+    if constexpr (PF == 5) {
+      prefetch_u(tk);
+      return;
+    }
     const int tt = L ? T - 1 - tk : T + 1 - tk;
     const bool ac = L ? tk < T : tk >= 2;
 #pragma unroll
@@ -277,15 +317,26 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
     if (tau >= 1) {
       const unsigned o1 = (unsigned)((s1 & 1) * slabn * sizeof(bf16));
       const unsigned o0 = (unsigned)((s0 & 1) * slabn * sizeof(bf16));
-      if (ld1) {
+      if constexpr (PF == 5) {  // unconditional: a skipped layer reads an empty descriptor
+        const __amdgpu_buffer_rsrc_t r1e = ld1 ? rz1 : make_rsrc(a.zring1, 0);
+        const __amdgpu_buffer_rsrc_t r0e = ld0 ? rz0 : make_rsrc(a.zring0, 0);
 #pragma unroll
         for (int s = 0; s < KS; ++s)
-          p1[s] = ld8_sc1(rz1, frag_load_off(col, kcol(s) >> 5, G4H, lane) + o1);
-      }
-      if (ld0) {
+          p1[s] = ld8_sc1(r1e, frag_load_off(col, kcol(s) >> 5, G4H, lane) + o1);
 #pragma unroll
         for (int s = 0; s < KS; ++s)
-          p0[s] = ld8_sc1(rz0, frag_load_off(col, kcol(s) >> 5, G4H, lane) + o0);
+          p0[s] = ld8_sc1(r0e, frag_load_off(col, kcol(s) >> 5, G4H, lane) + o0);
+      } else {
+        if (ld1) {
+#pragma unroll
+          for (int s = 0; s < KS; ++s)
+            p1[s] = ld8_sc1(rz1, frag_load_off(col, kcol(s) >> 5, G4H, lane) + o1);
+        }
+        if (ld0) {
+#pragma unroll
+          for (int s = 0; s < KS; ++s)
+            p0[s] = ld8_sc1(rz0, frag_load_off(col, kcol(s) >> 5, G4H, lane) + o0);
+        }
       }
       if (PF == 1 || PF == 5 || (PF == 3 && w == 0)) prefetch(tau);
       if constexpr (PF == 5) flush_dz();  // last tick's dZ rows, behind this tick's loads
@@ -399,7 +450,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
         df_[r] = dcv * cp[r] * gf * (1.f - gf);
         dc[r] = dcv * gf;
       }
-      if (a.diag && !a.diag_all && blockIdx.x == 0 && threadIdx.x == 0)
+      if (DIAG && a.diag && !a.diag_all && blockIdx.x == 0 && threadIdx.x == 0)
         a.diag[(size_t)tau * 8 + 5] = __builtin_amdgcn_s_memtime();
       // layer l+1's dZ_t feeds both layers at the next tick (t >= 0); layer l's only itself
       if (L || t >= 1) {
@@ -514,19 +565,23 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
   }
 }
 
-template <bool DROP, int PF>
+template <bool DROP, int PF, bool DIAG = false>
 static const void* lstm2_bwd_wide_pick_t(int H) {
   switch (H / 32) {  // KS = 4H / 4 waves / 32
-    case 4: return (const void*)lstm2_bwd_wide_kernel<4, DROP, PF>;
-    case 8: return (const void*)lstm2_bwd_wide_kernel<8, DROP, PF>;
-    case 12: return (const void*)lstm2_bwd_wide_kernel<12, DROP, PF>;
-    case 16: return (const void*)lstm2_bwd_wide_kernel<16, DROP, PF>;
+    case 4: return (const void*)lstm2_bwd_wide_kernel<4, DROP, PF, DIAG>;
+    case 8: return (const void*)lstm2_bwd_wide_kernel<8, DROP, PF, DIAG>;
+    case 12: return (const void*)lstm2_bwd_wide_kernel<12, DROP, PF, DIAG>;
+    case 16: return (const void*)lstm2_bwd_wide_kernel<16, DROP, PF, DIAG>;
   }
   return nullptr;
 }
+constexpr int kWidePfDefault = 1;
+// diag: the stamped instantiation (the default operand order, no dropout)
 template <bool DROP>
-static const void* lstm2_bwd_wide_pick(int H) {
-  switch (debug_int("wide_pf", 1)) {
+static const void* lstm2_bwd_wide_pick(int H, bool diag = false) {
+  const int pf = debug_int("wide_pf", kWidePfDefault);
+  if (diag && !DROP && pf == kWidePfDefault) return lstm2_bwd_wide_pick_t<false, kWidePfDefault, true>(H);
+  switch (pf) {
     case 0: return lstm2_bwd_wide_pick_t<DROP, 0>(H);
     case 2: return lstm2_bwd_wide_pick_t<DROP, 2>(H);
     case 3: return lstm2_bwd_wide_pick_t<DROP, 3>(H);
@@ -555,7 +610,8 @@ bool lstm2_bwd_wide_ok(int H, int B, int cus) {
 int launch_lstm2_bwd_wide(const Lstm2BwdArgs& a, int cus, hipStream_t s) {
   if (!lstm2_bwd_wide_ok(a.H, a.B, cus) || a.nbg != (a.B + 15) / 16) return -2;
   void* args[] = {const_cast<Lstm2BwdArgs*>(&a)};
-  const void* fn = a.xmask ? lstm2_bwd_wide_pick<true>(a.H) : lstm2_bwd_wide_pick<false>(a.H);
+  const void* fn = a.xmask ? lstm2_bwd_wide_pick<true>(a.H)
+                          : lstm2_bwd_wide_pick<false>(a.H, a.diag != nullptr);
   // the XCD-padded grid (persist_common.h xcd_grid) when it is co-resident
   int grid = (a.H / 32) * a.nbg, o = 0;
   const int padded = xcd_grid(a.H / 32, a.nbg);

@@ -39,7 +39,8 @@ DEBUG_KEYS = {
               "XCD-resident form (plain payload, L2 flags) on single-XCD columns (C++ launcher)",
     "wide_pf": "wide BPTT epilogue-operand loads: 0 before the poll, 1 (default) after the "
                "payload, 2 one tick ahead, 3 / 4 poller-wave variants, 5 1 + the row-major dZ "
-               "copy deferred behind the next payload + the dtop stash inside the drain (C++)",
+               "copy deferred behind the next payload + the dtop stash inside the drain, all "
+               "unconditional (exact waitcnt) (C++)",
     "fused_head": "0: library logits GEMM + CE kernel instead of the fused head",
     "dew": "layer-0 embedding-table gradient: gemm (one-hot MFMA GEMM, default) | segsum | fused",
     "side": "0: no side-stream weight GEMMs in overlap mode",
