@@ -3,60 +3,87 @@
 // Reference: the weight gradients of the unrolled cell (tf.gradients through model.py:72, summed
 // over all T x B tokens).  Both operands lie token-major in memory (A = h_{t-1} or the layer input
 // [K tokens, M], B = dZ [K tokens, N]), i.e. K is the OUTER index of both, so neither is an MFMA
-// fragment as stored.  Each workgroup streams [32 x 256] k-row panels of A and B through LDS as
-// they lie in memory (coalesced 512-B rows) and reads them back transposed with
-// ds_read_b64_tr_b16 (CDNA4's transposing LDS read), which hands every lane the 8 consecutive-k
-// bf16 values of one m (or n) -- exactly the A / B fragment of v_mfma_f32_16x16x32_bf16.
+// fragment as stored.  Each workgroup streams [32 x 256] k-row panels of A and B into LDS as they
+// lie in memory and reads them back transposed with ds_read_b64_tr_b16 (CDNA4's transposing LDS
+// read), which hands every lane the consecutive-k bf16 values of one m (or n) -- the A / B
+// fragment of v_mfma_f32_16x16x32_bf16.
 //
-// Tiling.  A workgroup owns a 256 x 256 output tile (4 waves of 128 x 128 = 8 x 8 MFMA tiles, 256
-// fp32 accumulators per lane) and one K chunk (split-K slab s); the slabs are summed by the
-// step's prep flush (prep.hip SUM), so every output element has one fixed summation order.  The
-// 256 x 256 tile halves the operand traffic of a 256 x 128 library tile (the three headline
-// gradients are operand-stream bound: 2 x 32768 x (512 + 2048) bf16 per GEMM, read by every
-// tile of a row / column).  Workgroups of one (problem, slab) -- which share their A and B panels
-// -- are placed on one XCD (round-robin dispatch), so those panels are fetched into one L2.
+// Tiling.  A workgroup owns a 256 x 256 output tile (8 waves of 128 x 64 = 8 x 4 MFMA tiles, 128
+// fp32 accumulators per lane; two waves per SIMD, so one wave's LDS reads and barrier waits
+// hide under the other's MFMAs -- 4 waves of 128 x 128 with one fragment set ran at 870 TF/s,
+// and a second fragment set did not fit beside 256 accumulators) and one K chunk (split-K slab
+// s); the slabs are summed by the step's prep flush (prep.hip SUM), so every output element has
+// one fixed summation order.
+// Workgroups of one (problem, slab) -- which share their A and B panels -- are placed on one XCD
+// (round-robin dispatch), so those panels are fetched into one L2.
 //
-// LDS layout.  A stage holds 32 k-rows of 256 bf16 at a row stride of 272 bf16 (136 dwords =
-// 8 mod 64 banks).  The 8 k values of lane group q (lanes 16q .. 16q+15) are the k-rows
-// {b_q .. b_q+3} (lo read) and {b_q+8 .. b_q+11} (hi read), b_q = 4q + 8 (q >> 1): the 32 lanes
-// of each half-wave then hit 64 distinct banks.  A and B use the same k permutation, so the
-// products are unchanged.  Two stages (69.6 KB), one barrier per k step; the next stage's global
-// loads are issued before the current stage's MFMAs and written to LDS after them.
+// Pipeline (v2).  The panels arrive by LDS-DMA (buffer_load ... lds, 16 B per lane, 1 KB = two
+// k-rows per instruction) into a ring of kWgStages 32 KB stages, kWgStages - 1 of them in
+// flight (v1 staged through registers one k-step ahead, too short to cover an L2 / HBM round
+// trip).  A wave's DMA count per stage is fixed (4), so the wait for a stage is a counted vmcnt;
+// the DMA is inline asm, invisible to the compiler's waitcnt pass, which would otherwise wait
+// vmcnt(0) for the whole ring before every LDS read.
 //
-// Measured (scripts/micro/wgrad_bench.py, same box as the library form): the three headline
-// gradients in one launch 230 us vs 279 us as split-K library bmm's in isolation, but on par in
-// the training step (228 vs ~220 us: there the library GEMMs find dZ partly in L2 / MALL right
-// after the BPTT), so the step keeps the library GEMMs by default (DCR_DEBUG=wgrad=1 selects this
-// kernel).  Rejected variants: BK = 64 (274 us), a second register stage (spills), a 4-stage
-// LDS-DMA pipeline with counted vmcnt and raw barriers (312 vs 299 us library on its box).
+// Measured (scripts/micro/wgrad2_bench.py, slabs only, 32768 tokens): [1024 x 2048] 140 vs
+// 150 us for the library split-K bmm, [2048 x 8192] 955 vs 968 us, [512 x 2048] 85 vs 80 us,
+// [1024 x 3072] 209 vs 203 us: at parity (46 % of the MFMA peak on the large shape), so the step
+// keeps the library form by default (DCR_DEBUG=wgrad=1 selects this kernel).
+//
+// LDS layout.  Row r of a stage holds 256 bf16 (32 chunks of 16 B, no padding); logical chunk c
+// sits at physical chunk c ^ f(r), f(r) = 2 (r & 7) + ((r >> 4) & 1).  One transposed read of a
+// 16-column tile touches rows {b_q + a} = {0..7, 16..23} (+ 8 for the high half) and two chunks
+// per row: under f the 32 (row, chunk) pairs cover each of the 16 bank groups exactly twice -- the
+// 2-pass minimum for 512 B -- where the unswizzled rows would all hit the same 8 banks.  The DMA
+// writes each lane's 16 B to physical position lane, so a lane fetches the logical chunk that
+// belongs there (the global reads stay two whole 512-B rows per instruction).
 #include "common.h"
 #include "kernels.h"
 
 namespace dcr {
 
-constexpr int kWgTile = 256;             // output tile edge (M and N)
-constexpr int kWgK = 32;                 // k rows per stage (one MFMA k step)
-constexpr int kWgLd = kWgTile + 16;      // LDS row stride (bf16): 136 dwords = 8 mod 64
+constexpr int kWgTile = 256;   // output tile edge (M and N)
+constexpr int kWgK = 32;       // k rows per stage (one MFMA k step)
+constexpr int kWgStages = 4;   // LDS ring stages (kWgStages - 1 in flight)
+constexpr int kWgStageB = 2 * kWgK * kWgTile * 2;  // bytes per stage (A + B panels)
+constexpr int kWgWaves = 8;                        // 2 per SIMD: one's LDS reads hide under the other's MFMAs
+constexpr int kWgDmaPerWave = 32 / kWgWaves;       // DMA instructions per wave and stage
 
+__device__ __forceinline__ int wg_swz(int r) { return 2 * (r & 7) + ((r >> 4) & 1); }
+
+// raw barrier: __syncthreads()' release fence would wait vmcnt(0) for the in-flight ring
+__device__ __forceinline__ void wg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ void wg_vm_wait(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+  }
+}
+// transposed 64-bit LDS read: 4 bf16 of 4 consecutive k for this lane's m (compiler-visible;
+// the ring's DMA is not, see wg_dma)
 typedef short s16x4_wg __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ bf16x8 wg_frag(const bf16* base) {
-  // base = &stage[b_q + a][col0 + 4 p]  for lane 16q + 4a + p
-  const s16x4_wg lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) s16x4_wg*)base);
-  const s16x4_wg hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) s16x4_wg*)(base + 8 * kWgLd));
-  u32x4 u;
-  u[0] = (unsigned)(unsigned short)lo[0] | ((unsigned)(unsigned short)lo[1] << 16);
-  u[1] = (unsigned)(unsigned short)lo[2] | ((unsigned)(unsigned short)lo[3] << 16);
-  u[2] = (unsigned)(unsigned short)hi[0] | ((unsigned)(unsigned short)hi[1] << 16);
-  u[3] = (unsigned)(unsigned short)hi[2] | ((unsigned)(unsigned short)hi[3] << 16);
-  return __builtin_bit_cast(bf16x8, u);
+__device__ __forceinline__ u32x2 wg_rd_tr(unsigned addr) {
+  return __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                                       (__attribute__((address_space(3))) s16x4_wg*)(size_t)addr));
+}
+// one LDS-DMA instruction (16 B per lane to LDS address lds + 16 lane), issued as inline asm so
+// that the compiler's waitcnt pass does not see an LDS write: it would otherwise wait vmcnt(0)
+// for the whole ring before every LDS read.  The stage waits are the counted wg_vm_wait; the
+// "memory" clobbers keep every LDS read of a slot on its side of the barriers.  (The kernel has
+// no other M0 user.)
+__device__ __forceinline__ void wg_dma(__amdgpu_buffer_rsrc_t r, unsigned lds, unsigned voff,
+                                       unsigned soff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               :: "s"(lds), "v"(voff), "s"(r), "s"(soff) : "memory");
 }
 
-__global__ void __launch_bounds__(256, 1) wgrad_kernel(WgradArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16 lds[2][2][kWgK][kWgLd];  // [stage][A/B][k][col]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+__global__ void __launch_bounds__(64 * kWgWaves, kWgWaves / 4) wgrad_kernel(WgradArgs a) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[kWgStages * kWgStageB];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // block -> (group = (problem, slab), tile in group); a group's tiles on one XCD
   const int nb = gridDim.x;
   const int lin = (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8;
@@ -68,60 +95,107 @@ __global__ void __launch_bounds__(256, 1) wgrad_kernel(WgradArgs a) {
   const int m0 = (tile / tn) * kWgTile, n0 = (tile % tn) * kWgTile;
   const int ksteps = a.K / kWgK;
   const int kt0 = (int)((long)ksteps * s / a.S), kt1 = (int)((long)ksteps * (s + 1) / a.S);
+  const int nk = kt1 - kt0;
 
-  // staging: thread t -> k-row (t >> 5) + 8 j, columns 8 (t & 31) .. +7, for j < 4
-  const int srow = threadIdx.x >> 5, scol = 8 * (threadIdx.x & 31);
-  const bf16* ga = P.A + (size_t)srow * P.lda + m0 + scol;
-  const bf16* gb = P.B + (size_t)srow * P.ldb + n0 + scol;
-  bf16x8 st[2][4];  // [A/B][j]
-  auto fetch = [&](int kt) {
-    const size_t k0 = (size_t)kt * kWgK;
+  // DMA: wave w fills k-rows [4 w, 4 w + 4) of both panels, 2 rows per instruction; lane l
+  // writes physical chunk (l & 31) of row 4 w + 2 j + (l >> 5)
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16*>(P.A), (short)0, 0x7FFFFFF0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16*>(P.B), (short)0, 0x7FFFFFF0, 0x00020000);
+  unsigned offa[kWgDmaPerWave / 2], offb[kWgDmaPerWave / 2];  // k-step 0 (+ kt * 32 rows)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      st[0][j] = ld8(ga + (k0 + 8 * j) * P.lda);
-      st[1][j] = ld8(gb + (k0 + 8 * j) * P.ldb);
+  for (int j = 0; j < kWgDmaPerWave / 2; ++j) {
+    const int r = (kWgDmaPerWave) * w + 2 * j + (lane >> 5);
+    const int c = (lane & 31) ^ wg_swz(r);  // logical chunk stored at this physical position
+    offa[j] = (unsigned)(((size_t)r * P.lda + m0 + 8 * c) * sizeof(bf16));
+    offb[j] = (unsigned)(((size_t)r * P.ldb + n0 + 8 * c) * sizeof(bf16));
+  }
+  const unsigned lds0 = (unsigned)(size_t)(const __attribute__((address_space(3))) void*)lds;
+  auto issue = [&](int kt) {  // stage kt into ring slot kt % kWgStages
+    const unsigned st = lds0 + ((kt - kt0) % kWgStages) * kWgStageB;
+    const unsigned sa = (unsigned)((size_t)kt * kWgK * P.lda * sizeof(bf16));
+    const unsigned sb = (unsigned)((size_t)kt * kWgK * P.ldb * sizeof(bf16));
+#pragma unroll
+    for (int j = 0; j < kWgDmaPerWave / 2; ++j) {
+      const unsigned r = (unsigned)(kWgDmaPerWave * w + 2 * j);
+      wg_dma(ra, st + r * 512, offa[j], sa);
+      wg_dma(rb, st + kWgK * 512 + r * 512, offb[j], sb);
     }
   };
-  auto stash = [&](int buf) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      *reinterpret_cast<bf16x8*>(&lds[buf][0][srow + 8 * j][scol]) = st[0][j];
-      *reinterpret_cast<bf16x8*>(&lds[buf][1][srow + 8 * j][scol]) = st[1][j];
-    }
-  };
 
-  // fragment read addresses: lane 16q + 4a + pp reads k-row b_q + a, columns 4 pp .. +3 of
-  // its 16-column tile
+  // fragment read addresses: lane 16q + 4ta + tp reads k-row b_q + ta (lo; + 8 hi), m columns
+  // 4 tp .. +3 of its 16-column tile; byte address within a stage panel
   const int q = lane >> 4, ta = (lane & 15) >> 2, tp = lane & 3;
   const int bq = 4 * q + 8 * (q >> 1);
-  const int wm = 128 * (w >> 1), wn = 128 * (w & 1);
-  f32x4 acc[8][8];
+  // wave w: 128 (M) x 64 (N) of the tile = 8 x 4 MFMA tiles
+  const int wm = 128 * (w >> 2), wn = 64 * (w & 3);
+  // tile i's column chunk is cbase + 2 i with cbase = wm / 8 + tp / 2 in {0, 1, 16, 17}: no bit
+  // overlaps 2 i, so its physical chunk is (cbase ^ f(row)) ^ 2 i -- one XOR per read, and only
+  // two per-lane constants per half (lo / hi row) instead of 32 addresses
+  const int cb_a = (wm >> 3) + (tp >> 1), cb_b = (wn >> 3) + (tp >> 1);
+  unsigned rowb[2], xa[2], xb[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = bq + ta + 8 * h;
+    rowb[h] = (unsigned)(row * 512 + ((tp & 1) << 3));
+    xa[h] = (unsigned)(cb_a ^ wg_swz(row));
+    xb[h] = (unsigned)(cb_b ^ wg_swz(row));
+  }
+  auto read_frags = [&](int kt, u32x4 (&fa)[8], u32x4 (&fb)[4]) {
+    const unsigned base = lds0 + ((kt - kt0) % kWgStages) * kWgStageB;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const u32x2 lo = wg_rd_tr(base + rowb[0] + ((xa[0] ^ (2u * i)) << 4));
+      const u32x2 hi = wg_rd_tr(base + rowb[1] + ((xa[1] ^ (2u * i)) << 4));
+      fa[i] = u32x4{lo[0], lo[1], hi[0], hi[1]};
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const u32x2 lo = wg_rd_tr(base + kWgK * 512 + rowb[0] + ((xb[0] ^ (2u * j)) << 4));
+      const u32x2 hi = wg_rd_tr(base + kWgK * 512 + rowb[1] + ((xb[1] ^ (2u * j)) << 4));
+      fb[j] = u32x4{lo[0], lo[1], hi[0], hi[1]};
+    }
+  };
+
+  f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (kt0 < kt1) {
-    fetch(kt0);
-    stash(0);
+  // prologue: the first kWgStages stages in flight, stage 0 landed everywhere, its fragments read
+  u32x4 fa0[8], fb0[4], fa1[8], fb1[4];
+  if (nk > 0) {
+    const int pro = nk < kWgStages ? nk : kWgStages;
+    for (int j = 0; j < pro; ++j) issue(kt0 + j);
+    wg_vm_wait((pro - 1) * kWgDmaPerWave);
+    wg_barrier();
+    read_frags(kt0, fa0, fb0);
   }
-  __syncthreads();
-  for (int kt = kt0; kt < kt1; ++kt) {
-    const int buf = (kt - kt0) & 1;
-    if (kt + 1 < kt1) fetch(kt + 1);
-    const bf16* la = &lds[buf][0][bq + ta][wm + 4 * tp];
-    const bf16* lb = &lds[buf][1][bq + ta][wn + 4 * tp];
-    bf16x8 fa[8], fb[8];
+  // k-step i: its fragments are in (fa, fb); stage i+1's are read into (na, nb) under its MFMAs
+  // (two statically indexed register sets: the loop runs two k-steps per trip)
+  auto kstep = [&](int i, u32x4 (&fa)[8], u32x4 (&fb)[4], u32x4 (&na)[8], u32x4 (&nb)[4]) {
+    const int kt = kt0 + i;
+    if (i + 1 < nk) {
+      // stage kt+1 landed (the later in-flight stages may stay outstanding), visible to every
+      // wave; stage kt's slot was read by every wave before this barrier: refill it
+      const int later = nk - 2 - i < kWgStages - 2 ? nk - 2 - i : kWgStages - 2;
+      wg_vm_wait(later * kWgDmaPerWave);
+      wg_barrier();
+      if (i + kWgStages < nk) issue(kt + kWgStages);
+      read_frags(kt + 1, na, nb);
+    }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) fa[i] = wg_frag(la + 16 * i);
+    for (int ii = 0; ii < 8; ++ii)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) fb[j] = wg_frag(lb + 16 * j);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(fa[i], fb[j], acc[i][j]);
-    if (kt + 1 < kt1) stash(buf ^ 1);  // that stage was last read before the previous barrier
-    __syncthreads();
+      for (int jj = 0; jj < 4; ++jj)
+        acc[ii][jj] = mfma16(__builtin_bit_cast(bf16x8, fa[ii]), __builtin_bit_cast(bf16x8, fb[jj]),
+                             acc[ii][jj]);
+  };
+  for (int i = 0; i < nk; i += 2) {
+    kstep(i, fa0, fb0, fa1, fb1);
+    if (i + 1 < nk) kstep(i + 1, fa1, fb1, fa0, fb0);
   }
 
   // D[4q + r][l & 15] of tile (i, j): row m0 + wm + 16 i + 4 q + r, column n0 + wn + 16 j + l%16
@@ -131,14 +205,14 @@ __global__ void __launch_bounds__(256, 1) wgrad_kernel(WgradArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) c[(size_t)(16 * i + r) * P.ldc + 16 * j] = acc[i][j][r];
+      for (int j = 0; j < 4; ++j) c[(size_t)(16 * i + r) * P.ldc + 16 * j] = acc[i][j][r];
 }
 
 bool wgrad_supported(int M, int N, int K) {
   return M > 0 && N > 0 && M % kWgTile == 0 && N % kWgTile == 0 && K % kWgK == 0 && K > 0;
 }
 
-// Slabs per problem.  One workgroup per CU (256 accumulators per lane), so a grid of np x tiles x S
+// Slabs per problem.  One workgroup per CU (128 KB of LDS ring), so a grid of np x tiles x S
 // workgroups runs in ceil(blocks / cus) rounds; pick the S with the best CU utilisation
 // blocks / (rounds x cus), less 1 % per slab (each slab is an extra M x N fp32 write + read in the
 // flush), each slab at least 1024 tokens deep.  (A second partial round costs a full round:
@@ -163,7 +237,7 @@ int wgrad_splits(int np, int M, int N, int K, int cus) {
 void launch_wgrad(const WgradArgs& a, hipStream_t s) {
   const int blocks = a.np * a.S * a.tiles;
   const int grid = (blocks + 7) / 8 * 8;
-  wgrad_kernel<<<grid, 256, 0, s>>>(a);
+  wgrad_kernel<<<grid, 64 * kWgWaves, 0, s>>>(a);
 }
 
 }  // namespace dcr

@@ -1,6 +1,7 @@
 #!/bin/bash
 # rocprofv3 PMC passes over a short headline bench run (one counter group per run, each under
 # its own time limit; the slot limits of MI355X_MICROARCH.md "rocprofv3 PMC slots").
+# PMC_SCRIPT=<script.py> profiles another python script instead of bench.py.
 set -o pipefail
 export TMPDIR=/tmp PYTHONPATH=$PWD
 D=${1:-gpurun_out/pmc}; shift
@@ -16,6 +17,6 @@ for pass in \
   i=$((i+1))
   echo "== pass $i: $pass"
   timeout -s KILL 90 rocprofv3 --pmc $pass -d $D/p$i -o run --output-format csv -- \
-    python3 bench.py $BA > $D/p$i.log 2>&1 || { tail -5 $D/p$i.log; exit 1; }
+    python3 ${PMC_SCRIPT:-bench.py} $BA > $D/p$i.log 2>&1 || { tail -5 $D/p$i.log; exit 1; }
 done
 echo done
