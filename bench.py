@@ -95,11 +95,12 @@ def main(argv=None) -> int:
                       output_keep_prob=a.output_keep_prob)
     model = CharRNN(cfg, device=device, seed=1234)
     opt = TFAdam(model.store, clip=5.0, guard=model.error_word())
-    sharded = a.dp_mode == "sharded" and world > 1
+    # (--force_sync: the exchange also runs on one rank, sharded or replicated)
+    sharded = a.dp_mode == "sharded" and (world > 1 or a.force_sync)
     sync = GradSync(model.store, world, a.bucket_mb, a.allreduce_dtype,
                     enabled=(world > 1 or a.force_sync) and not sharded,
                     guard=model.error_word(), timing=a.profile)
-    if a.force_sync and a.graph:
+    if (a.force_sync or sharded) and a.graph:
         # the captured step never calls sync.ready, so nothing would write the guard slot and
         # the exchange would not be measured at all
         raise SystemExit("bench.py: --force_sync measures the eager bucketed exchange; "
@@ -155,8 +156,14 @@ def main(argv=None) -> int:
             return graphed(x, y, state, 2e-3)
         if zstep is not None:  # each bucket's reduce-scatter leaves during the backward
             zstep.reset()
-            loss, state, _ = model.train_step(x, y, state, zstep)
-            zstep.step(2e-3)
+            if prof is None:
+                loss, state, _ = model.train_step(x, y, state, zstep)
+                zstep.step(2e-3)
+            else:
+                with prof.phase("fwd_bwd"):
+                    loss, state, _ = model.train_step(x, y, state, zstep)
+                with prof.phase("sharded_step"):
+                    zstep.step(2e-3)
             return loss, state
         sync.reset()
         if prof is None:
@@ -197,6 +204,9 @@ def main(argv=None) -> int:
     if rank == 0:
         if prof is not None:
             print(prof.table(), file=sys.stderr)
+            if zstep is not None:
+                print(f"sharded: {zstep.early} of {len(zstep.buckets)} bucket "
+                      f"reduce-scatters launched during the backward (last step)", file=sys.stderr)
             win = sync.windows()
             if win:
                 print("gradient buckets (last step): release after step start / overlap window "

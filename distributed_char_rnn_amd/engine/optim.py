@@ -101,6 +101,31 @@ class TFAdam:
         return self.last_norm
 
     @torch.no_grad()
+    def step_packed(self, lr: float, p: torch.Tensor, g: torch.Tensor, m: torch.Tensor,
+                    v: torch.Tensor, sumsq: torch.Tensor, grad_scale: float = 1.0) -> torch.Tensor:
+        """One update (Adam step t -> t+1) of a packed parameter vector ``p`` with its own packed
+        gradient / slot vectors (the sharded step's owned chunks, parallel/zero.py), clipped by
+        the GLOBAL norm sqrt(``sumsq``) * grad_scale: ONE fused launch however many buckets the
+        chunks come from."""
+        lr_t = self.lr_t(lr)
+        if p.numel() and self.native:
+            self._ops.adam_clip(p, g, m, v, None, self._partials, self.last_norm, lr_t, self.b1,
+                                self.b2, self.eps, self.clip, float(grad_scale), 0, sumsq,
+                                self.guard)
+        else:
+            norm = torch.sqrt(sumsq.double().sum()).float() * grad_scale
+            self.last_norm.copy_(norm.reshape(1))
+            if p.numel() and not self._guard_set():
+                s = self.clip / torch.clamp(norm, min=self.clip) if self.clip > 0 else torch.ones(())
+                gs = g * (s * grad_scale)
+                m.mul_(self.b1).add_(gs, alpha=1 - self.b1)
+                v.mul_(self.b2).addcmul_(gs, gs, value=1 - self.b2)
+                p.sub_(lr_t * m / (v.sqrt() + self.eps))
+        self.t += 1
+        self.store.version += 1
+        return self.last_norm
+
+    @torch.no_grad()
     def step_range(self, lr: float, lo: int, hi: int, sumsq: torch.Tensor,
                    grad_scale: float = 1.0) -> torch.Tensor:
         """One update of the parameters [lo, hi) only, clipped by the GLOBAL norm

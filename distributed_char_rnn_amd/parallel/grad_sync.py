@@ -165,10 +165,11 @@ class GradSync:
             self.store.grad[lo:hi].copy_(full[: hi - lo])
         self._work.clear()
         self._next = 0
-        if self.guard is not None and self.guard_view is not None:
+        if self.guard is not None and self.guard_view is not None and self.world > 1:
             # fold the reduced guard (non-zero iff any rank's word was) back into this rank's
-            # own error word: every rank then raises on the same step (trainer poll)
-            torch.maximum(self.guard, (self.guard_view != 0).to(self.guard.dtype), out=self.guard)
+            # own error word: every rank then raises on the same step (trainer poll).  One
+            # bitwise OR (the slot's bits are non-zero iff any rank's word was)
+            self.guard.bitwise_or_(self.guard_view)
         if defer_scale:
             return 1.0 / self.world
         self.store.grad.mul_(1.0 / self.world)  # (the guard slot stays non-zero iff it was)

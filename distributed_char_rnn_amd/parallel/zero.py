@@ -75,17 +75,64 @@ class ShardedStep:
         self.shard = p  # = store.numel // world
         dev = store.flat.device
         self.gown = torch.empty(self.shard, dtype=torch.float32, device=dev)   # reduced grads
-        self.pown = torch.empty(self.shard, dtype=torch.float32, device=dev)   # gather staging
+        # the owned chunks of the parameters and of Adam's slots, packed like gown: the update
+        # is ONE fused launch over them, and the packed parameters are the all-gathers' inputs
+        # (no staging copies); opt.m / opt.v hold full copies only after gather_slots
+        self.pown = torch.empty(self.shard, dtype=torch.float32, device=dev)
+        self.mown = torch.empty(self.shard, dtype=torch.float32, device=dev)
+        self.vown = torch.empty(self.shard, dtype=torch.float32, device=dev)
         self.sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
         self._wire16: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
         if wire == "bf16":
             self._wire16 = (torch.empty(store.numel, dtype=torch.bfloat16, device=dev),
                             torch.empty(store.numel, dtype=torch.bfloat16, device=dev))
         self.n_norm, self.use_slot = store.norm_terms()
+        # The norm terms this rank owns are ONE prefix gown[:P] of the packed owned vector: the
+        # buckets are in flat order and the norm terms are the flat prefix [0, n_norm) (+ the
+        # TF-mode slot, one element holding a sum of squares) -- so the owned sum of squares is
+        # one native launch instead of a loop of float64 torch ops per bucket
+        self._pre, self._slot_pos, prefix_ok = 0, -1, True
+        for (a, b), p in zip(self.own, self.pos):
+            e = min(b, self.n_norm)
+            if e > a:
+                prefix_ok &= p == self._pre
+                self._pre = p + (e - a)
+            if self.use_slot and a <= store.norm_slot < b:
+                self._slot_pos = p + store.norm_slot - a
+        # ... and the owned parameters (flat [0, norm_slot): the slot and the tail padding are
+        # not parameters) the prefix pown[:Q]
+        self._q = 0
+        for (a, b), p in zip(self.own, self.pos):
+            e = min(b, store.norm_slot)
+            if e > a:
+                prefix_ok &= p == self._q
+                self._q = p + (e - a)
+        if not prefix_ok:
+            raise AssertionError("sharded optimizer: owned norm terms are not a prefix")
+        self.refresh()
+        self._ops = None
+        if dev.type == "cuda":
+            from ..ops import native
+
+            self._ops = native.ops()
+            self._npart = torch.empty(max(1, int(self._ops.opt_num_partials(max(self._pre, 1)))),
+                                      dtype=torch.float32, device=dev)
+            self._ntick = torch.zeros(1, dtype=torch.int32, device=dev)  # the kernel resets it
+        self._gathers: list = []
         self._next = 0
         self._work: list = []
         # bucket indices in launch order of the current step (tests, --profile reports)
         self.launched: List[int] = []
+        self.early = 0
+
+    @torch.no_grad()
+    def refresh(self) -> None:
+        """(Re)pack the owned chunks of the parameters and Adam's slots from the full buffers
+        (construction; after a checkpoint restore or broadcast changed them)."""
+        for (a, b), p in zip(self.own, self.pos):
+            self.pown[p:p + (b - a)].copy_(self.store.flat[a:b])
+            self.mown[p:p + (b - a)].copy_(self.opt.m[a:b])
+            self.vown[p:p + (b - a)].copy_(self.opt.v[a:b])
 
     # -- the GradSync-compatible interface the backward drives ------------------------------
     def reset(self) -> None:
@@ -117,19 +164,18 @@ class ShardedStep:
 
     # -- the optimizer step ----------------------------------------------------------------
     def _owned_sumsq(self) -> None:
-        """Sum of squares of the norm terms this rank owns (reduced gradients), all-reduced."""
-        acc = torch.zeros((), dtype=torch.float64, device=self.gown.device)
-        for (a, b), p in zip(self.own, self.pos):
-            e = min(b, self.n_norm)
-            if e > a:
-                part = self.gown[p:p + (e - a)].double()
-                acc = acc + (part * part).sum()
-        slot = self.store.norm_slot
-        if self.use_slot:
-            for (a, b), p in zip(self.own, self.pos):
-                if a <= slot < b:
-                    acc = acc + self.gown[p + slot - a].double()
-        self.sumsq.copy_(acc.float().reshape(1))
+        """Sum of squares of the norm terms this rank owns (reduced gradients), all-reduced:
+        one native sumsq launch over the owned prefix gown[:P] (csrc/optim.hip, one-launch
+        form), plus the slot element if this rank owns it."""
+        pre = self.gown[:self._pre]
+        if self._pre == 0:
+            self.sumsq.zero_()
+        elif self._ops is not None:
+            self._ops.sumsq(pre, self._npart, self.sumsq, self._ntick)
+        else:
+            self.sumsq.copy_((pre.double() * pre.double()).sum().float().reshape(1))
+        if self._slot_pos >= 0:
+            self.sumsq.add_(self.gown[self._slot_pos:self._slot_pos + 1])
         dist.all_reduce(self.sumsq, group=self.group)
 
     @torch.no_grad()
@@ -137,6 +183,7 @@ class ShardedStep:
         """Gradients of this rank's batch are complete in ``store.grad`` (buckets already
         launched by the backward are not relaunched): finish the exchange, update the owned
         chunks, gather the parameters.  Returns the pre-clip global norm (device tensor)."""
+        self.early = len(self.launched)  # buckets the backward launched (reports)
         self.ready(None)
         for w, i, recv in self._work:
             w.wait()
@@ -146,25 +193,32 @@ class ShardedStep:
                           out=self.gown[self.pos[i]:self.pos[i] + c])
         self._work.clear()
         self._next = 0
-        g = self.store.grad
-        for (a, b), p in zip(self.own, self.pos):
-            g[a:b].copy_(self.gown[p:p + (b - a)])
         if self.guard is not None:
             dist.all_reduce(self.guard, op=dist.ReduceOp.MAX, group=self.group)
         self._owned_sumsq()
-        norm = self.opt.step_ranges(lr, self.own, self.sumsq, grad_scale=1.0 / self.world)
+        q = self._q
+        norm = self.opt.step_packed(lr, self.pown[:q], self.gown[:q], self.mown[:q],
+                                    self.vown[:q], self.sumsq, grad_scale=1.0 / self.world)
         flat = self.store.flat
+        # one asynchronous all-gather per bucket straight from the packed parameters; the
+        # gathers pipeline on the communication stream and the caller's stream waits for them
+        # (wait_gathers) before anything reads the parameters
         for (lo, hi), (a, b), p in zip(self.buckets, self.own, self.pos):
-            stage = self.pown[p:p + (b - a)]
-            stage.copy_(flat[a:b])
-            dist.all_gather_into_tensor(flat[lo:hi], stage, group=self.group)
+            self._gathers.append(dist.all_gather_into_tensor(
+                flat[lo:hi], self.pown[p:p + (b - a)], group=self.group, async_op=True))
+        self.wait_gathers()
         return norm
+
+    def wait_gathers(self) -> None:
+        """Make the current stream wait for the step's parameter all-gathers (on NCCL / RCCL a
+        stream dependency, not a host block)."""
+        for w in self._gathers:
+            w.wait()
+        self._gathers.clear()
 
     @torch.no_grad()
     def gather_slots(self) -> None:
         """Every rank's Adam slot chunks into the full m / v buffers (before a checkpoint)."""
-        for buf in (self.opt.m, self.opt.v):
+        for buf, own in ((self.opt.m, self.mown), (self.opt.v, self.vown)):
             for (lo, hi), (a, b), p in zip(self.buckets, self.own, self.pos):
-                stage = self.pown[p:p + (b - a)]
-                stage.copy_(buf[a:b])
-                dist.all_gather_into_tensor(buf[lo:hi], stage, group=self.group)
+                dist.all_gather_into_tensor(buf[lo:hi], own[p:p + (b - a)], group=self.group)
