@@ -81,7 +81,10 @@ class ShardedStep:
         self.pown = torch.empty(self.shard, dtype=torch.float32, device=dev)
         self.mown = torch.empty(self.shard, dtype=torch.float32, device=dev)
         self.vown = torch.empty(self.shard, dtype=torch.float32, device=dev)
-        self.sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
+        # [owned sum of squares, this rank's error word as a float]: ONE all-reduce (SUM) gives
+        # the global sum of squares and a guard that is non-zero iff any rank's word was
+        self.red = torch.zeros(2, dtype=torch.float32, device=dev)
+        self.sumsq = self.red[:1]
         self._wire16: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
         if wire == "bf16":
             self._wire16 = (torch.empty(store.numel, dtype=torch.bfloat16, device=dev),
@@ -176,7 +179,12 @@ class ShardedStep:
             self.sumsq.copy_((pre.double() * pre.double()).sum().float().reshape(1))
         if self._slot_pos >= 0:
             self.sumsq.add_(self.gown[self._slot_pos:self._slot_pos + 1])
-        dist.all_reduce(self.sumsq, group=self.group)
+        if self.guard is not None:
+            self.red[1:].copy_(self.guard)
+        dist.all_reduce(self.red, group=self.group)
+        if self.guard is not None:
+            # every rank's own word folded in (all ranks skip the update and raise together)
+            self.guard.bitwise_or_(self.red[1:].view(torch.int32))
 
     @torch.no_grad()
     def step(self, lr: float) -> torch.Tensor:
@@ -193,9 +201,7 @@ class ShardedStep:
                           out=self.gown[self.pos[i]:self.pos[i] + c])
         self._work.clear()
         self._next = 0
-        if self.guard is not None:
-            dist.all_reduce(self.guard, op=dist.ReduceOp.MAX, group=self.group)
-        self._owned_sumsq()
+        self._owned_sumsq()  # (also reduces the error words)
         q = self._q
         norm = self.opt.step_packed(lr, self.pown[:q], self.gown[:q], self.mown[:q],
                                     self.vown[:q], self.sumsq, grad_scale=1.0 / self.world)
