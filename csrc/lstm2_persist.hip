@@ -233,6 +233,25 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
   // retirement had made the poller's flag loads wait for them (4.10 -> 3.33 us per tick
   // without any row-major store, scripts/pair_bench.py).
   constexpr bool DEFER = G == 1;
+  // XIN: layer l's input rows of a tick, loaded one tick ahead into registers by unconditional
+  // buffer loads behind the payload (rows >= B and ticks >= T read zero); loading them at the
+  // tick start had put their HBM latency in front of the poll's flag loads (vmcnt in order)
+  bf16x8 xpf[XIN ? 2 : 1][XIN ? KS : 1];
+  const __amdgpu_buffer_rsrc_t r_x = make_rsrc(a.x0, XIN ? sizeof(bf16) * (size_t)T * B * H : 0);
+  auto x_prefetch = [&](int tk) {
+    if constexpr (XIN) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bool ok = tk < T && col * 32 + 16 * j + (lane & 15) < B;
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+          xpf[j][s] = ld8_sc1(r_x, ok ? (unsigned)((size_t)tk * B * H * sizeof(bf16)) + rm_lane +
+                                            rm_off(col, j, s)
+                                      : 0x7FFFFFF0u);
+      }
+    }
+  };
+  x_prefetch(0);
   bf16x4 rm_h = {}, rm_g[4] = {};
   float rm_c[4] = {};
   int rm_t = -1;
@@ -279,29 +298,19 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     }
     // XIN: layer l's input product of step tau (this wave's K quarter, both tiles, all gates),
     // the recurrent product is accumulated on top after the poll
+    // (the rows were loaded one tick ahead, behind the previous tick's payload; zero past T)
     f32x4 xin[XIN ? 2 : 1][4];
     if constexpr (XIN) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int gt = 0; gt < 4; ++gt) xin[j][gt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (tau < T) {
-        // rows >= B (padding) read as zero through the buffer range check
-        const __amdgpu_buffer_rsrc_t rx =
-            make_rsrc(a.x0 + (size_t)tau * B * H, sizeof(bf16) * (size_t)B * H);
-        bf16x8 xf[2][KS];
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-          for (int s = 0; s < KS; ++s)
-            xf[j][s] = ld8_sc1(rx, rm_lane + rm_off(col, j, s));
+        for (int s = 0; s < KS; ++s)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int s = 0; s < KS; ++s)
-#pragma unroll
-            for (int gt = 0; gt < 4; ++gt) xin[j][gt] = mfma16(wx0l[w][gt][s][lane], xf[j][s], xin[j][gt]);
-      }
+          for (int gt = 0; gt < 4; ++gt) xin[j][gt] = mfma16(wx0l[w][gt][s][lane], xpf[j][s], xin[j][gt]);
     }
     // dropout of layer l+1's input (layer l's h of step tau-1): the mask bytes of the
     // workgroup's 32G rows for this tick, DMA'd into LDS before the poll (no registers; the
@@ -428,6 +437,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
       } else {
         if (g > 0) load_group(g, pf0[0], pf1[0]);
       }
+      if constexpr (XIN) x_prefetch(tau + 1);
       if constexpr (ZXA) {
         // the next tick's row (and the id of the one after), behind this tick's payload loads
         if (zl && tau + 1 < T) {
@@ -960,7 +970,7 @@ static const void* lstm2_fwd_g(int G, bool xin, bool diag) {
   switch (G) {
     case 1:
       // (the stamped instantiation exists for the stamp-diagnosed shape only)
-      if (diag && !DROP) return (const void*)lstm2_fwd_persist_kernel<KS, 1, DROP, false, true>;
+      if (diag) return (const void*)lstm2_fwd_persist_kernel<KS, 1, DROP, false, true>;
       return (const void*)lstm2_fwd_persist_kernel<KS, 1, DROP, false, false>;
     case 2: return (const void*)lstm2_fwd_persist_kernel<KS, 2, DROP, false, false>;
     case 3: return (const void*)lstm2_fwd_persist_kernel<KS, 3, DROP, false, false>;

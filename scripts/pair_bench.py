@@ -89,7 +89,7 @@ def skew(d, H, B, T):
     return list(zip(names, r)), by_xcd
 
 
-def run(ops, H, T, B, G, want_stamps, reps=5, want_skew=False):
+def run(ops, H, T, B, G, want_stamps, reps=5, want_skew=False, drop=False, gather=False):
     dev = "cuda"
     G = int(ops.lstm2_plan(H, B, G))
     if not G:
@@ -99,6 +99,15 @@ def run(ops, H, T, B, G, want_stamps, reps=5, want_skew=False):
     r = lambda *s: (torch.randn(*s, device=dev) * 0.05).to(torch.bfloat16)  # noqa: E731
     W0T, W1T, X1T = r(4 * H, H), r(4 * H, H), r(4 * H, H)
     zx = torch.randn(T, B, 4 * H, device=dev) * 0.1
+    ids = None
+    if gather:  # the headline's layer 0: a [V, 4H] table gathered by token id
+        zx = torch.randn(65, 4 * H, device=dev) * 0.1
+        ids = torch.randint(0, 65, (T, B), dtype=torch.int32, device=dev)
+    # layer 1's input dropout: [T, B, H/8] keep bits (keep 0.8 per bit)
+    xm = (torch.rand(T, B, H, device=dev) < 0.8).view(T, B, H // 8, 8) if drop else None
+    if drop:
+        w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.int32, device=dev)
+        xm = (xm.int() * w).sum(-1).to(torch.uint8).contiguous()
     b1 = torch.zeros(4 * H, device=dev)
     hb0, hb1 = (torch.zeros(T + 1, B, H, dtype=torch.bfloat16, device=dev) for _ in range(2))
     cb0, cb1 = (torch.zeros(T + 1, B, H, device=dev) for _ in range(2))
@@ -112,7 +121,8 @@ def run(ops, H, T, B, G, want_stamps, reps=5, want_skew=False):
     def fwd(diag=None):
         cnt.zero_()
         ops.lstm2_persist_fwd(W0T, W1T, X1T, zx, None, b1, hb0, cb0, g0, hl0, hb1, cb1, g1, hl1,
-                              cnt[0], cnt[1], err, 1.0, 1 << 22, hr0, hr1, G, None, None, diag)
+                              cnt[0], cnt[1], err, 1.0, 1 << 22, hr0, hr1, G, None, None, diag,
+                              xm, 1.25 if drop else 1.0)
 
     Wh0, Wh1, Wx1 = r(H, 4 * H), r(H, 4 * H), r(H, 4 * H)
     dtop = torch.randn(T, B, H, device=dev) * 0.01
@@ -163,12 +173,14 @@ def main():
     ap.add_argument("--B", type=int, nargs="+", default=[256, 512, 1024])
     ap.add_argument("--G", type=int, nargs="+", default=[0])
     ap.add_argument("--stamps", action="store_true")
+    ap.add_argument("--drop", action="store_true", help="layer 1 input dropout (DROP kernels)")
+    ap.add_argument("--gather", action="store_true", help="layer 0 rows gathered from a table")
     ap.add_argument("--skew", action="store_true", help="every workgroup's hand-off timing (wide BPTT)")
     a = ap.parse_args()
     ops = native.ops()
     for B in a.B:
         for G in a.G:
-            o = run(ops, a.H, a.T, B, G, a.stamps, want_skew=a.skew)
+            o = run(ops, a.H, a.T, B, G, a.stamps, want_skew=a.skew, drop=a.drop, gather=a.gather)
             if o is None:
                 print(f"H={a.H} B={B} G={G}: no co-resident grid", flush=True)
                 continue

@@ -1,0 +1,99 @@
+"""Gradient comparisons of the GPU oracle tests: every native parameter gradient against the fp32
+reference backend (models/reference.py, the autograd model of /root/reference/model.py:19-98).
+
+Two errors per parameter:
+
+- ``rel``: the whole tensor's relative Frobenius error ||g - r|| / ||r||;
+- ``blk``: the worst row block -- the tensor flattened to [rows, cols] (a bias or a 1-D tensor
+  as [n/64, 64]) and cut into blocks of 16 rows, each block's ||g_b - r_b|| over
+  max(||r_b||, a quarter of the RMS block norm).  A single bad tile (one workgroup's column of a
+  wavefront kernel, one split-K slab) moves ``rel`` of a [4H, H] matrix by little; it moves its
+  block's error by all of it.  The floor keeps blocks whose reference is ~0 (embedding rows of
+  tokens absent from the batch, padding) from dividing by nothing.
+
+Tolerances are per test (``TOL``), set to about twice the largest error measured on an MI355X over
+every parametrisation of the test (profiles/r4_oracle_errors.md, from a run with
+``DCR_ORACLE_LOG=<file>``, which appends every measured error as a JSON line;
+scripts/oracle_tolerances.py summarises such a log).
+"""
+import json
+import math
+import os
+
+import torch
+
+# test key -> (rel tolerance, block tolerance); measured maxima in profiles/r4_oracle_errors.md
+TOL = {
+    "native_model": (6e-2, 0.15),
+    "native_model_lib": (6e-2, 0.15),
+    "persist": (6e-2, 0.15),
+    "persist_nt": (6e-2, 0.15),
+    "pair_batch": (6e-2, 0.15),
+    "bwd_wide": (5e-2, 0.15),
+    "gru_persist": (6e-2, 0.15),
+    "gru_persist_multi": (6e-2, 0.15),
+    "padded": (6e-2, 0.15),
+    "dropout": (6e-2, 0.15),
+    "ragged_persist": (6e-2, 0.15),
+    "head": (6e-2, 0.15),
+    "head_wide": (6e-2, 0.15),
+    "long_t": (5e-2, 0.15),
+    "big_batch": (6e-2, 0.15),
+}
+
+BLOCK_ROWS = 16
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+def block_err(got, ref):
+    """Worst 16-row block's relative error (see the module docstring)."""
+    g, r = got.double().cpu(), ref.double().cpu()
+    if r.dim() <= 1:
+        n = r.numel()
+        cols = 64 if n % 64 == 0 else 1
+        g, r = g.reshape(-1, cols), r.reshape(-1, cols)
+    else:
+        g, r = g.reshape(r.shape[0], -1), r.reshape(r.shape[0], -1)
+    rows = r.shape[0]
+    nb = (rows + BLOCK_ROWS - 1) // BLOCK_ROWS
+    pad = nb * BLOCK_ROWS - rows
+    if pad:
+        z = torch.zeros(pad, r.shape[1], dtype=r.dtype)
+        g, r = torch.cat([g, z]), torch.cat([r, z])
+    d = (g - r).reshape(nb, -1).norm(dim=1)
+    rb = r.reshape(nb, -1).norm(dim=1)
+    floor = 0.25 * r.norm() / math.sqrt(nb)
+    if floor.item() == 0.0:
+        return 0.0 if d.max().item() == 0.0 else float("inf")
+    return (d / torch.maximum(rb, floor)).max().item()
+
+
+def _log(key, name, e, b):
+    path = os.environ.get("DCR_ORACLE_LOG")
+    if not path:
+        return
+    with open(path, "a") as f:
+        f.write(json.dumps({"key": key, "test": os.environ.get("PYTEST_CURRENT_TEST", ""),
+                            "param": name, "rel": e, "blk": b}) + "\n")
+
+
+def check_grads(key, store, got, ref, names=None):
+    """Every parameter's (rel, blk) error of the flat gradient ``got`` against ``ref`` within
+    ``TOL[key]``; returns {name: (rel, blk)}."""
+    rt, bt = TOL[key]
+    errs, bad = {}, {}
+    for s in store.specs:
+        if names is not None and s.name not in names:
+            continue
+        g, r = store.view(s.name, got), store.view(s.name, ref)
+        e, b = rel(g, r), block_err(g, r)
+        _log(key, s.name, e, b)
+        errs[s.name] = (e, b)
+        if not (e < rt and b < bt):
+            bad[s.name] = (e, b)
+    assert not bad, (key, bad)
+    return errs

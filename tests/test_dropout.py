@@ -11,6 +11,7 @@ import torch
 from distributed_char_rnn_amd.models.char_rnn import CharRNN
 from distributed_char_rnn_amd.models.params import ModelConfig
 from distributed_char_rnn_amd.models.reference import ReferenceBackend
+from oracle import check_grads
 
 pytestmark = pytest.mark.gpu
 
@@ -34,7 +35,7 @@ def expand(bits, scale):
     return m.transpose(0, 1).contiguous()
 
 
-def _run(model, B, T, H, L, ikp, okp, env=None, monkeypatch=None, tol=6e-2):
+def _run(model, B, T, H, L, ikp, okp, env=None, monkeypatch=None, key="dropout"):
     for k, v in (env or {}).items():
         monkeypatch.setenv(k, v)
     cfg = ModelConfig(model=model, vocab_size=65, rnn_size=H, num_layers=L,
@@ -61,9 +62,7 @@ def _run(model, B, T, H, L, ikp, okp, env=None, monkeypatch=None, tol=6e-2):
     for a_r, a_n in zip(st_r, st_n):
         for s_r, s_n in zip(a_r, a_n):
             assert rel(s_n, s_r) < 3e-2
-    for s in nat.store.specs:
-        e = rel(nat.store.view(s.name, g_nat), nat.store.gview(s.name))
-        assert e < tol, (s.name, e)
+    check_grads(key, nat.store, g_nat, nat.store.grad)
     return nat, dm
 
 

@@ -9,6 +9,7 @@ import torch
 from distributed_char_rnn_amd.models.char_rnn import CharRNN
 from distributed_char_rnn_amd.models.params import ModelConfig
 from distributed_char_rnn_amd.models.reference import ReferenceBackend
+from oracle import check_grads
 
 pytestmark = pytest.mark.gpu
 
@@ -70,9 +71,7 @@ def test_nt_kernels_match_oracle(B, T, L, dbg, dcr_ops, monkeypatch):
     for a_r, a_n in zip(st_r, st_n):
         for s_r, s_n in zip(a_r, a_n):
             assert rel(s_n, s_r) < 3e-2
-    for s in nat.store.specs:
-        e = rel(nat.store.gview(s.name), nat.store.view(s.name, g_ref))
-        assert e < 6e-2, (s.name, e)
+    check_grads("persist_nt", nat.store, nat.store.grad, g_ref)
 
 
 def test_nt_kernels_match_library_path(monkeypatch):
