@@ -252,6 +252,28 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     }
   };
   x_prefetch(0);
+  // (G = 1) dropout: the mask bytes of tick tk (layer l's h of step tk-1) into mlds[tk & 1],
+  // DMA'd one tick ahead behind the payload loads by unconditional buffer loads (rows >= B
+  // and ticks without an input mask read zero).  Issued before the poll (G > 1), the DMA sat
+  // in front of the flag loads in vmcnt order, and the barrier after the poll -- which the
+  // compiler makes wait for every LDS-DMA (vmcnt(0)) -- exposed its whole latency every tick.
+  auto mask_dma = [&](int tk) {
+    if constexpr (DROP && G == 1) {
+      const int r0 = col * 32;
+      const bool okt = tk >= 1 && tk <= T;
+      const __amdgpu_buffer_rsrc_t rm = make_rsrc(a.xmask, sizeof(uint8_t) * (size_t)T * B * (H / 8));
+#pragma unroll
+      for (int k = 0; k < kMaskDw; ++k) {
+        const int i0 = 256 * k + 64 * w;  // this wave's 64 dwords of the 32 rows x H/32
+        const int di = i0 + lane;
+        const bool ok = okt && i0 < H && r0 + di / (H / 32) < B;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rm, (__attribute__((address_space(3))) void*)&mlds[tk & 1][i0], 4,
+            ok ? (unsigned)(((size_t)(tk - 1) * B + r0) * (H / 8) + 4 * (size_t)di) : 0x7FFFFFF0u,
+            0, 0, 0);
+      }
+    }
+  };
   bf16x4 rm_h = {}, rm_g[4] = {};
   float rm_c[4] = {};
   int rm_t = -1;
@@ -317,7 +339,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     // poll barrier waits for them).  A global byte load at each use had put its latency on the
     // tick's critical path.
     const bool xdrop = DROP && ld0 && tau >= 1;
-    if (xdrop) {
+    if (G > 1 && xdrop) {
       const int r0 = col * G * 32;
       const __amdgpu_buffer_rsrc_t rm =
           make_rsrc(a.xmask + ((size_t)(tau - 1) * B + r0) * (H / 8),
@@ -410,6 +432,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     };
     load_group(0, pf0[0], pf1[0]);
     if constexpr (DEFER) flush_rm();  // the previous tick's row-major copies
+    if constexpr (DROP && G == 1) mask_dma(tau + 1);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       STAMPF(g, 7)  // group phase start

@@ -139,12 +139,13 @@ class ForwardMixin:
                     X = x_prev.reshape(N, H)
                     if inb is not None:
                         X = self._masked(X, inb, dm["sin"], out=lb.x_drop)
-                # opt-in (DCR_DEBUG=xin=1): the G = 1 two-layer forward projects these bf16 rows
-                # in-kernel (no [N, 4H] fp32 zx round trip); measured slower than the library
-                # GEMM + zx once the forward's payload loads moved first (dropout headline 2.32
-                # vs 2.20 ms, same box)
+                # the G = 1 two-layer forward projects these bf16 rows in-kernel (no library
+                # GEMM, no [N, 4H] fp32 zx round trip; the rows are loaded one tick ahead behind
+                # the payload): dropout headline 1.937 vs 1.958 ms for the library route, same
+                # box, 3 alternating rounds (round 3, rows loaded at the tick start: 2.32 vs 2.20
+                # -- slower).  DCR_DEBUG=xin=0 forces the library route.
                 xin = (P.pair and layer + 1 < self.L and P.pair_g == 1 and lw.WxT is not None
-                       and self.knobs.debug.get("xin") == "1" and self._xin_ok())
+                       and self.knobs.debug.get("xin", "1") != "0" and self._xin_ok())
                 # (row-strided rows -- the h of a pair-interleaved layer -- feed the library
                 # GEMMs as they are; the in-kernel projection wants dense rows)
                 lb.x_in = X.contiguous() if (xin or X.stride(-1) != 1) else X

@@ -56,7 +56,8 @@ DEBUG_KEYS = {
     "bigstep_cfg": "id: force tile configuration id of the fused large-H step kernels (C++)",
     "sample_graph": "0: eager sampling loop (no hipGraph replay)",
     "head_omask": "0: top output dropout applied to dtop by a separate pass, not the head",
-    "xin": "1: in-kernel input projection of a dense layer-l input (G = 1 two-layer forward)",
+    "xin": "0: library zx GEMM for a dense layer-l input instead of the G = 1 two-layer "
+           "forward's in-kernel projection",
     "pair_dw": "0: separate h buffers per layer of a wavefront pair (two weight GEMMs for the "
                "upper layer instead of one over the pair-interleaved h)",
     "gru_dwx": "0: GRU input-weight gradient as one [H, 3H] temporary + sum + two copies",

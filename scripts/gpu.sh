@@ -16,6 +16,8 @@
 #   ab=<A.so>,<B.so>[,rounds,<bench args>]  same-box A/B of two builds (scripts/ab_bench.sh)
 #   abenv=<VAR=value>[;<bench args>]  same-box A/B of bench.py without / with an environment
 #                              setting (e.g. abenv=DCR_DEBUG=wide=0), 3 alternating rounds
+#   abargs=<args A>|<args B>[|...]  same-box comparison of bench.py argument sets (',' for ' ';
+#                              an empty set is the default run), 3 alternating rounds
 #
 # Example: gpurun --timeout 900 -- bash scripts/gpu.sh r3_base tests bench trace
 set -o pipefail
@@ -57,7 +59,8 @@ for step in "$@"; do
       cat "$O/pmc_summary.md" ;;
     py)
       read -r -a P <<< "$(sp "$arg")"
-      timeout -k 10 600 python -u "${P[@]}" > "$O/py_$(basename "${P[0]}" .py).log" 2>&1 || {
+      echo "== ${P[*]}" >> "$O/py_$(basename "${P[0]}" .py).log"
+      timeout -k 10 600 python -u "${P[@]}" >> "$O/py_$(basename "${P[0]}" .py).log" 2>&1 || {
         tail -40 "$O/py_$(basename "${P[0]}" .py).log"; exit 1; }
       tail -40 "$O/py_$(basename "${P[0]}" .py).log" ;;
     ab)
@@ -73,6 +76,14 @@ for step in "$@"; do
             ms=$(env "$EV" timeout -k 10 120 python bench.py $(sp "$BA") | python -c "import json,sys; print('%.4f' % json.loads(sys.stdin.read())['ms_per_step'])") || exit 1
           fi
           echo "$v $ms" | tee -a "$O/abenv.log"
+        done
+      done ;;
+    abargs)
+      IFS='|' read -r -a VS <<< "$arg"
+      for i in 1 2 3; do
+        for v in "${VS[@]}"; do
+          ms=$(timeout -k 10 120 python bench.py --steps 40 --warmup 5 $(sp "$v") | tail -1 | python -c "import json,sys; print('%.4f' % json.loads(sys.stdin.read())['ms_per_step'])") || exit 1
+          echo "[$v] $ms" | tee -a "$O/abargs.log"
         done
       done ;;
     *) echo "unknown step $step"; exit 2 ;;

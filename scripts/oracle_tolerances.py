@@ -5,6 +5,7 @@ tolerance in force and twice the measured maximum (the tolerance rule of tests/o
     python scripts/oracle_tolerances.py gpurun_out/<run>/oracle.jsonl > profiles/r4_oracle_errors.md
 """
 import json
+import re
 import os
 import sys
 
@@ -16,7 +17,10 @@ def main(path):
     rows = [json.loads(line) for line in open(path) if line.strip()]
     by = {}
     for r in rows:
-        by.setdefault(r["key"], []).append(r)
+        k = r["key"]
+        if k == "native_model" and re.search(r"[\[-]nas[\]-]", r["test"]):  # (pre-split logs)
+            k = "native_model_nas"
+        by.setdefault(k, []).append(r)
     print(f"# Oracle gradient errors ({len(rows)} parameter comparisons)\n")
     print("| key | cases | max rel | at | max blk | at | tol (rel, blk) | 2x measured |")
     print("|---|---|---|---|---|---|---|---|")

@@ -120,7 +120,7 @@ def run(ops, H, T, B, G, want_stamps, reps=5, want_skew=False, drop=False, gathe
 
     def fwd(diag=None):
         cnt.zero_()
-        ops.lstm2_persist_fwd(W0T, W1T, X1T, zx, None, b1, hb0, cb0, g0, hl0, hb1, cb1, g1, hl1,
+        ops.lstm2_persist_fwd(W0T, W1T, X1T, zx, ids, b1, hb0, cb0, g0, hl0, hb1, cb1, g1, hl1,
                               cnt[0], cnt[1], err, 1.0, 1 << 22, hr0, hr1, G, None, None, diag,
                               xm, 1.25 if drop else 1.0)
 

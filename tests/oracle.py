@@ -12,7 +12,8 @@ Two errors per parameter:
   tokens absent from the batch, padding) from dividing by nothing.
 
 Tolerances are per test (``TOL``), set to about twice the largest error measured on an MI355X over
-every parametrisation of the test (profiles/r4_oracle_errors.md, from a run with
+every parametrisation of the test (the round-3 tolerance was a flat 6e-2 relative error;
+profiles/r4_oracle_errors.md, from a run with
 ``DCR_ORACLE_LOG=<file>``, which appends every measured error as a JSON line;
 scripts/oracle_tolerances.py summarises such a log).
 """
@@ -24,21 +25,25 @@ import torch
 
 # test key -> (rel tolerance, block tolerance); measured maxima in profiles/r4_oracle_errors.md
 TOL = {
-    "native_model": (6e-2, 0.15),
-    "native_model_lib": (6e-2, 0.15),
-    "persist": (6e-2, 0.15),
-    "persist_nt": (6e-2, 0.15),
-    "pair_batch": (6e-2, 0.15),
-    "bwd_wide": (5e-2, 0.15),
-    "gru_persist": (6e-2, 0.15),
-    "gru_persist_multi": (6e-2, 0.15),
-    "padded": (6e-2, 0.15),
-    "dropout": (6e-2, 0.15),
-    "ragged_persist": (6e-2, 0.15),
-    "head": (6e-2, 0.15),
-    "head_wide": (6e-2, 0.15),
-    "long_t": (5e-2, 0.15),
-    "big_batch": (6e-2, 0.15),
+    "native_model": (1.4e-2, 1.6e-2),
+    # the NAS cell: its nested gate compositions (8 pre-activations per unit) amplify the bf16
+    # operand rounding far more than LSTM / GRU / RNN cells do; the error grows towards layer 0
+    # and the embedding (5.8e-2 measured at L = 3)
+    "native_model_nas": (1.2e-1, 1.6e-1),
+    "native_model_lib": (1.1e-2, 1.3e-2),
+    "persist": (1.1e-2, 1.2e-2),
+    "persist_nt": (1.1e-2, 1.2e-2),
+    "pair_batch": (1.4e-2, 1.4e-2),
+    "bwd_wide": (1.1e-2, 1.1e-2),
+    "gru_persist": (1.3e-2, 1.4e-2),
+    "gru_persist_multi": (1.3e-2, 1.4e-2),
+    "padded": (1.4e-2, 1.7e-2),
+    "dropout": (1.4e-2, 1.6e-2),
+    "ragged_persist": (1.3e-2, 1.3e-2),
+    "head": (1.1e-2, 1.2e-2),
+    "head_wide": (1.0e-2, 1.2e-2),
+    "long_t": (9e-3, 1.4e-2),
+    "big_batch": (1.0e-2, 1.3e-2),
 }
 
 BLOCK_ROWS = 16

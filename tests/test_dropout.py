@@ -104,9 +104,10 @@ def test_dropout_masks_statistics_and_fresh_per_step():
 
 
 @pytest.mark.parametrize("B,H,L", [(256, 512, 2), (50, 256, 4)])
-def test_dropout_in_kernel_input_projection_matches_oracle(B, H, L, monkeypatch):
-    """DCR_DEBUG=xin=1: the two-layer forward projects the masked embedding rows (and layer 2's
-    masked input) in-kernel instead of through the library zx GEMM."""
-    nat, _ = _run("lstm", B, 5, H, L, 0.8, 0.7, env={"DCR_DEBUG": "persist_min_t=1,xin=1"},
+def test_dropout_library_input_projection_matches_oracle(B, H, L, monkeypatch):
+    """DCR_DEBUG=xin=0: the masked embedding rows (and layer 2's masked input) through the library
+    zx GEMM instead of the two-layer forward's in-kernel projection (the default, covered by the
+    tests above)."""
+    nat, _ = _run("lstm", B, 5, H, L, 0.8, 0.7, env={"DCR_DEBUG": "persist_min_t=1,xin=0"},
                   monkeypatch=monkeypatch)
     assert nat.backend._persist_plan(B, True, 5).pair

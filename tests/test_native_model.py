@@ -45,7 +45,8 @@ def test_train_step_matches_reference(model, B, T, H, L):
     for (a_r, a_n) in zip(st_r, st_n):
         for s_r, s_n in zip(a_r, a_n):
             assert rel(s_n, s_r) < 3e-2
-    check_grads("native_model", nat.store, nat.store.grad, g_ref)
+    check_grads("native_model_nas" if model == "nas" else "native_model", nat.store,
+                nat.store.grad, g_ref)
     # TF clip-norm term: per-token sum of squares of the embedding-lookup gradient
     slot_r = nat.store.norm_slot_view(g_ref)
     slot_n = nat.store.norm_slot_view()
@@ -173,7 +174,8 @@ def test_per_step_batch_tiles_match_reference(model, nbt, monkeypatch):
     loss_n, _, _ = nat.backend.train_step(x, y, [tuple(s.clone() for s in t) for t in st0])
     torch.cuda.synchronize()
     assert abs(loss_n.item() - loss_r.item()) < 2e-2 * max(1.0, abs(loss_r.item()))
-    check_grads("native_model", nat.store, nat.store.grad, g_ref)
+    check_grads("native_model_nas" if model == "nas" else "native_model", nat.store,
+                nat.store.grad, g_ref)
 
 
 # B = 512: the BPTT step product runs as split-K slabs summed by the cell kernel
