@@ -112,9 +112,17 @@ __device__ __forceinline__ float row_reduce_scatter16(float (&v)[16], int lane) 
 //      first form of this order measured 1.630 vs 1.619 ms/step against 2 for that reason).
 //      Still slower than 1 (1.55 vs 1.52 ms/step, same box): the drain before the arrival now
 //      waits for the HBM operand loads and the deferred stores (3.4 k cycles incl. the stash).
-template <int KS, bool DROP, int PF, bool DIAG>
+//   6 (default): 1, with layer l's dtop stash moved from after the arrival into the MFMA phase, between
+//      layer l+1's chain and layer l's: its 32 LDS fragment reads and MFMAs per wave run while
+//      layer l's payload -- loaded second, the CU's L2 read port streaming 128 KB per workgroup
+//      and tick -- is still arriving.  After the arrival it delayed the next tick's poll (the
+//      stamps: ~1.35 us from the arrival to the next tick start, the poll then ~0.4 us, i.e. the
+//      hand-off had long landed).
+template <int KS, bool DROP, int PFA, bool DIAG>
 __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) {
   static_assert(KS % 4 == 0, "K quarter = whole 32-wide k-steps per gate");
+  constexpr int PF = PFA == 6 ? 1 : PFA;  // operand load order
+  constexpr bool ES = PFA == 6;           // early stash
   // partials [wave][layer][unit half][lane][4]
   __shared__ __attribute__((aligned(16))) float part[4][2][2][64][4];
   // W_x,l+1 fragments [wave][unit half][k-step][lane] (128 KB at H = 512), read back only by
@@ -353,6 +361,20 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
           *reinterpret_cast<float4*>(&part[w][1][u][lane][0]) =
               make_float4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
       }
+      f32x4 xsn[2];  // (ES) layer l's dtop partial for its next tick
+      if constexpr (ES) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (ld1) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < KS; ++s) x = mfma16(wx1l[w][u][s][lane], p1[s], x);
+            xsn[u] = x;
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
       if (on0) {  // layer l: dtop (stashed last tick) + dZ_l[t+1] · W_h,lᵀ
         f32x4 acc[2];
 #pragma unroll
@@ -379,6 +401,12 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
         for (int u = 0; u < 2; ++u)
           *reinterpret_cast<float4*>(&part[w][0][u][lane][0]) =
               make_float4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
+      }
+      if constexpr (ES) {
+        if (ld1) {
+          xs[0] = xsn[0];
+          xs[1] = xsn[1];
+        }
       }
     } else {
       // tick 0: layer l+1's first step has no recurrent input
@@ -532,7 +560,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
             rc, (__attribute__((address_space(3))) void*)&ob[12 + r][0], 4, oc + 4 * r, sc, 0, 0);
       }
     }
-    if (!stashed) do_stash();  // every wave (with an epilogue this tick or not)
+    if (!ES && !stashed) do_stash();  // every wave (with an epilogue this tick or not)
     // wave 0's dZ copy of tick tau-1 (layer l, step T+2-tau), written before this tick's first
     // barrier (wave 0 is active from tick 2)
     auto store_offl = [&](int tk) {
@@ -575,7 +603,7 @@ static const void* lstm2_bwd_wide_pick_t(int H) {
   }
   return nullptr;
 }
-constexpr int kWidePfDefault = 1;
+constexpr int kWidePfDefault = 6;  // headline 1.534 vs 1.558 ms, dropout 1.893 vs 1.963 (same box)
 // diag: the stamped instantiation (the default operand order, no dropout)
 template <bool DROP>
 static const void* lstm2_bwd_wide_pick(int H, bool diag = false) {
@@ -587,6 +615,7 @@ static const void* lstm2_bwd_wide_pick(int H, bool diag = false) {
     case 3: return lstm2_bwd_wide_pick_t<DROP, 3>(H);
     case 4: return DROP ? lstm2_bwd_wide_pick_t<DROP, 2>(H) : lstm2_bwd_wide_pick_t<DROP, 4>(H);
     case 5: return lstm2_bwd_wide_pick_t<DROP, 5>(H);
+    case 6: return lstm2_bwd_wide_pick_t<DROP, 6>(H);
   }
   return lstm2_bwd_wide_pick_t<DROP, 1>(H);
 }

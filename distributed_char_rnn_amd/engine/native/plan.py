@@ -37,10 +37,11 @@ DEBUG_KEYS = {
     "wgarr": "0: one hand-off counter add per epilogue wave in the pair kernels (C++ launcher)",
     "xcdloc": "0: write-through (sc1) hand-offs + atomic counters everywhere, never the "
               "XCD-resident form (plain payload, L2 flags) on single-XCD columns (C++ launcher)",
-    "wide_pf": "wide BPTT epilogue-operand loads: 0 before the poll, 1 (default) after the "
-               "payload, 2 one tick ahead, 3 / 4 poller-wave variants, 5 1 + the row-major dZ "
-               "copy deferred behind the next payload + the dtop stash inside the drain, all "
-               "unconditional (exact waitcnt) (C++)",
+    "wide_pf": "wide BPTT epilogue-operand loads: 0 before the poll, 1 after the payload, 2 "
+               "one tick ahead, 3 / 4 poller-wave variants, 5 1 + the row-major dZ copy "
+               "deferred behind the next payload + the dtop stash inside the drain, all "
+               "unconditional (exact waitcnt), 6 (default) 1 + the dtop stash inside the MFMA "
+               "phase (C++)",
     "fused_head": "0: library logits GEMM + CE kernel instead of the fused head",
     "dew": "layer-0 embedding-table gradient: gemm (one-hot MFMA GEMM, default) | segsum | fused",
     "side": "0: no side-stream weight GEMMs in overlap mode",

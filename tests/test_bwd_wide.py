@@ -39,7 +39,7 @@ def _run(cfg, B, T, wide, monkeypatch, steps=2, pf=None):
     return m, loss.item(), [s.clone() for t in st for s in t]
 
 
-@pytest.mark.parametrize("pf", [None, 0, 2, 3, 4, 5])
+@pytest.mark.parametrize("pf", [None, 0, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("B,T,H,drop", [(256, 8, 512, False), (50, 7, 128, False),
                                         (37, 6, 512, False), (100, 5, 256, True),
                                         (256, 6, 512, True)])
