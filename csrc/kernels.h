@@ -13,7 +13,8 @@ int opt_num_partials(int64_t n);
 void launch_global_norm(const float* g, int64_t n, float* partials, float* norm_out,
                         hipStream_t stream);
 void launch_sumsq(const void* x, bool is_bf16, int64_t n, float* partials, float* out,
-                  unsigned* ticket, hipStream_t stream);
+                  unsigned* ticket, hipStream_t stream, const float* extra = nullptr,
+                  const int* guard = nullptr);
 void launch_adam_clip(float* p, const float* g, float* m, float* v, bf16* pbf, int64_t n,
                       float* partials, float* norm_out, float lr_t, float b1, float b2, float eps,
                       float clip, float gscale, int64_t n_norm, const float* extra_sq,

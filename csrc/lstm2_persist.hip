@@ -46,6 +46,19 @@ constexpr int kPairMaxG = 4;
 
 // Dropout (dropout.hip bit masks): zero the elements of a bf16 MFMA fragment whose mask bit is
 // clear (8 consecutive k, bit e of `m` = element e); the 1/keep scale is applied to the product.
+// The same in 5 full-rate VALU ops per dword: the bit pair x of the dword is spread to bits 0
+// and 16 (x | x << 15, & 0x10001) and multiplied by 0xFFFF into the dword's keep mask (a 24-bit
+// multiply: the spread value is < 2^17).
+__device__ __forceinline__ bf16x8 mask_frag_fast(const bf16x8& v, unsigned m) {
+  u32x4 u = __builtin_bit_cast(u32x4, v);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const unsigned x = (m >> (2 * i)) & 3u;
+    u[i] &= __umul24((x | (x << 15)) & 0x10001u, 0xFFFFu);
+  }
+  return __builtin_bit_cast(bf16x8, u);
+}
+
 __device__ __forceinline__ bf16x8 mask_frag(const bf16x8& v, unsigned m) {
   u32x4 u = __builtin_bit_cast(u32x4, v);
 #pragma unroll
@@ -554,13 +567,27 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
       auto do_stash = [&]() {
         if constexpr (G == 1) {
           if (ld0 && tau >= 1) {
+            // dropout: the mask dwords of this lane's fragments, all read before any use (one
+            // LDS wait; a byte read at each use had serialised 8 LDS round trips); the byte of
+            // fragment (j, s) is byte lane/16 of dword s of its row's K range
+            unsigned mw[2][KS];
+            if (xdrop) {
+              const unsigned* mr = &mlds[tau & 1][(kbase >> 5)];
+#pragma unroll
+              for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int s = 0; s < KS; ++s) mw[j][s] = mr[(16 * j + (lane & 15)) * (H / 32) + s];
+              __builtin_amdgcn_sched_barrier(0);  // (keeps the reads together, ahead of the uses)
+            }
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
 #pragma unroll
               for (int gt = 0; gt < 4; ++gt) xs[0][j][gt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
               for (int s = 0; s < KS; ++s) {
-                const bf16x8 hm = xdrop ? mask_frag(hf0[j][s], mbyte(j, s)) : hf0[j][s];
+                const bf16x8 hm =
+                    xdrop ? mask_frag_fast(hf0[j][s], (mw[j][s] >> (8 * (lane >> 4))) & 0xFFu)
+                          : hf0[j][s];
 #pragma unroll
                 for (int gt = 0; gt < 4; ++gt) xs[0][j][gt] = mfma16(x1[gt][s], hm, xs[0][j][gt]);
               }
@@ -603,7 +630,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
                  h[2], h[3]);
         // the stash MFMAs run while the ring stores drain; with dropout (LDS mask reads and
         // fragment masking) the stash outlasts the drain, so it follows the arrival instead
-        if (!xdrop) do_stash();
+        do_stash();
         if (g == G - 1 && signal) {
           // one arrival per wave and tick, for all its groups' ring stores
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -618,7 +645,6 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
               __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
         }
-        if (xdrop) do_stash();
         if (DEFER) {  // row-major copies: stored behind the next tick's payload loads
 #pragma unroll
           for (int r = 0; r < 4; ++r) {

@@ -39,7 +39,8 @@ void global_norm(const at::Tensor& g, at::Tensor& partials, at::Tensor& norm_out
 
 // out[0] = sum(x^2) with fp32 accumulation; x fp32 or bf16
 void sumsq(const at::Tensor& x, at::Tensor& partials, at::Tensor& out,
-           const c10::optional<at::Tensor>& ticket) {
+           const c10::optional<at::Tensor>& ticket, const c10::optional<at::Tensor>& extra,
+           const c10::optional<at::Tensor>& guard) {
   CHECK_DEV(x); CHECK_CONTIG(x); CHECK_ALIGN16(x);
   TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16,
               "sumsq: fp32 or bf16");
@@ -51,8 +52,23 @@ void sumsq(const at::Tensor& x, at::Tensor& partials, at::Tensor& out,
     TORCH_CHECK(ticket->numel() >= 1, "sumsq: ticket needs one int32");
     tk = reinterpret_cast<unsigned*>(ticket->data_ptr());
   }
+  // extra (one fp32 element added to the sum) / guard (an int32 word copied as a float value
+  // into out[1]): one-launch form only
+  const bool hx = extra.has_value() && extra->defined();
+  const bool hg = guard.has_value() && guard->defined();
+  if (hx) {
+    CHECK_DEV(*extra); CHECK_F32(*extra);
+    TORCH_CHECK(tk && extra->numel() >= 1, "sumsq: extra needs the ticket form");
+  }
+  if (hg) {
+    CHECK_DEV(*guard); CHECK_I32(*guard);
+    TORCH_CHECK(tk && guard->numel() >= 1 && out.numel() >= 2, "sumsq: guard needs the ticket "
+                "form and out[2]");
+  }
   dcr::launch_sumsq(x.data_ptr(), x.scalar_type() == at::kBFloat16, x.numel(),
-                    ptr<float>(partials), ptr<float>(out), tk, cur_stream());
+                    ptr<float>(partials), ptr<float>(out), tk, cur_stream(),
+                    hx ? reinterpret_cast<const float*>(extra->data_ptr()) : nullptr,
+                    hg ? reinterpret_cast<const int*>(guard->data_ptr()) : nullptr);
 }
 
 void adam_clip(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
@@ -1411,7 +1427,8 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor(e!) partials, Tensor(f!) norm_out, float lr_t, float b1, float b2, float eps, "
       "float clip, float gscale=1.0, int n_norm=-1, Tensor? extra_sq=None, "
       "Tensor? skip_if=None, Tensor? lr_dev=None) -> ()");
-  m.def("sumsq(Tensor x, Tensor(a!) partials, Tensor(b!) out, Tensor(c!)? ticket=None) -> ()");
+  m.def("sumsq(Tensor x, Tensor(a!) partials, Tensor(b!) out, Tensor(c!)? ticket=None, "
+        "Tensor? extra=None, Tensor? guard=None) -> ()");
   m.def(
       "lstm_step_ew_fwd(Tensor zrec, Tensor zx, Tensor? ids, Tensor cprev, Tensor(a!) hout, "
       "Tensor(b!)? hout32, Tensor(c!) cout, Tensor(d!) gates, float forget_bias, "

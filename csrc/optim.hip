@@ -145,7 +145,7 @@ __global__ void __launch_bounds__(kOptThreads) norm_only_kernel(const float* __r
 template <typename T>
 __global__ void __launch_bounds__(kOptThreads) sumsq_final_kernel(
     const T* __restrict__ g, int64_t n, float* __restrict__ partials, unsigned* __restrict__ ticket,
-    float* __restrict__ out) {
+    float* __restrict__ out, const float* __restrict__ extra, const int* __restrict__ guard) {
   __shared__ float red[kOptThreads / 64];
   __shared__ unsigned last;
   constexpr int kVec = 16 / (int)sizeof(T);
@@ -179,7 +179,10 @@ __global__ void __launch_bounds__(kOptThreads) sumsq_final_kernel(
     s += __hip_atomic_load(partials + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const float total = block_sum<kOptThreads>(s, red);
   if (threadIdx.x == 0) {
-    out[0] = total;
+    // (extra: one more norm term, e.g. the TF token-norm slot; guard: an error word, copied as a
+    // float value into out[1] so that one all-reduce carries both)
+    out[0] = extra ? total + extra[0] : total;
+    if (guard) out[1] = (float)guard[0];
     __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -200,16 +203,16 @@ void launch_global_norm(const float* g, int64_t n, float* partials, float* norm_
 }
 
 void launch_sumsq(const void* x, bool is_bf16, int64_t n, float* partials, float* out,
-                  unsigned* ticket, hipStream_t stream) {
+                  unsigned* ticket, hipStream_t stream, const float* extra, const int* guard) {
   const int nb = opt_num_partials(n);
   if (ticket) {
     const int nb = opt_num_partials(n) < 256 ? opt_num_partials(n) : 256;
     if (is_bf16)
       sumsq_final_kernel<bf16><<<nb, kOptThreads, 0, stream>>>(static_cast<const bf16*>(x), n,
-                                                                partials, ticket, out);
+                                                                partials, ticket, out, extra, guard);
     else
       sumsq_final_kernel<float><<<nb, kOptThreads, 0, stream>>>(static_cast<const float*>(x), n,
-                                                                 partials, ticket, out);
+                                                                 partials, ticket, out, extra, guard);
     return;
   }
   if (is_bf16)

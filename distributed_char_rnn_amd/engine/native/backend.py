@@ -103,7 +103,11 @@ class NativeBackend(LayoutsMixin, BuffersMixin, ForwardMixin, BackwardMixin, Lib
             self.err.zero_()
             if self._err_host is not None:
                 self._err_host.zero_()
-            raise RuntimeError(f"persistent recurrent kernel timed out (code {v}); the "
+            # (under data parallelism the word also carries the fold of every rank's word as
+            # float bits -- non-zero iff any rank's kernel timed out: a code >= 0x3F800000
+            # may come from a peer)
+            who = " (this or a peer rank)" if v >= 0x3F800000 or v < 0 else ""
+            raise RuntimeError(f"persistent recurrent kernel timed out (code {v}{who}); the "
                                "optimizer skipped the step's update.  Another process sharing "
                                "this GPU can cause this (one rank per GPU); "
                                "DCR_RECURRENCE=step selects the per-step kernels")

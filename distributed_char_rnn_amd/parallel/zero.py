@@ -61,6 +61,10 @@ class ShardedStep:
                  guard: Optional[torch.Tensor] = None):
         self.store, self.opt, self.world, self.rank = store, opt, world, rank
         self.group, self.wire, self.guard = group, wire, guard
+        # RCCL runs the step's per-bucket all-gathers as ONE grouped launch (c10d coalescing);
+        # gloo has no coalesced all-gather, it keeps one call per bucket
+        self._coalesce = (dist.is_initialized() and dist.get_backend(group) == "nccl"
+                          and hasattr(dist, "_coalescing_manager"))
         self.enabled = True  # the backward's readiness callbacks drive ready()
         self.buckets = shard_buckets(store, world, bucket_mb)
         # this rank's chunk of every bucket, and where it sits in the packed owned vector
@@ -171,19 +175,24 @@ class ShardedStep:
         one native sumsq launch over the owned prefix gown[:P] (csrc/optim.hip, one-launch
         form), plus the slot element if this rank owns it."""
         pre = self.gown[:self._pre]
-        if self._pre == 0:
-            self.sumsq.zero_()
-        elif self._ops is not None:
-            self._ops.sumsq(pre, self._npart, self.sumsq, self._ntick)
+        slot = self.gown[self._slot_pos:self._slot_pos + 1] if self._slot_pos >= 0 else None
+        if self._pre > 0 and self._ops is not None:
+            # the slot term and the error word (as a float value in red[1]) ride in the same
+            # launch: no separate add / copy kernels in front of the all-reduce
+            self._ops.sumsq(pre, self._npart, self.red, self._ntick, slot, self.guard)
         else:
-            self.sumsq.copy_((pre.double() * pre.double()).sum().float().reshape(1))
-        if self._slot_pos >= 0:
-            self.sumsq.add_(self.gown[self._slot_pos:self._slot_pos + 1])
-        if self.guard is not None:
-            self.red[1:].copy_(self.guard)
+            if self._pre == 0:
+                self.sumsq.zero_()
+            else:
+                self.sumsq.copy_((pre.double() * pre.double()).sum().float().reshape(1))
+            if slot is not None:
+                self.sumsq.add_(slot)
+            if self.guard is not None:
+                self.red[1:].copy_(self.guard)
         dist.all_reduce(self.red, group=self.group)
-        if self.guard is not None:
-            # every rank's own word folded in (all ranks skip the update and raise together)
+        if self.guard is not None and self.world > 1:
+            # every rank's own word folded in (all ranks skip the update and raise together;
+            # at world 1 the reduced word is the rank's own)
             self.guard.bitwise_or_(self.red[1:].view(torch.int32))
 
     @torch.no_grad()
@@ -209,9 +218,16 @@ class ShardedStep:
         # one asynchronous all-gather per bucket straight from the packed parameters; the
         # gathers pipeline on the communication stream and the caller's stream waits for them
         # (wait_gathers) before anything reads the parameters
-        for (lo, hi), (a, b), p in zip(self.buckets, self.own, self.pos):
-            self._gathers.append(dist.all_gather_into_tensor(
-                flat[lo:hi], self.pown[p:p + (b - a)], group=self.group, async_op=True))
+        if self._coalesce:
+            with dist._coalescing_manager(self.group, async_ops=True) as cm:
+                for (lo, hi), (a, b), p in zip(self.buckets, self.own, self.pos):
+                    dist.all_gather_into_tensor(flat[lo:hi], self.pown[p:p + (b - a)],
+                                                group=self.group)
+            self._gathers.append(cm)
+        else:
+            for (lo, hi), (a, b), p in zip(self.buckets, self.own, self.pos):
+                self._gathers.append(dist.all_gather_into_tensor(
+                    flat[lo:hi], self.pown[p:p + (b - a)], group=self.group, async_op=True))
         self.wait_gathers()
         return norm
 

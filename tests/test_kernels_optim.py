@@ -92,6 +92,14 @@ def test_sumsq_kernel(dcr_ops, dtype, n):
         first = out1 if first is None else first
         assert torch.equal(out1, first)
         assert int(tick.item()) == 0
+    # extra term + error word (parallel/zero.py: one launch in front of the step's all-reduce)
+    extra = torch.tensor([0.25], device="cuda")
+    guard = torch.tensor([9], dtype=torch.int32, device="cuda")
+    out2 = torch.full((2,), -1.0, device="cuda")
+    dcr_ops.sumsq(x, parts, out2, tick, extra, guard)
+    torch.cuda.synchronize()
+    assert out2[0].item() == pytest.approx(first.item() + 0.25, rel=1e-6)
+    assert out2[1].item() == 9.0 and int(tick.item()) == 0
 
 
 @pytest.mark.parametrize("world", [2, 8])
