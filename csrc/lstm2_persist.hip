@@ -258,9 +258,11 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
         const bool ok = tk < T && col * 32 + 16 * j + (lane & 15) < B;
 #pragma unroll
         for (int s = 0; s < KS; ++s)
-          xpf[j][s] = ld8_sc1(r_x, ok ? (unsigned)((size_t)tk * B * H * sizeof(bf16)) + rm_lane +
-                                            rm_off(col, j, s)
-                                      : 0x7FFFFFF0u);
+          // (the offset through an opaque move: LLVM otherwise turns the select into a branch
+          // around the load, and the waitcnt pass then waits for everything at its use)
+          xpf[j][s] = ld8_sc1(r_x, opaque_vgpr(ok ? (unsigned)((size_t)tk * B * H * sizeof(bf16)) +
+                                                        rm_lane + rm_off(col, j, s)
+                                                  : 0x7FFFFFF0u));
       }
     }
   };
@@ -282,7 +284,8 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
         const bool ok = okt && i0 < H && r0 + di / (H / 32) < B;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             rm, (__attribute__((address_space(3))) void*)&mlds[tk & 1][i0], 4,
-            ok ? (unsigned)(((size_t)(tk - 1) * B + r0) * (H / 8) + 4 * (size_t)di) : 0x7FFFFFF0u,
+            opaque_vgpr(ok ? (unsigned)(((size_t)(tk - 1) * B + r0) * (H / 8) + 4 * (size_t)di)
+                           : 0x7FFFFFF0u),
             0, 0, 0);
       }
     }
@@ -628,8 +631,9 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
         STAMPF(g, 5)
         st4bf_ho(loc, ringL + (size_t)((t + 1) & 1) * ringsz + frag_index(b, u0, H), h[0], h[1],
                  h[2], h[3]);
-        // the stash MFMAs run while the ring stores drain; with dropout (LDS mask reads and
-        // fragment masking) the stash outlasts the drain, so it follows the arrival instead
+        // the stash MFMAs run while the ring stores drain (with dropout too, now that its mask
+        // reads are batched and the masking is 5 VALU ops per dword: 1.856 vs 1.860 ms with the
+        // stash behind the arrival, same box)
         do_stash();
         if (g == G - 1 && signal) {
           // one arrival per wave and tick, for all its groups' ring stores
@@ -1015,7 +1019,10 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_persist_kernel(Lstm2BwdArgs 
 // code is compiled out (same-box A/B: the runtime-conditional form cost 2.5 % per step)
 template <int KS, bool DROP>
 static const void* lstm2_fwd_g(int G, bool xin, bool diag) {
-  if (xin) return G == 1 ? (const void*)lstm2_fwd_persist_kernel<KS, 1, DROP, true, false> : nullptr;
+  if (xin)
+    return G != 1 ? nullptr
+           : diag ? (const void*)lstm2_fwd_persist_kernel<KS, 1, DROP, true, true>
+                  : (const void*)lstm2_fwd_persist_kernel<KS, 1, DROP, true, false>;
   switch (G) {
     case 1:
       // (the stamped instantiation exists for the stamp-diagnosed shape only)

@@ -89,7 +89,8 @@ def skew(d, H, B, T):
     return list(zip(names, r)), by_xcd
 
 
-def run(ops, H, T, B, G, want_stamps, reps=5, want_skew=False, drop=False, gather=False):
+def run(ops, H, T, B, G, want_stamps, reps=5, want_skew=False, drop=False, gather=False,
+        xin=False):
     dev = "cuda"
     G = int(ops.lstm2_plan(H, B, G))
     if not G:
@@ -118,11 +119,16 @@ def run(ops, H, T, B, G, want_stamps, reps=5, want_skew=False, drop=False, gathe
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     dfw = torch.zeros(T + 2, G, 8, dtype=torch.int64, device=dev) if want_stamps else None
 
+    # XIN: layer 0's input rows projected in-kernel (the dropout route's default)
+    x0 = r(T * B, H) if xin else None
+    X0T = r(4 * H, H) if xin else None
+    b0 = torch.zeros(4 * H, device=dev) if xin else None
+
     def fwd(diag=None):
         cnt.zero_()
         ops.lstm2_persist_fwd(W0T, W1T, X1T, zx, ids, b1, hb0, cb0, g0, hl0, hb1, cb1, g1, hl1,
                               cnt[0], cnt[1], err, 1.0, 1 << 22, hr0, hr1, G, None, None, diag,
-                              xm, 1.25 if drop else 1.0)
+                              xm, 1.25 if drop else 1.0, b0, x0, X0T)
 
     Wh0, Wh1, Wx1 = r(H, 4 * H), r(H, 4 * H), r(H, 4 * H)
     dtop = torch.randn(T, B, H, device=dev) * 0.01
@@ -175,12 +181,14 @@ def main():
     ap.add_argument("--stamps", action="store_true")
     ap.add_argument("--drop", action="store_true", help="layer 1 input dropout (DROP kernels)")
     ap.add_argument("--gather", action="store_true", help="layer 0 rows gathered from a table")
+    ap.add_argument("--xin", action="store_true", help="layer 0 input projected in-kernel")
     ap.add_argument("--skew", action="store_true", help="every workgroup's hand-off timing (wide BPTT)")
     a = ap.parse_args()
     ops = native.ops()
     for B in a.B:
         for G in a.G:
-            o = run(ops, a.H, a.T, B, G, a.stamps, want_skew=a.skew, drop=a.drop, gather=a.gather)
+            o = run(ops, a.H, a.T, B, G, a.stamps, want_skew=a.skew, drop=a.drop, gather=a.gather,
+                    xin=a.xin)
             if o is None:
                 print(f"H={a.H} B={B} G={G}: no co-resident grid", flush=True)
                 continue
