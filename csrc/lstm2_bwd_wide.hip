@@ -230,7 +230,11 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
   auto prefetch_u = [&](int tk) {  // PF = 5: unconditional, out-of-range lanes read zero
     const int tt = L ? T - 1 - tk : T + 1 - tk;
     const bool ac = L ? tk < T : tk >= 2;
-    const unsigned vgo = (ac && live) ? vg : kOut, vco = (ac && live) ? vc : kOut;
+    // (offsets through an opaque move: LLVM turns a select against an out-of-range offset into
+    // a branch around the load, and the waitcnt pass then drains everything at the next write
+    // of the destination registers)
+    const unsigned vgo = opaque_vgpr((ac && live) ? vg : kOut);
+    const unsigned vco = opaque_vgpr((ac && live) ? vc : kOut);
     const unsigned sg = ac ? (unsigned)((size_t)tt * B * G4H * sizeof(bf16)) : 0u;
     const unsigned sc = ac ? (unsigned)((size_t)tt * B * H * sizeof(float)) : 0u;
 #pragma unroll
@@ -250,11 +254,12 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
     if (DROP) {
       const bool md = tk >= 2 && tk <= T + 1 && live;
       mrow = __builtin_amdgcn_raw_buffer_load_b32(
-          rm, md ? vm : kOut, md ? (unsigned)((size_t)(T + 1 - tk) * B * (H / 8)) : 0u, 0);
+          rm, opaque_vgpr(md ? vm : kOut), md ? (unsigned)((size_t)(T + 1 - tk) * B * (H / 8)) : 0u,
+          0);
     }
   };
   auto prefetch = [&](int tk) {
-    if constexpr (PF == 5) {
+    if constexpr (PF == 5 || ES) {
       prefetch_u(tk);
       return;
     }
@@ -325,7 +330,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
     if (tau >= 1) {
       const unsigned o1 = (unsigned)((s1 & 1) * slabn * sizeof(bf16));
       const unsigned o0 = (unsigned)((s0 & 1) * slabn * sizeof(bf16));
-      if constexpr (PF == 5) {  // unconditional: a skipped layer reads an empty descriptor
+      if constexpr (PF == 5 || ES) {  // unconditional: a skipped layer reads an empty descriptor
         const __amdgpu_buffer_rsrc_t r1e = ld1 ? rz1 : make_rsrc(a.zring1, 0);
         const __amdgpu_buffer_rsrc_t r0e = ld0 ? rz0 : make_rsrc(a.zring0, 0);
 #pragma unroll
@@ -349,7 +354,43 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
       if (PF == 1 || PF == 5 || (PF == 3 && w == 0)) prefetch(tau);
       if constexpr (PF == 5) flush_dz();  // last tick's dZ rows, behind this tick's loads
       __builtin_amdgcn_sched_barrier(0);
-      if (on1) {  // layer l+1: dh partial = dZ_{l+1}[t+1] · W_h,l+1ᵀ, both unit halves
+      f32x4 xsn[2];  // (ES) layer l's dtop partial for its next tick
+      if constexpr (ES) {
+        // layer l+1's dh partial and layer l's next dtop partial in one pass over p1 (both
+        // unconditional: p1 reads zero from an empty descriptor when no slot is loaded); the
+        // W_x,l+1 fragment reads from LDS interleave with the W_h,l+1 chain
+        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        f32x4 xn[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        // W_x fragments read two k-steps ahead (a read waited at its use serialised 32 LDS round
+        // trips per tick)
+        constexpr int kAh = 2;
+        bf16x8 wq[kAh + 1][2];
+#pragma unroll
+        for (int s = 0; s < kAh; ++s) {
+          wq[s][0] = wx1l[w][0][s][lane];
+          wq[s][1] = wx1l[w][1][s][lane];
+        }
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          if (s + kAh < KS) {
+            wq[(s + kAh) % (kAh + 1)][0] = wx1l[w][0][s + kAh][lane];
+            wq[(s + kAh) % (kAh + 1)][1] = wx1l[w][1][s + kAh][lane];
+          }
+          acc[0] = mfma16(wh1[0][s], p1[s], acc[0]);
+          acc[1] = mfma16(wh1[1][s], p1[s], acc[1]);
+          xn[0] = mfma16(wq[s % (kAh + 1)][0], p1[s], xn[0]);
+          xn[1] = mfma16(wq[s % (kAh + 1)][1], p1[s], xn[1]);
+        }
+        if (on1) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+            *reinterpret_cast<float4*>(&part[w][1][u][lane][0]) =
+                make_float4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
+        }
+        xsn[0] = xn[0];
+        xsn[1] = xn[1];
+      }
+      if (!ES && on1) {  // layer l+1: dh partial = dZ_{l+1}[t+1] · W_h,l+1ᵀ, both unit halves
         f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
@@ -360,20 +401,6 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
         for (int u = 0; u < 2; ++u)
           *reinterpret_cast<float4*>(&part[w][1][u][lane][0]) =
               make_float4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
-      }
-      f32x4 xsn[2];  // (ES) layer l's dtop partial for its next tick
-      if constexpr (ES) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (ld1) {
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int s = 0; s < KS; ++s) x = mfma16(wx1l[w][u][s][lane], p1[s], x);
-            xsn[u] = x;
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
       }
       if (on0) {  // layer l: dtop (stashed last tick) + dZ_l[t+1] · W_h,lᵀ
         f32x4 acc[2];
