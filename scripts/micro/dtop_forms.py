@@ -26,10 +26,14 @@ def main():
     WsT = Ws.t().contiguous()                                      # [V, H] (hd["WsTw"])
     out = torch.empty(N, H, device="cuda")
     fl = 2.0 * N * V * H
+    dlogT = dlog.t().contiguous()                                  # [V, N]: a vocab-major dlogits
     forms = {
         "mm(dlog, Ws.t())  [TN view]": lambda: torch.mm(dlog, Ws.t(), out_dtype=torch.float32, out=out),
         "mm(dlog, WsT)     [contig] ": lambda: torch.mm(dlog, WsT, out_dtype=torch.float32, out=out),
         "(Ws @ dlog.t()).t() [NT]   ": lambda: torch.mm(Ws, dlog.t(), out_dtype=torch.float32),
+        "mm(dlogT.t(), Ws.t())      ": lambda: torch.mm(dlogT.t(), Ws.t(), out_dtype=torch.float32, out=out),
+        "mm(dlogT.t(), WsT)         ": lambda: torch.mm(dlogT.t(), WsT, out_dtype=torch.float32, out=out),
+        "(Ws @ dlogT).t()           ": lambda: torch.mm(Ws, dlogT, out_dtype=torch.float32),
     }
     ref = None
     for name, fn in forms.items():
@@ -40,6 +44,19 @@ def main():
             ref = r.clone()
         err = ((r - ref).abs().max() / ref.abs().max()).item()
         print(f"{name}: {t:8.1f} us  {fl / t / 1e6:7.1f} TF/s  max rel diff {err:.2e}", flush=True)
+    # d softmax_w [H, V] = Oᵀ · dlogits (K = N tokens), split-K slabs as engine/native/gemm.py
+    O = (torch.randn(N, H, device="cuda") * 0.5).to(torch.bfloat16)
+    for S in (1, 4, 8):
+        def dws(S=S, src=dlog):
+            if S == 1:
+                return torch.mm(O.t(), src, out_dtype=torch.float32)
+            part = torch.bmm(O.unflatten(0, (S, N // S)).transpose(1, 2),
+                             src.unflatten(0, (S, N // S)), out_dtype=torch.float32)
+            return part.sum(0)
+        t = bench(dws)
+        print(f"dWs = O^T dlog, split {S}: {t:8.1f} us  {fl / t / 1e6:7.1f} TF/s", flush=True)
+    t = bench(lambda: torch.mm(dlogT, O, out_dtype=torch.float32))
+    print(f"dWs^T = dlogT @ O (vocab-major dlogits): {t:8.1f} us  {fl / t / 1e6:7.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":
