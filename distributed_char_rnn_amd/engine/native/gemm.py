@@ -4,6 +4,8 @@ from __future__ import annotations
 
 from typing import Optional
 
+import os
+
 import torch
 
 bf16 = torch.bfloat16
@@ -51,9 +53,16 @@ def split_k(K: int, M: int, Nn: int) -> int:
             S //= 2
         return S
     S = 8 if M * Nn >= (1 << 18) else 16
+    if _SPLIT_CAP:
+        S = _SPLIT_CAP if _SPLIT_CAP > 0 else min(S, -_SPLIT_CAP)
     while S > 1 and (K % S or K // S < 1024):
         S //= 2
     return S
+
+
+# (measurement knob) the split factor of the long token reductions above: n > 0 forces n, n < 0
+# caps at -n (same-box A/B: a cap of 4 cost 53 us per headline step, 2 cost 250 us)
+_SPLIT_CAP = int(os.environ.get("DCR_SPLITK_CAP", "0") or 0)
 
 
 class SumQueue:
