@@ -99,23 +99,27 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_nt_kernel(PersistArgs
     const __amdgpu_buffer_rsrc_t hsrc =
         fring ? make_rsrc(a.hring + (size_t)(t & 1) * Bp * H, sizeof(bf16) * (size_t)Bp * H)
               : make_rsrc(a.hbuf, sizeof(bf16) * (size_t)B * H);
-    // every tile's h fragments are issued before the first MFMA (NT x KS loads in flight)
-    bf16x8 hfs[NT][KS];
-#pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      if (n >= ntl) break;  // wave-uniform
+    // the tiles' h fragments stream through two register buffers: tile n+1's loads are issued
+    // before tile n's MFMAs (NT = 4 would not fit every tile's fragments next to the 256 weight
+    // VGPRs; at NT <= 2 this is the all-tiles-first order).  Unconditional: a tile past the
+    // batch reads an empty descriptor (its MFMAs feed a partial slot no epilogue reads)
+    bf16x8 hb[2][KS];
+    const __amdgpu_buffer_rsrc_t hnone = make_rsrc(a.hring, 0);
+    auto load_tile = [&](int n, bf16x8 (&d)[KS]) {
       const int tile = tile0 + n;
+      const __amdgpu_buffer_rsrc_t src = n < ntl ? hsrc : hnone;
       const unsigned roff =
           (unsigned)(((size_t)(tile * 16 + (lane & 15)) * H + kbase + kq) * sizeof(bf16));
 #pragma unroll
       for (int s = 0; s < KS; ++s)
-        hfs[n][s] = fring ? ld8_sc1(hsrc, (unsigned)lane * 16u, frag_tile_off(tile, w * KS + s, H))
-                          : ld8_sc1(hsrc, roff + s * 64);
-    }
+        d[s] = fring ? ld8_sc1(src, (unsigned)lane * 16u, frag_tile_off(tile, w * KS + s, H))
+                     : ld8_sc1(src, roff + s * 64);
+    };
+    load_tile(0, hb[0]);
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
-      if (n >= ntl) break;  // wave-uniform
-      const bf16x8 (&hf)[KS] = hfs[n];
+      if (n + 1 < NT) load_tile(n + 1, hb[(n + 1) & 1]);
+      const bf16x8 (&hf)[KS] = hb[n & 1];
       f32x4 acc[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -250,18 +254,21 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_nt_kernel(PersistArgs
                          frag_tile_off(tile, (g * H + w * (H / 4)) / 32 + s, G4H));
       };
       load_chunk(0, db[0]);
-      f32x4 pacc = f32x4{0.f, 0.f, 0.f, 0.f};
+      // a tile loop that is not unrolled around the four gate chunks of a tile (c = 4 n + g:
+      // the chunk buffer parity is g's); fully unrolled over NT = 4 tiles the register
+      // allocator had spilled 1.5 KB per lane
+#pragma unroll 1
+      for (int n = 0; n < ntl; ++n) {
+        f32x4 pacc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int c = 0; c < 4 * NT; ++c) {
-        if (c >= nch) break;  // wave-uniform
-        if (c + 1 < nch) load_chunk(c + 1, db[(c + 1) & 1]);
+        for (int g = 0; g < 4; ++g) {
+          const int c = 4 * n + g;
+          if (c + 1 < nch) load_chunk(c + 1, db[(g + 1) & 1]);
 #pragma unroll
-        for (int s = 0; s < KSG; ++s) pacc = mfma16(wf[(c % 4) * KSG + s], db[c & 1][s], pacc);
-        if (c % 4 == 3) {
-          *reinterpret_cast<float4*>(&part[w][c / 4][lane][0]) =
-              make_float4(pacc[0], pacc[1], pacc[2], pacc[3]);
-          pacc = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int s = 0; s < KSG; ++s) pacc = mfma16(wf[g * KSG + s], db[g & 1][s], pacc);
         }
+        *reinterpret_cast<float4*>(&part[w][n][lane][0]) =
+            make_float4(pacc[0], pacc[1], pacc[2], pacc[3]);
       }
       __syncthreads();
     }
@@ -342,13 +349,13 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_nt_kernel(PersistArgs
 // ------------------------------------------------------------------------------------------
 // host side (called from lstm_persist.hip's selection for H > 1024)
 // ------------------------------------------------------------------------------------------
-// Batch tiles per workgroup: the smallest NT in {1, 2} whose (H/16) x ceil(B/16NT) grid fits
+// Batch tiles per workgroup: the smallest NT in {1, 2, 4} whose (H/16) x ceil(B/16NT) grid fits
 // one workgroup per CU; 0 if none does (the large-batch steps stay on the library form, where
 // the per-step GEMMs are efficient) or the shape has no instantiation.
 int lstm_persist_nt_tiles(int H, int B, int cus) {
   if (H != 2048 || B < 1 || cus <= 0) return 0;
   const int ntile = (B + 15) / 16;
-  for (int nt = 1; nt <= 2; nt *= 2)
+  for (int nt = 1; nt <= 4; nt *= 2)
     if ((H / 16) * ((ntile + nt - 1) / nt) <= cus) return nt;
   return 0;
 }
@@ -364,6 +371,8 @@ const void* lstm_persist_nt_fn(int bwd, int H, int B, int cus) {
                        : (const void*)lstm_fwd_persist_nt_kernel<16, 1>;
     case 2: return bwd ? (const void*)lstm_bwd_persist_nt_kernel<64, 2>
                        : (const void*)lstm_fwd_persist_nt_kernel<16, 2>;
+    case 4: return bwd ? (const void*)lstm_bwd_persist_nt_kernel<64, 4>
+                       : (const void*)lstm_fwd_persist_nt_kernel<16, 4>;
   }
   return nullptr;
 }

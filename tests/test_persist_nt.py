@@ -36,7 +36,11 @@ def _batch(B, T, H, L, seed):
 @pytest.mark.parametrize("B,T,L,dbg", [(64, 6, 2, "nt_bwd=0"), (20, 5, 1, "nt_bwd=0"),
                                        (64, 6, 2, "nt_bwd=1"), (20, 5, 1, "nt_bwd=1"),
                                        (7, 4, 1, "nt_bwd=1"), (64, 6, 2, "lib"),
-                                       (96, 4, 2, "lib,bigstep=2")])
+                                       (96, 4, 2, "lib,bigstep=2"),
+                                       # NT = 4 batch tiles per workgroup (B = 65-128); 96:
+                                       # the second batch group holds two tiles, 100: ragged rows
+                                       (128, 5, 2, "nt_bwd=1"), (96, 4, 2, "nt_bwd=1"),
+                                       (100, 4, 1, "nt_bwd=1")])
 def test_nt_kernels_match_oracle(B, T, L, dbg, dcr_ops, monkeypatch):
     """Default: both directions persistent; nt_bwd=0: persistent forward, library BPTT steps;
     lib: the per-step library / fused step kernels (the upper layer's input bias added by
@@ -46,7 +50,7 @@ def test_nt_kernels_match_oracle(B, T, L, dbg, dcr_ops, monkeypatch):
                        else f"persist_min_t=1,{dbg}")
     H = 2048
     if not lib:
-        assert int(dcr_ops.lstm_persist_nt_tiles(H, B)) in (1, 2)
+        assert int(dcr_ops.lstm_persist_nt_tiles(H, B)) in (1, 2, 4)
     cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=L)
     nat = CharRNN(cfg, device="cuda", seed=5)
     # non-zero biases (TF initialises them to zero): the upper layers' input bias is added in
