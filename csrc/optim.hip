@@ -229,10 +229,14 @@ void launch_adam_clip(float* p, const float* g, float* m, float* v, bf16* pbf, i
                       float clip, float gscale, int64_t n_norm, const float* extra_sq,
                       const unsigned* skip_if, const float* lr_dev, hipStream_t stream) {
   const int nb = opt_num_partials(n);
-  sumsq_partials_kernel<float><<<nb, kOptThreads, 0, stream>>>(g, n_norm, partials, extra_sq);
-  adam_apply_kernel<<<nb, kOptThreads, 0, stream>>>(p, g, m, v, pbf, n, partials, nb, norm_out,
-                                                    lr_t, b1, b2, eps, clip, gscale, skip_if,
-                                                    lr_dev);
+  // no norm terms in g (the sharded step's packed chunks: the reduced sum of squares comes in
+  // as extra_sq): the update reads that one value, no partials launch
+  const bool only_extra = n_norm == 0 && extra_sq;
+  if (!only_extra)
+    sumsq_partials_kernel<float><<<nb, kOptThreads, 0, stream>>>(g, n_norm, partials, extra_sq);
+  adam_apply_kernel<<<nb, kOptThreads, 0, stream>>>(
+      p, g, m, v, pbf, n, only_extra ? extra_sq : partials, only_extra ? 1 : nb, norm_out, lr_t,
+      b1, b2, eps, clip, gscale, skip_if, lr_dev);
 }
 
 }  // namespace dcr

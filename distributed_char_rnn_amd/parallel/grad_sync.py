@@ -111,9 +111,11 @@ class GradSync:
             self._ev_ready = []
             self._ev_end = None
 
-    def ready(self, upto: Optional[int] = None):
+    def ready(self, upto: Optional[int] = None, sync: bool = False):
         """Launch every not-yet-launched bucket that ends at or below flat offset ``upto``
-        (``None`` = everything)."""
+        (``None`` = everything).  ``sync``: as blocking collectives, which RCCL runs on the
+        caller's stream (no cross-stream event hop; for buckets whose exchange nothing is left
+        to overlap, after every earlier asynchronous one has been waited for)."""
         if not self.enabled:
             return
         lim = self.store.numel if upto is None else upto
@@ -133,10 +135,10 @@ class GradSync:
                 # ring hop: N-1 roundings of partial sums at N ranks.
                 send, recv = self._bufs_for(lo, hi, g.device)[:2]
                 send[: hi - lo].copy_(g)  # the tail padding stays zero (allocated zeroed)
-                w = dist.all_to_all_single(recv, send, group=self.group, async_op=True)
+                w = dist.all_to_all_single(recv, send, group=self.group, async_op=not sync)
                 self._work.append((w, lo, hi, recv))
             else:
-                w = dist.all_reduce(g, group=self.group, async_op=True)
+                w = dist.all_reduce(g, group=self.group, async_op=not sync)
                 self._work.append((w, lo, hi, None))
             self._next += 1
 
@@ -150,19 +152,18 @@ class GradSync:
         if self.timing:
             self._ev_end = torch.cuda.Event(enable_timing=True)
             self._ev_end.record()
-        self.ready(None)
-        gathers = []
+        # the buckets the backward launched first, then the rest on this stream (nothing is
+        # left to overlap them with, and a blocking collective costs no stream-event hop)
         for w, lo, hi, recv in self._work:
             w.wait()
+        self.ready(None, sync=True)
+        for w, lo, hi, recv in self._work:
             if recv is not None:  # bf16 wire: fp32 sum of my chunk, then gather every chunk
                 _, _, mine, mine16, full = self._bufs_for(lo, hi, recv.device)
                 torch.sum(recv.view(self.world, -1), 0, dtype=torch.float32, out=mine)
                 mine16.copy_(mine)
-                gw = dist.all_gather_into_tensor(full, mine16, group=self.group, async_op=True)
-                gathers.append((gw, lo, hi, full))
-        for gw, lo, hi, full in gathers:
-            gw.wait()
-            self.store.grad[lo:hi].copy_(full[: hi - lo])
+                dist.all_gather_into_tensor(full, mine16, group=self.group)
+                self.store.grad[lo:hi].copy_(full[: hi - lo])
         self._work.clear()
         self._next = 0
         if self.guard is not None and self.guard_view is not None and self.world > 1:

@@ -125,7 +125,6 @@ class ShardedStep:
             self._npart = torch.empty(max(1, int(self._ops.opt_num_partials(max(self._pre, 1)))),
                                       dtype=torch.float32, device=dev)
             self._ntick = torch.zeros(1, dtype=torch.int32, device=dev)  # the kernel resets it
-        self._gathers: list = []
         self._next = 0
         self._work: list = []
         # bucket indices in launch order of the current step (tests, --profile reports)
@@ -147,9 +146,10 @@ class ShardedStep:
         self._work.clear()
         self.launched = []
 
-    def ready(self, upto: Optional[int] = None) -> None:
+    def ready(self, upto: Optional[int] = None, sync: bool = False) -> None:
         """Launch the reduce-scatter of every not-yet-launched bucket ending at or below flat
-        offset ``upto`` (None = everything)."""
+        offset ``upto`` (None = everything); ``sync`` as blocking collectives on the caller's
+        stream (GradSync.ready)."""
         lim = self.store.numel if upto is None else upto
         g = self.store.grad
         while self._next < len(self.buckets) and self.buckets[self._next][1] <= lim:
@@ -160,11 +160,11 @@ class ShardedStep:
             if self._wire16 is not None:
                 send, recv = (b[lo:hi] for b in self._wire16)
                 send.copy_(g[lo:hi])
-                w = dist.all_to_all_single(recv, send, group=self.group, async_op=True)
+                w = dist.all_to_all_single(recv, send, group=self.group, async_op=not sync)
                 self._work.append((w, i, recv))
             else:
                 w = dist.reduce_scatter_tensor(out, g[lo:hi], op=dist.ReduceOp.SUM,
-                                               group=self.group, async_op=True)
+                                               group=self.group, async_op=not sync)
                 self._work.append((w, i, None))
             self.launched.append(i)
             self._next += 1
@@ -201,9 +201,12 @@ class ShardedStep:
         launched by the backward are not relaunched): finish the exchange, update the owned
         chunks, gather the parameters.  Returns the pre-clip global norm (device tensor)."""
         self.early = len(self.launched)  # buckets the backward launched (reports)
-        self.ready(None)
+        # the backward's buckets first, then the rest as blocking collectives on this stream
+        # (nothing left to overlap; no stream-event hop)
         for w, i, recv in self._work:
             w.wait()
+        self.ready(None, sync=True)
+        for w, i, recv in self._work:
             if recv is not None:  # bf16 wire: the owner sums the world copies of its chunk
                 c = (self.buckets[i][1] - self.buckets[i][0]) // self.world
                 torch.sum(recv.view(self.world, c), 0, dtype=torch.float32,
@@ -215,28 +218,18 @@ class ShardedStep:
         norm = self.opt.step_packed(lr, self.pown[:q], self.gown[:q], self.mown[:q],
                                     self.vown[:q], self.sumsq, grad_scale=1.0 / self.world)
         flat = self.store.flat
-        # one asynchronous all-gather per bucket straight from the packed parameters; the
-        # gathers pipeline on the communication stream and the caller's stream waits for them
-        # (wait_gathers) before anything reads the parameters
+        # one all-gather per bucket straight from the packed parameters (RCCL: one coalesced
+        # group), blocking, i.e. on this stream: the next forward reads the parameters anyway
         if self._coalesce:
-            with dist._coalescing_manager(self.group, async_ops=True) as cm:
+            with dist._coalescing_manager(self.group, async_ops=False):
                 for (lo, hi), (a, b), p in zip(self.buckets, self.own, self.pos):
                     dist.all_gather_into_tensor(flat[lo:hi], self.pown[p:p + (b - a)],
                                                 group=self.group)
-            self._gathers.append(cm)
         else:
             for (lo, hi), (a, b), p in zip(self.buckets, self.own, self.pos):
-                self._gathers.append(dist.all_gather_into_tensor(
-                    flat[lo:hi], self.pown[p:p + (b - a)], group=self.group, async_op=True))
-        self.wait_gathers()
+                dist.all_gather_into_tensor(flat[lo:hi], self.pown[p:p + (b - a)],
+                                            group=self.group)
         return norm
-
-    def wait_gathers(self) -> None:
-        """Make the current stream wait for the step's parameter all-gathers (on NCCL / RCCL a
-        stream dependency, not a host block)."""
-        for w in self._gathers:
-            w.wait()
-        self._gathers.clear()
 
     @torch.no_grad()
     def gather_slots(self) -> None:

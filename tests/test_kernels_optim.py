@@ -43,7 +43,7 @@ def test_adam_clip_matches_reference(dcr_ops, n, clip):
     torch.testing.assert_close(pbf.float(), p.to(torch.bfloat16).float(), rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("n,n_norm", [(4096, 4096), (100000, 60000), (4265088, 4265024)])
+@pytest.mark.parametrize("n,n_norm", [(4096, 4096), (100000, 60000), (4265088, 4265024), (5000, 0)])
 def test_adam_clip_partial_norm_plus_extra(dcr_ops, n, n_norm):
     """norm = sqrt(sum(g[:n_norm]^2) + extra) (TF IndexedSlices embedding term); the update
     still covers all n elements."""
