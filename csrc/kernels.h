@@ -181,7 +181,7 @@ int lstm_persist_supported(int H, int B, int cus);
 // H > 1024 (lstm_persist_nt.hip): 16-unit workgroups over NT 16-row batch tiles
 int lstm_persist_nt_tiles(int H, int B, int cus);
 int lstm_persist_nt_grid(int H, int B, int cus);
-const void* lstm_persist_nt_fn(int bwd, int H, int B, int cus);
+const void* lstm_persist_nt_fn(int bwd, int H, int B, int cus, int diag = 0);
 int lstm_persist_grid(int H, int B, int cus);
 int lstm_persist_xfuse_supported(int H, int B, int cus);
 // max co-resident workgroups per CU of the instantiation a launch with these flags would use

@@ -457,7 +457,8 @@ static int ub_for(int H, int B, int cus) {
 static const void* pick(int bwd, int H, int B, int flags, int cus) {
   // H > 1024: 16-unit x NT-tile workgroups (lstm_persist_nt.hip; no fused input, no fused
   // dEW, no diag stamps: the plain instantiation for every flag)
-  if (H > 1024) return (flags & PF_FUSED) ? nullptr : lstm_persist_nt_fn(bwd, H, B, cus);
+  if (H > 1024)
+    return (flags & PF_FUSED) ? nullptr : lstm_persist_nt_fn(bwd, H, B, cus, flags & PF_DIAG);
   const int ub = ub_for(H, B, cus);
   if (!bwd) {
     const int ks = H / 128;

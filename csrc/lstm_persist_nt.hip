@@ -31,15 +31,50 @@
 #include "common.h"
 #include "kernels.h"
 #include "persist_common.h"
+#include "debug_env.h"
 
 namespace dcr {
 
-template <int KS, int NT>
+// DIAG builds record s_memtime stamps of workgroup 0 per step (phase shares only, never timing
+// claims; cdna_hip_programming.md §7 "In-kernel stamps"); scripts/persist_stamps.py --H 2048
+#define STAMP(i)                                                                    \
+  if constexpr (DIAG) {                                                             \
+    if (blockIdx.x == 0 && threadIdx.x == 0)                                        \
+      a.diag[(size_t)t * 8 + (i)] = __builtin_amdgcn_s_memtime();                   \
+  }
+
+// one LDS fragment read (16 B per lane) at a byte offset, invisible to the compiler's waitcnt
+// pass (the DMA forward below counts its own lgkmcnt)
+template <int OFF>
+__device__ __forceinline__ void ds_rd128(bf16x8& d, unsigned addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait(bf16x8& d) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(d) : "i"(N) : "memory");
+}
+
+template <int KS, int NT, bool DIAG = false, bool DMA = false>
 __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_nt_kernel(PersistArgs a) {
-  // single-buffered partials: every step starts with a workgroup barrier that the epilogue
-  // waves reach only after reading the previous step's partials
-  __shared__ __attribute__((aligned(16))) float part[4][NT][4][64][4];
+  // single-buffered partials [wave][tile][gate][lane] (float4): every step starts with a
+  // workgroup barrier that the epilogue waves reach only after reading the previous step's
+  // partials.  DMA (NT = 4): the h tiles arrive by LDS-DMA, two per step through each of xa /
+  // xb ([wave][k-step][lane], each wave its own K quarter: 16 KB), and the partials go into
+  // slices already read (128 KB in all)
+  static_assert(!DMA || (NT == 4 && KS == 16), "LDS-DMA forward: NT = 4, H = 2048");
+  constexpr int kXtF4 = 4 * KS * 64;
+  __shared__ __attribute__((aligned(16))) float part[DMA ? 1 : 4][NT][4][64][4];
+  __shared__ __attribute__((aligned(16))) float4 xa[DMA ? kXtF4 : 1];
+  __shared__ __attribute__((aligned(16))) float4 xb[DMA ? kXtF4 : 1];
   __shared__ unsigned arr;
+  // partial slot (wave wv, tile n, gate g): 64 float4.  DMA: tile 2 -> xa, 3 -> xb, 0 / 1 ->
+  // xb +8 / +12 KB (the last tile read out of each)
+  auto pslot = [&](int wv, int n, int g) -> float4* {
+    if constexpr (DMA)
+      return (n == 2 ? xa : xb) + wv * KS * 64 + (n < 2 ? (n + 2) * 4 * 64 : 0) + g * 64;
+    else
+      return reinterpret_cast<float4*>(&part[wv][n][g][0][0]);
+  };
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, B = a.B, T = a.T;
@@ -81,8 +116,20 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_nt_kernel(PersistArgs
     for (int g = 0; g < 4; ++g) ld4f(a.bias + (size_t)g * H + u0, bx[g]);
   }
   __syncthreads();  // arr
+  if constexpr (DMA) {
+    // h_0 published into ring slot 0 in fragment order (padded rows as zeros) and signalled on
+    // counter 0: every step's tiles are then the same fragment-ring loads
+    if (epi) {
+      float h0[4] = {0.f, 0.f, 0.f, 0.f};
+      if (live) ld4bf(a.hbuf + bh, h0);
+      st4bf_sc1(a.hring + frag_index(b, u0, H), h0[0], h0[1], h0[2], h0[3]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) wg_arrive(&arr, (unsigned)ntl, cnt + (ubk & 3));
+    }
+  }
 
   for (int t = 0; t < T; ++t) {
+    STAMP(0);
     float zx[4][4] = {};
     if (live) {
       const float* zrow = a.ids ? a.zx + (size_t)a.ids[(size_t)t * B + b] * a.zx_ld
@@ -90,12 +137,14 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_nt_kernel(PersistArgs
 #pragma unroll
       for (int g = 0; g < 4; ++g) ld4f(zrow + (size_t)g * H + u0, zx[g]);
     }
-    if (t > 0) {
+    if (DMA || t > 0) {
       if ((int)threadIdx.x == a.poller && !dead)
         dead = !poll_shards4(cnt + (size_t)t * 4, target, a.spin_limit, a.err, 1u);
     }
+    STAMP(1);
     __syncthreads();
-    const bool fring = t > 0;  // slot 0 (initial state) is row-major
+    STAMP(2);
+    const bool fring = DMA || t > 0;  // slot 0 (initial state) is row-major (DMA: published)
     const __amdgpu_buffer_rsrc_t hsrc =
         fring ? make_rsrc(a.hring + (size_t)(t & 1) * Bp * H, sizeof(bf16) * (size_t)Bp * H)
               : make_rsrc(a.hbuf, sizeof(bf16) * (size_t)B * H);
@@ -115,32 +164,102 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_nt_kernel(PersistArgs
         d[s] = fring ? ld8_sc1(src, (unsigned)lane * 16u, frag_tile_off(tile, w * KS + s, H))
                      : ld8_sc1(src, roff + s * 64);
     };
-    load_tile(0, hb[0]);
+    auto put = [&](int n, const f32x4 (&acc)[4]) {
 #pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      if (n + 1 < NT) load_tile(n + 1, hb[(n + 1) & 1]);
-      const bf16x8 (&hf)[KS] = hb[n & 1];
-      f32x4 acc[4];
+      for (int g = 0; g < 4; ++g) {
+        if constexpr (DMA) {
+          // (inline asm: the waitcnt pass would hold a plain LDS store behind every LDS-DMA in
+          // flight; this slice was read by this wave already)
+          const unsigned addr =
+              (unsigned)(size_t)(__attribute__((address_space(3))) void*)(pslot(w, n, g) + lane);
+          asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(acc[g]) : "memory");
+        } else {
+          pslot(w, n, g)[lane] = make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
+        }
+      }
+    };
+    if constexpr (DMA) {
+      // tiles 0-1 by LDS-DMA (sc1, like every hand-off load) at once, tile 2 into xa as soon as
+      // tile 0 has been multiplied out of it, tile 3 into xb after tile 1: two round trips per
+      // step instead of the register double buffer's chain of four
+      auto dma_tile = [&](int n, float4* dst) {
+        const __amdgpu_buffer_rsrc_t src = n < ntl ? hsrc : hnone;
+        dst += w * KS * 64;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int s = 0; s < KS; ++s)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              src, (__attribute__((address_space(3))) void*)(dst + s * 64), 16,
+              (unsigned)lane * 16u, frag_tile_off(tile0 + n, w * KS + s, H), 0, kAuxSc1);
+      };
+      // a tile's fragments out of LDS three k-steps ahead of their MFMAs (one LDS round trip is
+      // longer than a k-step's four MFMAs), the waits counted here
+      auto lds_tile = [&](const float4* src, f32x4 (&acc)[4]) {
+        const unsigned base =
+            (unsigned)(size_t)(__attribute__((address_space(3))) const void*)(src + w * KS * 64 +
+                                                                               lane);
+        bf16x8 q[4];
 #pragma unroll
-      for (int s = 0; s < KS; ++s)
+        for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        ds_rd128<0 * 1024>(q[0], base);
+        ds_rd128<1 * 1024>(q[1], base);
+        ds_rd128<2 * 1024>(q[2], base);
+#define DCR_NT_KSTEP(S)                                                              \
+  if constexpr ((S) + 3 < KS) ds_rd128<((S) + 3) * 1024>(q[((S) + 3) & 3], base);   \
+  if constexpr ((S) + 3 < KS) lgkm_wait<3>(q[(S) & 3]);                              \
+  else if constexpr ((S) + 2 < KS) lgkm_wait<2>(q[(S) & 3]);                         \
+  else if constexpr ((S) + 1 < KS) lgkm_wait<1>(q[(S) & 3]);                         \
+  else lgkm_wait<0>(q[(S) & 3]);                                                     \
+  _Pragma("unroll") for (int g = 0; g < 4; ++g) acc[g] = mfma16(wf[g][S], q[(S) & 3], acc[g]);
+        DCR_NT_KSTEP(0) DCR_NT_KSTEP(1) DCR_NT_KSTEP(2) DCR_NT_KSTEP(3)
+        DCR_NT_KSTEP(4) DCR_NT_KSTEP(5) DCR_NT_KSTEP(6) DCR_NT_KSTEP(7)
+        DCR_NT_KSTEP(8) DCR_NT_KSTEP(9) DCR_NT_KSTEP(10) DCR_NT_KSTEP(11)
+        DCR_NT_KSTEP(12) DCR_NT_KSTEP(13) DCR_NT_KSTEP(14) DCR_NT_KSTEP(15)
+#undef DCR_NT_KSTEP
+      };
+      f32x4 a0[4], a1[4], acc[4];
+      dma_tile(0, xa);
+      dma_tile(1, xb);
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile 0 landed
+      lds_tile(xa, a0);
+      dma_tile(2, xa);  // (tile 0's reads have returned: the MFMAs above consumed them)
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile 1 landed
+      lds_tile(xb, a1);
+      dma_tile(3, xb);
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile 2 landed
+      lds_tile(xa, acc);
+      put(2, acc);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile 3 landed
+      lds_tile(xb, acc);
+      put(3, acc);
+      put(0, a0);
+      put(1, a1);
+    } else {
+      load_tile(0, hb[0]);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) acc[g] = mfma16(wf[g][s], hf[s], acc[g]);
+      for (int n = 0; n < NT; ++n) {
+        if (n + 1 < NT) load_tile(n + 1, hb[(n + 1) & 1]);
+        const bf16x8 (&hf)[KS] = hb[n & 1];
+        f32x4 acc[4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<float4*>(&part[w][n][g][lane][0]) =
-            make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
+        for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) acc[g] = mfma16(wf[g][s], hf[s], acc[g]);
+        put(n, acc);
+      }
     }
+    STAMP(3);
     __syncthreads();
+    STAMP(4);
     if (epi) {
       float z[4][4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const float4 s0 = *reinterpret_cast<const float4*>(&part[0][w][g][lane][0]);
-        const float4 s1 = *reinterpret_cast<const float4*>(&part[1][w][g][lane][0]);
-        const float4 s2 = *reinterpret_cast<const float4*>(&part[2][w][g][lane][0]);
-        const float4 s3 = *reinterpret_cast<const float4*>(&part[3][w][g][lane][0]);
+        const float4 s0 = pslot(0, w, g)[lane];
+        const float4 s1 = pslot(1, w, g)[lane];
+        const float4 s2 = pslot(2, w, g)[lane];
+        const float4 s3 = pslot(3, w, g)[lane];
         z[g][0] = s0.x + s1.x + s2.x + s3.x + (zx[g][0] + bx[g][0]);
         z[g][1] = s0.y + s1.y + s2.y + s3.y + (zx[g][1] + bx[g][1]);
         z[g][2] = s0.z + s1.z + s2.z + s3.z + (zx[g][2] + bx[g][2]);
@@ -157,11 +276,13 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_nt_kernel(PersistArgs
         h[r] = go[r] * tanhf_(c[r]);
       }
       // (padded rows are handed off too: zero inputs, finite values, never read back)
+      STAMP(5);
       st4bf_sc1(a.hring + (size_t)((t + 1) & 1) * Bp * H + frag_index(b, u0, H), h[0], h[1], h[2],
                 h[3]);
       if (t + 1 < T) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) wg_arrive(&arr, (unsigned)ntl, cnt + (size_t)(t + 1) * 4 + (ubk & 3));
+        STAMP(6);
       }
       if (live) {
         const size_t o = (size_t)(t + 1) * B * H + bh;
@@ -186,7 +307,7 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_nt_kernel(PersistArgs
 // KS = 4H / 128 k-steps per wave (K = 4H split by unit quarter inside every gate, as in
 // lstm_persist.hip); the payload of one tile is streamed in chunks of KSG = KS / 4 k-steps (one
 // gate segment), two chunks in flight next to the 256 weight VGPRs.
-template <int KS, int NT>
+template <int KS, int NT, bool DIAG = false>
 __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_nt_kernel(PersistArgs a) {
   __shared__ __attribute__((aligned(16))) float part[4][NT][64][4];
   __shared__ unsigned arr;
@@ -228,6 +349,7 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_nt_kernel(PersistArgs
   __syncthreads();  // arr
 
   for (int t = T - 1; t >= 0; --t) {
+    STAMP(0);
     float gi[4] = {}, gj[4] = {}, gf[4] = {}, go[4] = {}, cc[4] = {}, cp[4] = {}, dtop[4] = {};
     if (live) {
       const bf16* gp = a.gates + ((size_t)t * B + b) * G4H + u0;
@@ -239,7 +361,9 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_nt_kernel(PersistArgs
     if (t < T - 1) {
       if ((int)threadIdx.x == a.poller && !dead)
         dead = !poll_shards4(cnt + (size_t)(t + 1) * 4, target, a.spin_limit, a.err, 2u);
+      STAMP(1);
       __syncthreads();
+      STAMP(2);
       const __amdgpu_buffer_rsrc_t zsrc =
           make_rsrc(a.zring + (size_t)((t + 1) & 1) * Bp * G4H, sizeof(bf16) * (size_t)Bp * G4H);
       // chunk c = (tile n = c / 4, gate g = c % 4); two chunk buffers: the loads of chunk c+1
@@ -270,7 +394,9 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_nt_kernel(PersistArgs
         *reinterpret_cast<float4*>(&part[w][n][lane][0]) =
             make_float4(pacc[0], pacc[1], pacc[2], pacc[3]);
       }
+      STAMP(3);
       __syncthreads();
+      STAMP(4);
     }
     if (epi) {
       float dh[4];
@@ -298,6 +424,7 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_nt_kernel(PersistArgs
         dc[r] = dcv * gf[r];
       }
       bf16* const zr = a.zring + (size_t)(t & 1) * Bp * G4H;
+      STAMP(5);
       st4bf_sc1(zr + frag_index(b, u0, G4H), di[0], di[1], di[2], di[3]);
       st4bf_sc1(zr + frag_index(b, H + u0, G4H), dj[0], dj[1], dj[2], dj[3]);
       st4bf_sc1(zr + frag_index(b, 2 * H + u0, G4H), df_[0], df_[1], df_[2], df_[3]);
@@ -305,6 +432,7 @@ __global__ void __launch_bounds__(256, 1) lstm_bwd_persist_nt_kernel(PersistArgs
       if (t > 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) wg_arrive(&arr, (unsigned)ntl, cnt + (size_t)t * 4 + (ubk & 3));
+        STAMP(6);
       }
       if (live) {
         bf16* dz = a.dz + ((size_t)t * B + b) * G4H + u0;
@@ -365,14 +493,21 @@ int lstm_persist_nt_grid(int H, int B, int cus) {
   return nt ? (H / 16) * (((B + 15) / 16 + nt - 1) / nt) : 0;
 }
 
-const void* lstm_persist_nt_fn(int bwd, int H, int B, int cus) {
-  switch (lstm_persist_nt_tiles(H, B, cus)) {
+const void* lstm_persist_nt_fn(int bwd, int H, int B, int cus, int diag) {
+  switch (lstm_persist_nt_tiles(H, B, cus) * (diag ? -1 : 1)) {
     case 1: return bwd ? (const void*)lstm_bwd_persist_nt_kernel<64, 1>
                        : (const void*)lstm_fwd_persist_nt_kernel<16, 1>;
     case 2: return bwd ? (const void*)lstm_bwd_persist_nt_kernel<64, 2>
                        : (const void*)lstm_fwd_persist_nt_kernel<16, 2>;
+    // NT = 4 forward: h tiles by LDS-DMA (DCR_DEBUG=nt_dma=0: register double buffer)
     case 4: return bwd ? (const void*)lstm_bwd_persist_nt_kernel<64, 4>
-                       : (const void*)lstm_fwd_persist_nt_kernel<16, 4>;
+                   : debug_int("nt_dma", 1) ? (const void*)lstm_fwd_persist_nt_kernel<16, 4, false, true>
+                                            : (const void*)lstm_fwd_persist_nt_kernel<16, 4>;
+    case -2: return bwd ? (const void*)lstm_bwd_persist_nt_kernel<64, 2, true>
+                        : (const void*)lstm_fwd_persist_nt_kernel<16, 2, true>;
+    case -4: return bwd ? (const void*)lstm_bwd_persist_nt_kernel<64, 4, true>
+                    : debug_int("nt_dma", 1) ? (const void*)lstm_fwd_persist_nt_kernel<16, 4, true, true>
+                                             : (const void*)lstm_fwd_persist_nt_kernel<16, 4, true>;
   }
   return nullptr;
 }

@@ -66,6 +66,8 @@ DEBUG_KEYS = {
     "nt_bwd": "0: H > 1024: persistent forward (csrc/lstm_persist_nt.hip) but library-GEMM "
               "BPTT steps",
     "nt_poll": "w: hand-off poller on wave w in the H > 1024 persistent kernels (C++ launcher)",
+    "nt_dma": "0: H > 1024 persistent forward at NT = 4 streams its h tiles through registers "
+              "instead of LDS-DMA (C++ launcher)",
     "wgrad": "1: hand-written wgrad kernel for the weight gradients (default: library split-K)",
     "gru_ub": "1: 16-unit GRU workgroups (C++)",
     "gru_nt": "N: N batch tiles of 16 rows per GRU workgroup (C++)",
