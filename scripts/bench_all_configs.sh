@@ -10,6 +10,7 @@ run "lstm512x2 seq128 B256 (repeat)  " --steps 40 --warmup 5 || exit 1
 run "gru1024x3 seq256 B128           " --model gru --hidden 1024 --layers 3 --seq 256 --batch 128 --steps 10 --warmup 3 || exit 1
 run "gru1024x3 seq256 B256 (NT=2)    " --model gru --hidden 1024 --layers 3 --seq 256 --batch 256 --steps 10 --warmup 3 || exit 1
 run "lstm2048x4 seq512 B64           " --hidden 2048 --layers 4 --seq 512 --batch 64 --steps 3 --warmup 1 || exit 1
+run "lstm2048x4 seq512 B128 (NT=4)   " --hidden 2048 --layers 4 --seq 512 --batch 128 --steps 3 --warmup 1 || exit 1
 run "lstm2048x4 seq512 B1024 (large)  " --hidden 2048 --layers 4 --seq 512 --batch 1024 --steps 2 --warmup 1 || exit 1
 run "lstm512x2 seq128 B256 vocab8192 " --vocab 8192 --steps 10 --warmup 3 || exit 1
 run "lstm128x1 seq32 B50 (tiny)      " --hidden 128 --layers 1 --seq 32 --batch 64 --steps 20 --warmup 5 || exit 1
