@@ -123,3 +123,28 @@ def test_nt_spin_timeout_drains_and_guards(monkeypatch):
     assert torch.equal(m.store.flat, p0)
     with pytest.raises(RuntimeError, match="timed out"):
         m.check_errors()
+
+
+@pytest.mark.parametrize("B", [128, 100])
+def test_nt4_dma_forward_bitwise_equals_register_form(B, monkeypatch):
+    """The NT = 4 forward's h tiles by LDS-DMA (default) vs the register double buffer
+    (DCR_DEBUG=nt_dma=0) over T = 48 steps: the same MFMA and partial-sum order, so loss, state
+    and gradients must be bitwise equal -- a stale or misordered hand-off read in either form
+    would change them (B = 100: a ragged second batch group)."""
+    T, H, L = 48, 2048, 1
+    cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=L)
+    x, y, st0 = _batch(B, T, H, L, 21)
+    res = []
+    for dma in ("1", "0"):
+        monkeypatch.setenv("DCR_DEBUG", f"persist_min_t=1,nt_dma={dma}")
+        m = CharRNN(cfg, device="cuda:0", seed=3)
+        assert m.backend._persist_plan(B, True, T).persist
+        loss, st, _ = m.train_step(x, y, [tuple(s.clone() for s in t) for t in st0])
+        torch.cuda.synchronize()
+        m.backend.check_errors()
+        res.append((loss.item(), m.store.grad.clone(), [s.clone() for a in st for s in a]))
+    (l1, g1, s1), (l0, g0, s0) = res
+    assert l1 == l0
+    assert torch.equal(g1, g0)
+    for a, b in zip(s1, s0):
+        assert torch.equal(a, b)
