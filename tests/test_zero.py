@@ -27,17 +27,18 @@ def free_port():
     return p
 
 
-def _worker(rank, world, port, mode, steps, q):
+def _worker(rank, world, port, mode, steps, q, bucket_mb=8.0):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         m = CharRNN(ModelConfig(**CFG), device="cpu", seed=5)
         opt = TFAdam(m.store, clip=CLIP)
-        sync = GradSync(m.store, world, 8.0, "fp32", enabled=(mode == "replicated"))
+        sync = GradSync(m.store, world, bucket_mb, "fp32", enabled=(mode == "replicated"))
         sync.broadcast_params(0) if mode == "replicated" else dist.broadcast(m.store.flat, 0)
         zs = None if mode == "replicated" else ShardedStep(m.store, opt, world, rank,
-                                                           wire=mode.split("_")[1])
+                                                           wire=mode.split("_")[1],
+                                                           bucket_mb=bucket_mb)
         rng = np.random.default_rng(0)
         data = rng.integers(0, 11, size=(steps, 4 * world, 7)).astype(np.int32)
         st = m.zero_state(4)
@@ -59,11 +60,12 @@ def _worker(rank, world, port, mode, steps, q):
         dist.destroy_process_group()
 
 
-def _run(mode, world=2, steps=4):
+def _run(mode, world=2, steps=4, bucket_mb=8.0):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, mode, steps, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, mode, steps, q, bucket_mb))
+          for r in range(world)]
     for p in ps:
         p.start()
     out = [q.get(timeout=240) for _ in ps]
@@ -84,6 +86,18 @@ def test_sharded_step_equals_replicated():
         np.testing.assert_allclose(sh[r][4], rep[0][4], rtol=1e-5)              # norms
         assert sh[r][5] == rep[0][5] == 4
     np.testing.assert_array_equal(sh[0][1], sh[1][1])  # replicas stay identical
+
+
+def test_many_buckets_equal_one():
+    """Tiny buckets (a dozen per step, every one exchanged by the blocking collectives after
+    the backward, in flat order) give the one-bucket results bitwise, replicated and sharded."""
+    tiny = 1.0 / 1024  # 1 KB cap: one bucket per tensor boundary
+    one_r, many_r = _run("replicated"), _run("replicated", bucket_mb=tiny)
+    np.testing.assert_array_equal(many_r[0][1], one_r[0][1])
+    one_s, many_s = _run("sharded_fp32"), _run("sharded_fp32", bucket_mb=tiny)
+    for r in range(2):
+        np.testing.assert_allclose(many_s[r][1], one_s[r][1], rtol=1e-6, atol=1e-9)
+    np.testing.assert_array_equal(many_s[0][1], many_s[1][1])
 
 
 def test_sharded_step_bf16_wire_close():
