@@ -95,6 +95,7 @@ def main(argv=None) -> int:
                       output_keep_prob=a.output_keep_prob)
     model = CharRNN(cfg, device=device, seed=1234)
     opt = TFAdam(model.store, clip=5.0, guard=model.error_word())
+    model.bind_optimizer(opt)  # fused Adam + weight layouts (csrc/tail.hip)
     # (--force_sync: the exchange also runs on one rank, sharded or replicated)
     sharded = a.dp_mode == "sharded" and (world > 1 or a.force_sync)
     sync = GradSync(model.store, world, a.bucket_mb, a.allreduce_dtype,

@@ -403,6 +403,63 @@ struct PrepTable {
 void launch_prep(PrepTable& tab, hipStream_t s);
 
 
+// TF token-norm term sum_tok ||dZ0_tok · W_x0ᵀ||² without materialising dx (tokennorm.hip)
+constexpr int kTokenNormMaxGrid = 1024;
+struct TokenNormArgs {
+  const bf16* dz; long ld_dz;   // [N, K] bf16, K-contiguous rows
+  const bf16* w; long ld_w;     // [N_units, K] bf16 (W_x0 in TF layout [H, 4H])
+  int N, N_units, K;
+  float* part;                  // [grid] partials
+  unsigned* ticket;             // zeroed, reset by the kernel
+  float* out;                   // [1] the sum of squares
+};
+bool tokennorm_supported(int N, int H, int K);
+void launch_tokennorm(const TokenNormArgs& a, hipStream_t s);
+
+// the training step's tail (tail.hip): gradient finalize + fused Adam with the bf16 layouts
+enum TailOp : int { TAIL_SUM = 0, TAIL_COLSUM = 1, TAIL_SUMSQ = 2, TAIL_MM = 3, TAIL_ADAM = 4 };
+struct TailTask {
+  int op, rows, cols, tile0;   // output (SUM / COLSUM / MM) or region (SUMSQ / ADAM) shape
+  int norm;                    // FINALIZE: square the outputs into the global norm
+  int wait, need;              // wait until dep[wait] >= need (-1: none; producers come first)
+  int sig;                     // dep counter each finished tile adds 1 to (-1: none)
+  int vec4, nslab, k;          // float4 path; SUM slabs; MM reduction length
+  int o1_t, o2_t;              // ADAM layout outputs: 1 = transposed (o[c][r])
+  // SUM: a = slab 0 of [S, rows, cols] (row stride ar, slab stride ak); COLSUM: a = [k, cols]
+  // partials (row stride ar); SUMSQ: a = rows * cols contiguous floats;
+  // MM: dst[r, c] = bias[c] + sum_k a[r ar + k ak] * b[k bk + c bc]
+  const float* a; long ar, ak;
+  const float* b; long bk, bc;
+  const float* bias;
+  float* dst; long dst_ld;
+  long off, ld;                // ADAM: region flat[off + r ld + c] of p / g / m / v / mirror
+  bf16* o1; long o1_ld;
+  bf16* o2; long o2_ld;
+};
+constexpr int kTailMaxTasks = 16;  // the by-value table stays under 3 KB of kernel arguments
+constexpr int kTailMaxDeps = 4;
+constexpr int kTailMaxGrid = 1024;
+struct TailArgs {
+  TailTask t[kTailMaxTasks];
+  int n, ntiles, phase;        // phase 0 FINALIZE, 1 ADAM
+  float* part;                 // [kTailMaxGrid] per-workgroup sums of squares
+  unsigned* sync;              // [4] ticket (0), grid barrier (2); zeroed, reset by the kernel
+  unsigned* dep;               // [kTailMaxDeps] dependency counters (zeroed, reset)
+  unsigned* err;
+  unsigned spin_limit;
+  float* total_out;            // FINALIZE: global sum of squares (+ extra)
+  const float* total_in;       // ADAM: that sum (nullptr: computed here over g[0, n_norm))
+  const float* extra;          // one more norm term (the TF per-token embedding slot)
+  float* p; const float* g; float* m; float* v; bf16* mirror;
+  long n_norm;
+  float lr_t, b1, b2, eps, clip, gscale;
+  const float* lr_dev;
+  const unsigned* skip_if;
+  float* norm_out;
+};
+int tail_grid(int cus);
+int launch_tail(TailArgs& a, int cus, hipStream_t s);
+
 // on-device sampling step (sample.hip): softmax head + categorical draw, one workgroup per stream
 struct SampleArgs {
   const bf16* O;          // [S, H] top-layer output of this step

@@ -233,6 +233,10 @@ __global__ void __launch_bounds__(256, 1) lstm_fwd_persist_nt_kernel(PersistArgs
       put(3, acc);
       put(0, a0);
       put(1, a1);
+      // the partial stores above are inline asm, invisible to the compiler's waitcnt pass, and
+      // the barrier below does not wait for LDS operations by itself: drain them here so that
+      // other waves' pslot() reads after the barrier see every partial
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     } else {
       load_tile(0, hb[0]);
 #pragma unroll
@@ -503,6 +507,8 @@ const void* lstm_persist_nt_fn(int bwd, int H, int B, int cus, int diag) {
     case 4: return bwd ? (const void*)lstm_bwd_persist_nt_kernel<64, 4>
                    : debug_int("nt_dma", 1) ? (const void*)lstm_fwd_persist_nt_kernel<16, 4, false, true>
                                             : (const void*)lstm_fwd_persist_nt_kernel<16, 4>;
+    case -1: return bwd ? (const void*)lstm_bwd_persist_nt_kernel<64, 1, true>
+                        : (const void*)lstm_fwd_persist_nt_kernel<16, 1, true>;
     case -2: return bwd ? (const void*)lstm_bwd_persist_nt_kernel<64, 2, true>
                         : (const void*)lstm_fwd_persist_nt_kernel<16, 2, true>;
     case -4: return bwd ? (const void*)lstm_bwd_persist_nt_kernel<64, 4, true>

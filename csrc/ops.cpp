@@ -1310,6 +1310,139 @@ void wgrad(at::TensorList A, at::TensorList B, at::Tensor& part) {
   dcr::launch_wgrad(a, cur_stream());
 }
 
+// ------------------------------------------------------------------------------------------
+// the step's tail (tail.hip): FINALIZE (phase 0) / ADAM with the bf16 layouts (phase 1).  The
+// tasks arrive as kTailWords int64 words each (engine/native/tail.py builds them from tensors
+// it keeps alive; pointers as data_ptr integers), checked here before the launch.
+// ------------------------------------------------------------------------------------------
+constexpr int kTailWords = 27;
+void tail(at::IntArrayRef words, int64_t phase, at::Tensor& part, at::Tensor& sync, at::Tensor& dep,
+          at::Tensor& err, int64_t spin_limit, const c10::optional<at::Tensor>& total_out,
+          const c10::optional<at::Tensor>& total_in, const c10::optional<at::Tensor>& extra,
+          const c10::optional<at::Tensor>& p, const c10::optional<at::Tensor>& g,
+          const c10::optional<at::Tensor>& m, const c10::optional<at::Tensor>& v,
+          const c10::optional<at::Tensor>& mirror, int64_t n_norm, double lr_t, double b1,
+          double b2, double eps, double clip, double gscale, const c10::optional<at::Tensor>& lr_dev,
+          const c10::optional<at::Tensor>& skip_if, const c10::optional<at::Tensor>& norm_out) {
+  TORCH_CHECK(words.size() % kTailWords == 0, "tail: ", kTailWords, " words per task");
+  const int n = (int)(words.size() / kTailWords);
+  TORCH_CHECK(n >= 1 && n <= dcr::kTailMaxTasks, "tail: 1..", dcr::kTailMaxTasks, " tasks");
+  TORCH_CHECK(phase == 0 || phase == 1, "tail: phase 0 or 1");
+  CHECK_DEV(part); CHECK_F32(part);
+  TORCH_CHECK(part.numel() >= dcr::kTailMaxGrid, "tail: part needs ", dcr::kTailMaxGrid, " floats");
+  CHECK_DEV(sync); CHECK_I32(sync); TORCH_CHECK(sync.numel() >= 4, "tail: sync needs 4 words");
+  CHECK_DEV(dep); CHECK_I32(dep);
+  TORCH_CHECK(dep.numel() >= dcr::kTailMaxDeps, "tail: dep needs ", dcr::kTailMaxDeps, " words");
+  CHECK_DEV(err); CHECK_I32(err);
+  auto opt_ptr = [](const c10::optional<at::Tensor>& t) -> void* {
+    return (t.has_value() && t->defined()) ? t->data_ptr() : nullptr;
+  };
+  dcr::TailArgs a{};
+  a.n = n;
+  a.phase = (int)phase;
+  a.part = ptr<float>(part);
+  a.sync = reinterpret_cast<unsigned*>(sync.data_ptr());
+  a.dep = reinterpret_cast<unsigned*>(dep.data_ptr());
+  a.err = reinterpret_cast<unsigned*>(err.data_ptr());
+  a.spin_limit = (unsigned)spin_limit;
+  a.total_out = static_cast<float*>(opt_ptr(total_out));
+  a.total_in = static_cast<const float*>(opt_ptr(total_in));
+  a.extra = static_cast<const float*>(opt_ptr(extra));
+  if (phase == 1) {
+    TORCH_CHECK(p && g && m && v && p->defined() && g->defined() && m->defined() && v->defined(),
+                "tail ADAM: p, g, m, v");
+    for (const at::Tensor* t : {&*p, &*g, &*m, &*v}) {
+      CHECK_DEV(*t); CHECK_CONTIG(*t); CHECK_F32(*t); CHECK_ALIGN16(*t);
+      TORCH_CHECK(t->numel() == p->numel(), "tail ADAM: p, g, m, v sizes differ");
+    }
+    TORCH_CHECK(n_norm >= 0 && n_norm <= p->numel(), "tail ADAM: n_norm out of range");
+    a.p = ptr<float>(*p); a.g = ptr<float>(*g); a.m = ptr<float>(*m); a.v = ptr<float>(*v);
+    if (mirror && mirror->defined()) {
+      CHECK_BF16(*mirror); CHECK_CONTIG(*mirror); CHECK_ALIGN16(*mirror);
+      TORCH_CHECK(mirror->numel() >= p->numel(), "tail ADAM: mirror too small");
+      a.mirror = ptr<bf16>(*mirror);
+    }
+  }
+  a.n_norm = n_norm;
+  a.lr_t = (float)lr_t; a.b1 = (float)b1; a.b2 = (float)b2; a.eps = (float)eps;
+  a.clip = (float)clip; a.gscale = (float)gscale;
+  a.lr_dev = static_cast<const float*>(opt_ptr(lr_dev));
+  a.skip_if = static_cast<const unsigned*>(opt_ptr(skip_if));
+  a.norm_out = static_cast<float*>(opt_ptr(norm_out));
+  auto a16 = [](int64_t x) { return (x & 15) == 0; };
+  for (int i = 0; i < n; ++i) {
+    const int64_t* w = words.data() + (size_t)i * kTailWords;
+    dcr::TailTask& T = a.t[i];
+    T.op = (int)w[0]; T.rows = (int)w[1]; T.cols = (int)w[2]; T.norm = (int)w[3];
+    T.wait = (int)w[4]; T.need = (int)w[5]; T.sig = (int)w[6]; T.vec4 = (int)w[7];
+    T.nslab = (int)w[8]; T.k = (int)w[9]; T.o1_t = (int)w[10]; T.o2_t = (int)w[11];
+    T.a = reinterpret_cast<const float*>(w[12]); T.ar = w[13]; T.ak = w[14];
+    T.b = reinterpret_cast<const float*>(w[15]); T.bk = w[16]; T.bc = w[17];
+    T.bias = reinterpret_cast<const float*>(w[18]);
+    T.dst = reinterpret_cast<float*>(w[19]); T.dst_ld = w[20];
+    T.off = w[21]; T.ld = w[22];
+    T.o1 = reinterpret_cast<bf16*>(w[23]); T.o1_ld = w[24];
+    T.o2 = reinterpret_cast<bf16*>(w[25]); T.o2_ld = w[26];
+    TORCH_CHECK(T.op >= dcr::TAIL_SUM && T.op <= dcr::TAIL_ADAM, "tail: unknown op ", T.op);
+    TORCH_CHECK((T.op == dcr::TAIL_ADAM) == (phase == 1) || T.op == dcr::TAIL_MM,
+                "tail: ADAM tasks only in phase 1, SUM / COLSUM / SUMSQ only in phase 0");
+    TORCH_CHECK(T.rows > 0 && T.cols > 0, "tail: empty task");
+    TORCH_CHECK(T.wait < dcr::kTailMaxDeps && T.sig < dcr::kTailMaxDeps, "tail: dep index");
+    TORCH_CHECK(T.wait < 0 || T.need > 0, "tail: a waiting task needs a positive count");
+    if (T.op != dcr::TAIL_ADAM) TORCH_CHECK(T.a != nullptr, "tail: task without a source");
+    if (T.op == dcr::TAIL_SUM || T.op == dcr::TAIL_COLSUM || T.op == dcr::TAIL_MM)
+      TORCH_CHECK(T.dst != nullptr, "tail: task without a destination");
+    if (T.op == dcr::TAIL_SUM) {
+      TORCH_CHECK(T.nslab >= 1, "tail SUM: slabs");
+      if (T.vec4)
+        TORCH_CHECK(a16(w[12]) && a16(w[19]) && T.ar % 4 == 0 && T.ak % 4 == 0 && T.dst_ld % 4 == 0 &&
+                    T.cols % 4 == 0, "tail SUM: float4 path needs 16-B aligned rows");
+    }
+    if (T.op == dcr::TAIL_COLSUM) TORCH_CHECK(T.k >= 1, "tail COLSUM: partial rows in k");
+    if (T.op == dcr::TAIL_MM) TORCH_CHECK(T.b != nullptr && T.k >= 1, "tail MM: B and k");
+    if (T.op == dcr::TAIL_ADAM) {
+      TORCH_CHECK(phase == 1, "tail ADAM in phase 1");
+      TORCH_CHECK(T.off >= 0 && T.off + (T.rows - 1) * T.ld + T.cols <= p->numel(),
+                  "tail ADAM: region outside the parameter buffer");
+      if (T.vec4)
+        TORCH_CHECK(T.off % 4 == 0 && T.ld % 4 == 0 && T.cols % 4 == 0 &&
+                    (!T.o1 || T.o1_t || (T.o1_ld % 4 == 0 && (w[23] & 7) == 0)) &&
+                    (!T.o2 || T.o2_t || (T.o2_ld % 4 == 0 && (w[25] & 7) == 0)),
+                    "tail ADAM: float4 path alignment");
+    }
+  }
+  const int rc = dcr::launch_tail(a, num_cus(), cur_stream());
+  TORCH_CHECK(rc == 0, "tail: launch failed (", rc, ")");
+}
+
+int64_t tail_words() { return kTailWords; }
+// TF token-norm term (tokennorm.hip): out[0] = sum_tok ||dz[tok] · wᵀ||²
+void tokennorm(const at::Tensor& dz, const at::Tensor& w, at::Tensor& part, at::Tensor& ticket,
+               at::Tensor& out) {
+  for (const at::Tensor* t : {&dz, &w}) {
+    CHECK_DEV(*t); CHECK_BF16(*t);
+    TORCH_CHECK(t->dim() == 2 && t->stride(1) == 1 && t->stride(0) % 8 == 0 &&
+                    (reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0,
+                "tokennorm: 2-D bf16 views with 16-B aligned rows");
+  }
+  const int N = (int)dz.size(0), K = (int)dz.size(1), H = (int)w.size(0);
+  TORCH_CHECK(w.size(1) == K, "tokennorm: dz [N, K], w [H, K]");
+  TORCH_CHECK(dcr::tokennorm_supported(N, H, K), "tokennorm: unsupported shape N=", N, " H=", H,
+              " K=", K);
+  CHECK_DEV(part); CHECK_F32(part);
+  TORCH_CHECK(part.numel() >= dcr::kTokenNormMaxGrid, "tokennorm: part too small");
+  CHECK_DEV(ticket); CHECK_I32(ticket); CHECK_DEV(out); CHECK_F32(out);
+  dcr::TokenNormArgs a{};
+  a.dz = ptr<bf16>(dz); a.ld_dz = dz.stride(0);
+  a.w = ptr<bf16>(w); a.ld_w = w.stride(0);
+  a.N = N; a.N_units = H; a.K = K;
+  a.part = ptr<float>(part);
+  a.ticket = reinterpret_cast<unsigned*>(ticket.data_ptr());
+  a.out = ptr<float>(out);
+  dcr::launch_tokennorm(a, cur_stream());
+}
+
+
 void prep(at::TensorList src, at::TensorList dst, at::IntArrayRef mode, at::TensorList extra) {
   TORCH_CHECK(src.size() == dst.size() && dst.size() == mode.size(), "prep: list lengths differ");
   TORCH_CHECK((int)dst.size() <= dcr::kPrepMaxTasks, "prep: too many tasks");
@@ -1528,6 +1661,17 @@ TORCH_LIBRARY(dcr, m) {
       "float oscale=1.0) -> ()");
   m.def("prep(Tensor[] src, Tensor(a!)[] dst, int[] mode, Tensor[] extra) -> ()");
   m.def("prep_max_tasks() -> int", []() -> int64_t { return dcr::kPrepMaxTasks; });
+  m.def("tail(int[] words, int phase, Tensor(a!) part, Tensor(b!) sync, Tensor(c!) dep, "
+        "Tensor(d!) err, int spin_limit, Tensor(e!)? total_out, Tensor? total_in, Tensor? extra, "
+        "Tensor(f!)? p, Tensor? g, Tensor(g!)? m, Tensor(h!)? v, Tensor(i!)? mirror, int n_norm, "
+        "float lr_t, float b1, float b2, float eps, float clip, float gscale, Tensor? lr_dev, "
+        "Tensor? skip_if, Tensor(j!)? norm_out) -> ()");
+  m.def("tail_words() -> int", []() -> int64_t { return kTailWords; });
+  m.def("tokennorm(Tensor dz, Tensor w, Tensor(a!) part, Tensor(b!) ticket, Tensor(c!) out) -> ()");
+  m.def("tokennorm_supported(int N, int H, int K) -> int", [](int64_t N, int64_t H, int64_t K) -> int64_t {
+    return dcr::tokennorm_supported((int)N, (int)H, (int)K) ? 1 : 0; });
+  m.def("tail_max_tasks() -> int", []() -> int64_t { return dcr::kTailMaxTasks; });
+  m.def("tail_grid() -> int", []() -> int64_t { return dcr::tail_grid(num_cus()); });
   m.def("wgrad(Tensor[] A, Tensor[] B, Tensor(a!) part) -> ()");
   m.def("wgrad_plan(int np, int M, int N, int K) -> int",
         [](int64_t np, int64_t M, int64_t N, int64_t K) -> int64_t {
@@ -1607,6 +1751,8 @@ TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("lstm_persist_bwd", &lstm_persist_bwd);
   m.impl("head", &head);
   m.impl("prep", &prep);
+  m.impl("tail", &tail);
+  m.impl("tokennorm", &tokennorm);
   m.impl("wgrad", &wgrad);
   m.impl("gru_persist_fwd", &gru_persist_fwd);
   m.impl("lstm2_persist_fwd", &lstm2_persist_fwd);

@@ -94,6 +94,15 @@ class NativeBackend(LayoutsMixin, BuffersMixin, ForwardMixin, BackwardMixin, Lib
         self._sorted_ids = None  # wide vocabulary: (sorted ids, permutation) of this step
         self._dm_bufs: Dict[Tuple[int, int], dict] = {}
         self.last_dropout_masks: Optional[dict] = None
+        # the fused step tail (csrc/tail.hip, engine/native/tail.py): bf16 mirror of the flat
+        # parameters (layouts.py), the fused-Adam task table, and the global sum of squares the
+        # step's FINALIZE launch left for the update (valid until the optimizer consumes it)
+        self._mirror: Optional[torch.Tensor] = None
+        self._adam_tab = None
+        self._adam_ws = None
+        self._tail_total: Optional[torch.Tensor] = None
+        self._tail_total_ok = False
+        self._tn_ws = None  # token-norm kernel partials + ticket
 
     def check_errors(self):
         """Raise if a persistent kernel hit its spin timeout (forces a device sync).  The word

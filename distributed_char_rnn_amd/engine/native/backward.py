@@ -8,6 +8,7 @@ import torch
 from ...models.params import cell_specs
 from .gemm import SumQueue, f32, mm_into, mm_tn, mm_tn_cols, put
 from .layouts import SEG_LDS_MAX_V
+from .tail import TailQueue
 
 
 class BackwardMixin:
@@ -40,8 +41,14 @@ class BackwardMixin:
                 sort_ev.record(side)
             for t_ in self._sorted_ids:
                 t_.record_stream(torch.cuda.current_stream())
-        # deferred slab / bias sums of this step: one prep launch per flush (gemm.SumQueue)
-        q = SumQueue(self.ops, wgrad=self.knobs.debug.get("wgrad") == "1")
+        # deferred slab / bias sums of this step: one prep launch per flush (gemm.SumQueue), or
+        # on the LSTM gather route one tail FINALIZE launch (csrc/tail.hip) that also computes
+        # the layer-0 products and the global norm for the fused Adam
+        dp = on_ready is not None
+        use_wgrad = self.knobs.debug.get("wgrad") == "1"
+        tail = self._tail_backward_ok(bufs0)
+        q = TailQueue(self, wgrad=use_wgrad) if tail else SumQueue(self.ops, wgrad=use_wgrad)
+        self._tail_total_ok = False
         if on_ready is not None:
             cb_user = on_ready
 
@@ -68,6 +75,8 @@ class BackwardMixin:
                           bufs["head_part"], loss_buf, head_omask,
                           dm["sout"] if dm is not None else 1.0)
             mm_tn(O, dlog, s.gview("rnnlm/softmax_w"), q=q)
+            if tail:  # d softmax_b (written by the head kernel): a norm term of the finalize
+                q.add_sumsq(s.gview("rnnlm/softmax_b"))
             dtop = bufs["dtop"].view(T, B, H)
         elif self.wide_head:
             # wide vocabulary, one launch: logits (recomputed, never written unless asked for)
@@ -236,6 +245,22 @@ class BackwardMixin:
                 dXf = mm_into(dZx, lw.Wx.t(), bufs["dx"].view(N, H))
                 self._embed_grad(dXf, ids_tm, bufs)
                 self._token_norm(dXf)
+            elif gather and tail and self._tail_gather_ok(layer, bufs, fused_dew):
+                # tail route: dEW's split-K slabs, dW_x0 = Eᵀ·dEW and dE = dEW·W_x0ᵀ all in the
+                # step's FINALIZE launch (the products wait in-launch for the dEW slab sum)
+                self._bias_sum(self._db_part(bufs, layer), names, q)
+                dew = bufs["dew"]
+                q.signal_on(dew, 0)
+                mm_tn(bufs["onehot"], dZx, dew, q=q)
+                GW_ = dew.shape[1]
+                q.add_mm(s.gview(names[0])[:H], hd["E"], (1, H), dew, (GW_, 1), V, wait=0)
+                q.add_mm(s.gview("embedding"), dew, (GW_, 1), lw.Wx32, (1, GW_), GW_, wait=0)
+                written = True
+                if on_ready is not None:
+                    self._join_side()
+                    on_ready(s.layer_range(0)[1])
+                if tok_gemm:
+                    self._token_norm_gemm(dZx, lw.Wx)
             elif gather:
                 # the bias gradient from the BPTT kernel's partials: summed in the same flush
                 # as dEW's slabs (rather than a column sum of dEW after it)
@@ -260,7 +285,7 @@ class BackwardMixin:
                 if tok_gemm:
                     # sum_tok ||dZ0_tok·W_x0ᵀ||² into the norm slot: library GEMM to bf16 rows
                     # + the sumsq kernel (66 us at the headline shape)
-                    self._token_norm(torch.mm(dZx, lw.Wx.t()))
+                    self._token_norm_gemm(dZx, lw.Wx)
             else:
                 if lb.x_merged:  # written by the merged GEMM above
                     dWx = s.gview(names[0])[:H]
@@ -309,7 +334,14 @@ class BackwardMixin:
                 self._join_side()
             if on_ready is not None:
                 on_ready(None if layer == 0 else s.layer_range(layer)[1])
-        q.flush()
+        if tail:
+            # the last flush also leaves the global sum of squares for the fused Adam when
+            # nothing (no data-parallel exchange) changes the gradients before the update
+            if self._tail_total is None:
+                self._tail_total = torch.zeros(1, dtype=f32, device=self.dev)
+            self._tail_total_ok = q.flush(total_out=None if dp else self._tail_total)
+        else:
+            q.flush()
         self._join_side()
         if pending:
             _release()
@@ -318,6 +350,18 @@ class BackwardMixin:
         if P.persistent and not self.capturing and not self.defer_err_poll:
             self._poll_errors()
         return loss_buf[0], new_state, extras
+
+    def _tail_backward_ok(self, bufs) -> bool:
+        """The step's deferred gradient work runs as tail FINALIZE launches (csrc/tail.hip):
+        LSTM / BasicRNN with the fused head (the tasks the finalize covers)."""
+        return (self.knobs.on("tail") and self.cfg.model in ("lstm", "rnn") and self.fused_head
+                and int(self.ops.tail_grid()) > 0)
+
+    def _tail_gather_ok(self, layer: int, bufs, fused_dew: bool) -> bool:
+        """The layer-0 gather route's products in the finalize: the one-hot dEW GEMM with the
+        bias gradient from the BPTT kernel's partials."""
+        return (layer in bufs["bpart_layers"] and not fused_dew and self.dew_mode == "gemm"
+                and bufs["onehot"] is not None and self.V <= SEG_LDS_MAX_V)
 
     def _id_tasks(self, x: torch.Tensor, y: torch.Tensor, bufs) -> list:
         """Prep tasks (csrc/prep.hip) of the batch: x, y [B, T] int32 -> time-major [T, B]
@@ -396,6 +440,22 @@ class BackwardMixin:
             self._ntick = torch.zeros(1, dtype=torch.int32, device=self.dev)
         self.ops.sumsq(dx_tok.contiguous(), self._npart, self.store.norm_slot_view(),
                        self._ntick)
+
+    def _token_norm_gemm(self, dZ: torch.Tensor, Wx: torch.Tensor) -> None:
+        """TF clip-norm term sum_tok ||dZ_tok·W_xᵀ||² into the norm slot: one hand-written MFMA
+        launch that squares its accumulators in registers (csrc/tokennorm.hip) -- no dx rows in
+        HBM, no second pass; the library GEMM + sumsq form for shapes it does not tile."""
+        if not self.tf_norm:
+            return
+        N, K = dZ.shape
+        if self.knobs.on("tokennorm") and int(self.ops.tokennorm_supported(N, Wx.shape[0], K)):
+            if self._tn_ws is None:
+                self._tn_ws = (torch.empty(1024, dtype=f32, device=self.dev),
+                               torch.zeros(1, dtype=torch.int32, device=self.dev))
+            self.ops.tokennorm(dZ, Wx, self._tn_ws[0], self._tn_ws[1],
+                               self.store.norm_slot_view())
+            return
+        self._token_norm(torch.mm(dZ, Wx.t()))
 
     def _join_side(self) -> None:
         if self._side_used:

@@ -148,7 +148,12 @@ def mm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
         return q.add_gemm(a, b, out)
     S = split_k(K, M, Nn) if split else 1
     if S == 1:
-        return mm(a.t(), b) if out is None else mm_into(a.t(), b, out)
+        if out is None:
+            return mm(a.t(), b)
+        mm_into(a.t(), b, out)
+        if q is not None and hasattr(q, "add_sumsq"):
+            q.add_sumsq(out)  # (tail finalize: written here, still a term of the global norm)
+        return out
     part = torch.bmm(a.unflatten(0, (S, K // S)).transpose(1, 2), b.unflatten(0, (S, K // S)),
                      out_dtype=f32)
     if out is None:

@@ -11,6 +11,7 @@ import torch
 
 from ...models.params import cell_specs
 from .gemm import bf16, f32
+from . import tail as tailmod
 
 SEG_LDS_MAX_V = 96  # csrc/embed.hip kSegLdsMaxV: larger vocabularies take the atomic scatter
 
@@ -31,6 +32,91 @@ class LayoutsMixin:
     def params_changed(self):
         self._wver = None
 
+    # ---- the fused Adam of csrc/tail.hip (TFAdam.fused) -------------------------------------
+    def tail_adam_ok(self) -> bool:
+        """The fused Adam keeps the weight layouts current itself: LSTM / BasicRNN with the
+        layer-0 gather table of a narrow vocabulary (the layouts it writes are W_h / W_x /
+        softmax_w slices of one bf16 mirror plus the transposes and the table)."""
+        return (self.knobs.on("tail") and self.cfg.model in ("lstm", "rnn")
+                and self.V <= SEG_LDS_MAX_V and not getattr(self, "padded_inner", False)
+                and int(self.ops.tail_grid()) > 0)
+
+    def bind_optimizer(self, opt) -> None:
+        if self.tail_adam_ok() and opt.mirror is None and opt.native:
+            opt.fused = self
+
+    def fused_adam(self, opt, lr_t: float, grad_scale: float, lr_dev) -> bool:
+        """One TF-Adam update of every parameter + the bf16 layouts + the gather table in ONE
+        launch (csrc/tail.hip phase 1).  The global norm comes from this step's FINALIZE launch
+        when nothing changed the gradients since (no data-parallel exchange); otherwise the
+        launch computes it itself.  False: not applicable (the caller runs the plain kernel)."""
+        if not self._w or self._mirror is None:
+            return False
+        if self._adam_tab is None:
+            self._adam_tab = self._adam_table()
+            self._adam_ws = tailmod.workspace(self.ops, self.dev)
+        s = self.store
+        n = s.norm_slot
+        n_norm, use_slot = s.norm_terms()
+        total = self._tail_total if (self._tail_total_ok and grad_scale == 1.0) else None
+        self._tail_total_ok = False
+        tailmod.run(self.ops, self._adam_tab, 1, self._adam_ws, self.err, self.spin_limit,
+                    total_in=total, extra=s.norm_slot_view() if use_slot else None,
+                    p=s.flat.narrow(0, 0, n), g=s.grad.narrow(0, 0, n), m=opt.m.narrow(0, 0, n),
+                    v=opt.v.narrow(0, 0, n), mirror=self._mirror, n_norm=n_norm, lr_t=lr_t,
+                    b1=opt.b1, b2=opt.b2, eps=opt.eps, clip=opt.clip, gscale=float(grad_scale),
+                    lr_dev=lr_dev, skip_if=opt.guard, norm_out=opt.last_norm)
+        return True
+
+    def fused_adam_done(self) -> None:
+        """The update ran (the store's version was bumped): the layouts match it."""
+        self._wver = getattr(self.store, "version", 0)
+
+    def _adam_table(self) -> "tailmod.TailTable":
+        s, H, D = self.store, self.H, self.H
+        tab = tailmod.TailTable(int(self.ops.tail_max_tasks()))
+        cover = 0
+
+        def region(name, r0=0, r1=None, outs=(), sig=-1):
+            nonlocal cover
+            sp = s.by_name[name]
+            shape = sp.shape if len(sp.shape) == 2 else (1, sp.numel)
+            rows, cols = shape
+            r1 = rows if r1 is None else r1
+            tab.adam(sp.offset + r0 * cols, r1 - r0, cols, cols, outs=outs, sig=sig)
+            cover += (r1 - r0) * cols
+
+        names = [[sp.name for sp in cell_specs(self.cfg, l)] for l in range(self.L)]
+        w0 = self._w[0]
+        table = self._head.get("table") is not None and self.V <= SEG_LDS_MAX_V
+        # the gather table's operands first (they signal counter 0), then everything else
+        sig = 0 if table else -1
+        region("embedding", sig=sig)
+        region(names[0][0], 0, D, [(w0.WxT, D, True)] if w0.WxT is not None else (), sig=sig)
+        region(names[0][1], sig=sig)
+        for layer in range(self.L):
+            lw = self._w[layer]
+            k, b = names[layer]
+            if layer > 0:
+                region(k, 0, D, [(lw.WxT, D, True)] if lw.WxT is not None else ())
+                region(b)
+            region(k, D, 2 * D, [(lw.WhT, H, True)])
+        outs = []
+        hd = self._head
+        if "WsT" in hd:
+            outs.append((hd["WsT"], H, True))
+            outs.append((hd["Wsk"], hd["Wsk"].shape[1], False))
+        if "WsTw" in hd:
+            outs.append((hd["WsTw"], H, True))
+        region("rnnlm/softmax_w", outs=outs)
+        region("rnnlm/softmax_b")
+        if cover != s.norm_slot:
+            raise AssertionError(f"fused Adam covers {cover} of {s.norm_slot} parameters")
+        if table:
+            GW = w0.Wx32.shape[1]
+            tab.mm(hd["table"], hd["E"], (H, 1), w0.Wx32, (GW, 1), D, bias=w0.bias, wait=0)
+        return tab
+
     def _alloc_weights(self):
         """bf16 (and padded / concatenated fp32) layouts of the master weights, allocated once
         and refreshed by ``_prep`` through the batched prep kernel."""
@@ -38,6 +124,12 @@ class LayoutsMixin:
         self._w, self._wtasks = [], []
         T = self._wtasks
         e = lambda *shape, dt=bf16: torch.empty(*shape, dtype=dt, device=dev)  # noqa: E731
+        # with the fused Adam (csrc/tail.hip) the bf16 operand copies W_x / W_h / softmax_w are
+        # slices of ONE bf16 mirror of the flat parameter buffer, which the update writes in its
+        # own pass (the prep tasks below still fill them after any other parameter change)
+        self._mirror = e(s.numel) if self.tail_adam_ok() else None
+        self._adam_tab = None
+        mv = (lambda name: s.view(name, self._mirror)) if self._mirror is not None else None
         for layer in range(self.L):
             names = [sp.name for sp in cell_specs(self.cfg, layer)]
             if self.cfg.model in ("lstm", "rnn"):
@@ -47,7 +139,8 @@ class LayoutsMixin:
                 # dropout sends its masked embedding rows through the dense route (the two-layer
                 # forward then projects them in-kernel)
                 drop = self.cfg.input_keep_prob < 1.0 or self.cfg.output_keep_prob < 1.0
-                lw = LayerWeights(Wx=e(D, GW), Wx32=k[:D], bias=b, Wh=e(H, GW), WhT=e(GW, H),
+                lw = LayerWeights(Wx=mv(names[0])[:D] if mv else e(D, GW), Wx32=k[:D], bias=b,
+                                  Wh=mv(names[0])[D:] if mv else e(H, GW), WhT=e(GW, H),
                                   WxT=e(GW, D) if (self.cfg.model == "lstm" and (layer > 0 or drop))
                                   else None)
                 T += [(k[D:], lw.Wh, 0), (k[D:], lw.WhT, 1), (k[:D], lw.Wx, 0)]
@@ -70,7 +163,9 @@ class LayoutsMixin:
                 T += [(km, lw.Wh, 0), (km, lw.WhT, 1), (kx, lw.Wx, 0)]
             self._w.append(lw)
         Ws32 = s.view("rnnlm/softmax_w")
-        self._head = dict(E=s.view("embedding"), Ws=e(H, self.V), bs=s.view("rnnlm/softmax_b"))
+        self._head = dict(E=s.view("embedding"),
+                          Ws=mv("rnnlm/softmax_w") if mv else e(H, self.V),
+                          bs=s.view("rnnlm/softmax_b"))
         T.append((Ws32, self._head["Ws"], 0))
         if self.fused_head:
             VP, VK = self.ops.head_pads(self.V)

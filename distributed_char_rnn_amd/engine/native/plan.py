@@ -69,6 +69,10 @@ DEBUG_KEYS = {
     "nt_dma": "0: H > 1024 persistent forward at NT = 4 streams its h tiles through registers "
               "instead of LDS-DMA (C++ launcher)",
     "wgrad": "1: hand-written wgrad kernel for the weight gradients (default: library split-K)",
+    "tokennorm": "0: TF token-norm term as a library GEMM to bf16 rows + a sumsq launch instead "
+                 "of the fused MFMA kernel (csrc/tokennorm.hip)",
+    "tail": "0: no fused step tail (csrc/tail.hip): prep-launch slab flush, library fp32 "
+            "products, separate norm / Adam / weight-layout launches",
     "gru_ub": "1: 16-unit GRU workgroups (C++)",
     "gru_nt": "N: N batch tiles of 16 rows per GRU workgroup (C++)",
     "step_nbt": "1/2/4: batch tiles per per-step workgroup (C++)",

@@ -1,0 +1,261 @@
+"""Task tables of the step's tail kernel (csrc/tail.hip): FINALIZE (slab sums, bias column sums,
+the layer-0 gather route's fp32 products, the global norm) and the fused ADAM update that writes
+every bf16 kernel layout (model.py:88-98: clip_by_global_norm + AdamOptimizer.apply_gradients).
+
+A table is a list of tasks, each ``TAIL_WORDS`` int64 words (csrc/ops.cpp ``tail``): pointers
+travel as ``data_ptr()`` integers, so the table keeps references to every tensor it names.
+Producers must precede the tasks that wait on them (csrc/tail.hip: dependency counters)."""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+
+SUM, COLSUM, SUMSQ, MM, ADAM = 0, 1, 2, 3, 4
+TAIL_WORDS = 27
+MM_SHORT_K = 128  # csrc/tail.hip: MM with k <= 128 runs 64 x 64 VALU tiles, longer k fp32 MFMA
+
+
+def _a16(t: torch.Tensor) -> bool:
+    return t.data_ptr() % 16 == 0
+
+
+def task_tiles(op: int, rows: int, cols: int, k: int) -> int:
+    """Tiles of one task (csrc/tail.hip tail_tiles)."""
+    if op in (SUM, ADAM):
+        return -(-rows // 64) * -(-cols // 64)
+    if op == COLSUM:
+        return -(-cols // 64)
+    if op == SUMSQ:
+        return -(-(rows * cols) // 4096)
+    if op == MM:
+        return (-(-rows // 64) * -(-cols // 64)) if k <= MM_SHORT_K else (-(-rows // 16) * -(-cols // 16))
+    raise ValueError(op)
+
+
+class TailTable:
+    def __init__(self, max_tasks: int = 16):
+        self.words: List[int] = []
+        self.keep: List[torch.Tensor] = []
+        self.ops: List[int] = []
+        self.tiles: List[int] = []
+        self.max_tasks = max_tasks
+        self.sig_tiles = {}  # dependency counter -> producer tiles
+
+    def __len__(self) -> int:
+        return len(self.ops)
+
+    def _add(self, op, rows, cols, *, norm=0, wait=-1, sig=-1, vec4=0, nslab=0, k=0, o1_t=0,
+             o2_t=0, a=0, ar=0, ak=0, b=0, bk=0, bc=0, bias=0, dst=0, dst_ld=0, off=0, ld=0, o1=0,
+             o1_ld=0, o2=0, o2_ld=0, keep=()):
+        if len(self.ops) >= self.max_tasks:
+            raise ValueError(f"tail table: more than {self.max_tasks} tasks")
+        need = 0
+        if wait >= 0:
+            need = self.sig_tiles.get(wait, 0)
+            if need <= 0:
+                raise ValueError(f"tail table: nothing signals counter {wait} before this task")
+        nt = task_tiles(op, rows, cols, k)
+        if sig >= 0:
+            self.sig_tiles[sig] = self.sig_tiles.get(sig, 0) + nt
+        self.words += [op, rows, cols, int(norm), wait, need, sig, int(vec4), nslab, k, o1_t, o2_t,
+                       a, ar, ak, b, bk, bc, bias, dst, dst_ld, off, ld, o1, o1_ld, o2, o2_ld]
+        self.keep += list(keep)
+        self.ops.append(op)
+        self.tiles.append(nt)
+
+    # ---- FINALIZE ----------------------------------------------------------------------------
+    def sum(self, part: torch.Tensor, out: torch.Tensor, norm: bool, sig: int = -1):
+        """out [rows, cols] = sum over the slabs of part [S, rows, cols] (fp32)."""
+        assert part.dim() == 3 and out.dim() == 2 and part.stride(2) == 1 and out.stride(1) == 1
+        assert tuple(part.shape[1:]) == tuple(out.shape) and part.dtype == out.dtype == torch.float32
+        S, rows, cols = part.shape
+        vec4 = (cols % 4 == 0 and part.stride(1) % 4 == 0 and part.stride(0) % 4 == 0
+                and out.stride(0) % 4 == 0 and _a16(part) and _a16(out))
+        self._add(SUM, rows, cols, norm=norm, sig=sig, vec4=vec4, nslab=S, a=part.data_ptr(),
+                  ar=part.stride(1), ak=part.stride(0), dst=out.data_ptr(), dst_ld=out.stride(0),
+                  keep=(part, out))
+
+    def colsum(self, part: torch.Tensor, out: torch.Tensor, norm: bool):
+        """out [cols] = column sums of part [R, cols] (fp32, fixed order)."""
+        assert part.dim() == 2 and part.stride(1) == 1 and out.is_contiguous()
+        assert out.numel() == part.shape[1]
+        self._add(COLSUM, 1, part.shape[1], norm=norm, k=part.shape[0], a=part.data_ptr(),
+                  ar=part.stride(0), dst=out.data_ptr(), dst_ld=part.shape[1], keep=(part, out))
+
+    def sumsq(self, x: torch.Tensor):
+        """A norm term finished elsewhere (contiguous fp32)."""
+        assert x.is_contiguous() and x.dtype == torch.float32
+        self._add(SUMSQ, 1, x.numel(), norm=1, a=x.data_ptr(), keep=(x,))
+
+    def mm(self, out: torch.Tensor, a: torch.Tensor, a_strides, b: torch.Tensor, b_strides,
+           k: int, bias: Optional[torch.Tensor] = None, norm: bool = False, wait: int = -1,
+           sig: int = -1):
+        """out[r, c] = bias[c] + sum_k a[r ar + k ak] * b[k bk + c bc] (fp32)."""
+        assert out.dim() == 2 and out.stride(1) == 1 and out.dtype == torch.float32
+        ar, ak = a_strides
+        bk, bc = b_strides
+        rows, cols = out.shape
+        # every element the strides address lies inside the operands
+        assert (rows - 1) * ar + (k - 1) * ak < a.numel() and (k - 1) * bk + (cols - 1) * bc < b.numel()
+        self._add(MM, rows, cols, norm=norm, wait=wait, sig=sig, k=k, a=a.data_ptr(), ar=ar, ak=ak,
+                  b=b.data_ptr(), bk=bk, bc=bc, bias=0 if bias is None else bias.data_ptr(),
+                  dst=out.data_ptr(), dst_ld=out.stride(0),
+                  keep=(out, a, b) + (() if bias is None else (bias,)))
+
+    # ---- ADAM --------------------------------------------------------------------------------
+    def adam(self, off: int, rows: int, cols: int, ld: int, outs=(), sig: int = -1,
+             keep=()):
+        """One parameter region flat[off + r ld + c]; ``outs``: up to two (bf16 tensor, row
+        stride, transposed) layout outputs of it (besides the flat bf16 mirror)."""
+        assert len(outs) <= 2
+        w = dict(o1=0, o1_ld=0, o1_t=0, o2=0, o2_ld=0, o2_t=0)
+        vec4 = off % 4 == 0 and ld % 4 == 0 and cols % 4 == 0
+        for i, (t, tld, tr) in enumerate(outs):
+            assert t.dtype == torch.bfloat16
+            n = "o1" if i == 0 else "o2"
+            w[n], w[n + "_ld"], w[n + "_t"] = t.data_ptr(), tld, int(tr)
+            if not tr:
+                vec4 = vec4 and tld % 4 == 0 and t.data_ptr() % 8 == 0
+        self._add(ADAM, rows, cols, sig=sig, vec4=vec4, off=off, ld=ld,
+                  keep=tuple(t for t, _, _ in outs) + tuple(keep), **w)
+
+
+def run(ops, table: TailTable, phase: int, ws: dict, err: torch.Tensor, spin_limit: int, *,
+        total_out=None, total_in=None, extra=None, p=None, g=None, m=None, v=None, mirror=None,
+        n_norm: int = 0, lr_t: float = 0.0, b1: float = 0.9, b2: float = 0.999,
+        eps: float = 1e-8, clip: float = 0.0, gscale: float = 1.0, lr_dev=None, skip_if=None,
+        norm_out=None):
+    ops.tail(table.words, phase, ws["part"], ws["sync"], ws["dep"], err, spin_limit, total_out,
+             total_in, extra, p, g, m, v, mirror, n_norm, lr_t, b1, b2, eps, clip, gscale, lr_dev,
+             skip_if, norm_out)
+
+
+def workspace(ops, device) -> dict:
+    """Per-workgroup partials and the (zeroed, self-resetting) ticket / dependency counters."""
+    return dict(part=torch.zeros(1024, dtype=torch.float32, device=device),
+                sync=torch.zeros(4, dtype=torch.int32, device=device),
+                dep=torch.zeros(4, dtype=torch.int32, device=device))
+
+
+class TailQueue:
+    """The backward's deferred gradient work as ONE tail FINALIZE launch per flush (the role of
+    gemm.SumQueue's prep flush): split-K slab sums, bias column sums, the layer-0 gather route's
+    fp32 products dW_x0 = Eᵀ·dEW and dE = dEW·W_x0ᵀ (waiting in-launch for the dEW slab sum),
+    norm terms finished elsewhere, and -- on the step's last flush when nothing will change the
+    gradients before the update -- the global sum of squares for the fused Adam."""
+
+    SUM, COLSUM = 3, 4  # gemm.SumQueue task kinds (mm_tn / _bias_sum call add_sum / add_colsum)
+
+    def __init__(self, backend, wgrad: bool = False):
+        from .gemm import SumQueue
+
+        self.be = backend
+        self.ops = backend.ops
+        self._gemmq = SumQueue(backend.ops, wgrad=wgrad)  # its wgrad grouping, not its flush
+        self.wgrad = wgrad
+        self.sums = []      # (part, out, sig)
+        self.colsums = []   # (part, out)
+        self.sumsqs = []    # contiguous fp32 gradient views
+        self.mms = []       # (out, a, a_strides, b, b_strides, k, wait)
+        self._signals = {}  # out data_ptr -> dependency counter its slab sum signals
+
+    # -- the SumQueue interface used by gemm.mm_tn / backward._bias_sum ----------------------
+    def wgrad_ok(self, a, b, out) -> bool:
+        return self._gemmq.wgrad_ok(a, b, out)
+
+    def add_gemm(self, a, b, out):
+        return self._gemmq.add_gemm(a, b, out)
+
+    def add_sum(self, part, out, sig: int = -1):
+        if sig < 0:
+            sig = self._signals.get(out.data_ptr(), -1)
+        self.sums.append((part, out, sig))
+        return out
+
+    def signal_on(self, out: torch.Tensor, counter: int) -> None:
+        """The slab sum into ``out`` (queued later by mm_tn) signals dependency ``counter``."""
+        self._signals[out.data_ptr()] = counter
+
+    def add_colsum(self, part, out):
+        self.colsums.append((part, out))
+        return out
+
+    # -- tail-only tasks -----------------------------------------------------------------------
+    def add_sumsq(self, g):
+        self.sumsqs.append(g)
+
+    def add_mm(self, out, a, a_strides, b, b_strides, k, wait: int = -1):
+        self.mms.append((out, a, a_strides, b, b_strides, k, wait))
+        return out
+
+    def _norm_range(self, out: torch.Tensor):
+        """(flat offset, elements) of a gradient view inside the norm prefix, else None."""
+        s = self.be.store
+        base = s.grad.data_ptr()
+        off = (out.data_ptr() - base) // 4
+        if out.dtype != torch.float32 or not (0 <= off < s.grad.numel()):
+            return None
+        if not out.is_contiguous():
+            raise AssertionError("tail: gradient outputs must be contiguous views")
+        n_norm, _ = s.norm_terms()
+        if off >= n_norm:
+            return None
+        if off + out.numel() > n_norm:
+            raise AssertionError("tail: an output straddles the norm prefix")
+        return off, out.numel()
+
+    def flush(self, total_out: Optional[torch.Tensor] = None) -> bool:
+        """One FINALIZE launch over everything queued.  ``total_out``: also the global sum of
+        squares (+ the norm slot) -- returned True only if the queued norm terms tile the whole
+        norm prefix (otherwise the fused Adam computes the norm itself)."""
+        g = self._gemmq
+        if g.gemms:
+            g._run_gemms()  # hand-written wgrad launches; their slab sums land in g.tasks
+        for part, out, kind in g.tasks:
+            (self.add_sum if kind == self.SUM else self.add_colsum)(part, out)
+        g.tasks.clear()
+        if not (self.sums or self.colsums or self.sumsqs or self.mms) and total_out is None:
+            return False
+        be = self.be
+        tab = TailTable(int(self.ops.tail_max_tasks()))
+        spans = []
+
+        def norm_of(out):
+            r = self._norm_range(out)
+            if r is not None:
+                spans.append(r)
+            return r is not None
+        # producers first: the slab sums that signal a dependency counter
+        for part, out, sig in sorted(self.sums, key=lambda t: t[2] < 0):
+            if part.dim() == 2:
+                part = part.unsqueeze(0)
+            tab.sum(part, out, norm_of(out), sig)
+        for part, out in self.colsums:
+            tab.colsum(part, out.view(-1), norm_of(out))
+        for x in self.sumsqs:
+            if norm_of(x):  # (outside the norm prefix: nothing to do)
+                tab.sumsq(x)
+        for out, a, sa, b, sb, k, wait in self.mms:
+            tab.mm(out, a, sa, b, sb, k, norm=norm_of(out), wait=wait)
+        self.sums, self.colsums, self.sumsqs, self.mms = [], [], [], []
+        if not len(tab):
+            return False
+        ok = False
+        if total_out is not None:
+            n_norm, _ = be.store.norm_terms()
+            spans.sort()
+            pos = 0
+            ok = True
+            for off, n in spans:
+                ok &= off == pos
+                pos = off + n
+            ok &= pos == n_norm
+        if getattr(be, "_fin_ws", None) is None:
+            be._fin_ws = workspace(self.ops, be.dev)
+        s = be.store
+        _, use_slot = s.norm_terms()
+        run(self.ops, tab, 0, be._fin_ws, be.err, be.spin_limit,
+            total_out=total_out if ok else None,
+            extra=s.norm_slot_view() if (ok and use_slot) else None)
+        return ok

@@ -51,6 +51,10 @@ class TFAdam:
         self.native = store.device.type == "cuda"
         self.last_norm = torch.zeros(1, device=store.device)
         self.mirror: Optional[torch.Tensor] = None
+        # a backend that runs the update as its fused step-tail launch (csrc/tail.hip: Adam +
+        # the bf16 weight layouts + the gather table in one pass), bound by
+        # CharRNN.bind_optimizer; None: the two-launch kernel below
+        self.fused = None
         if bf16_mirror:
             self.mirror = store.flat.to(torch.bfloat16)
         if self.native:
@@ -74,6 +78,11 @@ class TFAdam:
         a hipGraph; the caller writes ``lr_t(lr)`` into it before every replay)."""
         lr_t = self.lr_t(lr)
         st = self.store
+        if self.fused is not None and self.fused.fused_adam(self, lr_t, grad_scale, lr_dev):
+            self.t += 1
+            st.version += 1
+            self.fused.fused_adam_done()
+            return self.last_norm
         n = st.norm_slot  # every parameter; the norm slot and the padding after it are not
         p, g, m, v = (b.narrow(0, 0, n) for b in (st.flat, st.grad, self.m, self.v))
         n_norm, use_slot = st.norm_terms()

@@ -206,6 +206,7 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
     model = build_model(args, loader.vocab_size, device, rank)
     # a persistent-kernel timeout makes the optimizer skip its update on device
     opt = TFAdam(model.store, clip=args.grad_clip, guard=model.error_word())
+    model.bind_optimizer(opt)  # fused Adam + weight layouts (csrc/tail.hip)
     global_step = 0
     start_epoch, start_batch = 0, 0
     sd = None

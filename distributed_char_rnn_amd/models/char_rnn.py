@@ -115,6 +115,13 @@ class CharRNN:
         if hasattr(be, "_drop_step"):
             be._drop_step = int(v)
 
+    def bind_optimizer(self, opt) -> None:
+        """Let the backend run ``opt``'s update as its fused step-tail launch when it can
+        (native LSTM / BasicRNN: Adam + the bf16 weight layouts in one pass, csrc/tail.hip)."""
+        hook = getattr(self.backend, "bind_optimizer", None)
+        if hook is not None:
+            hook(opt)
+
     def params_changed(self):
         """Call after parameters were modified outside the optimizer (restore/broadcast)."""
         self.store.version += 1

@@ -113,9 +113,10 @@ class GradSync:
 
     def ready(self, upto: Optional[int] = None, sync: bool = False):
         """Launch every not-yet-launched bucket that ends at or below flat offset ``upto``
-        (``None`` = everything).  ``sync``: as blocking collectives, which RCCL runs on the
-        caller's stream (no cross-stream event hop; for buckets whose exchange nothing is left
-        to overlap, after every earlier asynchronous one has been waited for)."""
+        (``None`` = everything).  ``sync``: as blocking collectives (c10d still runs them on
+        ProcessGroupNCCL's internal stream; ``async_op=False`` makes the current stream wait on
+        the collective's completion, with no Work object kept here), for buckets whose exchange
+        nothing is left to overlap, after every earlier asynchronous one has been waited for."""
         if not self.enabled:
             return
         lim = self.store.numel if upto is None else upto
@@ -152,8 +153,9 @@ class GradSync:
         if self.timing:
             self._ev_end = torch.cuda.Event(enable_timing=True)
             self._ev_end.record()
-        # the buckets the backward launched first, then the rest on this stream (nothing is
-        # left to overlap them with, and a blocking collective costs no stream-event hop)
+        # the buckets the backward launched first, then the rest as blocking collectives (the
+        # current stream waits on them; nothing is left to overlap them with -- the measured
+        # gain of this form comes from launch and wait ordering, not from where RCCL runs)
         for w, lo, hi, recv in self._work:
             w.wait()
         self.ready(None, sync=True)

@@ -139,6 +139,9 @@ class ShardedStep:
             self.pown[p:p + (b - a)].copy_(self.store.flat[a:b])
             self.mown[p:p + (b - a)].copy_(self.opt.m[a:b])
             self.vown[p:p + (b - a)].copy_(self.opt.v[a:b])
+        # the packed copies are authoritative from here on: a later change of the full buffers
+        # (restore, broadcast: both bump store.version) is picked up by step()'s version check
+        self._ver = self.store.version
 
     # -- the GradSync-compatible interface the backward drives ------------------------------
     def reset(self) -> None:
@@ -201,8 +204,12 @@ class ShardedStep:
         launched by the backward are not relaunched): finish the exchange, update the owned
         chunks, gather the parameters.  Returns the pre-clip global norm (device tensor)."""
         self.early = len(self.launched)  # buckets the backward launched (reports)
-        # the backward's buckets first, then the rest as blocking collectives on this stream
-        # (nothing left to overlap; no stream-event hop)
+        if self.store.version != self._ver:
+            # the full parameter buffer changed since the owned chunks were packed (a restore or
+            # broadcast after construction): re-pack, or the all-gather below would overwrite it
+            self.refresh()
+        # the backward's buckets first, then the rest as blocking collectives (RCCL's internal
+        # stream; the current stream waits on them -- nothing is left to overlap)
         for w, i, recv in self._work:
             w.wait()
         self.ready(None, sync=True)
@@ -219,7 +226,7 @@ class ShardedStep:
                                     self.vown[:q], self.sumsq, grad_scale=1.0 / self.world)
         flat = self.store.flat
         # one all-gather per bucket straight from the packed parameters (RCCL: one coalesced
-        # group), blocking, i.e. on this stream: the next forward reads the parameters anyway
+        # group), blocking (the current stream waits on it): the next forward reads the parameters
         if self._coalesce:
             with dist._coalescing_manager(self.group, async_ops=False):
                 for (lo, hi), (a, b), p in zip(self.buckets, self.own, self.pos):
@@ -229,6 +236,7 @@ class ShardedStep:
             for (lo, hi), (a, b), p in zip(self.buckets, self.own, self.pos):
                 dist.all_gather_into_tensor(flat[lo:hi], self.pown[p:p + (b - a)],
                                             group=self.group)
+        self._ver = self.store.version  # (the update above bumped it; flat now matches pown)
         return norm
 
     @torch.no_grad()

@@ -1,0 +1,191 @@
+"""The step's tail kernel (csrc/tail.hip): FINALIZE tasks against fp64 PyTorch, and the fused
+Adam (update + bf16 layouts + gather table in one launch) against the plain two-launch
+optimizer plus a from-scratch layout refresh."""
+import pytest
+import torch
+
+from distributed_char_rnn_amd.engine.native import tail as tailmod
+
+pytestmark = pytest.mark.gpu
+
+
+def test_finalize_tasks_and_norm(dcr_ops):
+    """Slab sums (float4 + scalar paths), a column sum, a norm-only term and both MM forms, the
+    MMs waiting in-launch on a slab sum that signals a counter; the global sum of squares of
+    the flagged outputs (+ the extra term) against fp64."""
+    torch.manual_seed(3)
+    dev = "cuda"
+    part = torch.randn(5, 300, 2048, device=dev)
+    out = torch.empty(300, 2048, device=dev)
+    part_s = torch.randn(16, 70, 65, device=dev)
+    out_s = torch.empty(70, 65, device=dev)
+    dbp = torch.randn(16, 2048, device=dev)
+    db = torch.empty(2048, device=dev)
+    x = torch.randn(1000, device=dev)
+    part_d = torch.randn(8, 72, 2048, device=dev)
+    dew = torch.empty(72, 2048, device=dev)
+    E = torch.randn(65, 512, device=dev)
+    Wx = torch.randn(512, 2048, device=dev)
+    o1 = torch.empty(512, 2048, device=dev)
+    o2 = torch.empty(65, 512, device=dev)
+    extra = torch.tensor([123.5], device=dev)
+    total = torch.zeros(1, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    tab = tailmod.TailTable(int(dcr_ops.tail_max_tasks()))
+    tab.sum(part_d, dew, norm=False, sig=0)          # the producer first
+    tab.sum(part, out, norm=True)
+    tab.sum(part_s, out_s, norm=True)
+    tab.colsum(dbp, db, norm=True)
+    tab.sumsq(x)
+    tab.mm(o1, E, (1, 512), dew, (2048, 1), 65, norm=True, wait=0)     # Eᵀ·dEW (short k)
+    tab.mm(o2, dew, (2048, 1), Wx, (1, 2048), 2048, norm=True, wait=0)  # dEW·Wxᵀ (long k)
+    ws = tailmod.workspace(dcr_ops, dev)
+    for _ in range(2):  # the counters reset themselves: a second launch gives the same result
+        tailmod.run(dcr_ops, tab, 0, ws, err, 1 << 22, total_out=total, extra=extra)
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    assert torch.count_nonzero(ws["sync"]) == 0 and torch.count_nonzero(ws["dep"]) == 0
+
+    def close(a, b, tol=1e-6):
+        err_ = (a.double() - b).norm() / b.norm()
+        assert err_ < tol, float(err_)
+    close(dew, part_d.double().sum(0))
+    close(out, part.double().sum(0))
+    close(out_s, part_s.double().sum(0))
+    close(db, dbp.double().sum(0))
+    ref_dew = part_d.double().sum(0)[:65]
+    close(o1, E.double().t() @ ref_dew, 1e-5)
+    close(o2, ref_dew @ Wx.double().t(), 1e-5)
+    ref_total = sum(float((t.double() ** 2).sum()) for t in (out, out_s, db, x, o1, o2)) + 123.5
+    assert abs(float(total) - ref_total) / ref_total < 1e-5
+
+
+def _models(fused: bool, H=128, L=2, V=65, seed=0):
+    from distributed_char_rnn_amd.engine.optim import TFAdam
+    from distributed_char_rnn_amd.models.char_rnn import CharRNN
+    from distributed_char_rnn_amd.models.params import ModelConfig
+
+    cfg = ModelConfig(model="lstm", vocab_size=V, rnn_size=H, num_layers=L)
+    model = CharRNN(cfg, device="cuda:0", seed=seed)
+    opt = TFAdam(model.store, clip=5.0, guard=model.error_word())
+    if fused:
+        model.bind_optimizer(opt)
+        assert opt.fused is not None
+    return model, opt
+
+
+class _Sync:
+    """A data-parallel stand-in that changes nothing: its callbacks make the backward treat the
+    gradients as exchanged (no finalize norm), so the fused Adam computes the norm itself."""
+    enabled = True
+
+    def ready(self, upto=None):
+        pass
+
+
+@pytest.mark.parametrize("dp", [False, True])
+@pytest.mark.parametrize("B,T", [(32, 16), (256, 24)])
+def test_fused_adam_matches_plain(B, T, dp):
+    """Three training steps with the fused tail vs the plain optimizer: parameters, slots and
+    the reported norm agree, and every bf16 layout the fused update wrote equals a fresh
+    refresh of the layouts from the fp32 masters (bitwise)."""
+    torch.manual_seed(5)
+    x = torch.randint(0, 65, (B, 3 * T), dtype=torch.int32, device="cuda")
+    y = torch.randint(0, 65, (B, 3 * T), dtype=torch.int32, device="cuda")
+    runs = []
+    for fused in (False, True):
+        model, opt = _models(fused)
+        st = model.zero_state(B)
+        for k in range(3):
+            _, st, _ = model.train_step(x[:, k * T:(k + 1) * T], y[:, k * T:(k + 1) * T], st,
+                                        _Sync() if dp else None)
+            opt.step(2e-3)
+        torch.cuda.synchronize()
+        runs.append((model, opt))
+    (m0, o0), (m1, o1) = runs
+    assert int(m1.backend.err.item()) == 0
+
+    def rel(a, b):
+        return float((a.double() - b.double()).norm() / b.double().norm())
+    assert rel(m1.store.flat, m0.store.flat) < 1e-5
+    assert rel(o1.m, o0.m) < 1e-4
+    assert rel(o1.v, o0.v) < 1e-4
+    assert abs(float(o1.last_norm) - float(o0.last_norm)) <= 1e-4 * float(o0.last_norm)
+    # layouts: what the fused update wrote vs a refresh from the same fp32 masters
+    be = m1.backend
+    w = be._w
+    snap = [(lw.WhT.clone(), lw.Wh.clone(), lw.Wx.clone(),
+             None if lw.WxT is None else lw.WxT.clone()) for lw in w]
+    hd = be._head
+    hsnap = {k: hd[k].clone() for k in ("Ws", "WsT", "Wsk", "table") if k in hd}
+    be.params_changed()
+    be._run_prep(be._prep())
+    torch.cuda.synchronize()
+    for lw, (wht, wh, wx, wxt) in zip(w, snap):
+        assert torch.equal(lw.WhT, wht)
+        assert torch.equal(lw.Wh, wh)
+        assert torch.equal(lw.Wx, wx)
+        if wxt is not None:
+            assert torch.equal(lw.WxT, wxt)
+    for k, v in hsnap.items():
+        if k == "table":
+            assert rel(hd[k], v) < 1e-6
+        else:
+            assert torch.equal(hd[k], v), k
+
+
+def test_fused_adam_skips_on_error_word():
+    """A set error word (a persistent kernel timed out) skips the fused update on device."""
+    model, opt = _models(True)
+    B, T = 32, 16
+    x = torch.randint(0, 65, (B, T), dtype=torch.int32, device="cuda")
+    st = model.zero_state(B)
+    model.train_step(x, x, st)
+    before = model.store.flat.clone()
+    model.backend.err.fill_(1)
+    opt.step(2e-3)
+    torch.cuda.synchronize()
+    assert torch.equal(model.store.flat, before)
+    model.backend.err.zero_()
+
+
+@pytest.mark.parametrize("B,T", [(32, 16), (256, 24)])
+def test_tail_backward_matches_prep_flush(monkeypatch, B, T):
+    """The gradients of the tail FINALIZE route equal the prep-flush + library route's (the
+    slab sums in the same fixed order; dW_x0 / dE as fp32 products either way)."""
+    torch.manual_seed(7)
+    x = torch.randint(0, 65, (B, T), dtype=torch.int32, device="cuda")
+    y = torch.randint(0, 65, (B, T), dtype=torch.int32, device="cuda")
+    grads = []
+    for knob in ("tail=0", ""):
+        monkeypatch.setenv("DCR_DEBUG", knob)
+        model, _ = _models(False)
+        model.train_step(x, y, model.zero_state(B))
+        torch.cuda.synchronize()
+        grads.append(model.store.grad.clone())
+        if knob == "":
+            assert model.backend._tail_total_ok  # the finalize covered the whole norm prefix
+            n_norm, _ = model.store.norm_terms()
+            g = model.store.grad
+            ref = float((g[:n_norm].double() ** 2).sum() + g[model.store.norm_slot].double() ** 2)
+            assert abs(float(model.backend._tail_total) - ref) <= 1e-5 * ref
+    a, b = grads
+    assert float((a - b).norm() / b.norm()) < 1e-6
+
+
+@pytest.mark.parametrize("N,H", [(2048, 256), (32768, 512)])
+def test_tokennorm_kernel(dcr_ops, N, H):
+    """sum_tok ||dZ_tok·Wᵀ||² without dx rows vs fp64 (bf16 operands, fp32 accumulation)."""
+    torch.manual_seed(11)
+    K = 4 * H
+    dz = (torch.randn(N, K, device="cuda") * 0.1).to(torch.bfloat16)
+    w = (torch.randn(H, K, device="cuda") * 0.05).to(torch.bfloat16)
+    part = torch.empty(1024, device="cuda")
+    ticket = torch.zeros(1, dtype=torch.int32, device="cuda")
+    out = torch.zeros(1, device="cuda")
+    for _ in range(2):
+        dcr_ops.tokennorm(dz, w, part, ticket, out)
+    torch.cuda.synchronize()
+    ref = float(((dz.double() @ w.double().t()) ** 2).sum())
+    assert abs(float(out) - ref) / ref < 1e-4
+    assert int(ticket.item()) == 0
