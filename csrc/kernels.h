@@ -336,14 +336,17 @@ struct WgradProblem {
   const bf16* B; long ldb;   // [K, N]
   float* C; long ldc;        // slab 0 of [S, M, N] fp32 partials (row stride ldc)
   long slab;                 // elements between slabs
+  int M, N, S;               // this problem's shape and split count
+  int tiles, item0;          // set by the launcher
 };
 struct WgradArgs {
   WgradProblem p[kWgradMaxProblems];
-  int np, S, M, N, K, tiles;  // tiles = (M / 256) * (N / 256) per (problem, slab)
+  int np, K, items;          // items: set by the launcher
 };
 bool wgrad_supported(int M, int N, int K);
 int wgrad_splits(int np, int M, int N, int K, int cus);
-void launch_wgrad(const WgradArgs& a, hipStream_t s);
+int wgrad_splits_tiles(int tiles, int K, int cus);
+void launch_wgrad(WgradArgs& a, hipStream_t s);
 int gru_persist_ub(int H, int B, int cus);
 int gru_persist_rows(int H, int B, int cus);  // padded batch rows of the launch plan (rings)
 int launch_gru_persist(int bwd, const GruPersistArgs& a, int cus, hipStream_t s);
@@ -416,6 +419,34 @@ struct TokenNormArgs {
 bool tokennorm_supported(int N, int H, int K);
 void launch_tokennorm(const TokenNormArgs& a, hipStream_t s);
 
+// single-launch autoregressive generation (generate.hip): LSTM layers + head + draw per char
+constexpr int kGenMaxLayers = 4;
+constexpr int kGenMaxStreams = 16;
+struct GenArgs {
+  int L, H, V, S;
+  const bf16* Wh[kGenMaxLayers];     // [H, 4H] bf16 TF layout (recurrent rows)
+  const bf16* Wx[kGenMaxLayers];     // [H, 4H] bf16 (input rows; layer 0 unused: the table)
+  const float* bias[kGenMaxLayers];  // [4H] fp32 (layer 0 unused: inside the table)
+  const float* table;                // [V, 4H] fp32 E·W_x0 + b0
+  const bf16* WsT;                   // [V, H] bf16 softmax_wᵀ
+  const float* bs;                   // [V]
+  float forget_bias;
+  const float* h0; const float* c0;  // [L, S, H] initial state
+  float* h_out; float* c_out;        // [L, S, H] final state
+  const int* prime; int P;           // prime ids (P >= 1); prime[:-1] warms the state
+  int num;                           // characters drawn
+  int* out;                          // [S, num]
+  unsigned long long* hx;            // [L, 2, S, H] tagged hand-off granules (zeroed per launch)
+  int mode, space_id;
+  unsigned long long seed;
+  const unsigned* ctr0;              // [S] first RNG counter of each stream
+  float* logits_out;                 // optional [num, S, V]
+  unsigned* err; unsigned spin_limit;
+  int ws_lds;                        // set by the launcher: softmax_wᵀ resident in LDS
+};
+int generate_supported(int L, int H, int V, int S, int cus);
+int launch_generate(GenArgs& a, int cus, hipStream_t s);
+
 // the training step's tail (tail.hip): gradient finalize + fused Adam with the bf16 layouts
 enum TailOp : int { TAIL_SUM = 0, TAIL_COLSUM = 1, TAIL_SUMSQ = 2, TAIL_MM = 3, TAIL_ADAM = 4 };
 struct TailTask {
@@ -439,16 +470,26 @@ struct TailTask {
 constexpr int kTailMaxTasks = 16;  // the by-value table stays under 3 KB of kernel arguments
 constexpr int kTailMaxDeps = 4;
 constexpr int kTailMaxGrid = 1024;
+constexpr int kTailMaxTiles = 16384;  // per-tile norm partials (the part buffer)
+// every counter of the tail on its own 256-B line: agent-scope atomics to one line serialise
+// (~90 per us), and the ticket / queue / dependency words are hit by different workgroup sets
+constexpr int kTailLine = 64;                          // words
+constexpr int kTailTop = 0, kTailQueue = 1, kTailGroup0 = 2;  // line indices in sync
+constexpr int kTailSyncWords = (kTailGroup0 + 8) * kTailLine;
+constexpr int kTailDepWords = kTailMaxDeps * kTailLine;
 struct TailArgs {
   TailTask t[kTailMaxTasks];
   int n, ntiles, phase;        // phase 0 FINALIZE, 1 ADAM
-  float* part;                 // [kTailMaxGrid] per-workgroup sums of squares
-  unsigned* sync;              // [4] ticket (0), grid barrier (2); zeroed, reset by the kernel
-  unsigned* dep;               // [kTailMaxDeps] dependency counters (zeroed, reset)
+  int static_tiles;            // set by the launcher: tiles before the first waiting task's
+  int dynamic;                 // 1: atomic tile queue (the GPU may be shared); 0: static tiles
+  float* part;                 // [kTailMaxTiles] per-tile sums of squares (norm)
+  unsigned* sync;              // [kTailSyncWords] top ticket, tile queue head, 8 group tickets
+                               //   (one line each); zeroed, reset by the kernel
+  unsigned* dep;               // [kTailDepWords] dependency counters (line i: counter i)
   unsigned* err;
   unsigned spin_limit;
   float* total_out;            // FINALIZE: global sum of squares (+ extra)
-  const float* total_in;       // ADAM: that sum (nullptr: computed here over g[0, n_norm))
+  const float* total_in;       // ADAM: that sum
   const float* extra;          // one more norm term (the TF per-token embedding slot)
   float* p; const float* g; float* m; float* v; bf16* mirror;
   long n_norm;

@@ -1277,36 +1277,37 @@ void head(const at::Tensor& O, const at::Tensor& WsT, const c10::optional<at::Te
 // ------------------------------------------------------------------------------------------
 // token-reduction weight-gradient GEMMs (wgrad.hip): part[p][s] = A_p[chunk s]ᵀ · B_p[chunk s]
 // ------------------------------------------------------------------------------------------
-void wgrad(at::TensorList A, at::TensorList B, at::Tensor& part) {
+void wgrad(at::TensorList A, at::TensorList B, at::TensorList part) {
   const int np = (int)A.size();
-  TORCH_CHECK(np >= 1 && np <= dcr::kWgradMaxProblems && (int)B.size() == np, "wgrad: 1..",
-              dcr::kWgradMaxProblems, " problems");
-  check_seq(part, at::kFloat, "part");
-  TORCH_CHECK(part.dim() == 4 && part.size(0) == np, "part must be [np, S, M, N]");
-  const int S = (int)part.size(1), M = (int)part.size(2), N = (int)part.size(3);
+  TORCH_CHECK(np >= 1 && np <= dcr::kWgradMaxProblems && (int)B.size() == np &&
+                  (int)part.size() == np, "wgrad: 1..", dcr::kWgradMaxProblems, " problems");
   const int K = (int)A[0].size(0);
-  TORCH_CHECK(S >= 1 && S <= dcr::kWgradMaxSplit, "wgrad: 1..", dcr::kWgradMaxSplit, " slabs");
-  TORCH_CHECK(dcr::wgrad_supported(M, N, K), "wgrad: unsupported shape M=", M, " N=", N, " K=", K);
   dcr::WgradArgs a{};
   for (int i = 0; i < np; ++i) {
     const at::Tensor& x = A[i];
     const at::Tensor& y = B[i];
+    const at::Tensor& c = part[i];
     for (const at::Tensor* t : {&x, &y}) {
       TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->dim() == 2 &&
                       t->stride(1) == 1 && t->stride(0) % 8 == 0 &&
                       reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
                   "wgrad operands: bf16 [K, *] views with unit column stride, 16-B aligned rows");
     }
+    check_seq(c, at::kFloat, "part");
+    TORCH_CHECK(c.dim() == 3, "wgrad: part[p] must be [S, M, N]");
+    const int S = (int)c.size(0), M = (int)c.size(1), N = (int)c.size(2);
+    TORCH_CHECK(S >= 1 && S <= dcr::kWgradMaxSplit, "wgrad: 1..", dcr::kWgradMaxSplit, " slabs");
     TORCH_CHECK(x.size(0) == K && y.size(0) == K && x.size(1) == M && y.size(1) == N,
-                "wgrad: A_p must be [K, M], B_p [K, N]");
+                "wgrad: A_p must be [K, M], B_p [K, N] (one K for every problem)");
+    TORCH_CHECK(dcr::wgrad_supported(M, N, K), "wgrad: unsupported shape M=", M, " N=", N, " K=", K);
     a.p[i].A = ptr<bf16>(x); a.p[i].lda = x.stride(0);
     a.p[i].B = ptr<bf16>(y); a.p[i].ldb = y.stride(0);
-    a.p[i].C = part.data_ptr<float>() + (size_t)i * S * M * N;
+    a.p[i].C = c.data_ptr<float>();
     a.p[i].ldc = N;
     a.p[i].slab = (long)M * N;
+    a.p[i].M = M; a.p[i].N = N; a.p[i].S = S;
   }
-  a.np = np; a.S = S; a.M = M; a.N = N; a.K = K;
-  a.tiles = (M / 256) * (N / 256);
+  a.np = np; a.K = K;
   dcr::launch_wgrad(a, cur_stream());
 }
 
@@ -1323,16 +1324,17 @@ void tail(at::IntArrayRef words, int64_t phase, at::Tensor& part, at::Tensor& sy
           const c10::optional<at::Tensor>& m, const c10::optional<at::Tensor>& v,
           const c10::optional<at::Tensor>& mirror, int64_t n_norm, double lr_t, double b1,
           double b2, double eps, double clip, double gscale, const c10::optional<at::Tensor>& lr_dev,
-          const c10::optional<at::Tensor>& skip_if, const c10::optional<at::Tensor>& norm_out) {
+          const c10::optional<at::Tensor>& skip_if, const c10::optional<at::Tensor>& norm_out,
+          bool dynamic) {
   TORCH_CHECK(words.size() % kTailWords == 0, "tail: ", kTailWords, " words per task");
   const int n = (int)(words.size() / kTailWords);
   TORCH_CHECK(n >= 1 && n <= dcr::kTailMaxTasks, "tail: 1..", dcr::kTailMaxTasks, " tasks");
   TORCH_CHECK(phase == 0 || phase == 1, "tail: phase 0 or 1");
   CHECK_DEV(part); CHECK_F32(part);
-  TORCH_CHECK(part.numel() >= dcr::kTailMaxGrid, "tail: part needs ", dcr::kTailMaxGrid, " floats");
-  CHECK_DEV(sync); CHECK_I32(sync); TORCH_CHECK(sync.numel() >= 4, "tail: sync needs 4 words");
+  TORCH_CHECK(part.numel() >= dcr::kTailMaxTiles, "tail: part needs ", dcr::kTailMaxTiles, " floats");
+  CHECK_DEV(sync); CHECK_I32(sync); TORCH_CHECK(sync.numel() >= dcr::kTailSyncWords, "tail: sync needs ", dcr::kTailSyncWords, " words");
   CHECK_DEV(dep); CHECK_I32(dep);
-  TORCH_CHECK(dep.numel() >= dcr::kTailMaxDeps, "tail: dep needs ", dcr::kTailMaxDeps, " words");
+  TORCH_CHECK(dep.numel() >= dcr::kTailDepWords, "tail: dep needs ", dcr::kTailDepWords, " words");
   CHECK_DEV(err); CHECK_I32(err);
   auto opt_ptr = [](const c10::optional<at::Tensor>& t) -> void* {
     return (t.has_value() && t->defined()) ? t->data_ptr() : nullptr;
@@ -1345,6 +1347,7 @@ void tail(at::IntArrayRef words, int64_t phase, at::Tensor& part, at::Tensor& sy
   a.dep = reinterpret_cast<unsigned*>(dep.data_ptr());
   a.err = reinterpret_cast<unsigned*>(err.data_ptr());
   a.spin_limit = (unsigned)spin_limit;
+  a.dynamic = dynamic ? 1 : 0;
   a.total_out = static_cast<float*>(opt_ptr(total_out));
   a.total_in = static_cast<const float*>(opt_ptr(total_in));
   a.extra = static_cast<const float*>(opt_ptr(extra));
@@ -1356,6 +1359,7 @@ void tail(at::IntArrayRef words, int64_t phase, at::Tensor& part, at::Tensor& sy
       TORCH_CHECK(t->numel() == p->numel(), "tail ADAM: p, g, m, v sizes differ");
     }
     TORCH_CHECK(n_norm >= 0 && n_norm <= p->numel(), "tail ADAM: n_norm out of range");
+    TORCH_CHECK(total_in && total_in->defined(), "tail ADAM: the global sum of squares (total_in)");
     a.p = ptr<float>(*p); a.g = ptr<float>(*g); a.m = ptr<float>(*m); a.v = ptr<float>(*v);
     if (mirror && mirror->defined()) {
       CHECK_BF16(*mirror); CHECK_CONTIG(*mirror); CHECK_ALIGN16(*mirror);
@@ -1399,7 +1403,18 @@ void tail(at::IntArrayRef words, int64_t phase, at::Tensor& part, at::Tensor& sy
                     T.cols % 4 == 0, "tail SUM: float4 path needs 16-B aligned rows");
     }
     if (T.op == dcr::TAIL_COLSUM) TORCH_CHECK(T.k >= 1, "tail COLSUM: partial rows in k");
-    if (T.op == dcr::TAIL_MM) TORCH_CHECK(T.b != nullptr && T.k >= 1, "tail MM: B and k");
+    if (T.op == dcr::TAIL_MM) {
+      TORCH_CHECK(T.b != nullptr && T.k >= 1, "tail MM: B and k");
+      if (T.k > 128)  // the long path: float4 loads of A along k, k in whole 4-element groups
+        TORCH_CHECK(T.ak == 1 && T.k % 4 == 0 && (w[12] & 15) == 0 && T.ar % 4 == 0 &&
+                        (T.bk != 1 || ((w[15] & 15) == 0 && T.bc % 4 == 0)),
+                    "tail MM (k > 128): A k-contiguous, 16-B aligned rows, k % 4 == 0");
+      if (T.nslab > 1)  // k-slabs (long path only) into dst + s * off, summed by a later SUM
+        TORCH_CHECK(T.k > 128 && !T.norm && T.off >= (int64_t)(T.rows - 1) * T.dst_ld + T.cols &&
+                        T.nslab <= T.k / 64,
+                    "tail MM: k-slabs need k > 128, no norm, a slab stride covering a slab and "
+                    "at least 64 k per slab");
+    }
     if (T.op == dcr::TAIL_ADAM) {
       TORCH_CHECK(phase == 1, "tail ADAM in phase 1");
       TORCH_CHECK(T.off >= 0 && T.off + (T.rows - 1) * T.ld + T.cols <= p->numel(),
@@ -1416,6 +1431,68 @@ void tail(at::IntArrayRef words, int64_t phase, at::Tensor& part, at::Tensor& sy
 }
 
 int64_t tail_words() { return kTailWords; }
+
+// single-launch generation (generate.hip)
+void generate(at::TensorList Wh, at::TensorList Wx, at::TensorList bias, const at::Tensor& table,
+              const at::Tensor& WsT, const at::Tensor& bs, double forget_bias, const at::Tensor& h0,
+              const at::Tensor& c0, at::Tensor& h_out, at::Tensor& c_out, const at::Tensor& prime,
+              int64_t num, at::Tensor& out, at::Tensor& hx, int64_t mode, int64_t space_id,
+              int64_t seed, const at::Tensor& ctr0, const c10::optional<at::Tensor>& logits_out,
+              at::Tensor& err, int64_t spin_limit) {
+  const int L = (int)Wh.size();
+  TORCH_CHECK(L >= 1 && L <= dcr::kGenMaxLayers && (int)Wx.size() == L && (int)bias.size() == L,
+              "generate: 1..", dcr::kGenMaxLayers, " layers");
+  CHECK_DEV(table); CHECK_F32(table); CHECK_CONTIG(table);
+  CHECK_DEV(WsT); CHECK_BF16(WsT); CHECK_CONTIG(WsT); CHECK_ALIGN16(WsT);
+  const int V = (int)WsT.size(0), H = (int)WsT.size(1);
+  TORCH_CHECK(table.dim() == 2 && table.size(0) == V && table.size(1) == 4 * H, "generate: table [V, 4H]");
+  CHECK_DEV(bs); CHECK_F32(bs); TORCH_CHECK(bs.numel() == V, "generate: bs [V]");
+  dcr::GenArgs a{};
+  a.L = L; a.H = H; a.V = V;
+  for (int l = 0; l < L; ++l) {
+    for (const at::Tensor* t : {&Wh[l], &Wx[l]}) {
+      CHECK_DEV(*t); CHECK_BF16(*t); CHECK_CONTIG(*t);
+      TORCH_CHECK(t->dim() == 2 && t->size(0) == H && t->size(1) == 4 * H, "generate: W [H, 4H]");
+    }
+    CHECK_DEV(bias[l]); CHECK_F32(bias[l]); CHECK_CONTIG(bias[l]);
+    TORCH_CHECK(bias[l].numel() == 4 * H, "generate: bias [4H]");
+    a.Wh[l] = ptr<bf16>(Wh[l]); a.Wx[l] = ptr<bf16>(Wx[l]); a.bias[l] = ptr<float>(bias[l]);
+  }
+  for (const at::Tensor* t : {&h0, &c0, (const at::Tensor*)&h_out, (const at::Tensor*)&c_out}) {
+    CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t);
+    TORCH_CHECK(t->dim() == 3 && t->size(0) == L && t->size(2) == H && t->size(1) == h0.size(1),
+                "generate: state [L, S, H]");
+  }
+  a.S = (int)h0.size(1);
+  CHECK_DEV(prime); CHECK_I32(prime); CHECK_CONTIG(prime);
+  a.P = (int)prime.numel();
+  TORCH_CHECK(a.P >= 1 && num >= 1, "generate: a prime of >= 1 ids and num >= 1");
+  CHECK_DEV(out); CHECK_I32(out); CHECK_CONTIG(out);
+  TORCH_CHECK(out.numel() == (int64_t)a.S * num, "generate: out [S, num]");
+  CHECK_DEV(hx); CHECK_CONTIG(hx);
+  TORCH_CHECK(hx.element_size() == 8 && hx.numel() >= (int64_t)L * 2 * a.S * H, "generate: hx [L, 2, S, H] of 8-B granules");
+  CHECK_DEV(ctr0); CHECK_I32(ctr0); TORCH_CHECK(ctr0.numel() >= a.S, "generate: ctr0 [S]");
+  CHECK_DEV(err); CHECK_I32(err);
+  a.table = ptr<float>(table); a.WsT = ptr<bf16>(WsT); a.bs = ptr<float>(bs);
+  a.forget_bias = (float)forget_bias;
+  a.h0 = ptr<float>(h0); a.c0 = ptr<float>(c0); a.h_out = ptr<float>(h_out); a.c_out = ptr<float>(c_out);
+  a.prime = ptr<int>(prime); a.num = (int)num; a.out = ptr<int>(out);
+  a.hx = reinterpret_cast<unsigned long long*>(hx.data_ptr());
+  a.mode = (int)mode; a.space_id = (int)space_id; a.seed = (unsigned long long)seed;
+  a.ctr0 = reinterpret_cast<const unsigned*>(ctr0.data_ptr());
+  if (logits_out.has_value() && logits_out->defined()) {
+    CHECK_DEV(*logits_out); CHECK_F32(*logits_out); CHECK_CONTIG(*logits_out);
+    TORCH_CHECK(logits_out->numel() >= num * a.S * V, "generate: logits_out [num, S, V]");
+    a.logits_out = ptr<float>(*logits_out);
+  }
+  a.err = reinterpret_cast<unsigned*>(err.data_ptr());
+  a.spin_limit = (unsigned)spin_limit;
+  // the hand-off tags must not match stale granules of an earlier launch
+  TORCH_CHECK(hipMemsetAsync(hx.data_ptr(), 0, (size_t)L * 2 * a.S * H * 8, cur_stream()) == hipSuccess,
+              "generate: clearing the hand-off buffer failed");
+  const int rc = dcr::launch_generate(a, num_cus(), cur_stream());
+  TORCH_CHECK(rc == 0, "generate: unsupported shape or launch failure (", rc, ")");
+}
 // TF token-norm term (tokennorm.hip): out[0] = sum_tok ||dz[tok] · wᵀ||²
 void tokennorm(const at::Tensor& dz, const at::Tensor& w, at::Tensor& part, at::Tensor& ticket,
                at::Tensor& out) {
@@ -1665,14 +1742,26 @@ TORCH_LIBRARY(dcr, m) {
         "Tensor(d!) err, int spin_limit, Tensor(e!)? total_out, Tensor? total_in, Tensor? extra, "
         "Tensor(f!)? p, Tensor? g, Tensor(g!)? m, Tensor(h!)? v, Tensor(i!)? mirror, int n_norm, "
         "float lr_t, float b1, float b2, float eps, float clip, float gscale, Tensor? lr_dev, "
-        "Tensor? skip_if, Tensor(j!)? norm_out) -> ()");
+        "Tensor? skip_if, Tensor(j!)? norm_out, bool dynamic=True) -> ()");
   m.def("tail_words() -> int", []() -> int64_t { return kTailWords; });
+  m.def("generate(Tensor[] Wh, Tensor[] Wx, Tensor[] bias, Tensor table, Tensor WsT, Tensor bs, "
+        "float forget_bias, Tensor h0, Tensor c0, Tensor(a!) h_out, Tensor(b!) c_out, Tensor prime, "
+        "int num, Tensor(c!) out, Tensor(d!) hx, int mode, int space_id, int seed, Tensor ctr0, "
+        "Tensor(e!)? logits_out, Tensor(f!) err, int spin_limit) -> ()");
+  m.def("generate_supported(int L, int H, int V, int S) -> int",
+        [](int64_t L, int64_t H, int64_t V, int64_t S) -> int64_t {
+          return dcr::generate_supported((int)L, (int)H, (int)V, (int)S, num_cus()); });
   m.def("tokennorm(Tensor dz, Tensor w, Tensor(a!) part, Tensor(b!) ticket, Tensor(c!) out) -> ()");
   m.def("tokennorm_supported(int N, int H, int K) -> int", [](int64_t N, int64_t H, int64_t K) -> int64_t {
     return dcr::tokennorm_supported((int)N, (int)H, (int)K) ? 1 : 0; });
   m.def("tail_max_tasks() -> int", []() -> int64_t { return dcr::kTailMaxTasks; });
+  m.def("tail_ws_words() -> int[]", []() -> std::vector<int64_t> {
+    return {dcr::kTailSyncWords, dcr::kTailDepWords};
+  });
   m.def("tail_grid() -> int", []() -> int64_t { return dcr::tail_grid(num_cus()); });
-  m.def("wgrad(Tensor[] A, Tensor[] B, Tensor(a!) part) -> ()");
+  m.def("wgrad(Tensor[] A, Tensor[] B, Tensor(a!)[] part) -> ()");
+  m.def("wgrad_plan_tiles(int tiles, int K) -> int", [](int64_t tiles, int64_t K) -> int64_t {
+    return dcr::wgrad_splits_tiles((int)tiles, (int)K, num_cus()); });
   m.def("wgrad_plan(int np, int M, int N, int K) -> int",
         [](int64_t np, int64_t M, int64_t N, int64_t K) -> int64_t {
           if (!dcr::wgrad_supported((int)M, (int)N, (int)K)) return 0;
@@ -1752,6 +1841,7 @@ TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("head", &head);
   m.impl("prep", &prep);
   m.impl("tail", &tail);
+  m.impl("generate", &generate);
   m.impl("tokennorm", &tokennorm);
   m.impl("wgrad", &wgrad);
   m.impl("gru_persist_fwd", &gru_persist_fwd);

@@ -263,11 +263,13 @@ __host__ __device__ __forceinline__ unsigned frag_tile_off(int bg, int kstep, in
   return (unsigned)(((size_t)bg * (K >> 5) + kstep) * 1024);
 }
 
-// Block -> (unit block, batch group).  Speed only: place the unit-block workgroups of one batch
-// group on the same XCD under the observed round-robin dispatch (blocks b, b+8, ... share an
-// XCD; MI355X_MICROARCH.md "Workgroup dispatch"), so the batch group's hand-off payload is
-// fetched into one L2 and served to all its consumers from there.  Correctness never depends
-// on it: every hand-off is sc1 + counters regardless of placement.
+// Block -> (unit block, batch group).  Place the unit-block workgroups of one batch group on the
+// same XCD under the observed round-robin dispatch (blocks b, b+8, ... share an XCD;
+// MI355X_MICROARCH.md "Workgroup dispatch"), so the batch group's hand-off payload stays in one
+// L2.  Correctness never depends on the placement: the kernel checks it at run time (xcd_decide
+// above) and a column takes the XCD-local form (plain stores + per-workgroup flags) only when
+// all its workgroups were found on one XCD, otherwise the write-through form (sc1 stores +
+// arrival counters).
 __host__ __device__ __forceinline__ void map_block(int bid, int nwg_u, int nbg, int& ubk,
                                                     int& bg) {
   if (nbg % 8 == 0 && XCD_GROUPING) {

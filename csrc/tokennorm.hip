@@ -73,12 +73,22 @@ __global__ void __launch_bounds__(64 * kTnWaves, kTnWaves / 4) tokennorm_kernel(
   const unsigned pch = (unsigned)((lane >> 4) ^ ((4 - ((lane & 15) >> 2)) & 3));
   const unsigned fa0 = (unsigned)((wm + (lane & 15)) * 64 + pch * 16);
   const unsigned fb0 = (unsigned)(kTnTile * 64 + (wn + (lane & 15)) * 64 + pch * 16);
-  auto read_frags = [&](int kt, u32x4 (&fa)[8], u32x4 (&fb)[4]) {
+  auto rd_a = [&](int kt, u32x4 (&fa)[8], int i0, int i1) {
     const unsigned base = lds0 + (kt % kTnStages) * kTnStageB;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) fa[i] = gemm_rd128(base + fa0 + 1024 * i);
+    for (int i = i0; i < i1; ++i) fa[i] = gemm_rd128(base + fa0 + 1024 * i);
+  };
+  auto rd_b = [&](int kt, u32x4 (&fb)[4]) {
+    const unsigned base = lds0 + (kt % kTnStages) * kTnStageB;
 #pragma unroll
     for (int j = 0; j < 4; ++j) fb[j] = gemm_rd128(base + fb0 + 1024 * j);
+  };
+  auto issue_pair = [&](int kt, int j) {  // this wave's DMA pair j of stage kt
+    const unsigned st = lds0 + (kt % kTnStages) * kTnStageB;
+    const unsigned sk = (unsigned)(kt * kTnK * sizeof(bf16));
+    const unsigned r = (unsigned)(16 * (2 * w + j));
+    gemm_dma(ra, st + r * 64, offa[j], sk);
+    gemm_dma(rb, st + kTnTile * 64 + r * 64, offb[j], sk);
   };
 
   f32x4 acc[8][4];
@@ -86,32 +96,58 @@ __global__ void __launch_bounds__(64 * kTnWaves, kTnWaves / 4) tokennorm_kernel(
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  u32x4 fa_0[8], fb_0[4], fa_1[8], fb_1[4];
+  auto mf = [&](int g, u32x4 (&fa)[8], u32x4 (&fb)[4]) {  // MFMA group g: A tiles 2g, 2g + 1
+#pragma unroll
+    for (int ii = 2 * g; ii < 2 * g + 2; ++ii)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        acc[ii][jj] = mfma16(__builtin_bit_cast(bf16x8, fa[ii]), __builtin_bit_cast(bf16x8, fb[jj]), acc[ii][jj]);
+  };
+  u32x4 fa[8], fb_0[4], fb_1[4];
   const int nk = ksteps;
   {
     const int pro = nk < kTnStages ? nk : kTnStages;
     for (int j = 0; j < pro; ++j) issue(j);
     gemm_vm_wait((pro - 1) * kTnDmaPerWave);
     gemm_barrier();
-    read_frags(0, fa_0, fb_0);
+    rd_b(0, fb_0);
+    rd_a(0, fa, 0, 8);
   }
-  auto kstep = [&](int i, u32x4 (&fa)[8], u32x4 (&fb)[4], u32x4 (&na)[8], u32x4 (&nb_)[4]) {
-    if (i + 1 < nk) {
+  // the k-step schedule of wgrad.hip v3: four MFMA groups of 8 with the refill DMA pairs and the
+  // next stage's fragment reads between them (A into the registers just consumed)
+  auto kstep = [&](int i, u32x4 (&fb)[4], u32x4 (&nb_)[4]) {
+    const bool more = i + 1 < nk;
+    const bool refill = more && i + kTnStages < nk;
+    if (more) {
       const int later = nk - 2 - i < kTnStages - 2 ? nk - 2 - i : kTnStages - 2;
       gemm_vm_wait(later * kTnDmaPerWave);
       gemm_barrier();
-      if (i + kTnStages < nk) issue(i + kTnStages);
-      read_frags(i + 1, na, nb_);
     }
-#pragma unroll
-    for (int ii = 0; ii < 8; ++ii)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-        acc[ii][jj] = mfma16(__builtin_bit_cast(bf16x8, fa[ii]), __builtin_bit_cast(bf16x8, fb[jj]), acc[ii][jj]);
+    __builtin_amdgcn_sched_barrier(0);
+    mf(0, fa, fb);
+    __builtin_amdgcn_sched_barrier(0);
+    if (refill) issue_pair(i + kTnStages, 0);
+    if (more) {
+      rd_b(i + 1, nb_);
+      rd_a(i + 1, fa, 0, 2);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mf(1, fa, fb);
+    __builtin_amdgcn_sched_barrier(0);
+    if (refill) issue_pair(i + kTnStages, 1);
+    if (more) rd_a(i + 1, fa, 2, 4);
+    __builtin_amdgcn_sched_barrier(0);
+    mf(2, fa, fb);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) rd_a(i + 1, fa, 4, 6);
+    __builtin_amdgcn_sched_barrier(0);
+    mf(3, fa, fb);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) rd_a(i + 1, fa, 6, 8);
   };
   for (int i = 0; i < nk; i += 2) {
-    kstep(i, fa_0, fb_0, fa_1, fb_1);
-    if (i + 1 < nk) kstep(i + 1, fa_1, fb_1, fa_0, fb_0);
+    kstep(i, fb_0, fb_1);
+    if (i + 1 < nk) kstep(i + 1, fb_1, fb_0);
   }
 
   // epilogue (the host requires N % 256 == 0: no ragged tile): the sum of squares of this

@@ -17,17 +17,23 @@
 // Workgroups of one (problem, slab) -- which share their A and B panels -- are placed on one XCD
 // (round-robin dispatch), so those panels are fetched into one L2.
 //
-// Pipeline (v2).  The panels arrive by LDS-DMA (buffer_load ... lds, 16 B per lane, 1 KB = two
+// Pipeline.  The panels arrive by LDS-DMA (buffer_load ... lds, 16 B per lane, 1 KB = two
 // k-rows per instruction) into a ring of kWgStages 32 KB stages, kWgStages - 1 of them in
-// flight (v1 staged through registers one k-step ahead, too short to cover an L2 / HBM round
-// trip).  A wave's DMA count per stage is fixed (4), so the wait for a stage is a counted vmcnt;
+// flight.  A wave's DMA count per stage is fixed (4), so the wait for a stage is a counted vmcnt;
 // the DMA is inline asm, invisible to the compiler's waitcnt pass, which would otherwise wait
-// vmcnt(0) for the whole ring before every LDS read.
+// vmcnt(0) for the whole ring before every LDS read.  v3: after the k-step's barrier the wave's
+// 32 MFMAs run in four groups of 8 with the stage refill (one DMA pair per group) and the next
+// stage's fragment reads between the groups, pinned there by sched_barrier (the A fragments of
+// the next stage land in the registers the group before has consumed: one A register set, 32
+// VGPRs fewer than two, no spill next to the 128 accumulators): in v2 every wave
+// issued its DMAs and all 24 reads right after the barrier, with both waves of a SIMD in
+// lockstep, so the matrix pipe idled through that burst (scripts/micro/gemm_lab.hip, headline
+// shapes, same box: [1024 x 2048] 127 -> 120 us, [512 x 2048] 70 -> 67 us, both in one launch
+// 211 -> 191 us).
 //
-// Measured (scripts/micro/wgrad2_bench.py, slabs only, 32768 tokens): [1024 x 2048] 140 vs
-// 150 us for the library split-K bmm, [2048 x 8192] 955 vs 968 us, [512 x 2048] 85 vs 80 us,
-// [1024 x 3072] 209 vs 203 us: at parity (46 % of the MFMA peak on the large shape), so the step
-// keeps the library form by default (DCR_DEBUG=wgrad=1 selects this kernel).
+// Problems of different shapes share one launch (the step's layer-1 [1024 x 2048] and layer-0
+// [512 x 2048] gradients, K = 32768): the work items are (problem, slab, tile), one per
+// workgroup, each problem with its own split count.
 //
 // LDS layout.  Row r of a stage holds 256 bf16 (32 chunks of 16 B, no padding); logical chunk c
 // sits at physical chunk c ^ f(r), f(r) = 2 (r & 7) + ((r >> 4) & 1).  One transposed read of a
@@ -36,7 +42,7 @@
 // 2-pass minimum for 512 B -- where the unswizzled rows would all hit the same 8 banks.  The DMA
 // writes each lane's 16 B to physical position lane, so a lane fetches the logical chunk that
 // belongs there (the global reads stay two whole 512-B rows per instruction).
-#include "common.h"
+#include "gemm_common.h"
 #include "kernels.h"
 
 namespace dcr {
@@ -45,64 +51,36 @@ constexpr int kWgTile = 256;   // output tile edge (M and N)
 constexpr int kWgK = 32;       // k rows per stage (one MFMA k step)
 constexpr int kWgStages = 4;   // LDS ring stages (kWgStages - 1 in flight)
 constexpr int kWgStageB = 2 * kWgK * kWgTile * 2;  // bytes per stage (A + B panels)
-constexpr int kWgWaves = 8;                        // 2 per SIMD: one's LDS reads hide under the other's MFMAs
+constexpr int kWgWaves = 8;                        // 2 per SIMD
 constexpr int kWgDmaPerWave = 32 / kWgWaves;       // DMA instructions per wave and stage
 
 __device__ __forceinline__ int wg_swz(int r) { return 2 * (r & 7) + ((r >> 4) & 1); }
-
-// raw barrier: __syncthreads()' release fence would wait vmcnt(0) for the in-flight ring
-__device__ __forceinline__ void wg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-__device__ __forceinline__ void wg_vm_wait(int n) {
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-  }
-}
-// transposed 64-bit LDS read: 4 bf16 of 4 consecutive k for this lane's m (compiler-visible;
-// the ring's DMA is not, see wg_dma)
-typedef short s16x4_wg __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ u32x2 wg_rd_tr(unsigned addr) {
-  return __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                                       (__attribute__((address_space(3))) s16x4_wg*)(size_t)addr));
-}
-// one LDS-DMA instruction (16 B per lane to LDS address lds + 16 lane), issued as inline asm so
-// that the compiler's waitcnt pass does not see an LDS write: it would otherwise wait vmcnt(0)
-// for the whole ring before every LDS read.  The stage waits are the counted wg_vm_wait; the
-// "memory" clobbers keep every LDS read of a slot on its side of the barriers.  (The kernel has
-// no other M0 user.)
-__device__ __forceinline__ void wg_dma(__amdgpu_buffer_rsrc_t r, unsigned lds, unsigned voff,
-                                       unsigned soff) {
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
-               :: "s"(lds), "v"(voff), "s"(r), "s"(soff) : "memory");
-}
 
 __global__ void __launch_bounds__(64 * kWgWaves, kWgWaves / 4) wgrad_kernel(WgradArgs a) {
   __shared__ __attribute__((aligned(1024))) unsigned char lds[kWgStages * kWgStageB];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // block -> (group = (problem, slab), tile in group); a group's tiles on one XCD
+  // block -> work item; the items of one (problem, slab) -- which share their A and B panels --
+  // are consecutive and dealt to one XCD (round-robin dispatch), so those panels are fetched
+  // into one L2
   const int nb = gridDim.x;
   const int lin = (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8;
-  const int grp = lin / a.tiles, tile = lin % a.tiles;
-  if (grp >= a.np * a.S) return;  // padding blocks (grid rounded to a multiple of 8)
-  const int p = grp / a.S, s = grp % a.S;
-  const WgradProblem& P = a.p[p];
-  const int tn = a.N / kWgTile;
+  if (lin >= a.items) return;  // padding blocks (grid rounded to a multiple of 8)
+  int pi = 0;
+  while (pi + 1 < a.np && lin >= a.p[pi + 1].item0) ++pi;
+  const WgradProblem& P = a.p[pi];
+  const int loc = lin - P.item0;
+  const int s = loc / P.tiles, tile = loc % P.tiles;
+  const int tn = P.N / kWgTile;
   const int m0 = (tile / tn) * kWgTile, n0 = (tile % tn) * kWgTile;
   const int ksteps = a.K / kWgK;
-  const int kt0 = (int)((long)ksteps * s / a.S), kt1 = (int)((long)ksteps * (s + 1) / a.S);
+  const int kt0 = (int)((long)ksteps * s / P.S), kt1 = (int)((long)ksteps * (s + 1) / P.S);
   const int nk = kt1 - kt0;
 
   // DMA: wave w fills k-rows [4 w, 4 w + 4) of both panels, 2 rows per instruction; lane l
   // writes physical chunk (l & 31) of row 4 w + 2 j + (l >> 5)
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16*>(P.A), (short)0, 0x7FFFFFF0, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16*>(P.B), (short)0, 0x7FFFFFF0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ra = gemm_rsrc(P.A);
+  const __amdgpu_buffer_rsrc_t rb = gemm_rsrc(P.B);
   unsigned offa[kWgDmaPerWave / 2], offb[kWgDmaPerWave / 2];  // k-step 0 (+ kt * 32 rows)
 #pragma unroll
   for (int j = 0; j < kWgDmaPerWave / 2; ++j) {
@@ -112,16 +90,14 @@ __global__ void __launch_bounds__(64 * kWgWaves, kWgWaves / 4) wgrad_kernel(Wgra
     offb[j] = (unsigned)(((size_t)r * P.ldb + n0 + 8 * c) * sizeof(bf16));
   }
   const unsigned lds0 = (unsigned)(size_t)(const __attribute__((address_space(3))) void*)lds;
-  auto issue = [&](int kt) {  // stage kt into ring slot kt % kWgStages
-    const unsigned st = lds0 + ((kt - kt0) % kWgStages) * kWgStageB;
+  auto stage_addr = [&](int kt) { return lds0 + ((kt - kt0) & (kWgStages - 1)) * kWgStageB; };
+  auto issue_pair = [&](int kt, int j) {  // this wave's DMA pair j of stage kt
+    const unsigned st = stage_addr(kt);
     const unsigned sa = (unsigned)((size_t)kt * kWgK * P.lda * sizeof(bf16));
     const unsigned sb = (unsigned)((size_t)kt * kWgK * P.ldb * sizeof(bf16));
-#pragma unroll
-    for (int j = 0; j < kWgDmaPerWave / 2; ++j) {
-      const unsigned r = (unsigned)(kWgDmaPerWave * w + 2 * j);
-      wg_dma(ra, st + r * 512, offa[j], sa);
-      wg_dma(rb, st + kWgK * 512 + r * 512, offb[j], sb);
-    }
+    const unsigned r = (unsigned)(kWgDmaPerWave * w + 2 * j);
+    gemm_dma(ra, st + r * 512, offa[j], sa);
+    gemm_dma(rb, st + kWgK * 512 + r * 512, offb[j], sb);
   };
 
   // fragment read addresses: lane 16q + 4ta + tp reads k-row b_q + ta (lo; + 8 hi), m columns
@@ -142,18 +118,21 @@ __global__ void __launch_bounds__(64 * kWgWaves, kWgWaves / 4) wgrad_kernel(Wgra
     xa[h] = (unsigned)(cb_a ^ wg_swz(row));
     xb[h] = (unsigned)(cb_b ^ wg_swz(row));
   }
-  auto read_frags = [&](int kt, u32x4 (&fa)[8], u32x4 (&fb)[4]) {
-    const unsigned base = lds0 + ((kt - kt0) % kWgStages) * kWgStageB;
+  auto rd_a = [&](int kt, u32x4 (&fa)[8], int i0, int i1) {
+    const unsigned base = stage_addr(kt);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const u32x2 lo = wg_rd_tr(base + rowb[0] + ((xa[0] ^ (2u * i)) << 4));
-      const u32x2 hi = wg_rd_tr(base + rowb[1] + ((xa[1] ^ (2u * i)) << 4));
+    for (int i = i0; i < i1; ++i) {
+      const u32x2 lo = gemm_rd_tr(base + rowb[0] + ((xa[0] ^ (2u * i)) << 4));
+      const u32x2 hi = gemm_rd_tr(base + rowb[1] + ((xa[1] ^ (2u * i)) << 4));
       fa[i] = u32x4{lo[0], lo[1], hi[0], hi[1]};
     }
+  };
+  auto rd_b = [&](int kt, u32x4 (&fb)[4]) {
+    const unsigned base = stage_addr(kt) + kWgK * 512;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const u32x2 lo = wg_rd_tr(base + kWgK * 512 + rowb[0] + ((xb[0] ^ (2u * j)) << 4));
-      const u32x2 hi = wg_rd_tr(base + kWgK * 512 + rowb[1] + ((xb[1] ^ (2u * j)) << 4));
+      const u32x2 lo = gemm_rd_tr(base + rowb[0] + ((xb[0] ^ (2u * j)) << 4));
+      const u32x2 hi = gemm_rd_tr(base + rowb[1] + ((xb[1] ^ (2u * j)) << 4));
       fb[j] = u32x4{lo[0], lo[1], hi[0], hi[1]};
     }
   };
@@ -163,39 +142,68 @@ __global__ void __launch_bounds__(64 * kWgWaves, kWgWaves / 4) wgrad_kernel(Wgra
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // prologue: the first kWgStages stages in flight, stage 0 landed everywhere, its fragments read
-  u32x4 fa0[8], fb0[4], fa1[8], fb1[4];
-  if (nk > 0) {
-    const int pro = nk < kWgStages ? nk : kWgStages;
-    for (int j = 0; j < pro; ++j) issue(kt0 + j);
-    wg_vm_wait((pro - 1) * kWgDmaPerWave);
-    wg_barrier();
-    read_frags(kt0, fa0, fb0);
-  }
-  // k-step i: its fragments are in (fa, fb); stage i+1's are read into (na, nb) under its MFMAs
-  // (two statically indexed register sets: the loop runs two k-steps per trip)
-  auto kstep = [&](int i, u32x4 (&fa)[8], u32x4 (&fb)[4], u32x4 (&na)[8], u32x4 (&nb)[4]) {
-    const int kt = kt0 + i;
-    if (i + 1 < nk) {
-      // stage kt+1 landed (the later in-flight stages may stay outstanding), visible to every
-      // wave; stage kt's slot was read by every wave before this barrier: refill it
-      const int later = nk - 2 - i < kWgStages - 2 ? nk - 2 - i : kWgStages - 2;
-      wg_vm_wait(later * kWgDmaPerWave);
-      wg_barrier();
-      if (i + kWgStages < nk) issue(kt + kWgStages);
-      read_frags(kt + 1, na, nb);
-    }
+  auto mf = [&](int g, u32x4 (&fa)[8], u32x4 (&fb)[4]) {  // MFMA group g: A tiles 2g, 2g + 1
 #pragma unroll
-    for (int ii = 0; ii < 8; ++ii)
+    for (int ii = 2 * g; ii < 2 * g + 2; ++ii)
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj)
         acc[ii][jj] = mfma16(__builtin_bit_cast(bf16x8, fa[ii]), __builtin_bit_cast(bf16x8, fb[jj]),
                              acc[ii][jj]);
   };
+
+  // prologue: the first kWgStages stages in flight, stage 0 landed everywhere, its fragments read
+  u32x4 fa[8], fb0[4], fb1[4];
+  if (nk > 0) {
+    const int pro = nk < kWgStages ? nk : kWgStages;
+    for (int j = 0; j < pro; ++j) {
+      issue_pair(kt0 + j, 0);
+      issue_pair(kt0 + j, 1);
+    }
+    gemm_vm_wait((pro - 1) * kWgDmaPerWave);
+    gemm_barrier();
+    rd_b(kt0, fb0);
+    rd_a(kt0, fa, 0, 8);
+  }
+  // k-step i: its fragments are in (fa, fb); between the MFMA groups the next stage's A tiles
+  // are read into the registers the previous group has just consumed (ONE A set), its B tiles
+  // into the other B set, next to the refill of stage i's slot (two statically indexed B sets:
+  // the loop runs two k-steps per trip)
+  auto kstep = [&](int i, u32x4 (&fb)[4], u32x4 (&nb_)[4]) {
+    const int kt = kt0 + i;
+    const bool more = i + 1 < nk;
+    const bool refill = more && i + kWgStages < nk;
+    if (more) {
+      // stage kt+1 landed (the later in-flight stages may stay outstanding), visible to every
+      // wave; stage kt's slot was read by every wave before this barrier: it may be refilled
+      const int later = nk - 2 - i < kWgStages - 2 ? nk - 2 - i : kWgStages - 2;
+      gemm_vm_wait(later * kWgDmaPerWave);
+      gemm_barrier();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mf(0, fa, fb);
+    __builtin_amdgcn_sched_barrier(0);
+    if (refill) issue_pair(kt + kWgStages, 0);
+    if (more) {
+      rd_b(kt + 1, nb_);
+      rd_a(kt + 1, fa, 0, 2);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mf(1, fa, fb);
+    __builtin_amdgcn_sched_barrier(0);
+    if (refill) issue_pair(kt + kWgStages, 1);
+    if (more) rd_a(kt + 1, fa, 2, 4);
+    __builtin_amdgcn_sched_barrier(0);
+    mf(2, fa, fb);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) rd_a(kt + 1, fa, 4, 6);
+    __builtin_amdgcn_sched_barrier(0);
+    mf(3, fa, fb);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) rd_a(kt + 1, fa, 6, 8);
+  };
   for (int i = 0; i < nk; i += 2) {
-    kstep(i, fa0, fb0, fa1, fb1);
-    if (i + 1 < nk) kstep(i + 1, fa1, fb1, fa0, fb0);
+    kstep(i, fb0, fb1);
+    if (i + 1 < nk) kstep(i + 1, fb1, fb0);
   }
 
   // D[4q + r][l & 15] of tile (i, j): row m0 + wm + 16 i + 4 q + r, column n0 + wn + 16 j + l%16
@@ -212,18 +220,18 @@ bool wgrad_supported(int M, int N, int K) {
   return M > 0 && N > 0 && M % kWgTile == 0 && N % kWgTile == 0 && K % kWgK == 0 && K > 0;
 }
 
-// Slabs per problem.  One workgroup per CU (128 KB of LDS ring), so a grid of np x tiles x S
-// workgroups runs in ceil(blocks / cus) rounds; pick the S with the best CU utilisation
-// blocks / (rounds x cus), less 1 % per slab (each slab is an extra M x N fp32 write + read in the
-// flush), each slab at least 1024 tokens deep.  (A second partial round costs a full round:
-// 3 x 16 tiles x 6 slabs = 288 workgroups ran 367 us vs 230 us at 5 slabs.)
-int wgrad_splits(int np, int M, int N, int K, int cus) {
-  const int tiles = (M / kWgTile) * (N / kWgTile);
+// One split count for a launch of problems with `tiles` output tiles in all (M, N multiples of
+// 256).  One workgroup per CU (128 KB of LDS ring), so a grid of tiles x S workgroups runs in
+// ceil(blocks / cus) rounds; pick the S with the best CU utilisation blocks / (rounds x cus),
+// less 1 % per slab (each slab is an extra M x N fp32 write + read in the finalize), each slab
+// at least 1024 tokens deep.  (A second partial round costs a full round: 3 x 16 tiles x 6
+// slabs = 288 workgroups ran 367 us vs 230 us at 5 slabs.)
+int wgrad_splits_tiles(int tiles, int K, int cus) {
   const int smax = K / 1024 > 1 ? (K / 1024 < kWgradMaxSplit ? K / 1024 : kWgradMaxSplit) : 1;
   int best = 1;
   double best_score = -1.0;
   for (int S = 1; S <= smax; ++S) {
-    const long blocks = (long)np * tiles * S;
+    const long blocks = (long)tiles * S;
     const long rounds = (blocks + cus - 1) / cus;
     const double score = (double)blocks / ((double)rounds * cus) - 0.01 * S;
     if (score > best_score + 1e-9) {
@@ -234,9 +242,19 @@ int wgrad_splits(int np, int M, int N, int K, int cus) {
   return best;
 }
 
-void launch_wgrad(const WgradArgs& a, hipStream_t s) {
-  const int blocks = a.np * a.S * a.tiles;
-  const int grid = (blocks + 7) / 8 * 8;
+int wgrad_splits(int np, int M, int N, int K, int cus) {
+  return wgrad_splits_tiles(np * (M / kWgTile) * (N / kWgTile), K, cus);
+}
+
+void launch_wgrad(WgradArgs& a, hipStream_t s) {
+  int items = 0;
+  for (int i = 0; i < a.np; ++i) {
+    a.p[i].tiles = (a.p[i].M / kWgTile) * (a.p[i].N / kWgTile);
+    a.p[i].item0 = items;
+    items += a.p[i].tiles * a.p[i].S;
+  }
+  a.items = items;
+  const int grid = (items + 7) / 8 * 8;
   wgrad_kernel<<<grid, 64 * kWgWaves, 0, s>>>(a);
 }
 

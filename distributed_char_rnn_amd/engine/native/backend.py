@@ -100,9 +100,11 @@ class NativeBackend(LayoutsMixin, BuffersMixin, ForwardMixin, BackwardMixin, Lib
         self._mirror: Optional[torch.Tensor] = None
         self._adam_tab = None
         self._adam_ws = None
+        self._adam_sq = None
         self._tail_total: Optional[torch.Tensor] = None
         self._tail_total_ok = False
         self._tn_ws = None  # token-norm kernel partials + ticket
+        self._gen_ver = None  # weight version of the generator's softmax_wᵀ copy
 
     def check_errors(self):
         """Raise if a persistent kernel hit its spin timeout (forces a device sync).  The word

@@ -45,7 +45,7 @@ class BackwardMixin:
         # on the LSTM gather route one tail FINALIZE launch (csrc/tail.hip) that also computes
         # the layer-0 products and the global norm for the fused Adam
         dp = on_ready is not None
-        use_wgrad = self.knobs.debug.get("wgrad") == "1"
+        use_wgrad = self.knobs.on("wgrad")  # hand-written token-reduction GEMMs (csrc/wgrad.hip)
         tail = self._tail_backward_ok(bufs0)
         q = TailQueue(self, wgrad=use_wgrad) if tail else SumQueue(self.ops, wgrad=use_wgrad)
         self._tail_total_ok = False

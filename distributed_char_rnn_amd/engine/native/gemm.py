@@ -100,18 +100,23 @@ class SumQueue:
         return out
 
     def _run_gemms(self) -> None:
+        """The pending token-reduction GEMMs as hand-written wgrad launches: up to 4 problems of
+        one token count per launch, whatever their shapes (the step's layer-1 [2H x 4H] and
+        layer-0 [H x 4H] gradients share one grid), one split count for the launch."""
         groups = {}
         for a, b, out in self.gemms:
-            groups.setdefault((a.shape[1], b.shape[1], a.shape[0]), []).append((a, b, out))
+            groups.setdefault(a.shape[0], []).append((a, b, out))
         self.gemms = []
-        for (M, Nn, K), items in groups.items():
+        for K, items in groups.items():
             for i in range(0, len(items), 4):  # csrc/kernels.h kWgradMaxProblems
                 chunk = items[i: i + 4]
-                S = int(self.ops.wgrad_plan(len(chunk), M, Nn, K))
-                part = torch.empty(len(chunk), S, M, Nn, dtype=f32, device=chunk[0][0].device)
-                self.ops.wgrad([c[0] for c in chunk], [c[1] for c in chunk], part)
-                for j, (_, _, out) in enumerate(chunk):
-                    self.add_sum(part[j], out)
+                tiles = sum((a.shape[1] // 256) * (b.shape[1] // 256) for a, b, _ in chunk)
+                S = int(self.ops.wgrad_plan_tiles(tiles, K))
+                parts = [torch.empty(S, a.shape[1], b.shape[1], dtype=f32, device=a.device)
+                         for a, b, _ in chunk]
+                self.ops.wgrad([c[0] for c in chunk], [c[1] for c in chunk], parts)
+                for part, (_, _, out) in zip(parts, chunk):
+                    self.add_sum(part, out)
 
     def add_sum(self, part: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         self.tasks.append((part, out, self.SUM))

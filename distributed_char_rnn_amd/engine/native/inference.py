@@ -34,8 +34,11 @@ class InferenceMixin:
 
     @torch.no_grad()
     def sample_sequence(self, prime_ids, num: int, sampling_type: int, seed: int, num_samples: int,
-                        space_id: int = -1, use_graph: bool = True):
+                        space_id: int = -1, use_graph: bool = True, use_generator: bool = True):
         """Device-side autoregressive sampling (model.py:105-140); returns [S][num] ids.
+
+        LSTM models take the single-launch generator (``generate``); otherwise, or with
+        ``use_generator=False``:
 
         Every generated character is [recurrent step kernels of all layers, ``dcr::sample_step``]
         (csrc/sample.hip: softmax head + argmax / inverse-CDF draw, the pick written straight
@@ -47,6 +50,8 @@ class InferenceMixin:
         S = num_samples
         if num <= 0:
             return [[] for _ in range(S)]
+        if use_generator and self._generate_ok(S):
+            return self.generate(prime_ids, num, sampling_type, seed, S, space_id)[0]
         if not self.ops.sample_supported(self.V, self.H):
             return self._sample_sequence_torch(prime_ids, num, sampling_type, seed, S, space_id)
         state = zero_state(self.cfg, S, self.dev)
@@ -88,6 +93,45 @@ class InferenceMixin:
                 else:
                     one()
         return out.cpu().tolist()
+
+    def _generate_ok(self, S: int) -> bool:
+        """The single-launch generator (csrc/generate.hip) covers LSTM stacks of up to 4 layers
+        with H a multiple of 128 up to 4 x the CU count, up to 16 streams."""
+        return (self.cfg.model == "lstm" and self.knobs.on("generate")
+                and bool(self.ops.generate_supported(self.L, self.H, self.V, S)))
+
+    @torch.no_grad()
+    def generate(self, prime_ids, num: int, sampling_type: int, seed: int, S: int = 1,
+                 space_id: int = -1, want_logits: bool = False):
+        """Every character of Model.sample (model.py:105-140) in ONE launch: the recurrence of
+        all layers, the softmax head and the draw, with the weights resident in LDS across the
+        grid (csrc/generate.hip); prime[:-1] warms the zero state inside the launch.  Returns
+        (ids [S][num], final state, logits [num, S, V] or None)."""
+        from .forward import FORGET_BIAS
+
+        self._run_prep(self._prep())  # weight layouts + the layer-0 gather table current
+        hd, dev, L, H = self._head, self.dev, self.L, self.H
+        if self._head.get("WsT_gen") is None or self._gen_ver != self._wver:
+            self._head["WsT_gen"] = hd["Ws"].t().contiguous()
+            self._gen_ver = self._wver
+        f32 = dict(dtype=torch.float32, device=dev)
+        h0 = torch.zeros(L, S, H, **f32)
+        c0 = torch.zeros(L, S, H, **f32)
+        h1, c1 = torch.empty_like(h0), torch.empty_like(c0)
+        prime = torch.tensor([int(i) for i in prime_ids], dtype=torch.int32, device=dev)
+        out = torch.empty(S, num, dtype=torch.int32, device=dev)
+        hx = torch.empty(L * 2 * S * H, dtype=torch.int64, device=dev)
+        ctr0 = torch.zeros(S, dtype=torch.int32, device=dev)
+        lg = torch.empty(num, S, self.V, **f32) if want_logits else None
+        w = self._w
+        self.ops.generate([lw.Wh for lw in w], [lw.Wx for lw in w], [lw.bias for lw in w],
+                          hd["table"], hd["WsT_gen"], hd["bs"], FORGET_BIAS, h0, c0, h1, c1,
+                          prime, int(num), out, hx, int(sampling_type), int(space_id),
+                          int(seed) & ((1 << 63) - 1), ctr0, lg, self.err, self.spin_limit)
+        ids = out.cpu().tolist()
+        self.check_errors()
+        state = [(c1[l], h1[l]) for l in range(L)]
+        return ids, state, lg
 
     @torch.no_grad()
     def _sample_sequence_torch(self, prime_ids, num, sampling_type, seed, S, space_id):

@@ -41,6 +41,12 @@ class LayoutsMixin:
                 and self.V <= SEG_LDS_MAX_V and not getattr(self, "padded_inner", False)
                 and int(self.ops.tail_grid()) > 0)
 
+    def tail_dynamic(self) -> bool:
+        """Tail launches hand out tiles through an atomic queue unless the GPU is this
+        process's alone (the persistent recurrence's assumption): then static tiles, with no
+        queue traffic (DCR_DEBUG=tail_queue=1 forces the queue)."""
+        return not self.knobs.persistent or self.knobs.dbg("tail_queue", "0") == "1"
+
     def bind_optimizer(self, opt) -> None:
         if self.tail_adam_ok() and opt.mirror is None and opt.native:
             opt.fused = self
@@ -58,14 +64,26 @@ class LayoutsMixin:
         s = self.store
         n = s.norm_slot
         n_norm, use_slot = s.norm_terms()
-        total = self._tail_total if (self._tail_total_ok and grad_scale == 1.0) else None
+        total = self._tail_total if self._tail_total_ok else None
         self._tail_total_ok = False
+        if total is None:
+            # the gradients changed since the finalize (data-parallel exchange): one
+            # sum-of-squares launch over g[0, n_norm) (+ the slot) first
+            if self._adam_sq is None:
+                self._adam_sq = (torch.empty(int(self.ops.opt_num_partials(max(n_norm, 1))),
+                                             dtype=f32, device=self.dev),
+                                 torch.zeros(1, dtype=torch.int32, device=self.dev),
+                                 torch.zeros(1, dtype=f32, device=self.dev))
+            part, ticket, total = self._adam_sq
+            self.ops.sumsq(s.grad.narrow(0, 0, n_norm), part, total, ticket,
+                           s.norm_slot_view() if use_slot else None, None)
         tailmod.run(self.ops, self._adam_tab, 1, self._adam_ws, self.err, self.spin_limit,
-                    total_in=total, extra=s.norm_slot_view() if use_slot else None,
+                    total_in=total,
                     p=s.flat.narrow(0, 0, n), g=s.grad.narrow(0, 0, n), m=opt.m.narrow(0, 0, n),
                     v=opt.v.narrow(0, 0, n), mirror=self._mirror, n_norm=n_norm, lr_t=lr_t,
                     b1=opt.b1, b2=opt.b2, eps=opt.eps, clip=opt.clip, gscale=float(grad_scale),
-                    lr_dev=lr_dev, skip_if=opt.guard, norm_out=opt.last_norm)
+                    lr_dev=lr_dev, skip_if=opt.guard, norm_out=opt.last_norm,
+                    dynamic=self.tail_dynamic())
         return True
 
     def fused_adam_done(self) -> None:
@@ -110,8 +128,9 @@ class LayoutsMixin:
             outs.append((hd["WsTw"], H, True))
         region("rnnlm/softmax_w", outs=outs)
         region("rnnlm/softmax_b")
-        if cover != s.norm_slot:
-            raise AssertionError(f"fused Adam covers {cover} of {s.norm_slot} parameters")
+        want = sum(sp.numel for sp in s.specs)  # (alignment padding between tensors: no params)
+        if cover != want:
+            raise AssertionError(f"fused Adam covers {cover} of {want} parameters")
         if table:
             GW = w0.Wx32.shape[1]
             tab.mm(hd["table"], hd["E"], (H, 1), w0.Wx32, (GW, 1), D, bias=w0.bias, wait=0)
@@ -129,6 +148,7 @@ class LayoutsMixin:
         # own pass (the prep tasks below still fill them after any other parameter change)
         self._mirror = e(s.numel) if self.tail_adam_ok() else None
         self._adam_tab = None
+        self._adam_sq = None
         mv = (lambda name: s.view(name, self._mirror)) if self._mirror is not None else None
         for layer in range(self.L):
             names = [sp.name for sp in cell_specs(self.cfg, layer)]

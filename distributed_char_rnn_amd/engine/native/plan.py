@@ -56,6 +56,8 @@ DEBUG_KEYS = {
     "bigstep_s": "n: force n split-K slices in the fused large-H step kernels",
     "bigstep_cfg": "id: force tile configuration id of the fused large-H step kernels (C++)",
     "sample_graph": "0: eager sampling loop (no hipGraph replay)",
+    "generate": "0: sampling as the replayed per-character step graph instead of the "
+                "single-launch generator (csrc/generate.hip)",
     "head_omask": "0: top output dropout applied to dtop by a separate pass, not the head",
     "xin": "0: library zx GEMM for a dense layer-l input instead of the G = 1 two-layer "
            "forward's in-kernel projection",
@@ -68,11 +70,14 @@ DEBUG_KEYS = {
     "nt_poll": "w: hand-off poller on wave w in the H > 1024 persistent kernels (C++ launcher)",
     "nt_dma": "0: H > 1024 persistent forward at NT = 4 streams its h tiles through registers "
               "instead of LDS-DMA (C++ launcher)",
-    "wgrad": "1: hand-written wgrad kernel for the weight gradients (default: library split-K)",
+    "wgrad": "0: library split-K GEMMs for the weight gradients instead of the hand-written "
+             "wgrad kernel (csrc/wgrad.hip)",
     "tokennorm": "0: TF token-norm term as a library GEMM to bf16 rows + a sumsq launch instead "
                  "of the fused MFMA kernel (csrc/tokennorm.hip)",
     "tail": "0: no fused step tail (csrc/tail.hip): prep-launch slab flush, library fp32 "
             "products, separate norm / Adam / weight-layout launches",
+    "tail_queue": "1: tail launches take tiles from the atomic queue even on an unshared GPU",
+    "tail_per": "N: tail workgroups per CU (C++, default 2)",
     "gru_ub": "1: 16-unit GRU workgroups (C++)",
     "gru_nt": "N: N batch tiles of 16 rows per GRU workgroup (C++)",
     "step_nbt": "1/2/4: batch tiles per per-step workgroup (C++)",

@@ -13,14 +13,16 @@ import torch
 
 SUM, COLSUM, SUMSQ, MM, ADAM = 0, 1, 2, 3, 4
 TAIL_WORDS = 27
-MM_SHORT_K = 128  # csrc/tail.hip: MM with k <= 128 runs 64 x 64 VALU tiles, longer k fp32 MFMA
+MM_SHORT_K = 128  # csrc/tail.hip: MM with k <= 128 runs LDS-staged 64 x 64 tiles, longer k 16 x 16
+MAX_DEPS = 4      # csrc/kernels.h kTailMaxDeps
+MM_ROWS = 80      # csrc/tail.hip kMmRows: rows per long-MM tile
 
 
 def _a16(t: torch.Tensor) -> bool:
     return t.data_ptr() % 16 == 0
 
 
-def task_tiles(op: int, rows: int, cols: int, k: int) -> int:
+def task_tiles(op: int, rows: int, cols: int, k: int, nslab: int = 0) -> int:
     """Tiles of one task (csrc/tail.hip tail_tiles)."""
     if op in (SUM, ADAM):
         return -(-rows // 64) * -(-cols // 64)
@@ -29,7 +31,9 @@ def task_tiles(op: int, rows: int, cols: int, k: int) -> int:
     if op == SUMSQ:
         return -(-(rows * cols) // 4096)
     if op == MM:
-        return (-(-rows // 64) * -(-cols // 64)) if k <= MM_SHORT_K else (-(-rows // 16) * -(-cols // 16))
+        if k <= MM_SHORT_K:
+            return -(-rows // 64) * -(-cols // 64)
+        return max(nslab, 1) * -(-rows // MM_ROWS) * -(-cols // 16)
     raise ValueError(op)
 
 
@@ -55,7 +59,7 @@ class TailTable:
             need = self.sig_tiles.get(wait, 0)
             if need <= 0:
                 raise ValueError(f"tail table: nothing signals counter {wait} before this task")
-        nt = task_tiles(op, rows, cols, k)
+        nt = task_tiles(op, rows, cols, k, nslab)
         if sig >= 0:
             self.sig_tiles[sig] = self.sig_tiles.get(sig, 0) + nt
         self.words += [op, rows, cols, int(norm), wait, need, sig, int(vec4), nslab, k, o1_t, o2_t,
@@ -65,14 +69,23 @@ class TailTable:
         self.tiles.append(nt)
 
     # ---- FINALIZE ----------------------------------------------------------------------------
-    def sum(self, part: torch.Tensor, out: torch.Tensor, norm: bool, sig: int = -1):
+    def sum(self, part: torch.Tensor, out: torch.Tensor, norm: bool, sig: int = -1,
+            wait: int = -1):
         """out [rows, cols] = sum over the slabs of part [S, rows, cols] (fp32)."""
         assert part.dim() == 3 and out.dim() == 2 and part.stride(2) == 1 and out.stride(1) == 1
         assert tuple(part.shape[1:]) == tuple(out.shape) and part.dtype == out.dtype == torch.float32
         S, rows, cols = part.shape
+        n = rows * cols
+        if (part.stride(1) == cols and out.stride(0) == cols and n % 256 == 0
+                and part.stride(0) % 4 == 0 and _a16(part) and _a16(out)):
+            # contiguous rows (e.g. softmax_w [H, 65]): summed as [n / 256, 256] float4 tiles
+            # instead of the odd-width scalar path
+            part = part.as_strided((S, n // 256, 256), (part.stride(0), 256, 1))
+            out = out.view(-1).view(n // 256, 256)
+            rows, cols = n // 256, 256
         vec4 = (cols % 4 == 0 and part.stride(1) % 4 == 0 and part.stride(0) % 4 == 0
                 and out.stride(0) % 4 == 0 and _a16(part) and _a16(out))
-        self._add(SUM, rows, cols, norm=norm, sig=sig, vec4=vec4, nslab=S, a=part.data_ptr(),
+        self._add(SUM, rows, cols, norm=norm, sig=sig, wait=wait, vec4=vec4, nslab=S, a=part.data_ptr(),
                   ar=part.stride(1), ak=part.stride(0), dst=out.data_ptr(), dst_ld=out.stride(0),
                   keep=(part, out))
 
@@ -90,18 +103,30 @@ class TailTable:
 
     def mm(self, out: torch.Tensor, a: torch.Tensor, a_strides, b: torch.Tensor, b_strides,
            k: int, bias: Optional[torch.Tensor] = None, norm: bool = False, wait: int = -1,
-           sig: int = -1):
-        """out[r, c] = bias[c] + sum_k a[r ar + k ak] * b[k bk + c bc] (fp32)."""
+           sig: int = -1, slabs: Optional[torch.Tensor] = None, slab_sig: int = -1):
+        """out[r, c] = bias[c] + sum_k a[r ar + k ak] * b[k bk + c bc] (fp32).  ``slabs``
+        ([S, rows, cols] fp32, S > 1, k > MM_SHORT_K): the reduction split into S k-slabs over
+        more workgroups, written there and signalled on ``slab_sig``; a SUM task waiting on it
+        adds them into ``out`` in slab order."""
         assert out.dim() == 2 and out.stride(1) == 1 and out.dtype == torch.float32
         ar, ak = a_strides
         bk, bc = b_strides
         rows, cols = out.shape
         # every element the strides address lies inside the operands
         assert (rows - 1) * ar + (k - 1) * ak < a.numel() and (k - 1) * bk + (cols - 1) * bc < b.numel()
-        self._add(MM, rows, cols, norm=norm, wait=wait, sig=sig, k=k, a=a.data_ptr(), ar=ar, ak=ak,
-                  b=b.data_ptr(), bk=bk, bc=bc, bias=0 if bias is None else bias.data_ptr(),
-                  dst=out.data_ptr(), dst_ld=out.stride(0),
-                  keep=(out, a, b) + (() if bias is None else (bias,)))
+        ops = dict(k=k, a=a.data_ptr(), ar=ar, ak=ak, b=b.data_ptr(), bk=bk, bc=bc,
+                   bias=0 if bias is None else bias.data_ptr())
+        keep = (out, a, b) + (() if bias is None else (bias,))
+        if slabs is None:
+            self._add(MM, rows, cols, norm=norm, wait=wait, sig=sig, dst=out.data_ptr(),
+                      dst_ld=out.stride(0), keep=keep, **ops)
+            return
+        S = slabs.shape[0]
+        assert (S > 1 and k > MM_SHORT_K and slab_sig >= 0 and slabs.is_contiguous()
+                and tuple(slabs.shape) == (S, rows, cols) and slabs.dtype == torch.float32)
+        self._add(MM, rows, cols, wait=wait, sig=slab_sig, nslab=S, dst=slabs.data_ptr(),
+                  dst_ld=cols, off=rows * cols, keep=keep + (slabs,), **ops)
+        self.sum(slabs, out, norm, sig=sig, wait=slab_sig)
 
     # ---- ADAM --------------------------------------------------------------------------------
     def adam(self, off: int, rows: int, cols: int, ld: int, outs=(), sig: int = -1,
@@ -125,17 +150,21 @@ def run(ops, table: TailTable, phase: int, ws: dict, err: torch.Tensor, spin_lim
         total_out=None, total_in=None, extra=None, p=None, g=None, m=None, v=None, mirror=None,
         n_norm: int = 0, lr_t: float = 0.0, b1: float = 0.9, b2: float = 0.999,
         eps: float = 1e-8, clip: float = 0.0, gscale: float = 1.0, lr_dev=None, skip_if=None,
-        norm_out=None):
+        norm_out=None, dynamic: bool = True):
+    """``dynamic``: atomic tile queue, safe when the grid is not co-resident (another process
+    on the GPU); False: static tiles, for a GPU this process has alone (the persistent
+    recurrence's assumption, csrc/tail.hip)."""
     ops.tail(table.words, phase, ws["part"], ws["sync"], ws["dep"], err, spin_limit, total_out,
              total_in, extra, p, g, m, v, mirror, n_norm, lr_t, b1, b2, eps, clip, gscale, lr_dev,
-             skip_if, norm_out)
+             skip_if, norm_out, dynamic)
 
 
 def workspace(ops, device) -> dict:
     """Per-workgroup partials and the (zeroed, self-resetting) ticket / dependency counters."""
-    return dict(part=torch.zeros(1024, dtype=torch.float32, device=device),
-                sync=torch.zeros(4, dtype=torch.int32, device=device),
-                dep=torch.zeros(4, dtype=torch.int32, device=device))
+    n_sync, n_dep = (int(w) for w in ops.tail_ws_words())
+    return dict(part=torch.zeros(16384, dtype=torch.float32, device=device),
+                sync=torch.zeros(n_sync, dtype=torch.int32, device=device),
+                dep=torch.zeros(n_dep, dtype=torch.int32, device=device))
 
 
 class TailQueue:
@@ -189,6 +218,23 @@ class TailQueue:
         self.mms.append((out, a, a_strides, b, b_strides, k, wait))
         return out
 
+    @staticmethod
+    def _mm_slabs(rows: int, cols: int, k: int, grid: int) -> int:
+        """k-slabs for a long-reduction MM whose 16 x 16 tiles alone would leave most of the
+        grid idle (dE = dEW·W_x0ᵀ: 160 tiles of k = 2048): about one tile per workgroup, at
+        least 256 k per slab."""
+        if k <= MM_SHORT_K:
+            return 1
+        tiles = -(-rows // MM_ROWS) * -(-cols // 16)
+        return max(1, min(grid // max(tiles, 1), k // 64, 8))
+
+    def _slab_buf(self, S: int, rows: int, cols: int) -> torch.Tensor:
+        bufs = self.be.__dict__.setdefault("_tail_slabs", {})
+        key = (S, rows, cols)
+        if key not in bufs:
+            bufs[key] = torch.empty(S, rows, cols, dtype=torch.float32, device=self.be.dev)
+        return bufs[key]
+
     def _norm_range(self, out: torch.Tensor):
         """(flat offset, elements) of a gradient view inside the norm prefix, else None."""
         s = self.be.store
@@ -236,26 +282,42 @@ class TailQueue:
         for x in self.sumsqs:
             if norm_of(x):  # (outside the norm prefix: nothing to do)
                 tab.sumsq(x)
+        grid = int(self.ops.tail_grid())
         for out, a, sa, b, sb, k, wait in self.mms:
-            tab.mm(out, a, sa, b, sb, k, norm=norm_of(out), wait=wait)
+            # (a producer that did not become a slab sum of this launch -- a GEMM short enough
+            # to run unsplit -- wrote its output in stream order before it: nothing to wait for)
+            wait = wait if tab.sig_tiles.get(wait, 0) > 0 else -1
+            S = self._mm_slabs(out.shape[0], out.shape[1], k, grid)
+            if S > 1 and len(tab) + 2 <= tab.max_tasks and len(tab.sig_tiles) < MAX_DEPS:
+                c = min(set(range(MAX_DEPS)) - set(tab.sig_tiles))
+                tab.mm(out, a, sa, b, sb, k, norm=norm_of(out), wait=wait,
+                       slabs=self._slab_buf(S, *out.shape), slab_sig=c)
+            else:
+                tab.mm(out, a, sa, b, sb, k, norm=norm_of(out), wait=wait)
         self.sums, self.colsums, self.sumsqs, self.mms = [], [], [], []
         if not len(tab):
             return False
         ok = False
         if total_out is not None:
+            # every parameter inside the norm prefix must be an output of this launch (the
+            # alignment padding between tensors holds zero gradients: gaps there are fine)
             n_norm, _ = be.store.norm_terms()
             spans.sort()
-            pos = 0
-            ok = True
-            for off, n in spans:
-                ok &= off == pos
-                pos = off + n
-            ok &= pos == n_norm
+            ok = all(b[0] >= a[0] + a[1] for a, b in zip(spans, spans[1:]))  # no overlaps
+            merged = []
+            for o, n in spans:
+                if merged and merged[-1][0] + merged[-1][1] == o:
+                    merged[-1] = (merged[-1][0], merged[-1][1] + n)
+                else:
+                    merged.append((o, n))
+            covered = lambda lo, hi: any(o <= lo and hi <= o + n for o, n in merged)  # noqa: E731
+            ok = ok and all(covered(sp.offset, sp.offset + sp.numel) for sp in be.store.specs
+                            if sp.offset < n_norm)
         if getattr(be, "_fin_ws", None) is None:
             be._fin_ws = workspace(self.ops, be.dev)
         s = be.store
         _, use_slot = s.norm_terms()
         run(self.ops, tab, 0, be._fin_ws, be.err, be.spin_limit,
             total_out=total_out if ok else None,
-            extra=s.norm_slot_view() if (ok and use_slot) else None)
+            extra=s.norm_slot_view() if (ok and use_slot) else None, dynamic=be.tail_dynamic())
         return ok

@@ -35,9 +35,59 @@ State = List[Tuple[torch.Tensor, ...]]
 LSTM_FORGET_BIAS = 1.0
 
 
+class _RoundGrad(torch.autograd.Function):
+    """Identity forward; the incoming gradient rounded to bf16 (the native backward stores the
+    pre-activation gradient dZ in bf16 before its GEMMs)."""
+
+    @staticmethod
+    def forward(ctx, z):
+        return z.view_as(z)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).float()
+
+
+class _RoundVal(torch.autograd.Function):
+    """Operand rounded to bf16 forward (the MFMA operands); gradient passed through."""
+
+    @staticmethod
+    def forward(ctx, a):
+        return a.to(torch.bfloat16).float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+_BF16_OPERANDS = [False]
+
+
+def _mm(a, b):
+    """Every GEMM of the oracle.  Under :func:`bf16_operands` both operands are rounded to bf16
+    and the product's incoming gradient too: fp32 math on exactly the operands the native
+    kernels feed their bf16 MFMAs, which separates kernel error from operand rounding."""
+    if not _BF16_OPERANDS[0]:
+        return a @ b
+    return _RoundGrad.apply(_RoundVal.apply(a) @ _RoundVal.apply(b))
+
+
+class bf16_operands:
+    """Context manager: the oracle's GEMMs take bf16-rounded operands (see :func:`_mm`)."""
+
+    def __enter__(self):
+        self._prev = _BF16_OPERANDS[0]
+        _BF16_OPERANDS[0] = True
+        return self
+
+    def __exit__(self, *exc):
+        _BF16_OPERANDS[0] = self._prev
+        return False
+
+
 def lstm_cell(x, state, kernel, bias):
     c, h = state
-    z = torch.cat([x, h], 1) @ kernel + bias
+    z = _mm(torch.cat([x, h], 1), kernel) + bias
     i, j, f, o = z.chunk(4, 1)
     c2 = torch.sigmoid(f + LSTM_FORGET_BIAS) * c + torch.sigmoid(i) * torch.tanh(j)
     h2 = torch.sigmoid(o) * torch.tanh(c2)
@@ -47,16 +97,16 @@ def lstm_cell(x, state, kernel, bias):
 def gru_cell(x, state, gk, gb, ck, cb):
     (h,) = state
     H = h.shape[1]
-    rv = torch.sigmoid(torch.cat([x, h], 1) @ gk + gb)
+    rv = torch.sigmoid(_mm(torch.cat([x, h], 1), gk) + gb)
     r, u = rv[:, :H], rv[:, H:]
-    c = torch.tanh(torch.cat([x, r * h], 1) @ ck + cb)
+    c = torch.tanh(_mm(torch.cat([x, r * h], 1), ck) + cb)
     h2 = u * h + (1 - u) * c
     return h2, (h2,)
 
 
 def rnn_cell(x, state, kernel, bias):
     (h,) = state
-    h2 = torch.tanh(torch.cat([x, h], 1) @ kernel + bias)
+    h2 = torch.tanh(_mm(torch.cat([x, h], 1), kernel) + bias)
     return h2, (h2,)
 
 
@@ -89,7 +139,7 @@ def nas_pointwise(p, c_prev):
 
 def nas_cell(x, state, kernel, recurrent_kernel):
     c, m = state
-    p = nas_preacts(x @ kernel, m @ recurrent_kernel)
+    p = nas_preacts(_mm(x, kernel), _mm(m, recurrent_kernel))
     new_c, new_m = nas_pointwise(p, c)
     return new_m, (new_c, new_m)
 
@@ -149,7 +199,7 @@ def forward(cfg: ModelConfig, params: dict, x: torch.Tensor, state: State, train
             inp = out
         outs.append(inp)
     out = torch.stack(outs, 1)  # [B, T, H]
-    logits = out.reshape(B * T, -1) @ params["rnnlm/softmax_w"] + params["rnnlm/softmax_b"]
+    logits = _mm(out.reshape(B * T, -1), params["rnnlm/softmax_w"]) + params["rnnlm/softmax_b"]
     return logits, state, out
 
 
@@ -170,7 +220,7 @@ def _forward_masked(cfg, params, emb, state, masks):
             inp = inp * masks["out"][:, t]
         outs.append(inp)
     out = torch.stack(outs, 1)
-    logits = out.reshape(B * T, -1) @ params["rnnlm/softmax_w"] + params["rnnlm/softmax_b"]
+    logits = _mm(out.reshape(B * T, -1), params["rnnlm/softmax_w"]) + params["rnnlm/softmax_b"]
     return logits, state, out
 
 

@@ -150,7 +150,97 @@ __global__ void __launch_bounds__(512, 2) lab_kernel(LabArgs a) {
     barrier_raw();
     read_frags(kt0, fa0, fb0);
   }
+  constexpr bool IL = (VAR & 16) != 0;
+  auto mf = [&](int g, u32x4 (&fa)[8], u32x4 (&fb)[4]) {  // MFMA group g: rows 2g, 2g+1
+#pragma unroll
+    for (int ii = 2 * g; ii < 2 * g + 2; ++ii)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        acc[ii][jj] = mfma16(__builtin_bit_cast(bf16x8, fa[ii]), __builtin_bit_cast(bf16x8, fb[jj]), acc[ii][jj]);
+  };
+  auto rd_a = [&](int kt, u32x4 (&fa)[8], int i0, int i1) {
+    const unsigned base = lds0 + ((kt - kt0) % ST) * kStageB;
+#pragma unroll
+    for (int i = i0; i < i1; ++i) {
+      const u32x2 lo = rd_tr(base + rowb[0] + ((xa[0] ^ (2u * i)) << 4));
+      const u32x2 hi = rd_tr(base + rowb[1] + ((xa[1] ^ (2u * i)) << 4));
+      fa[i] = u32x4{lo[0], lo[1], hi[0], hi[1]};
+    }
+  };
+  auto rd_b = [&](int kt, u32x4 (&fb)[4]) {
+    const unsigned base = lds0 + ((kt - kt0) % ST) * kStageB;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const u32x2 lo = rd_tr(base + kK * 512 + rowb[0] + ((xb[0] ^ (2u * j)) << 4));
+      const u32x2 hi = rd_tr(base + kK * 512 + rowb[1] + ((xb[1] ^ (2u * j)) << 4));
+      fb[j] = u32x4{lo[0], lo[1], hi[0], hi[1]};
+    }
+  };
+  auto kstep_il = [&](int i, u32x4 (&fa)[8], u32x4 (&fb)[4], u32x4 (&na)[8], u32x4 (&nb_)[4]) {
+    const int kt = kt0 + i;
+    const bool more = i + 1 < nk;
+    if (more) {
+      const int later = nk - 2 - i < ST - 2 ? nk - 2 - i : ST - 2;
+      vm_wait(later * kDmaPerWave);
+      barrier_raw();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mf(0, fa, fb);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more && i + ST < nk) issue(kt + ST);
+    __builtin_amdgcn_sched_barrier(0);
+    mf(1, fa, fb);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) { rd_b(kt + 1, nb_); rd_a(kt + 1, na, 0, 2); }
+    __builtin_amdgcn_sched_barrier(0);
+    mf(2, fa, fb);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) rd_a(kt + 1, na, 2, 8);
+    __builtin_amdgcn_sched_barrier(0);
+    mf(3, fa, fb);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  constexpr bool IL2 = (VAR & 32) != 0;
+  auto issue_part = [&](int kt, int j) {  // this wave's DMA pair j of stage kt
+    const unsigned st = lds0 + ((kt - kt0) % ST) * kStageB;
+    const unsigned sa = (unsigned)((size_t)kt * kK * P.lda * sizeof(bf16));
+    const unsigned sb = (unsigned)((size_t)kt * kK * P.ldb * sizeof(bf16));
+    const unsigned r = (unsigned)(kDmaPerWave * w + 2 * j);
+    dma(ra, st + r * 512, offa[j], sa);
+    dma(rb, st + kK * 512 + r * 512, offb[j], sb);
+  };
+  auto kstep_il2 = [&](int i, u32x4 (&fa)[8], u32x4 (&fb)[4], u32x4 (&na)[8], u32x4 (&nb_)[4]) {
+    const int kt = kt0 + i;
+    const bool more = i + 1 < nk;
+    const bool pf = more && i + ST < nk;
+    if (more) {
+      const int later = nk - 2 - i < ST - 2 ? nk - 2 - i : ST - 2;
+      vm_wait(later * kDmaPerWave);
+      barrier_raw();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(1);
+    mf(0, fa, fb);
+    __builtin_amdgcn_sched_barrier(0);
+    if (pf) issue_part(kt + ST, 0);
+    if (more) rd_b(kt + 1, nb_);
+    __builtin_amdgcn_sched_barrier(0);
+    mf(1, fa, fb);
+    __builtin_amdgcn_sched_barrier(0);
+    if (pf) issue_part(kt + ST, 1);
+    if (more) rd_a(kt + 1, na, 0, 3);
+    __builtin_amdgcn_sched_barrier(0);
+    mf(2, fa, fb);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) rd_a(kt + 1, na, 3, 8);
+    __builtin_amdgcn_sched_barrier(0);
+    mf(3, fa, fb);
+    if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
   auto kstep = [&](int i, u32x4 (&fa)[8], u32x4 (&fb)[4], u32x4 (&na)[8], u32x4 (&nb_)[4]) {
+    if constexpr (IL2) { kstep_il2(i, fa, fb, na, nb_); return; }
+    if constexpr (IL) { kstep_il(i, fa, fb, na, nb_); return; }
     const int kt = kt0 + i;
     if (i + 1 < nk) {
       const int later = nk - 2 - i < ST - 2 ? nk - 2 - i : ST - 2;
@@ -233,8 +323,9 @@ int main() {
 
   Variant vars[] = {
       {"v2", lab_kernel<0>, 4},         {"prio-static", lab_kernel<1>, 4},
-      {"prio-cluster", lab_kernel<2>, 4}, {"5stage", lab_kernel<4>, 5},
-      {"5stage+prio-static", lab_kernel<5>, 5},
+      {"prio-cluster", lab_kernel<2>, 4},
+      {"interleave", lab_kernel<16>, 4},  {"interleave2", lab_kernel<32>, 4},
+      {"interleave2+prio-static", lab_kernel<33>, 4}, {"interleave2+prio-cluster", lab_kernel<34>, 4},
   };
   const int nv = sizeof(vars) / sizeof(vars[0]);
   for (auto& v : vars)

@@ -38,10 +38,10 @@ for M, N in ((1024, 2048), (512, 2048), (2048, 8192), (1024, 3072)):
     b3 = B.unflatten(0, (S, K // S))
     t_lib = timeit(lambda: torch.bmm(a3, b3, out_dtype=f32))
     Sw = int(ops.wgrad_plan(1, M, N, K))
-    part = torch.empty(1, Sw, M, N, device="cuda")
-    t_wg = timeit(lambda: ops.wgrad([A], [B], part))
+    part = torch.empty(Sw, M, N, device="cuda")
+    t_wg = timeit(lambda: ops.wgrad([A], [B], [part]))
     ref = A.float().t() @ B.float()
-    err = ((part[0].sum(0) - ref).norm() / ref.norm()).item()
+    err = ((part.sum(0) - ref).norm() / ref.norm()).item()
     print(f"[{M} x {N}] K={K}: library S={S} {t_lib:7.1f} us ({fl / t_lib / 1e6:5.0f} TF/s)   "
           f"wgrad S={Sw} {t_wg:7.1f} us ({fl / t_wg / 1e6:5.0f} TF/s)   rel err {err:.1e}",
           flush=True)

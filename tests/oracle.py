@@ -26,10 +26,11 @@ import torch
 # test key -> (rel tolerance, block tolerance); measured maxima in profiles/r4_oracle_errors.md
 TOL = {
     "native_model": (1.4e-2, 1.6e-2),
-    # the NAS cell: its nested gate compositions (8 pre-activations per unit) amplify the bf16
-    # operand rounding far more than LSTM / GRU / RNN cells do; the error grows towards layer 0
-    # and the embedding (5.8e-2 measured at L = 3)
-    "native_model_nas": (1.2e-1, 1.6e-1),
+    # the NAS cell against the oracle on bf16-rounded GEMM operands (against the fp32 oracle
+    # bf16 operand rounding alone moves NAS gradients by ~8e-2: tests/test_native_model.py
+    # test_cell_error_is_bf16_operand_rounding, 7.6e-2 vs 3.3e-3 measured at L = 3); measured
+    # maxima 8.6e-3 / 1.66e-2 (test_per_step_batch_tiles_match_reference, embedding rows)
+    "native_model_nas": (1.7e-2, 3.3e-2),
     "native_model_lib": (1.1e-2, 1.3e-2),
     "persist": (1.1e-2, 1.2e-2),
     "persist_nt": (1.1e-2, 1.2e-2),

@@ -193,3 +193,23 @@ def test_tf_adam_grad_scale_equals_averaged_gradient():
     nb = ob.step(1e-2, grad_scale=0.25)
     torch.testing.assert_close(nb, na)
     torch.testing.assert_close(b.store.flat, a.store.flat)
+
+
+def test_bf16_operand_oracle_rounds_gemm_operands_and_dz():
+    """models/reference.py bf16_operands: fp32 GEMMs of bf16-rounded operands, a bf16-rounded
+    incoming gradient, and the switch restored on exit."""
+    from distributed_char_rnn_amd.models import reference as R
+
+    g = torch.Generator().manual_seed(0)
+    a = torch.randn(8, 16, generator=g, requires_grad=True)
+    b = torch.randn(16, 4, generator=g, requires_grad=True)
+    up = torch.randn(8, 4, generator=g)
+    with R.bf16_operands():
+        out = R._mm(a, b)
+        out.backward(up)
+    ab, bb, ub = (t.detach().bfloat16().float() for t in (a, b, up))
+    assert torch.equal(out, ab @ bb)
+    torch.testing.assert_close(a.grad, ub @ bb.t())
+    torch.testing.assert_close(b.grad, ab.t() @ ub)
+    assert not R._BF16_OPERANDS[0]
+    assert torch.equal(R._mm(a, b), a @ b)

@@ -20,6 +20,18 @@ def rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
 
 
+def _oracle_ctx(model):
+    """NAS gradients are checked against the oracle on bf16-rounded GEMM operands: the fp32
+    oracle differs from ANY bf16-operand computation of NAS by ~8e-2 (its nested gate products
+    amplify operand rounding), while the native kernels sit 3e-3 from the rounded-operand oracle
+    (test_cell_error_is_bf16_operand_rounding measures both)."""
+    import contextlib
+
+    from distributed_char_rnn_amd.models.reference import bf16_operands
+
+    return bf16_operands() if model == "nas" else contextlib.nullcontext()
+
+
 def _pair(model, B, T, H, L, V=65, seed=0, **kw):
     cfg = ModelConfig(model=model, vocab_size=V, rnn_size=H, num_layers=L, **kw)
     nat = CharRNN(cfg, device="cuda", seed=seed)
@@ -36,7 +48,8 @@ def test_train_step_matches_reference(model, B, T, H, L):
     y = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
     st0 = [tuple(torch.randn(B, H, device="cuda") * 0.5 for _ in range(cfg.state_arity))
            for _ in range(L)]
-    loss_r, st_r, _ = ref.train_step(x, y, [tuple(s.clone() for s in t) for t in st0])
+    with _oracle_ctx(model):
+        loss_r, st_r, _ = ref.train_step(x, y, [tuple(s.clone() for s in t) for t in st0])
     g_ref = nat.store.grad.clone()
     nat.store.grad.zero_()
     loss_n, st_n, _ = nat.backend.train_step(x, y, [tuple(s.clone() for s in t) for t in st0])
@@ -168,7 +181,8 @@ def test_per_step_batch_tiles_match_reference(model, nbt, monkeypatch):
     y = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
     st0 = [tuple(torch.randn(B, H, device="cuda") * 0.5 for _ in range(cfg.state_arity))
            for _ in range(L)]
-    loss_r, _, _ = ref.train_step(x, y, [tuple(s.clone() for s in t) for t in st0])
+    with _oracle_ctx(model):
+        loss_r, _, _ = ref.train_step(x, y, [tuple(s.clone() for s in t) for t in st0])
     g_ref = nat.store.grad.clone()
     nat.store.grad.zero_()
     loss_n, _, _ = nat.backend.train_step(x, y, [tuple(s.clone() for s in t) for t in st0])
@@ -203,3 +217,41 @@ def test_library_step_lstm_path_matches_reference(B, T, H, L, monkeypatch):
         for s_r, s_n in zip(a_r, a_n):
             assert rel(s_n, s_r) < 3e-2
     check_grads("native_model_lib", nat.store, nat.store.grad, g_ref)
+
+
+@pytest.mark.parametrize("model", ["nas", "lstm"])
+def test_cell_error_is_bf16_operand_rounding(model):
+    """Where the native error against the fp32 oracle comes from: the same oracle with every GEMM
+    fed bf16-rounded operands (and a bf16 dZ, models/reference.py bf16_operands) -- fp32 math on
+    the operands the kernels' MFMAs see -- must sit much closer to the native gradients than the
+    fp32 oracle does.  For NAS this is what justifies its looser fp32-oracle tolerance."""
+    from oracle import block_err
+    from distributed_char_rnn_amd.models.reference import bf16_operands
+
+    B, T, H, L = 48, 4, 96, 3
+    torch.manual_seed(0)
+    cfg, nat, ref = _pair(model, B, T, H, L)
+    x = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
+    y = torch.randint(0, 65, (B, T), device="cuda", dtype=torch.int32)
+    st0 = [tuple(torch.randn(B, H, device="cuda") * 0.5 for _ in range(cfg.state_arity))
+           for _ in range(L)]
+    cp = lambda: [tuple(s.clone() for s in t) for t in st0]  # noqa: E731
+    ref.train_step(x, y, cp())
+    g_f = nat.store.grad.clone()
+    with bf16_operands():
+        ref.train_step(x, y, cp())
+    g_e = nat.store.grad.clone()
+    nat.store.grad.zero_()
+    nat.backend.train_step(x, y, cp())
+    torch.cuda.synchronize()
+    g_n = nat.store.grad.clone()
+    worst_f = worst_e = 0.0
+    for s in nat.store.specs:
+        n, f, e = (nat.store.view(s.name, g) for g in (g_n, g_f, g_e))
+        ef, ee = max(rel(n, f), block_err(n, f)), max(rel(n, e), block_err(n, e))
+        print(f"{model} {s.name}: vs fp32 {ef:.2e}  vs bf16-operand oracle {ee:.2e}")
+        worst_f, worst_e = max(worst_f, ef), max(worst_e, ee)
+    print(f"{model} worst: vs fp32 {worst_f:.2e}  vs bf16-operand oracle {worst_e:.2e}")
+    assert worst_e < 2e-2, worst_e
+    if model == "nas":
+        assert worst_e < worst_f / 3, (worst_e, worst_f)

@@ -95,10 +95,11 @@ def test_sample_sequence_graph_equals_eager(model, S):
     cfg = ModelConfig(model=model, vocab_size=65, rnn_size=128, num_layers=2)
     m = CharRNN(cfg, device="cuda", seed=1)
     be = m.backend
-    a = be.sample_sequence([3, 7, 1], 40, 1, seed=99, num_samples=S, space_id=0, use_graph=True)
-    b = be.sample_sequence([3, 7, 1], 40, 1, seed=99, num_samples=S, space_id=0, use_graph=False)
+    kw = dict(num_samples=S, space_id=0, use_generator=False)
+    a = be.sample_sequence([3, 7, 1], 40, 1, seed=99, use_graph=True, **kw)
+    b = be.sample_sequence([3, 7, 1], 40, 1, seed=99, use_graph=False, **kw)
     assert a == b
     assert len(a) == S and all(len(r) == 40 for r in a)
     assert all(0 <= c < 65 for r in a for c in r)
-    c = be.sample_sequence([3, 7, 1], 40, 1, seed=100, num_samples=S, space_id=0)
+    c = be.sample_sequence([3, 7, 1], 40, 1, seed=100, **kw)
     assert c != a  # a different seed draws a different sequence

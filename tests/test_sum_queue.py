@@ -1,5 +1,5 @@
 """SumQueue (engine/native/gemm.py) deferral logic on the CPU with a stand-in op table: weight
-GEMMs the wgrad kernel covers are grouped by shape into one launch (at most 4 problems), each
+GEMMs the wgrad kernel covers are grouped by token count into one launch (at most 4 problems), each
 problem's split-K slabs become one SUM task of the flush, everything else runs immediately."""
 import torch
 
@@ -15,14 +15,16 @@ class FakeOps:
     def wgrad_plan(self, np_, M, N, K):
         return 0 if (M % 256 or N % 256 or K % 32) else 2
 
-    def wgrad(self, As, Bs, part):
+    def wgrad_plan_tiles(self, tiles, K):
+        return 2
+
+    def wgrad(self, As, Bs, parts):
         self.wgrad_calls.append(len(As))
-        S = part.shape[1]
-        for p, (a, b) in enumerate(zip(As, Bs)):
-            K = a.shape[0]
+        for part, a, b in zip(parts, As, Bs):
+            S, K = part.shape[0], a.shape[0]
             for s in range(S):
                 k0, k1 = K * s // S, K * (s + 1) // S
-                part[p, s] = a[k0:k1].float().t() @ b[k0:k1].float()
+                part[s] = a[k0:k1].float().t() @ b[k0:k1].float()
 
     def prep_max_tasks(self):
         return 64
@@ -53,7 +55,7 @@ def test_sum_queue_groups_wgrad_problems(monkeypatch):
         assert gemm.mm_tn(a, b, o, q=q) is o
     assert ops.wgrad_calls == [] and len(q.gemms) == 3   # deferred, nothing launched yet
     q.flush()
-    assert ops.wgrad_calls == [3]                      # one launch for the three same-shape GEMMs
+    assert ops.wgrad_calls == [3]                      # one launch for the three GEMMs
     assert ops.prep_calls == [[gemm.SumQueue.SUM] * 3]
     for a, b, o in zip(A, Bm, outs):
         ref = a.float().t() @ b.float()

@@ -9,10 +9,12 @@ from distributed_char_rnn_amd.engine.native import tail as tailmod
 pytestmark = pytest.mark.gpu
 
 
-def test_finalize_tasks_and_norm(dcr_ops):
+@pytest.mark.parametrize("dynamic", [False, True])
+def test_finalize_tasks_and_norm(dcr_ops, dynamic):
     """Slab sums (float4 + scalar paths), a column sum, a norm-only term and both MM forms, the
-    MMs waiting in-launch on a slab sum that signals a counter; the global sum of squares of
-    the flagged outputs (+ the extra term) against fp64."""
+    MMs waiting in-launch on a slab sum that signals a counter, one long MM split into k-slabs
+    (signalling a second counter to the SUM that adds them); the global sum of squares of the
+    flagged outputs (+ the extra term) against fp64.  Static tiles and the atomic queue."""
     torch.manual_seed(3)
     dev = "cuda"
     part = torch.randn(5, 300, 2048, device=dev)
@@ -28,6 +30,9 @@ def test_finalize_tasks_and_norm(dcr_ops):
     Wx = torch.randn(512, 2048, device=dev)
     o1 = torch.empty(512, 2048, device=dev)
     o2 = torch.empty(65, 512, device=dev)
+    o3 = torch.empty(65, 512, device=dev)
+    b3 = torch.randn(512, device=dev)
+    slabs = torch.full((3, 65, 512), float("nan"), device=dev)
     extra = torch.tensor([123.5], device=dev)
     total = torch.zeros(1, device=dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -39,9 +44,12 @@ def test_finalize_tasks_and_norm(dcr_ops):
     tab.sumsq(x)
     tab.mm(o1, E, (1, 512), dew, (2048, 1), 65, norm=True, wait=0)     # Eᵀ·dEW (short k)
     tab.mm(o2, dew, (2048, 1), Wx, (1, 2048), 2048, norm=True, wait=0)  # dEW·Wxᵀ (long k)
+    tab.mm(o3, dew, (2048, 1), Wx, (1, 2048), 2048, bias=b3, norm=True, wait=0, slabs=slabs,
+           slab_sig=1)                                                    # the same in 3 k-slabs
     ws = tailmod.workspace(dcr_ops, dev)
     for _ in range(2):  # the counters reset themselves: a second launch gives the same result
-        tailmod.run(dcr_ops, tab, 0, ws, err, 1 << 22, total_out=total, extra=extra)
+        tailmod.run(dcr_ops, tab, 0, ws, err, 1 << 22, total_out=total, extra=extra,
+                    dynamic=dynamic)
     torch.cuda.synchronize()
     assert int(err.item()) == 0
     assert torch.count_nonzero(ws["sync"]) == 0 and torch.count_nonzero(ws["dep"]) == 0
@@ -56,7 +64,8 @@ def test_finalize_tasks_and_norm(dcr_ops):
     ref_dew = part_d.double().sum(0)[:65]
     close(o1, E.double().t() @ ref_dew, 1e-5)
     close(o2, ref_dew @ Wx.double().t(), 1e-5)
-    ref_total = sum(float((t.double() ** 2).sum()) for t in (out, out_s, db, x, o1, o2)) + 123.5
+    close(o3, ref_dew @ Wx.double().t() + b3.double(), 1e-5)
+    ref_total = sum(float((t.double() ** 2).sum()) for t in (out, out_s, db, x, o1, o2, o3)) + 123.5
     assert abs(float(total) - ref_total) / ref_total < 1e-5
 
 
@@ -92,25 +101,32 @@ def test_fused_adam_matches_plain(B, T, dp):
     torch.manual_seed(5)
     x = torch.randint(0, 65, (B, 3 * T), dtype=torch.int32, device="cuda")
     y = torch.randint(0, 65, (B, 3 * T), dtype=torch.int32, device="cuda")
+    def rel(a, b):
+        return float((a.double() - b.double()).norm() / b.double().norm())
     runs = []
     for fused in (False, True):
         model, opt = _models(fused)
         st = model.zero_state(B)
+        snap = None
         for k in range(3):
             _, st, _ = model.train_step(x[:, k * T:(k + 1) * T], y[:, k * T:(k + 1) * T], st,
                                         _Sync() if dp else None)
             opt.step(2e-3)
+            if k == 0:  # after one update from identical gradients
+                torch.cuda.synchronize()
+                snap = (model.store.flat.clone(), opt.m.clone(), opt.v.clone(),
+                        float(opt.last_norm))
         torch.cuda.synchronize()
-        runs.append((model, opt))
-    (m0, o0), (m1, o1) = runs
+        runs.append((model, opt, snap))
+    (m0, o0, s0), (m1, o1, s1) = runs
     assert int(m1.backend.err.item()) == 0
-
-    def rel(a, b):
-        return float((a.double() - b.double()).norm() / b.double().norm())
-    assert rel(m1.store.flat, m0.store.flat) < 1e-5
-    assert rel(o1.m, o0.m) < 1e-4
-    assert rel(o1.v, o0.v) < 1e-4
-    assert abs(float(o1.last_norm) - float(o0.last_norm)) <= 1e-4 * float(o0.last_norm)
+    # one update: the same TF-Adam arithmetic (the norm summed in another order: fp32 rounding)
+    assert rel(s1[0], s0[0]) < 1e-6
+    assert rel(s1[1], s0[1]) < 1e-5 and rel(s1[2], s0[2]) < 1e-5
+    assert abs(s1[3] - s0[3]) <= 1e-5 * s0[3]
+    # three updates: fp32 ulps that flip a bf16 weight rounding make the trajectories drift
+    assert rel(m1.store.flat, m0.store.flat) < 1e-3
+    assert abs(float(o1.last_norm) - float(o0.last_norm)) <= 1e-3 * float(o0.last_norm)
     # layouts: what the fused update wrote vs a refresh from the same fp32 masters
     be = m1.backend
     w = be._w
@@ -167,7 +183,8 @@ def test_tail_backward_matches_prep_flush(monkeypatch, B, T):
             assert model.backend._tail_total_ok  # the finalize covered the whole norm prefix
             n_norm, _ = model.store.norm_terms()
             g = model.store.grad
-            ref = float((g[:n_norm].double() ** 2).sum() + g[model.store.norm_slot].double() ** 2)
+            # (the slot holds the TF per-token term, itself a sum of squares)
+            ref = float((g[:n_norm].double() ** 2).sum() + g[model.store.norm_slot].double())
             assert abs(float(model.backend._tail_total) - ref) <= 1e-5 * ref
     a, b = grads
     assert float((a - b).norm() / b.norm()) < 1e-6

@@ -8,25 +8,31 @@ from distributed_char_rnn_amd.ops import native
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("np_,M,N,K,S", [(1, 256, 256, 64, 1), (3, 512, 2048, 4096, 4),
-                                         (2, 256, 512, 3200, 3), (1, 1024, 3072, 2048, 2)])
-def test_wgrad_matches_fp32_reference(np_, M, N, K, S):
+@pytest.mark.parametrize("shapes,K,S", [([(256, 256)], 64, 1), ([(512, 2048)] * 3, 4096, 4),
+                                        ([(256, 512), (512, 256)], 3200, 3),
+                                        ([(1024, 3072)], 2048, 2),
+                                        ([(1024, 2048), (512, 2048)], 8192, 5)])
+def test_wgrad_matches_fp32_reference(shapes, K, S):
+    """One launch over problems of different shapes (the step's layer-1 and layer-0 weight
+    gradients), every (problem, slab) against fp32 PyTorch."""
     ops = native.ops()
     g = torch.Generator(device="cuda").manual_seed(0)
-    # A as a strided view (row stride > M, like [h0_t | h1_{t-1}] halves)
-    Abuf = torch.randn(K, 2 * M, device="cuda", generator=g).to(torch.bfloat16)
-    As = [Abuf[:, :M] if p % 2 == 0 else Abuf[:, M:] for p in range(np_)]
-    Bs = [torch.randn(K, N, device="cuda", generator=g).to(torch.bfloat16) for _ in range(np_)]
-    part = torch.full((np_, S, M, N), float("nan"), device="cuda")
-    ops.wgrad(As, Bs, part)
+    As, Bs, parts = [], [], []
+    for p, (M, N) in enumerate(shapes):
+        # A as a strided view (row stride > M, like [h0_t | h1_{t-1}] halves)
+        Abuf = torch.randn(K, 2 * M, device="cuda", generator=g).to(torch.bfloat16)
+        As.append(Abuf[:, :M] if p % 2 == 0 else Abuf[:, M:])
+        Bs.append(torch.randn(K, N, device="cuda", generator=g).to(torch.bfloat16))
+        parts.append(torch.full((S, M, N), float("nan"), device="cuda"))
+    ops.wgrad(As, Bs, parts)
     torch.cuda.synchronize()
     ks = 32  # csrc/wgrad.hip kWgK
     steps = K // ks
-    for p in range(np_):
+    for p in range(len(shapes)):
         for s in range(S):
             k0, k1 = steps * s // S * ks, steps * (s + 1) // S * ks
             ref = As[p][k0:k1].float().t() @ Bs[p][k0:k1].float()
-            err = ((part[p, s] - ref).norm() / ref.norm()).item()
+            err = ((parts[p][s] - ref).norm() / ref.norm()).item()
             assert err < 1e-5, (p, s, err)
 
 
