@@ -60,6 +60,7 @@ class LayoutsMixin:
             return False
         if self._adam_tab is None:
             self._adam_tab = self._adam_table()
+            self._adam_tabs = self._adam_tab.partition()
             self._adam_ws = tailmod.workspace(self.ops, self.dev)
         s = self.store
         n = s.norm_slot
@@ -77,13 +78,14 @@ class LayoutsMixin:
             part, ticket, total = self._adam_sq
             self.ops.sumsq(s.grad.narrow(0, 0, n_norm), part, total, ticket,
                            s.norm_slot_view() if use_slot else None, None)
-        tailmod.run(self.ops, self._adam_tab, 1, self._adam_ws, self.err, self.spin_limit,
-                    total_in=total,
-                    p=s.flat.narrow(0, 0, n), g=s.grad.narrow(0, 0, n), m=opt.m.narrow(0, 0, n),
-                    v=opt.v.narrow(0, 0, n), mirror=self._mirror, n_norm=n_norm, lr_t=lr_t,
-                    b1=opt.b1, b2=opt.b2, eps=opt.eps, clip=opt.clip, gscale=float(grad_scale),
-                    lr_dev=lr_dev, skip_if=opt.guard, norm_out=opt.last_norm,
-                    dynamic=self.tail_dynamic())
+        for tab in self._adam_tabs:  # (one launch unless the tiles exceed a launch's)
+            tailmod.run(self.ops, tab, 1, self._adam_ws, self.err, self.spin_limit,
+                        total_in=total,
+                        p=s.flat.narrow(0, 0, n), g=s.grad.narrow(0, 0, n), m=opt.m.narrow(0, 0, n),
+                        v=opt.v.narrow(0, 0, n), mirror=self._mirror, n_norm=n_norm, lr_t=lr_t,
+                        b1=opt.b1, b2=opt.b2, eps=opt.eps, clip=opt.clip, gscale=float(grad_scale),
+                        lr_dev=lr_dev, skip_if=opt.guard, norm_out=opt.last_norm,
+                        dynamic=self.tail_dynamic())
         return True
 
     def fused_adam_done(self) -> None:

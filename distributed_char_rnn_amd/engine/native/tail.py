@@ -37,8 +37,12 @@ def task_tiles(op: int, rows: int, cols: int, k: int, nslab: int = 0) -> int:
     raise ValueError(op)
 
 
+MAX_TILES = 16384  # csrc/kernels.h kTailMaxTiles: tiles of one launch
+
+
 class TailTable:
     def __init__(self, max_tasks: int = 16):
+        self.calls = []  # (method, args, kwargs) of every task, for partition()
         self.words: List[int] = []
         self.keep: List[torch.Tensor] = []
         self.ops: List[int] = []
@@ -48,6 +52,52 @@ class TailTable:
 
     def __len__(self) -> int:
         return len(self.ops)
+
+    def partition(self, max_tiles: int = MAX_TILES) -> List["TailTable"]:
+        """This table as consecutive launches of at most ``max_tiles`` tiles (and max_tasks
+        tasks) each, in task order.  A task whose producers all ran in an earlier launch waits
+        for nothing (stream order); a counter's ``need`` counts this launch's producers."""
+        if sum(self.tiles) <= max_tiles and len(self.ops) <= self.max_tasks:
+            return [self]
+        out, cur = [], TailTable(self.max_tasks)
+        for (meth, args, kw), nt in zip(self._flat_calls(), self.tiles):
+            if nt > max_tiles:
+                raise ValueError(f"tail task of {nt} tiles > {max_tiles}")
+            if len(cur) and (sum(cur.tiles) + nt > max_tiles or len(cur) >= cur.max_tasks):
+                out.append(cur)
+                cur = TailTable(self.max_tasks)
+            kw = dict(kw)
+            if kw.get("wait", -1) >= 0 and cur.sig_tiles.get(kw["wait"], 0) <= 0:
+                kw["wait"] = -1
+            getattr(cur, meth)(*args, **kw)
+        out.append(cur)
+        return out
+
+    def _flat_calls(self):
+        """One (method, args, kwargs) per task: a k-slab MM call is two tasks (MM + SUM)."""
+        for meth, args, kw in self.calls:
+            if meth == "mm" and kw.get("slabs") is not None:
+                out, a, sa, b, sb, k = args
+                kw = dict(kw)
+                slabs, slab_sig = kw.pop("slabs"), kw.pop("slab_sig")
+                norm, sig = kw.pop("norm", False), kw.pop("sig", -1)
+                yield ("_mm_slab_task", (out, a, sa, b, sb, k, slabs, slab_sig), kw)
+                yield ("sum", (slabs, out, norm), dict(sig=sig, wait=slab_sig))
+            else:
+                yield meth, args, kw
+
+    def _mm_slab_task(self, out, a, sa, b, sb, k, slabs, slab_sig, **kw):
+        """The MM task of a k-slab product alone (its SUM is a separate call)."""
+        S, rows, cols = slabs.shape
+        ar, ak = sa
+        bk, bc = sb
+        self.calls.append(("_mm_slab_task", (out, a, sa, b, sb, k, slabs, slab_sig), kw))
+        bias = kw.get("bias")
+        self._add(MM, rows, cols, wait=kw.get("wait", -1), sig=slab_sig, nslab=S,
+                  dst=slabs.data_ptr(), dst_ld=cols, off=rows * cols, k=k, a=a.data_ptr(),
+                  ar=ar, ak=ak, b=b.data_ptr(), bk=bk, bc=bc,
+                  bias=0 if bias is None else bias.data_ptr(),
+                  keep=(out, a, b, slabs) + (() if bias is None else (bias,)))
 
     def _add(self, op, rows, cols, *, norm=0, wait=-1, sig=-1, vec4=0, nslab=0, k=0, o1_t=0,
              o2_t=0, a=0, ar=0, ak=0, b=0, bk=0, bc=0, bias=0, dst=0, dst_ld=0, off=0, ld=0, o1=0,
@@ -72,6 +122,7 @@ class TailTable:
     def sum(self, part: torch.Tensor, out: torch.Tensor, norm: bool, sig: int = -1,
             wait: int = -1):
         """out [rows, cols] = sum over the slabs of part [S, rows, cols] (fp32)."""
+        self.calls.append(("sum", (part, out, norm), dict(sig=sig, wait=wait)))
         assert part.dim() == 3 and out.dim() == 2 and part.stride(2) == 1 and out.stride(1) == 1
         assert tuple(part.shape[1:]) == tuple(out.shape) and part.dtype == out.dtype == torch.float32
         S, rows, cols = part.shape
@@ -91,6 +142,7 @@ class TailTable:
 
     def colsum(self, part: torch.Tensor, out: torch.Tensor, norm: bool):
         """out [cols] = column sums of part [R, cols] (fp32, fixed order)."""
+        self.calls.append(("colsum", (part, out, norm), {}))
         assert part.dim() == 2 and part.stride(1) == 1 and out.is_contiguous()
         assert out.numel() == part.shape[1]
         self._add(COLSUM, 1, part.shape[1], norm=norm, k=part.shape[0], a=part.data_ptr(),
@@ -98,6 +150,7 @@ class TailTable:
 
     def sumsq(self, x: torch.Tensor):
         """A norm term finished elsewhere (contiguous fp32)."""
+        self.calls.append(("sumsq", (x,), {}))
         assert x.is_contiguous() and x.dtype == torch.float32
         self._add(SUMSQ, 1, x.numel(), norm=1, a=x.data_ptr(), keep=(x,))
 
@@ -108,6 +161,7 @@ class TailTable:
         ([S, rows, cols] fp32, S > 1, k > MM_SHORT_K): the reduction split into S k-slabs over
         more workgroups, written there and signalled on ``slab_sig``; a SUM task waiting on it
         adds them into ``out`` in slab order."""
+        n_calls = len(self.calls)
         assert out.dim() == 2 and out.stride(1) == 1 and out.dtype == torch.float32
         ar, ak = a_strides
         bk, bc = b_strides
@@ -118,6 +172,8 @@ class TailTable:
                    bias=0 if bias is None else bias.data_ptr())
         keep = (out, a, b) + (() if bias is None else (bias,))
         if slabs is None:
+            self.calls.append(("mm", (out, a, a_strides, b, b_strides, k),
+                               dict(bias=bias, norm=norm, wait=wait, sig=sig)))
             self._add(MM, rows, cols, norm=norm, wait=wait, sig=sig, dst=out.data_ptr(),
                       dst_ld=out.stride(0), keep=keep, **ops)
             return
@@ -127,12 +183,18 @@ class TailTable:
         self._add(MM, rows, cols, wait=wait, sig=slab_sig, nslab=S, dst=slabs.data_ptr(),
                   dst_ld=cols, off=rows * cols, keep=keep + (slabs,), **ops)
         self.sum(slabs, out, norm, sig=sig, wait=slab_sig)
+        # one recorded call for both tasks (partition() splits it again)
+        del self.calls[n_calls:]
+        self.calls.append(("mm", (out, a, a_strides, b, b_strides, k),
+                           dict(bias=bias, norm=norm, wait=wait, sig=sig, slabs=slabs,
+                                slab_sig=slab_sig)))
 
     # ---- ADAM --------------------------------------------------------------------------------
     def adam(self, off: int, rows: int, cols: int, ld: int, outs=(), sig: int = -1,
              keep=()):
         """One parameter region flat[off + r ld + c]; ``outs``: up to two (bf16 tensor, row
         stride, transposed) layout outputs of it (besides the flat bf16 mirror)."""
+        self.calls.append(("adam", (off, rows, cols, ld), dict(outs=outs, sig=sig, keep=keep)))
         assert len(outs) <= 2
         w = dict(o1=0, o1_ld=0, o1_t=0, o2=0, o2_ld=0, o2_t=0)
         vec4 = off % 4 == 0 and ld % 4 == 0 and cols % 4 == 0
@@ -317,7 +379,11 @@ class TailQueue:
             be._fin_ws = workspace(self.ops, be.dev)
         s = be.store
         _, use_slot = s.norm_terms()
-        run(self.ops, tab, 0, be._fin_ws, be.err, be.spin_limit,
-            total_out=total_out if ok else None,
-            extra=s.norm_slot_view() if (ok and use_slot) else None, dynamic=be.tail_dynamic())
+        parts = tab.partition()
+        ok = ok and len(parts) == 1  # (several launches: the fused Adam sums the norm itself)
+        for t in parts:
+            run(self.ops, t, 0, be._fin_ws, be.err, be.spin_limit,
+                total_out=total_out if ok else None,
+                extra=s.norm_slot_view() if (ok and use_slot) else None,
+                dynamic=be.tail_dynamic())
         return ok

@@ -11,3 +11,12 @@ timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 
   --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 4 --warmup 1 \
   --dist_backend gloo --batch 64 --seq 32 > gpurun_out/dp_rehearsal.log 2>&1 || { tail -30 gpurun_out/dp_rehearsal.log; exit 1; }
 grep '"metric"' gpurun_out/dp_rehearsal.log
+# the JSON line must report the 2-rank job with a finite loss
+python - <<'PY' || exit 1
+import json, math
+line = [l for l in open("gpurun_out/dp_rehearsal.log") if l.startswith('{"metric"')][-1]
+r = json.loads(line)
+assert r["n_gpus"] == 2, r["n_gpus"]
+assert math.isfinite(r["final_loss"]) and r["value"] > 0, r
+print("dp rehearsal ok: n_gpus", r["n_gpus"], "final_loss", r["final_loss"])
+PY

@@ -4,7 +4,8 @@ one-GPU box cannot host two ranks on separate devices, and RCCL refuses two rank
 * a 1-rank ``nccl`` process group with ``GradSync(enabled=True)`` in the headline configuration
   (two-layer wavefront kernels, exclusive schedule, deferred 1/world scaling): RCCL's stream
   ordering against the persistent grids and the bucket releases must leave the gradients and
-  the updated weights bitwise equal to the run without a process group;
+  the updated weights equal to the run without a process group (to the last bits: the
+  weight-gradient launches are grouped by bucket release there);
 * a forced persistent-kernel spin timeout (tiny DCR_SPIN_LIMIT) must leave the weights and the
   Adam slots unchanged (the optimizer reads the error word on device) and raise on the host.
 """
@@ -46,7 +47,7 @@ def _steps(model, opt, sync, x, y, n):
     return loss.item(), norms
 
 
-def test_rccl_one_rank_grad_sync_is_bitwise_identity(monkeypatch):
+def test_rccl_one_rank_grad_sync_matches_no_sync(monkeypatch):
     monkeypatch.setenv("DCR_SPIN_LIMIT", str(1 << 22))
     B, T = 256, 32
     g = torch.Generator().manual_seed(0)
@@ -70,9 +71,20 @@ def test_rccl_one_rank_grad_sync_is_bitwise_identity(monkeypatch):
         dist.destroy_process_group()
     a.check_errors()
     b.check_errors()
-    assert la == lb and na == nb
-    assert torch.equal(a.store.flat, b.store.flat)
-    assert torch.equal(oa.m, ob.m) and torch.equal(oa.v, ob.v)
+    # the hand-written weight-gradient GEMM picks its split-K slab count for the problems of
+    # one launch, and under data parallelism the launches follow the bucket releases (the
+    # layer-1 and layer-0 gradients in separate launches instead of one): the same products
+    # summed in another order, last-bit differences in the first step's gradients (its norm
+    # agrees to 1e-6); Adam's m / sqrt(v) turns last-bit differences of near-zero gradients into
+    # lr-sized update differences, so later steps agree to ~1e-5.  A stream-ordering race
+    # would show as stale or partial gradients, orders of magnitude above this.
+    assert abs(na[0] - nb[0]) <= 1e-6 * abs(na[0]), (na, nb)
+    assert all(abs(x - y) <= 1e-3 * abs(x) for x, y in zip(na, nb)), (na, nb)
+    assert abs(la - lb) <= 1e-4 * abs(la), (la, lb)
+    d = ((a.store.flat - b.store.flat).norm() / a.store.flat.norm()).item()
+    assert d < 1e-4, d
+    assert ((oa.m - ob.m).norm() / oa.m.norm()).item() < 1e-3
+    assert ((oa.v - ob.v).norm() / oa.v.norm()).item() < 1e-3
 
 
 def test_spin_timeout_leaves_weights_unchanged(monkeypatch):
