@@ -443,6 +443,8 @@ struct GenArgs {
   float* logits_out;                 // optional [num, S, V]
   unsigned* err; unsigned spin_limit;
   int ws_lds;                        // set by the launcher: softmax_wᵀ resident in LDS
+  unsigned long long* stamps;        // optional [2][8][16] phase timestamps (diagnostics)
+  int dbg;                           // diagnostics (DCR_DEBUG=gen_dbg): 1 no head, 2 head w/o h
 };
 int generate_supported(int L, int H, int V, int S, int cus);
 int launch_generate(GenArgs& a, int cus, hipStream_t s);

@@ -1438,7 +1438,7 @@ void generate(at::TensorList Wh, at::TensorList Wx, at::TensorList bias, const a
               const at::Tensor& c0, at::Tensor& h_out, at::Tensor& c_out, const at::Tensor& prime,
               int64_t num, at::Tensor& out, at::Tensor& hx, int64_t mode, int64_t space_id,
               int64_t seed, const at::Tensor& ctr0, const c10::optional<at::Tensor>& logits_out,
-              at::Tensor& err, int64_t spin_limit) {
+              at::Tensor& err, int64_t spin_limit, const c10::optional<at::Tensor>& stamps) {
   const int L = (int)Wh.size();
   TORCH_CHECK(L >= 1 && L <= dcr::kGenMaxLayers && (int)Wx.size() == L && (int)bias.size() == L,
               "generate: 1..", dcr::kGenMaxLayers, " layers");
@@ -1474,6 +1474,10 @@ void generate(at::TensorList Wh, at::TensorList Wx, at::TensorList bias, const a
   CHECK_DEV(ctr0); CHECK_I32(ctr0); TORCH_CHECK(ctr0.numel() >= a.S, "generate: ctr0 [S]");
   CHECK_DEV(err); CHECK_I32(err);
   a.table = ptr<float>(table); a.WsT = ptr<bf16>(WsT); a.bs = ptr<float>(bs);
+  if (stamps && stamps->defined()) {
+    CHECK_DEV(*stamps); TORCH_CHECK(stamps->element_size() == 8 && stamps->numel() >= 256, "generate: stamps [256] of 8 B");
+    a.stamps = reinterpret_cast<unsigned long long*>(stamps->data_ptr());
+  }
   a.forget_bias = (float)forget_bias;
   a.h0 = ptr<float>(h0); a.c0 = ptr<float>(c0); a.h_out = ptr<float>(h_out); a.c_out = ptr<float>(c_out);
   a.prime = ptr<int>(prime); a.num = (int)num; a.out = ptr<int>(out);
@@ -1747,7 +1751,7 @@ TORCH_LIBRARY(dcr, m) {
   m.def("generate(Tensor[] Wh, Tensor[] Wx, Tensor[] bias, Tensor table, Tensor WsT, Tensor bs, "
         "float forget_bias, Tensor h0, Tensor c0, Tensor(a!) h_out, Tensor(b!) c_out, Tensor prime, "
         "int num, Tensor(c!) out, Tensor(d!) hx, int mode, int space_id, int seed, Tensor ctr0, "
-        "Tensor(e!)? logits_out, Tensor(f!) err, int spin_limit) -> ()");
+        "Tensor(e!)? logits_out, Tensor(f!) err, int spin_limit, Tensor(g!)? stamps=None) -> ()");
   m.def("generate_supported(int L, int H, int V, int S) -> int",
         [](int64_t L, int64_t H, int64_t V, int64_t S) -> int64_t {
           return dcr::generate_supported((int)L, (int)H, (int)V, (int)S, num_cus()); });

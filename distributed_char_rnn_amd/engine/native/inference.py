@@ -127,7 +127,8 @@ class InferenceMixin:
         self.ops.generate([lw.Wh for lw in w], [lw.Wx for lw in w], [lw.bias for lw in w],
                           hd["table"], hd["WsT_gen"], hd["bs"], FORGET_BIAS, h0, c0, h1, c1,
                           prime, int(num), out, hx, int(sampling_type), int(space_id),
-                          int(seed) & ((1 << 63) - 1), ctr0, lg, self.err, self.spin_limit)
+                          int(seed) & ((1 << 63) - 1), ctr0, lg, self.err, self.spin_limit,
+                          getattr(self, "gen_stamps", None))
         ids = out.cpu().tolist()
         self.check_errors()
         state = [(c1[l], h1[l]) for l in range(L)]
