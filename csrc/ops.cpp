@@ -1388,8 +1388,9 @@ void tail(at::IntArrayRef words, int64_t phase, at::Tensor& part, at::Tensor& sy
     T.o1 = reinterpret_cast<bf16*>(w[23]); T.o1_ld = w[24];
     T.o2 = reinterpret_cast<bf16*>(w[25]); T.o2_ld = w[26];
     TORCH_CHECK(T.op >= dcr::TAIL_SUM && T.op <= dcr::TAIL_ADAM, "tail: unknown op ", T.op);
-    TORCH_CHECK((T.op == dcr::TAIL_ADAM) == (phase == 1) || T.op == dcr::TAIL_MM,
-                "tail: ADAM tasks only in phase 1, SUM / COLSUM / SUMSQ only in phase 0");
+    TORCH_CHECK((T.op == dcr::TAIL_ADAM) == (phase == 1) || T.op == dcr::TAIL_MM ||
+                    (T.op == dcr::TAIL_SUM && !T.norm),
+                "tail: ADAM tasks only in phase 1, COLSUM / SUMSQ / norm SUMs only in phase 0");
     TORCH_CHECK(T.rows > 0 && T.cols > 0, "tail: empty task");
     TORCH_CHECK(T.wait < dcr::kTailMaxDeps && T.sig < dcr::kTailMaxDeps, "tail: dep index");
     TORCH_CHECK(T.wait < 0 || T.need > 0, "tail: a waiting task needs a positive count");

@@ -425,8 +425,11 @@ __device__ __forceinline__ void put_bf4(bf16* d, float4 v) {
 
 __device__ void tail_adam(const TailArgs& a, const TailTask& T, int local, const AdamCtx& A,
                           bool sc1_out, float (*tile)[65]) {
+  // 64 x 64 tiles (float4 path) or 16 x 64 (scalar path: odd widths, e.g. softmax_w [H, 65],
+  // 4 rows per thread in one batch of loads instead of 16 in four)
+  const int TR = T.vec4 ? 64 : 16;
   const int tiles_c = (T.cols + 63) / 64;
-  const int r0 = (local / tiles_c) * 64, c0 = (local % tiles_c) * 64;
+  const int r0 = (local / tiles_c) * TR, c0 = (local % tiles_c) * 64;
   const bool tr = (T.o1 && T.o1_t) || (T.o2 && T.o2_t);
   // every load of the tile's rows is issued before the first store (the stores could alias the
   // next row's loads for all the compiler knows, which would serialise the rows' round trips)
@@ -448,16 +451,24 @@ __device__ void tail_adam(const TailArgs& a, const TailTask& T, int local, const
       M[i] = *reinterpret_cast<const float4*>(a.m + idx[i]);
       Vv[i] = *reinterpret_cast<const float4*>(a.v + idx[i]);
     }
+    // (the update is computed for every row, clamped ones included, and only the stores are
+    // guarded: a guarded use lets the compiler sink each row's loads into its own branch,
+    // one serialised round trip per row)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int ri = (threadIdx.x >> 4) + 16 * i, r = r0 + ri;
-      if (!ok[i]) continue;
       float4 p = P[i], m = M[i], v = Vv[i];
       const float4 g = Gv[i];
       adam1(p.x, g.x, m.x, v.x, A.s, A.lr_t, A.b1, A.b2, A.eps);
       adam1(p.y, g.y, m.y, v.y, A.s, A.lr_t, A.b1, A.b2, A.eps);
       adam1(p.z, g.z, m.z, v.z, A.s, A.lr_t, A.b1, A.b2, A.eps);
       adam1(p.w, g.w, m.w, v.w, A.s, A.lr_t, A.b1, A.b2, A.eps);
+      P[i] = p; M[i] = m; Vv[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ri = (threadIdx.x >> 4) + 16 * i, r = r0 + ri;
+      if (!ok[i]) continue;
+      const float4 p = P[i], m = M[i], v = Vv[i];
       st4(a.p + idx[i], p, sc1_out);
       *reinterpret_cast<float4*>(a.m + idx[i]) = m;
       *reinterpret_cast<float4*>(a.v + idx[i]) = v;
@@ -472,7 +483,7 @@ __device__ void tail_adam(const TailArgs& a, const TailTask& T, int local, const
     // 16 rows per thread in 4 batches of 4 (loads of a batch in flight together)
     const int tx = threadIdx.x & 63, c = c0 + tx;
     if (c < T.cols) {
-      for (int rb = threadIdx.x >> 6; rb < 64; rb += 16) {
+      for (int rb = threadIdx.x >> 6; rb < 16; rb += 16) {
         float P[4], Gv[4], M[4], Vv[4];
         size_t idx[4];
 #pragma unroll
@@ -482,11 +493,12 @@ __device__ void tail_adam(const TailArgs& a, const TailTask& T, int local, const
           P[i] = a.p[idx[i]]; Gv[i] = a.g[idx[i]]; M[i] = a.m[idx[i]]; Vv[i] = a.v[idx[i]];
         }
 #pragma unroll
+        for (int i = 0; i < 4; ++i) adam1(P[i], Gv[i], M[i], Vv[i], A.s, A.lr_t, A.b1, A.b2, A.eps);
+#pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int ri = rb + 4 * i, r = r0 + ri;
           if (r >= T.rows) continue;
-          float p = P[i], m = M[i], v = Vv[i];
-          adam1(p, Gv[i], m, v, A.s, A.lr_t, A.b1, A.b2, A.eps);
+          const float p = P[i], m = M[i], v = Vv[i];
           if (sc1_out) st_sc1(a.p + idx[i], p); else a.p[idx[i]] = p;
           a.m[idx[i]] = m;
           a.v[idx[i]] = v;
@@ -511,6 +523,7 @@ __device__ void tail_adam(const TailArgs& a, const TailTask& T, int local, const
       const int c = c0 + cc;
       if (c >= T.cols) continue;
       bf16* row = d + (size_t)c * ld + r0;
+      if (rq >= TR) continue;
       if (r0 + rq + 3 < T.rows && (ld & 3) == 0 && (r0 & 3) == 0) {
         put_bf4(row + rq, make_float4(tile[rq][cc], tile[rq + 1][cc], tile[rq + 2][cc], tile[rq + 3][cc]));
       } else {
@@ -648,8 +661,8 @@ __global__ void __launch_bounds__(kTailThreads, 2) tail_kernel(TailArgs a) {
 
 int tail_tiles(const TailTask& t) {
   switch (t.op) {
-    case TAIL_SUM:
-    case TAIL_ADAM: return ((t.rows + 63) / 64) * ((t.cols + 63) / 64);
+    case TAIL_SUM: return ((t.rows + 63) / 64) * ((t.cols + 63) / 64);
+    case TAIL_ADAM: return ((t.rows + (t.vec4 ? 63 : 15)) / (t.vec4 ? 64 : 16)) * ((t.cols + 63) / 64);
     case TAIL_COLSUM: return (t.cols + 63) / 64;
     case TAIL_SUMSQ: return (int)(((long)t.rows * t.cols + 4095) / 4096);
     case TAIL_MM:

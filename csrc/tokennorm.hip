@@ -24,6 +24,7 @@
 // reproducible) and writes the result.  The ticket is reset by that workgroup.
 #include "gemm_common.h"
 #include "kernels.h"
+#include "debug_env.h"
 
 namespace dcr {
 
@@ -31,12 +32,14 @@ constexpr int kTnTile = 256, kTnK = 32, kTnStages = 4, kTnWaves = 8;
 constexpr int kTnStageB = 2 * kTnTile * kTnK * 2;   // A + B panels, bytes
 constexpr int kTnDmaPerWave = 32 / kTnWaves;
 
+template <int NST>
 __global__ void __launch_bounds__(64 * kTnWaves, kTnWaves / 4) tokennorm_kernel(TokenNormArgs a) {
   // ONE shared array (a second __shared__ object beside a DMA ring can make the compiler wait
   // vmcnt(0) in front of the k-step's first LDS read): the ring, then the reduction words
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[kTnStages * kTnStageB + 64];
-  float* const red = reinterpret_cast<float*>(lds + kTnStages * kTnStageB);
-  unsigned& last = *reinterpret_cast<unsigned*>(lds + kTnStages * kTnStageB + 4 * kTnWaves);
+  // (the reduction words reuse the ring after the main loop: NST = 5 fills all 160 KB)
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[NST * kTnStageB];
+  float* const red = reinterpret_cast<float*>(lds);
+  unsigned& last = *reinterpret_cast<unsigned*>(lds + 4 * kTnWaves);
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tn = a.N_units / kTnTile;
@@ -58,8 +61,8 @@ __global__ void __launch_bounds__(64 * kTnWaves, kTnWaves / 4) tokennorm_kernel(
     offb[j] = (unsigned)(((size_t)(n0 + row) * a.ld_w + 8 * c) * sizeof(bf16));
   }
   const unsigned lds0 = (unsigned)(size_t)(const __attribute__((address_space(3))) void*)lds;
-  auto issue = [&](int kt) {
-    const unsigned st = lds0 + (kt % kTnStages) * kTnStageB;
+  auto issue = [&](int kt) {  // (prologue: kt < NST)
+    const unsigned st = lds0 + kt * kTnStageB;
     const unsigned sk = (unsigned)(kt * kTnK * sizeof(bf16));
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -73,18 +76,19 @@ __global__ void __launch_bounds__(64 * kTnWaves, kTnWaves / 4) tokennorm_kernel(
   const unsigned pch = (unsigned)((lane >> 4) ^ ((4 - ((lane & 15) >> 2)) & 3));
   const unsigned fa0 = (unsigned)((wm + (lane & 15)) * 64 + pch * 16);
   const unsigned fb0 = (unsigned)(kTnTile * 64 + (wn + (lane & 15)) * 64 + pch * 16);
-  auto rd_a = [&](int kt, u32x4 (&fa)[8], int i0, int i1) {
-    const unsigned base = lds0 + (kt % kTnStages) * kTnStageB;
+  // (ring slots tracked by the caller: no runtime modulo by NST)
+  auto rd_a = [&](int slot, u32x4 (&fa)[8], int i0, int i1) {
+    const unsigned base = lds0 + slot * kTnStageB;
 #pragma unroll
     for (int i = i0; i < i1; ++i) fa[i] = gemm_rd128(base + fa0 + 1024 * i);
   };
-  auto rd_b = [&](int kt, u32x4 (&fb)[4]) {
-    const unsigned base = lds0 + (kt % kTnStages) * kTnStageB;
+  auto rd_b = [&](int slot, u32x4 (&fb)[4]) {
+    const unsigned base = lds0 + slot * kTnStageB;
 #pragma unroll
     for (int j = 0; j < 4; ++j) fb[j] = gemm_rd128(base + fb0 + 1024 * j);
   };
-  auto issue_pair = [&](int kt, int j) {  // this wave's DMA pair j of stage kt
-    const unsigned st = lds0 + (kt % kTnStages) * kTnStageB;
+  auto issue_pair = [&](int kt, int slot, int j) {  // this wave's DMA pair j of stage kt
+    const unsigned st = lds0 + slot * kTnStageB;
     const unsigned sk = (unsigned)(kt * kTnK * sizeof(bf16));
     const unsigned r = (unsigned)(16 * (2 * w + j));
     gemm_dma(ra, st + r * 64, offa[j], sk);
@@ -106,7 +110,7 @@ __global__ void __launch_bounds__(64 * kTnWaves, kTnWaves / 4) tokennorm_kernel(
   u32x4 fa[8], fb_0[4], fb_1[4];
   const int nk = ksteps;
   {
-    const int pro = nk < kTnStages ? nk : kTnStages;
+    const int pro = nk < NST ? nk : NST;
     for (int j = 0; j < pro; ++j) issue(j);
     gemm_vm_wait((pro - 1) * kTnDmaPerWave);
     gemm_barrier();
@@ -115,40 +119,44 @@ __global__ void __launch_bounds__(64 * kTnWaves, kTnWaves / 4) tokennorm_kernel(
   }
   // the k-step schedule of wgrad.hip v3: four MFMA groups of 8 with the refill DMA pairs and the
   // next stage's fragment reads between them (A into the registers just consumed)
+  int si = 0;  // ring slot of stage i
   auto kstep = [&](int i, u32x4 (&fb)[4], u32x4 (&nb_)[4]) {
     const bool more = i + 1 < nk;
-    const bool refill = more && i + kTnStages < nk;
+    const bool refill = more && i + NST < nk;
+    const int s1 = si + 1 == NST ? 0 : si + 1;
     if (more) {
-      const int later = nk - 2 - i < kTnStages - 2 ? nk - 2 - i : kTnStages - 2;
+      const int later = nk - 2 - i < NST - 2 ? nk - 2 - i : NST - 2;
       gemm_vm_wait(later * kTnDmaPerWave);
       gemm_barrier();
     }
     __builtin_amdgcn_sched_barrier(0);
     mf(0, fa, fb);
     __builtin_amdgcn_sched_barrier(0);
-    if (refill) issue_pair(i + kTnStages, 0);
+    if (refill) issue_pair(i + NST, si, 0);  // (stage i + NST refills stage i's slot)
     if (more) {
-      rd_b(i + 1, nb_);
-      rd_a(i + 1, fa, 0, 2);
+      rd_b(s1, nb_);
+      rd_a(s1, fa, 0, 2);
     }
     __builtin_amdgcn_sched_barrier(0);
     mf(1, fa, fb);
     __builtin_amdgcn_sched_barrier(0);
-    if (refill) issue_pair(i + kTnStages, 1);
-    if (more) rd_a(i + 1, fa, 2, 4);
+    if (refill) issue_pair(i + NST, si, 1);
+    if (more) rd_a(s1, fa, 2, 4);
     __builtin_amdgcn_sched_barrier(0);
     mf(2, fa, fb);
     __builtin_amdgcn_sched_barrier(0);
-    if (more) rd_a(i + 1, fa, 4, 6);
+    if (more) rd_a(s1, fa, 4, 6);
     __builtin_amdgcn_sched_barrier(0);
     mf(3, fa, fb);
     __builtin_amdgcn_sched_barrier(0);
-    if (more) rd_a(i + 1, fa, 6, 8);
+    if (more) rd_a(s1, fa, 6, 8);
+    si = s1;
   };
   for (int i = 0; i < nk; i += 2) {
     kstep(i, fb_0, fb_1);
     if (i + 1 < nk) kstep(i + 1, fb_1, fb_0);
   }
+  __syncthreads();  // (every stage read: the ring's first bytes become the reduction words)
 
   // epilogue (the host requires N % 256 == 0: no ragged tile): the sum of squares of this
   // workgroup's 256 x 256 outputs
@@ -188,6 +196,147 @@ __global__ void __launch_bounds__(64 * kTnWaves, kTnWaves / 4) tokennorm_kernel(
   }
 }
 
+// ---- v4: 4 waves of 128 x 128 (one workgroup per CU, 256 accumulators per lane) ---------------
+// The 8-wave form reads 8 x (128 + 64) fragment rows per 32-deep k-step (96 KB) besides the
+// 32 KB of DMA writes: about the MFMA time of the step, so the two contend for the CU.  Four
+// waves of 128 x 128 read 4 x (128 + 128) rows (64 KB): the k-step is MFMA-bound.  Same ring,
+// swizzle and schedule idea (8 MFMA groups of one A tile x 8 B tiles, the refill DMAs and the
+// next stage's fragment reads between them).
+constexpr int kT4Waves = 4;
+constexpr int kT4DmaPerWave = 32 / kT4Waves;
+
+__global__ void __launch_bounds__(64 * kT4Waves, 1) tokennorm4_kernel(TokenNormArgs a) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[kTnStages * kTnStageB + 64];
+  float* const red = reinterpret_cast<float*>(lds + kTnStages * kTnStageB);
+  unsigned& last = *reinterpret_cast<unsigned*>(lds + kTnStages * kTnStageB + 4 * kT4Waves);
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tn = a.N_units / kTnTile;
+  const int nb = gridDim.x;
+  const int lin = (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8;  // an m-tile's n-tiles on one XCD
+  const int m0 = (lin / tn) * kTnTile, n0 = (lin % tn) * kTnTile;
+  const int nk = a.K / kTnK;
+
+  // DMA: wave w fills rows 64 w .. 64 w + 63 of both panels (4 instructions of 16 rows each)
+  const __amdgpu_buffer_rsrc_t ra = gemm_rsrc(a.dz);
+  const __amdgpu_buffer_rsrc_t rb = gemm_rsrc(a.w);
+  unsigned offa[4], offb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = 16 * (4 * w + j) + (lane >> 2);
+    const int c = (lane & 3) ^ ((4 - ((lane >> 4) & 3)) & 3);
+    offa[j] = (unsigned)(((size_t)(m0 + row) * a.ld_dz + 8 * c) * sizeof(bf16));
+    offb[j] = (unsigned)(((size_t)(n0 + row) * a.ld_w + 8 * c) * sizeof(bf16));
+  }
+  const unsigned lds0 = (unsigned)(size_t)(const __attribute__((address_space(3))) void*)lds;
+  auto issue_pair = [&](int kt, int j) {
+    const unsigned st = lds0 + (kt % kTnStages) * kTnStageB;
+    const unsigned sk = (unsigned)(kt * kTnK * sizeof(bf16));
+    const unsigned r = (unsigned)(16 * (4 * w + j));
+    gemm_dma(ra, st + r * 64, offa[j], sk);
+    gemm_dma(rb, st + kTnTile * 64 + r * 64, offb[j], sk);
+  };
+  const int wm = 128 * (w >> 1), wn = 128 * (w & 1);
+  const unsigned pch = (unsigned)((lane >> 4) ^ ((4 - ((lane & 15) >> 2)) & 3));
+  const unsigned fa0 = (unsigned)((wm + (lane & 15)) * 64 + pch * 16);
+  const unsigned fb0 = (unsigned)(kTnTile * 64 + (wn + (lane & 15)) * 64 + pch * 16);
+  auto rd_a = [&](int kt, u32x4 (&fa)[8], int i) {
+    fa[i] = gemm_rd128(lds0 + (kt % kTnStages) * kTnStageB + fa0 + 1024 * i);
+  };
+  auto rd_b = [&](int kt, u32x4 (&fb)[8]) {
+    const unsigned base = lds0 + (kt % kTnStages) * kTnStageB;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fb[j] = gemm_rd128(base + fb0 + 1024 * j);
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mf = [&](int g, u32x4 (&fa)[8], u32x4 (&fb)[8]) {  // MFMA group g: A tile g x 8 B tiles
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj)
+      acc[g][jj] = mfma16(__builtin_bit_cast(bf16x8, fa[g]), __builtin_bit_cast(bf16x8, fb[jj]), acc[g][jj]);
+  };
+  // one operand set: A tile g of the next stage is read right after group g used it; the B
+  // tiles of the next stage one by one inside the last group (B tile j after MFMA (7, j))
+  u32x4 fa[8], fb[8];
+  {
+    const int pro = nk < kTnStages ? nk : kTnStages;
+    for (int j = 0; j < pro; ++j)
+#pragma unroll
+      for (int d = 0; d < 4; ++d) issue_pair(j, d);
+    gemm_vm_wait((pro - 1) * kT4DmaPerWave);
+    gemm_barrier();
+    rd_b(0, fb);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rd_a(0, fa, i);
+  }
+  for (int i = 0; i < nk; ++i) {
+    const bool more = i + 1 < nk;
+    const bool refill = more && i + kTnStages < nk;
+    if (more) {
+      const int later = nk - 2 - i < kTnStages - 2 ? nk - 2 - i : kTnStages - 2;
+      gemm_vm_wait(later * kT4DmaPerWave);
+      gemm_barrier();
+    }
+#pragma unroll
+    for (int g = 0; g < 7; ++g) {
+      __builtin_amdgcn_sched_barrier(0);
+      mf(g, fa, fb);
+      __builtin_amdgcn_sched_barrier(0);
+      if (refill && g < 4) issue_pair(i + kTnStages, g);
+      if (more) rd_a(i + 1, fa, g);
+    }
+    const unsigned nbase = lds0 + ((i + 1) % kTnStages) * kTnStageB + fb0;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      __builtin_amdgcn_sched_barrier(0);
+      acc[7][jj] = mfma16(__builtin_bit_cast(bf16x8, fa[7]), __builtin_bit_cast(bf16x8, fb[jj]), acc[7][jj]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (more) fb[jj] = gemm_rd128(nbase + 1024 * jj);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) rd_a(i + 1, fa, 7);
+  }
+
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sq += acc[i][j][r] * acc[i][j][r];
+  sq = wave_sum(sq);
+  if (lane == 0) red[w] = sq;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < kT4Waves; ++i) t += red[i];
+    __hip_atomic_store(a.part + blockIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned k = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = k == (unsigned)gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  float s2 = 0.f;
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += 64 * kT4Waves)
+    s2 += __hip_atomic_load(a.part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  s2 = wave_sum(s2);
+  if (lane == 0) red[w] = s2;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < kT4Waves; ++i) t += red[i];
+    a.out[0] = t;
+    __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 bool tokennorm_supported(int N, int H, int K) {
   return N > 0 && N % kTnTile == 0 && H % kTnTile == 0 && K % kTnK == 0 && K >= kTnK &&
          (long)(N / kTnTile) * (H / kTnTile) <= kTokenNormMaxGrid && ((N / kTnTile) * (H / kTnTile)) % 8 == 0;
@@ -195,7 +344,13 @@ bool tokennorm_supported(int N, int H, int K) {
 
 void launch_tokennorm(const TokenNormArgs& a, hipStream_t s) {
   const int grid = (a.N / kTnTile) * (a.N_units / kTnTile);
-  tokennorm_kernel<<<grid, 64 * kTnWaves, 0, s>>>(a);
+  const int v = debug_int("tn_v", 3);
+  if (v == 4)
+    tokennorm4_kernel<<<grid, 64 * kT4Waves, 0, s>>>(a);
+  else if (v == 5)
+    tokennorm_kernel<5><<<grid, 64 * kTnWaves, 0, s>>>(a);
+  else
+    tokennorm_kernel<4><<<grid, 64 * kTnWaves, 0, s>>>(a);
 }
 
 }  // namespace dcr

@@ -134,6 +134,8 @@ class LayoutsMixin:
         if cover != want:
             raise AssertionError(f"fused Adam covers {cover} of {want} parameters")
         if table:
+            # (E·W_x0 + b0 as 80-row tiles of the full k = H: splitting it into k-slabs summed
+            # in the same launch measured slower, 56 vs 38 us for the launch)
             GW = w0.Wx32.shape[1]
             tab.mm(hd["table"], hd["E"], (H, 1), w0.Wx32, (GW, 1), D, bias=w0.bias, wait=0)
         return tab

@@ -79,6 +79,8 @@ DEBUG_KEYS = {
     "tail_queue": "1: tail launches take tiles from the atomic queue even on an unshared GPU",
     "tail_per": "N: tail workgroups per CU (C++, default 2)",
     "gen_dbg": "1: generator without the head, 2: head without h loads (C++, timing only)",
+    "tn_v": "token-norm GEMM: 3 (default) 8 waves, 4-stage ring; 5 the same with 5 stages; 4 four "
+            "waves of 128 x 128 (C++)",
     "gru_ub": "1: 16-unit GRU workgroups (C++)",
     "gru_nt": "N: N batch tiles of 16 rows per GRU workgroup (C++)",
     "step_nbt": "1/2/4: batch tiles per per-step workgroup (C++)",

@@ -22,10 +22,12 @@ def _a16(t: torch.Tensor) -> bool:
     return t.data_ptr() % 16 == 0
 
 
-def task_tiles(op: int, rows: int, cols: int, k: int, nslab: int = 0) -> int:
+def task_tiles(op: int, rows: int, cols: int, k: int, nslab: int = 0, vec4: int = 1) -> int:
     """Tiles of one task (csrc/tail.hip tail_tiles)."""
-    if op in (SUM, ADAM):
+    if op == SUM:
         return -(-rows // 64) * -(-cols // 64)
+    if op == ADAM:
+        return -(-rows // (64 if vec4 else 16)) * -(-cols // 64)
     if op == COLSUM:
         return -(-cols // 64)
     if op == SUMSQ:
@@ -109,7 +111,7 @@ class TailTable:
             need = self.sig_tiles.get(wait, 0)
             if need <= 0:
                 raise ValueError(f"tail table: nothing signals counter {wait} before this task")
-        nt = task_tiles(op, rows, cols, k, nslab)
+        nt = task_tiles(op, rows, cols, k, nslab, int(vec4))
         if sig >= 0:
             self.sig_tiles[sig] = self.sig_tiles.get(sig, 0) + nt
         self.words += [op, rows, cols, int(norm), wait, need, sig, int(vec4), nslab, k, o1_t, o2_t,
