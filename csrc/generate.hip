@@ -256,25 +256,40 @@ __global__ void __launch_bounds__(kGenThreads, 1) generate_kernel(GenArgs a) {
         // lgkmcnt(0): one serialised round trip per element), 4 k-steps per batch
         const float* hrow = ht + (size_t)(sv ? m : 0) * H;
         const float zs = sv ? 1.f : 0.f;
-        auto step = [&](int k0) {
-          bf16x8 av;
-          if (WsL) av = *reinterpret_cast<const bf16x8*>(WsL + (size_t)row * wsld + k0);
-          else av = ld8(a.WsT + (size_t)row * H + k0);
+        // (two accumulator chains over alternate k-steps: their operand reads overlap; H is a
+        // multiple of 128, so the k-steps pair up)
+        f32x4 acc2 = f32x4{0.f, 0.f, 0.f, 0.f};
+        auto step2 = [&](int k0) {
+          bf16x8 av0, av1;
+          if (WsL) {
+            av0 = *reinterpret_cast<const bf16x8*>(WsL + (size_t)row * wsld + k0);
+            av1 = *reinterpret_cast<const bf16x8*>(WsL + (size_t)row * wsld + k0 + 32);
+          } else {
+            av0 = ld8(a.WsT + (size_t)row * H + k0);
+            av1 = ld8(a.WsT + (size_t)row * H + k0 + 32);
+          }
           const float4 h0 = *reinterpret_cast<const float4*>(hrow + k0);
           const float4 h1 = *reinterpret_cast<const float4*>(hrow + k0 + 4);
-          bf16x8 bv;
-          bv[0] = (bf16)(h0.x * zs); bv[1] = (bf16)(h0.y * zs); bv[2] = (bf16)(h0.z * zs);
-          bv[3] = (bf16)(h0.w * zs); bv[4] = (bf16)(h1.x * zs); bv[5] = (bf16)(h1.y * zs);
-          bv[6] = (bf16)(h1.z * zs); bv[7] = (bf16)(h1.w * zs);
-          acc = mfma16(av, bv, acc);
+          const float4 h2 = *reinterpret_cast<const float4*>(hrow + k0 + 32);
+          const float4 h3 = *reinterpret_cast<const float4*>(hrow + k0 + 36);
+          bf16x8 b0, b1;
+          b0[0] = (bf16)(h0.x * zs); b0[1] = (bf16)(h0.y * zs); b0[2] = (bf16)(h0.z * zs);
+          b0[3] = (bf16)(h0.w * zs); b0[4] = (bf16)(h1.x * zs); b0[5] = (bf16)(h1.y * zs);
+          b0[6] = (bf16)(h1.z * zs); b0[7] = (bf16)(h1.w * zs);
+          b1[0] = (bf16)(h2.x * zs); b1[1] = (bf16)(h2.y * zs); b1[2] = (bf16)(h2.z * zs);
+          b1[3] = (bf16)(h2.w * zs); b1[4] = (bf16)(h3.x * zs); b1[5] = (bf16)(h3.y * zs);
+          b1[6] = (bf16)(h3.z * zs); b1[7] = (bf16)(h3.w * zs);
+          acc = mfma16(av0, b0, acc);
+          acc2 = mfma16(av1, b1, acc2);
         };
         if (WsL) {
-#pragma unroll 4
-          for (int k0 = 8 * q; k0 < H; k0 += 32) step(k0);
+#pragma unroll 2
+          for (int k0 = 8 * q; k0 < H; k0 += 64) step2(k0);
         } else {
-#pragma unroll 4
-          for (int k0 = 8 * q; k0 < H; k0 += 32) step(k0);
+#pragma unroll 2
+          for (int k0 = 8 * q; k0 < H; k0 += 64) step2(k0);
         }
+        acc += acc2;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int v = 16 * rb + 4 * q + r;
