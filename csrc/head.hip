@@ -23,8 +23,9 @@
 
 namespace dcr {
 
-constexpr int kHeadThreads = 256;
-constexpr int kHeadTPW = 2;  // token tiles (16 tokens each) per wave chunk
+constexpr int kHeadWaves = 8;   // (two waves per SIMD: one wave's L2 round trips hide behind the other's work)
+constexpr int kHeadThreads = 64 * kHeadWaves;
+constexpr int kHeadTPW = 1;  // token tiles (16 tokens each) per wave chunk
 
 template <int NVT>
 __global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs a) {
@@ -32,8 +33,8 @@ __global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs a) {
   constexpr int VK = 32 * ((VP + 31) / 32);  // padded K for the dtop MFMA
   constexpr int SLD = VK + 8;              // LDS row stride (bf16), keeps 16-B alignment
   constexpr int TPW = kHeadTPW;
-  __shared__ __attribute__((aligned(16))) bf16 sdl[4][TPW * 16][SLD];
-  __shared__ float red[4][VP + 1];
+  __shared__ __attribute__((aligned(16))) bf16 sdl[kHeadWaves][TPW * 16][SLD];
+  __shared__ float red[kHeadWaves][VP + 1];
   // softmax_wᵀ [VP, H] staged once per workgroup (shared by its 4 waves), 16-B chunk c of row r
   // at chunk c ^ (r & 15): the 16 rows of a fragment read hit 16 distinct bank groups
   extern __shared__ __attribute__((aligned(16))) bf16 swt[];
@@ -82,7 +83,7 @@ __global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs a) {
     }
     __syncthreads();
   }
-  for (int chunk = blockIdx.x * 4 + w; chunk < nchunks; chunk += gridDim.x * 4) {
+  for (int chunk = blockIdx.x * kHeadWaves + w; chunk < nchunks; chunk += gridDim.x * kHeadWaves) {
     const int nb = chunk * TPW * 16;
     // ---- logits
     f32x4 acc[TPW][NVT];
@@ -103,7 +104,7 @@ __global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs a) {
         for (int j = 0; j < 8; ++j)
 #pragma unroll
           for (int tp = 0; tp < TPW; ++tp)
-            bo[j][tp] = k0 + 32 * j < H ? ld8(orow[tp] + k0 + 32 * j) : zero8();
+            bo[j][tp] = ld8(orow[tp] + min(k0 + 32 * j, H - 32));  // (clamped: unused past H)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           if (k0 + 32 * j >= H) break;
@@ -159,7 +160,8 @@ __global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs a) {
       const float lse = m + __logf(s);
       int y = -1;
       if (a.targets) {
-        y = valid ? a.targets[n] : 0;
+        y = a.targets[min(n, N - 1)];
+        if (!valid) y = 0;
         float xy = 0.f;
 #pragma unroll
         for (int vt = 0; vt < NVT; ++vt)
@@ -217,8 +219,7 @@ __global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs a) {
       for (int j = 0; j < HG; ++j)
 #pragma unroll
         for (int ks = 0; ks < VK / 32; ++ks)
-          af[j][ks] = ht0 + j < H / 16 ? ld8(wk + (size_t)(ht0 + j) * 16 * VK + ks * 32)
-                                       : bf16x8{};
+          af[j][ks] = ld8(wk + (size_t)min(ht0 + j, H / 16 - 1) * 16 * VK + ks * 32);  // (clamped)
 #pragma unroll
       for (int j = 0; j < HG; ++j) {
         if (ht0 + j >= H / 16) break;
@@ -270,8 +271,12 @@ __global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs a) {
   if (lane == 0) red[w][VP] = lacc;
   __syncthreads();
   float* part = a.part + (size_t)blockIdx.x * (VP + 1);
-  for (int i = threadIdx.x; i <= VP; i += kHeadThreads)
-    part[i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  for (int i = threadIdx.x; i <= VP; i += kHeadThreads) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < kHeadWaves; ++k) t += red[k][i];
+    part[i] = t;
+  }
 }
 
 // one wave per output column, lanes stride the partial rows (deterministic order per lane,
@@ -304,7 +309,7 @@ int head_supported(int V, int H) { return V >= 1 && V <= 256 && H % 32 == 0 && H
 
 int head_num_partials(int N, int cus) {
   const int nchunks = (N + kHeadTPW * 16 - 1) / (kHeadTPW * 16);
-  int g = (nchunks + 3) / 4;
+  int g = (nchunks + kHeadWaves - 1) / kHeadWaves;
   const int cap = 2 * (cus > 0 ? cus : 256);
   return g < cap ? (g > 0 ? g : 1) : cap;
 }
@@ -342,7 +347,7 @@ int launch_head(const HeadArgs& a, int cus, float* db_out, float* loss_out, hipS
 #undef HC
     default: return -1;
   }
-  const int fw = (head_vpad(a.V) + 1 + 3) / 4;  // one wave per column
+  const int fw = (head_vpad(a.V) + 1 + kHeadWaves - 1) / kHeadWaves;  // one wave per column
   head_finalize_kernel<<<fw, kHeadThreads, 0, s>>>(a.part, grid, head_vpad(a.V), a.V,
                                                   1.0f / (float)a.N, db_out, loss_out);
   return 0;

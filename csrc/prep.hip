@@ -73,22 +73,44 @@ __global__ void __launch_bounds__(256) prep_kernel(PrepTable tab) {
     case PREP_COPY:
       if (T.kind == PREP_RAW32) {
         const unsigned* s = static_cast<const unsigned*>(T.src);
-        for (int r = r0 + ty; r < r1; r += 4)
-          if (c0 + tx < T.cols)
-            reinterpret_cast<unsigned*>(T.dst)[(size_t)r * T.dst_ld + c0 + tx] =
-                s[(size_t)r * T.src_ld + c0 + tx];
+        const int cc = min(c0 + tx, T.cols - 1);
+        unsigned v[kPrepTile / 4];  // (all loads before the first store)
+#pragma unroll
+        for (int i = 0; i < kPrepTile / 4; ++i)
+          v[i] = s[(size_t)min(r0 + ty + 4 * i, T.rows - 1) * T.src_ld + cc];
+        if (c0 + tx < T.cols)
+#pragma unroll
+          for (int i = 0; i < kPrepTile / 4; ++i)
+            if (r0 + ty + 4 * i < r1)
+              reinterpret_cast<unsigned*>(T.dst)[(size_t)(r0 + ty + 4 * i) * T.dst_ld + c0 + tx] = v[i];
         return;
       }
       if (T.vec4) {  // 16 lanes x float4 per 64-column row, 16 rows per pass
         const int c = c0 + 4 * (threadIdx.x & 15);
         if (c >= T.cols) return;
-        for (int r = r0 + (threadIdx.x >> 4); r < r1; r += 16)
-          prep_put4(T, (size_t)r * T.dst_ld + c,
-                    *reinterpret_cast<const float4*>(src + (size_t)r * T.src_ld + c));
+        float4 v[kPrepTile / 16];  // (all loads before the first store)
+#pragma unroll
+        for (int i = 0; i < kPrepTile / 16; ++i)
+          v[i] = *reinterpret_cast<const float4*>(
+              src + (size_t)min(r0 + (threadIdx.x >> 4) + 16 * i, T.rows - 1) * T.src_ld + c);
+#pragma unroll
+        for (int i = 0; i < kPrepTile / 16; ++i) {
+          const int r = r0 + (threadIdx.x >> 4) + 16 * i;
+          if (r < r1) prep_put4(T, (size_t)r * T.dst_ld + c, v[i]);
+        }
         return;
       }
-      for (int r = r0 + ty; r < r1; r += 4)
-        if (c0 + tx < T.cols) prep_put(T, (size_t)r * T.dst_ld + c0 + tx, src[(size_t)r * T.src_ld + c0 + tx]);
+      {
+        const int cc = min(c0 + tx, T.cols - 1);
+        float v[kPrepTile / 4];  // (all loads before the first store)
+#pragma unroll
+        for (int i = 0; i < kPrepTile / 4; ++i)
+          v[i] = src[(size_t)min(r0 + ty + 4 * i, T.rows - 1) * T.src_ld + cc];
+        if (c0 + tx < T.cols)
+#pragma unroll
+          for (int i = 0; i < kPrepTile / 4; ++i)
+            if (r0 + ty + 4 * i < r1) prep_put(T, (size_t)(r0 + ty + 4 * i) * T.dst_ld + c0 + tx, v[i]);
+      }
       return;
     case PREP_SUM: {
       if (T.vec4) {
@@ -184,13 +206,23 @@ __global__ void __launch_bounds__(256) prep_kernel(PrepTable tab) {
     }
     case PREP_ONEHOT: {
       // dst row n = t*B + b (time-major) <- ids[b][t] of the batch-major source view
+      // (the 16 ids of a thread's rows loaded together, unconditionally at clamped rows: a
+      // guarded load in the row loop is one serialised round trip per row)
       const int* ids = static_cast<const int*>(T.src);
       const int B = T.kdim;
-      for (int n = r0 + ty; n < r1; n += 4)
-        if (c0 + tx < T.cols) {
-          const int id = ids[(size_t)(n % B) * T.src_ld + n / B];
-          reinterpret_cast<bf16*>(T.dst)[(size_t)n * T.dst_ld + c0 + tx] =
-              f2bf(id == c0 + tx ? 1.f : 0.f);
+      int idv[kPrepTile / 4];
+#pragma unroll
+      for (int i = 0; i < kPrepTile / 4; ++i) {
+        const int n = min(r0 + ty + 4 * i, T.rows - 1);
+        idv[i] = ids[(size_t)(n % B) * T.src_ld + n / B];
+      }
+      if (c0 + tx < T.cols)
+#pragma unroll
+        for (int i = 0; i < kPrepTile / 4; ++i) {
+          const int n = r0 + ty + 4 * i;
+          if (n < r1)
+            reinterpret_cast<bf16*>(T.dst)[(size_t)n * T.dst_ld + c0 + tx] =
+                f2bf(idv[i] == c0 + tx ? 1.f : 0.f);
         }
       return;
     }
@@ -212,11 +244,12 @@ __global__ void __launch_bounds__(256) prep_kernel(PrepTable tab) {
       for (int k0 = ka; k0 < kz; k0 += 64) {
         float av[16], bv[16];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
+        for (int j = 0; j < 16; ++j) {  // (unconditional loads at a clamped k, then a select)
           const int k = k0 + 4 * j + (lane >> 4);
-          const bool ok = k < kz;
-          av[j] = ok ? Ep[k] : 0.f;
-          bv[j] = ok ? Wp[(size_t)k * T.src2_ld] : 0.f;
+          const int kc = min(k, kz - 1);
+          const float a_ = Ep[kc], b_ = Wp[(size_t)kc * T.src2_ld];
+          av[j] = k < kz ? a_ : 0.f;
+          bv[j] = k < kz ? b_ : 0.f;
         }
 #pragma unroll
         for (int j = 0; j < 16; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc, 0, 0, 0);
@@ -247,10 +280,16 @@ __global__ void __launch_bounds__(256) prep_kernel(PrepTable tab) {
   }
   // TRANSPOSE: coalesced read of rows r, coalesced write of dst rows c
   if (T.kind == PREP_RAW32) {
+    // (every load of the tile issued before the LDS stores, unconditionally at clamped
+    // coordinates: guarded loads in the row loop serialise one round trip per row)
     const unsigned* s = static_cast<const unsigned*>(T.src);
-    for (int r = ty; r < kPrepTile; r += 4)
-      if (r0 + r < T.rows && c0 + tx < T.cols)
-        tile[r][tx] = __builtin_bit_cast(float, s[(size_t)(r0 + r) * T.src_ld + c0 + tx]);
+    const int cc = min(c0 + tx, T.cols - 1);
+    unsigned v[kPrepTile / 4];
+#pragma unroll
+    for (int i = 0; i < kPrepTile / 4; ++i)
+      v[i] = s[(size_t)min(r0 + ty + 4 * i, T.rows - 1) * T.src_ld + cc];
+#pragma unroll
+    for (int i = 0; i < kPrepTile / 4; ++i) tile[ty + 4 * i][tx] = __builtin_bit_cast(float, v[i]);
     __syncthreads();
     for (int c = ty; c < kPrepTile; c += 4)
       if (c0 + c < T.cols && r0 + tx < T.rows)
@@ -262,11 +301,17 @@ __global__ void __launch_bounds__(256) prep_kernel(PrepTable tab) {
     // float4 row reads into the tile; each thread then writes 4 consecutive destination
     // elements (source rows r..r+3 of one column) as one 8-B (bf16) / 16-B (fp32) store
     const int cq = 4 * (threadIdx.x & 15);
-    for (int r = threadIdx.x >> 4; r < kPrepTile; r += 16)
-      if (r0 + r < T.rows && c0 + cq < T.cols) {
-        const float4 v = *reinterpret_cast<const float4*>(src + (size_t)(r0 + r) * T.src_ld + c0 + cq);
-        tile[r][cq] = v.x; tile[r][cq + 1] = v.y; tile[r][cq + 2] = v.z; tile[r][cq + 3] = v.w;
-      }
+    const int cqc = min(c0 + cq, T.cols - 4);  // (vec4: cols % 4 == 0)
+    float4 v[kPrepTile / 16];
+#pragma unroll
+    for (int i = 0; i < kPrepTile / 16; ++i)
+      v[i] = *reinterpret_cast<const float4*>(
+          src + (size_t)min(r0 + (threadIdx.x >> 4) + 16 * i, T.rows - 1) * T.src_ld + cqc);
+#pragma unroll
+    for (int i = 0; i < kPrepTile / 16; ++i) {
+      const int r = (threadIdx.x >> 4) + 16 * i;
+      tile[r][cq] = v[i].x; tile[r][cq + 1] = v[i].y; tile[r][cq + 2] = v[i].z; tile[r][cq + 3] = v[i].w;
+    }
     __syncthreads();
     const int rq = 4 * (threadIdx.x & 15);
     for (int c = threadIdx.x >> 4; c < kPrepTile; c += 16)
@@ -275,9 +320,15 @@ __global__ void __launch_bounds__(256) prep_kernel(PrepTable tab) {
                   make_float4(tile[rq][c], tile[rq + 1][c], tile[rq + 2][c], tile[rq + 3][c]));
     return;
   }
-  for (int r = ty; r < kPrepTile; r += 4)
-    if (r0 + r < T.rows && c0 + tx < T.cols)
-      tile[r][tx] = src[(size_t)(r0 + r) * T.src_ld + c0 + tx];
+  {
+    const int cc = min(c0 + tx, T.cols - 1);
+    float v[kPrepTile / 4];
+#pragma unroll
+    for (int i = 0; i < kPrepTile / 4; ++i)
+      v[i] = src[(size_t)min(r0 + ty + 4 * i, T.rows - 1) * T.src_ld + cc];
+#pragma unroll
+    for (int i = 0; i < kPrepTile / 4; ++i) tile[ty + 4 * i][tx] = v[i];
+  }
   __syncthreads();
   for (int c = ty; c < kPrepTile; c += 4)
     if (c0 + c < T.cols && r0 + tx < T.rows) prep_put(T, (size_t)(c0 + c) * T.dst_ld + r0 + tx, tile[tx][c]);
