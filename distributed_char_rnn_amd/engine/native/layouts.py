@@ -114,6 +114,7 @@ class LayoutsMixin:
         region("embedding", sig=sig)
         region(names[0][0], 0, D, [(w0.WxT, D, True)] if w0.WxT is not None else (), sig=sig)
         region(names[0][1], sig=sig)
+        hd = self._head
         for layer in range(self.L):
             lw = self._w[layer]
             k, b = names[layer]
@@ -122,7 +123,6 @@ class LayoutsMixin:
                 region(b)
             region(k, D, 2 * D, [(lw.WhT, H, True)])
         outs = []
-        hd = self._head
         if "WsT" in hd:
             outs.append((hd["WsT"], H, True))
             outs.append((hd["Wsk"], hd["Wsk"].shape[1], False))
@@ -134,8 +134,9 @@ class LayoutsMixin:
         if cover != want:
             raise AssertionError(f"fused Adam covers {cover} of {want} parameters")
         if table:
-            # (E·W_x0 + b0 as 80-row tiles of the full k = H: splitting it into k-slabs summed
-            # in the same launch measured slower, 56 vs 38 us for the launch)
+            # E·W_x0 + b0 last (its tiles in the launch's last round, when the operand updates
+            # are done; right after them its workgroups spun in the first round: 61 vs 39 us),
+            # as 80-row tiles of the full k = H (k-slabs summed in the same launch: 56 vs 38 us)
             GW = w0.Wx32.shape[1]
             tab.mm(hd["table"], hd["E"], (H, 1), w0.Wx32, (GW, 1), D, bias=w0.bias, wait=0)
         return tab

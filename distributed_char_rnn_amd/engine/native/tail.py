@@ -336,7 +336,10 @@ class TailQueue:
             if r is not None:
                 spans.append(r)
             return r is not None
-        # producers first: the slab sums that signal a dependency counter
+        # producers first (the slab sums that signal a dependency counter), the products waiting
+        # on them last: their tiles come in the launch's last round, when their producers are
+        # long done (dealt in the first round right after the producers, their workgroups spun
+        # instead of summing: FINALIZE 55 vs 45 us)
         for part, out, sig in sorted(self.sums, key=lambda t: t[2] < 0):
             if part.dim() == 2:
                 part = part.unsqueeze(0)
@@ -346,7 +349,11 @@ class TailQueue:
         for x in self.sumsqs:
             if norm_of(x):  # (outside the norm prefix: nothing to do)
                 tab.sumsq(x)
-        grid = int(self.ops.tail_grid())
+        self._put_mms(tab, norm_of, int(self.ops.tail_grid()))
+        self.sums, self.colsums, self.sumsqs, self.mms = [], [], [], []
+        return self._launch(tab, spans, total_out)
+
+    def _put_mms(self, tab, norm_of, grid):
         for out, a, sa, b, sb, k, wait in self.mms:
             # (a producer that did not become a slab sum of this launch -- a GEMM short enough
             # to run unsplit -- wrote its output in stream order before it: nothing to wait for)
@@ -358,7 +365,9 @@ class TailQueue:
                        slabs=self._slab_buf(S, *out.shape), slab_sig=c)
             else:
                 tab.mm(out, a, sa, b, sb, k, norm=norm_of(out), wait=wait)
-        self.sums, self.colsums, self.sumsqs, self.mms = [], [], [], []
+
+    def _launch(self, tab, spans, total_out) -> bool:
+        be = self.be
         if not len(tab):
             return False
         ok = False
