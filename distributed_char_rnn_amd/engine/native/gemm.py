@@ -65,6 +65,9 @@ def split_k(K: int, M: int, Nn: int) -> int:
 _SPLIT_CAP = int(os.environ.get("DCR_SPLITK_CAP", "0") or 0)
 
 
+WGRAD_MAX_TILES = 128  # output tiles per weight-gradient problem on the hand-written kernel
+
+
 class SumQueue:
     """Deferred reductions of one training step, executed together as ONE prep launch
     (csrc/prep.hip SUM / COLSUM tasks) instead of one torch reduce kernel each (~5-10 us per
@@ -92,8 +95,14 @@ class SumQueue:
                     or t.stride(0) % 8 or t.data_ptr() % 16):
                 return False
         K, M = a.shape
-        return (b.shape[0] == K and tuple(out.shape) == (M, b.shape[1])
-                and int(self.ops.wgrad_plan(1, M, b.shape[1], K)) > 0)
+        N = b.shape[1]
+        # large outputs stay on the library GEMM: hipBLASLt's big-tile kernels run those near
+        # peak (config 4 at B = 1024, [4096 x 8192] per layer pair: 439.7 vs 449.3 ms per step
+        # with the hand-written kernel); up to WGRAD_MAX_TILES 256 x 256 tiles (the headline's
+        # 32 + 16, config 5's 64) the hand-written one is at parity or ahead
+        return (b.shape[0] == K and tuple(out.shape) == (M, N)
+                and (M // 256) * (N // 256) <= WGRAD_MAX_TILES
+                and int(self.ops.wgrad_plan(1, M, N, K)) > 0)
 
     def add_gemm(self, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         self.gemms.append((a, b, out))
