@@ -674,9 +674,14 @@ int tail_tiles(const TailTask& t) {
 
 // the persistent grid: every workgroup co-resident (grid barrier, dependency waits)
 int tail_grid(int cus) {
-  int o = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (const void*)tail_kernel, kTailThreads, 0) != hipSuccess || o < 1)
-    return 0;
+  static int occ = -1;  // (the kernel's occupancy never changes: queried once per process)
+  if (occ < 0) {
+    int o = 0;
+    occ = hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (const void*)tail_kernel, kTailThreads, 0) ==
+                  hipSuccess ? o : 0;
+  }
+  const int o = occ;
+  if (o < 1) return 0;
   const int want = debug_int("tail_per", 2);  // workgroups per CU (speed only)
   const int per = o < want ? o : want;
   const int g = per * cus < kTailMaxGrid ? per * cus : kTailMaxGrid;
