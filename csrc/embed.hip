@@ -404,6 +404,184 @@ static void launch_segsum_t(const T* X, int ldx, const int* ids, int N, int W, i
   launch_reduce(workspace, nchunks, (int64_t)V * W, out, accumulate, s);
 }
 
+// ---- stable id sort for the wide-vocabulary segment sum (a V-bucketed counting sort) --------
+// The atomic route above wants the ids sorted (sid) with their source rows (perm).  Instead of a
+// general radix / merge sort (~10 small library launches) the ids are bucketed by value in three
+// launches over kSortChunk-id chunks:
+//   hist     chunk b counts its ids per value (LDS, two 16-bit counts per word) -> cnt[b][v]
+//   colscan  one thread per value: cnt[b][v] <- sum_{b' < b} cnt[b'][v] (in place), tot[v]
+//   scatter  chunk b: start(v) = exclusive scan of tot (every chunk scans the V totals itself),
+//            offs[v] = start(v) + cnt[b][v] (16-bit, LDS); then one wave places the chunk's ids
+//            in 64-id rounds: lanes holding the same value are found with one ballot per value
+//            bit, ranked by lane and written at offs[v] + rank; the value's lowest lane advances
+//            offs[v] by their count.
+// Positions within a value follow the id order: the result is torch.sort(ids, stable=True).
+// The LDS tables hold 16-bit words (N <= 65535, V <= 16384: at most 16 KB).
+constexpr int kSortChunk = 1024, kSortThreads = 256;
+
+__device__ __forceinline__ void lds_add16(unsigned* w, int v, unsigned x) {
+  atomicAdd(w + (v >> 1), x << ((v & 1) * 16));
+}
+__device__ __forceinline__ unsigned lds_get16(const unsigned* w, int v) {
+  return (w[v >> 1] >> ((v & 1) * 16)) & 0xFFFFu;
+}
+
+__global__ void __launch_bounds__(kSortThreads) id_hist_kernel(const int* __restrict__ ids, int N,
+                                                               int V4, int* __restrict__ cnt) {
+  extern __shared__ unsigned hist[];  // [V4 / 2] packed 16-bit counts
+  for (int i = threadIdx.x; i < V4 / 2; i += kSortThreads) hist[i] = 0u;
+  __syncthreads();
+  const int n0 = blockIdx.x * kSortChunk;
+  int id[kSortChunk / kSortThreads];
+#pragma unroll
+  for (int i = 0; i < kSortChunk / kSortThreads; ++i) {  // every load before the first atomic
+    const int n = n0 + i * kSortThreads + threadIdx.x;
+    id[i] = ids[n < N ? n : N - 1];
+  }
+#pragma unroll
+  for (int i = 0; i < kSortChunk / kSortThreads; ++i)
+    if (n0 + i * kSortThreads + (int)threadIdx.x < N) lds_add16(hist, id[i], 1u);
+  __syncthreads();
+  int4* const o = reinterpret_cast<int4*>(cnt + (size_t)blockIdx.x * V4);
+  for (int q = threadIdx.x; q < V4 / 4; q += kSortThreads) {
+    const unsigned a = hist[2 * q], b = hist[2 * q + 1];
+    o[q] = int4{(int)(a & 0xFFFFu), (int)(a >> 16), (int)(b & 0xFFFFu), (int)(b >> 16)};
+  }
+}
+
+constexpr int kSortRows = 8;  // count rows in flight per thread
+
+__global__ void __launch_bounds__(kSortThreads) id_colscan_kernel(int V4, int nblk, int* __restrict__ cnt,
+                                                                  int* __restrict__ tot) {
+  const int v = blockIdx.x * kSortThreads + threadIdx.x;
+  if (v >= V4) return;
+  int run = 0;
+  for (int b0 = 0; b0 < nblk; b0 += kSortRows) {
+    int x[kSortRows];
+#pragma unroll
+    for (int j = 0; j < kSortRows; ++j)  // clamped rows: all loads unconditional
+      x[j] = cnt[(size_t)(b0 + j < nblk ? b0 + j : nblk - 1) * V4 + v];
+#pragma unroll
+    for (int j = 0; j < kSortRows; ++j)
+      if (b0 + j < nblk) {
+        cnt[(size_t)(b0 + j) * V4 + v] = run;
+        run += x[j];
+      }
+  }
+  tot[v] = run;
+}
+
+// Q: value quads per thread (V <= 4 Q kSortThreads; Q = 8 at V = 8192)
+template <int Q>
+__global__ void __launch_bounds__(kSortThreads) id_scatter_kernel(const int* __restrict__ ids, int N,
+                                                                  int V4, int nbits,
+                                                                  const int* __restrict__ cnt,
+                                                                  const int* __restrict__ tot,
+                                                                  int* __restrict__ sid,
+                                                                  int* __restrict__ perm) {
+  extern __shared__ unsigned offs[];  // [V4 / 2] packed 16-bit first positions
+  __shared__ int wsum[kSortThreads / 64];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int b = blockIdx.x;
+  const int nq = V4 / 4;  // value quads; segment k covers quads [k kSortThreads, (k + 1) kSortThreads)
+  const int4* const t4 = reinterpret_cast<const int4*>(tot);
+  const int4* const r4 = reinterpret_cast<const int4*>(cnt + (size_t)b * V4);
+  int4 tq[Q], rq[Q];
+#pragma unroll
+  for (int k = 0; k < Q; ++k) {  // clamped quads: all loads unconditional
+    const int q = k * kSortThreads + t < nq ? k * kSortThreads + t : nq - 1;
+    tq[k] = t4[q];
+    rq[k] = r4[q];
+  }
+  int carry = 0;
+#pragma unroll
+  for (int k = 0; k < Q; ++k) {
+    if (k * kSortThreads >= nq) break;  // (uniform)
+    const int q = k * kSortThreads + t;
+    const int4 c = q < nq ? tq[k] : int4{0, 0, 0, 0};
+    const int mine = c.x + c.y + c.z + c.w;
+    int inc = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int o = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += o;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    int before = carry, seg = 0;
+#pragma unroll
+    for (int i = 0; i < kSortThreads / 64; ++i) {
+      before += i < w ? wsum[i] : 0;
+      seg += wsum[i];
+    }
+    __syncthreads();  // (wsum is reused by the next segment)
+    carry += seg;
+    if (q < nq) {
+      const int e = before + inc - mine;  // start of value 4 q
+      const int4 r = rq[k];
+      offs[2 * q] = (unsigned)(e + r.x) | ((unsigned)(e + c.x + r.y) << 16);
+      offs[2 * q + 1] =
+          (unsigned)(e + c.x + c.y + r.z) | ((unsigned)(e + c.x + c.y + c.z + r.w) << 16);
+    }
+  }
+  __syncthreads();
+  if (w != 0) return;
+  // one wave: 64-id rounds in id order (all ids loaded first)
+  const int n0 = b * kSortChunk;
+  int idv[kSortChunk / 64];
+#pragma unroll
+  for (int r = 0; r < kSortChunk / 64; ++r) {
+    const int n = n0 + r * 64 + lane;
+    idv[r] = ids[n < N ? n : N - 1];
+  }
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  for (int r = 0; r < kSortChunk / 64; ++r) {
+    const int n = n0 + r * 64 + lane;
+    const bool ok = n < N;
+    const int id = idv[r];
+    unsigned long long m = __ballot(ok);
+    for (int bit = 0; bit < nbits; ++bit) {
+      const bool on = (id >> bit) & 1;
+      const unsigned long long bal = __ballot(on);
+      m &= on ? bal : ~bal;
+    }
+    const int base = (int)lds_get16(offs, id);
+    const int pos = base + __popcll(m & lt);
+    if (ok) {
+      sid[pos] = id;
+      perm[pos] = n;
+      if ((m & lt) == 0ull) lds_add16(offs, id, (unsigned)__popcll(m));  // the value's lowest lane
+    }
+    // (one wave: its LDS operations complete in order, so the next round reads the updates)
+  }
+}
+
+int id_sort_blocks(int N) { return (N + kSortChunk - 1) / kSortChunk; }
+int id_sort_cols(int V) { return (V + 3) / 4 * 4; }
+size_t id_sort_workspace(int N, int V) {
+  return (size_t)(id_sort_blocks(N) + 1) * id_sort_cols(V);  // counts + totals
+}
+
+int launch_id_sort(const int* ids, int N, int V, int* ws, int* sid, int* perm, hipStream_t s) {
+  if (N <= 0 || N > 65535 || V <= 0 || V > 16384) return -1;
+  const int nblk = id_sort_blocks(N), V4 = id_sort_cols(V);
+  int nbits = 0;
+  while ((1 << nbits) < V) ++nbits;
+  int* const tot = ws + (size_t)nblk * V4;
+  const size_t lds = sizeof(unsigned) * (size_t)V4 / 2;
+  id_hist_kernel<<<nblk, kSortThreads, lds, s>>>(ids, N, V4, ws);
+  id_colscan_kernel<<<(V4 + kSortThreads - 1) / kSortThreads, kSortThreads, 0, s>>>(V4, nblk, ws, tot);
+  const int q = (V4 / 4 + kSortThreads - 1) / kSortThreads;
+#define SCAT(Q) id_scatter_kernel<Q><<<nblk, kSortThreads, lds, s>>>(ids, N, V4, nbits, ws, tot, sid, perm)
+  if (q <= 1) SCAT(1);
+  else if (q <= 2) SCAT(2);
+  else if (q <= 4) SCAT(4);
+  else if (q <= 8) SCAT(8);
+  else SCAT(16);
+#undef SCAT
+  return 0;
+}
+
 void launch_segsum_bf16(const bf16* X, int ldx, const int* ids, int N, int W, int V, float* out,
                         float* workspace, int accumulate, hipStream_t s, const int* perm) {
   launch_segsum_t<bf16>(X, ldx, ids, N, W, V, out, workspace, accumulate, perm, s);

@@ -135,6 +135,12 @@ void launch_embed_dropout(const int* ids, const float* E, const uint8_t* bits, b
                           int64_t rows, int K, float scale, hipStream_t s);
 
 // ---- embed.hip --------------------------------------------------------------------------
+// stable counting sort of N <= 65535 ids in [0, V), V <= 16384: sid = sorted ids, perm = their
+// positions; ws holds id_sort_workspace(N, V) ints; returns -1 for other shapes
+int id_sort_blocks(int N);
+int id_sort_cols(int V);
+size_t id_sort_workspace(int N, int V);
+int launch_id_sort(const int* ids, int N, int V, int* ws, int* sid, int* perm, hipStream_t s);
 int segsum_rows_per_chunk(int N);
 size_t segsum_workspace_floats(int N, int W, int V);
 // perm (atomic route only): ids are sorted and perm[n] is the source row of position n
@@ -415,9 +421,13 @@ struct TokenNormArgs {
   float* part;                  // [grid] partials
   unsigned* ticket;             // zeroed, reset by the kernel
   float* out;                   // [1] the sum of squares
+  float* c; long ldc;           // gemm_nt: C [N, N_units] fp32 (the products themselves)
 };
 bool tokennorm_supported(int N, int H, int K);
 void launch_tokennorm(const TokenNormArgs& a, hipStream_t s);
+// the same pipeline storing C = dz · wᵀ (config 5's dtop = dlogits · softmax_wᵀ)
+bool gemm_nt_supported(int M, int N, int K);
+void launch_gemm_nt(const TokenNormArgs& a, hipStream_t s);
 
 // single-launch autoregressive generation (generate.hip): LSTM layers + head + draw per char
 constexpr int kGenMaxLayers = 4;

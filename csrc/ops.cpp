@@ -630,6 +630,21 @@ void segsum(const at::Tensor& X, const c10::optional<at::Tensor>& ids, int64_t V
   }
 }
 
+// stable counting sort of ids (embed.hip): sid = sorted ids, perm = their source positions
+void id_sort(const at::Tensor& ids, int64_t V, at::Tensor& ws, at::Tensor& sid, at::Tensor& perm) {
+  check_seq(ids, at::kInt, "ids");
+  check_seq(ws, at::kInt, "ws");
+  check_seq(sid, at::kInt, "sid");
+  check_seq(perm, at::kInt, "perm");
+  const int N = (int)ids.numel();
+  TORCH_CHECK(sid.numel() == N && perm.numel() == N, "id_sort: sid and perm must be [N]");
+  TORCH_CHECK(V > 0 && (size_t)ws.numel() >= dcr::id_sort_workspace(N, (int)V),
+              "id_sort: workspace too small");
+  TORCH_CHECK(dcr::launch_id_sort(ptr<int>(ids), N, (int)V, ptr<int>(ws), ptr<int>(sid),
+                                  ptr<int>(perm), cur_stream()) == 0,
+              "id_sort: unsupported vocabulary size ", V);
+}
+
 // ------------------------------------------------------------------------------------------
 // persistent LSTM recurrence (lstm_persist.hip)
 // ------------------------------------------------------------------------------------------
@@ -1524,6 +1539,32 @@ void tokennorm(const at::Tensor& dz, const at::Tensor& w, at::Tensor& part, at::
   dcr::launch_tokennorm(a, cur_stream());
 }
 
+// C [M, N] fp32 = a [M, K] · bᵀ (b [N, K]), both bf16 K-contiguous (tokennorm.hip's pipeline)
+void gemm_nt(const at::Tensor& a_, const at::Tensor& b, at::Tensor& c) {
+  for (const at::Tensor* t : {&a_, &b}) {
+    CHECK_DEV(*t); CHECK_BF16(*t);
+    TORCH_CHECK(t->dim() == 2 && t->stride(1) == 1 && t->stride(0) % 8 == 0 &&
+                    (reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0,
+                "gemm_nt: 2-D bf16 views with 16-B aligned rows");
+  }
+  const int M = (int)a_.size(0), K = (int)a_.size(1), N = (int)b.size(0);
+  TORCH_CHECK(b.size(1) == K, "gemm_nt: a [M, K], b [N, K]");
+  TORCH_CHECK(dcr::gemm_nt_supported(M, N, K), "gemm_nt: unsupported shape M=", M, " N=", N,
+              " K=", K);
+  // the DMA offsets are 32-bit buffer offsets
+  TORCH_CHECK((double)(M - 1) * a_.stride(0) * 2 + (double)K * 2 < 2147483632.0 &&
+                  (double)(N - 1) * b.stride(0) * 2 + (double)K * 2 < 2147483632.0,
+              "gemm_nt: operands beyond the 2 GB buffer range");
+  CHECK_DEV(c); CHECK_F32(c);
+  TORCH_CHECK(c.dim() == 2 && c.size(0) == M && c.size(1) == N && c.stride(1) == 1,
+              "gemm_nt: c [M, N] with unit column stride");
+  dcr::TokenNormArgs a{};
+  a.dz = ptr<bf16>(a_); a.ld_dz = a_.stride(0);
+  a.w = ptr<bf16>(b); a.ld_w = b.stride(0);
+  a.N = M; a.N_units = N; a.K = K;
+  a.c = ptr<float>(c); a.ldc = c.stride(0);
+  dcr::launch_gemm_nt(a, cur_stream());
+}
 
 void prep(at::TensorList src, at::TensorList dst, at::IntArrayRef mode, at::TensorList extra) {
   TORCH_CHECK(src.size() == dst.size() && dst.size() == mode.size(), "prep: list lengths differ");
@@ -1757,6 +1798,13 @@ TORCH_LIBRARY(dcr, m) {
         [](int64_t L, int64_t H, int64_t V, int64_t S) -> int64_t {
           return dcr::generate_supported((int)L, (int)H, (int)V, (int)S, num_cus()); });
   m.def("tokennorm(Tensor dz, Tensor w, Tensor(a!) part, Tensor(b!) ticket, Tensor(c!) out) -> ()");
+  m.def("gemm_nt(Tensor a, Tensor b, Tensor(a!) c) -> ()");
+  m.def("id_sort(Tensor ids, int V, Tensor(a!) ws, Tensor(b!) sid, Tensor(c!) perm) -> ()");
+  m.def("id_sort_workspace(int N, int V) -> int", [](int64_t N, int64_t V) -> int64_t {
+    return V > 0 && V <= 16384 && N > 0 && N <= 65535
+               ? (int64_t)dcr::id_sort_workspace((int)N, (int)V) : 0; });
+  m.def("gemm_nt_supported(int M, int N, int K) -> int", [](int64_t M, int64_t N, int64_t K) -> int64_t {
+    return dcr::gemm_nt_supported((int)M, (int)N, (int)K) ? 1 : 0; });
   m.def("tokennorm_supported(int N, int H, int K) -> int", [](int64_t N, int64_t H, int64_t K) -> int64_t {
     return dcr::tokennorm_supported((int)N, (int)H, (int)K) ? 1 : 0; });
   m.def("tail_max_tasks() -> int", []() -> int64_t { return dcr::kTailMaxTasks; });
@@ -1848,6 +1896,8 @@ TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("tail", &tail);
   m.impl("generate", &generate);
   m.impl("tokennorm", &tokennorm);
+  m.impl("gemm_nt", &gemm_nt);
+  m.impl("id_sort", &id_sort);
   m.impl("wgrad", &wgrad);
   m.impl("gru_persist_fwd", &gru_persist_fwd);
   m.impl("lstm2_persist_fwd", &lstm2_persist_fwd);

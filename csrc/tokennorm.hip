@@ -19,9 +19,15 @@
 // 1 ^ G(1), 1 ^ G(2) distinct).  The DMA writes lane-linearly, so each lane fetches the logical
 // chunk that belongs at its physical position.
 //
+// gemm_nt (STORE): the same kernel with the products stored as fp32 C instead of squared --
+// config 5's dtop = dlogits [N, V] · softmax_wᵀ (softmax_w [H, V]), K = V = 8192, where the
+// library GEMM ran at 0.75 PF/s.
+//
 // Reduction.  Each workgroup's sum of squares is stored write-through (sc1) and drained before
 // an agent-scope ticket add; the last workgroup adds the partials in workgroup order (bitwise
 // reproducible) and writes the result.  The ticket is reset by that workgroup.
+#include <type_traits>
+
 #include "gemm_common.h"
 #include "kernels.h"
 #include "debug_env.h"
@@ -32,7 +38,7 @@ constexpr int kTnTile = 256, kTnK = 32, kTnStages = 4, kTnWaves = 8;
 constexpr int kTnStageB = 2 * kTnTile * kTnK * 2;   // A + B panels, bytes
 constexpr int kTnDmaPerWave = 32 / kTnWaves;
 
-template <int NST>
+template <int NST, bool STORE>
 __global__ void __launch_bounds__(64 * kTnWaves, kTnWaves / 4) tokennorm_kernel(TokenNormArgs a) {
   // ONE shared array (a second __shared__ object beside a DMA ring can make the compiler wait
   // vmcnt(0) in front of the k-step's first LDS read): the ring, then the reduction words
@@ -119,14 +125,20 @@ __global__ void __launch_bounds__(64 * kTnWaves, kTnWaves / 4) tokennorm_kernel(
   }
   // the k-step schedule of wgrad.hip v3: four MFMA groups of 8 with the refill DMA pairs and the
   // next stage's fragment reads between them (A into the registers just consumed)
+  // (STEADY k-steps refill: compile-time conditions and wait count, as in wgrad.hip)
   int si = 0;  // ring slot of stage i
-  auto kstep = [&](int i, u32x4 (&fb)[4], u32x4 (&nb_)[4]) {
-    const bool more = i + 1 < nk;
-    const bool refill = more && i + NST < nk;
+  auto kstep = [&](int i, u32x4 (&fb)[4], u32x4 (&nb_)[4], auto steady) {
+    constexpr bool STEADY = decltype(steady)::value;
+    const bool more = STEADY || i + 1 < nk;
+    const bool refill = STEADY || (more && i + NST < nk);
     const int s1 = si + 1 == NST ? 0 : si + 1;
     if (more) {
-      const int later = nk - 2 - i < NST - 2 ? nk - 2 - i : NST - 2;
-      gemm_vm_wait(later * kTnDmaPerWave);
+      if constexpr (STEADY) {
+        gemm_vm_wait((NST - 2) * kTnDmaPerWave);
+      } else {
+        const int later = nk - 2 - i < NST - 2 ? nk - 2 - i : NST - 2;
+        gemm_vm_wait(later * kTnDmaPerWave);
+      }
       gemm_barrier();
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -152,9 +164,27 @@ __global__ void __launch_bounds__(64 * kTnWaves, kTnWaves / 4) tokennorm_kernel(
     if (more) rd_a(s1, fa, 6, 8);
     si = s1;
   };
-  for (int i = 0; i < nk; i += 2) {
-    kstep(i, fb_0, fb_1);
-    if (i + 1 < nk) kstep(i + 1, fb_1, fb_0);
+  using steady_t = std::integral_constant<bool, true>;
+  using tail_t = std::integral_constant<bool, false>;
+  int i = 0;
+  for (; i + 1 + NST < nk; i += 2) {
+    kstep(i, fb_0, fb_1, steady_t{});
+    kstep(i + 1, fb_1, fb_0, steady_t{});
+  }
+  for (; i < nk; i += 2) {
+    kstep(i, fb_0, fb_1, tail_t{});
+    if (i + 1 < nk) kstep(i + 1, fb_1, fb_0, tail_t{});
+  }
+  if constexpr (STORE) {
+    // D[4q + r][l & 15] of tile (i, j): row m0 + wm + 16 i + 4 q + r, column n0 + wn + 16 j + l%16
+    float* c = a.c + (size_t)(m0 + wm + 4 * (lane >> 4)) * a.ldc + n0 + wn + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[(size_t)(16 * i + r) * a.ldc + 16 * j] = acc[i][j][r];
+    return;
   }
   __syncthreads();  // (every stage read: the ring's first bytes become the reduction words)
 
@@ -348,9 +378,22 @@ void launch_tokennorm(const TokenNormArgs& a, hipStream_t s) {
   if (v == 4)
     tokennorm4_kernel<<<grid, 64 * kT4Waves, 0, s>>>(a);
   else if (v == 5)
-    tokennorm_kernel<5><<<grid, 64 * kTnWaves, 0, s>>>(a);
+    tokennorm_kernel<5, false><<<grid, 64 * kTnWaves, 0, s>>>(a);
   else
-    tokennorm_kernel<4><<<grid, 64 * kTnWaves, 0, s>>>(a);
+    tokennorm_kernel<4, false><<<grid, 64 * kTnWaves, 0, s>>>(a);
+}
+
+bool gemm_nt_supported(int M, int N, int K) {
+  return M > 0 && N > 0 && M % kTnTile == 0 && N % kTnTile == 0 && K % kTnK == 0 && K >= kTnK &&
+         ((long)(M / kTnTile) * (N / kTnTile)) % 8 == 0 && (long)M * N < (1L << 31);
+}
+
+void launch_gemm_nt(const TokenNormArgs& a, hipStream_t s) {
+  const int grid = (a.N / kTnTile) * (a.N_units / kTnTile);
+  if (debug_int("gnt_st", 4) == 5)
+    tokennorm_kernel<5, true><<<grid, 64 * kTnWaves, 0, s>>>(a);
+  else
+    tokennorm_kernel<4, true><<<grid, 64 * kTnWaves, 0, s>>>(a);
 }
 
 }  // namespace dcr

@@ -42,6 +42,8 @@
 // 2-pass minimum for 512 B -- where the unswizzled rows would all hit the same 8 banks.  The DMA
 // writes each lane's 16 B to physical position lane, so a lane fetches the logical chunk that
 // belongs there (the global reads stay two whole 512-B rows per instruction).
+#include <type_traits>
+
 #include "gemm_common.h"
 #include "kernels.h"
 
@@ -56,8 +58,17 @@ constexpr int kWgDmaPerWave = 32 / kWgWaves;       // DMA instructions per wave 
 
 __device__ __forceinline__ int wg_swz(int r) { return 2 * (r & 7) + ((r >> 4) & 1); }
 
+// V: measurement variants (scripts/micro/wgrad_lab.hip; the step runs V = 0): bit 0 every k-step
+// re-reads the slab's first stage (L2-hot operands), bit 1 no DMA and no stage waits (LDS reads
+// of whatever the ring holds), bit 2 (with bit 1) no barriers, bit 3 a 5-stage ring (160 KB),
+// bit 4 only the A panel is DMA'd, bit 5 the DMA is issued but never waited for, bit 6 the
+// k-step barrier without its lgkmcnt(0), bit 7 no steady-state k-steps (round-5 code: every
+// k-step's wait count chosen at run time)
+template <int V>
 __global__ void __launch_bounds__(64 * kWgWaves, kWgWaves / 4) wgrad_kernel(WgradArgs a) {
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[kWgStages * kWgStageB];
+  constexpr bool HOT = V & 1, NODMA = V & 2, NOBAR = (V & 6) == 6, NOB = V & 16, NOWAIT = V & 34;
+  constexpr int ST = (V & 8) ? 5 : kWgStages;
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[ST * kWgStageB];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // block -> work item; the items of one (problem, slab) -- which share their A and B panels --
@@ -90,14 +101,21 @@ __global__ void __launch_bounds__(64 * kWgWaves, kWgWaves / 4) wgrad_kernel(Wgra
     offb[j] = (unsigned)(((size_t)r * P.ldb + n0 + 8 * c) * sizeof(bf16));
   }
   const unsigned lds0 = (unsigned)(size_t)(const __attribute__((address_space(3))) void*)lds;
-  auto stage_addr = [&](int kt) { return lds0 + ((kt - kt0) & (kWgStages - 1)) * kWgStageB; };
+  auto stage_addr = [&](int kt) { return lds0 + ((unsigned)(kt - kt0) % ST) * kWgStageB; };
+  // the per-stage strides live in registers: read through P inside the loop, every DMA's
+  // "memory" clobber made the compiler reload them (s_load + s_waitcnt lgkmcnt(0) before each
+  // DMA pair, which also waited for the wave's in-flight LDS fragment reads: 181 -> 150 us)
+  const unsigned stra = (unsigned)(kWgK * P.lda * sizeof(bf16));
+  const unsigned strb = (unsigned)(kWgK * P.ldb * sizeof(bf16));
   auto issue_pair = [&](int kt, int j) {  // this wave's DMA pair j of stage kt
+    if constexpr (NODMA) return;
     const unsigned st = stage_addr(kt);
-    const unsigned sa = (unsigned)((size_t)kt * kWgK * P.lda * sizeof(bf16));
-    const unsigned sb = (unsigned)((size_t)kt * kWgK * P.ldb * sizeof(bf16));
+    const unsigned ktd = (unsigned)(HOT ? kt0 : kt);
+    const unsigned sa = ktd * stra;
+    const unsigned sb = ktd * strb;
     const unsigned r = (unsigned)(kWgDmaPerWave * w + 2 * j);
     gemm_dma(ra, st + r * 512, offa[j], sa);
-    gemm_dma(rb, st + kWgK * 512 + r * 512, offb[j], sb);
+    if constexpr (!NOB) gemm_dma(rb, st + kWgK * 512 + r * 512, offb[j], sb);
   };
 
   // fragment read addresses: lane 16q + 4ta + tp reads k-row b_q + ta (lo; + 8 hi), m columns
@@ -154,12 +172,12 @@ __global__ void __launch_bounds__(64 * kWgWaves, kWgWaves / 4) wgrad_kernel(Wgra
   // prologue: the first kWgStages stages in flight, stage 0 landed everywhere, its fragments read
   u32x4 fa[8], fb0[4], fb1[4];
   if (nk > 0) {
-    const int pro = nk < kWgStages ? nk : kWgStages;
+    const int pro = nk < ST ? nk : ST;
     for (int j = 0; j < pro; ++j) {
       issue_pair(kt0 + j, 0);
       issue_pair(kt0 + j, 1);
     }
-    gemm_vm_wait((pro - 1) * kWgDmaPerWave);
+    gemm_vm_wait(NOWAIT ? 0 : (pro - 1) * (NOB ? kWgDmaPerWave / 2 : kWgDmaPerWave));
     gemm_barrier();
     rd_b(kt0, fb0);
     rd_a(kt0, fa, 0, 8);
@@ -168,21 +186,34 @@ __global__ void __launch_bounds__(64 * kWgWaves, kWgWaves / 4) wgrad_kernel(Wgra
   // are read into the registers the previous group has just consumed (ONE A set), its B tiles
   // into the other B set, next to the refill of stage i's slot (two statically indexed B sets:
   // the loop runs two k-steps per trip)
-  auto kstep = [&](int i, u32x4 (&fb)[4], u32x4 (&nb_)[4]) {
+  // STEADY: a k-step with a refill (i + ST < nk), so its conditions and its counted wait are
+  // compile-time constants -- no branch cascade of gemm_vm_wait between the barrier-aligned
+  // waves' MFMA groups
+  auto kstep = [&](int i, u32x4 (&fb)[4], u32x4 (&nb_)[4], auto steady) {
+    constexpr bool STEADY = decltype(steady)::value;
     const int kt = kt0 + i;
-    const bool more = i + 1 < nk;
-    const bool refill = more && i + kWgStages < nk;
+    const bool more = STEADY || i + 1 < nk;
+    const bool refill = STEADY || (more && i + ST < nk);
     if (more) {
       // stage kt+1 landed (the later in-flight stages may stay outstanding), visible to every
       // wave; stage kt's slot was read by every wave before this barrier: it may be refilled
-      const int later = nk - 2 - i < kWgStages - 2 ? nk - 2 - i : kWgStages - 2;
-      gemm_vm_wait(later * kWgDmaPerWave);
-      gemm_barrier();
+      constexpr int per = NOB ? kWgDmaPerWave / 2 : kWgDmaPerWave;
+      if constexpr (NOWAIT) {
+      } else if constexpr (STEADY) {
+        gemm_vm_wait((ST - 2) * per);
+      } else {
+        const int later = nk - 2 - i < ST - 2 ? nk - 2 - i : ST - 2;
+        gemm_vm_wait(later * per);
+      }
+      if constexpr (V & 64)
+        asm volatile("s_barrier" ::: "memory");
+      else if constexpr (!NOBAR)
+        gemm_barrier();
     }
     __builtin_amdgcn_sched_barrier(0);
     mf(0, fa, fb);
     __builtin_amdgcn_sched_barrier(0);
-    if (refill) issue_pair(kt + kWgStages, 0);
+    if (refill) issue_pair(kt + ST, 0);
     if (more) {
       rd_b(kt + 1, nb_);
       rd_a(kt + 1, fa, 0, 2);
@@ -190,7 +221,7 @@ __global__ void __launch_bounds__(64 * kWgWaves, kWgWaves / 4) wgrad_kernel(Wgra
     __builtin_amdgcn_sched_barrier(0);
     mf(1, fa, fb);
     __builtin_amdgcn_sched_barrier(0);
-    if (refill) issue_pair(kt + kWgStages, 1);
+    if (refill) issue_pair(kt + ST, 1);
     if (more) rd_a(kt + 1, fa, 2, 4);
     __builtin_amdgcn_sched_barrier(0);
     mf(2, fa, fb);
@@ -201,9 +232,17 @@ __global__ void __launch_bounds__(64 * kWgWaves, kWgWaves / 4) wgrad_kernel(Wgra
     __builtin_amdgcn_sched_barrier(0);
     if (more) rd_a(kt + 1, fa, 6, 8);
   };
-  for (int i = 0; i < nk; i += 2) {
-    kstep(i, fb0, fb1);
-    if (i + 1 < nk) kstep(i + 1, fb1, fb0);
+  using steady_t = std::integral_constant<bool, true>;
+  using tail_t = std::integral_constant<bool, false>;
+  int i = 0;
+  if constexpr (!(V & 128))
+    for (; i + 1 + ST < nk; i += 2) {
+      kstep(i, fb0, fb1, steady_t{});
+      kstep(i + 1, fb1, fb0, steady_t{});
+    }
+  for (; i < nk; i += 2) {
+    kstep(i, fb0, fb1, tail_t{});
+    if (i + 1 < nk) kstep(i + 1, fb1, fb0, tail_t{});
   }
 
   // D[4q + r][l & 15] of tile (i, j): row m0 + wm + 16 i + 4 q + r, column n0 + wn + 16 j + l%16
@@ -255,7 +294,7 @@ void launch_wgrad(WgradArgs& a, hipStream_t s) {
   }
   a.items = items;
   const int grid = (items + 7) / 8 * 8;
-  wgrad_kernel<<<grid, 64 * kWgWaves, 0, s>>>(a);
+  wgrad_kernel<0><<<grid, 64 * kWgWaves, 0, s>>>(a);
 }
 
 }  // namespace dcr

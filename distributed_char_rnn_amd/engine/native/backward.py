@@ -25,9 +25,10 @@ class BackwardMixin:
                                                    want_logits=not (self.fused_head
                                                                     or self.wide_head),
                                                    logits_bias=not wide, extra_tasks=id_tasks)
-        # wide vocabulary: the embedding gradient's id sort (~10 small rocPRIM launches, ~50 us)
-        # runs on the side stream beside the (non-persistent) wide head instead of at the end
-        # of the backward; the main stream joins it before the persistent BPTT launches
+        # wide vocabulary: the embedding gradient's id sort (three counting-sort launches,
+        # csrc/embed.hip id_sort) runs on the side stream beside the (non-persistent) wide head
+        # instead of at the end of the backward; the main stream joins it before the
+        # persistent BPTT launches
         self._sorted_ids = None
         sort_ev = None
         if (self.V > SEG_LDS_MAX_V and self.knobs.on("seg_sort") and not self._dropout(True)
@@ -35,8 +36,7 @@ class BackwardMixin:
             side = self._side_stream()
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
-                sid, perm = torch.sort(ids_tm.view(-1))
-                self._sorted_ids = (sid, perm.int())
+                self._sorted_ids = self._sort_ids(ids_tm.view(-1))
                 sort_ev = torch.cuda.Event()
                 sort_ev.record(side)
             for t_ in self._sorted_ids:
@@ -85,7 +85,7 @@ class BackwardMixin:
                                logits if want_extras else None, bufs["hw_colpart"],
                                s.gview("rnnlm/softmax_b"), bufs["hw_part"], loss_buf)
             mm_tn(O, dlog, s.gview("rnnlm/softmax_w"), q=q)
-            dtop = mm_into(dlog, hd["Ws"].t(), bufs["dtop"].view(N, H)).view(T, B, H)
+            dtop = self._dtop_wide(dlog, bufs["dtop"].view(N, H)).view(T, B, H)
         elif wide:
             # wide vocabulary: one-read CE (bias added in-kernel), d softmax_b fused (xent_wide)
             self.ops.xent_wide(logits, hd["bs"], tgt, 1.0 / N, bufs["row_loss"], dlog,
@@ -94,7 +94,7 @@ class BackwardMixin:
             if want_extras:
                 logits += hd["bs"]
             mm_tn(O, dlog, s.gview("rnnlm/softmax_w"), q=q)
-            dtop = mm_into(dlog, hd["Ws"].t(), bufs["dtop"].view(N, H)).view(T, B, H)
+            dtop = self._dtop_wide(dlog, bufs["dtop"].view(N, H)).view(T, B, H)
         else:
             self.ops.xent(logits, tgt, 1.0 / N, bufs["row_loss"], dlog, bufs["xpart"], loss_buf)
             # ---- head gradients
@@ -421,11 +421,24 @@ class BackwardMixin:
             if self._sorted_ids is not None:  # sorted beside the head (train_step)
                 sid, perm = self._sorted_ids
             else:
-                sid, perm = torch.sort(ids)
-                perm = perm.int()
+                sid, perm = self._sort_ids(ids)
             self.ops.segsum(dX, sid, self.V, out, bufs["ws"], False, perm)
         else:
             self.ops.segsum(dX, ids, self.V, out, bufs["ws"], False)
+
+    def _sort_ids(self, ids: torch.Tensor):
+        """(sorted ids, source positions) as int32 -- torch.sort(ids, stable=True) -- by the
+        V-bucketed counting sort (csrc/embed.hip id_sort: histogram, scan, ballot-ranked
+        scatter) where the vocabulary fits its LDS histogram, else the library sort."""
+        n = ids.numel()
+        nws = int(self.ops.id_sort_workspace(n, self.V))
+        if nws and self.knobs.on("id_sort"):
+            i32 = dict(dtype=torch.int32, device=ids.device)
+            ws, sid, perm = torch.empty(nws, **i32), torch.empty(n, **i32), torch.empty(n, **i32)
+            self.ops.id_sort(ids.contiguous(), self.V, ws, sid, perm)
+            return sid, perm
+        sid, perm = torch.sort(ids, stable=True)
+        return sid, perm.int()
 
     def _token_norm(self, dx_tok: torch.Tensor) -> None:
         """TF clip-norm term of the embedding (ModelConfig.clip_norm == "tf"): the sum of
@@ -456,6 +469,17 @@ class BackwardMixin:
                                self.store.norm_slot_view())
             return
         self._token_norm(torch.mm(dZ, Wx.t()))
+
+    def _dtop_wide(self, dlog: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """dtop = dlogits · softmax_wᵀ (model.py:76's input gradient) for the wide vocabulary:
+        the token-norm pipeline's store form (csrc/tokennorm.hip gemm_nt, both operands
+        K = V-contiguous) where it tiles, else the library GEMM."""
+        Ws = self._head["Ws"]  # [H, V] bf16
+        N, V = dlog.shape
+        if self.knobs.on("dtop_nt") and int(self.ops.gemm_nt_supported(N, Ws.shape[0], V)):
+            self.ops.gemm_nt(dlog, Ws, out)
+            return out
+        return mm_into(dlog, Ws.t(), out)
 
     def _join_side(self) -> None:
         if self._side_used:

@@ -74,6 +74,10 @@ DEBUG_KEYS = {
              "wgrad kernel (csrc/wgrad.hip)",
     "tokennorm": "0: TF token-norm term as a library GEMM to bf16 rows + a sumsq launch instead "
                  "of the fused MFMA kernel (csrc/tokennorm.hip)",
+    "id_sort": "0: library sort of the wide-vocabulary segment-sum ids instead of the counting "
+               "sort (csrc/embed.hip id_sort)",
+    "dtop_nt": "0: wide-vocabulary dtop = dlogits·softmax_wᵀ as a library GEMM instead of the "
+               "token-norm pipeline's store form (csrc/tokennorm.hip gemm_nt)",
     "tail": "0: no fused step tail (csrc/tail.hip): prep-launch slab flush, library fp32 "
             "products, separate norm / Adam / weight-layout launches",
     "tail_queue": "1: tail launches take tiles from the atomic queue even on an unshared GPU",

@@ -117,3 +117,50 @@ def test_model_wide_head_matches_reference_v8192():
     assert abs(loss_l.item() - loss_n.item()) < 2e-3
     assert rel(ex["logits"], ex_l["logits"]) < 1e-3
     assert rel(g_wide, lib.store.grad) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,K,lda", [(2048, 512, 8192, 8192), (1024, 512, 1024, 1032),
+                                       (4096, 256, 256, 256)])
+def test_gemm_nt_matches_torch(M, N, K, lda, dcr_ops):
+    """gemm_nt (csrc/tokennorm.hip's pipeline storing its products): C = A · Bᵀ with both bf16
+    operands K-contiguous -- config 5's dtop = dlogits · softmax_wᵀ -- against fp32 torch on the
+    same bf16 operands (a row stride beyond K included)."""
+    assert dcr_ops.gemm_nt_supported(M, N, K)
+    g = torch.Generator(device="cuda").manual_seed(M + K)
+    A = torch.randn(M, lda, device="cuda", generator=g).bfloat16()[:, :K]
+    B = torch.randn(N, K, device="cuda", generator=g).bfloat16()
+    C = torch.full((M, N), float("nan"), device="cuda")
+    dcr_ops.gemm_nt(A, B, C)
+    torch.cuda.synchronize()
+    ref = A.float() @ B.float().t()
+    assert rel(C, ref) < 1e-5
+    assert not dcr_ops.gemm_nt_supported(M + 16, N, K)
+
+
+def test_model_wide_head_dtop_nt_matches_library():
+    """The wide head's dtop through gemm_nt (N = 1024 tokens tile it) against the library GEMM
+    (DCR_DEBUG dtop_nt=0): same loss, gradients equal up to fp32 summation order."""
+    import os
+
+    from distributed_char_rnn_amd.models.char_rnn import CharRNN
+    from distributed_char_rnn_amd.models.params import ModelConfig
+
+    B, T, H, V = 64, 16, 512, 8192
+    cfg = ModelConfig(model="lstm", vocab_size=V, rnn_size=H, num_layers=2)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randint(0, V, (B, T), device="cuda", dtype=torch.int32, generator=g)
+    y = torch.randint(0, V, (B, T), device="cuda", dtype=torch.int32, generator=g)
+    res = []
+    for dbg in (None, "dtop_nt=0"):
+        if dbg:
+            os.environ["DCR_DEBUG"] = dbg
+        try:
+            m = CharRNN(cfg, device="cuda", seed=5)
+        finally:
+            os.environ.pop("DCR_DEBUG", None)
+        assert m.backend.wide_head
+        loss, _, _ = m.backend.train_step(x, y, m.zero_state(B))
+        torch.cuda.synchronize()
+        res.append((loss.item(), m.store.grad.clone()))
+    assert abs(res[0][0] - res[1][0]) < 1e-6
+    assert rel(res[0][1], res[1][1]) < 1e-4
