@@ -27,6 +27,8 @@
 // wave's O rows), so a lane holds 4 consecutive vocab entries of one token.  softmax_wᵀ rows
 // arrive by LDS-DMA (one 1 KB buffer_load ... lds per row at H = 512) into a padded 1056-B row
 // stride: conflict-free ds_read_b128 fragment reads.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 #include "persist_common.h"
@@ -116,8 +118,10 @@ __device__ __forceinline__ HwMap hw_map(int g, int nblk) {
   return {g >> 1, g & 1};
 }
 
-// PASS 1: stats; PASS 2: lse, row loss, dlogits / logits, d softmax_b partials
-template <int KS, int PASS>
+// PASS 1: stats; PASS 2: lse, row loss, dlogits / logits, d softmax_b partials.  FL >= 0: the
+// argument flags at compile time (bit 0 softmax_b, 1 dlogits, 2 logits, 3 colpart; the training
+// step's combinations), so the per-tile counted waits are constants; FL = -1 reads them from a.
+template <int KS, int PASS, int FL>
 __global__ void __launch_bounds__(512, 1) head_wide_kernel(HeadWideArgs a) {
   static_assert(KS * 32 * 2 == 1024, "one 1 KB LDS-DMA instruction per vocab row (H = 512)");
   __shared__ __attribute__((aligned(16))) unsigned char wl[kHwBuf][kHwVt * kHwRow];
@@ -145,8 +149,9 @@ __global__ void __launch_bounds__(512, 1) head_wide_kernel(HeadWideArgs a) {
     const int n = n0 + 16 * tt + nl;
     y[tt] = (a.targets && n < N) ? a.targets[n] : -1;
   }
-  const bool grad = PASS == 2 && a.dlogits != nullptr;
-  const bool want_logits = PASS == 2 && a.logits != nullptr;
+  const bool grad = PASS == 2 && (FL < 0 ? a.dlogits != nullptr : (FL & 2) != 0);
+  const bool want_logits = PASS == 2 && (FL < 0 ? a.logits != nullptr : (FL & 4) != 0);
+  const bool has_colpart = FL < 0 ? a.colpart != nullptr : (FL & 8) != 0;
   float lse[2] = {0.f, 0.f};
   if constexpr (PASS == 2) {
     // merge the two halves' stats; the half-0 workgroups write the row losses
@@ -204,11 +209,14 @@ __global__ void __launch_bounds__(512, 1) head_wide_kernel(HeadWideArgs a) {
   // wave issues the same number of stores per tile (the counted vmcnt waits rely on it)
   const __amdgpu_buffer_rsrc_t rdl = make_rsrc(a.dlogits, sizeof(bf16) * (size_t)N * V);
   const __amdgpu_buffer_rsrc_t rlg = make_rsrc(a.logits, sizeof(float) * (size_t)N * V);
-  const bool has_bias = a.bias != nullptr;
-  // vector-memory operations this wave issues per tile: DMA rows (+ the bias row on wave 0) and
-  // pass-2 stores (dlogits, logits, the wave's colpart row)
-  const int dper = 4 + ((w == 0 && has_bias) ? 1 : 0);
-  const int sper = (grad ? 2 : 0) + (want_logits ? 4 : 0) + ((grad && a.colpart) ? 1 : 0);
+  const bool has_bias = FL < 0 ? a.bias != nullptr : (FL & 1) != 0;
+  // the bias row: wave 0 (FL < 0) or every wave (FL >= 0: the same 256 B into the same LDS
+  // words, so every wave's count is the same constant)
+  const bool bias_dma = has_bias && (FL >= 0 || w == 0);
+  // vector-memory operations this wave issues per tile: DMA rows (+ the bias row) and pass-2
+  // stores (dlogits, logits, the wave's colpart row)
+  const int dper = 4 + (bias_dma ? 1 : 0);
+  const int sper = (grad ? 2 : 0) + (want_logits ? 4 : 0) + ((grad && has_colpart) ? 1 : 0);
 
   // softmax_wᵀ rows of tile i into buffer i % 4: wave w DMAs rows [4 w, 4 w + 4); wave 0 also
   // the tile's softmax_b values.  Everything a tile reads arrives through this DMA.
@@ -222,7 +230,7 @@ __global__ void __launch_bounds__(512, 1) head_wide_kernel(HeadWideArgs a) {
           rw, (__attribute__((address_space(3))) void*)&wl[b][r * kHwRow], 16,
           (unsigned)(lane * 16), (unsigned)((size_t)(v0 + r) * H * sizeof(bf16)), 0, 0);
     }
-    if (w == 0 && has_bias)
+    if (bias_dma)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (__attribute__((address_space(3))) void*)&bl[b][0],
                                                4, (unsigned)(lane * 4),
                                                (unsigned)(v0 * sizeof(float)), 0, 0);
@@ -272,11 +280,29 @@ __global__ void __launch_bounds__(512, 1) head_wide_kernel(HeadWideArgs a) {
   // top of tile i: this wave's DMA of tile i has landed once only the operations issued after
   // it remain: the DMAs of tiles i+1, i+2 (those that exist) and the stores of tiles
   // max(0, i-3) .. i-1; then every wave's rows have landed after the barrier
-  auto wait_tile = [&](int i) {
-    const int nd = (i + 1 < ntile ? 1 : 0) + (i + 2 < ntile ? 1 : 0);
-    hw_vm_wait(nd * dper + (i < 3 ? i : 3) * sper);
-    hw_barrier();
-    if (i + 3 < ntile) load_tile(i + 3);  // into the buffer tile i-1 was read from
+  // A steady tile (3 <= i, i + 3 < ntile) has both later DMAs and three tiles of stores behind
+  // its own DMA: with the flags compile-time (FL >= 0) its count is a constant -- one s_waitcnt
+  // instead of hw_vm_wait's branch tree -- and its refill unconditional
+  auto wait_tile = [&](int i, auto steady) {
+    if constexpr (decltype(steady)::value) {
+      hw_vm_wait(2 * dper + 3 * sper);
+      hw_barrier();
+      load_tile(i + 3);
+    } else {
+      const int nd = (i + 1 < ntile ? 1 : 0) + (i + 2 < ntile ? 1 : 0);
+      hw_vm_wait(nd * dper + (i < 3 ? i : 3) * sper);
+      hw_barrier();
+      if (i + 3 < ntile) load_tile(i + 3);  // into the buffer tile i-1 was read from
+    }
+  };
+  auto run_tiles = [&](auto& body) {
+    using steady_t = std::integral_constant<bool, true>;
+    using edge_t = std::integral_constant<bool, false>;
+    int i = 0;
+    for (; i < ntile && i < 3; ++i) body(i, edge_t{});
+    if constexpr (FL >= 0)
+      for (; i + 3 < ntile; ++i) body(i, steady_t{});
+    for (; i < ntile; ++i) body(i, edge_t{});
   };
 
 #pragma unroll
@@ -286,8 +312,8 @@ __global__ void __launch_bounds__(512, 1) head_wide_kernel(HeadWideArgs a) {
   if constexpr (PASS == 1) {
     float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f}, ty[2] = {0.f, 0.f};
     float found[2] = {0.f, 0.f};
-    for (int i = 0; i < ntile; ++i) {
-      wait_tile(i);
+    auto body = [&](int i, auto steady) {
+      wait_tile(i, steady);
       f32x4 acc[2][2];
       tile_logits(i, acc);
 #pragma unroll
@@ -311,7 +337,8 @@ __global__ void __launch_bounds__(512, 1) head_wide_kernel(HeadWideArgs a) {
         m[tt] = mx;
         l[tt] = s;
       }
-    }
+    };
+    run_tiles(body);
     // merge the 4 lanes of each token (lanes nl, nl + 16, nl + 32, nl + 48)
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt) {
@@ -332,8 +359,8 @@ __global__ void __launch_bounds__(512, 1) head_wide_kernel(HeadWideArgs a) {
       }
     }
   } else {
-    for (int i = 0; i < ntile; ++i) {
-      wait_tile(i);
+    auto body = [&](int i, auto steady) {
+      wait_tile(i, steady);
       f32x4 acc[2][2];
       tile_logits(i, acc);
       float cs[16];  // this lane's column sums over its 2 tokens: [4 vt + r], 8..15 zero
@@ -380,7 +407,7 @@ __global__ void __launch_bounds__(512, 1) head_wide_kernel(HeadWideArgs a) {
           __builtin_amdgcn_raw_buffer_store_b128(rd[k], rdl, off, 0, 0);
         }
       }
-      if (grad && a.colpart) {
+      if (grad && has_colpart) {
         // over the wave's 16 token lanes: lane nl < 8 of lane group q ends with value nl =
         // 4 vt + r -> vocab 16 vt + 4 q + r of the tile, stored into the wave's own partial row
         // (no cross-wave step: the finalize kernel sums 8 rows per token block)
@@ -389,7 +416,8 @@ __global__ void __launch_bounds__(512, 1) head_wide_kernel(HeadWideArgs a) {
           a.colpart[(size_t)(mp.tb * 8 + w) * V + vbase + i * kHwVt + 16 * (nl >> 2) + 4 * q +
                     (nl & 3)] = sv;
       }
-    }
+    };
+    run_tiles(body);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0 && mp.half == 0 && a.partial) {
@@ -437,9 +465,19 @@ int launch_head_wide(const HeadWideArgs& a, float* db, float* loss_out, hipStrea
     if (a.colpart) c.colpart = a.colpart + (size_t)b0 * 8 * a.V;
     if (a.partial) c.partial = a.partial + b0;
     c.stats = a.stats + (size_t)(2 * kHwSplit + 1) * n0;
-    if (c.targets || c.dlogits)
-      hipLaunchKernelGGL((head_wide_kernel<16, 1>), dim3(cb * kHwSplit), dim3(512), 0, s, c);
-    hipLaunchKernelGGL((head_wide_kernel<16, 2>), dim3(cb * kHwSplit), dim3(512), 0, s, c);
+    // the training step's flags (softmax_b, dlogits, colpart, no logits) take the
+    // compile-time-flag kernels; other combinations the generic ones
+    const bool train = c.bias && c.dlogits && c.colpart && !c.logits && debug_int("hw_fl", 1);
+    if (c.targets || c.dlogits) {
+      if (train)
+        hipLaunchKernelGGL((head_wide_kernel<16, 1, 11>), dim3(cb * kHwSplit), dim3(512), 0, s, c);
+      else
+        hipLaunchKernelGGL((head_wide_kernel<16, 1, -1>), dim3(cb * kHwSplit), dim3(512), 0, s, c);
+    }
+    if (train)
+      hipLaunchKernelGGL((head_wide_kernel<16, 2, 11>), dim3(cb * kHwSplit), dim3(512), 0, s, c);
+    else
+      hipLaunchKernelGGL((head_wide_kernel<16, 2, -1>), dim3(cb * kHwSplit), dim3(512), 0, s, c);
   }
   launch_xent_finalize(a.partial, nb, a.N, loss_out, a.dlogits ? a.colpart : nullptr, 8 * nb, a.V,
                        db, s);

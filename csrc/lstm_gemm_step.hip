@@ -243,7 +243,10 @@ __global__ void __launch_bounds__(C::NW * 64, 1) lstm_gemm_step_kernel(BigStepAr
     } else if (it + 1 < nk) {
       // stage it+1 landed (only stage it+2 may still be in flight), every wave is done
       // reading stage it (retired above): refill its buffer with stage it+3
-      bs_vm_wait(it + 2 < nk ? C::DPW : 0);
+      if (it + 2 < nk)  // (a constant count per branch: no runtime-count switch in the loop)
+        bs_vm_wait(C::DPW);
+      else
+        bs_vm_wait0();
       bs_barrier();
       if (it + 3 < nk) dma(it + 3);
       reads(it + 1, 0, na, nb);

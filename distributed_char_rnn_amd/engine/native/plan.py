@@ -83,6 +83,9 @@ DEBUG_KEYS = {
     "tail_queue": "1: tail launches take tiles from the atomic queue even on an unshared GPU",
     "tail_per": "N: tail workgroups per CU (C++, default 2)",
     "gen_dbg": "1: generator without the head, 2: head without h loads (C++, timing only)",
+    "hw_fl": "0: wide head always on its generic kernels (runtime flags and counted-wait trees) "
+             "instead of the training step's compile-time-flag kernels (C++)",
+    "gnt_st": "5: gemm_nt (wide dtop) with a 5-stage ring (C++)",
     "tn_v": "token-norm GEMM: 3 (default) 8 waves, 4-stage ring; 5 the same with 5 stages; 4 four "
             "waves of 128 x 128 (C++)",
     "gru_ub": "1: 16-unit GRU workgroups (C++)",

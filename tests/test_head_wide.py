@@ -164,3 +164,32 @@ def test_model_wide_head_dtop_nt_matches_library():
         res.append((loss.item(), m.store.grad.clone()))
     assert abs(res[0][0] - res[1][0]) < 1e-6
     assert rel(res[0][1], res[1][1]) < 1e-4
+
+
+def test_head_wide_train_flags_kernel_identical(dcr_ops, monkeypatch):
+    """The training step's flag combination (softmax_b, dlogits, colpart, no logits) runs the
+    compile-time-flag kernels (constant counted waits, every wave DMAs the bias row); DCR_DEBUG
+    hw_fl=0 forces the generic ones: bitwise the same outputs."""
+    H, V, N = 512, 8192, 2048 + 77
+    g = torch.Generator(device="cuda").manual_seed(11)
+    O = (torch.randn(N, H, device="cuda", generator=g) * 0.5).bfloat16()
+    WsT = (torch.randn(V, H, device="cuda", generator=g) * 0.1).bfloat16()
+    bias = torch.randn(V, device="cuda", generator=g)
+    y = torch.randint(0, V, (N,), device="cuda", dtype=torch.int32, generator=g)
+
+    def run():
+        rl = torch.empty(N, device="cuda")
+        dl = torch.empty(N, V, dtype=torch.bfloat16, device="cuda")
+        colpart = torch.empty(dcr_ops.head_wide_colpart_rows(N) * V, device="cuda")
+        db = torch.empty(V, device="cuda")
+        part = torch.empty(dcr_ops.head_wide_workspace(N), device="cuda")
+        loss = torch.empty(1, device="cuda")
+        dcr_ops.head_wide(O, WsT, bias, y, 1.0 / N, rl, dl, None, colpart, db, part, loss)
+        torch.cuda.synchronize()
+        return rl, dl, db, loss
+
+    fast = run()
+    monkeypatch.setenv("DCR_DEBUG", "hw_fl=0")
+    generic = run()
+    for a, b in zip(fast, generic):
+        assert torch.equal(a, b)
