@@ -197,7 +197,7 @@ __global__ void __launch_bounds__(kHeadThreads) head_kernel(HeadArgs a) {
             const bf16 db = f2bf(valid && v < V ? d : 0.f);
             q[r] = (float)db;
             dbacc[vt][r] += q[r];
-            if (a.dlogits && valid && v < V) a.dlogits[(size_t)n * V + v] = db;
+            if (a.dlogits && valid && v < V) a.dlogits[(size_t)n * a.ldl + v] = db;
           }
           bf16x4 pk;
           pk[0] = f2bf(q[0]); pk[1] = f2bf(q[1]); pk[2] = f2bf(q[2]); pk[3] = f2bf(q[3]);

@@ -369,7 +369,9 @@ struct HeadArgs {
   float grad_scale;     // d loss / d logit scale (1/N for cost = sum/B/T)
   float* logits;        // [N, V] fp32 or nullptr
   float* row_loss;      // [N] or nullptr
-  bf16* dlogits;        // [N, V] bf16 or nullptr
+  bf16* dlogits;        // [N, ldl] bf16 (columns < V written) or nullptr
+  int ldl;              // dlogits row stride (V, or 256: the zero-padded operand of the
+                        //   softmax_w gradient's wgrad tile)
   float* dtop;          // [N, H] fp32 or nullptr
   float* part;          // [grid, VP+1] partials workspace
   const uint8_t* omask; // optional dropout bits of O ([N, H/8], dropout.hip): dtop is written

@@ -1255,7 +1255,18 @@ void head(const at::Tensor& O, const at::Tensor& WsT, const c10::optional<at::Te
   }
   if (has(logits)) { check_seq(*logits, at::kFloat, "logits"); TORCH_CHECK(logits->numel() == (int64_t)N * V, "logits must be [N, V]"); }
   if (has(row_loss)) { check_seq(*row_loss, at::kFloat, "row_loss"); TORCH_CHECK(row_loss->numel() == N, "row_loss must be [N]"); }
-  if (has(dlogits)) { check_seq(*dlogits, at::kBFloat16, "dlogits"); TORCH_CHECK(dlogits->numel() == (int64_t)N * V, "dlogits must be [N, V]"); }
+  int ldl = V;
+  if (has(dlogits)) {
+    // contiguous [N, V], or a [N, V] view of zero-padded rows (row stride ldl >= V)
+    const at::Tensor& d = *dlogits;
+    TORCH_CHECK(d.is_cuda() && d.scalar_type() == at::kBFloat16, "dlogits must be bf16 on the GPU");
+    if (d.dim() == 2 && d.size(0) == N && d.size(1) == V && d.stride(1) == 1) {
+      ldl = (int)d.stride(0);
+      TORCH_CHECK(ldl >= V, "dlogits: row stride below V");
+    } else {
+      TORCH_CHECK(d.is_contiguous() && d.numel() == (int64_t)N * V, "dlogits must be [N, V]");
+    }
+  }
   if (has(db)) { check_seq(*db, at::kFloat, "db"); TORCH_CHECK(db->numel() == V, "db must be [V]"); }
   if (has(loss)) { check_seq(*loss, at::kFloat, "loss"); TORCH_CHECK(loss->numel() >= 1, "loss must hold 1 float"); }
   check_seq(part, at::kFloat, "part");
@@ -1273,6 +1284,7 @@ void head(const at::Tensor& O, const at::Tensor& WsT, const c10::optional<at::Te
   a.logits = optr<float>(logits);
   a.row_loss = optr<float>(row_loss);
   a.dlogits = optr<bf16>(dlogits);
+  a.ldl = ldl;
   a.dtop = optr<float>(dtop);
   a.part = ptr<float>(part);
   if (has(omask)) {

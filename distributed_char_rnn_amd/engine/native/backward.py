@@ -6,7 +6,7 @@ from __future__ import annotations
 import torch
 
 from ...models.params import cell_specs
-from .gemm import SumQueue, f32, mm_into, mm_tn, mm_tn_cols, put
+from .gemm import SumQueue, f32, mm_into, mm_tn, mm_tn_cols, mm_tn_pad, put
 from .layouts import SEG_LDS_MAX_V
 from .tail import TailQueue
 
@@ -74,7 +74,10 @@ class BackwardMixin:
                           bufs["dtop"].view(N, H), s.gview("rnnlm/softmax_b"),
                           bufs["head_part"], loss_buf, head_omask,
                           dm["sout"] if dm is not None else 1.0)
-            mm_tn(O, dlog, s.gview("rnnlm/softmax_w"), q=q)
+            if bufs["dlogits_pad"] is not None:
+                mm_tn_pad(O, bufs["dlogits_pad"], s.gview("rnnlm/softmax_w"), q=q)
+            else:
+                mm_tn(O, dlog, s.gview("rnnlm/softmax_w"), q=q)
             if tail:  # d softmax_b (written by the head kernel): a norm term of the finalize
                 q.add_sumsq(s.gview("rnnlm/softmax_b"))
             dtop = bufs["dtop"].view(T, B, H)

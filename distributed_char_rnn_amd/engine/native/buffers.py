@@ -101,6 +101,7 @@ class BuffersMixin:
             pair_h=pair_h,
             logits=e(N, self.V),
             dlogits=e(N, self.V, dt=bf16) if training else None,
+            dlogits_pad=None,
             row_loss=e(N),
             xpart=e(self.ops.xent_num_partials(N)),
             loss=e(2, 4),  # two 16-B slots, ping-pong by step parity (see train_step)
@@ -145,6 +146,12 @@ class BuffersMixin:
             zring2=e(2 * Bp * GW, dt=bf16) if plan.pair_bwd else None,
             o_drop=e(N, H, dt=bf16) if (training and drop) else None,
         )
+        if training and self.fused_head and self.V <= 256 and self.knobs.on("dws_wgrad"):
+            # the fused head writes its bf16 dlogits into rows of 256 whose other columns stay
+            # zero: the softmax_w gradient Oᵀ·dlogits is then a [H x 256] problem of the step's
+            # wgrad launch (backward.py) instead of a library GEMM of its own
+            bufs["dlogits_pad"] = torch.zeros(N, 256, dtype=bf16, device=dev)
+            bufs["dlogits"] = bufs["dlogits_pad"][:, : self.V]
         # layers run by the persistent LSTM kernels (their final state is written into fresh
         # tensors, their bias gradients come from the kernels' db_part partials)
         npair = 2 * (self.L // 2) if plan.pair else 0

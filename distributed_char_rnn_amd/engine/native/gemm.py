@@ -87,7 +87,9 @@ class SumQueue:
         self.wgrad = wgrad
         self.gemms = []
 
-    def wgrad_ok(self, a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor]) -> bool:
+    def wgrad_ok(self, a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor],
+                 padded: bool = False) -> bool:
+        """``padded``: ``out`` takes the first out.shape[1] columns of aᵀ·b (b zero-padded)."""
         if not self.wgrad or out is None or out.dim() != 2 or out.stride(1) != 1:
             return False
         for t in (a, b):
@@ -100,11 +102,13 @@ class SumQueue:
         # peak (config 4 at B = 1024, [4096 x 8192] per layer pair: 439.7 vs 449.3 ms per step
         # with the hand-written kernel); up to WGRAD_MAX_TILES 256 x 256 tiles (the headline's
         # 32 + 16, config 5's 64) the hand-written one is at parity or ahead
-        return (b.shape[0] == K and tuple(out.shape) == (M, N)
+        shape_ok = (out.shape[0] == M and out.shape[1] <= N) if padded else tuple(out.shape) == (M, N)
+        return (b.shape[0] == K and shape_ok
                 and (M // 256) * (N // 256) <= WGRAD_MAX_TILES
                 and int(self.ops.wgrad_plan(1, M, N, K)) > 0)
 
     def add_gemm(self, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """aᵀ·b into ``out`` [M, N'] (N' <= b's N: the first N' columns -- b zero-padded)."""
         self.gemms.append((a, b, out))
         return out
 
@@ -125,7 +129,7 @@ class SumQueue:
                          for a, b, _ in chunk]
                 self.ops.wgrad([c[0] for c in chunk], [c[1] for c in chunk], parts)
                 for part, (_, _, out) in zip(parts, chunk):
-                    self.add_sum(part, out)
+                    self.add_sum(part[:, :, : out.shape[1]], out)
 
     def add_sum(self, part: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         self.tasks.append((part, out, self.SUM))
@@ -176,6 +180,18 @@ def mm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
         return q.add_sum(part, out)
     torch.sum(part, 0, out=out)
     return out
+
+
+def mm_tn_pad(a: torch.Tensor, b_pad: torch.Tensor, out: torch.Tensor, q: SumQueue) -> None:
+    """``out`` [M, n] = aᵀ·b_pad[:, :n] where b_pad's columns >= n are zero (the fused head's
+    dlogits rows padded to 256): a whole-tile problem of the queue's wgrad launch (the padding
+    costs that launch nothing while its grid stays under one workgroup per CU), else the
+    library GEMM on the n columns."""
+    K, M = a.shape
+    if q.wgrad_ok(a, b_pad, out, padded=True):
+        q.add_gemm(a, b_pad, out)
+        return
+    mm_tn(a, b_pad[:, : out.shape[1]], out, q=q)
 
 
 def mm_tn_cols(a: torch.Tensor, b: torch.Tensor, outs, q: SumQueue) -> None:

@@ -254,8 +254,8 @@ class TailQueue:
         self._signals = {}  # out data_ptr -> dependency counter its slab sum signals
 
     # -- the SumQueue interface used by gemm.mm_tn / backward._bias_sum ----------------------
-    def wgrad_ok(self, a, b, out) -> bool:
-        return self._gemmq.wgrad_ok(a, b, out)
+    def wgrad_ok(self, a, b, out, padded: bool = False) -> bool:
+        return self._gemmq.wgrad_ok(a, b, out, padded)
 
     def add_gemm(self, a, b, out):
         return self._gemmq.add_gemm(a, b, out)
