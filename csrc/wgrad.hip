@@ -63,7 +63,8 @@ __device__ __forceinline__ int wg_swz(int r) { return 2 * (r & 7) + ((r >> 4) & 
 // of whatever the ring holds), bit 2 (with bit 1) no barriers, bit 3 a 5-stage ring (160 KB),
 // bit 4 only the A panel is DMA'd, bit 5 the DMA is issued but never waited for, bit 6 the
 // k-step barrier without its lgkmcnt(0), bit 7 no steady-state k-steps (round-5 code: every
-// k-step's wait count chosen at run time)
+// k-step's wait count chosen at run time), bit 8 s_setprio(1) over each MFMA group, bit 9 the
+// refill DMA pairs after MFMA groups 1 and 2 (instead of 0 and 1)
 template <int V>
 __global__ void __launch_bounds__(64 * kWgWaves, kWgWaves / 4) wgrad_kernel(WgradArgs a) {
   constexpr bool HOT = V & 1, NODMA = V & 2, NOBAR = (V & 6) == 6, NOB = V & 16, NOWAIT = V & 34;
@@ -210,25 +211,33 @@ __global__ void __launch_bounds__(64 * kWgWaves, kWgWaves / 4) wgrad_kernel(Wgra
       else if constexpr (!NOBAR)
         gemm_barrier();
     }
+    constexpr bool PRIO = V & 256, LATE = V & 512;
+    auto mfp = [&](int g) {
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+      mf(g, fa, fb);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+    };
     __builtin_amdgcn_sched_barrier(0);
-    mf(0, fa, fb);
+    mfp(0);
     __builtin_amdgcn_sched_barrier(0);
-    if (refill) issue_pair(kt + ST, 0);
+    if (!LATE && refill) issue_pair(kt + ST, 0);
     if (more) {
       rd_b(kt + 1, nb_);
       rd_a(kt + 1, fa, 0, 2);
     }
     __builtin_amdgcn_sched_barrier(0);
-    mf(1, fa, fb);
+    mfp(1);
     __builtin_amdgcn_sched_barrier(0);
-    if (refill) issue_pair(kt + ST, 1);
+    if (!LATE && refill) issue_pair(kt + ST, 1);
+    if (LATE && refill) issue_pair(kt + ST, 0);
     if (more) rd_a(kt + 1, fa, 2, 4);
     __builtin_amdgcn_sched_barrier(0);
-    mf(2, fa, fb);
+    mfp(2);
     __builtin_amdgcn_sched_barrier(0);
+    if (LATE && refill) issue_pair(kt + ST, 1);
     if (more) rd_a(kt + 1, fa, 4, 6);
     __builtin_amdgcn_sched_barrier(0);
-    mf(3, fa, fb);
+    mfp(3);
     __builtin_amdgcn_sched_barrier(0);
     if (more) rd_a(kt + 1, fa, 6, 8);
   };

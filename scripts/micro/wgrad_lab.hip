@@ -73,6 +73,9 @@ int main() {
   Variant vars[] = {
       {"step (V=0)", wgrad_kernel<0>, true},
       {"runtime waits (r5)", wgrad_kernel<128>, true},
+      {"prio over MFMA groups", wgrad_kernel<256>, true},
+      {"DMA after groups 1, 2", wgrad_kernel<512>, true},
+      {"prio + late DMA", wgrad_kernel<768>, true},
       {"5-stage ring", wgrad_kernel<8>, true},
       {"L2-hot operands", wgrad_kernel<1>, false},
       {"no DMA", wgrad_kernel<2>, false},
