@@ -270,20 +270,22 @@ bool wgrad_supported(int M, int N, int K) {
 
 // One split count for a launch of problems with `tiles` output tiles in all (M, N multiples of
 // 256).  One workgroup per CU (128 KB of LDS ring), so a grid of tiles x S workgroups runs in
-// ceil(blocks / cus) rounds; pick the S with the best CU utilisation blocks / (rounds x cus),
-// less 1 % per slab (each slab is an extra M x N fp32 write + read in the finalize), each slab
-// at least 1024 tokens deep.  (A second partial round costs a full round: 3 x 16 tiles x 6
-// slabs = 288 workgroups ran 367 us vs 230 us at 5 slabs.)
+// ceil(blocks / cus) rounds of K / S tokens each; every slab adds an M x N fp32 write + read
+// (summed by the step tail).  Modelled time: rounds x (K / S) x 0.85 us per 32-token k-step
+// + S x tiles x 0.1 us, each slab at least 1024 tokens deep.  (A second partial round costs a
+// full round: 3 x 16 tiles x 6 slabs = 288 workgroups ran 367 us vs 230 us at 5 slabs.  The
+// round-5 score -- CU utilisation less 1 % per slab -- chose S = 1 for a 2-tile launch, one
+// bucket's softmax_w gradient under data parallelism: 2 workgroups, 639 us.)
 int wgrad_splits_tiles(int tiles, int K, int cus) {
   const int smax = K / 1024 > 1 ? (K / 1024 < kWgradMaxSplit ? K / 1024 : kWgradMaxSplit) : 1;
   int best = 1;
-  double best_score = -1.0;
+  double best_cost = 1e300;
   for (int S = 1; S <= smax; ++S) {
     const long blocks = (long)tiles * S;
     const long rounds = (blocks + cus - 1) / cus;
-    const double score = (double)blocks / ((double)rounds * cus) - 0.01 * S;
-    if (score > best_score + 1e-9) {
-      best_score = score;
+    const double cost = (double)rounds * ((double)K / S / kWgK) * 0.85 + 0.1 * S * tiles;
+    if (cost < best_cost - 1e-9) {
+      best_cost = cost;
       best = S;
     }
   }

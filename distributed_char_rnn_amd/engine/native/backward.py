@@ -52,7 +52,12 @@ class BackwardMixin:
         if on_ready is not None:
             cb_user = on_ready
 
+            gs = getattr(cb_user, "__self__", None)
+            probe = getattr(gs, "launches_at", None)
+
             def on_ready(off, _cb=cb_user):  # noqa: F811 - sums complete before a bucket leaves
+                if probe is not None and not probe(off):
+                    return  # completes no bucket: no flush (its sums join the next one)
                 q.flush()
                 _cb(off)
         P = bufs["plan"]
@@ -75,6 +80,9 @@ class BackwardMixin:
                           bufs["head_part"], loss_buf, head_omask,
                           dm["sout"] if dm is not None else 1.0)
             if bufs["dlogits_pad"] is not None:
+                # (data parallel: the softmax gradients' bucket also holds layer L-1's weight
+                # gradient, so this problem joins that layer's wgrad launch -- on_ready skips
+                # the flush of a report that completes no bucket)
                 mm_tn_pad(O, bufs["dlogits_pad"], s.gview("rnnlm/softmax_w"), q=q)
             else:
                 mm_tn(O, dlog, s.gview("rnnlm/softmax_w"), q=q)

@@ -111,6 +111,14 @@ class GradSync:
             self._ev_ready = []
             self._ev_end = None
 
+    def launches_at(self, upto: Optional[int] = None) -> bool:
+        """Whether ``ready(upto)`` would launch a bucket (the backward skips its deferred-sum
+        flush for a readiness report that completes none: one tail launch fewer)."""
+        if not self.enabled:
+            return False
+        lim = self.store.numel if upto is None else upto
+        return self._next < len(self.buckets) and self.buckets[self._next][1] <= lim
+
     def ready(self, upto: Optional[int] = None, sync: bool = False):
         """Launch every not-yet-launched bucket that ends at or below flat offset ``upto``
         (``None`` = everything).  ``sync``: as blocking collectives (c10d still runs them on

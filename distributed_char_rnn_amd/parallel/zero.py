@@ -149,6 +149,14 @@ class ShardedStep:
         self._work.clear()
         self.launched = []
 
+    def launches_at(self, upto: Optional[int] = None) -> bool:
+        """Whether ``ready(upto)`` would launch a bucket (the backward skips its deferred-sum
+        flush for a readiness report that completes none: one tail launch fewer)."""
+        if not self.enabled:
+            return False
+        lim = self.store.numel if upto is None else upto
+        return self._next < len(self.buckets) and self.buckets[self._next][1] <= lim
+
     def ready(self, upto: Optional[int] = None, sync: bool = False) -> None:
         """Launch the reduce-scatter of every not-yet-launched bucket ending at or below flat
         offset ``upto`` (None = everything); ``sync`` as blocking collectives on the caller's
