@@ -43,6 +43,11 @@ class CharRNN:
         if backend == "auto":
             # fp32 on the GPU runs the autograd oracle; the native kernels compute in bf16
             backend = "native" if (self.device.type == "cuda" and dtype != "fp32") else "reference"
+            if self.device.type == "cuda" and dtype == "fp32":
+                import warnings
+
+                warnings.warn("dtype fp32 on the GPU: running the PyTorch autograd path (fp32 "
+                              "hipBLASLt GEMMs); the native HIP kernels compute in bf16")
             if backend == "native" and cfg.rnn_size % 32 != 0 and cfg.model == "nas":
                 import warnings
 

@@ -60,7 +60,9 @@ def train_parser() -> argparse.ArgumentParser:
     g.add_argument("--device", default="auto", choices=["auto", "cpu", "cuda"],
                    help="execution device (auto = GPU when available)")
     g.add_argument("--dtype", default="auto", choices=["auto", "bf16", "fp32"],
-                   help="compute dtype of the GPU kernels (auto = bf16 on GPU, fp32 on CPU)")
+                   help="compute dtype (auto = bf16 on GPU, fp32 on CPU).  The native HIP kernels "
+                        "compute in bf16 (fp32 state and accumulation); fp32 on a GPU runs the "
+                        "PyTorch autograd path (hipBLASLt fp32 GEMMs) and says so at start-up")
     g.add_argument("--seed", type=int, default=0, help="parameter-init / dropout seed")
     g.add_argument("--log_every", type=int, default=1, help="print a progress line every N steps")
     g.add_argument("--summary_every", type=int, default=100,
