@@ -277,6 +277,7 @@ bool wgrad_supported(int M, int N, int K) {
 // round-5 score -- CU utilisation less 1 % per slab -- chose S = 1 for a 2-tile launch, one
 // bucket's softmax_w gradient under data parallelism: 2 workgroups, 639 us.)
 int wgrad_splits_tiles(int tiles, int K, int cus) {
+  if (cus <= 0) cus = 256;  // (no device: the MI355X's count)
   const int smax = K / 1024 > 1 ? (K / 1024 < kWgradMaxSplit ? K / 1024 : kWgradMaxSplit) : 1;
   int best = 1;
   double best_cost = 1e300;
