@@ -105,7 +105,8 @@ __global__ void __launch_bounds__(64 * kWgWaves, kWgWaves / 4) wgrad_kernel(Wgra
   auto stage_addr = [&](int kt) { return lds0 + ((unsigned)(kt - kt0) % ST) * kWgStageB; };
   // the per-stage strides live in registers: read through P inside the loop, every DMA's
   // "memory" clobber made the compiler reload them (s_load + s_waitcnt lgkmcnt(0) before each
-  // DMA pair, which also waited for the wave's in-flight LDS fragment reads: 181 -> 150 us)
+  // DMA pair, which also waits for the wave's in-flight LDS fragment reads; no measurable
+  // change on its own, profiles/r5_wgrad_lab.txt wl2 / wl3)
   const unsigned stra = (unsigned)(kWgK * P.lda * sizeof(bf16));
   const unsigned strb = (unsigned)(kWgK * P.ldb * sizeof(bf16));
   auto issue_pair = [&](int kt, int j) {  // this wave's DMA pair j of stage kt
