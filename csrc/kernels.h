@@ -351,7 +351,7 @@ struct WgradArgs {
 };
 bool wgrad_supported(int M, int N, int K);
 int wgrad_splits(int np, int M, int N, int K, int cus);
-int wgrad_splits_tiles(int tiles, int K, int cus);
+int wgrad_splits_tiles(int tiles, int K, int cus, double* cost_out = nullptr);  // (+ modelled us)
 void launch_wgrad(WgradArgs& a, hipStream_t s);
 int gru_persist_ub(int H, int B, int cus);
 int gru_persist_rows(int H, int B, int cus);  // padded batch rows of the launch plan (rings)

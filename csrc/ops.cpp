@@ -1827,6 +1827,10 @@ TORCH_LIBRARY(dcr, m) {
   m.def("wgrad(Tensor[] A, Tensor[] B, Tensor(a!)[] part) -> ()");
   m.def("wgrad_plan_tiles(int tiles, int K) -> int", [](int64_t tiles, int64_t K) -> int64_t {
     return dcr::wgrad_splits_tiles((int)tiles, (int)K, num_cus()); });
+  m.def("wgrad_plan_cost(int tiles, int K) -> float", [](int64_t tiles, int64_t K) -> double {
+    double c = 0.0;
+    dcr::wgrad_splits_tiles((int)tiles, (int)K, num_cus(), &c);
+    return c; });
   m.def("wgrad_plan(int np, int M, int N, int K) -> int",
         [](int64_t np, int64_t M, int64_t N, int64_t K) -> int64_t {
           if (!dcr::wgrad_supported((int)M, (int)N, (int)K)) return 0;

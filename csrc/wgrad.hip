@@ -277,7 +277,7 @@ bool wgrad_supported(int M, int N, int K) {
 // full round: 3 x 16 tiles x 6 slabs = 288 workgroups ran 367 us vs 230 us at 5 slabs.  The
 // round-5 score -- CU utilisation less 1 % per slab -- chose S = 1 for a 2-tile launch, one
 // bucket's softmax_w gradient under data parallelism: 2 workgroups, 639 us.)
-int wgrad_splits_tiles(int tiles, int K, int cus) {
+int wgrad_splits_tiles(int tiles, int K, int cus, double* cost_out) {
   if (cus <= 0) cus = 256;  // (no device: the MI355X's count)
   const int smax = K / 1024 > 1 ? (K / 1024 < kWgradMaxSplit ? K / 1024 : kWgradMaxSplit) : 1;
   int best = 1;
@@ -291,6 +291,7 @@ int wgrad_splits_tiles(int tiles, int K, int cus) {
       best = S;
     }
   }
+  if (cost_out) *cost_out = tiles > 0 ? best_cost : 0.0;
   return best;
 }
 

@@ -107,9 +107,16 @@ class SumQueue:
                 and (M // 256) * (N // 256) <= WGRAD_MAX_TILES
                 and int(self.ops.wgrad_plan(1, M, N, K)) > 0)
 
-    def add_gemm(self, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
-        """aᵀ·b into ``out`` [M, N'] (N' <= b's N: the first N' columns -- b zero-padded)."""
-        self.gemms.append((a, b, out))
+    # modelled cost (us) of computing an optional problem elsewhere (the softmax_w gradient's
+    # library GEMM: ~20 us in the headline trace)
+    OPTIONAL_ELSEWHERE_US = 20.0
+
+    def add_gemm(self, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor,
+                 fallback=None) -> torch.Tensor:
+        """aᵀ·b into ``out`` [M, N'] (N' <= b's N: the first N' columns -- b zero-padded).
+        ``fallback``: the problem is optional -- if its tiles would push the launch into a
+        worse split (e.g. a second round of workgroups), ``fallback()`` computes it instead."""
+        self.gemms.append((a, b, out, fallback))
         return out
 
     def _run_gemms(self) -> None:
@@ -117,10 +124,26 @@ class SumQueue:
         one token count per launch, whatever their shapes (the step's layer-1 [2H x 4H] and
         layer-0 [H x 4H] gradients share one grid), one split count for the launch."""
         groups = {}
-        for a, b, out in self.gemms:
-            groups.setdefault(a.shape[0], []).append((a, b, out))
+        for a, b, out, fb in self.gemms:
+            groups.setdefault(a.shape[0], []).append((a, b, out, fb))
         self.gemms = []
+        tiles_of = lambda t: (t[0].shape[1] // 256) * (t[1].shape[1] // 256)  # noqa: E731
         for K, items in groups.items():
+            opt = [t for t in items if t[3] is not None]
+            if opt and len(items) <= 4:
+                # drop the optional problems when the launch without them (plus their own
+                # routes) is modelled cheaper: the dropout headline's 64 + 2 tiles would need
+                # a second round of workgroups (S = 7) where 64 tiles fill one (S = 4)
+                t_all = sum(tiles_of(t) for t in items)
+                t_req = t_all - sum(tiles_of(t) for t in opt)
+                c_all = float(self.ops.wgrad_plan_cost(t_all, K))
+                c_req = (float(self.ops.wgrad_plan_cost(t_req, K)) if t_req else 0.0) \
+                    + self.OPTIONAL_ELSEWHERE_US * len(opt)
+                if c_req < c_all:
+                    for t in opt:
+                        t[3]()
+                    items = [t for t in items if t[3] is None]
+            items = [t[:3] for t in items]
             for i in range(0, len(items), 4):  # csrc/kernels.h kWgradMaxProblems
                 chunk = items[i: i + 4]
                 tiles = sum((a.shape[1] // 256) * (b.shape[1] // 256) for a, b, _ in chunk)
@@ -188,10 +211,13 @@ def mm_tn_pad(a: torch.Tensor, b_pad: torch.Tensor, out: torch.Tensor, q: SumQue
     costs that launch nothing while its grid stays under one workgroup per CU), else the
     library GEMM on the n columns."""
     K, M = a.shape
+    def library():
+        mm_tn(a, b_pad[:, : out.shape[1]], out, q=q)
+
     if q.wgrad_ok(a, b_pad, out, padded=True):
-        q.add_gemm(a, b_pad, out)
+        q.add_gemm(a, b_pad, out, fallback=library)
         return
-    mm_tn(a, b_pad[:, : out.shape[1]], out, q=q)
+    library()
 
 
 def mm_tn_cols(a: torch.Tensor, b: torch.Tensor, outs, q: SumQueue) -> None:

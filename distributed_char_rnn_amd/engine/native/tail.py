@@ -257,8 +257,8 @@ class TailQueue:
     def wgrad_ok(self, a, b, out, padded: bool = False) -> bool:
         return self._gemmq.wgrad_ok(a, b, out, padded)
 
-    def add_gemm(self, a, b, out):
-        return self._gemmq.add_gemm(a, b, out)
+    def add_gemm(self, a, b, out, fallback=None):
+        return self._gemmq.add_gemm(a, b, out, fallback)
 
     def add_sum(self, part, out, sig: int = -1):
         if sig < 0:
