@@ -1551,6 +1551,43 @@ void tokennorm(const at::Tensor& dz, const at::Tensor& w, at::Tensor& part, at::
   dcr::launch_tokennorm(a, cur_stream());
 }
 
+// dropout route's embedding input gradient (tokennorm.hip, masked form): dx [N, H] bf16 =
+// (dz · wᵀ) ⊙ mask · scale and out[0] = sum of the squares of dx's values, in one launch
+void tokennorm_masked(const at::Tensor& dz, const at::Tensor& w, const at::Tensor& mask,
+                      double scale, at::Tensor& dx, at::Tensor& part, at::Tensor& ticket,
+                      at::Tensor& out) {
+  for (const at::Tensor* t : {&dz, &w}) {
+    CHECK_DEV(*t); CHECK_BF16(*t);
+    TORCH_CHECK(t->dim() == 2 && t->stride(1) == 1 && t->stride(0) % 8 == 0 &&
+                    (reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0,
+                "tokennorm_masked: 2-D bf16 views with 16-B aligned rows");
+  }
+  const int N = (int)dz.size(0), K = (int)dz.size(1), H = (int)w.size(0);
+  TORCH_CHECK(w.size(1) == K, "tokennorm_masked: dz [N, K], w [H, K]");
+  TORCH_CHECK(dcr::tokennorm_supported(N, H, K), "tokennorm_masked: unsupported shape N=", N,
+              " H=", H, " K=", K);
+  TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == at::kByte && mask.is_contiguous() &&
+                  mask.numel() == (int64_t)N * (H / 8) &&
+                  (reinterpret_cast<uintptr_t>(mask.data_ptr()) & 7) == 0,
+              "tokennorm_masked: mask must be uint8 [N, H/8] bits, 8-B aligned");
+  CHECK_DEV(dx); CHECK_BF16(dx);
+  TORCH_CHECK(dx.dim() == 2 && dx.size(0) == N && dx.size(1) == H && dx.stride(1) == 1,
+              "tokennorm_masked: dx [N, H] with unit column stride");
+  CHECK_DEV(part); CHECK_F32(part);
+  TORCH_CHECK(part.numel() >= dcr::kTokenNormMaxGrid, "tokennorm_masked: part too small");
+  CHECK_DEV(ticket); CHECK_I32(ticket); CHECK_DEV(out); CHECK_F32(out);
+  dcr::TokenNormArgs a{};
+  a.dz = ptr<bf16>(dz); a.ld_dz = dz.stride(0);
+  a.w = ptr<bf16>(w); a.ld_w = w.stride(0);
+  a.N = N; a.N_units = H; a.K = K;
+  a.part = ptr<float>(part);
+  a.ticket = reinterpret_cast<unsigned*>(ticket.data_ptr());
+  a.out = ptr<float>(out);
+  a.mask = mask.data_ptr<uint8_t>();
+  a.cb = ptr<bf16>(dx); a.ldc = dx.stride(0); a.mscale = (float)scale;
+  dcr::launch_tokennorm(a, cur_stream());
+}
+
 // C [M, N] fp32 = a [M, K] · bᵀ (b [N, K]), both bf16 K-contiguous (tokennorm.hip's pipeline)
 void gemm_nt(const at::Tensor& a_, const at::Tensor& b, at::Tensor& c) {
   for (const at::Tensor* t : {&a_, &b}) {
@@ -1811,6 +1848,8 @@ TORCH_LIBRARY(dcr, m) {
           return dcr::generate_supported((int)L, (int)H, (int)V, (int)S, num_cus()); });
   m.def("tokennorm(Tensor dz, Tensor w, Tensor(a!) part, Tensor(b!) ticket, Tensor(c!) out) -> ()");
   m.def("gemm_nt(Tensor a, Tensor b, Tensor(a!) c) -> ()");
+  m.def("tokennorm_masked(Tensor dz, Tensor w, Tensor mask, float scale, Tensor(a!) dx, "
+        "Tensor(b!) part, Tensor(c!) ticket, Tensor(d!) out) -> ()");
   m.def("id_sort(Tensor ids, int V, Tensor(a!) ws, Tensor(b!) sid, Tensor(c!) perm) -> ()");
   m.def("id_sort_workspace(int N, int V) -> int", [](int64_t N, int64_t V) -> int64_t {
     return V > 0 && V <= 16384 && N > 0 && N <= 65535
@@ -1913,6 +1952,7 @@ TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("generate", &generate);
   m.impl("tokennorm", &tokennorm);
   m.impl("gemm_nt", &gemm_nt);
+  m.impl("tokennorm_masked", &tokennorm_masked);
   m.impl("id_sort", &id_sort);
   m.impl("wgrad", &wgrad);
   m.impl("gru_persist_fwd", &gru_persist_fwd);

@@ -38,8 +38,13 @@ constexpr int kTnTile = 256, kTnK = 32, kTnStages = 4, kTnWaves = 8;
 constexpr int kTnStageB = 2 * kTnTile * kTnK * 2;   // A + B panels, bytes
 constexpr int kTnDmaPerWave = 32 / kTnWaves;
 
-template <int NST, bool STORE>
+// MODE 0: the sum of squares; 1: the products stored as fp32 C (gemm_nt); 2: the products
+// masked by dropout bits, scaled, stored as bf16 C and their sum of squares (the dropout
+// route's embedding input gradient dX = (dZ0·W_x0ᵀ) ⊙ mask / keep and its TF token-norm term,
+// one launch instead of a library GEMM, a mask pass and a sum-of-squares pass)
+template <int NST, int MODE>
 __global__ void __launch_bounds__(64 * kTnWaves, kTnWaves / 4) tokennorm_kernel(TokenNormArgs a) {
+  constexpr bool STORE = MODE == 1;
   // ONE shared array (a second __shared__ object beside a DMA ring can make the compiler wait
   // vmcnt(0) in front of the k-step's first LDS read): the ring, then the reduction words
   // (the reduction words reuse the ring after the main loop: NST = 5 fills all 160 KB)
@@ -191,12 +196,42 @@ __global__ void __launch_bounds__(64 * kTnWaves, kTnWaves / 4) tokennorm_kernel(
   // epilogue (the host requires N % 256 == 0: no ragged tile): the sum of squares of this
   // workgroup's 256 x 256 outputs
   float sq = 0.f;
+  if constexpr (MODE == 2) {
+    // lane (q, l%16) of tile (i, j) holds row m0 + wm + 16 i + 4 q + r, column c = n0 + wn +
+    // 16 j + l%16: mask byte c / 8 = (n0 + wn) / 8 + 2 j + (l%16) / 8, bit c & 7 = l & 7, so
+    // one 8-byte load per row covers the lane's four j; all 32 loads before any store
+    const int H8 = a.N_units / 8;
+    const int q4 = 4 * (lane >> 4), e = (lane & 15) >> 3, bit = lane & 7;
+    const uint8_t* mrow = a.mask + (size_t)(m0 + wm + q4) * H8 + (n0 + wn) / 8;
+    unsigned long long mw[8][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+      for (int r = 0; r < 4; ++r)
+        mw[i][r] = *reinterpret_cast<const unsigned long long*>(mrow + (size_t)(16 * i + r) * H8);
+    bf16* crow = a.cb + (size_t)(m0 + wm + q4) * a.ldc + n0 + wn + (lane & 15);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sq += acc[i][j][r] * acc[i][j][r];
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          // (the GEMM's bf16 rounding, then the mask pass's: the values of the unfused route)
+          const unsigned byte = (unsigned)(mw[i][r] >> (8 * (2 * j + e))) & 0xFFu;
+          const float v1 = bf2f(f2bf(acc[i][j][r]));
+          const bf16 v2 = f2bf((byte >> bit) & 1u ? v1 * a.mscale : 0.f);
+          crow[(size_t)(16 * i + r) * a.ldc + 16 * j] = v2;
+          const float f = bf2f(v2);
+          sq += f * f;
+        }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sq += acc[i][j][r] * acc[i][j][r];
+  }
   sq = wave_sum(sq);
   if (lane == 0) red[w] = sq;
   __syncthreads();
@@ -375,12 +410,14 @@ bool tokennorm_supported(int N, int H, int K) {
 void launch_tokennorm(const TokenNormArgs& a, hipStream_t s) {
   const int grid = (a.N / kTnTile) * (a.N_units / kTnTile);
   const int v = debug_int("tn_v", 3);
-  if (v == 4)
+  if (a.mask)  // (the masked form has the default geometry only)
+    tokennorm_kernel<4, 2><<<grid, 64 * kTnWaves, 0, s>>>(a);
+  else if (v == 4)
     tokennorm4_kernel<<<grid, 64 * kT4Waves, 0, s>>>(a);
   else if (v == 5)
-    tokennorm_kernel<5, false><<<grid, 64 * kTnWaves, 0, s>>>(a);
+    tokennorm_kernel<5, 0><<<grid, 64 * kTnWaves, 0, s>>>(a);
   else
-    tokennorm_kernel<4, false><<<grid, 64 * kTnWaves, 0, s>>>(a);
+    tokennorm_kernel<4, 0><<<grid, 64 * kTnWaves, 0, s>>>(a);
 }
 
 bool gemm_nt_supported(int M, int N, int K) {
@@ -391,9 +428,9 @@ bool gemm_nt_supported(int M, int N, int K) {
 void launch_gemm_nt(const TokenNormArgs& a, hipStream_t s) {
   const int grid = (a.N / kTnTile) * (a.N_units / kTnTile);
   if (debug_int("gnt_st", 4) == 5)
-    tokennorm_kernel<5, true><<<grid, 64 * kTnWaves, 0, s>>>(a);
+    tokennorm_kernel<5, 1><<<grid, 64 * kTnWaves, 0, s>>>(a);
   else
-    tokennorm_kernel<4, true><<<grid, 64 * kTnWaves, 0, s>>>(a);
+    tokennorm_kernel<4, 1><<<grid, 64 * kTnWaves, 0, s>>>(a);
 }
 
 }  // namespace dcr

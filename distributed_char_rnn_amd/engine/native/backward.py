@@ -323,11 +323,23 @@ class BackwardMixin:
                         on_ready(s.layer_range(layer)[1])
                     dtop = None
                     continue
-                if layer > 0:
+                fused_dx = (layer == 0 and dm is not None and dm["inb"][0] is not None
+                             and self.tf_norm and self.knobs.on("dx_fused")
+                             and int(self.ops.tokennorm_supported(N, H, dZx.shape[1])))
+                if fused_dx:
+                    # one launch: dX = (dZ0·W_x0ᵀ) ⊙ mask / keep as bf16 rows and its TF
+                    # token-norm term into the norm slot (csrc/tokennorm.hip masked form)
+                    ws = self._tn_workspace()
+                    self.ops.tokennorm_masked(dZx, lw.Wx, dm["inb"][0].view(-1), dm["sin"],
+                                              bufs["dx_bf"].view(N, H), ws[0], ws[1],
+                                              self.store.norm_slot_view())
+                    dX = bufs["dx_bf"].view(T, B, H)
+                elif layer > 0:
                     dX = mm_into(dZx, lw.Wx.t(), bufs["dx"].view(N, H)).view(T, B, H)
                 else:  # only the embedding gradient reads it: bf16 rows for the segment sum
                     dX = torch.mm(dZx, lw.Wx.t(), out=bufs["dx_bf"]).view(T, B, H)
-                if dm is not None and dm["inb"][layer] is not None:  # this layer's input mask
+                if (not fused_dx and dm is not None
+                        and dm["inb"][layer] is not None):  # this layer's input mask
                     dX = self._masked(dX, dm["inb"][layer], dm["sin"], out=dX).view(T, B, H)
                 if layer > 0:
                     dtop = dX
@@ -336,7 +348,8 @@ class BackwardMixin:
                     # fp32 either way)
                     dXt = dX.reshape(N, H)
                     self._embed_grad(dXt, ids_tm, bufs)
-                    self._token_norm(dXt)
+                    if not fused_dx:  # (else written by the masked token-norm launch)
+                        self._token_norm(dXt)
             if not written:
                 self._write_input_grads(layer, names, dWx, dbias)
             if layer == 0:
@@ -473,13 +486,18 @@ class BackwardMixin:
             return
         N, K = dZ.shape
         if self.knobs.on("tokennorm") and int(self.ops.tokennorm_supported(N, Wx.shape[0], K)):
-            if self._tn_ws is None:
-                self._tn_ws = (torch.empty(1024, dtype=f32, device=self.dev),
-                               torch.zeros(1, dtype=torch.int32, device=self.dev))
-            self.ops.tokennorm(dZ, Wx, self._tn_ws[0], self._tn_ws[1],
-                               self.store.norm_slot_view())
+            ws = self._tn_workspace()
+            self.ops.tokennorm(dZ, Wx, ws[0], ws[1], self.store.norm_slot_view())
             return
         self._token_norm(torch.mm(dZ, Wx.t()))
+
+    def _tn_workspace(self):
+        """Partials + ticket of the token-norm launches (the ticket starts at zero and every
+        launch leaves it at zero)."""
+        if self._tn_ws is None:
+            self._tn_ws = (torch.empty(1024, dtype=f32, device=self.dev),
+                           torch.zeros(1, dtype=torch.int32, device=self.dev))
+        return self._tn_ws
 
     def _dtop_wide(self, dlog: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         """dtop = dlogits · softmax_wᵀ (model.py:76's input gradient) for the wide vocabulary:

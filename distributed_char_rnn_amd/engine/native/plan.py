@@ -74,6 +74,8 @@ DEBUG_KEYS = {
              "wgrad kernel (csrc/wgrad.hip)",
     "tokennorm": "0: TF token-norm term as a library GEMM to bf16 rows + a sumsq launch instead "
                  "of the fused MFMA kernel (csrc/tokennorm.hip)",
+    "dx_fused": "0: dropout route's embedding input gradient as a library GEMM + mask pass + "
+                "sum-of-squares pass instead of the masked token-norm launch",
     "dws_wgrad": "0: softmax_w gradient (fused head) as a library GEMM instead of a zero-padded "
                  "[H x 256] problem of the wgrad launch",
     "id_sort": "0: library sort of the wide-vocabulary segment-sum ids instead of the counting "

@@ -206,3 +206,30 @@ def test_tokennorm_kernel(dcr_ops, N, H):
     ref = float(((dz.double() @ w.double().t()) ** 2).sum())
     assert abs(float(out) - ref) / ref < 1e-4
     assert int(ticket.item()) == 0
+
+
+@pytest.mark.parametrize("N,H", [(2048, 256), (32768, 512)])
+def test_tokennorm_masked_kernel(dcr_ops, N, H):
+    """Masked form (the dropout route's embedding input gradient): dx = bf16 of (dz·wᵀ) ⊙ mask
+    / keep as the library GEMM (bf16 output) + mask pass would write it, and sum(dx²) in the
+    same launch."""
+    torch.manual_seed(12)
+    K, keep = 4 * H, 0.8
+    dz = (torch.randn(N, K, device="cuda") * 0.1).to(torch.bfloat16)
+    w = (torch.randn(H, K, device="cuda") * 0.05).to(torch.bfloat16)
+    bits = (torch.rand(N, H, device="cuda") < keep)
+    packed = (bits.view(N, H // 8, 8).to(torch.int32)
+              * (2 ** torch.arange(8, device="cuda", dtype=torch.int32))).sum(-1).to(torch.uint8)
+    part = torch.empty(1024, device="cuda")
+    ticket = torch.zeros(1, dtype=torch.int32, device="cuda")
+    out = torch.zeros(1, device="cuda")
+    dx = torch.full((N, H), float("nan"), device="cuda").to(torch.bfloat16)
+    dcr_ops.tokennorm_masked(dz, w, packed.view(-1), 1.0 / keep, dx, part, ticket, out)
+    torch.cuda.synchronize()
+    ref = ((dz.float() @ w.float().t()).to(torch.bfloat16).float() * (1.0 / keep))
+    ref = torch.where(bits, ref, torch.zeros_like(ref)).to(torch.bfloat16).float()
+    err = ((dx.float() - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, err  # (fp32 accumulation order differs from the reference GEMM)
+    assert torch.equal(dx.float() == 0, ~bits | (ref == 0))
+    assert abs(float(out) - float((dx.float() ** 2).sum())) / float(out) < 1e-4
+    assert int(ticket.item()) == 0
