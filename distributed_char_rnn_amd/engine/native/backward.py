@@ -324,6 +324,7 @@ class BackwardMixin:
                     dtop = None
                     continue
                 fused_dx = (layer == 0 and dm is not None and dm["inb"][0] is not None
+                             and dm["inb"][0].data_ptr() % 8 == 0
                              and self.tf_norm and self.knobs.on("dx_fused")
                              and int(self.ops.tokennorm_supported(N, H, dZx.shape[1])))
                 if fused_dx:
