@@ -1588,6 +1588,37 @@ void tokennorm_masked(const at::Tensor& dz, const at::Tensor& w, const at::Tenso
   dcr::launch_tokennorm(a, cur_stream());
 }
 
+// wide-vocabulary route's embedding input gradient (tokennorm.hip, storing form): dx [N, H]
+// fp32 = dz · wᵀ and out[0] = sum of its squares, in one launch
+void tokennorm_store(const at::Tensor& dz, const at::Tensor& w, at::Tensor& dx, at::Tensor& part,
+                     at::Tensor& ticket, at::Tensor& out) {
+  for (const at::Tensor* t : {&dz, &w}) {
+    CHECK_DEV(*t); CHECK_BF16(*t);
+    TORCH_CHECK(t->dim() == 2 && t->stride(1) == 1 && t->stride(0) % 8 == 0 &&
+                    (reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0,
+                "tokennorm_store: 2-D bf16 views with 16-B aligned rows");
+  }
+  const int N = (int)dz.size(0), K = (int)dz.size(1), H = (int)w.size(0);
+  TORCH_CHECK(w.size(1) == K, "tokennorm_store: dz [N, K], w [H, K]");
+  TORCH_CHECK(dcr::tokennorm_supported(N, H, K), "tokennorm_store: unsupported shape N=", N,
+              " H=", H, " K=", K);
+  CHECK_DEV(dx); CHECK_F32(dx);
+  TORCH_CHECK(dx.dim() == 2 && dx.size(0) == N && dx.size(1) == H && dx.stride(1) == 1,
+              "tokennorm_store: dx [N, H] with unit column stride");
+  CHECK_DEV(part); CHECK_F32(part);
+  TORCH_CHECK(part.numel() >= dcr::kTokenNormMaxGrid, "tokennorm_store: part too small");
+  CHECK_DEV(ticket); CHECK_I32(ticket); CHECK_DEV(out); CHECK_F32(out);
+  dcr::TokenNormArgs a{};
+  a.dz = ptr<bf16>(dz); a.ld_dz = dz.stride(0);
+  a.w = ptr<bf16>(w); a.ld_w = w.stride(0);
+  a.N = N; a.N_units = H; a.K = K;
+  a.part = ptr<float>(part);
+  a.ticket = reinterpret_cast<unsigned*>(ticket.data_ptr());
+  a.out = ptr<float>(out);
+  a.c = ptr<float>(dx); a.ldc = dx.stride(0);
+  dcr::launch_tokennorm(a, cur_stream());
+}
+
 // C [M, N] fp32 = a [M, K] · bᵀ (b [N, K]), both bf16 K-contiguous (tokennorm.hip's pipeline)
 void gemm_nt(const at::Tensor& a_, const at::Tensor& b, at::Tensor& c) {
   for (const at::Tensor* t : {&a_, &b}) {
@@ -1848,6 +1879,8 @@ TORCH_LIBRARY(dcr, m) {
           return dcr::generate_supported((int)L, (int)H, (int)V, (int)S, num_cus()); });
   m.def("tokennorm(Tensor dz, Tensor w, Tensor(a!) part, Tensor(b!) ticket, Tensor(c!) out) -> ()");
   m.def("gemm_nt(Tensor a, Tensor b, Tensor(a!) c) -> ()");
+  m.def("tokennorm_store(Tensor dz, Tensor w, Tensor(a!) dx, Tensor(b!) part, Tensor(c!) ticket, "
+        "Tensor(d!) out) -> ()");
   m.def("tokennorm_masked(Tensor dz, Tensor w, Tensor mask, float scale, Tensor(a!) dx, "
         "Tensor(b!) part, Tensor(c!) ticket, Tensor(d!) out) -> ()");
   m.def("id_sort(Tensor ids, int V, Tensor(a!) ws, Tensor(b!) sid, Tensor(c!) perm) -> ()");
@@ -1953,6 +1986,7 @@ TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("tokennorm", &tokennorm);
   m.impl("gemm_nt", &gemm_nt);
   m.impl("tokennorm_masked", &tokennorm_masked);
+  m.impl("tokennorm_store", &tokennorm_store);
   m.impl("id_sort", &id_sort);
   m.impl("wgrad", &wgrad);
   m.impl("gru_persist_fwd", &gru_persist_fwd);

@@ -41,7 +41,8 @@ constexpr int kTnDmaPerWave = 32 / kTnWaves;
 // MODE 0: the sum of squares; 1: the products stored as fp32 C (gemm_nt); 2: the products
 // masked by dropout bits, scaled, stored as bf16 C and their sum of squares (the dropout
 // route's embedding input gradient dX = (dZ0·W_x0ᵀ) ⊙ mask / keep and its TF token-norm term,
-// one launch instead of a library GEMM, a mask pass and a sum-of-squares pass)
+// one launch instead of a library GEMM, a mask pass and a sum-of-squares pass); 3: the
+// products stored as fp32 C and their sum of squares (the wide-vocabulary route's dX)
 template <int NST, int MODE>
 __global__ void __launch_bounds__(64 * kTnWaves, kTnWaves / 4) tokennorm_kernel(TokenNormArgs a) {
   constexpr bool STORE = MODE == 1;
@@ -225,6 +226,15 @@ __global__ void __launch_bounds__(64 * kTnWaves, kTnWaves / 4) tokennorm_kernel(
           sq += f * f;
         }
   } else {
+    if constexpr (MODE == 3) {
+      float* c = a.c + (size_t)(m0 + wm + 4 * (lane >> 4)) * a.ldc + n0 + wn + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) c[(size_t)(16 * i + r) * a.ldc + 16 * j] = acc[i][j][r];
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -410,8 +420,10 @@ bool tokennorm_supported(int N, int H, int K) {
 void launch_tokennorm(const TokenNormArgs& a, hipStream_t s) {
   const int grid = (a.N / kTnTile) * (a.N_units / kTnTile);
   const int v = debug_int("tn_v", 3);
-  if (a.mask)  // (the masked form has the default geometry only)
+  if (a.mask)  // (the masked / storing forms have the default geometry only)
     tokennorm_kernel<4, 2><<<grid, 64 * kTnWaves, 0, s>>>(a);
+  else if (a.c)
+    tokennorm_kernel<4, 3><<<grid, 64 * kTnWaves, 0, s>>>(a);
   else if (v == 4)
     tokennorm4_kernel<<<grid, 64 * kT4Waves, 0, s>>>(a);
   else if (v == 5)

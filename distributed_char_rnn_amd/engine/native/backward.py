@@ -253,9 +253,18 @@ class BackwardMixin:
                 else:
                     self.ops.segsum(dZx, None, 1, bufs["colsum"][:, :GW], bufs["ws"], False)
                     dbias = bufs["colsum"][0, :GW]
-                dXf = mm_into(dZx, lw.Wx.t(), bufs["dx"].view(N, H))
-                self._embed_grad(dXf, ids_tm, bufs)
-                self._token_norm(dXf)
+                if (self.tf_norm and self.knobs.on("dx_fused")
+                        and int(self.ops.tokennorm_supported(N, H, dZx.shape[1]))):
+                    # one launch: the fp32 dX rows and their TF token-norm term
+                    ws = self._tn_workspace()
+                    dXf = bufs["dx"].view(N, H)
+                    self.ops.tokennorm_store(dZx, lw.Wx, dXf, ws[0], ws[1],
+                                             self.store.norm_slot_view())
+                    self._embed_grad(dXf, ids_tm, bufs)
+                else:
+                    dXf = mm_into(dZx, lw.Wx.t(), bufs["dx"].view(N, H))
+                    self._embed_grad(dXf, ids_tm, bufs)
+                    self._token_norm(dXf)
             elif gather and tail and self._tail_gather_ok(layer, bufs, fused_dew):
                 # tail route: dEW's split-K slabs, dW_x0 = Eᵀ·dEW and dE = dEW·W_x0ᵀ all in the
                 # step's FINALIZE launch (the products wait in-launch for the dEW slab sum)

@@ -208,6 +208,25 @@ def test_tokennorm_kernel(dcr_ops, N, H):
     assert int(ticket.item()) == 0
 
 
+def test_tokennorm_store_kernel(dcr_ops):
+    """Storing form (the wide-vocabulary route's embedding input gradient): fp32 dx = dz·wᵀ and
+    sum(dx²) in one launch."""
+    torch.manual_seed(13)
+    N, H = 4096, 512
+    dz = (torch.randn(N, 4 * H, device="cuda") * 0.1).to(torch.bfloat16)
+    w = (torch.randn(H, 4 * H, device="cuda") * 0.05).to(torch.bfloat16)
+    part = torch.empty(1024, device="cuda")
+    ticket = torch.zeros(1, dtype=torch.int32, device="cuda")
+    out = torch.zeros(1, device="cuda")
+    dx = torch.full((N, H), float("nan"), device="cuda")
+    dcr_ops.tokennorm_store(dz, w, dx, part, ticket, out)
+    torch.cuda.synchronize()
+    ref = dz.double() @ w.double().t()
+    assert float((dx.double() - ref).norm() / ref.norm()) < 1e-5
+    assert abs(float(out) - float((dx.double() ** 2).sum())) / float(out) < 1e-4
+    assert int(ticket.item()) == 0
+
+
 @pytest.mark.parametrize("N,H", [(2048, 256), (32768, 512)])
 def test_tokennorm_masked_kernel(dcr_ops, N, H):
     """Masked form (the dropout route's embedding input gradient): dx = bf16 of (dz·wᵀ) ⊙ mask
