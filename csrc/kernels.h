@@ -424,6 +424,7 @@ struct TokenNormArgs {
   unsigned* ticket;             // zeroed, reset by the kernel
   float* out;                   // [1] the sum of squares
   float* c; long ldc;           // gemm_nt: C [N, N_units] fp32 (the products themselves)
+  const float* cbias;           // gemm_nt: optional [N_units] added to every row of C
   const uint8_t* mask;          // masked form: dropout bits [N, N_units / 8] (dropout.hip), and
   bf16* cb; float mscale;       //   C [N, N_units] bf16 (row stride ldc) = products ⊙ mask · mscale
 };

@@ -1620,7 +1620,8 @@ void tokennorm_store(const at::Tensor& dz, const at::Tensor& w, at::Tensor& dx, 
 }
 
 // C [M, N] fp32 = a [M, K] · bᵀ (b [N, K]), both bf16 K-contiguous (tokennorm.hip's pipeline)
-void gemm_nt(const at::Tensor& a_, const at::Tensor& b, at::Tensor& c) {
+void gemm_nt(const at::Tensor& a_, const at::Tensor& b, at::Tensor& c,
+             const c10::optional<at::Tensor>& bias) {
   for (const at::Tensor* t : {&a_, &b}) {
     CHECK_DEV(*t); CHECK_BF16(*t);
     TORCH_CHECK(t->dim() == 2 && t->stride(1) == 1 && t->stride(0) % 8 == 0 &&
@@ -1643,6 +1644,11 @@ void gemm_nt(const at::Tensor& a_, const at::Tensor& b, at::Tensor& c) {
   a.w = ptr<bf16>(b); a.ld_w = b.stride(0);
   a.N = M; a.N_units = N; a.K = K;
   a.c = ptr<float>(c); a.ldc = c.stride(0);
+  if (has(bias)) {
+    CHECK_DEV(*bias); CHECK_F32(*bias);
+    TORCH_CHECK(bias->is_contiguous() && bias->numel() == N, "gemm_nt: bias must be [N]");
+    a.cbias = ptr<float>(*bias);
+  }
   dcr::launch_gemm_nt(a, cur_stream());
 }
 
@@ -1878,7 +1884,7 @@ TORCH_LIBRARY(dcr, m) {
         [](int64_t L, int64_t H, int64_t V, int64_t S) -> int64_t {
           return dcr::generate_supported((int)L, (int)H, (int)V, (int)S, num_cus()); });
   m.def("tokennorm(Tensor dz, Tensor w, Tensor(a!) part, Tensor(b!) ticket, Tensor(c!) out) -> ()");
-  m.def("gemm_nt(Tensor a, Tensor b, Tensor(a!) c) -> ()");
+  m.def("gemm_nt(Tensor a, Tensor b, Tensor(a!) c, Tensor? bias=None) -> ()");
   m.def("tokennorm_store(Tensor dz, Tensor w, Tensor(a!) dx, Tensor(b!) part, Tensor(c!) ticket, "
         "Tensor(d!) out) -> ()");
   m.def("tokennorm_masked(Tensor dz, Tensor w, Tensor mask, float scale, Tensor(a!) dx, "

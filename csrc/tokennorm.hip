@@ -184,12 +184,17 @@ __global__ void __launch_bounds__(64 * kTnWaves, kTnWaves / 4) tokennorm_kernel(
   if constexpr (STORE) {
     // D[4q + r][l & 15] of tile (i, j): row m0 + wm + 16 i + 4 q + r, column n0 + wn + 16 j + l%16
     float* c = a.c + (size_t)(m0 + wm + 4 * (lane >> 4)) * a.ldc + n0 + wn + (lane & 15);
+    float bj[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.cbias) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bj[j] = a.cbias[n0 + wn + 16 * j + (lane & 15)];
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) c[(size_t)(16 * i + r) * a.ldc + 16 * j] = acc[i][j][r];
+        for (int j = 0; j < 4; ++j) c[(size_t)(16 * i + r) * a.ldc + 16 * j] = acc[i][j][r] + bj[j];
     return;
   }
   __syncthreads();  // (every stage read: the ring's first bytes become the reduction words)

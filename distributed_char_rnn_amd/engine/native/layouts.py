@@ -162,12 +162,14 @@ class LayoutsMixin:
                 GW = k.shape[1]
                 # W_xᵀ: the fused input projections of layers above 0, and of layer 0 when
                 # dropout sends its masked embedding rows through the dense route (the two-layer
-                # forward then projects them in-kernel)
+                # forward then projects them in-kernel) or a wide vocabulary's gather table is
+                # the gemm_nt product E·W_x0 (both operands K-contiguous)
                 drop = self.cfg.input_keep_prob < 1.0 or self.cfg.output_keep_prob < 1.0
+                want_t = self.cfg.model == "lstm" and (
+                    layer > 0 or drop or (self.V > SEG_LDS_MAX_V and self._table_nt_ok(D, GW)))
                 lw = LayerWeights(Wx=mv(names[0])[:D] if mv else e(D, GW), Wx32=k[:D], bias=b,
                                   Wh=mv(names[0])[D:] if mv else e(H, GW), WhT=e(GW, H),
-                                  WxT=e(GW, D) if (self.cfg.model == "lstm" and (layer > 0 or drop))
-                                  else None)
+                                  WxT=e(GW, D) if want_t else None)
                 T += [(k[D:], lw.Wh, 0), (k[D:], lw.WhT, 1), (k[:D], lw.Wx, 0)]
                 if lw.WxT is not None:
                     T.append((k[:D], lw.WxT, 1))
@@ -203,6 +205,10 @@ class LayoutsMixin:
             self._head["WsTw"] = e(self.V, H)   # softmax_wᵀ [V, H] (head_wide.hip)
             T.append((Ws32, self._head["WsTw"], 1))
 
+    def _table_nt_ok(self, D: int, GW: int) -> bool:
+        """The wide-vocabulary gather table as a gemm_nt launch ([V, D] x [GW, D]ᵀ)."""
+        return self.knobs.on("table_nt") and bool(self.ops.gemm_nt_supported(self.V, GW, D))
+
     def _prep(self) -> list:
         """Prep-kernel tasks that refresh the weight layouts after a parameter change (empty
         when the weights are current).  The layer-0 ``E·W_x + b`` table: for LSTM / RNN with a
@@ -236,9 +242,15 @@ class LayoutsMixin:
                 Eb = self._head.get("Ebf")
                 if Eb is None or Eb.shape != self._head["E"].shape:
                     Eb = self._head["Ebf"] = torch.empty_like(self._head["E"], dtype=bf16)
-                tasks += [(w0.bias.view(1, -1).expand(self.V, -1), tab, 0),
-                          (self._head["E"], Eb, 0)]
-                self._table_bias_in = True
+                if w0.WxT is not None:
+                    # E·W_x0 + b0 as ONE gemm_nt launch with the bias in its epilogue, after
+                    # this launch wrote Eb and W_x0ᵀ (no bias-row pass, no library GEMM)
+                    tasks.append((self._head["E"], Eb, 0))
+                    self._table_nt = True
+                else:
+                    tasks += [(w0.bias.view(1, -1).expand(self.V, -1), tab, 0),
+                              (self._head["E"], Eb, 0)]
+                    self._table_bias_in = True
         return tasks
 
     def _run_prep(self, tasks: list):
@@ -256,7 +268,10 @@ class LayoutsMixin:
                 # precision as a bf16 layer-0 input projection; the bf16 E copy is also the
                 # row source of the dense backward route's X0 gather
                 Eb = self._head.get("Ebf")
-                if getattr(self, "_table_bias_in", False):  # bias rows + Eb written by prep
+                if getattr(self, "_table_nt", False):  # Eb and W_x0ᵀ written by prep
+                    self._table_nt = False
+                    self.ops.gemm_nt(Eb, w0.WxT, self._head["table"], w0.bias)
+                elif getattr(self, "_table_bias_in", False):  # bias rows + Eb written by prep
                     self._table_bias_in = False
                     tab = self._head["table"]
                     try:

@@ -74,6 +74,8 @@ DEBUG_KEYS = {
              "wgrad kernel (csrc/wgrad.hip)",
     "tokennorm": "0: TF token-norm term as a library GEMM to bf16 rows + a sumsq launch instead "
                  "of the fused MFMA kernel (csrc/tokennorm.hip)",
+    "table_nt": "0: wide-vocabulary gather table E·W_x0 + b0 as a library GEMM on bias rows "
+                "instead of one gemm_nt launch with the bias in its epilogue",
     "dx_fused": "0: dropout route's embedding input gradient as a library GEMM + mask pass + "
                 "sum-of-squares pass instead of the masked token-norm launch",
     "dws_wgrad": "0: softmax_w gradient (fused head) as a library GEMM instead of a zero-padded "
