@@ -268,6 +268,7 @@ struct Lstm2Args {
   int xcdloc;           // 1: XCD-resident hand-offs for columns found on one XCD (persist_common.h;
                         //   exchange word: dwords 2-3 of cnt0's slot 0 per column); 0: write-through
   int zx_rows;          // gather mode: rows of the zx0 table (the vocabulary), else 0
+  int steady;           // forward: ticks LAG+1 .. T-3 on the steady-state (constant-condition) body
 };
 // batch groups per workgroup for the two-layer kernels at (H, B) (force > 0: only that value),
 // 0 = unsupported

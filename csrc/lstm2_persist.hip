@@ -26,6 +26,8 @@
 // fragment-order ring stores, the storing wave's vmcnt(0), one agent-scope counter add per
 // storing wave per (column, slot); ONE poller per workgroup watches both layers' counters; every
 // load of handed-off bytes is a buffer_load sc1.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 #include "persist_common.h"
@@ -313,16 +315,19 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     rm_t = -1;
   };
 
-  for (int tau = 0; tau <= T + LAG - 1; ++tau) {
-    const bool on0 = tau < T;                  // layer l   computes step tau
-    const bool on1 = tau >= LAG;               // layer l+1 computes step tau-LAG
-    const bool ld0 = tau <= T;                 // slot tau of h_l (layer l's h_{tau-1})
+  // one tick; SDY (steady): LAG + 1 <= tau <= T - 3, where every edge condition below is a
+  // compile-time constant (both layers active, every slot a ring slot, no final step)
+  auto tick = [&](int tau, auto sdy_c) __attribute__((always_inline)) {
+    constexpr bool SDY = decltype(sdy_c)::value;
+    const bool on0 = SDY || tau < T;           // layer l   computes step tau
+    const bool on1 = SDY || tau >= LAG;        // layer l+1 computes step tau-LAG
+    const bool ld0 = SDY || tau <= T;          // slot tau of h_l (layer l's h_{tau-1})
     const bool ld1 = on1;                      // slot tau-LAG of h_{l+1}
     const int t = L == 0 ? tau : tau - LAG;    // this role's step
     const bool act = L == 0 ? on0 : on1;
     // this role's slot t+1 is read by a later tick: layer l's up to slot T, layer l+1's up to
     // slot T-1 (by itself)
-    const bool signal = act && (L == 0 || t + 1 < T);
+    const bool signal = act && (SDY || L == 0 || t + 1 < T);
     STAMPF(0, 0)
     // layer-l input projections of step tau (independent of the hand-off): group 0's rows are
     // loaded before the poll, group g+1's right behind group g's payload (a gathered row needs
@@ -354,7 +359,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     // workgroup's 32G rows for this tick, DMA'd into LDS before the poll (no registers; the
     // poll barrier waits for them).  A global byte load at each use had put its latency on the
     // tick's critical path.
-    const bool xdrop = DROP && ld0 && tau >= 1;
+    const bool xdrop = DROP && ld0 && (SDY || tau >= 1);
     if (G > 1 && xdrop) {
       const int r0 = col * G * 32;
       const __amdgpu_buffer_rsrc_t rm =
@@ -371,7 +376,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     }
     // hand-offs of the previous tick: layer l's slot tau, layer l+1's slot tau-LAG (slot 0 of
     // either is the prep-written initial state)
-    const bool pw0 = ld0 && tau >= 1, pw1 = ld1 && tau >= LAG + 1;
+    const bool pw0 = ld0 && (SDY || tau >= 1), pw1 = ld1 && (SDY || tau >= LAG + 1);
     if (loc) {  // flags of both layers' producing ticks (tau - 1) + 1
       if ((pw0 || pw1) && w == 0 && !dead)
         dead = !poll_flags2(fl0, pw0, fl1, pw1, nwg_u, (unsigned)tau, a.spin_limit, a.err, 9u);
@@ -398,13 +403,13 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     auto load_group = [&](int g, bf16x8 (&hf0)[2][KS], bf16x8 (&hf1)[2][KS]) {
       const int bg = col * G + g;
       if constexpr (G == 1) {  // unconditional: a skipped layer reads an empty descriptor
-        const bool ring0 = tau > 0;
+        const bool ring0 = SDY || tau > 0;
         const __amdgpu_buffer_rsrc_t r0 =
             !ld0 ? make_rsrc(a.hring0, 0)
                  : ring0 ? make_rsrc(a.hring0 + (size_t)(tau & 1) * ringsz, sizeof(bf16) * ringsz)
                          : make_rsrc(a.hbuf0, sizeof(bf16) * (size_t)B * hld);
         const int s1 = tau - LAG;
-        const bool ring1 = s1 > 0;
+        const bool ring1 = SDY || s1 > 0;
         const __amdgpu_buffer_rsrc_t r1 =
             !ld1 ? make_rsrc(a.hring1, 0)
                  : ring1 ? make_rsrc(a.hring1 + (size_t)(s1 & 1) * ringsz, sizeof(bf16) * ringsz)
@@ -421,7 +426,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
         return;
       }
       if (ld0) {
-        const bool ring0 = tau > 0;
+        const bool ring0 = SDY || tau > 0;
         const __amdgpu_buffer_rsrc_t r0 =
             ring0 ? make_rsrc(a.hring0 + (size_t)(tau & 1) * ringsz, sizeof(bf16) * ringsz)
                   : make_rsrc(a.hbuf0, sizeof(bf16) * (size_t)B * hld);
@@ -434,7 +439,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
       }
       if (ld1) {
         const int s1 = tau - LAG;
-        const bool ring1 = s1 > 0;
+        const bool ring1 = SDY || s1 > 0;
         const __amdgpu_buffer_rsrc_t r1 =
             ring1 ? make_rsrc(a.hring1 + (size_t)(s1 & 1) * ringsz, sizeof(bf16) * ringsz)
                   : make_rsrc(a.hbuf1, sizeof(bf16) * (size_t)B * hld);
@@ -479,9 +484,9 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
       if constexpr (XIN) x_prefetch(tau + 1);
       if constexpr (ZXA) {
         // the next tick's row (and the id of the one after), behind this tick's payload loads
-        if (zl && tau + 1 < T) {
+        if (zl && (SDY || tau + 1 < T)) {
           zx_load(zx_row1(tau + 1, idn), zxn);
-          if (a.ids && tau + 2 < T) idn = a.ids[(size_t)(tau + 2) * B + bz];
+          if (a.ids && (SDY || tau + 2 < T)) idn = a.ids[(size_t)(tau + 2) * B + bz];
         }
       } else {
         if (g + 1 < G) zx_load(zrows[g + 1], zxn);
@@ -569,7 +574,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
       // (G = 1) layer l+1's x-part of its step tau-1 (next tick) from slot tau of layer l
       auto do_stash = [&]() {
         if constexpr (G == 1) {
-          if (ld0 && tau >= 1) {
+          if (ld0 && (SDY || tau >= 1)) {
             // dropout: the mask dwords of this lane's fragments, all read before any use (one
             // LDS wait; a byte read at each use had serialised 8 LDS round trips); the byte of
             // fragment (j, s) is byte lane/16 of dword s of its row's K range
@@ -658,9 +663,9 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
             rm_g[2][r] = f2bf(gf[r]); rm_g[3][r] = f2bf(go[r]);
           }
           rm_t = t;
-          if (live && t == T - 1 && hlL)
+          if (live && (!SDY && t == T - 1) && hlL)
             *reinterpret_cast<float4*>(hlL + bh) = make_float4(h[0], h[1], h[2], h[3]);
-          if (live && t == T - 1 && clL)
+          if (live && (!SDY && t == T - 1) && clL)
             *reinterpret_cast<float4*>(clL + bh) = make_float4(c[g][0], c[g][1], c[g][2], c[g][3]);
         } else if (live) {  // row-major copies for the GEMMs / head (not handed off)
           const size_t o = (size_t)(t + 1) * B * H + bh;
@@ -673,15 +678,24 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
             st4bf(gp + 2 * H, gf[0], gf[1], gf[2], gf[3]);
             st4bf(gp + 3 * H, go[0], go[1], go[2], go[3]);
           }
-          if (t == T - 1 && hlL)
+          if ((!SDY && t == T - 1) && hlL)
             *reinterpret_cast<float4*>(hlL + bh) = make_float4(h[0], h[1], h[2], h[3]);
-          if (t == T - 1 && clL)
+          if ((!SDY && t == T - 1) && clL)
             *reinterpret_cast<float4*>(clL + bh) = make_float4(c[g][0], c[g][1], c[g][2], c[g][3]);
         }
       } else {
         do_stash();  // waves without an epilogue this tick
       }
     }
+    };
+  {
+    using sdy_t = std::integral_constant<bool, true>;
+    using edge_t = std::integral_constant<bool, false>;
+    const int sdy_lo = LAG + 1, sdy_hi = a.steady ? T - 3 : -1;  // (steady range)
+    int tau = 0;
+    for (; tau <= T + LAG - 1 && tau < sdy_lo; ++tau) tick(tau, edge_t{});
+    for (; tau <= sdy_hi; ++tau) tick(tau, sdy_t{});
+    for (; tau <= T + LAG - 1; ++tau) tick(tau, edge_t{});
   }
   if constexpr (DEFER) flush_rm();
 }

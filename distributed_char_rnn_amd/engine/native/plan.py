@@ -74,6 +74,8 @@ DEBUG_KEYS = {
              "wgrad kernel (csrc/wgrad.hip)",
     "tokennorm": "0: TF token-norm term as a library GEMM to bf16 rows + a sumsq launch instead "
                  "of the fused MFMA kernel (csrc/tokennorm.hip)",
+    "fwd_steady": "0: the two-layer forward's steady ticks on the generic tick body (run-time "
+                  "edge conditions) instead of the constant-condition one (C++)",
     "table_nt": "0: wide-vocabulary gather table E·W_x0 + b0 as a library GEMM on bias rows "
                 "instead of one gemm_nt launch with the bias in its epilogue",
     "dx_fused": "0: dropout route's embedding input gradient as a library GEMM + mask pass + "
