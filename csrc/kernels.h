@@ -269,6 +269,8 @@ struct Lstm2Args {
                         //   exchange word: dwords 2-3 of cnt0's slot 0 per column); 0: write-through
   int zx_rows;          // gather mode: rows of the zx0 table (the vocabulary), else 0
   int steady;           // forward: ticks LAG+1 .. T-3 on the steady-state (constant-condition) body
+  bf16* xdst;           // optional (dropout, G = 1): layer l+1's masked input rows h_l ⊙ mask /
+  int xdld;             //   keep [T·B, H] (row stride xdld), written with layer l's row-major h
 };
 // batch groups per workgroup for the two-layer kernels at (H, B) (force > 0: only that value),
 // 0 = unsupported

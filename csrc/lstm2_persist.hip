@@ -298,6 +298,8 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
   const __amdgpu_buffer_rsrc_t r_h = make_rsrc(hbL, sizeof(bf16) * (size_t)(T + 1) * B * hld);
   const __amdgpu_buffer_rsrc_t r_c = make_rsrc(cbL, sizeof(float) * (size_t)(T + 1) * B * H);
   const __amdgpu_buffer_rsrc_t r_g = make_rsrc(gtL, gtL ? sizeof(bf16) * (size_t)T * B * 4 * H : 0);
+  const __amdgpu_buffer_rsrc_t r_xd =
+      make_rsrc(a.xdst, a.xdst ? sizeof(bf16) * (size_t)T * B * a.xdld : 0);
   const int brow = col * G * 32 + 16 * J + (lane & 15);  // (G = 1) this lane's row
   auto flush_rm = [&]() {
     constexpr unsigned kOut = 0x7FFFFFF0u;  // out of range: dropped
@@ -312,6 +314,21 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
     for (int gt = 0; gt < 4; ++gt)
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, rm_g[gt]), r_g,
                                             og + gt * H * (unsigned)sizeof(bf16), 0, 0);
+    if constexpr (DROP && G == 1) {
+      // layer l+1's masked input row h_l(t) ⊙ mask / keep for its weight gradient (the separate
+      // mask pass over [T·B, H] otherwise): the mask bytes of step t are the ones the tick-t
+      // DMA staged in mlds[(t + 1) & 1] for the stash (overwritten two ticks later)
+      if (L == 0 && a.xdst) {
+        const uint8_t* mb = reinterpret_cast<const uint8_t*>(mlds[(rm_t + 1) & 1]);
+        const unsigned m = mb[(16 * J + (lane & 15)) * (H / 8) + (u0 >> 3)] >> (u0 & 7);
+        bf16x4 xd;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          xd[r] = f2bf((m >> r & 1u) ? bf2f(rm_h[r]) * a.xscale : 0.f);
+        const unsigned ox = ok ? (unsigned)((((size_t)rm_t * B + brow) * a.xdld + u0) * sizeof(bf16)) : kOut;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, xd), r_xd, ox, 0, 0);
+      }
+    }
     rm_t = -1;
   };
 

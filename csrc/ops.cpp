@@ -909,7 +909,8 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
                        const c10::optional<at::Tensor>& xmask, double xscale,
                        const c10::optional<at::Tensor>& bias0,
                        const c10::optional<at::Tensor>& x0,
-                       const c10::optional<at::Tensor>& X0T) {
+                       const c10::optional<at::Tensor>& X0T,
+                       const c10::optional<at::Tensor>& xdst) {
   for (auto* t : {&W0T, &W1T, &X1T}) check_seq(*t, at::kBFloat16, "W");
   TORCH_CHECK(has(x0) == has(X0T), "pass x0 and X0T together");
   const bool xin = has(x0);
@@ -1003,6 +1004,16 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
   a.clast1 = optr<float>(clast1);
   a.xmask = drop_bits(xmask, T, B, H, "xmask");
   a.xscale = (float)xscale;
+  if (has(xdst)) {  // layer l+1's masked input rows, written beside layer l's row-major h
+    TORCH_CHECK(has(xmask) && G == 1, "xdst: dropout (xmask) with one batch group per workgroup");
+    TORCH_CHECK(xdst->is_cuda() && xdst->scalar_type() == at::kBFloat16 && xdst->dim() == 2 &&
+                    xdst->size(0) == (int64_t)T * B && xdst->size(1) == H && xdst->stride(1) == 1 &&
+                    xdst->stride(0) >= H && xdst->stride(0) % 4 == 0 &&
+                    (reinterpret_cast<uintptr_t>(xdst->data_ptr()) & 7) == 0,
+                "xdst must be bf16 [T*B, H] rows, unit-stride, 8-B aligned, stride a multiple of 4");
+    a.xdst = ptr<bf16>(*xdst);
+    a.xdld = (int)xdst->stride(0);
+  }
   const int rc = dcr::launch_lstm2_fwd_persist(a, num_cus(), cur_stream());
   TORCH_CHECK(rc == 0, "two-layer persistent LSTM forward not launched (", rc, ")");
 }
@@ -1933,7 +1944,8 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor(i!) cnt0, Tensor(j!) cnt1, Tensor(k!) err, float forget_bias, int spin_limit, "
       "Tensor(l!) hring0, Tensor(m!) hring1, int G, Tensor(o!)? clast0=None, "
       "Tensor(p!)? clast1=None, Tensor(q!)? diag=None, Tensor? xmask=None, "
-      "float xscale=1.0, Tensor? bias0=None, Tensor? x0=None, Tensor? X0T=None) -> ()");
+      "float xscale=1.0, Tensor? bias0=None, Tensor? x0=None, Tensor? X0T=None, "
+      "Tensor(r!)? xdst=None) -> ()");
   m.def(
       "lstm2_persist_bwd(Tensor Wh0, Tensor Wh1, Tensor Wx1, Tensor dtop1, Tensor gates0, "
       "Tensor cbuf0, Tensor gates1, Tensor cbuf1, Tensor(a!) dz0, Tensor(b!) dz1, "

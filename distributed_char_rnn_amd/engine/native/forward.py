@@ -167,6 +167,10 @@ class ForwardMixin:
                 # l+1's input dropout is applied to its fragments in-kernel
                 lw1, lb1 = self._w[layer + 1], bufs["layers"][layer + 1]
                 xm = dm["inb"][layer + 1] if dm else None
+                # G = 1: the kernel writes layer l+1's masked input rows (x_drop) itself, beside
+                # layer l's row-major h (no separate mask pass; DCR_DEBUG=xdst=0: the pass)
+                xdst = (lb1.x_drop if (xm is not None and P.pair_g == 1 and lb1.x_drop is not None
+                                       and self.knobs.debug.get("xdst", "1") != "0") else None)
                 self.ops.lstm2_persist_fwd(lw.WhT, lw1.WhT, lw1.WxT, zx, ids_arg, lw1.bias,
                                            lb.hbuf, lb.cbuf, lb.gates, lb.hlast32,
                                            lb1.hbuf, lb1.cbuf, lb1.gates, lb1.hlast32,
@@ -175,11 +179,15 @@ class ForwardMixin:
                                            P.pair_g, lb.clast32, lb1.clast32, None, xm,
                                            dm["sin"] if dm else 1.0,
                                            lw.bias if ids_arg is None else None,
-                                           lb.x_in if xin else None, lw.WxT if xin else None)
+                                           lb.x_in if xin else None, lw.WxT if xin else None,
+                                           xdst)
                 # layer l+1's (masked) input rows for its weight gradient; unmasked rows of a
                 # pair-interleaved buffer feed ONE GEMM for both of its weight gradients
-                lb1.x_in = (self._masked(lb.hbuf[1:], xm, dm["sin"], out=lb1.x_drop)
-                            if xm is not None else lb.hbuf[1:].reshape(N, H))
+                if xdst is not None:
+                    lb1.x_in = xdst.view(N, H)
+                else:
+                    lb1.x_in = (self._masked(lb.hbuf[1:], xm, dm["sin"], out=lb1.x_drop)
+                                if xm is not None else lb.hbuf[1:].reshape(N, H))
                 ph = bufs.get("pair_h", {}).get(layer + 1)
                 lb1.x_merged = ph is not None and (xm is None) == (ph[1] == "h")
                 x_prev = lb1.hbuf[1:]

@@ -61,6 +61,8 @@ DEBUG_KEYS = {
     "head_omask": "0: top output dropout applied to dtop by a separate pass, not the head",
     "xin": "0: library zx GEMM for a dense layer-l input instead of the G = 1 two-layer "
            "forward's in-kernel projection",
+    "xdst": "0: layer l+1's masked input rows by a separate mask pass instead of the G = 1 "
+            "two-layer dropout forward's in-kernel store",
     "pair_dw": "0: separate h buffers per layer of a wavefront pair (two weight GEMMs for the "
                "upper layer instead of one over the pair-interleaved h)",
     "gru_dwx": "0: GRU input-weight gradient as one [H, 3H] temporary + sum + two copies",

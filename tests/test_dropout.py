@@ -111,3 +111,27 @@ def test_dropout_library_input_projection_matches_oracle(B, H, L, monkeypatch):
     nat, _ = _run("lstm", B, 5, H, L, 0.8, 0.7, env={"DCR_DEBUG": "persist_min_t=1,xin=0"},
                   monkeypatch=monkeypatch)
     assert nat.backend._persist_plan(B, True, 5).pair
+
+
+@pytest.mark.parametrize("B,T", [(256, 24), (256, 130)])
+def test_pair_forward_masked_rows_match_mask_pass(B, T, monkeypatch):
+    """The G = 1 two-layer dropout forward writes layer l+1's masked input rows itself
+    (Lstm2Args.xdst): bitwise the rows of the separate mask pass (DCR_DEBUG=xdst=0), so the
+    step's gradients match."""
+    cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=512, num_layers=2,
+                      input_keep_prob=0.8, output_keep_prob=0.7)
+    x = torch.randint(0, 65, (B, T), dtype=torch.int32, device="cuda")
+    y = torch.randint(0, 65, (B, T), dtype=torch.int32, device="cuda")
+    out = []
+    for knob in ("xdst=0", ""):
+        monkeypatch.setenv("DCR_DEBUG", knob)
+        m = CharRNN(cfg, device="cuda", seed=9)
+        assert m.backend._persist_plan(B, True, T).pair_g == 1
+        m.backend.train_step(x, y, m.zero_state(B))
+        torch.cuda.synchronize()
+        m.backend.check_errors()
+        bufs = m.backend._bufs[(B, T, True)]
+        out.append((bufs["layers"][1].x_drop.clone(), m.store.grad.clone()))
+    (xa, ga), (xb, gb) = out
+    assert torch.equal(xa, xb)
+    assert float((ga - gb).norm() / gb.norm()) < 1e-6
