@@ -271,6 +271,9 @@ struct Lstm2Args {
   int steady;           // forward: ticks LAG+1 .. T-3 on the steady-state (constant-condition) body
   bf16* xdst;           // optional (dropout, G = 1): layer l+1's masked input rows h_l ⊙ mask /
   int xdld;             //   keep [T·B, H] (row stride xdld), written with layer l's row-major h
+  const uint8_t* omask; // optional (dropout, G = 1): layer l+1's output dropout bits [T, B, H/8],
+  float oscale;         //   their 1/keep and the masked rows h_l+1 ⊙ mask / keep [T·B, H]
+  bf16* odst;           //   (dense) written with layer l+1's row-major h
 };
 // batch groups per workgroup for the two-layer kernels at (H, B) (force > 0: only that value),
 // 0 = unsupported

@@ -300,6 +300,10 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
   const __amdgpu_buffer_rsrc_t r_g = make_rsrc(gtL, gtL ? sizeof(bf16) * (size_t)T * B * 4 * H : 0);
   const __amdgpu_buffer_rsrc_t r_xd =
       make_rsrc(a.xdst, a.xdst ? sizeof(bf16) * (size_t)T * B * a.xdld : 0);
+  const __amdgpu_buffer_rsrc_t r_od = make_rsrc(a.odst, a.odst ? sizeof(bf16) * (size_t)T * B * H : 0);
+  const __amdgpu_buffer_rsrc_t r_om =
+      make_rsrc(a.omask, (DROP && a.odst) ? sizeof(uint8_t) * (size_t)T * B * (H / 8) : 0);
+  unsigned rm_m = 0;  // (dropout) the output-mask byte of this lane's deferred layer l+1 row
   const int brow = col * G * 32 + 16 * J + (lane & 15);  // (G = 1) this lane's row
   auto flush_rm = [&]() {
     constexpr unsigned kOut = 0x7FFFFFF0u;  // out of range: dropped
@@ -327,6 +331,16 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
           xd[r] = f2bf((m >> r & 1u) ? bf2f(rm_h[r]) * a.xscale : 0.f);
         const unsigned ox = ok ? (unsigned)((((size_t)rm_t * B + brow) * a.xdld + u0) * sizeof(bf16)) : kOut;
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, xd), r_xd, ox, 0, 0);
+      }
+      // the top layer's output dropout rows (the head's input) from the byte loaded a tick ago
+      if (L == 1 && a.odst) {
+        const unsigned m = rm_m >> (u0 & 7);
+        bf16x4 od;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          od[r] = f2bf((m >> r & 1u) ? bf2f(rm_h[r]) * a.oscale : 0.f);
+        const unsigned oo = ok ? (unsigned)((((size_t)rm_t * B + brow) * H + u0) * sizeof(bf16)) : kOut;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, od), r_od, oo, 0, 0);
       }
     }
     rm_t = -1;
@@ -680,6 +694,11 @@ __global__ void __launch_bounds__(256, 1) lstm2_fwd_persist_kernel(Lstm2Args a) 
             rm_g[2][r] = f2bf(gf[r]); rm_g[3][r] = f2bf(go[r]);
           }
           rm_t = t;
+          if constexpr (DROP) {
+            if (L == 1 && a.odst)  // consumed by the next tick's flush (rows >= B read zero)
+              rm_m = __builtin_amdgcn_raw_buffer_load_b8(
+                  r_om, live ? (unsigned)(((size_t)t * B + b) * (H / 8) + (u0 >> 3)) : 0x7FFFFFF0u, 0, 0);
+          }
           if (live && (!SDY && t == T - 1) && hlL)
             *reinterpret_cast<float4*>(hlL + bh) = make_float4(h[0], h[1], h[2], h[3]);
           if (live && (!SDY && t == T - 1) && clL)

@@ -910,7 +910,9 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
                        const c10::optional<at::Tensor>& bias0,
                        const c10::optional<at::Tensor>& x0,
                        const c10::optional<at::Tensor>& X0T,
-                       const c10::optional<at::Tensor>& xdst) {
+                       const c10::optional<at::Tensor>& xdst,
+                       const c10::optional<at::Tensor>& omask, double oscale,
+                       const c10::optional<at::Tensor>& odst) {
   for (auto* t : {&W0T, &W1T, &X1T}) check_seq(*t, at::kBFloat16, "W");
   TORCH_CHECK(has(x0) == has(X0T), "pass x0 and X0T together");
   const bool xin = has(x0);
@@ -1013,6 +1015,15 @@ void lstm2_persist_fwd(const at::Tensor& W0T, const at::Tensor& W1T, const at::T
                 "xdst must be bf16 [T*B, H] rows, unit-stride, 8-B aligned, stride a multiple of 4");
     a.xdst = ptr<bf16>(*xdst);
     a.xdld = (int)xdst->stride(0);
+  }
+  if (has(odst)) {  // layer l+1's output-dropout rows (the head's input), written beside its h
+    TORCH_CHECK(has(xmask) && G == 1 && has(omask),
+                "odst: dropout (xmask, omask) with one batch group per workgroup");
+    check_seq(*odst, at::kBFloat16, "odst");
+    TORCH_CHECK(odst->numel() == (int64_t)T * B * H, "odst must be [T*B, H]");
+    a.omask = drop_bits(omask, T, B, H, "omask");
+    a.oscale = (float)oscale;
+    a.odst = ptr<bf16>(*odst);
   }
   const int rc = dcr::launch_lstm2_fwd_persist(a, num_cus(), cur_stream());
   TORCH_CHECK(rc == 0, "two-layer persistent LSTM forward not launched (", rc, ")");
@@ -1945,7 +1956,7 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor(l!) hring0, Tensor(m!) hring1, int G, Tensor(o!)? clast0=None, "
       "Tensor(p!)? clast1=None, Tensor(q!)? diag=None, Tensor? xmask=None, "
       "float xscale=1.0, Tensor? bias0=None, Tensor? x0=None, Tensor? X0T=None, "
-      "Tensor(r!)? xdst=None) -> ()");
+      "Tensor(r!)? xdst=None, Tensor? omask=None, float oscale=1.0, Tensor(s!)? odst=None) -> ()");
   m.def(
       "lstm2_persist_bwd(Tensor Wh0, Tensor Wh1, Tensor Wx1, Tensor dtop1, Tensor gates0, "
       "Tensor cbuf0, Tensor gates1, Tensor cbuf1, Tensor(a!) dz0, Tensor(b!) dz1, "

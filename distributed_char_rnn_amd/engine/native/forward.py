@@ -105,6 +105,7 @@ class ForwardMixin:
             lb.clast32 = torch.empty(B, H, dtype=f32, device=self.dev)
         x_prev = None  # bf16 [T, B, H] input for the next layer
         paired = -1  # layer already computed by the previous layer's two-layer wavefront
+        o_done = False  # the top output-dropout rows written by the top pair's forward
         for layer in range(self.L):
             if layer == paired:
                 continue
@@ -171,6 +172,9 @@ class ForwardMixin:
                 # layer l's row-major h (no separate mask pass; DCR_DEBUG=xdst=0: the pass)
                 xdst = (lb1.x_drop if (xm is not None and P.pair_g == 1 and lb1.x_drop is not None
                                        and self.knobs.debug.get("xdst", "1") != "0") else None)
+                # ... and, for the top pair, the output-dropout rows the head reads (o_drop)
+                om = dm["out"] if (dm and xdst is not None and layer + 2 == self.L) else None
+                odst = bufs["o_drop"] if om is not None else None
                 self.ops.lstm2_persist_fwd(lw.WhT, lw1.WhT, lw1.WxT, zx, ids_arg, lw1.bias,
                                            lb.hbuf, lb.cbuf, lb.gates, lb.hlast32,
                                            lb1.hbuf, lb1.cbuf, lb1.gates, lb1.hlast32,
@@ -180,7 +184,9 @@ class ForwardMixin:
                                            dm["sin"] if dm else 1.0,
                                            lw.bias if ids_arg is None else None,
                                            lb.x_in if xin else None, lw.WxT if xin else None,
-                                           xdst)
+                                           xdst, om, dm["sout"] if om is not None else 1.0,
+                                           odst)
+                o_done = odst is not None
                 # layer l+1's (masked) input rows for its weight gradient; unmasked rows of a
                 # pair-interleaved buffer feed ONE GEMM for both of its weight gradients
                 if xdst is not None:
@@ -215,7 +221,8 @@ class ForwardMixin:
             x_prev = lb.hbuf[1:]
         O = x_prev.reshape(N, H)
         if dm is not None and dm["out"] is not None:  # the top layer's output dropout
-            O = self._masked(O, dm["out"], dm["sout"], out=bufs["o_drop"])
+            O = (bufs["o_drop"] if o_done   # written by the top pair's forward
+                 else self._masked(O, dm["out"], dm["sout"], out=bufs["o_drop"]))
         if O.stride(-1) != 1 or O.stride(0) % 8:  # the heads take row-strided O (ldo)
             O = O.contiguous()
         logits = bufs["logits"]

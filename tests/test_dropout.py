@@ -116,8 +116,8 @@ def test_dropout_library_input_projection_matches_oracle(B, H, L, monkeypatch):
 @pytest.mark.parametrize("B,T", [(256, 24), (256, 130)])
 def test_pair_forward_masked_rows_match_mask_pass(B, T, monkeypatch):
     """The G = 1 two-layer dropout forward writes layer l+1's masked input rows itself
-    (Lstm2Args.xdst): bitwise the rows of the separate mask pass (DCR_DEBUG=xdst=0), so the
-    step's gradients match."""
+    (Lstm2Args.xdst) and the top layer's output-dropout rows (odst): bitwise the rows of the
+    separate mask passes (DCR_DEBUG=xdst=0), so the step's gradients match."""
     cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=512, num_layers=2,
                       input_keep_prob=0.8, output_keep_prob=0.7)
     x = torch.randint(0, 65, (B, T), dtype=torch.int32, device="cuda")
@@ -131,7 +131,9 @@ def test_pair_forward_masked_rows_match_mask_pass(B, T, monkeypatch):
         torch.cuda.synchronize()
         m.backend.check_errors()
         bufs = m.backend._bufs[(B, T, True)]
-        out.append((bufs["layers"][1].x_drop.clone(), m.store.grad.clone()))
-    (xa, ga), (xb, gb) = out
+        out.append((bufs["layers"][1].x_drop.clone(), bufs["o_drop"].clone(),
+                    m.store.grad.clone()))
+    (xa, oa, ga), (xb, ob, gb) = out
     assert torch.equal(xa, xb)
+    assert torch.equal(oa, ob)
     assert float((ga - gb).norm() / gb.norm()) < 1e-6
