@@ -20,8 +20,12 @@ constexpr int kDropThreads = 256;
 // 16-bit uniforms (keep resolution 2^-16): 8 hashes per 32 elements.  One launch fills all the
 // step's masks: segment m (nwords each, consecutive in memory) draws from its own stream with
 // its own keep threshold, element indices local to the segment (the bits equal a launch per mask).
+// With ``e.out``: the words of segment 0 (layer 0's input mask) also write their 32 masked
+// embedding elements out[r, 32c .. 32c+31] = E[ids[r], ...] * (bit ? scale : 0) as bf16 -- the
+// embed_dropout rows, bit for bit, without a second launch re-reading the bits.
 __global__ void __launch_bounds__(kDropThreads) dropout_bits_kernel(unsigned* __restrict__ bits,
-                                                                    DropSegs d, uint64_t seed) {
+                                                                    DropSegs d, uint64_t seed,
+                                                                    DropEmbed e) {
   const int64_t total = d.nwords * d.n;
   for (int64_t i = blockIdx.x * (int64_t)kDropThreads + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * kDropThreads) {
@@ -38,6 +42,22 @@ __global__ void __launch_bounds__(kDropThreads) dropout_bits_kernel(unsigned* __
         w |= ((unsigned)(r >> (16 * e)) & 0xFFFFu) < kt ? 1u << (4 * q + e) : 0u;
     }
     bits[i] = w;
+    if (e.out && m == 0) {
+      const int kw = e.K / 32;
+      const int64_t r = li / kw;
+      const int c0 = 32 * (int)(li - r * kw);
+      const float4* src = reinterpret_cast<const float4*>(e.E + (int64_t)e.ids[r] * e.K + c0);
+      bf16x8* dst = reinterpret_cast<bf16x8*>(e.out + r * e.K + c0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 a = src[2 * q], b = src[2 * q + 1];
+        const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        bf16x8 o;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = f2bf((w >> (8 * q + k) & 1u) ? v[k] * e.scale : 0.f);
+        dst[q] = o;
+      }
+    }
   }
 }
 
@@ -119,9 +139,10 @@ unsigned drop_threshold(float keep) {
   return kt >= 65536.0 ? 65536u : (kt <= 0.0 ? 0u : (unsigned)(kt + 0.5));
 }
 
-void launch_dropout_bits(uint8_t* bits, const DropSegs& d, uint64_t seed, hipStream_t s) {
+void launch_dropout_bits(uint8_t* bits, const DropSegs& d, uint64_t seed, hipStream_t s,
+                         const DropEmbed& e) {
   dropout_bits_kernel<<<drop_grid(d.nwords * d.n), kDropThreads, 0, s>>>(
-      reinterpret_cast<unsigned*>(bits), d, seed);
+      reinterpret_cast<unsigned*>(bits), d, seed, e);
 }
 
 void launch_mask_apply(const void* in, bool in_bf16, int64_t ld_in, void* out, bool out_bf16,

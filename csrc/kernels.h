@@ -126,8 +126,16 @@ struct DropSegs {             // n masks of nwords 32-bit words each, consecutiv
   uint64_t stream[kDropMaxSegs];
   unsigned kt[kDropMaxSegs];  // keep threshold on a 16-bit uniform (drop_threshold)
 };
+struct DropEmbed {            // optional: segment 0's masked embedding rows (embed_dropout)
+  const int* ids = nullptr;   // [rows] ids of the rows (time-major)
+  const float* E = nullptr;   // [V, K] fp32 embedding
+  bf16* out = nullptr;        // [rows, K] bf16 (null: bits only)
+  int K = 0;                  // row width, a multiple of 32
+  float scale = 1.f;
+};
 unsigned drop_threshold(float keep);
-void launch_dropout_bits(uint8_t* bits, const DropSegs& d, uint64_t seed, hipStream_t s);
+void launch_dropout_bits(uint8_t* bits, const DropSegs& d, uint64_t seed, hipStream_t s,
+                         const DropEmbed& e = DropEmbed{});
 void launch_mask_apply(const void* in, bool in_bf16, int64_t ld_in, void* out, bool out_bf16,
                        int64_t ld_out, const uint8_t* bits, int64_t rows, int K, float scale,
                        hipStream_t s);

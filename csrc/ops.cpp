@@ -832,7 +832,9 @@ void dropout_bits(at::Tensor& bits, int64_t seed, int64_t stream, double keep) {
 
 // all masks of a step in one launch: bits [n, ...] (segment m = bits[m]), streams / keeps per m
 void dropout_bits_multi(at::Tensor& bits, int64_t seed, at::IntArrayRef streams,
-                        at::ArrayRef<double> keeps) {
+                        at::ArrayRef<double> keeps, const c10::optional<at::Tensor>& ids,
+                        const c10::optional<at::Tensor>& E, double scale,
+                        const c10::optional<at::Tensor>& out) {
   TORCH_CHECK(bits.is_cuda() && bits.is_contiguous() && bits.scalar_type() == at::kByte &&
                   bits.dim() >= 1, "bits must be a contiguous uint8 GPU tensor [n, ...]");
   const int n = (int)bits.size(0);
@@ -848,8 +850,21 @@ void dropout_bits_multi(at::Tensor& bits, int64_t seed, at::IntArrayRef streams,
     d.stream[i] = (uint64_t)streams[i];
     d.kt[i] = dcr::drop_threshold((float)keeps[i]);
   }
+  dcr::DropEmbed e{};
+  if (has(out)) {  // segment 0 is layer 0's input mask: its masked embedding rows too
+    TORCH_CHECK(has(ids) && has(E), "dropout_bits_multi: out needs ids and E");
+    check_seq(*ids, at::kInt, "ids");
+    check_seq(*E, at::kFloat, "E");
+    check_seq(*out, at::kBFloat16, "out");
+    const int64_t R = ids->numel();
+    const int K = (int)E->size(1);
+    TORCH_CHECK(K % 32 == 0 && out->numel() == R * K && per == R * (K / 8),
+                "dropout_bits_multi: out [rows, K] (K % 32 == 0) over segment 0's [rows, K/8] bits");
+    e.ids = ptr<int>(*ids); e.E = ptr<float>(*E); e.out = ptr<bf16>(*out);
+    e.K = K; e.scale = (float)scale;
+  }
   dcr::launch_dropout_bits(reinterpret_cast<uint8_t*>(bits.data_ptr()), d, (uint64_t)seed,
-                           cur_stream());
+                           cur_stream(), e);
 }
 
 void mask_apply(const at::Tensor& in, const at::Tensor& bits, double scale, at::Tensor& out) {
@@ -1964,7 +1979,9 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor(g!) cnt0, Tensor(h!) cnt1, Tensor(i!) err, int spin_limit, int G, "
       "Tensor(j!)? diag=None, Tensor? xmask=None, float xscale=1.0) -> ()");
   m.def("dropout_bits(Tensor(a!) bits, int seed, int stream, float keep) -> ()");
-  m.def("dropout_bits_multi(Tensor(a!) bits, int seed, int[] streams, float[] keeps) -> ()");
+  m.def(
+      "dropout_bits_multi(Tensor(a!) bits, int seed, int[] streams, float[] keeps, "
+      "Tensor? ids=None, Tensor? E=None, float scale=1.0, Tensor(b!)? out=None) -> ()");
   m.def("mask_apply(Tensor input, Tensor bits, float scale, Tensor(a!) out) -> ()");
   m.def("embed_dropout(Tensor ids, Tensor E, Tensor? bits, float scale, Tensor(a!) out) -> ()");
   m.def("sample_supported(int V, int H) -> int", [](int64_t V, int64_t H) -> int64_t {

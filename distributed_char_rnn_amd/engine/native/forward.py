@@ -17,7 +17,7 @@ class ForwardMixin:
         c = self.cfg
         return training and (c.input_keep_prob < 1.0 or c.output_keep_prob < 1.0)
 
-    def _drop_masks(self, T: int, B: int) -> dict:
+    def _drop_masks(self, T: int, B: int, defer: bool = False) -> dict:
         """This step's dropout masks as bits (csrc/dropout.hip), drawn once per training step.
 
         DropoutWrapper(input_keep_prob, output_keep_prob) around every layer plus the
@@ -48,11 +48,27 @@ class ForwardMixin:
         if m["out"] is not None:
             streams.append(stream + 255)
             keeps.append(p_out)
-        if streams:
-            self.ops.dropout_bits_multi(m["all"], self._drop_seed, streams, keeps)
         dm = dict(inb=m["inb"], out=m["out"], sin=1.0 / p_in, sout=1.0 / p_out)
+        if streams:
+            if defer:  # launched by _draw_masks (with layer 0's masked embedding rows)
+                dm["pending"] = (m["all"], streams, keeps)
+            else:
+                self.ops.dropout_bits_multi(m["all"], self._drop_seed, streams, keeps)
         self.last_dropout_masks = dm
         return dm
+
+    def _draw_masks(self, dm: Optional[dict], ids=None, E=None, X=None) -> None:
+        """The deferred mask launch of ``_drop_masks(defer=True)``; with ``X`` the same launch
+        writes layer 0's masked embedding rows E[ids] ⊙ mask / keep (segment 0 is layer 0's
+        input mask), bit for bit the embed_dropout kernel's."""
+        pend = dm.pop("pending", None) if dm else None
+        if pend is None:
+            return
+        allb, streams, keeps = pend
+        if X is not None:
+            self.ops.dropout_bits_multi(allb, self._drop_seed, streams, keeps, ids, E, dm["sin"], X)
+        else:
+            self.ops.dropout_bits_multi(allb, self._drop_seed, streams, keeps)
 
     def _masked(self, x: torch.Tensor, bits: Optional[torch.Tensor], scale: float,
                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -81,7 +97,8 @@ class ForwardMixin:
         bufs = self._buffers(B, T, training)
         P = bufs["plan"]
         drop = self._dropout(training)
-        dm = self._drop_masks(T, B) if drop else None
+        # (launched after the prep launch has written the ids: with layer 0's embedding rows)
+        dm = self._drop_masks(T, B, defer=True) if drop else None
         # initial state into slot 0 of the sequence buffers, hand-off counters zeroed: all in
         # the same prep launch as the weight layouts
         for layer in range(self.L):
@@ -134,8 +151,14 @@ class ForwardMixin:
                 if layer == 0:  # the embedding rows (masked: embedding x input dropout)
                     X = lb.x_drop if inb is not None else torch.empty(N, H, dtype=bf16,
                                                                       device=self.dev)
-                    self.ops.embed_dropout(ids_tm.reshape(-1), self._head["E"], inb,
-                                           dm["sin"] if dm else 1.0, X)
+                    fuse = (dm is not None and inb is not None and "pending" in dm
+                            and H % 32 == 0 and self.knobs.debug.get("bits_embed", "1") != "0")
+                    if fuse:
+                        self._draw_masks(dm, ids_tm.reshape(-1), self._head["E"], X)
+                    else:
+                        self._draw_masks(dm)
+                        self.ops.embed_dropout(ids_tm.reshape(-1), self._head["E"], inb,
+                                               dm["sin"] if dm else 1.0, X)
                 else:
                     X = x_prev.reshape(N, H)
                     if inb is not None:

@@ -61,6 +61,8 @@ DEBUG_KEYS = {
     "head_omask": "0: top output dropout applied to dtop by a separate pass, not the head",
     "xin": "0: library zx GEMM for a dense layer-l input instead of the G = 1 two-layer "
            "forward's in-kernel projection",
+    "bits_embed": "0: layer 0's masked embedding rows by their own launch after the dropout bits "
+                  "instead of inside the bits launch",
     "xdst": "0: layer l+1's masked input rows by a separate mask pass instead of the G = 1 "
             "two-layer dropout forward's in-kernel store",
     "pair_dw": "0: separate h buffers per layer of a wavefront pair (two weight GEMMs for the "

@@ -137,3 +137,25 @@ def test_pair_forward_masked_rows_match_mask_pass(B, T, monkeypatch):
     assert torch.equal(xa, xb)
     assert torch.equal(oa, ob)
     assert float((ga - gb).norm() / gb.norm()) < 1e-6
+
+
+def test_bits_launch_writes_embedding_rows(monkeypatch):
+    """Layer 0's masked embedding rows written by the dropout-bits launch itself equal the
+    separate embed_dropout launch's (DCR_DEBUG=bits_embed=0), with the same masks."""
+    cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=256, num_layers=2,
+                      input_keep_prob=0.8, output_keep_prob=0.7)
+    B, T = 64, 12
+    x = torch.randint(0, 65, (B, T), dtype=torch.int32, device="cuda")
+    out = []
+    for knob in ("bits_embed=0", ""):
+        monkeypatch.setenv("DCR_DEBUG", knob)
+        m = CharRNN(cfg, device="cuda", seed=4)
+        m.backend.train_step(x, x, m.zero_state(B))
+        torch.cuda.synchronize()
+        bufs = m.backend._bufs[(B, T, True)]
+        dm = m.backend.last_dropout_masks
+        out.append((bufs["layers"][0].x_drop.clone(), dm["inb"][0].clone(), m.store.grad.clone()))
+    (xa, ma, ga), (xb, mb, gb) = out
+    assert torch.equal(ma, mb)
+    assert torch.equal(xa, xb)
+    assert float((ga - gb).norm() / gb.norm()) < 1e-6
