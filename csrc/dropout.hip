@@ -27,9 +27,11 @@ __global__ void __launch_bounds__(kDropThreads) dropout_bits_kernel(unsigned* __
                                                                     DropSegs d, uint64_t seed,
                                                                     DropEmbed e) {
   const int64_t total = d.nwords * d.n;
+  // (32-bit index math while it fits: a 64-bit division per word had cost more than its hashes)
+  const bool small = total < ((int64_t)1 << 31);
   for (int64_t i = blockIdx.x * (int64_t)kDropThreads + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * kDropThreads) {
-    const int m = (int)(i / d.nwords);
+    const int m = small ? (int)((unsigned)i / (unsigned)d.nwords) : (int)(i / d.nwords);
     const int64_t li = i - (int64_t)m * d.nwords;
     const uint64_t key = seed ^ mix64(d.stream[m] * 0x632BE59BD9B4E019ull);
     const unsigned kt = d.kt[m];
@@ -44,7 +46,7 @@ __global__ void __launch_bounds__(kDropThreads) dropout_bits_kernel(unsigned* __
     bits[i] = w;
     if (e.out && m == 0) {
       const int kw = e.K / 32;
-      const int64_t r = li / kw;
+      const int64_t r = small ? (int64_t)((unsigned)li / (unsigned)kw) : li / kw;
       const int c0 = 32 * (int)(li - r * kw);
       const float4* src = reinterpret_cast<const float4*>(e.E + (int64_t)e.ids[r] * e.K + c0);
       bf16x8* dst = reinterpret_cast<bf16x8*>(e.out + r * e.K + c0);

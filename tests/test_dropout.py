@@ -159,3 +159,36 @@ def test_bits_launch_writes_embedding_rows(monkeypatch):
     assert torch.equal(ma, mb)
     assert torch.equal(xa, xb)
     assert float((ga - gb).norm() / gb.norm()) < 1e-6
+
+
+def _mix64(z):
+    import numpy as np
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def test_dropout_bits_match_host_hash(dcr_ops):
+    """The mask words against a host (numpy uint64) evaluation of the same counter hash: word i
+    of segment m = 8 hashes of (seed ^ mix64(stream_m * C)) + 8 i + q, four 16-bit uniforms
+    each against keep * 65536 (csrc/dropout.hip)."""
+    import numpy as np
+    nseg, nw = 3, 1000
+    bits = torch.empty(nseg, nw * 4, dtype=torch.uint8, device="cuda")
+    seed, streams, keeps = 12345, [7, 8, 255], [0.8, 0.5, 0.64]
+    dcr_ops.dropout_bits_multi(bits, seed, streams, keeps)
+    got = bits.view(torch.int32).cpu().numpy().view(np.uint32)
+    with np.errstate(over="ignore"):
+        for m in range(nseg):
+            key = np.uint64(seed) ^ _mix64(np.uint64(streams[m]) * np.uint64(0x632BE59BD9B4E019))
+            kt = int(keeps[m] * 65536.0 + 0.5)
+            li = np.arange(nw, dtype=np.uint64)
+            w = np.zeros(nw, dtype=np.uint64)
+            for q in range(8):
+                r = _mix64(key + li * np.uint64(8) + np.uint64(q))
+                for e in range(4):
+                    u = (r >> np.uint64(16 * e)) & np.uint64(0xFFFF)
+                    w |= (u < np.uint64(kt)).astype(np.uint64) << np.uint64(4 * q + e)
+            assert np.array_equal(got[m], w.astype(np.uint32))
