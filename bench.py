@@ -39,6 +39,9 @@ def parse(argv=None):
     ap.add_argument("--layers", type=int, default=2)
     ap.add_argument("--vocab", type=int, default=65)
     ap.add_argument("--model", default="lstm")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="compute dtype on the GPU: bf16 MFMA operands (default) or the native "
+                         "fp32-operand recurrence (engine/native/fp32.py, a numerics mode)")
     ap.add_argument("--bucket_mb", type=float, default=8.0)
     ap.add_argument("--allreduce_dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--dp_mode", default="replicated", choices=["replicated", "sharded"],
@@ -93,7 +96,7 @@ def main(argv=None) -> int:
     cfg = ModelConfig(model=a.model, vocab_size=a.vocab, rnn_size=a.hidden, num_layers=a.layers,
                       clip_norm=a.clip_norm, input_keep_prob=a.input_keep_prob,
                       output_keep_prob=a.output_keep_prob)
-    model = CharRNN(cfg, device=device, seed=1234)
+    model = CharRNN(cfg, device=device, seed=1234, dtype=a.dtype)
     opt = TFAdam(model.store, clip=5.0, guard=model.error_word())
     model.bind_optimizer(opt)  # fused Adam + weight layouts (csrc/tail.hip)
     # (--force_sync: the exchange also runs on one rank, sharded or replicated)
@@ -224,14 +227,15 @@ def main(argv=None) -> int:
             "metric": METRIC, "value": cps, "unit": "chars/sec", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16" if device.type == "cuda" else "fp32",
+            "dtype": a.dtype if device.type == "cuda" else "fp32",
+            "backend": model.backend_name,
             "data": "synthetic (Shakespeare-unigram token stream, random-init weights)",
             "config": {"model": f"{a.layers}-layer {a.model.upper()}-{a.hidden} (vocab {a.vocab})",
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": T,
                        "parallelism": f"dp{world}" + ("-zero1" if sharded else "")},
             "vs_torch_nn_lstm_miopen": (cps / (MIOPEN_1GPU_CPS * world)
-                                        if (a.model, a.hidden, a.layers, T, B) ==
-                                        ("lstm", 512, 2, 128, 256) else None),
+                                        if (a.model, a.hidden, a.layers, T, B, a.dtype) ==
+                                        ("lstm", 512, 2, 128, 256, "bf16") else None),
             "keep_prob": [a.input_keep_prob, a.output_keep_prob],
             "graph": bool(a.graph),
             "final_loss": final_loss,

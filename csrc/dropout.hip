@@ -40,8 +40,8 @@ __global__ void __launch_bounds__(kDropThreads) dropout_bits_kernel(unsigned* __
     for (int q = 0; q < 8; ++q) {
       const uint64_t r = mix64(key + (uint64_t)li * 8 + q);
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        w |= ((unsigned)(r >> (16 * e)) & 0xFFFFu) < kt ? 1u << (4 * q + e) : 0u;
+      for (int u = 0; u < 4; ++u)
+        w |= ((unsigned)(r >> (16 * u)) & 0xFFFFu) < kt ? 1u << (4 * q + u) : 0u;
     }
     bits[i] = w;
     if (e.out && m == 0) {

@@ -113,6 +113,29 @@ int launch_big_step(bool bwd, const BigStepArgs& a, int cus, int force_S, hipStr
 void launch_fwd_step(int cell, const FwdStepArgs& a, hipStream_t s);
 void launch_bwd_step(int cell, const BwdStepArgs& a, hipStream_t s);
 
+// ---- cell_f32.hip: fp32-operand sequences (--dtype fp32) ------------------------------------
+struct F32Seq {
+  int cell;              // CELL_LSTM, CELL_GRU_A (the GRU), CELL_RNN
+  const float* WT;       // fwd: W_hᵀ [G·H, H] (GRU: Wg_hᵀ [2H, H])
+  const float* WT2;      // fwd GRU: Wc_hᵀ [H, H]
+  const float* W;        // bwd: W_h [H, GW] TF layout (GRU: Wc_h [H, H])
+  const float* W2;       // bwd GRU: Wg_h [H, 2H]
+  const float* zx;       // [T, B, GW] input projection + bias
+  const float* dtop;     // [T, B, H] or null
+  float* hs;             // [T+1, B, H]
+  float* cs;             // [T+1, B, H] (LSTM)
+  float* gates;          // [T, B, GW] (LSTM, GRU)
+  float* rh;             // [T, B, H] (GRU)
+  float* dz;             // [T, B, GW]
+  float* work0;          // [B, H]
+  float* work1;          // [B, H]
+  int T, B, H, GW;
+  float forget_bias;
+};
+bool f32_seq_supported(int cell, int H);
+void launch_f32_fwd_seq(const F32Seq& q, hipStream_t s);
+void launch_f32_bwd_seq(const F32Seq& q, hipStream_t s);
+
 // ---- xent.hip ---------------------------------------------------------------------------
 int xent_num_partials(int N);
 void launch_xent(const float* logits, const int* targets, int N, int V, float grad_scale,

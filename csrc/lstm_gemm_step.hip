@@ -441,6 +441,10 @@ using Cfg4 = BsCfg<64, 128, 4, 2, 1, false>;   // FwdL8: 256 x 128, 8 waves of 6
 using Cfg5 = BsCfg<128, 128, 2, 4, 1, true>;   // BwdL8: 128 x 128, 8 waves of 64 x 32
 using Cfg6 = BsCfg<32, 128, 2, 4, 1, false>;   // FwdM8: 128 x 128, 8 waves of 64 x 32
 using Cfg7 = BsCfg<32, 256, 2, 4, 1, false>;   // FwdW8: 128 x 256, 8 waves of 64 x 64
+using Cfg8 = BsCfg<64, 128, 1, 4, 1, true>;    // BwdN : 64 x 128, 4 waves of 64 x 32 (no split)
+using Cfg9 = BsCfg<64, 128, 1, 4, 2, true>;    // BwdN8: 64 x 128, 8 waves (2-way wave k split)
+using Cfg10 = BsCfg<128, 64, 2, 2, 1, true>;   // BwdM : 128 x 64, 4 waves of 64 x 32
+using Cfg11 = BsCfg<64, 256, 1, 4, 1, true>;   // BwdW : 64 x 256, 4 waves of 64 x 64
 
 namespace {
 struct BsPlan {
@@ -467,10 +471,14 @@ BsPlan bs_cfg(int id) {
     case 4: return bs_fill<Cfg4>(4);
     case 5: return bs_fill<Cfg5>(5);
     case 6: return bs_fill<Cfg6>(6);
+    case 8: return bs_fill<Cfg8>(8);
+    case 9: return bs_fill<Cfg9>(9);
+    case 10: return bs_fill<Cfg10>(10);
+    case 11: return bs_fill<Cfg11>(11);
     default: return bs_fill<Cfg7>(7);
   }
 }
-bool bs_cfg_bwd(int id) { return id == 2 || id == 3 || id == 5; }
+bool bs_cfg_bwd(int id) { return id == 2 || id == 3 || id == 5 || id >= 8; }
 
 BsPlan bs_plan(bool bwd, int B, int H, int cus, int force_S) {
   // forward: the configuration whose grid is closest to one workgroup per CU without a K split
@@ -478,7 +486,7 @@ BsPlan bs_plan(bool bwd, int B, int H, int cus, int force_S) {
   // B = 1024 cfg 4 45.7 us; split-K slices of large tiles lose to the serial slab reduction)
   int id = bwd ? (B >= 256 ? 2 : 3) : (B <= 160 ? 1 : B <= 640 ? 6 : 7);
   const int forced = debug_int("bigstep_cfg", -1);
-  if (forced >= 0 && forced <= 7 && bs_cfg_bwd(forced) == bwd && H % bs_cfg(forced).BU == 0)
+  if (forced >= 0 && forced <= 11 && bs_cfg_bwd(forced) == bwd && H % bs_cfg(forced).BU == 0)
     id = forced;
   BsPlan p = bs_cfg(id);
   p.tiles = (H / p.BU) * ((B + p.BN - 1) / p.BN);
@@ -523,6 +531,10 @@ int launch_big_step(bool bwd, const BigStepArgs& a0, int cus, int force_S, hipSt
     case 4: bs_launch<Cfg4>(grid, a, s); break;
     case 5: bs_launch<Cfg5>(grid, a, s); break;
     case 6: bs_launch<Cfg6>(grid, a, s); break;
+    case 8: bs_launch<Cfg8>(grid, a, s); break;
+    case 9: bs_launch<Cfg9>(grid, a, s); break;
+    case 10: bs_launch<Cfg10>(grid, a, s); break;
+    case 11: bs_launch<Cfg11>(grid, a, s); break;
     default: bs_launch<Cfg7>(grid, a, s); break;
   }
   return p.S;

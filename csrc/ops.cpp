@@ -393,6 +393,93 @@ int64_t lstm_big_step_bwd(const at::Tensor& Wh, const at::Tensor& dznext, const 
   return dcr::launch_big_step(true, a, num_cus(), (int)force_S, cur_stream());
 }
 
+// fp32-operand sequences (cell_f32.hip): the native --dtype fp32 recurrence
+dcr::F32Seq f32_seq_common(int64_t cell, const at::Tensor& hs, const at::Tensor& gates_or_dz) {
+  check_seq(hs, at::kFloat, "hs");
+  TORCH_CHECK(hs.dim() == 3, "hs must be [T+1, B, H]");
+  dcr::F32Seq q{};
+  q.cell = (int)cell;
+  q.T = (int)hs.size(0) - 1;
+  q.B = (int)hs.size(1);
+  q.H = (int)hs.size(2);
+  q.GW = (int)gates_or_dz.size(-1);
+  TORCH_CHECK(q.T >= 1 && q.B >= 1, "empty sequence");
+  TORCH_CHECK(dcr::f32_seq_supported(q.cell, q.H), "f32 sequence: unsupported cell / rnn_size");
+  const int G = q.cell == dcr::CELL_LSTM ? 4 : q.cell == dcr::CELL_GRU_A ? 3 : 1;
+  TORCH_CHECK(q.GW == G * q.H, "row width must be G * H");
+  return q;
+}
+
+void f32_fwd_seq(int64_t cell, const at::Tensor& WT, const c10::optional<at::Tensor>& WT2,
+                 const at::Tensor& zx, at::Tensor& hs, const c10::optional<at::Tensor>& cs,
+                 const c10::optional<at::Tensor>& gates, const c10::optional<at::Tensor>& rh,
+                 double forget_bias) {
+  dcr::F32Seq q = f32_seq_common(cell, hs, zx);
+  check_seq(WT, at::kFloat, "WT");
+  check_seq(zx, at::kFloat, "zx");
+  check_opt(WT2, at::kFloat, "WT2");
+  check_opt(cs, at::kFloat, "cs");
+  check_opt(gates, at::kFloat, "gates");
+  check_opt(rh, at::kFloat, "rh");
+  const int64_t T = q.T, B = q.B, H = q.H;
+  TORCH_CHECK(zx.numel() == T * B * q.GW, "zx must be [T, B, GW]");
+  const bool gru = q.cell == dcr::CELL_GRU_A, lstm = q.cell == dcr::CELL_LSTM;
+  TORCH_CHECK(WT.size(0) == (gru ? 2 : lstm ? 4 : 1) * H && WT.size(1) == H, "WT shape");
+  if (lstm) TORCH_CHECK(has(cs) && cs->numel() == (T + 1) * B * H, "cs must be [T+1, B, H]");
+  if (lstm || gru) TORCH_CHECK(has(gates) && gates->numel() == T * B * q.GW, "gates must be [T, B, GW]");
+  if (gru) {
+    TORCH_CHECK(has(WT2) && WT2->size(0) == H && WT2->size(1) == H, "WT2 must be [H, H]");
+    TORCH_CHECK(has(rh) && rh->numel() == T * B * H, "rh must be [T, B, H]");
+  }
+  q.WT = ptr<float>(WT);
+  q.WT2 = optr<float>(WT2);
+  q.zx = ptr<float>(zx);
+  q.hs = ptr<float>(hs);
+  q.cs = optr<float>(cs);
+  q.gates = optr<float>(gates);
+  q.rh = optr<float>(rh);
+  q.forget_bias = (float)forget_bias;
+  dcr::launch_f32_fwd_seq(q, cur_stream());
+}
+
+void f32_bwd_seq(int64_t cell, const at::Tensor& W, const c10::optional<at::Tensor>& W2,
+                 const c10::optional<at::Tensor>& dtop, const at::Tensor& hs,
+                 const c10::optional<at::Tensor>& cs, const c10::optional<at::Tensor>& gates,
+                 at::Tensor& dz, at::Tensor& work0, at::Tensor& work1) {
+  dcr::F32Seq q = f32_seq_common(cell, hs, dz);
+  check_seq(W, at::kFloat, "W");
+  check_opt(W2, at::kFloat, "W2");
+  check_opt(dtop, at::kFloat, "dtop");
+  check_opt(cs, at::kFloat, "cs");
+  check_opt(gates, at::kFloat, "gates");
+  check_seq(dz, at::kFloat, "dz");
+  check_seq(work0, at::kFloat, "work0");
+  check_seq(work1, at::kFloat, "work1");
+  const int64_t T = q.T, B = q.B, H = q.H;
+  const bool gru = q.cell == dcr::CELL_GRU_A, lstm = q.cell == dcr::CELL_LSTM;
+  TORCH_CHECK(dz.numel() == T * B * q.GW, "dz must be [T, B, GW]");
+  TORCH_CHECK(work0.numel() >= B * H && work1.numel() >= B * H, "work buffers must hold [B, H]");
+  if (has(dtop)) TORCH_CHECK(dtop->numel() == T * B * H, "dtop must be [T, B, H]");
+  if (lstm) TORCH_CHECK(has(cs) && cs->numel() == (T + 1) * B * H, "cs must be [T+1, B, H]");
+  if (lstm || gru) TORCH_CHECK(has(gates) && gates->numel() == T * B * q.GW, "gates must be [T, B, GW]");
+  if (gru) {
+    TORCH_CHECK(W.size(0) == H && W.size(1) == H, "W (Wc_h) must be [H, H]");
+    TORCH_CHECK(has(W2) && W2->size(0) == H && W2->size(1) == 2 * H, "W2 (Wg_h) must be [H, 2H]");
+  } else {
+    TORCH_CHECK(W.size(0) == H && W.size(1) == q.GW, "W must be [H, GW]");
+  }
+  q.W = ptr<float>(W);
+  q.W2 = optr<float>(W2);
+  q.dtop = optr<float>(dtop);
+  q.hs = const_cast<float*>(ptr<float>(hs));
+  q.cs = const_cast<float*>(optr<float>(cs));
+  q.gates = optr<float>(gates);
+  q.dz = ptr<float>(dz);
+  q.work0 = ptr<float>(work0);
+  q.work1 = ptr<float>(work1);
+  dcr::launch_f32_bwd_seq(q, cur_stream());
+}
+
 void rnn_bwd_seq(int64_t cell, const at::Tensor& W, const c10::optional<at::Tensor>& W2,
                  const at::Tensor& dtop, at::Tensor& dz, const c10::optional<at::Tensor>& dzx,
                  const c10::optional<at::Tensor>& gates, const c10::optional<at::Tensor>& pre,
@@ -1833,6 +1920,13 @@ TORCH_LIBRARY(dcr, m) {
   m.def("big_step_supported(int B, int H) -> bool", [](int64_t B, int64_t H) -> bool {
     return dcr::big_step_supported((int)B, (int)H);
   });
+  m.def("f32_fwd_seq(int cell, Tensor WT, Tensor? WT2, Tensor zx, Tensor(a!) hs, Tensor(b!)? cs, "
+        "Tensor(c!)? gates, Tensor(d!)? rh, float forget_bias) -> ()");
+  m.def("f32_bwd_seq(int cell, Tensor W, Tensor? W2, Tensor? dtop, Tensor hs, Tensor? cs, "
+        "Tensor? gates, Tensor(a!) dz, Tensor(b!) work0, Tensor(c!) work1) -> ()");
+  m.def("f32_seq_supported(int cell, int H) -> bool", [](int64_t c, int64_t H) -> bool {
+    return dcr::f32_seq_supported((int)c, (int)H);
+  });
   m.def(
       "rnn_fwd_seq(int cell, Tensor WT, Tensor? WT2, Tensor zx, Tensor? ids, Tensor(a!) hbuf, "
       "Tensor(b!)? h32, Tensor(c!)? cbuf, Tensor(d!)? gates, Tensor(e!)? pre, Tensor(f!)? aux, "
@@ -2020,6 +2114,8 @@ TORCH_LIBRARY_IMPL(dcr, CUDA, m) {
   m.impl("head_wide", &head_wide);
   m.impl("adam_clip", &adam_clip);
   m.impl("rnn_fwd_seq", &rnn_fwd_seq);
+  m.impl("f32_fwd_seq", &f32_fwd_seq);
+  m.impl("f32_bwd_seq", &f32_bwd_seq);
   m.impl("rnn_bwd_seq", &rnn_bwd_seq);
   m.impl("xent", &xent);
   m.impl("xent_wide", &xent_wide);

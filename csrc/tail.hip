@@ -544,11 +544,6 @@ __global__ void __launch_bounds__(kTailThreads, 2) tail_kernel(TailArgs a) {
   float (*tile)[65] = reinterpret_cast<float (*)[65]>(lds_buf);
   const int G = gridDim.x;
   (void)G;
-  // a step whose persistent kernels timed out: no update (weights and slots stay unchanged; the
-  // host raises when it reads the word).  FINALIZE still runs (its sums are harmless).
-  if (a.phase == 1 && a.skip_if &&
-      __hip_atomic_load(a.skip_if, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
-    return;
   AdamCtx A{};
   if (a.phase == 1) {
     // the global sum of squares: from this step's FINALIZE launch, or (data parallelism: the
@@ -557,7 +552,13 @@ __global__ void __launch_bounds__(kTailThreads, 2) tail_kernel(TailArgs a) {
     const float lr_t = a.lr_dev ? *a.lr_dev : a.lr_t;
     const float norm = sqrtf(total) * a.gscale;
     const float s = ((a.clip > 0.f) ? a.clip / fmaxf(norm, a.clip) : 1.f) * a.gscale;
+    // (the pre-clip norm is reported for a guarded step too, as the plain adam_clip does)
     if (blockIdx.x == 0 && threadIdx.x == 0 && a.norm_out) a.norm_out[0] = norm;
+    // a step whose persistent kernels timed out: no update (weights and slots stay unchanged;
+    // the host raises when it reads the word).  FINALIZE still runs (its sums are harmless).
+    if (a.skip_if &&
+        __hip_atomic_load(a.skip_if, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
+      return;
     A = AdamCtx{s, lr_t, a.b1, a.b2, a.eps};
   }
 

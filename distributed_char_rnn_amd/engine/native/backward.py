@@ -47,13 +47,18 @@ class BackwardMixin:
         dp = on_ready is not None
         use_wgrad = self.knobs.on("wgrad")  # hand-written token-reduction GEMMs (csrc/wgrad.hip)
         tail = self._tail_backward_ok(bufs0)
-        q = TailQueue(self, wgrad=use_wgrad) if tail else SumQueue(self.ops, wgrad=use_wgrad)
+        q = (TailQueue(self, wgrad=use_wgrad, collectives=dp) if tail
+             else SumQueue(self.ops, wgrad=use_wgrad))
         self._tail_total_ok = False
         if on_ready is not None:
             cb_user = on_ready
 
-            gs = getattr(cb_user, "__self__", None)
-            probe = getattr(gs, "launches_at", None)
+            # which reports complete a bucket: an on_ready object that exposes launches_at()
+            # itself, or the GradSync / ShardedStep a bound ready() belongs to (any other
+            # callable flushes on every report)
+            probe = getattr(cb_user, "launches_at", None)
+            if probe is None:
+                probe = getattr(getattr(cb_user, "__self__", None), "launches_at", None)
 
             def on_ready(off, _cb=cb_user):  # noqa: F811 - sums complete before a bucket leaves
                 if probe is not None and not probe(off):

@@ -51,6 +51,7 @@ class TailTable:
         self.tiles: List[int] = []
         self.max_tasks = max_tasks
         self.sig_tiles = {}  # dependency counter -> producer tiles
+        self.waits = 0       # tasks that wait in-launch on a dependency counter
 
     def __len__(self) -> int:
         return len(self.ops)
@@ -111,6 +112,7 @@ class TailTable:
             need = self.sig_tiles.get(wait, 0)
             if need <= 0:
                 raise ValueError(f"tail table: nothing signals counter {wait} before this task")
+            self.waits += 1
         nt = task_tiles(op, rows, cols, k, nslab, int(vec4))
         if sig >= 0:
             self.sig_tiles[sig] = self.sig_tiles.get(sig, 0) + nt
@@ -240,10 +242,14 @@ class TailQueue:
 
     SUM, COLSUM = 3, 4  # gemm.SumQueue task kinds (mm_tn / _bias_sum call add_sum / add_colsum)
 
-    def __init__(self, backend, wgrad: bool = False):
+    def __init__(self, backend, wgrad: bool = False, collectives: bool = False):
         from .gemm import SumQueue
 
         self.be = backend
+        # gradient buckets may be in flight on RCCL's stream while a flush runs (data
+        # parallel): its collectives hold CUs, so a flush whose tiles wait in-launch on other
+        # tiles takes the atomic tile queue (static tiles need the whole grid co-resident)
+        self.collectives = collectives
         self.ops = backend.ops
         self._gemmq = SumQueue(backend.ops, wgrad=wgrad)  # its wgrad grouping, not its flush
         self.wgrad = wgrad
@@ -396,5 +402,5 @@ class TailQueue:
             run(self.ops, t, 0, be._fin_ws, be.err, be.spin_limit,
                 total_out=total_out if ok else None,
                 extra=s.norm_slot_view() if (ok and use_slot) else None,
-                dynamic=be.tail_dynamic())
+                dynamic=be.tail_dynamic() or (self.collectives and t.waits > 0))
         return ok

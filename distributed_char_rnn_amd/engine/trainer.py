@@ -263,13 +263,15 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
     summary_every = getattr(args, "summary_every", 100)
     max_steps = getattr(args, "max_steps", 0)
     steps_done = 0
-    pending = None  # (global_step, epoch, loss_tensor, t_start)
-    last_t = time.time()
+    # Only logged steps (every --log_every, the last, and checkpoint steps) read their loss back:
+    # a logged step is flushed after the NEXT step was enqueued, so the host never drains the
+    # GPU, and time/batch is the mean over the steps since the previous logged step.
+    pending = None  # (global_step, epoch, loss_tensor, steps in its span, span start)
+    span_t0, span_n = None, 0
 
     def flush(p, now):
-        nonlocal last_t
-        gs, e, loss_t, t0 = p
-        dt = now - t0
+        gs, e, loss_t, n, ts = p
+        dt = (now - ts) / max(n, 1)
         loss = float(loss_t)
         if chief and (gs % log_every == 0 or gs == total):
             print(progress_line(gs, total, e, loss, dt, chars_per_step / max(dt, 1e-9)), flush=True)
@@ -313,6 +315,8 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
                 state = saved_state
         for b in range(b0, nb):
             t0 = time.time()
+            if span_t0 is None:
+                span_t0 = t0
             x, y = loader.next_batch()
             if dev_batches is not None:  # the same batch, already resident on the device
                 x, y = dev_batches[0][b], dev_batches[1][b]
@@ -341,7 +345,8 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
             process_group.maybe_inject_fault(rank, global_step)
             if pending is not None:
                 flush(pending, t0)
-            pending = (global_step, e, loss_t, t0)
+                pending = None
+            span_n += 1
             if want and extras:
                 if extras.get("logits") is not None:
                     logger.histogram("logits", extras["logits"].float().cpu().numpy(), global_step)
@@ -351,7 +356,11 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
             last = (e == args.num_epochs - 1 and b == nb - 1)
             if max_steps and steps_done >= max_steps:
                 last, stop = True, True
-            if step_idx % args.save_every == 0 or last:
+            saving = step_idx % args.save_every == 0 or last
+            if global_step % log_every == 0 or global_step == total or saving:
+                pending = (global_step, e, loss_t, span_n, span_t0)
+                span_t0, span_n = None, 0
+            if saving:
                 if pending is not None:
                     flush(pending, time.time())
                     pending = None

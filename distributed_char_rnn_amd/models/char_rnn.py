@@ -6,6 +6,8 @@ Equivalent of the reference ``Model`` (model.py:8-140) minus the TF graph: param
 * ``native``    -- gfx950 HIP kernels (engine/native/): fused recurrent cell
                    kernels, fused softmax-CE, embedding-projection gather/segment-sum, etc.
                    Mandatory on GPU; raises if the native library is missing.
+* ``native32``  -- ``dtype="fp32"`` on a GPU: the oracle's step with every recurrent cell step
+                   on the fp32-operand HIP kernels (engine/native/fp32.py).
 * ``reference`` -- pure PyTorch autograd with TF cell semantics (models/reference.py); the
                    CPU path and the numerical oracle.
 
@@ -41,13 +43,19 @@ class CharRNN:
         self.device = torch.device(device)
         self.store = ParamStore(cfg, self.device, seed)
         if backend == "auto":
-            # fp32 on the GPU runs the autograd oracle; the native kernels compute in bf16
+            # fp32 on the GPU: the native fp32-operand recurrence (engine/native/fp32.py) for
+            # LSTM / GRU / BasicRNN; the default native kernels compute with bf16 operands
             backend = "native" if (self.device.type == "cuda" and dtype != "fp32") else "reference"
             if self.device.type == "cuda" and dtype == "fp32":
-                import warnings
+                from ..engine.native import fp32 as f32mod
 
-                warnings.warn("dtype fp32 on the GPU: running the PyTorch autograd path (fp32 "
-                              "hipBLASLt GEMMs); the native HIP kernels compute in bf16")
+                if f32mod.supported(cfg):
+                    backend = "native32"
+                else:
+                    import warnings
+
+                    warnings.warn(f"dtype fp32 with {cfg.model} / rnn_size {cfg.rnn_size}: no "
+                                  "fp32 native kernels; running the PyTorch autograd path")
             if backend == "native" and cfg.rnn_size % 32 != 0 and cfg.model == "nas":
                 import warnings
 
@@ -64,6 +72,10 @@ class CharRNN:
             from ..engine.native import NativeBackend
 
             self.backend = NativeBackend(self.store, dtype=dtype, seed=seed or 0, rank=rank)
+        elif backend == "native32":
+            from ..engine.native.fp32 import NativeFp32Backend
+
+            self.backend = NativeFp32Backend(self.store, seed=(seed or 0) + 7919 * rank)
         elif backend == "reference":
             self.backend = ReferenceBackend(self.store, seed=(seed or 0) + 7919 * rank)
         else:

@@ -245,6 +245,10 @@ class ReferenceBackend:
         self.gen = torch.Generator(device=store.device.type if store.device.type == "cpu" else "cpu")
         self.gen.manual_seed(seed)
 
+    def _forward(self, cfg, params, x, state, training=True, gen=None, taps=None, masks=None):
+        """The model's forward (engine/native/fp32.py swaps in the native fp32 recurrence)."""
+        return forward(cfg, params, x, state, training=training, gen=gen, taps=taps, masks=masks)
+
     def params(self, requires_grad: bool):
         out = {}
         for n in self.store.names():
@@ -257,8 +261,8 @@ class ReferenceBackend:
         params = self.params(True)
         gen = self.gen if self.store.device.type == "cpu" else None
         taps = {}
-        logits, new_state, _ = forward(self.cfg, params, x, state, training=True, gen=gen,
-                                       taps=taps, masks=masks)
+        logits, new_state, _ = self._forward(self.cfg, params, x, state, training=True, gen=gen,
+                                             taps=taps, masks=masks)
         cost, per = loss_fn(logits, y)
         names = self.store.names()
         grads = torch.autograd.grad(cost, [params[n] for n in names] + [taps["emb"]],
@@ -290,11 +294,13 @@ class ReferenceBackend:
     @torch.no_grad()
     def step_logits(self, x_t: torch.Tensor, state: State):
         """One inference step (B, 1) -> (logits [B, V], new_state); no dropout."""
-        logits, new_state, _ = forward(self.cfg, self.params(False), x_t, state, training=False)
+        logits, new_state, _ = self._forward(self.cfg, self.params(False), x_t, state,
+                                             training=False)
         return logits, new_state
 
     @torch.no_grad()
     def eval_loss(self, x, y, state: State):
-        logits, new_state, _ = forward(self.cfg, self.params(False), x, state, training=False)
+        logits, new_state, _ = self._forward(self.cfg, self.params(False), x, state,
+                                             training=False)
         cost, _ = loss_fn(logits, y)
         return cost, new_state

@@ -98,7 +98,7 @@ def main():
         if a.cfgs:
             for cid in (int(x) for x in a.cfgs.replace(":", ",").split(",")):
                 os.environ["DCR_DEBUG"] = f"bigstep_cfg={cid}"
-                bwd = cid in (2, 3, 5)
+                bwd = cid in (2, 3, 5) or cid >= 8
                 # the workspace depends on the configuration's tile count
                 wf, nt = ops.big_step_workspace(bwd, B, H, a.S)
                 ws_c = torch.empty(max(wf, 4), device=dev)

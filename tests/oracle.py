@@ -45,6 +45,9 @@ TOL = {
     "head_wide": (1.0e-2, 1.2e-2),
     "long_t": (9e-3, 1.4e-2),
     "big_batch": (1.0e-2, 1.3e-2),
+    # the native fp32-operand recurrence (csrc/cell_f32.hip): no operand rounding, so only
+    # summation order and the v_exp / v_rcp activations separate it from the oracle
+    "fp32": (1e-4, 1e-4),
 }
 
 BLOCK_ROWS = 16

@@ -113,7 +113,7 @@ def test_dropout_library_input_projection_matches_oracle(B, H, L, monkeypatch):
     assert nat.backend._persist_plan(B, True, 5).pair
 
 
-@pytest.mark.parametrize("B,T", [(256, 24), (256, 130)])
+@pytest.mark.parametrize("B,T", [(256, 24), (256, 130), (200, 24)])
 def test_pair_forward_masked_rows_match_mask_pass(B, T, monkeypatch):
     """The G = 1 two-layer dropout forward writes layer l+1's masked input rows itself
     (Lstm2Args.xdst) and the top layer's output-dropout rows (odst): bitwise the rows of the
