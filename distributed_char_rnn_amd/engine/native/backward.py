@@ -391,9 +391,14 @@ class BackwardMixin:
         return loss_buf[0], new_state, extras
 
     def _tail_backward_ok(self, bufs) -> bool:
-        """The step's deferred gradient work runs as tail FINALIZE launches (csrc/tail.hip):
-        LSTM / BasicRNN with the fused head (the tasks the finalize covers)."""
-        return (self.knobs.on("tail") and self.cfg.model in ("lstm", "rnn") and self.fused_head
+        """The step's deferred gradient work (slab sums, bias sums, the gather route's
+        products) runs as tail FINALIZE launches (csrc/tail.hip) instead of prep-launch flushes:
+        LSTM / BasicRNN / GRU with the fused head.  The wide head's step keeps the prep flush by
+        default (DCR_DEBUG=fin_wide=1: FINALIZE; config 5 trace: 24.2 vs 17.8 us, the global
+        norm then needs its own launch either way since the atomic embedding scatter is not a
+        FINALIZE output)."""
+        return (self.knobs.on("tail") and self.cfg.model in ("lstm", "rnn", "gru")
+                and (self.fused_head or (self.wide_head and self.knobs.dbg("fin_wide", "0") == "1"))
                 and int(self.ops.tail_grid()) > 0)
 
     def _tail_gather_ok(self, layer: int, bufs, fused_dew: bool) -> bool:

@@ -34,11 +34,13 @@ class LayoutsMixin:
 
     # ---- the fused Adam of csrc/tail.hip (TFAdam.fused) -------------------------------------
     def tail_adam_ok(self) -> bool:
-        """The fused Adam keeps the weight layouts current itself: LSTM / BasicRNN with the
-        layer-0 gather table of a narrow vocabulary (the layouts it writes are W_h / W_x /
-        softmax_w slices of one bf16 mirror plus the transposes and the table)."""
-        return (self.knobs.on("tail") and self.cfg.model in ("lstm", "rnn")
-                and self.V <= SEG_LDS_MAX_V and not getattr(self, "padded_inner", False)
+        """The fused Adam keeps the weight layouts current itself: LSTM / BasicRNN (the layouts
+        it writes are W_h / W_x / softmax_w / embedding slices of one bf16 mirror plus the
+        transposes; a narrow vocabulary's layer-0 gather table is a task of the same launch, a
+        wide one's the gemm_nt launch behind it, reading the mirror's bf16 E)."""
+        wide_ok = self.V <= SEG_LDS_MAX_V or self.knobs.on("tail_wide")
+        return (self.knobs.on("tail") and self.cfg.model in ("lstm", "rnn") and wide_ok
+                and not getattr(self, "padded_inner", False)
                 and int(self.ops.tail_grid()) > 0)
 
     def tail_dynamic(self) -> bool:
@@ -86,7 +88,21 @@ class LayoutsMixin:
                         b1=opt.b1, b2=opt.b2, eps=opt.eps, clip=opt.clip, gscale=float(grad_scale),
                         lr_dev=lr_dev, skip_if=opt.guard, norm_out=opt.last_norm,
                         dynamic=self.tail_dynamic())
+        if self.V > SEG_LDS_MAX_V and self._head.get("table") is not None:
+            # wide vocabulary: the E·W_x0 + b0 table from the updated bf16 mirror (E) and W_x0ᵀ
+            # (an output of the update); a skipped (guarded) update leaves both unchanged, so
+            # the table stays consistent with the weights either way
+            self._wide_table()
         return True
+
+    def _wide_table(self) -> None:
+        w0, hd = self._w[0], self._head
+        Eb = hd.get("Ebf")
+        if w0.WxT is not None and Eb is not None and self._table_nt_ok(self.H, w0.WxT.shape[0]):
+            self.ops.gemm_nt(Eb, w0.WxT, hd["table"], w0.bias)
+        else:
+            E = Eb if Eb is not None else hd["E"].to(bf16)
+            torch.addmm(w0.bias, E, w0.Wx, out_dtype=f32, out=hd["table"])
 
     def fused_adam_done(self) -> None:
         """The update ran (the store's version was bumped): the layouts match it."""
@@ -190,6 +206,10 @@ class LayoutsMixin:
                 T += [(km, lw.Wh, 0), (km, lw.WhT, 1), (kx, lw.Wx, 0)]
             self._w.append(lw)
         Ws32 = s.view("rnnlm/softmax_w")
+        if mv is not None and self.V > SEG_LDS_MAX_V:
+            # the wide vocabulary's bf16 E (the gemm_nt table's operand) is the mirror's slice:
+            # the fused Adam writes it with every update
+            self._head_ebf = mv("embedding")
         self._head = dict(E=s.view("embedding"),
                           Ws=mv("rnnlm/softmax_w") if mv else e(H, self.V),
                           bs=s.view("rnnlm/softmax_b"))
@@ -204,6 +224,9 @@ class LayoutsMixin:
         if self.wide_head:
             self._head["WsTw"] = e(self.V, H)   # softmax_wᵀ [V, H] (head_wide.hip)
             T.append((Ws32, self._head["WsTw"], 1))
+        if getattr(self, "_head_ebf", None) is not None:
+            self._head["Ebf"] = self._head_ebf
+            self._head_ebf = None
 
     def _table_nt_ok(self, D: int, GW: int) -> bool:
         """The wide-vocabulary gather table as a gemm_nt launch ([V, D] x [GW, D]ᵀ)."""

