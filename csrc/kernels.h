@@ -337,8 +337,14 @@ struct Lstm2BwdArgs {
   int wgarr;            // as Lstm2Args::wgarr
   int diag_all;         // diag holds [grid, T+2, 8] s_memrealtime stamps of every workgroup
   int xcdloc;           // as Lstm2Args::xcdloc (exchange word: dwords 2-3 of cnt0's slot 0)
+  float* pring;         // optional reduce-scatter partial ring (lstm2_bwd_rs.hip), fp32
 };
 int launch_lstm2_bwd_persist(const Lstm2BwdArgs& a, int cus, hipStream_t s);
+// the reduce-scatter form of the 32 x 16 BPTT (lstm2_bwd_rs.hip): no dropout, H in {128, 256,
+// 512}; pring holds lstm2_bwd_rs_ring_floats(H, B) floats
+size_t lstm2_bwd_rs_ring_floats(int H, int B);
+bool lstm2_bwd_rs_ok(int H, int B, int cus);
+int launch_lstm2_bwd_rs(const Lstm2BwdArgs& a, int cus, hipStream_t s);
 // the 32-unit x 16-row form of the same BPTT (lstm2_bwd_wide.hip): nbg = ceil(B / 16) 16-row
 // columns, G = 1
 bool lstm2_bwd_wide_ok(int H, int B, int cus);

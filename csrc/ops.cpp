@@ -1140,7 +1140,8 @@ void lstm2_persist_bwd(const at::Tensor& Wh0, const at::Tensor& Wh1, const at::T
                        const c10::optional<at::Tensor>& db_part1, at::Tensor& cnt0,
                        at::Tensor& cnt1, at::Tensor& err, int64_t spin_limit, int64_t G,
                        const c10::optional<at::Tensor>& diag,
-                       const c10::optional<at::Tensor>& xmask, double xscale) {
+                       const c10::optional<at::Tensor>& xmask, double xscale,
+                       const c10::optional<at::Tensor>& pring) {
   for (auto* t : {&Wh0, &Wh1, &Wx1}) check_seq(*t, at::kBFloat16, "W");
   check_seq(dtop1, at::kFloat, "dtop1");
   for (const at::Tensor* t : {&gates0, &gates1, (const at::Tensor*)&dz0, (const at::Tensor*)&dz1,
@@ -1195,7 +1196,21 @@ void lstm2_persist_bwd(const at::Tensor& Wh0, const at::Tensor& Wh1, const at::T
   a.db_rows = 2 * nbg / (int)G;
   int rc;
   // (the wide kernel addresses its activation operands with 32-bit buffer offsets)
-  if (G == 1 && dcr::lstm2_bwd_wide_ok(H, B, num_cus()) && n4 * 2 < ((int64_t)1 << 32)) {
+  // (the reduce-scatter form is opt-in, DCR_DEBUG=bwd_rs=1: 7.1 vs 4.6 us per tick at the
+  // headline shape, BASELINE.md "Measured and rejected")
+  const bool rs = G == 1 && has(pring) && !a.xmask && dcr::debug_int("bwd_rs", 0) == 1 &&
+                  dcr::lstm2_bwd_rs_ok(H, B, num_cus()) && n4 * 2 < ((int64_t)1 << 32);
+  if (rs) {
+    // reduce-scatter hand-off: each workgroup sends every unit block its [16 x 32] fp32 slice
+    // of dZ_own·Wᵀ instead of every workgroup reading the column's whole dZ rows
+    check_seq(*pring, at::kFloat, "pring");
+    TORCH_CHECK(pring->numel() >= (int64_t)dcr::lstm2_bwd_rs_ring_floats(H, B),
+                "pring must hold ", dcr::lstm2_bwd_rs_ring_floats(H, B), " floats");
+    a.pring = ptr<float>(*pring);
+    a.nbg = (B + 15) / 16;
+    check_lstm2_counters(cnt0, a.nbg, T);
+    rc = dcr::launch_lstm2_bwd_rs(a, num_cus(), cur_stream());
+  } else if (G == 1 && dcr::lstm2_bwd_wide_ok(H, B, num_cus()) && n4 * 2 < ((int64_t)1 << 32)) {
     // 32-unit x 16-row workgroups: half the dZ payload per workgroup and tick
     a.nbg = (B + 15) / 16;
     for (auto* c : {&cnt0, &cnt1}) check_lstm2_counters(*c, a.nbg, T);
@@ -2052,6 +2067,12 @@ TORCH_LIBRARY(dcr, m) {
         });
   m.def("lstm2_xin_ok(int H) -> bool",
         [](int64_t H) -> bool { return dcr::lstm2_xin_ok((int)H, num_cus()); });
+  m.def("lstm2_bwd_rs_ring_floats(int H, int B) -> int", [](int64_t H, int64_t B) -> int64_t {
+    return (int64_t)dcr::lstm2_bwd_rs_ring_floats((int)H, (int)B);
+  });
+  m.def("lstm2_bwd_rs_ok(int H, int B) -> bool", [](int64_t H, int64_t B) -> bool {
+    return dcr::lstm2_bwd_rs_ok((int)H, (int)B, num_cus());
+  });
   m.def("lstm2_bwd_wide_ok(int H, int B) -> bool", [](int64_t H, int64_t B) -> bool {
     return dcr::lstm2_bwd_wide_ok((int)H, (int)B, num_cus());
   });
@@ -2071,7 +2092,7 @@ TORCH_LIBRARY(dcr, m) {
       "Tensor cbuf0, Tensor gates1, Tensor cbuf1, Tensor(a!) dz0, Tensor(b!) dz1, "
       "Tensor(c!) zring0, Tensor(d!) zring1, Tensor(e!)? db_part0, Tensor(f!)? db_part1, "
       "Tensor(g!) cnt0, Tensor(h!) cnt1, Tensor(i!) err, int spin_limit, int G, "
-      "Tensor(j!)? diag=None, Tensor? xmask=None, float xscale=1.0) -> ()");
+      "Tensor(j!)? diag=None, Tensor? xmask=None, float xscale=1.0, Tensor(k!)? pring=None) -> ()");
   m.def("dropout_bits(Tensor(a!) bits, int seed, int stream, float keep) -> ()");
   m.def(
       "dropout_bits_multi(Tensor(a!) bits, int seed, int[] streams, float[] keeps, "

@@ -172,7 +172,7 @@ class BackwardMixin:
                                            bufs["cnt"][self.L + layer], self.err,
                                            self.spin_limit, P.pair_g, None,
                                            dm["inb"][layer] if dm else None,
-                                           dm["sin"] if dm else 1.0)
+                                           dm["sin"] if dm else 1.0, bufs.get("prs"))
                 paired_done = lo
                 if lo == 0 and user_ready is not None:
                     on_ready = _release()

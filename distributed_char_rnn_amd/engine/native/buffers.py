@@ -145,6 +145,12 @@ class BuffersMixin:
             zring=e(2 * Bp * GW, dt=bf16) if (training and m == "lstm") else None,
             zring2=e(2 * Bp * GW, dt=bf16) if plan.pair_bwd else None,
             o_drop=e(N, H, dt=bf16) if (training and drop) else None,
+            # fp32 partial ring of the reduce-scatter pair BPTT (csrc/lstm2_bwd_rs.hip; no
+            # dropout; opt-in DCR_DEBUG=bwd_rs=1: slower than the all-gather kernel)
+            prs=(e(int(self.ops.lstm2_bwd_rs_ring_floats(H, B)))
+                 if (plan.pair_bwd and not drop and m == "lstm"
+                     and self.knobs.dbg("bwd_rs", "0") == "1"
+                     and bool(self.ops.lstm2_bwd_rs_ok(H, B))) else None),
         )
         if training and self.fused_head and self.V <= 256 and self.knobs.on("dws_wgrad"):
             # the fused head writes its bf16 dlogits into rows of 256 whose other columns stay

@@ -43,6 +43,8 @@ DEBUG_KEYS = {
                "unconditional (exact waitcnt), 6 (default) 1 + the dtop stash inside the MFMA "
                "phase (C++)",
     "fused_head": "0: library logits GEMM + CE kernel instead of the fused head",
+    "bwd_rs": "1: the reduce-scatter pair BPTT (lstm2_bwd_rs.hip) instead of the all-gather "
+              "one (lstm2_bwd_wide.hip); default 0 (measured slower)",
     "tail_wide": "0: the wide-vocabulary head's step keeps the plain Adam + prep layout "
                  "refresh instead of the fused Adam (csrc/tail.hip phase 1)",
     "fin_wide": "1: the wide-vocabulary head's deferred sums as a tail FINALIZE launch "

@@ -89,8 +89,51 @@ def skew(d, H, B, T):
     return list(zip(names, r)), by_xcd
 
 
+RS_PHASES = ["poll", "barrier + partial/operand loads landed", "epilogue -> dZ in LDS",
+             "barrier", "products + partial stores issued", "store drain", "arrival"]
+
+
+def rs_stamps(d, n_ticks):
+    """Mean per-tick phase durations (s_memtime ticks) of the reduce-scatter BPTT's workgroup 0
+    (RS_STAMP 0..7 of csrc/lstm2_bwd_rs.hip) over the steady ticks."""
+    d = d.cpu().numpy().astype("float64").reshape(-1, 8)[:n_ticks]
+    lo, hi = 3, n_ticks - 3
+    tick = (d[hi, 0] - d[lo, 0]) / (hi - lo)
+    return tick, [(RS_PHASES[i], np.mean(d[lo:hi, i + 1] - d[lo:hi, i])) for i in range(7)]
+
+
+def rs_skew(d, H, B, T):
+    """Every workgroup's reduce-scatter BPTT stamps [grid, T+2, 8] (s_memrealtime, 10 ns; RS_STAMP
+    0..7): per-workgroup phase means over steady ticks (median / max over workgroups) and the
+    hand-off: a column's last arrival (stamp 6) of tick tau-1 -> each member's poll done (1)."""
+    d = d.cpu().numpy().astype("float64") * 0.01  # us
+    nu, ncol = H // 32, (B + 15) // 16
+    lo, hi = 3, T - 3
+    rows = []
+    live = [bid for bid in range(d.shape[0]) if d[bid, lo, 0] > 0]
+    for i, name in enumerate(RS_PHASES):
+        v = np.array([np.mean(d[bid, lo:hi, i + 1] - d[bid, lo:hi, i]) for bid in live])
+        rows.append((f"{name} (median / max WG)", np.median(v), v.max()))
+    # the column of a block under the XCD-grouped map (persist_common.h map_block_grid)
+    colof = {}
+    for bid in live:
+        x, j = bid % 8, bid // 8
+        colof[bid] = x + 8 * (j // nu)
+    lat, work = [], []
+    for c in set(colof.values()):
+        members = [bid for bid in live if colof[bid] == c]
+        for t in range(lo, hi):
+            last = max(d[bid, t - 1, 6] for bid in members)
+            lat += [d[bid, t, 1] - last for bid in members]
+            work += [d[bid, t, 6] - d[bid, t, 1] for bid in members]
+    rows.append(("last arrival -> poll done", np.median(lat), np.max(lat)))
+    rows.append(("poll done -> own arrival", np.median(work), np.max(work)))
+    rows.append(("tick period", np.median(np.diff(d[live[0], lo:hi, 0])), 0.0))
+    return rows
+
+
 def run(ops, H, T, B, G, want_stamps, reps=5, want_skew=False, drop=False, gather=False,
-        xin=False):
+        xin=False, rs=False):
     dev = "cuda"
     G = int(ops.lstm2_plan(H, B, G))
     if not G:
@@ -136,16 +179,22 @@ def run(ops, H, T, B, G, want_stamps, reps=5, want_skew=False, drop=False, gathe
     zr0, zr1 = (torch.empty(2 * Bp * 4 * H, dtype=torch.bfloat16, device=dev) for _ in range(2))
     db0, db1 = (torch.empty(2 * nbg // G, 4 * H, device=dev) for _ in range(2))
     dbw = torch.zeros(T + 2, G, 8, dtype=torch.int64, device=dev) if want_stamps else None
+    # the reduce-scatter BPTT (csrc/lstm2_bwd_rs.hip): its fp32 partial ring, T + 1 ticks
+    rs = rs and not drop and bool(ops.lstm2_bwd_rs_ok(H, B))
+    prs = torch.empty(int(ops.lstm2_bwd_rs_ring_floats(H, B)), device=dev) if rs else None
 
     def bwd(diag=None):
         cnt.zero_()
         ops.lstm2_persist_bwd(Wh0, Wh1, Wx1, dtop, g0, cb0, g1, cb1, dz0, dz1, zr0, zr1, db0, db1,
-                              cnt[0], cnt[1], err, 1 << 22, G, diag)
+                              cnt[0], cnt[1], err, 1 << 22, G, diag, xm, 1.25 if drop else 1.0,
+                              prs)
 
     out = {"B": B, "G": G, "grid": (H // 16) * (nbg // G)}
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     fticks = T + 2 if G == 1 else T + 1  # forward lag: 2 ticks at G = 1, else 1
-    for name, fn, ticks in (("fwd", fwd, fticks), ("bwd", bwd, T + 2)):
+    bticks = T + 1 if rs else T + 2
+    out["rs"] = rs
+    for name, fn, ticks in (("fwd", fwd, fticks), ("bwd", bwd, bticks)):
         for _ in range(2):
             fn()
         torch.cuda.synchronize()
@@ -156,14 +205,20 @@ def run(ops, H, T, B, G, want_stamps, reps=5, want_skew=False, drop=False, gathe
         torch.cuda.synchronize()
         out[name] = e0.elapsed_time(e1) * 1e3 / reps / ticks
     out["err"] = int(err.item())
-    out["cps"] = B * T / ((out["fwd"] * fticks + out["bwd"] * (T + 2)) * 1e-6)
+    out["cps"] = B * T / ((out["fwd"] * fticks + out["bwd"] * bticks) * 1e-6)
     if want_stamps:
         fwd(dfw)
         bwd(dbw)
         torch.cuda.synchronize()
         out["stamps_fwd"] = stamps(dfw, fticks, G, False)
-        out["stamps_bwd"] = stamps(dbw, T + 2, G, True)
-    if want_skew and G == 1 and ops.lstm2_bwd_wide_ok(H, B):
+        out["stamps_bwd"] = rs_stamps(dbw, bticks) if rs else stamps(dbw, T + 2, G, True)
+    if want_skew and rs:
+        grid = 8 * (H // 32) * -(-((B + 15) // 16) // 8)  # the XCD-padded grid (xcd_grid)
+        dall = torch.zeros(grid, T + 2, 8, dtype=torch.int64, device=dev)
+        bwd(dall)
+        torch.cuda.synchronize()
+        out["skew_rs"] = rs_skew(dall, H, B, T)
+    if want_skew and G == 1 and ops.lstm2_bwd_wide_ok(H, B) and not rs:
         grid = (H // 32) * ((B + 15) // 16)
         dall = torch.zeros(grid, T + 2, 8, dtype=torch.int64, device=dev)
         bwd(dall)
@@ -183,24 +238,33 @@ def main():
     ap.add_argument("--gather", action="store_true", help="layer 0 rows gathered from a table")
     ap.add_argument("--xin", action="store_true", help="layer 0 input projected in-kernel")
     ap.add_argument("--skew", action="store_true", help="every workgroup's hand-off timing (wide BPTT)")
+    ap.add_argument("--rs", action="store_true", help="the reduce-scatter BPTT (lstm2_bwd_rs.hip)")
     a = ap.parse_args()
+    if a.rs:  # (the C++ launcher's opt-in switch for the reduce-scatter BPTT)
+        import os
+
+        os.environ["DCR_DEBUG"] = "bwd_rs=1"
     ops = native.ops()
     for B in a.B:
         for G in a.G:
             o = run(ops, a.H, a.T, B, G, a.stamps, want_skew=a.skew, drop=a.drop, gather=a.gather,
-                    xin=a.xin)
+                    xin=a.xin, rs=a.rs)
             if o is None:
                 print(f"H={a.H} B={B} G={G}: no co-resident grid", flush=True)
                 continue
             print(f"H={a.H} T={a.T} B={B:5d} G={o['G']} grid={o['grid']:4d}  fwd {o['fwd']:6.2f} "
                   f"us/tick  bwd {o['bwd']:6.2f} us/tick  (two launches: {o['cps'] / 1e6:6.1f} M "
-                  f"chars/s) err={o['err']}", flush=True)
+                  f"chars/s) err={o['err']} rs={int(o['rs'])}", flush=True)
             for k in ("stamps_fwd", "stamps_bwd"):
                 if k in o:
                     tot, parts = o[k]
                     print(f"   {k}: {tot:.0f} s_memtime ticks per tick (workgroup 0)")
                     for n, v in parts:
                         print(f"     {n:<40}{v:8.0f}  {100 * v / tot:5.1f}%")
+            if "skew_rs" in o:
+                print("   skew_rs (every workgroup, s_memrealtime, us; median, max over workgroups):")
+                for n, v, mx in o["skew_rs"]:
+                    print(f"     {n:<46}{v:7.2f} {mx:7.2f}")
             if "skew_bwd" in o:
                 rows, by_xcd = o["skew_bwd"]
                 print("   skew_bwd (every workgroup, s_memrealtime, us, mean over steady ticks):")

@@ -21,10 +21,10 @@ def rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
 
 
-def _run(cfg, B, T, wide, monkeypatch, steps=2, pf=None):
+def _run(cfg, B, T, wide, monkeypatch, steps=2, pf=None, rs=False):
     monkeypatch.setenv("DCR_SPIN_LIMIT", str(1 << 20))
     monkeypatch.setenv("DCR_DEBUG", "persist_min_t=1" + ("" if wide else ",wide=0") +
-                       (f",wide_pf={pf}" if pf is not None else ""))
+                       (f",wide_pf={pf}" if pf is not None else "") + (",bwd_rs=1" if rs else ""))
     m = CharRNN(cfg, device="cuda", seed=21)
     plan = m.backend._persist_plan(B, True, T)
     assert plan.pair_bwd and plan.pair_g == 1, plan
@@ -62,11 +62,13 @@ def test_wide_bptt_equals_narrow(B, T, H, drop, pf, monkeypatch, dcr_ops):
             assert torch.equal(ga, gb), s.name
 
 
-def test_wide_bptt_matches_oracle_headline_shape(monkeypatch, dcr_ops):
-    """H = 512, B = 256 (the headline's 256-workgroup grid) against the fp32 autograd oracle."""
+@pytest.mark.parametrize("rs", [False, True])
+def test_wide_bptt_matches_oracle_headline_shape(rs, monkeypatch, dcr_ops):
+    """H = 512, B = 256 (the headline's 256-workgroup grid) against the fp32 autograd oracle:
+    the all-gather kernel (lstm2_bwd_wide.hip) and the reduce-scatter one (lstm2_bwd_rs.hip)."""
     B, T, H = 256, 16, 512
-    assert dcr_ops.lstm2_bwd_wide_ok(H, B)
-    monkeypatch.setenv("DCR_DEBUG", "persist_min_t=1")
+    assert dcr_ops.lstm2_bwd_wide_ok(H, B) and dcr_ops.lstm2_bwd_rs_ok(H, B)
+    monkeypatch.setenv("DCR_DEBUG", "persist_min_t=1" + (",bwd_rs=1" if rs else ""))
     cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=2)
     nat = CharRNN(cfg, device="cuda", seed=4)
     ref = ReferenceBackend(nat.store)
@@ -91,3 +93,21 @@ def test_wide_plan_limits(dcr_ops):
     for H, B in ((512, 256), (512, 1), (256, 512), (128, 1024)):
         assert dcr_ops.lstm2_bwd_wide_ok(H, B) == ((H // 32) * ((B + 15) // 16) <= cus), (H, B)
     assert not dcr_ops.lstm2_bwd_wide_ok(1024, 64)
+
+
+@pytest.mark.parametrize("B,T,H", [(256, 8, 512), (50, 7, 128), (37, 6, 512), (100, 12, 256),
+                                   (256, 130, 512), (16, 2, 512), (40, 1, 256)])
+def test_rs_bptt_matches_all_gather(B, T, H, monkeypatch, dcr_ops):
+    """The reduce-scatter BPTT (csrc/lstm2_bwd_rs.hip, opt-in) against the all-gather one over two steps
+    (TBPTT carry, ragged batches, T = 1 and 2, the XCD-local form from T = 8): the same products
+    summed in another order, so a few ulp apart -- a wrong slice, slot or tick would be O(1)."""
+    assert dcr_ops.lstm2_bwd_rs_ok(H, B)
+    cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=2)
+    a, la, sa = _run(cfg, B, T, True, monkeypatch, rs=True)
+    assert a.backend._bufs[(B, T, True)]["prs"] is not None
+    b, lb, sb = _run(cfg, B, T, True, monkeypatch, rs=False)
+    assert abs(la - lb) < 1e-4 * max(1.0, abs(lb))
+    for u, v in zip(sa, sb):
+        assert rel(u, v) < 2e-3
+    for s in a.store.specs:
+        assert rel(a.store.gview(s.name), b.store.gview(s.name)) < 5e-3, s.name
