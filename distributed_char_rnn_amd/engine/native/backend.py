@@ -21,6 +21,7 @@ backward, libstep (large-H library path), inference (logits, eval, sampling).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -37,6 +38,45 @@ from .plan import Knobs
 
 CELL_ID = {"lstm": 0, "gru": 1, "rnn": 3, "nas": 4}
 
+# launches whose grid must be co-resident on the whole chip (hand-offs between workgroups)
+PERSISTENT_OPS = ("lstm2_persist_fwd", "lstm2_persist_bwd", "lstm_persist_fwd",
+                  "lstm_persist_bwd", "gru_persist_fwd", "gru_persist_bwd", "generate")
+
+
+class SharedGpuOps:
+    """``DCR_GPU_SHARE=<lock file>``: several processes (data-parallel ranks) share one GPU and
+    still run the persistent kernels.  Two co-residency-dependent grids of different processes
+    must never overlap (each would wait on workgroups the other keeps off the chip), so every
+    persistent launch takes an inter-process file lock, runs, and is synchronised before the
+    lock is released; everything else runs concurrently (a persistent grid beside another
+    process's ordinary kernels only waits for their CUs).  The step's tail launches then use
+    the atomic tile queue (layouts.tail_dynamic).  For multi-process tests on one GPU
+    (tests/test_gpu_dp2.py): one rank per GPU needs none of this."""
+
+    def __init__(self, ops, path: str):
+        self._ops = ops
+        self._path = path
+        self._fd = None
+
+    def __getattr__(self, name):
+        fn = getattr(self._ops, name)
+        if name not in PERSISTENT_OPS:
+            return fn
+
+        def locked(*args, **kwargs):
+            import fcntl
+
+            if self._fd is None:
+                self._fd = open(self._path, "a+")
+            fcntl.flock(self._fd, fcntl.LOCK_EX)
+            try:
+                out = fn(*args, **kwargs)
+                torch.cuda.synchronize()
+                return out
+            finally:
+                fcntl.flock(self._fd, fcntl.LOCK_UN)
+        return locked
+
 
 class NativeBackend(LayoutsMixin, BuffersMixin, ForwardMixin, BackwardMixin, LibStepMixin,
                     InferenceMixin):
@@ -45,6 +85,10 @@ class NativeBackend(LayoutsMixin, BuffersMixin, ForwardMixin, BackwardMixin, Lib
         if dtype not in ("auto", "bf16"):
             raise ValueError("the native GPU path computes in bf16 (use --dtype bf16/auto)")
         self.ops = native.ops()
+        share = os.environ.get("DCR_GPU_SHARE")
+        self.gpu_shared = bool(share)
+        if share:
+            self.ops = SharedGpuOps(self.ops, share)
         self.store = store
         self.cfg = store.cfg
         self.dev = store.device

@@ -46,8 +46,9 @@ class LayoutsMixin:
     def tail_dynamic(self) -> bool:
         """Tail launches hand out tiles through an atomic queue unless the GPU is this
         process's alone (the persistent recurrence's assumption): then static tiles, with no
-        queue traffic (DCR_DEBUG=tail_queue=1 forces the queue)."""
-        return not self.knobs.persistent or self.knobs.dbg("tail_queue", "0") == "1"
+        queue traffic (DCR_DEBUG=tail_queue=1 forces the queue; DCR_GPU_SHARE shares the GPU)."""
+        return (not self.knobs.persistent or getattr(self, "gpu_shared", False)
+                or self.knobs.dbg("tail_queue", "0") == "1")
 
     def bind_optimizer(self, opt) -> None:
         if self.tail_adam_ok() and opt.mirror is None and opt.native:

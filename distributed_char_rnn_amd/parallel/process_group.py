@@ -166,7 +166,10 @@ def pick_device(topo: Topology, requested: str = "auto", log=print) -> torch.dev
             # more local ranks than GPUs: ranks share a device.  The persistent recurrent
             # kernels need every CU of the chip (one workgroup per CU, co-resident grids), so two
             # processes' grids on one GPU spin into the timeout: use the per-step kernels.
-            if os.environ.get("DCR_RECURRENCE", "auto") in ("auto", "single"):
+            # (DCR_GPU_SHARE keeps them: persistent launches serialised across processes by a
+            # file lock, engine/native/backend.py SharedGpuOps -- a test mode)
+            if (os.environ.get("DCR_RECURRENCE", "auto") in ("auto", "single")
+                    and not os.environ.get("DCR_GPU_SHARE")):
                 log(f"[rank {topo.rank}] {local_world} local ranks share {n} GPU(s): persistent "
                     "kernels disabled (DCR_RECURRENCE=step); run one rank per GPU for speed")
                 os.environ["DCR_RECURRENCE"] = "step"

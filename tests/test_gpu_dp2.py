@@ -1,6 +1,7 @@
 """The native GPU data-parallel path across processes: 2 ranks on cuda:0 (gloo: RCCL refuses
 two ranks on one device; DCR_RECURRENCE=step: no persistent grids, which must not share CUs
-with another process), replicated and sharded (ZeRO-1) steps with clipping active, the TF
+with another process -- or DCR_GPU_SHARE: the headline shape on the persistent kernels, their
+launches serialised across the processes), replicated and sharded (ZeRO-1) steps with clipping active, the TF
 per-token norm slot and the fused step tail, against ONE process on the 2x batch; and a forced
 error word on one rank makes every rank skip the update and raise on the same step.
 
@@ -19,6 +20,11 @@ pytestmark = pytest.mark.gpu
 CFG = dict(model="lstm", vocab_size=65, rnn_size=128, num_layers=2)
 CLIP = 0.01
 B, T, STEPS = 16, 16, 3
+# the headline's model shape on the persistent kernels (two-layer wavefront forward, wide BPTT,
+# exclusive-mode bucket release, per-bucket wgrad / FINALIZE launches): DCR_GPU_SHARE serialises
+# the two processes' persistent launches with a file lock (engine/native/backend.py)
+CFG_HL = dict(model="lstm", vocab_size=65, rnn_size=512, num_layers=2)
+B_HL = 64
 
 
 def _port():
@@ -34,20 +40,27 @@ def _data(rows):
     return rng.integers(0, 65, size=(STEPS, rows, T + 1)).astype(np.int32)
 
 
-def _model():
+def _model(cfg=None):
     from distributed_char_rnn_amd.engine.optim import TFAdam
     from distributed_char_rnn_amd.models.char_rnn import CharRNN
     from distributed_char_rnn_amd.models.params import ModelConfig
 
-    m = CharRNN(ModelConfig(**CFG), device="cuda:0", seed=4)
+    m = CharRNN(ModelConfig(**(cfg or CFG)), device="cuda:0", seed=4)
     opt = TFAdam(m.store, clip=CLIP, guard=m.error_word())
     m.bind_optimizer(opt)
     return m, opt
 
 
-def _worker(rank, world, port, mode, fault_step, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DCR_RECURRENCE="step",
-                      HSA_ENABLE_IPC_MODE_LEGACY="0")
+def _worker(rank, world, port, mode, fault_step, q, share=None):
+    env = dict(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    if share:
+        env["DCR_GPU_SHARE"] = share
+    else:
+        env["DCR_RECURRENCE"] = "step"
+    os.environ.update(env)
+    global B, CFG
+    if share:
+        B, CFG = B_HL, CFG_HL
     import torch.distributed as dist
 
     from distributed_char_rnn_amd.parallel.grad_sync import GradSync
@@ -65,6 +78,9 @@ def _worker(rank, world, port, mode, fault_step, q):
         else:
             sync = ShardedStep(m.store, opt, world, rank, wire="fp32", bucket_mb=0.05, guard=guard)
         m.backend.defer_err_poll = True
+        if share:  # the persistent wavefront kernels ran (not the per-step fallback)
+            P = m.backend._persist_plan(B, True, T)
+            assert P.pair and P.pair_bwd and P.persistent, P
         data = _data(B * world)
         st = m.zero_state(B)
         snaps, norms, raised = [], [], []
@@ -90,11 +106,12 @@ def _worker(rank, world, port, mode, fault_step, q):
         dist.destroy_process_group()
 
 
-def _run(mode, fault_step=-1, world=2):
+def _run(mode, fault_step=-1, world=2, share=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, mode, fault_step, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, mode, fault_step, q, share))
+          for r in range(world)]
     for p in ps:
         p.start()
     out = [q.get(timeout=300) for _ in ps]
@@ -104,12 +121,14 @@ def _run(mode, fault_step=-1, world=2):
     return sorted(out, key=lambda o: o[0])
 
 
-def _single(world=2):
-    os.environ["DCR_RECURRENCE"] = "step"
+def _single(world=2, persistent=False):
+    b = B_HL if persistent else B
+    if not persistent:
+        os.environ["DCR_RECURRENCE"] = "step"
     try:
-        m, opt = _model()
-        data = _data(B * world)
-        st = m.zero_state(B * world)
+        m, opt = _model(CFG_HL if persistent else None)
+        data = _data(b * world)
+        st = m.zero_state(b * world)
         snaps, norms = [], []
         for s in range(STEPS):
             blk = torch.from_numpy(data[s]).cuda()
@@ -118,7 +137,7 @@ def _single(world=2):
             snaps.append(m.store.flat.cpu().numpy().copy())
         return snaps, norms
     finally:
-        del os.environ["DCR_RECURRENCE"]
+        os.environ.pop("DCR_RECURRENCE", None)
 
 
 @pytest.mark.parametrize("mode", ["replicated", "sharded"])
@@ -141,3 +160,20 @@ def test_error_word_on_one_rank_stops_every_rank(mode):
         assert raised == [False, True, False], (rank, raised)
         np.testing.assert_array_equal(snaps[1], snaps[0])  # the faulted step was skipped
         np.testing.assert_array_equal(snaps[-1], out[0][1][-1])
+
+
+@pytest.mark.parametrize("mode", ["replicated", "sharded"])
+def test_two_ranks_headline_shape_persistent(mode, tmp_path):
+    """The code the benchmark runs, across two processes: H = 512, L = 2 on the persistent
+    two-layer wavefront kernels, exclusive-mode bucket release after the BPTT launch, the
+    per-bucket weight-gradient / FINALIZE flushes, the TF norm slot and the error-word guard
+    riding the last bucket -- against ONE process on the 2x batch (also persistent)."""
+    ref, ref_norms = _single(persistent=True)
+    assert all(n > CLIP for n in ref_norms), ("clipping must be active", ref_norms)
+    out = _run(mode, share=str(tmp_path / "gpu.lock"))
+    for rank, snaps, norms, raised in out:
+        assert not any(raised)
+        np.testing.assert_allclose(norms, ref_norms, rtol=3e-3)
+        d = np.abs(snaps[-1] - ref[-1]).max() / np.abs(ref[-1]).max()
+        assert d < 3e-3, d
+        np.testing.assert_array_equal(snaps[-1], out[0][1][-1])  # replicas identical
