@@ -295,7 +295,13 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
     # --graph: the whole step (fwd, head, BPTT, weight grads, clip + Adam) as one replayed
     # hipGraph; summary steps that want the logits run eagerly
     graphed = None
-    if getattr(args, "graph", "off") != "off":
+    gmode = getattr(args, "graph", "off")
+    if gmode == "auto" and args.batch_size * args.seq_length * args.rnn_size > GRAPH_AUTO_MAX_WORK:
+        # a step this large is not launch-bound: the replay's input / state / loss copies cost
+        # more than the launches they save (headline shape, same box: eager 1.394-1.412 vs
+        # graph 1.454-1.456 ms per train.py step; bench.py 1.390-1.396 vs --graph 1.425-1.436)
+        gmode = "off"
+    if gmode != "off":
         ok, why = GraphedStep.supported(model, ctx.world_size)
         if ok:
             graphed = GraphedStep(model, opt, log=lambda m: _log(m, rank))
@@ -390,6 +396,9 @@ def _train(args, ctx, device, rank: int, chief: bool) -> int:
 
 
 DEVICE_BATCHES_MAX_BYTES = 4 << 30
+# --graph auto replays captured steps only below this B·T·H (launch-bound shapes, e.g. the
+# reference default B = 50, T = 50, H = 128)
+GRAPH_AUTO_MAX_WORK = 1 << 21
 
 
 def _device_batches(loader, nb: int, device: torch.device):

@@ -61,8 +61,9 @@ def train_parser() -> argparse.ArgumentParser:
                    help="execution device (auto = GPU when available)")
     g.add_argument("--dtype", default="auto", choices=["auto", "bf16", "fp32"],
                    help="compute dtype (auto = bf16 on GPU, fp32 on CPU).  The native HIP kernels "
-                        "compute in bf16 (fp32 state and accumulation); fp32 on a GPU runs the "
-                        "PyTorch autograd path (hipBLASLt fp32 GEMMs) and says so at start-up")
+                        "compute with bf16 MFMA operands (fp32 state and accumulation); fp32 on a "
+                        "GPU runs every LSTM / GRU / RNN cell step on the fp32-operand kernels "
+                        "(csrc/cell_f32.hip, a numerics mode; NAS: the autograd path)")
     g.add_argument("--seed", type=int, default=0, help="parameter-init / dropout seed")
     g.add_argument("--log_every", type=int, default=1, help="print a progress line every N steps")
     g.add_argument("--summary_every", type=int, default=100,
@@ -97,7 +98,8 @@ def train_parser() -> argparse.ArgumentParser:
     g.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                    help="replay the whole GPU training step (forward, BPTT, weight gradients, "
                         "clip + Adam) as one captured HIP graph (engine/graph_step.py); auto = "
-                        "on wherever it applies (one rank, native backend, no dropout)")
+                        "on wherever it applies (one rank, native backend, no dropout) for "
+                        "launch-bound steps (B·T·rnn_size <= 2^21)")
     return p
 
 
