@@ -68,6 +68,48 @@ def _torch_flags():
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
           "-ffp-contract=fast"]
+# per-kernel register / scratch report of every device compile (parsed into _C.resources.json)
+DEV_FLAGS = ["-Rpass-analysis=kernel-resource-usage"]
+RESOURCES = os.path.join(PKG_DIR, "_C.resources.json")
+# Sources whose kernels spin on each other across workgroups (persistent hand-offs, in-launch
+# waits).  None of their kernels may spill to scratch: at the register limit this compiler has
+# reloaded a spilled 128-bit MFMA fragment without one of its dwords (round 6, docs/STATUS.md:
+# the wide BPTT's steady tick body with wide_pf=0 computed NaN gradients), and a wrong value
+# in a hand-off index is a spin timeout, not a wrong number.  The build fails instead (except
+# for KNOWN_SPILLS).
+NO_SPILL_SOURCES = ("lstm2_persist.hip", "lstm2_bwd_wide.hip", "lstm2_bwd_rs.hip",
+                    "lstm_persist.hip", "lstm_persist_nt.hip", "gru_persist.hip",
+                    "generate.hip", "tail.hip")
+# instantiations that spilled before the guard existed (all covered by the GPU oracle tests;
+# none is on the headline path): the two-layer forward at H = 128 with 2-4 row groups per
+# workgroup (lstm2_persist.hip G >= 2), the single-layer forward with the fused input rows at
+# H = 192 / 256 (lstm_persist.hip XF), and the stamped (DIAG) NT forward instantiations.
+KNOWN_SPILLS = frozenset({
+    "_ZN3dcr24lstm2_fwd_persist_kernelILi4ELi2ELb1ELb0ELb0EEEvNS_9Lstm2ArgsE",
+    "_ZN3dcr24lstm2_fwd_persist_kernelILi4ELi3ELb1ELb0ELb0EEEvNS_9Lstm2ArgsE",
+    "_ZN3dcr24lstm2_fwd_persist_kernelILi4ELi4ELb1ELb0ELb0EEEvNS_9Lstm2ArgsE",
+    "_ZN3dcr24lstm2_fwd_persist_kernelILi4ELi2ELb0ELb0ELb0EEEvNS_9Lstm2ArgsE",
+    "_ZN3dcr23lstm_fwd_persist_kernelILi6ELi2ELb0ELb1EEEvNS_11PersistArgsE",
+    "_ZN3dcr23lstm_fwd_persist_kernelILi8ELi2ELb0ELb1EEEvNS_11PersistArgsE",
+    "_ZN3dcr26lstm_fwd_persist_nt_kernelILi16ELi2ELb1ELb0EEEvNS_11PersistArgsE",
+    "_ZN3dcr26lstm_fwd_persist_nt_kernelILi16ELi4ELb1ELb0EEEvNS_11PersistArgsE",
+})
+
+
+def parse_resource_remarks(text: str) -> dict:
+    """``-Rpass-analysis=kernel-resource-usage`` output -> {kernel: {field: int}}."""
+    import re
+
+    out, cur = {}, None
+    for line in text.splitlines():
+        m = re.search(r"remark: Function Name: (\S+)", line)
+        if m:
+            cur = out.setdefault(m.group(1), {})
+            continue
+        m = re.search(r"remark:\s+([A-Za-z ]+?)(?: \[[^\]]*\])?: (\d+) \[-Rpass", line)
+        if m and cur is not None:
+            cur[m.group(1).strip()] = int(m.group(2))
+    return out
 
 
 def source_hash() -> str:
@@ -75,7 +117,7 @@ def source_hash() -> str:
     import hashlib
 
     h = hashlib.sha256()
-    h.update(" ".join(COMMON).encode())
+    h.update(" ".join(COMMON + DEV_FLAGS).encode())
     for f in sorted(glob.glob(os.path.join(CSRC, "*"))):
         if os.path.isfile(f):
             h.update(os.path.basename(f).encode() + b"\0")
@@ -143,10 +185,12 @@ def _build_locked(force: bool, jobs: int | None, verbose: bool) -> str:
 
     def compile_one(src: str):
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
-        if not force and not _stale(obj, src, headers):
+        res = obj + ".res.json"
+        if not force and not _stale(obj, src, headers) and (src.endswith(".cpp") or
+                                                              os.path.exists(res)):
             return obj, None
         if src.endswith(".hip"):
-            cmd = [hipcc, *COMMON, "-I", CSRC, "-c", src, "-o", obj]
+            cmd = [hipcc, *COMMON, *DEV_FLAGS, "-I", CSRC, "-c", src, "-o", obj]
         else:  # torch bindings: host-only C++ (no device code), compiled by the host compiler
             cmd = [_cxx(), "-O2", "-std=c++17", "-fPIC", "-I", CSRC, *cflags, "-c", src, "-o", obj]
         if verbose:
@@ -154,6 +198,12 @@ def _build_locked(force: bool, jobs: int | None, verbose: bool) -> str:
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             return obj, f"{' '.join(cmd)}\n{r.stdout}\n{r.stderr}"
+        if src.endswith(".hip"):
+            import json
+
+            with open(res, "w") as fh:
+                json.dump({"source": os.path.basename(src),
+                           "kernels": parse_resource_remarks(r.stderr)}, fh)
         return obj, None
 
     with ThreadPoolExecutor(jobs) as ex:
@@ -162,6 +212,7 @@ def _build_locked(force: bool, jobs: int | None, verbose: bool) -> str:
     if errs:
         raise RuntimeError("native build failed:\n" + "\n\n".join(errs))
     objs = [o for o, _ in results]
+    _check_resources(dev_srcs)
     if force or not os.path.exists(OUT) or any(os.path.getmtime(o) > os.path.getmtime(OUT)
                                                for o in objs):
         tmp = f"{OUT}.tmp{os.getpid()}"
@@ -177,6 +228,28 @@ def _build_locked(force: bool, jobs: int | None, verbose: bool) -> str:
         fh.write(want + "\n")
     os.replace(tmp_hash, OUT + ".srchash")
     return OUT
+
+
+def _check_resources(dev_srcs) -> None:
+    """Collect the per-kernel reports into _C.resources.json; fail on a spilling kernel of a
+    NO_SPILL_SOURCES file."""
+    import json
+
+    table, bad = {}, []
+    for src in dev_srcs:
+        with open(os.path.join(BUILD, os.path.basename(src) + ".o.res.json")) as fh:
+            rep = json.load(fh)
+        table[rep["source"]] = rep["kernels"]
+        if rep["source"] in NO_SPILL_SOURCES:
+            for k, v in rep["kernels"].items():
+                if (v.get("ScratchSize", 0) or v.get("VGPRs Spill", 0)) and k not in KNOWN_SPILLS:
+                    bad.append(f"{rep['source']}: {k} scratch {v.get('ScratchSize')} B/lane, "
+                               f"{v.get('VGPRs Spill')} VGPRs spilled")
+    with open(RESOURCES, "w") as fh:
+        json.dump(table, fh, indent=0, sort_keys=True)
+    if bad:
+        raise RuntimeError("persistent kernels must not spill (see _build.NO_SPILL_SOURCES):\n"
+                           + "\n".join(bad))
 
 
 def main(argv=None):
