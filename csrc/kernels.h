@@ -338,7 +338,6 @@ struct Lstm2BwdArgs {
   int diag_all;         // diag holds [grid, T+2, 8] s_memrealtime stamps of every workgroup
   int xcdloc;           // as Lstm2Args::xcdloc (exchange word: dwords 2-3 of cnt0's slot 0)
   float* pring;         // optional reduce-scatter partial ring (lstm2_bwd_rs.hip), fp32
-  int steady;           // wide BPTT: ticks 3 .. T-1 on the steady-state (constant-condition) body
 };
 int launch_lstm2_bwd_persist(const Lstm2BwdArgs& a, int cus, hipStream_t s);
 // the reduce-scatter form of the 32 x 16 BPTT (lstm2_bwd_rs.hip): no dropout, H in {128, 256,

@@ -118,7 +118,6 @@ __device__ __forceinline__ float row_reduce_scatter16(float (&v)[16], int lane) 
 //      and tick -- is still arriving.  After the arrival it delayed the next tick's poll (the
 //      stamps: ~1.35 us from the arrival to the next tick start, the poll then ~0.4 us, i.e. the
 //      hand-off had long landed).
-constexpr int kWidePfDefaultK = 6;  // the default operand order (kWidePfDefault below)
 template <int KS, bool DROP, int PFA, bool DIAG>
 __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) {
   static_assert(KS % 4 == 0, "K quarter = whole 32-wide k-steps per gate");
@@ -228,13 +227,9 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
   const unsigned vc = opaque_vgpr((unsigned)(bh * sizeof(float)));
   const unsigned vm = (unsigned)(b * (H / 8) + (ub0 >> 3));
   const __amdgpu_buffer_rsrc_t rdL = make_rsrc(a.dtop1, L ? sizeof(float) * (size_t)T * B * H : 0);
-  using sdy_t = std::integral_constant<bool, true>;
-  using edge_t = std::integral_constant<bool, false>;
-  // (sdy_c: a steady tick -- 3 <= tk <= T - 1 -- where every edge condition is true)
-  auto prefetch_u = [&](int tk, auto sdy_c) {  // PF = 5: unconditional, out-of-range lanes read zero
-    constexpr bool SDY = decltype(sdy_c)::value;
+  auto prefetch_u = [&](int tk) {  // PF = 5: unconditional, out-of-range lanes read zero
     const int tt = L ? T - 1 - tk : T + 1 - tk;
-    const bool ac = SDY || (L ? tk < T : tk >= 2);
+    const bool ac = L ? tk < T : tk >= 2;
     // (offsets through an opaque move: LLVM turns a select against an out-of-range offset into
     // a branch around the load, and the waitcnt pass then drains everything at the next write
     // of the destination registers)
@@ -257,15 +252,15 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
       dtop[r] = d[r];
     }
     if (DROP) {
-      const bool md = (SDY || (tk >= 2 && tk <= T + 1)) && live;
+      const bool md = tk >= 2 && tk <= T + 1 && live;
       mrow = __builtin_amdgcn_raw_buffer_load_b32(
           rm, opaque_vgpr(md ? vm : kOut), md ? (unsigned)((size_t)(T + 1 - tk) * B * (H / 8)) : 0u,
           0);
     }
   };
-  auto prefetch = [&](int tk, auto sdy_c) {
+  auto prefetch = [&](int tk) {
     if constexpr (PF == 5 || ES) {
-      prefetch_u(tk, sdy_c);
+      prefetch_u(tk);
       return;
     }
     const int tt = L ? T - 1 - tk : T + 1 - tk;
@@ -303,25 +298,22 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
       mrow = __builtin_amdgcn_raw_buffer_load_b32(rm, vm, (unsigned)((size_t)(T + 1 - tk) * B * (H / 8)), 0);
   };
 
-  // one tick; SDY (steady): 3 <= tau <= T - 1, where every edge condition below is a
-  // compile-time constant (both layers active and loading, no first or last step)
-  auto tick = [&](int tau, auto sdy_c) __attribute__((always_inline)) {
-    constexpr bool SDY = decltype(sdy_c)::value;
-    const bool on1 = SDY || tau < T;                   // layer l+1 computes step T-1-tau
-    const bool on0 = SDY || tau >= 2;                  // layer l computes step T+1-tau (two ticks behind)
-    const bool ld1 = SDY || (tau >= 1 && tau <= T);    // dZ_{l+1}[T-tau] (published at tick tau-1)
-    const bool ld0 = SDY || tau >= 3;                  // dZ_l[T+2-tau]   (published at tick tau-1)
+  for (int tau = 0; tau <= T + 1; ++tau) {
+    const bool on1 = tau < T;                 // layer l+1 computes step T-1-tau
+    const bool on0 = tau >= 2;                // layer l computes step T+1-tau (two ticks behind)
+    const bool ld1 = tau >= 1 && tau <= T;    // dZ_{l+1}[T-tau] (published at tick tau-1)
+    const bool ld0 = tau >= 3;                // dZ_l[T+2-tau]   (published at tick tau-1)
     const int t = L ? T - 1 - tau : T + 1 - tau;  // this role's step
     const bool act = L ? on1 : on0;
     STAMPW(0)
-    if (PF == 0 || (!SDY && (((PF == 1 || PF == 5) && tau == 0) ||
-                             ((PF >= 2 && PF <= 4) && tau == 0 && !(PF == 4 && w == 0)))))
-      prefetch(tau, sdy_c);
+    if (PF == 0 || ((PF == 1 || PF == 5) && tau == 0) ||
+        ((PF >= 2 && PF <= 4) && tau == 0 && !(PF == 4 && w == 0)))
+      prefetch(tau);
     const int s1 = T - tau, s0 = T + 2 - tau;  // ring slots of dZ_{l+1} and dZ_l
-    if ((SDY || tau >= 1) && loc) {  // flags of both layers' producing tick (tau - 1) + 1
+    if (tau >= 1 && loc) {  // flags of both layers' producing tick (tau - 1) + 1
       if (w == 0 && !dead && (ld1 || ld0))
         dead = !poll_flags2(fl0, ld0, fl1, ld1, H / 32, (unsigned)tau, a.spin_limit, a.err, 10u);
-    } else if (SDY || tau >= 1) {
+    } else if (tau >= 1) {
       if (threadIdx.x == kLstmPollerThread && !dead && (ld1 || ld0)) {
         dead = (ld1 && ld0)
                    ? !poll_counter2(cnt1 + (size_t)s1 * 4, target, cnt0 + (size_t)s0 * 4, target,
@@ -335,7 +327,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
     __syncthreads();
     STAMPW(2)
     bf16x8 p1[KS], p0[KS];
-    if (SDY || tau >= 1) {
+    if (tau >= 1) {
       const unsigned o1 = (unsigned)((s1 & 1) * slabn * sizeof(bf16));
       const unsigned o0 = (unsigned)((s0 & 1) * slabn * sizeof(bf16));
       if constexpr (PF == 5 || ES) {  // unconditional: a skipped layer reads an empty descriptor
@@ -359,7 +351,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
             p0[s] = ld8_sc1(rz0, frag_load_off(col, kcol(s) >> 5, G4H, lane) + o0);
         }
       }
-      if (PF == 1 || PF == 5 || (PF == 3 && w == 0)) prefetch(tau, sdy_c);
+      if (PF == 1 || PF == 5 || (PF == 3 && w == 0)) prefetch(tau);
       if constexpr (PF == 5) flush_dz();  // last tick's dZ rows, behind this tick's loads
       __builtin_amdgcn_sched_barrier(0);
       f32x4 xsn[2];  // (ES) layer l's dtop partial for its next tick
@@ -516,7 +508,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
       if (DIAG && a.diag && !a.diag_all && blockIdx.x == 0 && threadIdx.x == 0)
         a.diag[(size_t)tau * 8 + 5] = __builtin_amdgcn_s_memtime();
       // layer l+1's dZ_t feeds both layers at the next tick (t >= 0); layer l's only itself
-      if (SDY || L || t >= 1) {
+      if (L || t >= 1) {
         bf16* const zr = zrL + (size_t)(t & 1) * slabn;
         st4bf_ho(loc, zr + frag_index(b, u0, G4H), di[0], di[1], di[2], di[3]);
         st4bf_ho(loc, zr + frag_index(b, H + u0, G4H), dj[0], dj[1], dj[2], dj[3]);
@@ -569,7 +561,7 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
       for (int i = 0; i < 16; ++i) dcur[i] = (float)f2bf(dcur[i]);
       dbacc += row_reduce_scatter16(dcur, lane);
     }
-    if ((PF == 2 || ((PF == 3 || PF == 4) && w != 0)) && tau < T + 1) prefetch(tau + 1, edge_t{});
+    if ((PF == 2 || ((PF == 3 || PF == 4) && w != 0)) && tau < T + 1) prefetch(tau + 1);
     if constexpr (PF == 4) if (w == 1 && tau + 1 >= 2 && tau + 1 <= T + 1) {
       // wave 0's (layer l, unit half 0) operands of the next tick into opb[(tau + 1) & 1]
       const int tt = T - tau;  // = T + 1 - (tau + 1)
@@ -604,27 +596,8 @@ __global__ void __launch_bounds__(256, 1) lstm2_bwd_wide_kernel(Lstm2BwdArgs a) 
 #pragma unroll
       for (int gt = 0; gt < 4; ++gt) *reinterpret_cast<u32x2*>(dz + gt * H) = offl[tk & 1][gt][lane];
     };
-    if (OFFL && w == 2 && (SDY || tau >= 3) && live) store_offl(tau - 1);
+    if (OFFL && w == 2 && tau >= 3 && live) store_offl(tau - 1);
     STAMPW(7)
-  };
-  if constexpr (!DROP && PFA == kWidePfDefaultK) {
-    // one loop, two inlined bodies
-    const int sdy_lo = 3, sdy_hi = a.steady ? T - 1 : -1;  // (steady range)
-    for (int tau = 0; tau <= T + 1; ++tau) {
-      if (tau >= sdy_lo && tau <= sdy_hi)
-        tick(tau, sdy_t{});
-      else
-        tick(tau, edge_t{});
-    }
-  } else {
-    // generic ticks only: the dropout and non-default operand orders run at the register limit,
-    // and a second tick body pushes them into VGPR spills -- whose reloads this compiler has been
-    // seen to get wrong (docs/STATUS.md, round 6: a 128-bit W fragment reloaded without one of
-    // its dwords).  (Two loops over the one body: the dropout instantiation allocated without
-    // spills this way, not as one loop.)
-    int tau = 0;
-    for (; tau <= T + 1 && tau < 3; ++tau) tick(tau, edge_t{});
-    for (; tau <= T + 1; ++tau) tick(tau, edge_t{});
   }
   if constexpr (PF == 5) flush_dz();
   if constexpr (OFFL) {  // wave 0's last copy (tick T + 1, step 0)
@@ -657,7 +630,7 @@ static const void* lstm2_bwd_wide_pick_t(int H) {
   }
   return nullptr;
 }
-constexpr int kWidePfDefault = kWidePfDefaultK;  // headline 1.534 vs 1.558 ms, dropout 1.893 vs 1.963 (same box)
+constexpr int kWidePfDefault = 6;  // headline 1.534 vs 1.558 ms, dropout 1.893 vs 1.963 (same box)
 // diag: the stamped instantiation (the default operand order, no dropout)
 template <bool DROP>
 static const void* lstm2_bwd_wide_pick(int H, bool diag = false) {

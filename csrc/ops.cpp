@@ -1183,7 +1183,6 @@ void lstm2_persist_bwd(const at::Tensor& Wh0, const at::Tensor& Wh1, const at::T
   a.spin_limit = (unsigned)spin_limit;
   a.wgarr = dcr::debug_int("wgarr", 1);  // one hand-off add per workgroup and layer
   a.xcdloc = dcr::debug_int("xcdloc", 1);  // XCD-resident hand-offs where placement allows
-  a.steady = dcr::debug_int("bwd_steady", 1);  // wide BPTT: constant-condition steady ticks
   if (has(diag)) {
     TORCH_CHECK(diag->element_size() == 8 && diag->numel() >= (int64_t)(T + 2) * G * 8,
                 "diag must hold [T+2, G, 8] int64 (ticks 0..T+1)");

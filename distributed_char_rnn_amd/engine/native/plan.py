@@ -84,8 +84,6 @@ DEBUG_KEYS = {
              "wgrad kernel (csrc/wgrad.hip)",
     "tokennorm": "0: TF token-norm term as a library GEMM to bf16 rows + a sumsq launch instead "
                  "of the fused MFMA kernel (csrc/tokennorm.hip)",
-    "bwd_steady": "0: the wide two-layer BPTT's steady ticks (3 .. T-1) on the generic tick body "
-                  "(run-time edge conditions)",
     "fwd_steady": "0: the two-layer forward's steady ticks on the generic tick body (run-time "
                   "edge conditions) instead of the constant-condition one (C++)",
     "table_nt": "0: wide-vocabulary gather table E·W_x0 + b0 as a library GEMM on bias rows "
