@@ -11,6 +11,17 @@ from .layouts import SEG_LDS_MAX_V
 from .tail import TailQueue
 
 
+
+def bucket_probe(on_ready):
+    """Which gradient-ready reports complete a bucket: ``launches_at(offset)`` of an on_ready
+    object that exposes it, or of the GradSync / ShardedStep a bound ``ready`` belongs to.  None
+    for any other callable: the backward then flushes its deferred sums on every report (safe,
+    one flush per report)."""
+    probe = getattr(on_ready, "launches_at", None)
+    if probe is None:
+        probe = getattr(getattr(on_ready, "__self__", None), "launches_at", None)
+    return probe
+
 class BackwardMixin:
     def train_step(self, x, y, state, on_ready=None, want_extras: bool = False):
         B, T = x.shape
@@ -53,12 +64,7 @@ class BackwardMixin:
         if on_ready is not None:
             cb_user = on_ready
 
-            # which reports complete a bucket: an on_ready object that exposes launches_at()
-            # itself, or the GradSync / ShardedStep a bound ready() belongs to (any other
-            # callable flushes on every report)
-            probe = getattr(cb_user, "launches_at", None)
-            if probe is None:
-                probe = getattr(getattr(cb_user, "__self__", None), "launches_at", None)
+            probe = bucket_probe(cb_user)
 
             def on_ready(off, _cb=cb_user):  # noqa: F811 - sums complete before a bucket leaves
                 if probe is not None and not probe(off):
