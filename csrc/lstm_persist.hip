@@ -434,7 +434,12 @@ enum : int { PF_FUSED = 1, PF_DIAG = 2, PF_EXCL = 4 };
 
 template <int KS, int UB>
 static const void* fwd_fn(int flags) {
-  if (flags & PF_FUSED) return (const void*)lstm_fwd_persist_kernel<KS, UB, false, true>;
+  // (the fused-input form runs only at H <= 512, lstm_persist_xfuse_supported: KS <= 4; at
+  // KS = 6 / 8 its resident W_x and W_h had spilled to scratch, so it is not instantiated)
+  if (flags & PF_FUSED) {
+    if constexpr (KS <= 4) return (const void*)lstm_fwd_persist_kernel<KS, UB, false, true>;
+    return nullptr;
+  }
   if (flags & PF_DIAG) return (const void*)lstm_fwd_persist_kernel<KS, UB, true, false>;
   return (const void*)lstm_fwd_persist_kernel<KS, UB, false, false>;
 }
