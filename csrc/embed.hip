@@ -426,8 +426,12 @@ __device__ __forceinline__ unsigned lds_get16(const unsigned* w, int v) {
   return (w[v >> 1] >> ((v & 1) * 16)) & 0xFFFFu;
 }
 
+// (zero, nz4): an fp32 buffer of nz4 float4s to clear on the side -- the segment sum's atomic
+// output (the embedding gradient), which then needs no separate fill launch
 __global__ void __launch_bounds__(kSortThreads) id_hist_kernel(const int* __restrict__ ids, int N,
-                                                               int V4, int* __restrict__ cnt) {
+                                                               int V4, int* __restrict__ cnt,
+                                                               float4* __restrict__ zero,
+                                                               long nz4) {
   extern __shared__ unsigned hist[];  // [V4 / 2] packed 16-bit counts
   for (int i = threadIdx.x; i < V4 / 2; i += kSortThreads) hist[i] = 0u;
   __syncthreads();
@@ -446,6 +450,12 @@ __global__ void __launch_bounds__(kSortThreads) id_hist_kernel(const int* __rest
   for (int q = threadIdx.x; q < V4 / 4; q += kSortThreads) {
     const unsigned a = hist[2 * q], b = hist[2 * q + 1];
     o[q] = int4{(int)(a & 0xFFFFu), (int)(a >> 16), (int)(b & 0xFFFFu), (int)(b >> 16)};
+  }
+  if (zero) {
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (long i = (long)blockIdx.x * kSortThreads + threadIdx.x; i < nz4;
+         i += (long)gridDim.x * kSortThreads)
+      zero[i] = z;
   }
 }
 
@@ -562,14 +572,17 @@ size_t id_sort_workspace(int N, int V) {
   return (size_t)(id_sort_blocks(N) + 1) * id_sort_cols(V);  // counts + totals
 }
 
-int launch_id_sort(const int* ids, int N, int V, int* ws, int* sid, int* perm, hipStream_t s) {
+int launch_id_sort(const int* ids, int N, int V, int* ws, int* sid, int* perm, hipStream_t s,
+                   float* zero, size_t zero_n) {
   if (N <= 0 || N > 65535 || V <= 0 || V > 16384) return -1;
   const int nblk = id_sort_blocks(N), V4 = id_sort_cols(V);
   int nbits = 0;
   while ((1 << nbits) < V) ++nbits;
   int* const tot = ws + (size_t)nblk * V4;
   const size_t lds = sizeof(unsigned) * (size_t)V4 / 2;
-  id_hist_kernel<<<nblk, kSortThreads, lds, s>>>(ids, N, V4, ws);
+  // (zero: 16-B aligned, a whole number of float4s -- the caller checks)
+  id_hist_kernel<<<nblk, kSortThreads, lds, s>>>(ids, N, V4, ws, reinterpret_cast<float4*>(zero),
+                                                 zero ? (long)(zero_n / 4) : 0L);
   id_colscan_kernel<<<(V4 + kSortThreads - 1) / kSortThreads, kSortThreads, 0, s>>>(V4, nblk, ws, tot);
   const int q = (V4 / 4 + kSortThreads - 1) / kSortThreads;
 #define SCAT(Q) id_scatter_kernel<Q><<<nblk, kSortThreads, lds, s>>>(ids, N, V4, nbits, ws, tot, sid, perm)

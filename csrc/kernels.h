@@ -171,7 +171,9 @@ void launch_embed_dropout(const int* ids, const float* E, const uint8_t* bits, b
 int id_sort_blocks(int N);
 int id_sort_cols(int V);
 size_t id_sort_workspace(int N, int V);
-int launch_id_sort(const int* ids, int N, int V, int* ws, int* sid, int* perm, hipStream_t s);
+// zero (optional): zero_n floats (16-B aligned, zero_n % 4 == 0) cleared by the first launch
+int launch_id_sort(const int* ids, int N, int V, int* ws, int* sid, int* perm, hipStream_t s,
+                   float* zero = nullptr, size_t zero_n = 0);
 int segsum_rows_per_chunk(int N);
 size_t segsum_workspace_floats(int N, int W, int V);
 // perm (atomic route only): ids are sorted and perm[n] is the source row of position n

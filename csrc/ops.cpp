@@ -718,7 +718,10 @@ void segsum(const at::Tensor& X, const c10::optional<at::Tensor>& ids, int64_t V
 }
 
 // stable counting sort of ids (embed.hip): sid = sorted ids, perm = their source positions
-void id_sort(const at::Tensor& ids, int64_t V, at::Tensor& ws, at::Tensor& sid, at::Tensor& perm) {
+// zero (optional): an fp32 buffer the first launch clears on the side (the atomic segment sum's
+// output, so that it needs no fill launch); returns whether it did (alignment / size permitting)
+bool id_sort(const at::Tensor& ids, int64_t V, at::Tensor& ws, at::Tensor& sid, at::Tensor& perm,
+             const c10::optional<at::Tensor>& zero) {
   check_seq(ids, at::kInt, "ids");
   check_seq(ws, at::kInt, "ws");
   check_seq(sid, at::kInt, "sid");
@@ -727,9 +730,20 @@ void id_sort(const at::Tensor& ids, int64_t V, at::Tensor& ws, at::Tensor& sid, 
   TORCH_CHECK(sid.numel() == N && perm.numel() == N, "id_sort: sid and perm must be [N]");
   TORCH_CHECK(V > 0 && (size_t)ws.numel() >= dcr::id_sort_workspace(N, (int)V),
               "id_sort: workspace too small");
+  float* zp = nullptr;
+  size_t zn = 0;
+  if (has(zero)) {
+    TORCH_CHECK(zero->is_cuda() && zero->scalar_type() == at::kFloat && zero->is_contiguous(),
+                "id_sort: zero must be a contiguous fp32 GPU tensor");
+    if (zero->numel() % 4 == 0 && (reinterpret_cast<uintptr_t>(zero->data_ptr()) & 15) == 0) {
+      zp = zero->data_ptr<float>();
+      zn = (size_t)zero->numel();
+    }
+  }
   TORCH_CHECK(dcr::launch_id_sort(ptr<int>(ids), N, (int)V, ptr<int>(ws), ptr<int>(sid),
-                                  ptr<int>(perm), cur_stream()) == 0,
+                                  ptr<int>(perm), cur_stream(), zp, zn) == 0,
               "id_sort: unsupported vocabulary size ", V);
+  return zp != nullptr;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2036,7 +2050,8 @@ TORCH_LIBRARY(dcr, m) {
         "Tensor(d!) out) -> ()");
   m.def("tokennorm_masked(Tensor dz, Tensor w, Tensor mask, float scale, Tensor(a!) dx, "
         "Tensor(b!) part, Tensor(c!) ticket, Tensor(d!) out) -> ()");
-  m.def("id_sort(Tensor ids, int V, Tensor(a!) ws, Tensor(b!) sid, Tensor(c!) perm) -> ()");
+  m.def("id_sort(Tensor ids, int V, Tensor(a!) ws, Tensor(b!) sid, Tensor(c!) perm, "
+        "Tensor(d!)? zero=None) -> bool");
   m.def("id_sort_workspace(int N, int V) -> int", [](int64_t N, int64_t V) -> int64_t {
     return V > 0 && V <= 16384 && N > 0 && N <= 65535
                ? (int64_t)dcr::id_sort_workspace((int)N, (int)V) : 0; });

@@ -200,10 +200,22 @@ __global__ void __launch_bounds__(256) xent_wide_kernel(
 // columns x 64 row groups (16 independent float4 loads per thread at nrows = 1024, all in flight;
 // 512 workgroups at V = 8192), reduced in a fixed order through LDS (bitwise reproducible).
 // (One column per thread over 256 serial rows took 62 us at V = 8192 with 1024 partials.)
+// The last workgroup also sums the loss partials (lpart[0, nlp) x lscale -> loss_out): one
+// launch instead of a separate one-workgroup sum_partials_kernel.
 __global__ void __launch_bounds__(256) xent_colsum_kernel(const float* __restrict__ colpart,
                                                           int nrows, int V,
-                                                          float* __restrict__ out) {
+                                                          float* __restrict__ out,
+                                                          const float* __restrict__ lpart, int nlp,
+                                                          float lscale,
+                                                          float* __restrict__ loss_out) {
   __shared__ float4 red[64][4];
+  if (lpart && blockIdx.x == gridDim.x - 1) {
+    __shared__ float lred[256 / 64];
+    float a = 0.f;
+    for (int i = threadIdx.x; i < nlp; i += 256) a += lpart[i];
+    const float t = block_sum<256>(a, lred);
+    if (threadIdx.x == 0) loss_out[0] = t * lscale;
+  }
   const int cl = threadIdx.x & 3, rg = threadIdx.x >> 2;
   const int f = blockIdx.x * 4 + cl, V4 = V / 4;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -233,8 +245,11 @@ __global__ void __launch_bounds__(256) xent_colsum_kernel(const float* __restric
 
 void launch_xent_finalize(const float* partial, int nb, int N, float* loss_out,
                           const float* colpart, int ncp, int V, float* db, hipStream_t s) {
-  sum_partials_kernel<<<1, kXentThreads, 0, s>>>(partial, nb, 1.0f / (float)N, loss_out);
-  if (colpart && db) xent_colsum_kernel<<<(V / 4 + 3) / 4, 256, 0, s>>>(colpart, ncp, V, db);
+  if (colpart && db)
+    xent_colsum_kernel<<<(V / 4 + 3) / 4, 256, 0, s>>>(colpart, ncp, V, db, partial, nb,
+                                                       1.0f / (float)N, loss_out);
+  else
+    sum_partials_kernel<<<1, kXentThreads, 0, s>>>(partial, nb, 1.0f / (float)N, loss_out);
 }
 
 int xent_wide_blocks(int N) { return (N + kWideRPB - 1) / kWideRPB; }
@@ -253,9 +268,11 @@ void launch_xent_wide(const float* logits, const float* bias, const int* targets
   } else
   XW(1) XW(2) XW(4) XW(8) XW(16) {}
 #undef XW
-  sum_partials_kernel<<<1, kXentThreads, 0, s>>>(partial, nb, 1.0f / (float)N, loss_out);
   if (dlogits && colpart && db)
-    xent_colsum_kernel<<<(V / 4 + 3) / 4, 256, 0, s>>>(colpart, nb, V, db);
+    xent_colsum_kernel<<<(V / 4 + 3) / 4, 256, 0, s>>>(colpart, nb, V, db, partial, nb,
+                                                       1.0f / (float)N, loss_out);
+  else
+    sum_partials_kernel<<<1, kXentThreads, 0, s>>>(partial, nb, 1.0f / (float)N, loss_out);
 }
 
 }  // namespace dcr

@@ -41,13 +41,17 @@ class BackwardMixin:
         # instead of at the end of the backward; the main stream joins it before the
         # persistent BPTT launches
         self._sorted_ids = None
+        self._de_zeroed = False
         sort_ev = None
         if (self.V > SEG_LDS_MAX_V and self.knobs.on("seg_sort") and not self._dropout(True)
                 and self.cfg.model != "nas" and not self.capturing):
             side = self._side_stream()
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
-                self._sorted_ids = self._sort_ids(ids_tm.view(-1))
+                # (its first launch also clears the embedding gradient the atomic segment sum
+                # accumulates into: no fill launch on the main stream)
+                self._sorted_ids = self._sort_ids(ids_tm.view(-1),
+                                                  zero=self.store.gview("embedding"))
                 sort_ev = torch.cuda.Event()
                 sort_ev.record(side)
             for t_ in self._sorted_ids:
@@ -468,24 +472,30 @@ class BackwardMixin:
         ids = ids_tm.view(-1)
         out = self.store.gview("embedding")
         if self.V > SEG_LDS_MAX_V and self.knobs.on("seg_sort"):
+            zeroed = False
             if self._sorted_ids is not None:  # sorted beside the head (train_step)
                 sid, perm = self._sorted_ids
+                zeroed = self._de_zeroed
             else:
                 sid, perm = self._sort_ids(ids)
-            self.ops.segsum(dX, sid, self.V, out, bufs["ws"], False, perm)
+            self.ops.segsum(dX, sid, self.V, out, bufs["ws"], zeroed, perm)
         else:
             self.ops.segsum(dX, ids, self.V, out, bufs["ws"], False)
 
-    def _sort_ids(self, ids: torch.Tensor):
+    def _sort_ids(self, ids: torch.Tensor, zero: torch.Tensor = None):
         """(sorted ids, source positions) as int32 -- torch.sort(ids, stable=True) -- by the
         V-bucketed counting sort (csrc/embed.hip id_sort: histogram, scan, ballot-ranked
-        scatter) where the vocabulary fits its LDS histogram, else the library sort."""
+        scatter) where the vocabulary fits its LDS histogram, else the library sort.
+        ``zero``: an fp32 buffer the sort's first launch clears (``self._de_zeroed`` tells
+        whether it did)."""
         n = ids.numel()
         nws = int(self.ops.id_sort_workspace(n, self.V))
         if nws and self.knobs.on("id_sort"):
             i32 = dict(dtype=torch.int32, device=ids.device)
             ws, sid, perm = torch.empty(nws, **i32), torch.empty(n, **i32), torch.empty(n, **i32)
-            self.ops.id_sort(ids.contiguous(), self.V, ws, sid, perm)
+            done = self.ops.id_sort(ids.contiguous(), self.V, ws, sid, perm, zero)
+            if zero is not None:
+                self._de_zeroed = bool(done)
             return sid, perm
         sid, perm = torch.sort(ids, stable=True)
         return sid, perm.int()

@@ -43,3 +43,25 @@ def test_sorted_segsum_matches_unsorted(dcr_ops):
     dcr_ops.segsum(X, sid, V, out, seg_ws, False, perm)
     ref = torch.zeros(V, W, device="cuda").index_add_(0, ids.long(), X)
     torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-4)
+
+
+def test_id_sort_clears_the_segsum_output(dcr_ops):
+    """The sort's first launch clears the atomic segment sum's output on the side (the
+    wide-vocabulary step then runs no fill launch): the accumulating segment sum into the
+    cleared buffer equals the plain one; a buffer that is not 16-B aligned is left alone."""
+    N, V, W = 4096, 8192, 512
+    g = torch.Generator(device="cuda").manual_seed(3)
+    ids = torch.randint(0, V, (N,), device="cuda", dtype=torch.int32, generator=g)
+    X = torch.randn(N, W, device="cuda", generator=g)
+    ws = torch.empty(dcr_ops.id_sort_workspace(N, V), dtype=torch.int32, device="cuda")
+    sid, perm = torch.empty_like(ids), torch.empty_like(ids)
+    out = torch.full((V, W), 7.0, device="cuda")
+    assert dcr_ops.id_sort(ids, V, ws, sid, perm, out)
+    assert not bool(out.any())
+    seg_ws = torch.empty(max(1, dcr_ops.segsum_workspace(N, W, V)), device="cuda")
+    dcr_ops.segsum(X, sid, V, out, seg_ws, True, perm)
+    ref = torch.zeros(V, W, device="cuda").index_add_(0, ids.long(), X)
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-4)
+    odd = torch.full((V * W + 1,), 7.0, device="cuda")[1:]  # 4-B but not 16-B aligned
+    assert not dcr_ops.id_sort(ids, V, ws, sid, perm, odd)
+    assert bool((odd == 7.0).all())
