@@ -111,6 +111,8 @@ class BackwardMixin:
                                logits if want_extras else None, bufs["hw_colpart"],
                                s.gview("rnnlm/softmax_b"), bufs["hw_part"], loss_buf)
             mm_tn(O, dlog, s.gview("rnnlm/softmax_w"), q=q)
+            if tail:  # d softmax_b (written by the head's column-sum launch): a norm term
+                q.add_sumsq(s.gview("rnnlm/softmax_b"))
             dtop = self._dtop_wide(dlog, bufs["dtop"].view(N, H)).view(T, B, H)
         elif wide:
             # wide vocabulary: one-read CE (bias added in-kernel), d softmax_b fused (xent_wide)
@@ -403,12 +405,13 @@ class BackwardMixin:
     def _tail_backward_ok(self, bufs) -> bool:
         """The step's deferred gradient work (slab sums, bias sums, the gather route's
         products) runs as tail FINALIZE launches (csrc/tail.hip) instead of prep-launch flushes:
-        LSTM / BasicRNN / GRU with the fused head.  The wide head's step keeps the prep flush by
-        default (DCR_DEBUG=fin_wide=1: FINALIZE; config 5 trace: 24.2 vs 17.8 us, the global
-        norm then needs its own launch either way since the atomic embedding scatter is not a
-        FINALIZE output)."""
+        LSTM / BasicRNN / GRU with the fused head or the wide head.  On the wide head's step the
+        FINALIZE (24 us) also leaves the global norm -- every norm term but the embedding's
+        (outside the norm prefix in TF clip mode, the token-norm slot stands in) is one of its
+        outputs -- so the fused Adam needs no sum-of-squares launch: prep flush 18-21 us +
+        sumsq_final 11 us before (DCR_DEBUG=fin_wide=0 restores that route)."""
         return (self.knobs.on("tail") and self.cfg.model in ("lstm", "rnn", "gru")
-                and (self.fused_head or (self.wide_head and self.knobs.dbg("fin_wide", "0") == "1"))
+                and (self.fused_head or (self.wide_head and self.knobs.dbg("fin_wide", "1") == "1"))
                 and int(self.ops.tail_grid()) > 0)
 
     def _tail_gather_ok(self, layer: int, bufs, fused_dew: bool) -> bool:

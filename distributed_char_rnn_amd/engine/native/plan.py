@@ -47,8 +47,8 @@ DEBUG_KEYS = {
               "one (lstm2_bwd_wide.hip); default 0 (measured slower)",
     "tail_wide": "0: the wide-vocabulary head's step keeps the plain Adam + prep layout "
                  "refresh instead of the fused Adam (csrc/tail.hip phase 1)",
-    "fin_wide": "1: the wide-vocabulary head's deferred sums as a tail FINALIZE launch "
-                "instead of a prep-launch flush (default 0)",
+    "fin_wide": "0: the wide-vocabulary head's deferred sums as a prep-launch flush (+ a "
+                "sum-of-squares launch for the norm) instead of the tail FINALIZE (default 1)",
     "dew": "layer-0 embedding-table gradient: gemm (one-hot MFMA GEMM, default) | segsum | fused",
     "side": "0: no side-stream weight GEMMs in overlap mode",
     "xfuse": "0: no fused input projection in the single-layer persistent forward",
