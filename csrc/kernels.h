@@ -432,7 +432,7 @@ int launch_head(const HeadArgs& a, int cus, float* db_out, float* loss_out, hipS
 // batched per-step data movement (prep.hip)
 enum PrepMode : int {
   PREP_COPY = 0, PREP_TRANSPOSE = 1, PREP_ZERO = 2, PREP_SUM = 3, PREP_COLSUM = 4,
-  PREP_ONEHOT = 5, PREP_TABLE = 6
+  PREP_ONEHOT = 5, PREP_TABLE = 6, PREP_GATHER = 7
 };
 enum PrepKind : int { PREP_F32 = 0, PREP_BF16 = 1, PREP_RAW32 = 2 };  // destination element
 struct PrepTask {

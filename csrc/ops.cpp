@@ -1866,6 +1866,25 @@ void prep(at::TensorList src, at::TensorList dst, at::IntArrayRef mode, at::Tens
       TORCH_CHECK(s.size(0) * s.size(1) == d.size(0), "prep ONEHOT: dst rows must be B*T");
       continue;
     }
+    if (T.mode == dcr::PREP_GATHER) {
+      // batch-major ids [B, T] -> time-major bf16 rows E[id] [T*B, cols] (E fp32 [V, cols] in
+      // `extra`; the ids must be < V: they index E unchecked)
+      TORCH_CHECK(xi + 1 <= extra.size(), "prep GATHER: needs E in `extra`");
+      const at::Tensor& E = extra[xi];
+      xi += 1;
+      TORCH_CHECK(s.scalar_type() == at::kInt && E.scalar_type() == at::kFloat &&
+                  d.scalar_type() == at::kBFloat16, "prep GATHER: int32 ids, fp32 E -> bf16");
+      TORCH_CHECK(E.is_cuda() && E.dim() == 2 && E.size(1) == d.size(1) &&
+                  s.size(0) * s.size(1) == d.size(0), "prep GATHER: shape mismatch");
+      T.src_ld = ld(s);
+      T.src2 = E.data_ptr<float>();
+      T.src2_ld = ld(E);
+      T.kdim = (int)s.size(0);
+      T.kind = dcr::PREP_BF16;
+      T.vec4 = (T.cols % 4 == 0 && T.src2_ld % 4 == 0 && T.dst_ld % 4 == 0 && a16(T.src2) &&
+                (reinterpret_cast<uintptr_t>(T.dst) & 7) == 0) ? 1 : 0;
+      continue;
+    }
     if (T.mode == dcr::PREP_TABLE) {
       // E [rows, K] · W [K, cols] + bias [cols], fp32
       TORCH_CHECK(xi + 2 <= extra.size(), "prep TABLE: needs W and bias in `extra`");

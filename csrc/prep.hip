@@ -18,6 +18,8 @@
 //   COLSUM     dst[0, c] = sum_r src[r, c]               bias partials, fixed order
 //   ONEHOT     dst[n, v] = (ids[n % B][n / B] == v)      bf16 one-hot of the time-major ids
 //   TABLE      dst[v, c] = bias[c] + sum_k E[v, k] W[k, c]   fp32 FMA (layer-0 gather table)
+//   GATHER     dst[n, c] = bf16(E[ids[n % B][n / B], c])    time-major embedding rows (the wide-
+//              vocabulary dW_x0 = X0ᵀ·dZ0 operand: no separate gather launch mid-backward)
 // Every output element is written by exactly one thread with a fixed summation order, so the
 // results are bitwise reproducible.
 #include "common.h"
@@ -223,6 +225,49 @@ __global__ void __launch_bounds__(256) prep_kernel(PrepTable tab) {
           if (n < r1)
             reinterpret_cast<bf16*>(T.dst)[(size_t)n * T.dst_ld + c0 + tx] =
                 f2bf(idv[i] == c0 + tx ? 1.f : 0.f);
+        }
+      return;
+    }
+    case PREP_GATHER: {
+      // as ONEHOT: dst row n = t*B + b <- E row ids[b][t]; every load of the tile (the 16 ids,
+      // then the 16 E values at clamped rows / columns) before the first store
+      const int* ids = static_cast<const int*>(T.src);
+      const int B = T.kdim;
+      if (T.vec4) {  // 16 lanes x float4 per 64-column row, 16 rows per pass (as COPY)
+        const int c = c0 + 4 * (threadIdx.x & 15);
+        if (c >= T.cols) return;
+        int idv[kPrepTile / 16];
+#pragma unroll
+        for (int i = 0; i < kPrepTile / 16; ++i) {
+          const int n = min(r0 + (int)(threadIdx.x >> 4) + 16 * i, T.rows - 1);
+          idv[i] = ids[(size_t)(n % B) * T.src_ld + n / B];
+        }
+        float4 v[kPrepTile / 16];
+#pragma unroll
+        for (int i = 0; i < kPrepTile / 16; ++i)
+          v[i] = *reinterpret_cast<const float4*>(T.src2 + (size_t)idv[i] * T.src2_ld + c);
+#pragma unroll
+        for (int i = 0; i < kPrepTile / 16; ++i) {
+          const int n = r0 + (threadIdx.x >> 4) + 16 * i;
+          if (n < r1) prep_put4(T, (size_t)n * T.dst_ld + c, v[i]);
+        }
+        return;
+      }
+      int idv[kPrepTile / 4];
+#pragma unroll
+      for (int i = 0; i < kPrepTile / 4; ++i) {
+        const int n = min(r0 + ty + 4 * i, T.rows - 1);
+        idv[i] = ids[(size_t)(n % B) * T.src_ld + n / B];
+      }
+      const int cc = min(c0 + tx, T.cols - 1);
+      float v[kPrepTile / 4];
+#pragma unroll
+      for (int i = 0; i < kPrepTile / 4; ++i) v[i] = T.src2[(size_t)idv[i] * T.src2_ld + cc];
+      if (c0 + tx < T.cols)
+#pragma unroll
+        for (int i = 0; i < kPrepTile / 4; ++i) {
+          const int n = r0 + ty + 4 * i;
+          if (n < r1) reinterpret_cast<bf16*>(T.dst)[(size_t)n * T.dst_ld + c0 + tx] = f2bf(v[i]);
         }
       return;
     }

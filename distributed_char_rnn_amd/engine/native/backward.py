@@ -257,8 +257,10 @@ class BackwardMixin:
                 # N x GW values plus two fp32 [V, GW] GEMMs; the dense route scatters N x H
                 # instead: dW_x0 = E[ids]ᵀ·dZ0 (split-K), dE = segsum(dZ0·W_x0ᵀ)
                 # X0 = E[ids] as bf16 rows: one gather kernel (embed_dropout without a mask)
-                X0 = bufs["dx_bf"]
-                self.ops.embed_dropout(ids_tm.reshape(-1), hd["E"], None, 1.0, X0)
+                X0 = getattr(self, "_x0_rows", None)
+                if X0 is None:  # (written by this step's prep launch otherwise, _id_tasks)
+                    X0 = bufs["dx_bf"]
+                    self.ops.embed_dropout(ids_tm.reshape(-1), hd["E"], None, 1.0, X0)
                 # (written into the gradient buffer; the slab and bias-partial sums go to the
                 # step's deferred flush instead of separate reduce launches)
                 lstm_like = self.cfg.model in ("lstm", "rnn")
@@ -431,6 +433,19 @@ class BackwardMixin:
         if (bufs["onehot"] is not None and not self._dropout(True)
                 and self.cfg.model != "nas"):
             tasks.append((x, bufs["onehot"], 5))
+        # wide vocabulary: the time-major bf16 embedding rows X0 = E[ids] (dW_x0 = X0ᵀ·dZ0 of
+        # the dense backward route) as a GATHER task of the same launch, not a gather launch in
+        # the middle of the backward
+        self._x0_rows = None
+        if (self.V > SEG_LDS_MAX_V and not self._dropout(True) and self.cfg.model != "nas"
+                and self.knobs.on("x0_prep")):
+            N = x.shape[0] * x.shape[1]
+            X0 = bufs.get("x0_rows")
+            if X0 is None or X0.shape != (N, self.H):
+                X0 = bufs["x0_rows"] = torch.empty(N, self.H, dtype=torch.bfloat16,
+                                                   device=self.dev)
+            tasks.append((x, X0, 7, [self.store.view("embedding")]))
+            self._x0_rows = X0
         return tasks
 
     def _dew(self, dZ0: torch.Tensor, ids_tm: torch.Tensor, bufs, fused: bool,

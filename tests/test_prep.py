@@ -95,3 +95,26 @@ def test_prep_copy_transpose_vec4(dcr_ops):
     assert torch.equal(d_copy32, sub)
     assert torch.equal(d_t, sub.t().to(torch.bfloat16))
     assert torch.equal(d_t32, sub.t().contiguous())
+
+
+def test_prep_gather_rows(dcr_ops):
+    """GATHER: time-major bf16 embedding rows E[ids[b][t]] (the wide-vocabulary backward's
+    X0 operand), from a row-strided batch-major id view, beside a TABLE task that also takes
+    its operands from ``extra`` (E for GATHER, then W and bias for TABLE)."""
+    torch.manual_seed(2)
+    dev = "cuda"
+    B, T, V, H = 40, 23, 8192, 512
+    idsrc = torch.randint(0, V, (B, 2 * T), dtype=torch.int32, device=dev)
+    x = idsrc[:, T:]
+    E = torch.randn(V, H, device=dev)
+    X0 = torch.full((T * B, H), 3.0, dtype=torch.bfloat16, device=dev)
+    E2 = torch.randn(65, 256, device=dev)
+    W = torch.randn(256, 1024, device=dev)
+    bias = torch.randn(1024, device=dev)
+    tab = torch.empty(65, 1024, device=dev)
+    dcr_ops.prep([x, E2], [X0, tab], [7, 6], [E, W, bias])
+    torch.cuda.synchronize()
+    ref = E[x.t().reshape(-1).long()].to(torch.bfloat16)
+    assert torch.equal(X0, ref)
+    torch.testing.assert_close(tab, (E2.double() @ W.double() + bias.double()).float(),
+                               rtol=1e-5, atol=1e-3)
