@@ -333,6 +333,9 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
   const unsigned offB = (unsigned)(((size_t)bm * G3 + kB + kq) * sizeof(bf16));
   const unsigned tile_off = (unsigned)(16 * G3 * sizeof(bf16));
   float dhp[4] = {0.f, 0.f, 0.f, 0.f};
+  // bias-gradient sums of this lane's row over all steps, of the bf16-rounded dZ values exactly
+  // as the weight GEMMs see them (padded rows add zero); reduced over the tile's rows at the end
+  float dbr[4] = {0.f, 0.f, 0.f, 0.f}, dbu[4] = {0.f, 0.f, 0.f, 0.f}, dbc[4] = {0.f, 0.f, 0.f, 0.f};
 
   // dZc_{T-1} from the top gradient alone
   if (epi) {
@@ -345,7 +348,10 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
     }
     float z0[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) z0[r] = dhp[r] * (1.f - uu[r]) * (1.f - cc[r] * cc[r]);
+    for (int r = 0; r < 4; ++r) {
+      z0[r] = dhp[r] * (1.f - uu[r]) * (1.f - cc[r] * cc[r]);
+      dbc[r] += (float)f2bf(z0[r]);
+    }
     bf16* const zrow = a.dz + ((size_t)(T - 1) * B + b) * G3 + 2 * H + u0;
     if (a.ring0)
       st4bf_ho(loc, a.ring0 + (size_t)((T - 1) & 1) * Bp * H + frag_index(b, u0, H), z0[0], z0[1],
@@ -429,6 +435,8 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
         dzu[r] = du * uu[r] * (1.f - uu[r]);
         dzr[r] = drh[r] * hp[r] * rr[r] * (1.f - rr[r]);
         P[r] = dhp[r] * uu[r] + drh[r] * rr[r];
+        dbr[r] += (float)f2bf(dzr[r]);
+        dbu[r] += (float)f2bf(dzu[r]);
       }
       bf16* dz = a.dz + ((size_t)t * B + b) * G3 + u0;
       if (a.ring1) {
@@ -497,7 +505,10 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
       dhp[3] = dt[3] + P[3] + s0.w + s1.w + s2.w + s3.w;
       float dzc[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dzc[r] = dhp[r] * (1.f - up[r]) * (1.f - cp[r] * cp[r]);
+      for (int r = 0; r < 4; ++r) {
+        dzc[r] = dhp[r] * (1.f - up[r]) * (1.f - cp[r] * cp[r]);
+        dbc[r] += (float)f2bf(dzc[r]);
+      }
       bf16* const crow = a.dz + ((size_t)(t - 1) * B + b) * G3 + 2 * H + u0;
       if (a.ring0)
         st4bf_ho(loc, a.ring0 + (size_t)((t - 1) & 1) * Bp * H + frag_index(b, u0, H), dzc[0],
@@ -512,6 +523,28 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_persist_kernel(GruPersistArgs 
           wg_arrive(&wg_cnt[1], UB * NT, cntC + (size_t)(t - 1) * 4 + (u0 / (H / 4)));
       }
       if (a.ring0 && live) st4bf(crow, dzc[0], dzc[1], dzc[2], dzc[3]);
+    }
+  }
+  // bias-gradient partial of this lane group's 4 units over the tile's 16 rows (lane bits 0-3)
+  if (epi && a.db_part) {
+    float v[12];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v[r] = dbr[r]; v[4 + r] = dbu[r]; v[8 + r] = dbc[r];
+    }
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      v[i] += __shfl_xor(v[i], 1, 64);
+      v[i] += __shfl_xor(v[i], 2, 64);
+      v[i] += __shfl_xor(v[i], 4, 64);
+      v[i] += __shfl_xor(v[i], 8, 64);
+    }
+    const int tile0 = b0 + 16 * en;
+    if ((lane & 15) == 0 && tile0 < B) {
+      float* dst = a.db_part + (size_t)(tile0 / 16) * G3 + u0;
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+        *reinterpret_cast<float4*>(dst + g * H) = make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
     }
   }
 }

@@ -378,6 +378,8 @@ struct GruPersistArgs {
   int cnt_zeroed;
   int xcdloc;           // as Lstm2Args::xcdloc (exchange word: dwords 2-3 of slot 0 of the fwd's
                         //   h set / the bwd's dZg set, which no counter uses)
+  float* db_part;       // bwd (optional): [ceil(B/16), 3H] bias-gradient partials, one row per
+                        //   16-row batch tile (sums of the bf16-rounded dZr, dZu, dZc)
 };
 // token-reduction weight-gradient GEMM (wgrad.hip): C_s = A_chunkᵀ · B_chunk per split-K slab
 constexpr int kWgradMaxProblems = 4;

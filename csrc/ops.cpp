@@ -1354,7 +1354,8 @@ void gru_persist_fwd(const at::Tensor& WgT, const at::Tensor& WcT, const at::Ten
 void gru_persist_bwd(const at::Tensor& Wg, const at::Tensor& Wc, const at::Tensor& dtop,
                      at::Tensor& dz, const at::Tensor& gates, const at::Tensor& h32,
                      at::Tensor& cnt, at::Tensor& err, int64_t spin_limit, bool cnt_zeroed,
-                     const c10::optional<at::Tensor>& ring0, const c10::optional<at::Tensor>& ring1) {
+                     const c10::optional<at::Tensor>& ring0, const c10::optional<at::Tensor>& ring1,
+                     const c10::optional<at::Tensor>& db_part) {
   check_seq(Wg, at::kBFloat16, "Wg");
   check_seq(Wc, at::kBFloat16, "Wc");
   check_seq(dtop, at::kFloat, "dtop");
@@ -1370,6 +1371,12 @@ void gru_persist_bwd(const at::Tensor& Wg, const at::Tensor& Wc, const at::Tenso
   a.Wc = ptr<bf16>(Wc);
   a.dtop = ptr<float>(dtop);
   a.dz = ptr<bf16>(dz);
+  check_opt(db_part, at::kFloat, "db_part");
+  if (has(db_part)) {
+    TORCH_CHECK(db_part->numel() >= (int64_t)((B + 15) / 16) * 3 * H,
+                "db_part must hold [ceil(B/16), 3H]");
+    a.db_part = optr<float>(db_part);
+  }
   const int rc = dcr::launch_gru_persist(1, a, num_cus(), cur_stream());
   TORCH_CHECK(rc == 0, "persistent GRU BPTT not launched (", rc, ")");
 }
@@ -2151,7 +2158,7 @@ TORCH_LIBRARY(dcr, m) {
   m.def(
       "gru_persist_bwd(Tensor Wg, Tensor Wc, Tensor dtop, Tensor(a!) dz, Tensor gates, "
       "Tensor h32, Tensor(b!) cnt, Tensor(c!) err, int spin_limit, bool cnt_zeroed=False, "
-      "Tensor(d!)? ring0=None, Tensor(e!)? ring1=None) -> ()");
+      "Tensor(d!)? ring0=None, Tensor(e!)? ring1=None, Tensor(f!)? db_part=None) -> ()");
   m.def("segsum(Tensor X, Tensor? ids, int V, Tensor(a!) out, Tensor(b!) workspace, bool accumulate, "
         "Tensor? perm=None) -> ()");
   m.def("segsum_workspace(int N, int W, int V) -> int", [](int64_t N, int64_t W, int64_t V) -> int64_t {

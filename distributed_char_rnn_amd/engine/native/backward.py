@@ -205,7 +205,9 @@ class BackwardMixin:
                 gr = bufs["grings"]
                 self.ops.gru_persist_bwd(lw.W2, lw.Wh, dtop, lb.dz, lb.gates, lb.h32,
                                          bufs["cnt"][self.L + layer], self.err, self.spin_limit,
-                                         cnt_zeroed=True, ring0=gr[0], ring1=gr[2])
+                                         cnt_zeroed=True, ring0=gr[0], ring1=gr[2],
+                                         db_part=(self._db_part(bufs, layer)
+                                                  if layer in bufs["bpart_layers"] else None))
                 if layer == 0 and user_ready is not None:
                     on_ready = _release()
             elif self._lib_step("bwd", B):
@@ -303,7 +305,8 @@ class BackwardMixin:
             elif gather:
                 # the bias gradient from the BPTT kernel's partials: summed in the same flush
                 # as dEW's slabs (rather than a column sum of dEW after it)
-                part_bias = layer in bufs["bpart_layers"] and self.cfg.model in ("lstm", "rnn")
+                part_bias = layer in bufs["bpart_layers"] and self.cfg.model in ("lstm", "rnn",
+                                                                                  "gru")
                 if part_bias:
                     dbias = self._bias_sum(self._db_part(bufs, layer), names, q)
                 dEW = self._dew(dZx, ids_tm, bufs, fused_dew, q)  # [V, GW] fp32 (flushes q)
@@ -420,7 +423,8 @@ class BackwardMixin:
         """The layer-0 gather route's products in the finalize: the one-hot dEW GEMM with the
         bias gradient from the BPTT kernel's partials."""
         return (layer in bufs["bpart_layers"] and not fused_dew and self.dew_mode == "gemm"
-                and bufs["onehot"] is not None and self.V <= SEG_LDS_MAX_V)
+                and bufs["onehot"] is not None and self.V <= SEG_LDS_MAX_V
+                and self.cfg.model in ("lstm", "rnn"))
 
     def _id_tasks(self, x: torch.Tensor, y: torch.Tensor, bufs) -> list:
         """Prep tasks (csrc/prep.hip) of the batch: x, y [B, T] int32 -> time-major [T, B]
@@ -576,8 +580,9 @@ class BackwardMixin:
             if dWx is not None:  # (None: written by mm_tn_cols's deferred slab sums)
                 s.gview(gk)[:H].copy_(dWx[:, : 2 * H])
                 s.gview(ck)[:H].copy_(dWx[:, 2 * H:])
-            s.gview(gb).copy_(dbias[: 2 * H])
-            s.gview(cb).copy_(dbias[2 * H:])
+            if dbias is not None:  # (None: column sums of the BPTT partials, _bias_sum)
+                s.gview(gb).copy_(dbias[: 2 * H])
+                s.gview(cb).copy_(dbias[2 * H:])
         elif self.cfg.model == "nas":
             s.gview(names[0]).copy_(dWx)
         else:

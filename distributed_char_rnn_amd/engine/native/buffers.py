@@ -166,6 +166,10 @@ class BuffersMixin:
         # layers whose BPTT kernel writes bias-gradient partials (db_part)
         bufs["bpart_layers"] = (bufs["pers_layers"] if plan.persist_bwd
                                 else set(range(npair)))
+        if (m == "gru" and training and getattr(plan, "gru_persist", False)
+                and self.knobs.on("gru_bpart")):
+            # the persistent GRU BPTT writes its bias partials too (csrc/gru_persist.hip)
+            bufs["bpart_layers"] = set(range(self.L))
         self._bufs[key] = bufs
         return bufs
 
@@ -196,4 +200,16 @@ class BuffersMixin:
             if q is not None:
                 return q.add_colsum(part, self.store.gview(names[1]))
             return torch.sum(part, 0, out=self.store.gview(names[1]))
+        if self.cfg.model == "gru":
+            # [r | u] columns -> the gates bias, [c] -> the candidate bias; written here (None:
+            # nothing left for _write_input_grads to copy)
+            H = self.H
+            gb, cb = self.store.gview(names[1]), self.store.gview(names[3])
+            if q is not None:
+                q.add_colsum(part[:, : 2 * H], gb)
+                q.add_colsum(part[:, 2 * H:], cb)
+            else:
+                torch.sum(part[:, : 2 * H], 0, out=gb)
+                torch.sum(part[:, 2 * H:], 0, out=cb)
+            return None
         return part.sum(0)

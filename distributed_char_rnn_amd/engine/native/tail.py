@@ -43,8 +43,11 @@ MAX_TILES = 16384  # csrc/kernels.h kTailMaxTiles: tiles of one launch
 
 
 class TailTable:
-    def __init__(self, max_tasks: int = 16):
+    def __init__(self, max_tasks: int = 16, launch_tasks: Optional[int] = None):
+        """``max_tasks``: tasks this table may hold; ``launch_tasks``: tasks per launch (the
+        kernel's by-value table) when a larger logical table is partitioned into launches."""
         self.calls = []  # (method, args, kwargs) of every task, for partition()
+        self.launch_tasks = launch_tasks or max_tasks
         self.words: List[int] = []
         self.keep: List[torch.Tensor] = []
         self.ops: List[int] = []
@@ -60,15 +63,16 @@ class TailTable:
         """This table as consecutive launches of at most ``max_tiles`` tiles (and max_tasks
         tasks) each, in task order.  A task whose producers all ran in an earlier launch waits
         for nothing (stream order); a counter's ``need`` counts this launch's producers."""
-        if sum(self.tiles) <= max_tiles and len(self.ops) <= self.max_tasks:
+        lt = self.launch_tasks
+        if sum(self.tiles) <= max_tiles and len(self.ops) <= lt:
             return [self]
-        out, cur = [], TailTable(self.max_tasks)
+        out, cur = [], TailTable(lt)
         for (meth, args, kw), nt in zip(self._flat_calls(), self.tiles):
             if nt > max_tiles:
                 raise ValueError(f"tail task of {nt} tiles > {max_tiles}")
             if len(cur) and (sum(cur.tiles) + nt > max_tiles or len(cur) >= cur.max_tasks):
                 out.append(cur)
-                cur = TailTable(self.max_tasks)
+                cur = TailTable(lt)
             kw = dict(kw)
             if kw.get("wait", -1) >= 0 and cur.sig_tiles.get(kw["wait"], 0) <= 0:
                 kw["wait"] = -1
@@ -334,7 +338,9 @@ class TailQueue:
         if not (self.sums or self.colsums or self.sumsqs or self.mms) and total_out is None:
             return False
         be = self.be
-        tab = TailTable(int(self.ops.tail_max_tasks()))
+        # (a logical table: more tasks than one launch's table become consecutive launches,
+        # partition(); the GRU's per-layer slab and bias sums exceed one)
+        tab = TailTable(1 << 12, launch_tasks=int(self.ops.tail_max_tasks()))
         spans = []
 
         def norm_of(out):
