@@ -294,7 +294,14 @@ class BackwardMixin:
                 q.signal_on(dew, 0)
                 mm_tn(bufs["onehot"], dZx, dew, q=q)
                 GW_ = dew.shape[1]
-                q.add_mm(s.gview(names[0])[:H], hd["E"], (1, H), dew, (GW_, 1), V, wait=0)
+                if self.cfg.model == "gru":
+                    # W_x0's gradient belongs to two kernels: gates [:, :2H], candidate [:, 2H:]
+                    gk, _, ck, _ = names
+                    q.add_mm(s.gview(gk)[:H], hd["E"], (1, H), dew, (GW_, 1), V, wait=0)
+                    q.add_mm(s.gview(ck)[:H], hd["E"], (1, H), dew[:, 2 * H:], (GW_, 1), V,
+                             wait=0)
+                else:
+                    q.add_mm(s.gview(names[0])[:H], hd["E"], (1, H), dew, (GW_, 1), V, wait=0)
                 q.add_mm(s.gview("embedding"), dew, (GW_, 1), lw.Wx32, (1, GW_), GW_, wait=0)
                 written = True
                 if on_ready is not None:
@@ -424,7 +431,7 @@ class BackwardMixin:
         bias gradient from the BPTT kernel's partials."""
         return (layer in bufs["bpart_layers"] and not fused_dew and self.dew_mode == "gemm"
                 and bufs["onehot"] is not None and self.V <= SEG_LDS_MAX_V
-                and self.cfg.model in ("lstm", "rnn"))
+                and self.cfg.model in ("lstm", "rnn", "gru"))
 
     def _id_tasks(self, x: torch.Tensor, y: torch.Tensor, bufs) -> list:
         """Prep tasks (csrc/prep.hip) of the batch: x, y [B, T] int32 -> time-major [T, B]

@@ -174,8 +174,10 @@ class TailTable:
         ar, ak = a_strides
         bk, bc = b_strides
         rows, cols = out.shape
-        # every element the strides address lies inside the operands
-        assert (rows - 1) * ar + (k - 1) * ak < a.numel() and (k - 1) * bk + (cols - 1) * bc < b.numel()
+        # every element the strides address lies inside the operands (a view's extent: from its
+        # first element to its last, e.g. a column block of a wider matrix)
+        ext = lambda t: 1 + sum((n - 1) * st for n, st in zip(t.shape, t.stride())) if t.numel() else 0  # noqa: E731
+        assert (rows - 1) * ar + (k - 1) * ak < ext(a) and (k - 1) * bk + (cols - 1) * bc < ext(b)
         ops = dict(k=k, a=a.data_ptr(), ar=ar, ak=ak, b=b.data_ptr(), bk=bk, bc=bc,
                    bias=0 if bias is None else bias.data_ptr())
         keep = (out, a, b) + (() if bias is None else (bias,))
