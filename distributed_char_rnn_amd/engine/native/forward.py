@@ -230,8 +230,10 @@ class ForwardMixin:
                                           bias=lw.bias if (ids_arg is None and H > 1024) else None)
             elif P.gru_persist:
                 gr = bufs["grings"]
+                # the final h straight into a fresh tensor: the returned TBPTT state (no copy)
+                lb.hlast32 = torch.empty(B, H, dtype=f32, device=self.dev)
                 self.ops.gru_persist_fwd(lw.WhT, lw.WT2, zx, ids_arg, lb.hbuf, lb.h32, lb.rh,
-                                         lb.gates, None, bufs["cnt"][layer], self.err,
+                                         lb.gates, lb.hlast32, bufs["cnt"][layer], self.err,
                                          self.spin_limit, cnt_zeroed=True, ring0=gr[0],
                                          ring1=gr[1], bias_x=lw.bias if ids_arg is None else None)
             elif self._lib_step("fwd", B):
@@ -260,7 +262,7 @@ class ForwardMixin:
                 new_state.append((lb.clast32, lb.hlast32) if layer in fresh
                                  else (lb.cbuf[T].clone(), lb.hlast32.clone()))
             elif self.cfg.model == "gru":
-                new_state.append((lb.h32[T].clone(),))
+                new_state.append((lb.hlast32,) if P.gru_persist else (lb.h32[T].clone(),))
             else:
                 new_state.append((lb.hlast32.clone(),))
         return bufs, O, logits, new_state
