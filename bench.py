@@ -57,8 +57,10 @@ def parse(argv=None):
     ap.add_argument("--force_sync", action="store_true",
                     help="run the bucketed RCCL gradient exchange even on one rank (measures its "
                          "cost and release schedule on a one-GPU box)")
-    ap.add_argument("--graph", action="store_true",
-                    help="replay each step from one captured HIP graph (one GPU, no dropout)")
+    ap.add_argument("--graph", nargs="?", const="on", default="auto", choices=["auto", "on", "off"],
+                    help="replay each step from one captured HIP graph (one GPU, no dropout); "
+                         "auto (the default, as train.py) = only for launch-bound steps "
+                         "(batch x seq x hidden <= 2^21), where the replay wins; eager otherwise")
     ap.add_argument("--dist_backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="auto = nccl (RCCL over xGMI) on GPUs; gloo = multi-rank rehearsal on "
                          "one GPU (with DCR_RECURRENCE=step: persistent grids of two processes cannot "
@@ -104,7 +106,7 @@ def main(argv=None) -> int:
     sync = GradSync(model.store, world, a.bucket_mb, a.allreduce_dtype,
                     enabled=(world > 1 or a.force_sync) and not sharded,
                     guard=model.error_word(), timing=a.profile)
-    if (a.force_sync or sharded) and a.graph:
+    if (a.force_sync or sharded) and a.graph == "on":
         # the captured step never calls sync.ready, so nothing would write the guard slot and
         # the exchange would not be measured at all
         raise SystemExit("bench.py: --force_sync measures the eager bucketed exchange; "
@@ -141,14 +143,21 @@ def main(argv=None) -> int:
         prof = PhaseProfiler(True, device)
 
     graphed = None
-    if a.graph:
+    use_graph = a.graph == "on"
+    if a.graph == "auto":
+        from distributed_char_rnn_amd.engine.trainer import GRAPH_AUTO_MAX_WORK
+
+        use_graph = (not (a.force_sync or sharded) and torch.device(device).type == "cuda"
+                     and B * T * a.hidden <= GRAPH_AUTO_MAX_WORK)
+    if use_graph:
         from distributed_char_rnn_amd.engine.graph_step import GraphedStep
 
         ok, why = GraphedStep.supported(model, world)
-        if not ok:
+        if not ok and a.graph == "on":
             print(f"--graph: {why}", file=sys.stderr)
             return 2
-        graphed = GraphedStep(model, opt, log=lambda m: print(m, file=sys.stderr))
+        if ok:
+            graphed = GraphedStep(model, opt, log=lambda m: print(m, file=sys.stderr))
 
     def step(i, state):
         k = i % nbat
@@ -237,7 +246,7 @@ def main(argv=None) -> int:
                                         if (a.model, a.hidden, a.layers, T, B, a.dtype) ==
                                         ("lstm", 512, 2, 128, 256, "bf16") else None),
             "keep_prob": [a.input_keep_prob, a.output_keep_prob],
-            "graph": bool(a.graph),
+            "graph": graphed is not None,
             "final_loss": final_loss,
         }
         print(json.dumps(out), flush=True)
