@@ -39,7 +39,13 @@ class LayoutsMixin:
         transposes; a narrow vocabulary's layer-0 gather table is a task of the same launch, a
         wide one's the gemm_nt launch behind it, reading the mirror's bf16 E)."""
         wide_ok = self.V <= SEG_LDS_MAX_V or self.knobs.on("tail_wide")
-        return (self.knobs.on("tail") and self.cfg.model in ("lstm", "rnn") and wide_ok
+        # GRU: its W_x [D, 3H] concatenates two kernels (not a mirror slice) -- both halves are
+        # layout outputs of the update; the fp32 W_x0 / bias concatenations follow in the next
+        # step-start prep launch (_prep); narrow vocabularies only (the table is in-launch)
+        gru_ok = (self.cfg.model == "gru" and self.V <= SEG_LDS_MAX_V
+                  and self.knobs.on("gru_adam"))
+        return (self.knobs.on("tail") and (self.cfg.model in ("lstm", "rnn") or gru_ok)
+                and wide_ok
                 and not getattr(self, "padded_inner", False)
                 and int(self.ops.tail_grid()) > 0)
 
@@ -106,12 +112,16 @@ class LayoutsMixin:
             torch.addmm(w0.bias, E, w0.Wx, out_dtype=f32, out=hd["table"])
 
     def fused_adam_done(self) -> None:
-        """The update ran (the store's version was bumped): the layouts match it."""
+        """The update ran (the store's version was bumped): the layouts match it (GRU: but for
+        the fp32 concatenations, which the next prep launch copies)."""
         self._wver = getattr(self.store, "version", 0)
+        if self.cfg.model == "gru":
+            self._post_adam = self._gru_f32_tasks
 
     def _adam_table(self) -> "tailmod.TailTable":
         s, H, D = self.store, self.H, self.H
-        tab = tailmod.TailTable(int(self.ops.tail_max_tasks()))
+        # (GRU: 6 regions per layer -- more tasks than one launch's table holds)
+        tab = tailmod.TailTable(1 << 12, launch_tasks=int(self.ops.tail_max_tasks()))
         cover = 0
 
         def region(name, r0=0, r1=None, outs=(), sig=-1):
@@ -129,10 +139,29 @@ class LayoutsMixin:
         # the gather table's operands first (they signal counter 0), then everything else
         sig = 0 if table else -1
         region("embedding", sig=sig)
-        region(names[0][0], 0, D, [(w0.WxT, D, True)] if w0.WxT is not None else (), sig=sig)
-        region(names[0][1], sig=sig)
         hd = self._head
-        for layer in range(self.L):
+        if self.cfg.model == "gru":
+            # W_x's halves [:, :2H] (gates) / [:, 2H:] (candidate) are column blocks of one
+            # [D, 3H] tensor; W_h's: the gates' [H, 2H] and the candidate's [H, H] are mirror
+            # slices, their transposes outputs
+            for layer in range(self.L):
+                lw = self._w[layer]
+                gk, gb, ck, cb = names[layer]
+                ls = sig if layer == 0 else -1
+                region(gk, 0, D, [(lw.Wx[:, : 2 * H], 3 * H, False)], sig=ls)
+                region(gb, sig=ls)
+                region(ck, 0, D, [(lw.Wx[:, 2 * H:], 3 * H, False)], sig=ls)
+                region(cb, sig=ls)
+            for layer in range(self.L):
+                lw = self._w[layer]
+                gk, _, ck, _ = names[layer]
+                region(gk, D, 2 * D, [(lw.WhT, H, True)])
+                region(ck, D, 2 * D, [(lw.WT2, H, True)])
+        else:
+            region(names[0][0], 0, D, [(w0.WxT, D, True)] if w0.WxT is not None else (),
+                   sig=sig)
+            region(names[0][1], sig=sig)
+        for layer in range(self.L if self.cfg.model != "gru" else 0):
             lw = self._w[layer]
             k, b = names[layer]
             if layer > 0:
@@ -150,7 +179,13 @@ class LayoutsMixin:
         want = sum(sp.numel for sp in s.specs)  # (alignment padding between tensors: no params)
         if cover != want:
             raise AssertionError(f"fused Adam covers {cover} of {want} parameters")
-        if table:
+        if table and self.cfg.model == "gru":
+            # the two kernels' column blocks of E·W_x0 + b0, from the updated fp32 masters
+            gk, gb, ck, cb = (s.view(n) for n in names[0])
+            tb = hd["table"]
+            tab.mm(tb[:, : 2 * H], hd["E"], (H, 1), gk[:D], (2 * H, 1), D, bias=gb, wait=0)
+            tab.mm(tb[:, 2 * H:], hd["E"], (H, 1), ck[:D], (H, 1), D, bias=cb, wait=0)
+        elif table:
             # E·W_x0 + b0 last (its tiles in the launch's last round, when the operand updates
             # are done; right after them its workgroups spun in the first round: 61 vs 39 us),
             # as 80-row tiles of the full k = H (k-slabs summed in the same launch: 56 vs 38 us)
@@ -163,6 +198,7 @@ class LayoutsMixin:
         and refreshed by ``_prep`` through the batched prep kernel."""
         s, H, D, dev = self.store, self.H, self.H, self.dev
         self._w, self._wtasks = [], []
+        self._gru_f32_tasks, self._post_adam = [], []
         T = self._wtasks
         e = lambda *shape, dt=bf16: torch.empty(*shape, dtype=dt, device=dev)  # noqa: E731
         # with the fused Adam (csrc/tail.hip) the bf16 operand copies W_x / W_h / softmax_w are
@@ -192,14 +228,23 @@ class LayoutsMixin:
                     T.append((k[:D], lw.WxT, 1))
             elif self.cfg.model == "gru":
                 gk, gb, ck, cb = (s.view(n) for n in names)
-                Wx32, bias = e(D, 3 * H, dt=f32), e(3 * H, dt=f32)
-                lw = LayerWeights(Wx=e(D, 3 * H), Wx32=Wx32, bias=bias, Wh=e(H, H),
-                                  WhT=e(2 * H, H), W2=e(H, 2 * H), WT2=e(H, H))
-                T += [(gk[:D], Wx32[:, : 2 * H], 0), (ck[:D], Wx32[:, 2 * H:], 0),
-                      (gk[:D], lw.Wx[:, : 2 * H], 0), (ck[:D], lw.Wx[:, 2 * H:], 0),
-                      (gk[D:], lw.W2, 0), (gk[D:], lw.WhT, 1), (ck[D:], lw.Wh, 0),
-                      (ck[D:], lw.WT2, 1), (gb.view(1, -1), bias[: 2 * H].view(1, -1), 0),
-                      (cb.view(1, -1), bias[2 * H:].view(1, -1), 0)]
+                # (the fp32 W_x: layer 0's table / dE only)
+                Wx32 = e(D, 3 * H, dt=f32) if layer == 0 else None
+                bias = e(3 * H, dt=f32)
+                lw = LayerWeights(Wx=e(D, 3 * H), Wx32=Wx32, bias=bias,
+                                  Wh=mv(names[2])[D:] if mv else e(H, H), WhT=e(2 * H, H),
+                                  W2=mv(names[0])[D:] if mv else e(H, 2 * H), WT2=e(H, H))
+                # the fp32 concatenations (W_x0 for the dE product, the biases for the
+                # forward): also what a fused update leaves to the next prep launch
+                f32_tasks = [(gb.view(1, -1), bias[: 2 * H].view(1, -1), 0),
+                             (cb.view(1, -1), bias[2 * H:].view(1, -1), 0)]
+                if layer == 0:
+                    f32_tasks += [(gk[:D], Wx32[:, : 2 * H], 0), (ck[:D], Wx32[:, 2 * H:], 0)]
+                self._gru_f32_tasks += f32_tasks
+                T += f32_tasks + [
+                    (gk[:D], lw.Wx[:, : 2 * H], 0), (ck[:D], lw.Wx[:, 2 * H:], 0),
+                    (gk[D:], lw.W2, 0), (gk[D:], lw.WhT, 1), (ck[D:], lw.Wh, 0),
+                    (ck[D:], lw.WT2, 1)]
             else:  # nas
                 kx, km = s.view(names[0]), s.view(names[1])
                 lw = LayerWeights(Wx=e(D, 8 * H), Wx32=kx, bias=torch.zeros(8 * H, device=dev),
@@ -243,8 +288,10 @@ class LayoutsMixin:
         if not self._w:
             self._alloc_weights()
         elif self._wver == ver:
-            return []
+            tasks, self._post_adam = self._post_adam, []
+            return list(tasks)
         self._wver = ver
+        self._post_adam = []
         tasks = list(self._wtasks)
         w0 = self._w[0]
         if self.V <= SEG_LDS_MAX_V and self.cfg.model in ("lstm", "rnn"):
@@ -308,5 +355,10 @@ class LayoutsMixin:
                     Eb.copy_(self._head["E"])
                     self._head["table"] = torch.addmm(w0.bias, Eb, w0.Wx, out_dtype=f32)
             else:
-                self._head["table"] = torch.addmm(w0.bias, self._head["E"], w0.Wx32)  # [V, GW]
+                # in place: the fused Adam's table task (GRU) writes this tensor
+                tab = self._head.get("table")
+                if tab is None or tab.shape != (self.V, w0.Wx32.shape[1]):
+                    tab = self._head["table"] = torch.empty(self.V, w0.Wx32.shape[1],
+                                                            dtype=f32, device=self.dev)
+                torch.addmm(w0.bias, self._head["E"], w0.Wx32, out=tab)  # [V, GW]
             self._table_dirty = False

@@ -49,6 +49,8 @@ DEBUG_KEYS = {
                  "refresh instead of the fused Adam (csrc/tail.hip phase 1)",
     "gru_bpart": "0: GRU bias gradients as column sums of the row-major dZ (a colsum launch per "
                  "layer) instead of the persistent BPTT kernel's partials",
+    "gru_adam": "0: the GRU step keeps the plain Adam + prep layout refresh instead of the "
+                "fused Adam (csrc/tail.hip phase 1)",
     "x0_prep": "0: the wide-vocabulary backward gathers its bf16 embedding rows X0 = E[ids] in "
                "a launch of its own instead of a GATHER task of the step-start prep launch",
     "fin_wide": "0: the wide-vocabulary head's deferred sums as a prep-launch flush (+ a "

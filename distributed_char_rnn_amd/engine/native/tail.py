@@ -176,7 +176,9 @@ class TailTable:
         rows, cols = out.shape
         # every element the strides address lies inside the operands (a view's extent: from its
         # first element to its last, e.g. a column block of a wider matrix)
-        ext = lambda t: 1 + sum((n - 1) * st for n, st in zip(t.shape, t.stride())) if t.numel() else 0  # noqa: E731
+        def ext(t):
+            return 1 + sum((n - 1) * st for n, st in zip(t.shape, t.stride())) if t.numel() else 0
+
         assert (rows - 1) * ar + (k - 1) * ak < ext(a) and (k - 1) * bk + (cols - 1) * bc < ext(b)
         ops = dict(k=k, a=a.data_ptr(), ar=ar, ak=ak, b=b.data_ptr(), bk=bk, bc=bc,
                    bias=0 if bias is None else bias.data_ptr())
@@ -404,11 +406,12 @@ class TailQueue:
             be._fin_ws = workspace(self.ops, be.dev)
         s = be.store
         _, use_slot = s.norm_terms()
-        parts = tab.partition()
-        ok = ok and len(parts) == 1  # (several launches: the fused Adam sums the norm itself)
-        for t in parts:
+        # several launches: each adds its terms to the previous one's total (the kernel's
+        # ``extra`` addend; the first one's is the norm slot)
+        extra = s.norm_slot_view() if (ok and use_slot) else None
+        for t in tab.partition():
             run(self.ops, t, 0, be._fin_ws, be.err, be.spin_limit,
-                total_out=total_out if ok else None,
-                extra=s.norm_slot_view() if (ok and use_slot) else None,
+                total_out=total_out if ok else None, extra=extra,
                 dynamic=be.tail_dynamic() or (self.collectives and t.waits > 0))
+            extra = total_out if ok else None
         return ok

@@ -69,12 +69,12 @@ def test_finalize_tasks_and_norm(dcr_ops, dynamic):
     assert abs(float(total) - ref_total) / ref_total < 1e-5
 
 
-def _models(fused: bool, H=128, L=2, V=65, seed=0):
+def _models(fused: bool, H=128, L=2, V=65, seed=0, kind="lstm"):
     from distributed_char_rnn_amd.engine.optim import TFAdam
     from distributed_char_rnn_amd.models.char_rnn import CharRNN
     from distributed_char_rnn_amd.models.params import ModelConfig
 
-    cfg = ModelConfig(model="lstm", vocab_size=V, rnn_size=H, num_layers=L)
+    cfg = ModelConfig(model=kind, vocab_size=V, rnn_size=H, num_layers=L)
     model = CharRNN(cfg, device="cuda:0", seed=seed)
     opt = TFAdam(model.store, clip=5.0, guard=model.error_word())
     if fused:
@@ -92,12 +92,15 @@ class _Sync:
         pass
 
 
+@pytest.mark.parametrize("kind", ["lstm", "gru"])
 @pytest.mark.parametrize("dp", [False, True])
 @pytest.mark.parametrize("B,T", [(32, 16), (256, 24)])
-def test_fused_adam_matches_plain(B, T, dp):
+def test_fused_adam_matches_plain(B, T, dp, kind):
     """Three training steps with the fused tail vs the plain optimizer: parameters, slots and
     the reported norm agree, and every bf16 layout the fused update wrote equals a fresh
-    refresh of the layouts from the fp32 masters (bitwise)."""
+    refresh of the layouts from the fp32 masters (bitwise).  GRU: W_x's two kernels are column
+    blocks of one layout, the table two products; the fp32 concatenations follow in the next
+    prep launch."""
     torch.manual_seed(5)
     x = torch.randint(0, 65, (B, 3 * T), dtype=torch.int32, device="cuda")
     y = torch.randint(0, 65, (B, 3 * T), dtype=torch.int32, device="cuda")
@@ -105,7 +108,7 @@ def test_fused_adam_matches_plain(B, T, dp):
         return float((a.double() - b.double()).norm() / b.double().norm())
     runs = []
     for fused in (False, True):
-        model, opt = _models(fused)
+        model, opt = _models(fused, kind=kind)
         st = model.zero_state(B)
         snap = None
         for k in range(3):
@@ -130,19 +133,24 @@ def test_fused_adam_matches_plain(B, T, dp):
     # layouts: what the fused update wrote vs a refresh from the same fp32 masters
     be = m1.backend
     w = be._w
-    snap = [(lw.WhT.clone(), lw.Wh.clone(), lw.Wx.clone(),
-             None if lw.WxT is None else lw.WxT.clone()) for lw in w]
+    opt_names = ("WxT", "W2", "WT2")
     hd = be._head
     hsnap = {k: hd[k].clone() for k in ("Ws", "WsT", "Wsk", "table") if k in hd}
+    if kind == "gru":
+        be._run_prep(be._prep())  # the fp32 concatenations the update left to the prep launch
+    snap = [(lw.WhT.clone(), lw.Wh.clone(), lw.Wx.clone(), lw.bias.clone(),
+             {n: getattr(lw, n).clone() for n in opt_names + ("Wx32",)
+              if getattr(lw, n) is not None}) for lw in w]
     be.params_changed()
     be._run_prep(be._prep())
     torch.cuda.synchronize()
-    for lw, (wht, wh, wx, wxt) in zip(w, snap):
+    for lw, (wht, wh, wx, b, opt_ws) in zip(w, snap):
         assert torch.equal(lw.WhT, wht)
         assert torch.equal(lw.Wh, wh)
         assert torch.equal(lw.Wx, wx)
-        if wxt is not None:
-            assert torch.equal(lw.WxT, wxt)
+        assert torch.equal(lw.bias, b)
+        for n, t in opt_ws.items():
+            assert torch.equal(getattr(lw, n), t), n
     for k, v in hsnap.items():
         if k == "table":
             assert rel(hd[k], v) < 1e-6
@@ -165,17 +173,19 @@ def test_fused_adam_skips_on_error_word():
     model.backend.err.zero_()
 
 
+@pytest.mark.parametrize("kind", ["lstm", "gru"])
 @pytest.mark.parametrize("B,T", [(32, 16), (256, 24)])
-def test_tail_backward_matches_prep_flush(monkeypatch, B, T):
+def test_tail_backward_matches_prep_flush(monkeypatch, B, T, kind):
     """The gradients of the tail FINALIZE route equal the prep-flush + library route's (the
-    slab sums in the same fixed order; dW_x0 / dE as fp32 products either way)."""
+    slab sums in the same fixed order; dW_x0 / dE as fp32 products either way).  GRU: more
+    tasks than one launch holds -- each launch adds its norm terms to the previous total."""
     torch.manual_seed(7)
     x = torch.randint(0, 65, (B, T), dtype=torch.int32, device="cuda")
     y = torch.randint(0, 65, (B, T), dtype=torch.int32, device="cuda")
     grads = []
     for knob in ("tail=0", ""):
         monkeypatch.setenv("DCR_DEBUG", knob)
-        model, _ = _models(False)
+        model, _ = _models(False, kind=kind)
         model.train_step(x, y, model.zero_state(B))
         torch.cuda.synchronize()
         grads.append(model.store.grad.clone())
