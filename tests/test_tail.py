@@ -69,6 +69,31 @@ def test_finalize_tasks_and_norm(dcr_ops, dynamic):
     assert abs(float(total) - ref_total) / ref_total < 1e-5
 
 
+def test_finalize_total_across_launches(dcr_ops):
+    """A table partitioned into several launches: each adds its norm terms to the previous
+    launch's total through the ``extra`` addend (the first one's: the norm slot)."""
+    torch.manual_seed(4)
+    parts = [torch.randn(3, 40, 96, device="cuda") for _ in range(5)]
+    outs = [torch.empty(40, 96, device="cuda") for _ in parts]
+    slot = torch.tensor([7.25], device="cuda")
+    total = torch.zeros(1, device="cuda")
+    err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    tab = tailmod.TailTable(64, launch_tasks=2)
+    for p, o in zip(parts, outs):
+        tab.sum(p, o, norm=True)
+    launches = tab.partition()
+    assert len(launches) == 3
+    ws = tailmod.workspace(dcr_ops, "cuda")
+    extra = slot
+    for t in launches:
+        tailmod.run(dcr_ops, t, 0, ws, err, 1 << 22, total_out=total, extra=extra, dynamic=True)
+        extra = total
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    ref = sum(float((p.double().sum(0) ** 2).sum()) for p in parts) + 7.25
+    assert abs(float(total) - ref) <= 1e-5 * ref
+
+
 def _models(fused: bool, H=128, L=2, V=65, seed=0, kind="lstm"):
     from distributed_char_rnn_amd.engine.optim import TFAdam
     from distributed_char_rnn_amd.models.char_rnn import CharRNN
@@ -177,8 +202,7 @@ def test_fused_adam_skips_on_error_word():
 @pytest.mark.parametrize("B,T", [(32, 16), (256, 24)])
 def test_tail_backward_matches_prep_flush(monkeypatch, B, T, kind):
     """The gradients of the tail FINALIZE route equal the prep-flush + library route's (the
-    slab sums in the same fixed order; dW_x0 / dE as fp32 products either way).  GRU: more
-    tasks than one launch holds -- each launch adds its norm terms to the previous total."""
+    slab sums in the same fixed order; dW_x0 / dE as fp32 products either way)."""
     torch.manual_seed(7)
     x = torch.randint(0, 65, (B, T), dtype=torch.int32, device="cuda")
     y = torch.randint(0, 65, (B, T), dtype=torch.int32, device="cuda")
@@ -190,7 +214,10 @@ def test_tail_backward_matches_prep_flush(monkeypatch, B, T, kind):
         torch.cuda.synchronize()
         grads.append(model.store.grad.clone())
         if knob == "":
-            assert model.backend._tail_total_ok  # the finalize covered the whole norm prefix
+            if kind == "lstm":  # (GRU at this size: the W_h gradients come from elsewhere)
+                assert model.backend._tail_total_ok  # the finalize covered the norm prefix
+            if not model.backend._tail_total_ok:
+                continue
             n_norm, _ = model.store.norm_terms()
             g = model.store.grad
             # (the slot holds the TF per-token term, itself a sum of squares)
