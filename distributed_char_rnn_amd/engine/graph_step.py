@@ -62,7 +62,13 @@ class GraphedStep:
         self.x, self.y = x.clone(), y.clone()
         self.state_in = [tuple(t.clone() for t in layer) for layer in state]
         torch.cuda.synchronize()
-        be._wver = None  # the captured prep launch must refresh the weight layouts every replay
+        if (getattr(self.opt, "fused", None) is be and be._wver == self.model.store.version
+                and be.knobs.dbg("graph_refresh", "0") != "1"):
+            # the fused Adam writes every layout itself: the captured prep launch carries only
+            # what it leaves behind (GRU: the fp32 concatenations; nothing for LSTM / RNN)
+            be._post_adam = list(getattr(be, "_gru_f32_tasks", []))
+        else:
+            be._wver = None  # the captured prep launch must refresh the layouts every replay
         g = torch.cuda.CUDAGraph()
         # the capture records one optimizer step without running it: its host counters (Adam's
         # t, the parameter version, the backend's step count) are restored whether or not the

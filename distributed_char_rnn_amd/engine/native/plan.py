@@ -49,6 +49,8 @@ DEBUG_KEYS = {
                  "refresh instead of the fused Adam (csrc/tail.hip phase 1)",
     "gru_bpart": "0: GRU bias gradients as column sums of the row-major dZ (a colsum launch per "
                  "layer) instead of the persistent BPTT kernel's partials",
+    "graph_refresh": "1: a captured step (--graph) refreshes every weight layout in its prep "
+                     "launch even when the fused Adam keeps them current",
     "gru_adam": "0: the GRU step keeps the plain Adam + prep layout refresh instead of the "
                 "fused Adam (csrc/tail.hip phase 1)",
     "x0_prep": "0: the wide-vocabulary backward gathers its bf16 embedding rows X0 = E[ids] in "

@@ -16,9 +16,12 @@ def test_graph_step_unsupported_cases_cpu():
     assert not ok and "native" in why
 
 
-def _run(graph, cfg, B, T, steps, lr=2e-3):
+def _run(graph, cfg, B, T, steps, lr=2e-3, fused=False):
     m = CharRNN(cfg, device="cuda", seed=21)
     opt = TFAdam(m.store, clip=5.0, guard=m.error_word())
+    if fused:  # the fused Adam tail (as bench.py / train.py bind it)
+        m.bind_optimizer(opt)
+        assert opt.fused is not None
     gstep = GraphedStep(m, opt) if graph else None
     g = torch.Generator().manual_seed(4)
     data = [(torch.randint(0, cfg.vocab_size, (B, T), generator=g, dtype=torch.int32),
@@ -41,11 +44,16 @@ def _run(graph, cfg, B, T, steps, lr=2e-3):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("B,T,H,L", [(50, 50, 128, 2), (64, 16, 256, 3)])
-def test_graph_step_equals_eager(B, T, H, L):
-    cfg = ModelConfig(model="lstm", vocab_size=65, rnn_size=H, num_layers=L)
-    le, pe, oe, _, se = _run(False, cfg, B, T, 7)
-    lg, pg, og, gs, sg = _run(True, cfg, B, T, 7)
+@pytest.mark.parametrize("kind,B,T,H,L,fused", [
+    ("lstm", 50, 50, 128, 2, False), ("lstm", 64, 16, 256, 3, False),
+    ("lstm", 50, 50, 128, 2, True), ("gru", 50, 50, 128, 2, True),
+    ("gru", 64, 16, 256, 3, False)])
+def test_graph_step_equals_eager(kind, B, T, H, L, fused):
+    """Fused: the captured step's prep launch carries only what the fused Adam leaves behind
+    (GRU: the fp32 concatenations), not the whole layout refresh."""
+    cfg = ModelConfig(model=kind, vocab_size=65, rnn_size=H, num_layers=L)
+    le, pe, oe, _, se = _run(False, cfg, B, T, 7, fused=fused)
+    lg, pg, og, gs, sg = _run(True, cfg, B, T, 7, fused=fused)
     assert gs.graph is not None and not gs.failed and gs.replays >= 4
     assert og.t == oe.t == 7
     assert lg == le
