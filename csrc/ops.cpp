@@ -1871,6 +1871,7 @@ void prep(at::TensorList src, at::TensorList dst, at::IntArrayRef mode, at::Tens
       T.src_ld = ld(s);
       T.kdim = (int)s.size(0);
       TORCH_CHECK(s.size(0) * s.size(1) == d.size(0), "prep ONEHOT: dst rows must be B*T");
+      T.vec4 = (T.cols % 8 == 0 && T.cols <= 256 && T.dst_ld % 8 == 0 && a16(T.dst)) ? 1 : 0;
       continue;
     }
     if (T.mode == dcr::PREP_GATHER) {

@@ -34,8 +34,9 @@ constexpr int kPrepTile = 64;
 __host__ __device__ __forceinline__ int prep_tile_rows(int mode, int vec4) {
   return (mode == PREP_TABLE || (mode == PREP_SUM && !vec4)) ? 16 : kPrepTile;
 }
-__host__ __device__ __forceinline__ int prep_tile_cols(int mode) {
-  return mode == PREP_TABLE ? 16 : kPrepTile;
+// (ONEHOT vec4: a tile spans the whole row, up to 256 columns, in 16-B chunks)
+__host__ __device__ __forceinline__ int prep_tile_cols(int mode, int vec4) {
+  return mode == PREP_TABLE ? 16 : (mode == PREP_ONEHOT && vec4) ? 256 : kPrepTile;
 }
 
 __device__ __forceinline__ void prep_put(const PrepTask& T, size_t idx, float v) {
@@ -60,7 +61,7 @@ __global__ void __launch_bounds__(256) prep_kernel(PrepTable tab) {
   while (k + 1 < tab.n && bid >= tab.t[k + 1].tile0) ++k;
   const PrepTask& T = tab.t[k];
   const int local = bid - T.tile0;
-  const int tcw = prep_tile_cols(T.mode);
+  const int tcw = prep_tile_cols(T.mode, T.vec4);
   const int tiles_c = (T.cols + tcw - 1) / tcw;
   const int tr = prep_tile_rows(T.mode, T.vec4);
   const int r0 = (local / tiles_c) * tr, c0 = (local % tiles_c) * tcw;
@@ -212,6 +213,26 @@ __global__ void __launch_bounds__(256) prep_kernel(PrepTable tab) {
       // guarded load in the row loop is one serialised round trip per row)
       const int* ids = static_cast<const int*>(T.src);
       const int B = T.kdim;
+      if (T.vec4) {
+        // whole rows in 16-B chunks of 8 columns: 4 threads per row, chunks j = t % 4 + 4 i
+        // (2-byte stores of 64-column tiles wrote the 72-column rows at 0.9 TB/s)
+        const int r = r0 + (threadIdx.x >> 2);
+        if (r >= r1) return;
+        const int id = ids[(size_t)(r % B) * T.src_ld + r / B];
+        bf16* row = reinterpret_cast<bf16*>(T.dst) + (size_t)r * T.dst_ld;
+        for (int j = threadIdx.x & 3; 8 * j < T.cols; j += 4) {
+          const int k = id - 8 * j;  // the one's position in this chunk (outside: none)
+          const unsigned one = (k >= 0 && k < 8) ? 0x3F80u << (16 * (k & 1)) : 0u;  // bf16 1.0
+          const int wd = k >> 1;
+          uint4 v;
+          v.x = wd == 0 ? one : 0u;
+          v.y = wd == 1 ? one : 0u;
+          v.z = wd == 2 ? one : 0u;
+          v.w = wd == 3 ? one : 0u;
+          *reinterpret_cast<uint4*>(row + 8 * j) = v;
+        }
+        return;
+      }
       int idv[kPrepTile / 4];
 #pragma unroll
       for (int i = 0; i < kPrepTile / 4; ++i) {
@@ -380,7 +401,7 @@ __global__ void __launch_bounds__(256) prep_kernel(PrepTable tab) {
 }
 
 int prep_tiles(const PrepTask& t) {
-  const int tcw = prep_tile_cols(t.mode);
+  const int tcw = prep_tile_cols(t.mode, t.vec4);
   const int tc = (t.cols + tcw - 1) / tcw;
   if (t.mode == PREP_COLSUM) return tc;  // one tile row spans every source row
   const int tr = prep_tile_rows(t.mode, t.vec4);

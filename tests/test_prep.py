@@ -67,7 +67,11 @@ def test_prep_sum_colsum_onehot_table_raw(dcr_ops):
     torch.testing.assert_close(out_s, part_s.sum(0), rtol=1e-6, atol=1e-5)
     torch.testing.assert_close(db, dbp.sum(0), rtol=1e-6, atol=1e-5)
     ref_oh = torch.nn.functional.one_hot(x.t().reshape(-1).long(), VP).to(torch.bfloat16)
-    assert torch.equal(oh, ref_oh)
+    assert torch.equal(oh, ref_oh)  # (72 columns: the 16-B chunk path)
+    oh70 = torch.full((T * B, 70), 5.0, dtype=torch.bfloat16, device=dev)  # the scalar path
+    dcr_ops.prep([x], [oh70], [5], [])
+    torch.cuda.synchronize()
+    assert torch.equal(oh70, ref_oh[:, :70])
     assert torch.equal(x_tm, x.t())
     ref_tab = (E.double() @ W.double() + bias.double()).float()
     torch.testing.assert_close(tab, ref_tab, rtol=1e-5, atol=1e-3)
